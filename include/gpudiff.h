@@ -1,0 +1,204 @@
+/*
+ * gpudiff.h -- C ABI of the MI355X batched reconciliation-diff engine.
+ *
+ * Drop-in boundary for kcp's syncer change detection.  Each entry point names
+ * the reference interface (paths relative to the sttts/kcp tree) it replaces;
+ * INTEGRATION.md shows the cgo binding a maintainer adds to pkg/syncer.
+ *
+ *   reference seam                                   replaced by
+ *   ------------------------------------------------ ---------------------------
+ *   deepEqualApartFromStatus  specsyncer.go:17-41    gpudiff_spec_equal (1 pair),
+ *                                                    spec bits of gpudiff_wait
+ *   deepEqualStatus           statussyncer.go:15-27  gpudiff_status_equal (1 pair),
+ *                                                    status bits of gpudiff_wait
+ *   UpdateFunc gates          specsyncer.go:47-51,   gpudiff_submit/gpudiff_wait:
+ *                             statussyncer.go:32-36  dirty IDs -> AddToQueue
+ *   Controller.AddToQueue     syncer.go:222-224      consumer of dirty_ids
+ *
+ * Conventions: 0 = OK, negative = error (gpudiff_strerror).  No exceptions or
+ * longjmp cross the ABI.  The caller owns inputs until the call that reads
+ * them returns (gpudiff_encode_pairs copies everything it needs).  The library
+ * owns result buffers until gpudiff_result_release.  A context is not
+ * reentrant: one submitting thread per context (the Go shim's batcher
+ * goroutine).  Errors are conservative, as in the reference
+ * (specsyncer.go:20-22): a pair that cannot be decoded is reported dirty in
+ * both regions with GPUDIFF_DECODE_ERROR set, never "equal".
+ *
+ * There is no CPU fallback for the diff: device entry points on a context
+ * without a GPU return GPUDIFF_E_NODEVICE.
+ */
+#ifndef GPUDIFF_H
+#define GPUDIFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gpudiff_format.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPUDIFF_ABI_VERSION 1
+
+enum {
+    GPUDIFF_OK = 0,
+    GPUDIFF_E_INVAL = -1,     /* bad argument */
+    GPUDIFF_E_NOMEM = -2,     /* host allocation failed */
+    GPUDIFF_E_DEVICE = -3,    /* HIP runtime error */
+    GPUDIFF_E_NODEVICE = -4,  /* context has no GPU */
+    GPUDIFF_E_CAPACITY = -5,  /* device batch capacity exceeded */
+    GPUDIFF_E_STATE = -6,     /* call order violated (e.g. wait on unknown ticket) */
+    GPUDIFF_E_DECODE = -7,    /* single-pair helpers: an input failed to decode */
+    GPUDIFF_E_NOTFOUND = -8,  /* gpudiff_resolve_path: hash not in either object */
+};
+
+/* per-pair result flags */
+#define GPUDIFF_SPEC_DIRTY 0x1u
+#define GPUDIFF_STATUS_DIRTY 0x2u
+#define GPUDIFF_DECODE_ERROR 0x4u
+
+/* changed-path kinds (low 2 bits); bit 7 = status region */
+#define GPUDIFF_PATH_CHANGED 0u        /* present in both, value differs */
+#define GPUDIFF_PATH_ADDED 1u          /* only in new (B) */
+#define GPUDIFF_PATH_REMOVED 2u        /* only in old (A) */
+#define GPUDIFF_PATH_STATUS_ABSENT 3u  /* new has no "status" key (statussyncer.go:22-26) */
+#define GPUDIFF_PATH_REGION_STATUS 0x80u
+
+/* context option flags */
+#define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
+#define GPUDIFF_OPT_HOST_VALUE_HASH 0x2u /* hash long values on the host instead of K1 */
+
+#define GPUDIFF_DEVICE_CURRENT (-1)
+#define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */
+
+typedef struct gpudiff_opts {
+    int32_t device;          /* HIP ordinal, GPUDIFF_DEVICE_CURRENT or GPUDIFF_DEVICE_NONE */
+    uint32_t encode_threads; /* 0 = all host cores */
+    void* stream;            /* hipStream_t to launch on; NULL = context-owned stream */
+    uint32_t flags;          /* GPUDIFF_OPT_* */
+    uint32_t path_hash_bits; /* 0 or 64 normally; 8..63 only to force collisions in tests */
+} gpudiff_opts;
+
+typedef struct gpudiff_json_pair {
+    const uint8_t* old_json;  /* A: upstream (kcp) copy / old version */
+    size_t old_len;
+    const uint8_t* new_json;  /* B: downstream copy / new version */
+    size_t new_len;
+    uint32_t pair_id;         /* echoed in results */
+    uint32_t cluster_id;      /* logical cluster (shard key, syncer.go:106-108) */
+} gpudiff_json_pair;
+
+typedef struct gpudiff_ctx gpudiff_ctx;
+typedef struct gpudiff_hbatch gpudiff_hbatch;  /* encoded pairs in host memory */
+typedef struct gpudiff_dbatch gpudiff_dbatch;  /* encoded pairs resident in HBM */
+typedef uint64_t gpudiff_ticket;
+
+typedef struct gpudiff_hbatch_info {
+    size_t n_pairs;
+    const gpudiff_pair_row* rows;   /* offsets relative to pool */
+    const uint8_t* pool;
+    uint64_t pool_bytes;
+    uint64_t total_leaves;          /* over both objects of every pair */
+    uint64_t n_decode_errors;
+    uint64_t n_reseeded;            /* pairs whose path hash needed seed > 0 */
+} gpudiff_hbatch_info;
+
+typedef struct gpudiff_result {
+    size_t n_pairs;
+    const uint8_t* pair_flags;          /* [n_pairs], batch order, GPUDIFF_*_DIRTY */
+    size_t n_spec_dirty;
+    const uint32_t* spec_dirty_ids;     /* pair_id, batch order */
+    size_t n_status_dirty;
+    const uint32_t* status_dirty_ids;
+    size_t n_dirty;                     /* spec or status dirty */
+    const uint32_t* dirty_ids;
+    const uint32_t* path_offsets;       /* [n_dirty + 1] into the path arrays */
+    size_t n_paths;
+    const uint64_t* path_hashes;        /* per dirty pair: spec asc, status asc, sentinel */
+    const uint8_t* path_kinds;
+    void* internal_;
+} gpudiff_result;
+
+/* device-side view of a diffed batch (for RCCL gathers; pointers are HBM) */
+typedef struct gpudiff_device_view {
+    const uint8_t* pair_flags;
+    const uint32_t* spec_dirty_ids;
+    const uint32_t* status_dirty_ids;
+    const uint32_t* dirty_ids;
+    const uint32_t* counts;   /* [0]=n_spec [1]=n_status [2]=n_dirty [3]=n_paths [4]=overflow */
+} gpudiff_device_view;
+
+typedef struct gpudiff_batch_stats {
+    uint64_t n_pairs;
+    uint64_t pool_bytes;       /* bytes of object blobs resident */
+    uint64_t total_leaves;
+    uint64_t compare_bytes;    /* algorithmic bytes of one diff pass */
+} gpudiff_batch_stats;
+
+typedef struct gpudiff_timings {
+    float value_hash_ms;  /* K1 over the last appended chunk */
+    float compare_ms;     /* K2 */
+    float compact_ms;     /* K3 (scan + compaction) */
+    float join_ms;        /* K4 changed-path merge-join */
+    float emit_ms;        /* K5 + K6 path scan and copy */
+    float total_ms;       /* first to last event of gpudiff_diff */
+} gpudiff_timings;
+
+/* ---- library ---- */
+const char* gpudiff_strerror(int err);
+int gpudiff_abi_version(void);
+int gpudiff_device_count(int* n);
+
+/* ---- context ---- */
+int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out);
+void gpudiff_close(gpudiff_ctx* ctx);
+
+/* ---- host encoding (canonical CSR, no GPU needed) ---- */
+int gpudiff_encode_pairs(gpudiff_ctx* ctx, const gpudiff_json_pair* pairs, size_t n,
+                         gpudiff_hbatch** out);
+int gpudiff_hbatch_info_get(const gpudiff_hbatch* hb, gpudiff_hbatch_info* info);
+void gpudiff_hbatch_free(gpudiff_ctx* ctx, gpudiff_hbatch* hb);
+
+/* ---- device batches ---- */
+int gpudiff_dbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, uint64_t max_pairs,
+                          gpudiff_dbatch** out);
+/* async H2D of hb into the batch + K1 value hashing of the new objects */
+int gpudiff_dbatch_append(gpudiff_ctx* ctx, gpudiff_dbatch* db, const gpudiff_hbatch* hb);
+int gpudiff_dbatch_reset(gpudiff_ctx* ctx, gpudiff_dbatch* db);
+int gpudiff_dbatch_stats_get(const gpudiff_dbatch* db, gpudiff_batch_stats* st);
+int gpudiff_dbatch_device_view(const gpudiff_dbatch* db, gpudiff_device_view* v);
+/* synchronous D2H copy of resident pool bytes (inspection / tests) */
+int gpudiff_dbatch_read_pool(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint64_t off, void* dst,
+                             uint64_t bytes);
+void gpudiff_dbatch_free(gpudiff_ctx* ctx, gpudiff_dbatch* db);
+
+/* ---- diff (the hot path) ---- */
+/* enqueue K2..K6 on the context stream; returns immediately */
+int gpudiff_diff(gpudiff_ctx* ctx, gpudiff_dbatch* db, gpudiff_ticket* ticket);
+/* block until the ticket's diff finished and copy results to host */
+int gpudiff_wait(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_result* res);
+void gpudiff_result_release(gpudiff_ctx* ctx, gpudiff_result* res);
+int gpudiff_last_timings(gpudiff_ctx* ctx, gpudiff_timings* t);
+int gpudiff_sync(gpudiff_ctx* ctx);
+
+/* encode + upload into a context-owned batch + diff (the syncer batcher's call) */
+int gpudiff_submit(gpudiff_ctx* ctx, const gpudiff_json_pair* pairs, size_t n,
+                   gpudiff_ticket* ticket);
+
+/* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
+int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,
+                       const uint8_t* new_json, size_t new_len, int* equal);
+int gpudiff_status_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,
+                         const uint8_t* new_json, size_t new_len, int* equal);
+
+/* ---- host helper: render a changed path ("spec.containers[0].image") ----
+ * path_kind is the kind byte reported with the hash (selects the region). */
+int gpudiff_resolve_path(const uint8_t* old_json, size_t old_len, const uint8_t* new_json,
+                         size_t new_len, uint64_t path_hash, uint8_t path_kind,
+                         uint32_t path_hash_bits, char* buf, size_t cap, size_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

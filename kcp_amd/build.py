@@ -1,0 +1,61 @@
+"""In-tree build of libgpudiff.so (hipcc, gfx950) -- no JIT cache, the .so
+travels to the GPU box with the repo snapshot."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libgpudiff.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+SOURCES = ["kernels.hip", "api.cpp", "encoder.cpp", "json.cpp"]
+HEADERS = ["kernels.h", "encoder.h", "json.h", "xxh64.h"]
+INCLUDES = [os.path.join(ROOT, "include", h) for h in ("gpudiff.h", "gpudiff_format.h")]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}",
+          "-I" + os.path.join(ROOT, "include")]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src, verbose):
+    s = os.path.join(CSRC, src)
+    o = os.path.join(OUT, src + ".o")
+    deps = [s] + [os.path.join(CSRC, h) for h in HEADERS] + INCLUDES
+    if not _newer(o, deps):
+        return o
+    cmd = [HIPCC] + CFLAGS + ["-c", s, "-o", o]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed for %s:\n%s%s" % (src, r.stdout, r.stderr))
+    return o
+
+
+def build(verbose: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose), SOURCES))
+    if _newer(LIB, objs + [os.path.join(CSRC, "gpudiff.map")]):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
+            "-lpthread", "-Wl,--version-script=" + os.path.join(CSRC, "gpudiff.map")]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s%s" % (r.stdout, r.stderr))
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

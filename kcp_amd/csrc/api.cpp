@@ -1,0 +1,726 @@
+// C-ABI of the gpudiff engine (include/gpudiff.h): contexts, host encoding,
+// device batches, the diff pipeline and result retrieval.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gpudiff.h"
+#include "encoder.h"
+#include "kernels.h"
+#include "xxh64.h"
+
+using namespace gd;
+
+namespace {
+
+thread_local std::string g_last_hip_error;
+
+#define HIPCHK(x)                                             \
+    do {                                                      \
+        hipError_t e_ = (x);                                  \
+        if (e_ != hipSuccess) {                               \
+            g_last_hip_error = hipGetErrorString(e_);         \
+            return GPUDIFF_E_DEVICE;                          \
+        }                                                     \
+    } while (0)
+
+struct Part {
+    std::vector<uint8_t> pool;
+    std::vector<gpudiff_pair_row> rows;
+    uint64_t leaves = 0, errors = 0, reseeded = 0;
+};
+
+}  // namespace
+
+struct gpudiff_hbatch {
+    uint8_t* pool = nullptr;
+    gpudiff_pair_row* rows = nullptr;
+    size_t n = 0;
+    uint64_t pool_bytes = 0;
+    uint64_t leaves = 0, errors = 0, reseeded = 0;
+    bool pinned = false;
+    hipEvent_t used = nullptr;  // last async copy that reads this batch
+};
+
+struct gpudiff_dbatch {
+    uint64_t pool_cap = 0, pool_used = 0;
+    uint64_t max_pairs = 0, n_pairs = 0;
+    uint64_t leaves = 0, compare_bytes = 0;
+    uint8_t* pool = nullptr;
+    gpudiff_pair_row* rows = nullptr;
+    uint32_t* pair_ids = nullptr;
+    uint8_t* flags = nullptr;
+    uint32_t* caps = nullptr;
+    void* chunk_counts = nullptr;
+    uint32_t* summary = nullptr;
+    uint32_t* spec_ids = nullptr;
+    uint32_t* status_ids = nullptr;
+    uint32_t* dirty_ids = nullptr;
+    uint32_t* dirty_idx = nullptr;
+    uint32_t* scratch_off = nullptr;
+    uint32_t* path_count = nullptr;
+    uint32_t* path_off = nullptr;
+    uint32_t* tile_sums = nullptr;
+    uint64_t scratch_cap = 0;
+    uint64_t* scratch_h = nullptr;
+    uint8_t* scratch_k = nullptr;
+    uint64_t* out_h = nullptr;
+    uint8_t* out_k = nullptr;
+    hipEvent_t done = nullptr;
+    gpudiff_ticket ticket = 0;
+};
+
+struct ResultStore {
+    std::vector<uint8_t> flags;
+    std::vector<uint32_t> spec, status, dirty, off;
+    std::vector<uint64_t> hashes;
+    std::vector<uint8_t> kinds;
+};
+
+struct gpudiff_ctx {
+    int device = GPUDIFF_DEVICE_NONE;
+    bool has_device = false;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t threads = 1;
+    uint32_t flags = 0;
+    EncodeConfig ecfg;
+    uint64_t hash_mask = ~0ULL;
+    std::vector<std::unique_ptr<PairEncoder>> encoders;
+    std::vector<Part> parts;
+    gpudiff_ticket next_ticket = 1;
+    std::unordered_map<gpudiff_ticket, gpudiff_dbatch*> tickets;
+    hipEvent_t ev[7] = {};
+    bool timing_valid = false;
+    // submit ring
+    gpudiff_dbatch* ring[2] = {nullptr, nullptr};
+    gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
+    uint32_t ring_next = 0;
+};
+
+// ------------------------------------------------------------------ helpers
+static int set_device(gpudiff_ctx* c) {
+    if (!c->has_device) return GPUDIFF_E_NODEVICE;
+    HIPCHK(hipSetDevice(c->device));
+    return GPUDIFF_OK;
+}
+
+template <class T>
+static int dalloc(T** p, uint64_t count) {
+    *p = nullptr;
+    size_t bytes = (size_t)std::max<uint64_t>(count, 1) * sizeof(T);
+    HIPCHK(hipMalloc((void**)p, bytes));
+    return GPUDIFF_OK;
+}
+
+static void dfree_all(gpudiff_dbatch* d) {
+    void* ps[] = {d->pool, d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
+                  d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
+                  d->tile_sums, d->scratch_h, d->scratch_k, d->out_h, d->out_k};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    if (d->done) (void)hipEventDestroy(d->done);
+}
+
+static int ensure_scratch(gpudiff_dbatch* d, uint64_t need) {
+    if (need <= d->scratch_cap && d->scratch_h) return GPUDIFF_OK;
+    uint64_t cap = std::max<uint64_t>(need + need / 8, 1u << 16);
+    if (d->scratch_h) (void)hipFree(d->scratch_h);
+    if (d->scratch_k) (void)hipFree(d->scratch_k);
+    if (d->out_h) (void)hipFree(d->out_h);
+    if (d->out_k) (void)hipFree(d->out_k);
+    d->scratch_h = d->out_h = nullptr;
+    d->scratch_k = d->out_k = nullptr;
+    int rc;
+    if ((rc = dalloc(&d->scratch_h, cap)) || (rc = dalloc(&d->scratch_k, cap)) || (rc = dalloc(&d->out_h, cap)) ||
+        (rc = dalloc(&d->out_k, cap)))
+        return rc;
+    d->scratch_cap = cap;
+    return GPUDIFF_OK;
+}
+
+static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
+    DiffBuffers b;
+    b.rows = d->rows;
+    b.pool = d->pool;
+    b.pair_ids = d->pair_ids;
+    b.n_pairs = (uint32_t)d->n_pairs;
+    b.flags = d->flags;
+    b.caps = d->caps;
+    b.chunk_counts = d->chunk_counts;
+    b.summary = d->summary;
+    b.spec_ids = d->spec_ids;
+    b.status_ids = d->status_ids;
+    b.dirty_ids = d->dirty_ids;
+    b.dirty_idx = d->dirty_idx;
+    b.scratch_off = d->scratch_off;
+    b.path_count = d->path_count;
+    b.path_off = d->path_off;
+    b.tile_sums = d->tile_sums;
+    b.scratch_h = d->scratch_h;
+    b.scratch_k = d->scratch_k;
+    b.scratch_cap = d->scratch_cap;
+    b.out_h = d->out_h;
+    b.out_k = d->out_k;
+    b.hash_mask = c->hash_mask;
+    return b;
+}
+
+// bytes the decision kernel must read for this pair (DESIGN.md "Roofline")
+static uint64_t pair_compare_bytes(const gpudiff_pair_row& r) {
+    uint64_t b = sizeof(gpudiff_pair_row) + 1;
+    if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) return b;
+    if (r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b) b += 2 * gpudiff_seg_bytes(r.spec_l_a, r.spec_ar_a);
+    if ((r.flags_b & GPUDIFF_OBJ_HAS_STATUS) && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b)
+        b += 2 * gpudiff_seg_bytes(r.stat_l_a, r.stat_ar_a);
+    return b;
+}
+
+// ------------------------------------------------------------------ library
+extern "C" {
+
+const char* gpudiff_strerror(int err) {
+    switch (err) {
+        case GPUDIFF_OK: return "ok";
+        case GPUDIFF_E_INVAL: return "invalid argument";
+        case GPUDIFF_E_NOMEM: return "out of host memory";
+        case GPUDIFF_E_DEVICE: return g_last_hip_error.empty() ? "HIP runtime error" : g_last_hip_error.c_str();
+        case GPUDIFF_E_NODEVICE: return "no GPU in this context (there is no CPU fallback)";
+        case GPUDIFF_E_CAPACITY: return "device batch capacity exceeded";
+        case GPUDIFF_E_STATE: return "invalid call order / unknown ticket";
+        case GPUDIFF_E_DECODE: return "input failed to decode as a JSON object";
+        case GPUDIFF_E_NOTFOUND: return "path hash not found";
+        default: return "unknown error";
+    }
+}
+
+int gpudiff_abi_version(void) { return GPUDIFF_ABI_VERSION; }
+
+int gpudiff_device_count(int* n) {
+    if (!n) return GPUDIFF_E_INVAL;
+    *n = 0;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) return GPUDIFF_OK;
+    *n = c;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
+    if (!out) return GPUDIFF_E_INVAL;
+    *out = nullptr;
+    gpudiff_opts o{};
+    o.device = GPUDIFF_DEVICE_CURRENT;
+    if (opts) o = *opts;
+    std::unique_ptr<gpudiff_ctx> c(new (std::nothrow) gpudiff_ctx());
+    if (!c) return GPUDIFF_E_NOMEM;
+    uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    c->threads = o.encode_threads ? o.encode_threads : std::min(hw, 16u);
+    c->flags = o.flags;
+    c->ecfg.hash_bits = (o.path_hash_bits == 0 || o.path_hash_bits >= 64) ? 64 : o.path_hash_bits;
+    if (c->ecfg.hash_bits < 8) return GPUDIFF_E_INVAL;
+    c->ecfg.host_value_hash = (o.flags & GPUDIFF_OPT_HOST_VALUE_HASH) != 0;
+    c->hash_mask = c->ecfg.hash_bits >= 64 ? ~0ULL : ((1ULL << c->ecfg.hash_bits) - 1);
+    if (o.device != GPUDIFF_DEVICE_NONE) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return GPUDIFF_E_NODEVICE;
+        int dev = o.device;
+        if (dev == GPUDIFF_DEVICE_CURRENT) HIPCHK(hipGetDevice(&dev));
+        if (dev < 0 || dev >= n) return GPUDIFF_E_INVAL;
+        c->device = dev;
+        c->has_device = true;
+        HIPCHK(hipSetDevice(dev));
+        if (o.stream) {
+            c->stream = (hipStream_t)o.stream;
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            c->own_stream = true;
+        }
+        for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    }
+    *out = c.release();
+    return GPUDIFF_OK;
+}
+
+void gpudiff_close(gpudiff_ctx* c) {
+    if (!c) return;
+    if (c->has_device) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        for (int i = 0; i < 2; i++) {
+            if (c->ring[i]) gpudiff_dbatch_free(c, c->ring[i]);
+            if (c->ring_hb[i]) gpudiff_hbatch_free(c, c->ring_hb[i]);
+        }
+        for (auto& e : c->ev)
+            if (e) (void)hipEventDestroy(e);
+        if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    }
+    delete c;
+}
+
+// ------------------------------------------------------------------ encoding
+int gpudiff_encode_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpudiff_hbatch** out) {
+    if (!c || !out || (n && !pairs)) return GPUDIFF_E_INVAL;
+    if (n > 0xFFFFFFFFull) return GPUDIFF_E_INVAL;
+    *out = nullptr;
+    uint32_t T = (uint32_t)std::min<size_t>(c->threads, std::max<size_t>(1, n / 256));
+    while (c->encoders.size() < T) c->encoders.emplace_back(new PairEncoder(c->ecfg));
+    if (c->parts.size() < T) c->parts.resize(T);
+    try {
+        auto work = [&](uint32_t t) {
+            Part& part = c->parts[t];
+            part.pool.clear();
+            part.rows.clear();
+            PairEncoder& enc = *c->encoders[t];
+            enc.leaves_written = enc.reseeded = enc.decode_errors = 0;
+            size_t b = n * t / T, e = n * (t + 1) / T;
+            part.rows.resize(e - b);
+            for (size_t i = b; i < e; i++) {
+                const gpudiff_json_pair& p = pairs[i];
+                enc.encode_json(p.old_json, p.old_len, p.new_json, p.new_len, p.pair_id, p.cluster_id, part.pool,
+                                part.rows[i - b]);
+            }
+            size_t pad = (part.pool.size() + 15) & ~(size_t)15;
+            part.pool.resize(pad, 0);
+            part.leaves = enc.leaves_written;
+            part.errors = enc.decode_errors;
+            part.reseeded = enc.reseeded;
+        };
+        if (T == 1) {
+            work(0);
+        } else {
+            std::vector<std::thread> th;
+            for (uint32_t t = 0; t < T; t++) th.emplace_back(work, t);
+            for (auto& x : th) x.join();
+        }
+    } catch (const std::bad_alloc&) {
+        return GPUDIFF_E_NOMEM;
+    }
+    std::unique_ptr<gpudiff_hbatch> hb(new (std::nothrow) gpudiff_hbatch());
+    if (!hb) return GPUDIFF_E_NOMEM;
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < T; t++) total += c->parts[t].pool.size();
+    hb->n = n;
+    hb->pool_bytes = total;
+    size_t pool_alloc = (size_t)std::max<uint64_t>(total, 16);
+    size_t rows_alloc = std::max<size_t>(n, 1) * sizeof(gpudiff_pair_row);
+    if (c->has_device) {
+        HIPCHK(hipSetDevice(c->device));
+        if (hipHostMalloc((void**)&hb->pool, pool_alloc, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&hb->rows, rows_alloc, hipHostMallocDefault) != hipSuccess) {
+            if (hb->pool) (void)hipHostFree(hb->pool);
+            return GPUDIFF_E_NOMEM;
+        }
+        hb->pinned = true;
+        HIPCHK(hipEventCreateWithFlags(&hb->used, hipEventDisableTiming));
+    } else {
+        hb->pool = (uint8_t*)aligned_alloc(64, (pool_alloc + 63) & ~(size_t)63);
+        hb->rows = (gpudiff_pair_row*)aligned_alloc(64, (rows_alloc + 63) & ~(size_t)63);
+        if (!hb->pool || !hb->rows) {
+            free(hb->pool);
+            free(hb->rows);
+            return GPUDIFF_E_NOMEM;
+        }
+    }
+    uint64_t base = 0;
+    size_t r0 = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        Part& part = c->parts[t];
+        if (!part.pool.empty()) memcpy(hb->pool + base, part.pool.data(), part.pool.size());
+        for (size_t i = 0; i < part.rows.size(); i++) {
+            gpudiff_pair_row r = part.rows[i];
+            r.off_a += base;
+            r.off_b += base;
+            hb->rows[r0 + i] = r;
+        }
+        r0 += part.rows.size();
+        base += part.pool.size();
+        hb->leaves += part.leaves;
+        hb->errors += part.errors;
+        hb->reseeded += part.reseeded;
+    }
+    *out = hb.release();
+    return GPUDIFF_OK;
+}
+
+int gpudiff_hbatch_info_get(const gpudiff_hbatch* hb, gpudiff_hbatch_info* info) {
+    if (!hb || !info) return GPUDIFF_E_INVAL;
+    info->n_pairs = hb->n;
+    info->rows = hb->rows;
+    info->pool = hb->pool;
+    info->pool_bytes = hb->pool_bytes;
+    info->total_leaves = hb->leaves;
+    info->n_decode_errors = hb->errors;
+    info->n_reseeded = hb->reseeded;
+    return GPUDIFF_OK;
+}
+
+void gpudiff_hbatch_free(gpudiff_ctx* c, gpudiff_hbatch* hb) {
+    if (!hb) return;
+    if (hb->pinned) {
+        if (c && c->has_device) (void)hipSetDevice(c->device);
+        if (hb->used) {
+            (void)hipEventSynchronize(hb->used);
+            (void)hipEventDestroy(hb->used);
+        }
+        (void)hipHostFree(hb->pool);
+        (void)hipHostFree(hb->rows);
+    } else {
+        free(hb->pool);
+        free(hb->rows);
+    }
+    delete hb;
+}
+
+// ------------------------------------------------------------------ device batches
+int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pairs, gpudiff_dbatch** out) {
+    if (!c || !out) return GPUDIFF_E_INVAL;
+    *out = nullptr;
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (max_pairs > 0xFFFFFFF0ull) return GPUDIFF_E_INVAL;
+    std::unique_ptr<gpudiff_dbatch> d(new (std::nothrow) gpudiff_dbatch());
+    if (!d) return GPUDIFF_E_NOMEM;
+    d->pool_cap = (pool_bytes + 15) & ~15ull;
+    d->max_pairs = max_pairs;
+    const uint64_t np = std::max<uint64_t>(max_pairs, 1);
+    const uint64_t nchunks = (np + 63) / 64;
+    const uint64_t ntiles = np / 4096 + 2;
+    uint4* cc = nullptr;
+    if ((rc = dalloc(&d->pool, d->pool_cap)) || (rc = dalloc(&d->rows, np)) || (rc = dalloc(&d->pair_ids, np)) ||
+        (rc = dalloc(&d->flags, np)) || (rc = dalloc(&d->caps, np)) || (rc = dalloc(&cc, nchunks)) ||
+        (rc = dalloc(&d->summary, 8)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
+        (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
+        (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
+        (rc = dalloc(&d->tile_sums, ntiles))) {
+        d->chunk_counts = cc;
+        dfree_all(d.get());
+        return rc;
+    }
+    d->chunk_counts = cc;
+    if (hipEventCreateWithFlags(&d->done, hipEventDisableTiming) != hipSuccess) {
+        dfree_all(d.get());
+        return GPUDIFF_E_DEVICE;
+    }
+    *out = d.release();
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatch* hb) {
+    if (!c || !d || !hb) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (d->pool_used + hb->pool_bytes > d->pool_cap || d->n_pairs + hb->n > d->max_pairs) return GPUDIFF_E_CAPACITY;
+    if (hb->n == 0) return GPUDIFF_OK;
+    const uint64_t base = d->pool_used;
+    const uint32_t begin = (uint32_t)d->n_pairs, end = (uint32_t)(d->n_pairs + hb->n);
+    if (hb->pool_bytes)
+        HIPCHK(hipMemcpyAsync(d->pool + base, hb->pool, hb->pool_bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d->rows + begin, hb->rows, hb->n * sizeof(gpudiff_pair_row), hipMemcpyHostToDevice,
+                          c->stream));
+    if (hb->used) HIPCHK(hipEventRecord(hb->used, c->stream));
+    HIPCHK(launch_rebase(c->stream, d->rows, begin, end, base, d->pair_ids));
+    if (!c->ecfg.host_value_hash) {
+        if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        HIPCHK(launch_value_hash(c->stream, d->rows, begin, end, d->pool));
+        if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    }
+    uint64_t cb = 0;
+    for (size_t i = 0; i < hb->n; i++) cb += pair_compare_bytes(hb->rows[i]);
+    d->compare_bytes += cb;
+    d->pool_used += hb->pool_bytes;
+    d->n_pairs = end;
+    d->leaves += hb->leaves;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
+    if (!c || !d) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = 0;
+    d->ticket = 0;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_stats_get(const gpudiff_dbatch* d, gpudiff_batch_stats* st) {
+    if (!d || !st) return GPUDIFF_E_INVAL;
+    st->n_pairs = d->n_pairs;
+    st->pool_bytes = d->pool_used;
+    st->total_leaves = d->leaves;
+    st->compare_bytes = d->compare_bytes;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_device_view(const gpudiff_dbatch* d, gpudiff_device_view* v) {
+    if (!d || !v) return GPUDIFF_E_INVAL;
+    v->pair_flags = d->flags;
+    v->spec_dirty_ids = d->spec_ids;
+    v->status_dirty_ids = d->status_ids;
+    v->dirty_ids = d->dirty_ids;
+    v->counts = d->summary;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_read_pool(gpudiff_ctx* c, const gpudiff_dbatch* d, uint64_t off, void* dst, uint64_t bytes) {
+    if (!c || !d || (!dst && bytes)) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (off > d->pool_used || bytes > d->pool_used - off) return GPUDIFF_E_INVAL;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (bytes) HIPCHK(hipMemcpy(dst, d->pool + off, bytes, hipMemcpyDeviceToHost));
+    return GPUDIFF_OK;
+}
+
+void gpudiff_dbatch_free(gpudiff_ctx* c, gpudiff_dbatch* d) {
+    if (!d) return;
+    if (c && c->has_device) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        if (d->ticket) c->tickets.erase(d->ticket);
+    }
+    dfree_all(d);
+    delete d;
+}
+
+// ------------------------------------------------------------------ diff
+static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d, bool timing) {
+    DiffBuffers b = buffers_of(c, d);
+    HIPCHK(launch_join(c->stream, b));
+    if (timing) HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    HIPCHK(launch_emit(c->stream, b));
+    if (timing) HIPCHK(hipEventRecord(c->ev[6], c->stream));
+    return GPUDIFF_OK;
+}
+
+int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
+    if (!c || !d) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    // scratch for changed paths: sized from the batch, grown on overflow
+    if ((rc = ensure_scratch(d, std::max<uint64_t>(d->n_pairs * 2 + d->leaves / 8, 1u << 16)))) return rc;
+    const bool timing = (c->flags & GPUDIFF_OPT_TIMING) != 0;
+    HIPCHK(hipMemsetAsync(d->summary, 0, 8 * sizeof(uint32_t), c->stream));
+    if (timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    DiffBuffers b = buffers_of(c, d);
+    if (d->n_pairs) {
+        HIPCHK(launch_compare(c->stream, b));
+        if (timing) HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        HIPCHK(launch_compact(c->stream, b));
+        if (timing) HIPCHK(hipEventRecord(c->ev[5], c->stream));
+        rc = enqueue_join_emit(c, d, timing);
+        if (rc) return rc;
+    } else {
+        HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), c->stream));
+    }
+    HIPCHK(hipEventRecord(d->done, c->stream));
+    c->timing_valid = timing && d->n_pairs;
+    if (d->ticket) c->tickets.erase(d->ticket);
+    d->ticket = c->next_ticket++;
+    c->tickets[d->ticket] = d;
+    if (ticket) *ticket = d->ticket;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_sync(gpudiff_ctx* c) {
+    if (!c) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return GPUDIFF_OK;
+}
+
+int gpudiff_last_timings(gpudiff_ctx* c, gpudiff_timings* t) {
+    if (!c || !t) return GPUDIFF_E_INVAL;
+    memset(t, 0, sizeof(*t));
+    if (!c->has_device) return GPUDIFF_E_NODEVICE;
+    if (!(c->flags & GPUDIFF_OPT_TIMING)) return GPUDIFF_E_STATE;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) t->value_hash_ms = ms;
+    if (!c->timing_valid) return GPUDIFF_OK;
+    HIPCHK(hipEventElapsedTime(&t->compare_ms, c->ev[2], c->ev[3]));
+    HIPCHK(hipEventElapsedTime(&t->compact_ms, c->ev[3], c->ev[5]));
+    HIPCHK(hipEventElapsedTime(&t->join_ms, c->ev[5], c->ev[4]));
+    HIPCHK(hipEventElapsedTime(&t->emit_ms, c->ev[4], c->ev[6]));
+    HIPCHK(hipEventElapsedTime(&t->total_ms, c->ev[2], c->ev[6]));
+    return GPUDIFF_OK;
+}
+
+int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
+    if (!c || !res) return GPUDIFF_E_INVAL;
+    memset(res, 0, sizeof(*res));
+    int rc = set_device(c);
+    if (rc) return rc;
+    auto it = c->tickets.find(ticket);
+    if (it == c->tickets.end()) return GPUDIFF_E_STATE;
+    gpudiff_dbatch* d = it->second;
+    HIPCHK(hipEventSynchronize(d->done));
+    uint32_t sum[8];
+    HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
+    if (sum[4]) {  // path scratch overflow: grow to the exact need and redo the join
+        if ((rc = ensure_scratch(d, sum[3]))) return rc;
+        uint32_t zero = 0;
+        HIPCHK(hipMemcpyAsync(d->summary + 4, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
+        if ((rc = enqueue_join_emit(c, d, false))) return rc;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
+        if (sum[4]) return GPUDIFF_E_CAPACITY;
+    }
+    std::unique_ptr<ResultStore> rs(new (std::nothrow) ResultStore());
+    if (!rs) return GPUDIFF_E_NOMEM;
+    try {
+        rs->flags.resize(d->n_pairs);
+        rs->spec.resize(sum[0]);
+        rs->status.resize(sum[1]);
+        rs->dirty.resize(sum[2]);
+        rs->off.resize((size_t)sum[2] + 1);
+        rs->hashes.resize(sum[5]);
+        rs->kinds.resize(sum[5]);
+    } catch (const std::bad_alloc&) {
+        return GPUDIFF_E_NOMEM;
+    }
+    if (d->n_pairs) HIPCHK(hipMemcpy(rs->flags.data(), d->flags, d->n_pairs, hipMemcpyDeviceToHost));
+    if (sum[0]) HIPCHK(hipMemcpy(rs->spec.data(), d->spec_ids, sum[0] * 4ull, hipMemcpyDeviceToHost));
+    if (sum[1]) HIPCHK(hipMemcpy(rs->status.data(), d->status_ids, sum[1] * 4ull, hipMemcpyDeviceToHost));
+    if (sum[2]) HIPCHK(hipMemcpy(rs->dirty.data(), d->dirty_ids, sum[2] * 4ull, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(rs->off.data(), d->path_off, (sum[2] + 1ull) * 4ull, hipMemcpyDeviceToHost));
+    if (sum[5]) {
+        HIPCHK(hipMemcpy(rs->hashes.data(), d->out_h, sum[5] * 8ull, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(rs->kinds.data(), d->out_k, sum[5], hipMemcpyDeviceToHost));
+    }
+    res->n_pairs = d->n_pairs;
+    res->pair_flags = rs->flags.data();
+    res->n_spec_dirty = sum[0];
+    res->spec_dirty_ids = rs->spec.data();
+    res->n_status_dirty = sum[1];
+    res->status_dirty_ids = rs->status.data();
+    res->n_dirty = sum[2];
+    res->dirty_ids = rs->dirty.data();
+    res->path_offsets = rs->off.data();
+    res->n_paths = sum[5];
+    res->path_hashes = rs->hashes.data();
+    res->path_kinds = rs->kinds.data();
+    res->internal_ = rs.release();
+    return GPUDIFF_OK;
+}
+
+void gpudiff_result_release(gpudiff_ctx* c, gpudiff_result* res) {
+    (void)c;
+    if (!res) return;
+    delete (ResultStore*)res->internal_;
+    memset(res, 0, sizeof(*res));
+}
+
+int gpudiff_submit(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpudiff_ticket* ticket) {
+    if (!c || (n && !pairs)) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    gpudiff_hbatch* hb = nullptr;
+    if ((rc = gpudiff_encode_pairs(c, pairs, n, &hb))) return rc;
+    const uint32_t slot = c->ring_next;
+    c->ring_next ^= 1u;
+    gpudiff_dbatch*& d = c->ring[slot];
+    if (d) HIPCHK(hipEventSynchronize(d->done));
+    if (c->ring_hb[slot]) {
+        gpudiff_hbatch_free(c, c->ring_hb[slot]);
+        c->ring_hb[slot] = nullptr;
+    }
+    if (d && (d->pool_cap < hb->pool_bytes || d->max_pairs < n)) {
+        gpudiff_dbatch_free(c, d);
+        d = nullptr;
+    }
+    if (!d) {
+        uint64_t pool = std::max<uint64_t>(hb->pool_bytes * 2, 1u << 20);
+        uint64_t np = std::max<uint64_t>(n * 2, 1024);
+        if ((rc = gpudiff_dbatch_create(c, pool, np, &d))) {
+            gpudiff_hbatch_free(c, hb);
+            return rc;
+        }
+    }
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = 0;
+    if ((rc = gpudiff_dbatch_append(c, d, hb)) || (rc = gpudiff_diff(c, d, ticket))) {
+        gpudiff_hbatch_free(c, hb);
+        return rc;
+    }
+    c->ring_hb[slot] = hb;  // freed when the slot is reused (after its copy completed)
+    return GPUDIFF_OK;
+}
+
+static int single_pair(gpudiff_ctx* c, const uint8_t* a, size_t al, const uint8_t* b, size_t bl, uint32_t bit,
+                       int* equal) {
+    if (!c || !equal || !a || !b) return GPUDIFF_E_INVAL;
+    gpudiff_json_pair p{a, al, b, bl, 0, 0};
+    gpudiff_ticket t = 0;
+    int rc = gpudiff_submit(c, &p, 1, &t);
+    if (rc) return rc;
+    gpudiff_result r;
+    if ((rc = gpudiff_wait(c, t, &r))) return rc;
+    const uint8_t f = r.pair_flags[0];
+    gpudiff_result_release(c, &r);
+    *equal = (f & bit) ? 0 : 1;
+    return (f & GPUDIFF_DECODE_ERROR) ? GPUDIFF_E_DECODE : GPUDIFF_OK;
+}
+
+int gpudiff_spec_equal(gpudiff_ctx* c, const uint8_t* a, size_t al, const uint8_t* b, size_t bl, int* equal) {
+    return single_pair(c, a, al, b, bl, GPUDIFF_SPEC_DIRTY, equal);
+}
+
+int gpudiff_status_equal(gpudiff_ctx* c, const uint8_t* a, size_t al, const uint8_t* b, size_t bl, int* equal) {
+    return single_pair(c, a, al, b, bl, GPUDIFF_STATUS_DIRTY, equal);
+}
+
+int gpudiff_resolve_path(const uint8_t* a, size_t al, const uint8_t* b, size_t bl, uint64_t h, uint8_t kind,
+                         uint32_t bits, char* buf, size_t cap, size_t* out_len) {
+    if (!a || !b) return GPUDIFF_E_INVAL;
+    EncodeConfig cfg;
+    cfg.hash_bits = (bits == 0 || bits >= 64) ? 64 : bits;
+    PairEncoder enc(cfg);
+    std::vector<uint8_t> pool;
+    gpudiff_pair_row row;
+    enc.encode_json(a, al, b, bl, 0, 0, pool, row);
+    if (row.flags_a & GPUDIFF_OBJ_DECODE_ERR) return GPUDIFF_E_DECODE;
+    // encode_json left both flattened objects (with seed-assigned hashes) in place
+    std::string s;
+    bool found = false;
+    const bool status = (kind & GPUDIFF_PATH_REGION_STATUS) != 0;
+    if ((kind & 3u) != GPUDIFF_PATH_STATUS_ABSENT) {
+        for (const FlatObject* o : {&enc.flat_a, &enc.flat_b}) {
+            const std::vector<LeafRec>& v = status ? o->stat : o->spec;
+            auto it = std::lower_bound(v.begin(), v.end(), h, [](const LeafRec& r, uint64_t x) { return r.h < x; });
+            if (it != v.end() && it->h == h) {
+                s = render_path(o->paths.data() + it->path_off, it->path_len);
+                found = true;
+                break;
+            }
+        }
+    } else {
+        const uint64_t mask = cfg.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg.hash_bits) - 1);
+        const uint32_t seed = (row.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFF;
+        const std::string& sp = status_path_bytes();
+        if ((xxh64_host(sp.data(), sp.size(), seed) & mask) == h) {
+            s = "status";
+            found = true;
+        }
+    }
+    if (!found) return GPUDIFF_E_NOTFOUND;
+    if (out_len) *out_len = s.size();
+    if (buf && cap) {
+        size_t k = std::min(cap - 1, s.size());
+        memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return GPUDIFF_OK;
+}
+
+}  // extern "C"

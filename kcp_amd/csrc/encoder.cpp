@@ -1,0 +1,319 @@
+// Host canonical encoder (see encoder.h and include/gpudiff_format.h).
+#include "encoder.h"
+
+#include <string.h>
+
+#include <algorithm>
+
+#include "xxh64.h"
+
+namespace gd {
+
+static const Node* find_member(const Node& obj, const char* key, uint32_t klen) {
+    if (obj.t != J_OBJ) return nullptr;
+    for (uint32_t i = 0; i < obj.n; i++) {
+        const Member& m = obj.u.mem[i];
+        if (m.klen == klen && memcmp(m.k, key, klen) == 0) return &m.v;
+    }
+    return nullptr;
+}
+
+static inline void push_key(std::string& p, const char* k, uint32_t n) {
+    char hdr[5];
+    hdr[0] = 0x01;
+    memcpy(hdr + 1, &n, 4);
+    p.append(hdr, 5);
+    p.append(k, n);
+}
+
+static inline void push_idx(std::string& p, uint32_t i) {
+    char hdr[5];
+    hdr[0] = 0x02;
+    memcpy(hdr + 1, &i, 4);
+    p.append(hdr, 5);
+}
+
+const std::string& status_path_bytes() {
+    static const std::string s = [] {
+        std::string p;
+        push_key(p, "status", 6);
+        return p;
+    }();
+    return s;
+}
+
+namespace {
+struct Flattener {
+    FlatObject& o;
+    std::string path;
+    std::vector<LeafRec>* cur = nullptr;
+
+    explicit Flattener(FlatObject& out) : o(out) {}
+
+    void leaf(const Node& n) {
+        LeafRec r;
+        r.h = 0;
+        r.val = 0;
+        r.vptr = nullptr;
+        r.vlen = 0;
+        uint32_t tag = n.t, len = 0;
+        switch (n.t) {
+            case J_INT:
+                len = 8;
+                r.val = (uint64_t)n.u.i;
+                break;
+            case J_FLOAT: {
+                len = 8;
+                double d = n.u.d == 0.0 ? 0.0 : n.u.d;  // -0.0 == 0.0 under Go ==
+                memcpy(&r.val, &d, 8);
+                break;
+            }
+            case J_STR:
+                len = n.n;
+                r.vptr = n.u.s;
+                r.vlen = n.n;
+                if (n.n <= GPUDIFF_INLINE_MAX) memcpy(&r.val, n.u.s, n.n);
+                break;
+            default:
+                break;  // null, bools, empty {} / []: tag only
+        }
+        r.meta = (len << 3) | tag;
+        r.path_off = (uint32_t)o.paths.size();
+        r.path_len = (uint32_t)path.size();
+        o.paths.append(path);
+        cur->push_back(r);
+    }
+
+    void walk(const Node& n) {
+        if (n.t == J_OBJ && n.n) {
+            size_t l = path.size();
+            for (uint32_t i = 0; i < n.n; i++) {
+                const Member& m = n.u.mem[i];
+                push_key(path, m.k, m.klen);
+                walk(m.v);
+                path.resize(l);
+            }
+        } else if (n.t == J_ARR && n.n) {
+            size_t l = path.size();
+            for (uint32_t i = 0; i < n.n; i++) {
+                push_idx(path, i);
+                walk(n.u.items[i]);
+                path.resize(l);
+            }
+        } else {
+            leaf(n);
+        }
+    }
+
+    // GetLabels / GetAnnotations (NestedStringMap): nil unless metadata.<field>
+    // is a map whose values are all strings; nil and empty compare equal, so an
+    // empty map contributes no leaves either.
+    void string_map(const Node& root, const char* field, uint32_t flen) {
+        const Node* md = find_member(root, "metadata", 8);
+        if (!md || md->t != J_OBJ) return;
+        const Node* m = find_member(*md, field, flen);
+        if (!m || m->t != J_OBJ || m->n == 0) return;
+        for (uint32_t i = 0; i < m->n; i++)
+            if (m->u.mem[i].v.t != J_STR) return;
+        path.clear();
+        push_key(path, "metadata", 8);
+        push_key(path, field, flen);
+        size_t l = path.size();
+        for (uint32_t i = 0; i < m->n; i++) {
+            push_key(path, m->u.mem[i].k, m->u.mem[i].klen);
+            leaf(m->u.mem[i].v);
+            path.resize(l);
+        }
+    }
+};
+}  // namespace
+
+void flatten_object(const Node& root, FlatObject& o) {
+    o.clear();
+    Flattener f(o);
+    // spec region S (specsyncer.go:30-39)
+    f.cur = &o.spec;
+    for (uint32_t i = 0; i < root.n; i++) {
+        const Member& m = root.u.mem[i];
+        if ((m.klen == 8 && memcmp(m.k, "metadata", 8) == 0) || (m.klen == 6 && memcmp(m.k, "status", 6) == 0))
+            continue;
+        if (m.v.t == J_NULL) continue;  // top-level null == missing key
+        f.path.clear();
+        push_key(f.path, m.k, m.klen);
+        f.walk(m.v);
+    }
+    // regions L and N (specsyncer.go:23,26)
+    f.string_map(root, "labels", 6);
+    f.string_map(root, "annotations", 11);
+    // status region T (statussyncer.go:22-24)
+    const Node* st = find_member(root, "status", 6);
+    if (st) {
+        o.flags |= GPUDIFF_OBJ_HAS_STATUS;
+        if (st->t != J_NULL) {
+            f.cur = &o.stat;
+            f.path = status_path_bytes();
+            f.walk(*st);
+        }
+    }
+}
+
+static inline bool path_eq(const FlatObject& a, const LeafRec& x, const FlatObject& b, const LeafRec& y) {
+    return x.path_len == y.path_len && memcmp(a.paths.data() + x.path_off, b.paths.data() + y.path_off, x.path_len) == 0;
+}
+
+static bool merge_check(const FlatObject& a, const std::vector<LeafRec>& va, const FlatObject& b,
+                        const std::vector<LeafRec>& vb) {
+    size_t i = 0, j = 0;
+    while (i < va.size() && j < vb.size()) {
+        if (va[i].h < vb[j].h) i++;
+        else if (va[i].h > vb[j].h) j++;
+        else {
+            if (!path_eq(a, va[i], b, vb[j])) return false;
+            i++;
+            j++;
+        }
+    }
+    return true;
+}
+
+static bool sentinel_check(const FlatObject& o, const std::vector<LeafRec>& v, uint64_t hs) {
+    auto it = std::lower_bound(v.begin(), v.end(), hs, [](const LeafRec& r, uint64_t h) { return r.h < h; });
+    if (it == v.end() || it->h != hs) return true;
+    const std::string& sp = status_path_bytes();
+    return it->path_len == sp.size() && memcmp(o.paths.data() + it->path_off, sp.data(), sp.size()) == 0;
+}
+
+bool PairEncoder::assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed_out) {
+    const uint64_t mask = cfg_.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg_.hash_bits) - 1);
+    auto by_h = [](const LeafRec& x, const LeafRec& y) { return x.h < y.h; };
+    for (uint32_t seed = 0; seed <= 255; seed++) {
+        for (FlatObject* o : {&a, &b})
+            for (std::vector<LeafRec>* v : {&o->spec, &o->stat}) {
+                for (LeafRec& r : *v) r.h = xxh64_host(o->paths.data() + r.path_off, r.path_len, seed) & mask;
+                std::sort(v->begin(), v->end(), by_h);
+            }
+        bool ok = true;
+        for (FlatObject* o : {&a, &b})
+            for (std::vector<LeafRec>* v : {&o->spec, &o->stat})
+                for (size_t i = 1; ok && i < v->size(); i++)
+                    if ((*v)[i].h == (*v)[i - 1].h) ok = false;  // paths are unique within an object
+        ok = ok && merge_check(a, a.spec, b, b.spec) && merge_check(a, a.stat, b, b.stat);
+        if (ok) {
+            const std::string& sp = status_path_bytes();
+            uint64_t hs = xxh64_host(sp.data(), sp.size(), seed) & mask;
+            ok = sentinel_check(a, a.stat, hs) && sentinel_check(b, b.stat, hs);
+        }
+        if (ok) {
+            *seed_out = seed;
+            return true;
+        }
+    }
+    return false;
+}
+
+static inline void pool_align16(std::vector<uint8_t>& pool) {
+    size_t n = (pool.size() + 15) & ~(size_t)15;
+    pool.resize(n, 0);
+}
+
+void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
+                             uint32_t* sar, uint32_t* tl, uint32_t* tar) {
+    pool_align16(pool);
+    *off = pool.size();
+    auto seg = [&](const std::vector<LeafRec>& v, uint32_t* L, uint32_t* AR) {
+        const size_t n = v.size();
+        uint32_t arena = 0;
+        for (const LeafRec& r : v)
+            if (gpudiff_meta_is_long(r.meta)) arena += (r.vlen + 15u) & ~15u;
+        const size_t head = ((n * 20) + 15) & ~(size_t)15;
+        const size_t base = pool.size();
+        pool.resize(base + head + arena, 0);
+        uint8_t* p = pool.data() + base;
+        uint64_t* keys = (uint64_t*)p;
+        uint8_t* vals = p + 8 * n;
+        uint8_t* metas = p + 16 * n;
+        uint8_t* ar = p + head;
+        uint32_t aoff = 0;
+        for (size_t i = 0; i < n; i++) {
+            const LeafRec& r = v[i];
+            uint64_t val = r.val;
+            if (gpudiff_meta_is_long(r.meta)) {
+                memcpy(ar + aoff, r.vptr, r.vlen);
+                aoff += (r.vlen + 15u) & ~15u;
+                val = cfg_.host_value_hash ? xxh64_host(r.vptr, r.vlen, 0) : 0;
+            }
+            memcpy(&keys[i], &r.h, 8);
+            memcpy(vals + 8 * i, &val, 8);
+            memcpy(metas + 4 * i, &r.meta, 4);
+        }
+        *L = (uint32_t)n;
+        *AR = arena;
+        leaves_written += n;
+    };
+    seg(o.spec, sl, sar);
+    seg(o.stat, tl, tar);
+}
+
+void PairEncoder::encode_flat(FlatObject* fa, FlatObject* fb, uint32_t pair_id, uint32_t cluster_id,
+                              std::vector<uint8_t>& pool, gpudiff_pair_row& row) {
+    memset(&row, 0, sizeof(row));
+    row.pair_id = pair_id;
+    row.cluster_id = cluster_id;
+    uint32_t seed = 0;
+    if (!fa || !fb || !assign_seed(*fa, *fb, &seed)) {
+        decode_errors++;
+        pool_align16(pool);
+        row.off_a = row.off_b = pool.size();
+        row.flags_a = row.flags_b = GPUDIFF_OBJ_DECODE_ERR;
+        return;
+    }
+    if (seed) reseeded++;
+    write_blob(*fa, pool, &row.off_a, &row.spec_l_a, &row.spec_ar_a, &row.stat_l_a, &row.stat_ar_a);
+    write_blob(*fb, pool, &row.off_b, &row.spec_l_b, &row.spec_ar_b, &row.stat_l_b, &row.stat_ar_b);
+    row.flags_a = fa->flags | (seed << GPUDIFF_OBJ_SEED_SHIFT);
+    row.flags_b = fb->flags | (seed << GPUDIFF_OBJ_SEED_SHIFT);
+}
+
+void PairEncoder::encode_nodes(const Node* a, const Node* b, uint32_t pair_id, uint32_t cluster_id,
+                               std::vector<uint8_t>& pool, gpudiff_pair_row& row) {
+    FlatObject* fa = nullptr;
+    FlatObject* fb = nullptr;
+    if (a && b) {
+        flatten_object(*a, flat_a);
+        flatten_object(*b, flat_b);
+        fa = &flat_a;
+        fb = &flat_b;
+    }
+    encode_flat(fa, fb, pair_id, cluster_id, pool, row);
+}
+
+void PairEncoder::encode_json(const uint8_t* a, size_t alen, const uint8_t* b, size_t blen, uint32_t pair_id,
+                              uint32_t cluster_id, std::vector<uint8_t>& pool, gpudiff_pair_row& row) {
+    arena_a.reset();
+    arena_b.reset();
+    Node na, nb;
+    bool oka = a && parser.parse_object(a, alen, arena_a, &na);
+    bool okb = oka && b && parser.parse_object(b, blen, arena_b, &nb);
+    encode_nodes(oka ? &na : nullptr, okb ? &nb : nullptr, pair_id, cluster_id, pool, row);
+}
+
+std::string render_path(const char* p, size_t n) {
+    std::string s;
+    size_t i = 0;
+    while (i + 5 <= n) {
+        uint8_t k = (uint8_t)p[i];
+        uint32_t v;
+        memcpy(&v, p + i + 1, 4);
+        i += 5;
+        if (k == 0x01) {
+            if (!s.empty()) s.push_back('.');
+            s.append(p + i, v);
+            i += v;
+        } else {
+            s += "[" + std::to_string(v) + "]";
+        }
+    }
+    return s;
+}
+
+}  // namespace gd

@@ -1,0 +1,88 @@
+// Host canonical encoder: decoded unstructured object -> sorted CSR leaf
+// segments (include/gpudiff_format.h).
+//
+// The leaf set it extracts is exactly what the reference predicates compare:
+//   spec region   = top-level keys except metadata/status with top-level
+//                   nulls dropped (specsyncer.go:30-39; a missing key reads as
+//                   nil, so `k: null` == absent), plus canonical labels and
+//                   annotations (GetLabels/GetAnnotations at specsyncer.go:23,26:
+//                   NestedStringMap, nil unless every value is a string)
+//   status region = the "status" subtree (statussyncer.go:22-24), a top-level
+//                   `status: null` contributes no leaves but sets HAS_STATUS.
+// Leaves are scalars and empty containers; paths are encoded component by
+// component (0x01 u32le(len) key | 0x02 u32le(index)) and hashed with XXH64.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gpudiff.h"
+#include "json.h"
+
+namespace gd {
+
+struct LeafRec {
+    uint64_t h;
+    uint64_t val;
+    uint32_t meta;
+    uint32_t path_off;
+    uint32_t path_len;
+    uint32_t vlen;
+    const char* vptr;
+};
+
+struct FlatObject {
+    std::vector<LeafRec> spec, stat;
+    std::string paths;   // concatenated path bytes
+    uint32_t flags = 0;  // GPUDIFF_OBJ_*
+    void clear() {
+        spec.clear();
+        stat.clear();
+        paths.clear();
+        flags = 0;
+    }
+};
+
+struct EncodeConfig {
+    uint32_t hash_bits = 64;
+    bool host_value_hash = false;
+};
+
+// Flattens a decoded top-level object into its spec/status leaves.
+void flatten_object(const Node& root, FlatObject& out);
+
+class PairEncoder {
+   public:
+    explicit PairEncoder(const EncodeConfig& cfg) : cfg_(cfg) {}
+    // Encodes one pair from JSON bytes; appends blob A then blob B to pool.
+    void encode_json(const uint8_t* a, size_t alen, const uint8_t* b, size_t blen, uint32_t pair_id,
+                     uint32_t cluster_id, std::vector<uint8_t>& pool, gpudiff_pair_row& row);
+    // Encodes one pair from decoded trees (nullptr = decode error).
+    void encode_nodes(const Node* a, const Node* b, uint32_t pair_id, uint32_t cluster_id,
+                      std::vector<uint8_t>& pool, gpudiff_pair_row& row);
+    // Assigns the pair seed, sorts, and writes both blobs.
+    void encode_flat(FlatObject* fa, FlatObject* fb, uint32_t pair_id, uint32_t cluster_id,
+                     std::vector<uint8_t>& pool, gpudiff_pair_row& row);
+    uint64_t leaves_written = 0;
+    uint64_t reseeded = 0;
+    uint64_t decode_errors = 0;
+
+    JsonParser parser;
+    Arena arena_a, arena_b;
+    FlatObject flat_a, flat_b;
+
+   private:
+    bool assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed);
+    void write_blob(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
+                    uint32_t* sar, uint32_t* tl, uint32_t* tar);
+    EncodeConfig cfg_;
+};
+
+// Status-region sentinel path bytes: [Key "status"]
+const std::string& status_path_bytes();
+
+// Renders encoded path bytes as "a.b[3].c".
+std::string render_path(const char* p, size_t n);
+
+}  // namespace gd

@@ -1,0 +1,45 @@
+// Launchers of the gpudiff HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpudiff_format.h"
+
+namespace gd {
+
+// Device buffers of one diff pass.  summary[]: 0 n_spec, 1 n_status,
+// 2 n_dirty, 3 total scratch cap, 4 overflow, 5 n_paths, 6..7 reserved.
+struct DiffBuffers {
+    const gpudiff_pair_row* rows;
+    const uint8_t* pool;
+    const uint32_t* pair_ids;
+    uint32_t n_pairs;
+    uint8_t* flags;
+    uint32_t* caps;
+    void* chunk_counts;  // uint4 per 64 pairs
+    uint32_t* summary;
+    uint32_t* spec_ids;
+    uint32_t* status_ids;
+    uint32_t* dirty_ids;
+    uint32_t* dirty_idx;
+    uint32_t* scratch_off;
+    uint32_t* path_count;
+    uint32_t* path_off;   // n_pairs + 1
+    uint32_t* tile_sums;
+    uint64_t* scratch_h;
+    uint8_t* scratch_k;
+    uint64_t scratch_cap;
+    uint64_t* out_h;
+    uint8_t* out_k;
+    uint64_t hash_mask;
+};
+
+hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
+                         uint32_t* pair_ids);
+hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool);
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b);
+hipError_t launch_compact(hipStream_t s, const DiffBuffers& b);
+hipError_t launch_join(hipStream_t s, const DiffBuffers& b);
+hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
+
+}  // namespace gd

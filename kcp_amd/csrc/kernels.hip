@@ -1,0 +1,665 @@
+// HIP kernels of the gpudiff engine, written for gfx950 (CDNA4, wave64).
+//
+//   K1 k_value_hash   XXH64 of every long string leaf value (ingest)
+//   K2 k_compare      spec/status decision per pair: 16-B-per-lane streaming
+//                     compare of the two canonical segments (one wave per
+//                     pair, 64 pairs per wave-chunk, ballot counts per chunk)
+//   K3 k_scan_chunks  exclusive scan of chunk counts (one workgroup)
+//      k_compact      ballot/prefix compaction of dirty pair IDs + scratch
+//                     slots for the changed-path join
+//   K4 k_join         wave-per-dirty-pair merge-join of the sorted leaf keys
+//                     in 64-key windows held in registers (cross-lane binary
+//                     search with ds_bpermute), byte-exact confirmation of
+//                     hash-equal long values, emits changed paths
+//   K5 k_scan_*       exclusive scan of per-pair path counts
+//   K6 k_copy_paths   compaction of the path scratch into the output CSR
+//
+// Semantics: DESIGN.md "Kernels"; reference predicates
+// pkg/syncer/specsyncer.go:17-41 and pkg/syncer/statussyncer.go:15-27.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpudiff.h"
+#include "kernels.h"
+#include "xxh64.h"
+
+namespace gd {
+
+constexpr uint32_t F_SPEC = 1u, F_STATUS = 2u, F_ERR = 4u;
+
+// ---------------------------------------------------------------- wave helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    uint32_t lo = shfl32((uint32_t)v, src), hi = shfl32((uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+__device__ __forceinline__ uint64_t mask_lt(uint32_t n) { return n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL); }
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        uint32_t o = shfl32(v, lane >= d ? lane - d : lane);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
+    return v;
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
+    return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
+}
+__device__ __forceinline__ bool meta_long(uint32_t m) { return (m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > 8u; }
+__device__ __forceinline__ uint32_t meta_arena(uint32_t m) { return meta_long(m) ? (((m >> 3) + 15u) & ~15u) : 0u; }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bool neq16(const u32x4& a, const u32x4& b) {
+    const u32x4 x = a ^ b;
+    return (x.x | x.y | x.z | x.w) != 0u;
+}
+
+// ---------------------------------------------------------------- K1
+// XXH64 over a value stored 16-byte aligned (zero padded) in the arena.
+__device__ uint64_t xxh64_a16(const uint4* p, uint32_t len, uint64_t seed) {
+    uint64_t h;
+    uint32_t stripes = len >> 5;
+    if (stripes) {
+        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+        for (uint32_t s = 0; s < stripes; s++) {
+            uint4 a = p[2 * s], b = p[2 * s + 1];
+            v1 = xround(v1, ((uint64_t)a.y << 32) | a.x);
+            v2 = xround(v2, ((uint64_t)a.w << 32) | a.z);
+            v3 = xround(v3, ((uint64_t)b.y << 32) | b.x);
+            v4 = xround(v4, ((uint64_t)b.w << 32) | b.z);
+        }
+        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = seed + XP5;
+    }
+    h += len;
+    uint32_t rem = len & 31u;
+    uint64_t w[4] = {0, 0, 0, 0};
+    if (rem) {
+        uint4 a = p[2 * stripes];
+        w[0] = ((uint64_t)a.y << 32) | a.x;
+        w[1] = ((uint64_t)a.w << 32) | a.z;
+        if (rem > 16) {
+            uint4 b = p[2 * stripes + 1];
+            w[2] = ((uint64_t)b.y << 32) | b.x;
+            w[3] = ((uint64_t)b.w << 32) | b.z;
+        }
+    }
+    h = xxh64_tail(h, w, rem);
+    return xavalanche(h);
+}
+
+// One wave per (row, object, region) item.
+__global__ __launch_bounds__(256) void k_value_hash(const gpudiff_pair_row* __restrict__ rows, uint32_t row_begin,
+                                                    uint32_t row_end, uint8_t* __restrict__ pool) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nitems = (row_end - row_begin) * 4u;
+    for (uint32_t it = wave; it < nitems; it += nwaves) {
+        const gpudiff_pair_row& r = rows[row_begin + (it >> 2)];
+        const bool b = it & 1u, st = it & 2u;
+        const uint64_t off = b ? r.off_b : r.off_a;
+        const uint32_t sl = b ? r.spec_l_b : r.spec_l_a, sar = b ? r.spec_ar_b : r.spec_ar_a;
+        const uint32_t L = st ? (b ? r.stat_l_b : r.stat_l_a) : sl;
+        const uint32_t AR = st ? (b ? r.stat_ar_b : r.stat_ar_a) : sar;
+        if (AR == 0 || L == 0) continue;
+        uint8_t* seg = pool + off + (st ? seg_bytes(sl, sar) : 0);
+        uint64_t* vals = (uint64_t*)(seg + 8ull * L);
+        const uint32_t* metas = (const uint32_t*)(seg + 16ull * L);
+        const uint4* arena = (const uint4*)(seg + ((20ull * L + 15ull) & ~15ull));
+        uint32_t run = 0;  // running arena byte offset
+        for (uint32_t w = 0; w < L; w += 64) {
+            const uint32_t i = w + lane;
+            const uint32_t m = i < L ? metas[i] : 0u;
+            const uint32_t asz = meta_arena(m);
+            const uint32_t incl = wave_incl_scan(asz);
+            if (asz) vals[i] = xxh64_a16(arena + ((run + incl - asz) >> 4), m >> 3, 0);
+            run += shfl32(incl, 63);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- K2
+struct PairDecision {
+    uint32_t flag;
+    uint32_t cap;
+};
+
+__device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, const uint8_t* __restrict__ pool,
+                                                     uint32_t lane) {
+    PairDecision d{0u, 0u};
+    if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) {
+        d.flag = F_SPEC | F_STATUS | F_ERR;
+        return d;
+    }
+    const bool spec_sz = r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b;
+    const bool has_st_b = (r.flags_b & GPUDIFF_OBJ_HAS_STATUS) != 0u;
+    const bool stat_sz = has_st_b && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b;
+    const uint64_t seg_a = seg_bytes(r.spec_l_a, r.spec_ar_a);
+    const uint64_t seg_b = seg_bytes(r.spec_l_b, r.spec_ar_b);
+    const uint32_t n1 = spec_sz ? (uint32_t)(seg_a >> 4) : 0u;
+    const uint32_t n2 = stat_sz ? (uint32_t)(seg_bytes(r.stat_l_a, r.stat_ar_a) >> 4) : 0u;
+    const u32x4* a1 = (const u32x4*)(pool + r.off_a);
+    const u32x4* b1 = (const u32x4*)(pool + r.off_b);
+    const u32x4* a2 = (const u32x4*)(pool + r.off_a + seg_a);
+    const u32x4* b2 = (const u32x4*)(pool + r.off_b + seg_b);
+    const uint32_t ntot = n1 + n2;
+    bool mis1 = false, mis2 = false;
+    for (uint32_t base = 0; base < ntot; base += 256) {
+        u32x4 va[4], vb[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = base + u * 64 + lane;
+            if (i < ntot) {
+                const bool in1 = i < n1;
+                const u32x4* pa = in1 ? a1 + i : a2 + (i - n1);
+                const u32x4* pb = in1 ? b1 + i : b2 + (i - n1);
+                va[u] = __builtin_nontemporal_load(pa);
+                vb[u] = __builtin_nontemporal_load(pb);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = base + u * 64 + lane;
+            if (i < ntot) {
+                const bool ne = neq16(va[u], vb[u]);
+                if (i < n1) mis1 |= ne;
+                else mis2 |= ne;
+            }
+        }
+    }
+    const bool spec_dirty = !spec_sz || ballot(mis1) != 0;
+    const bool stat_dirty = !stat_sz || ballot(mis2) != 0;
+    d.flag = (spec_dirty ? F_SPEC : 0u) | (stat_dirty ? F_STATUS : 0u);
+    d.cap = (spec_dirty ? r.spec_l_a + r.spec_l_b : 0u) +
+            (stat_dirty ? r.stat_l_a + r.stat_l_b + (has_st_b ? 0u : 1u) : 0u);
+    return d;
+}
+
+// One wave per chunk of 64 consecutive pairs; the wave walks its pairs in
+// order, all 64 lanes streaming both objects of a pair with 16-byte loads.
+__global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restrict__ rows,
+                                                 const uint8_t* __restrict__ pool, uint32_t n,
+                                                 uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
+                                                 uint4* __restrict__ chunk_counts) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nchunks = (n + 63u) >> 6;
+    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+        const uint32_t p0 = c << 6;
+        const uint32_t cnt = min(64u, n - p0);
+        uint32_t myflag = 0, mycap = 0;
+        for (uint32_t k = 0; k < cnt; k++) {
+            const gpudiff_pair_row r = rows[p0 + k];
+            const PairDecision d = compare_pair(r, pool, lane);
+            if (lane == k) {
+                myflag = d.flag;
+                mycap = d.cap;
+            }
+        }
+        if (lane < cnt) {
+            flags[p0 + lane] = (uint8_t)myflag;
+            if (myflag & (F_SPEC | F_STATUS)) caps[p0 + lane] = mycap;
+        }
+        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
+        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
+        const uint32_t nd = popc64(ballot(myflag & (F_SPEC | F_STATUS)));
+        const uint32_t cs = wave_sum((myflag & (F_SPEC | F_STATUS)) ? mycap : 0u);
+        if (lane == 0) chunk_counts[c] = make_uint4(ns, nt, nd, cs);
+    }
+}
+
+// ---------------------------------------------------------------- K3
+// Exclusive scan of per-chunk uint4 counts by one 1024-thread workgroup.
+// summary[0..3] = totals (n_spec, n_status, n_dirty, total scratch cap).
+__global__ __launch_bounds__(1024) void k_scan_chunks(uint4* __restrict__ cc, uint32_t nchunks,
+                                                      uint32_t* __restrict__ summary) {
+    __shared__ uint4 part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nchunks + 1023u) / 1024u;
+    const uint32_t b = min(nchunks, t * per), e = min(nchunks, b + per);
+    uint4 s = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = b; i < e; i++) {
+        uint4 v = cc[i];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        uint4 o = make_uint4(0, 0, 0, 0);
+        if (t >= d) o = part[t - d];
+        __syncthreads();
+        if (t >= d) {
+            uint4 v = part[t];
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            part[t] = v;
+        }
+        __syncthreads();
+    }
+    uint4 run = t ? part[t - 1] : make_uint4(0, 0, 0, 0);
+    for (uint32_t i = b; i < e; i++) {
+        uint4 v = cc[i];
+        cc[i] = run;
+        run.x += v.x; run.y += v.y; run.z += v.z; run.w += v.w;
+    }
+    if (t == 1023) {
+        uint4 tot = part[1023];
+        summary[0] = tot.x;
+        summary[1] = tot.y;
+        summary[2] = tot.z;
+        summary[3] = tot.w;
+    }
+}
+
+// One wave per chunk: ballot + prefix compaction into the ID lists.
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ flags, const uint32_t* __restrict__ caps,
+                                                 const uint32_t* __restrict__ pair_ids, uint32_t n,
+                                                 const uint4* __restrict__ cbase, uint32_t* __restrict__ spec_ids,
+                                                 uint32_t* __restrict__ status_ids, uint32_t* __restrict__ dirty_ids,
+                                                 uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t nchunks = (n + 63u) >> 6;
+    const uint64_t lt = mask_lt(lane);
+    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+        const uint32_t p = (c << 6) + lane;
+        const bool valid = p < n;
+        const uint32_t f = valid ? flags[p] : 0u;
+        const uint64_t bs = ballot(f & F_SPEC), bt = ballot(f & F_STATUS), bd = ballot(f & (F_SPEC | F_STATUS));
+        if (bd == 0) continue;
+        const uint4 base = cbase[c];
+        const bool dirty = (f & (F_SPEC | F_STATUS)) != 0u;
+        const uint32_t id = dirty ? pair_ids[p] : 0u;
+        const uint32_t cap = dirty ? caps[p] : 0u;
+        const uint32_t cincl = wave_incl_scan(cap);
+        if (f & F_SPEC) spec_ids[base.x + popc64(bs & lt)] = id;
+        if (f & F_STATUS) status_ids[base.y + popc64(bt & lt)] = id;
+        if (dirty) {
+            const uint32_t d = base.z + popc64(bd & lt);
+            dirty_ids[d] = id;
+            dirty_idx[d] = p;
+            scratch_off[d] = base.w + cincl - cap;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- K4
+struct RegionView {
+    const uint64_t* keys;
+    const uint64_t* vals;
+    const uint32_t* metas;
+    const uint8_t* arena;
+    uint32_t L;
+};
+
+__device__ __forceinline__ RegionView region_view(const uint8_t* pool, uint64_t off, uint32_t sl, uint32_t sar,
+                                                  bool status, uint32_t L) {
+    const uint8_t* seg = pool + off + (status ? seg_bytes(sl, sar) : 0);
+    RegionView v;
+    v.keys = (const uint64_t*)seg;
+    v.vals = (const uint64_t*)(seg + 8ull * L);
+    v.metas = (const uint32_t*)(seg + 16ull * L);
+    v.arena = seg + ((20ull * L + 15ull) & ~15ull);
+    v.L = L;
+    return v;
+}
+
+// number of tile keys (lanes < nt, ascending) strictly less than x
+__device__ __forceinline__ uint32_t tile_lower_bound(uint64_t x, uint64_t tile, uint32_t nt) {
+    uint32_t j = 0;
+#pragma unroll
+    for (uint32_t s = 64; s >= 1; s >>= 1) {
+        const uint32_t cand = j + s;
+        const uint64_t t = shfl64(tile, min(cand, 64u) - 1u);
+        if (cand <= nt && t < x) j = cand;
+    }
+    return j;
+}
+
+// byte-exact confirmation of two 16-aligned, zero padded values of equal length
+__device__ __forceinline__ bool bytes_differ(const uint8_t* a, const uint8_t* b, uint32_t len) {
+    const u32x4* pa = (const u32x4*)a;
+    const u32x4* pb = (const u32x4*)b;
+    const uint32_t n16 = (len + 15u) >> 4;
+    for (uint32_t k = 0; k < n16; k += 4) {
+        u32x4 xa[4], xb[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (k + u < n16) {
+                xa[u] = pa[k + u];
+                xb[u] = pb[k + u];
+            }
+        bool ne = false;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (k + u < n16) ne |= neq16(xa[u], xb[u]);
+        if (ne) return true;
+    }
+    return false;
+}
+
+// Merge-join of one region; returns the number of paths emitted.  Emission
+// order = ascending key (the union of both sorted key lists).
+template <bool EMIT>
+__device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_t region_bit,
+                                uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
+                                uint32_t lane) {
+    uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
+    const uint64_t lt = mask_lt(lane);
+    while (ia < A.L || ib < B.L) {
+        const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
+        const bool va = lane < na, vb = lane < nb;
+        const uint64_t ka = va ? A.keys[ia + lane] : 0ull;
+        const uint64_t kb = vb ? B.keys[ib + lane] : 0ull;
+        const uint32_t ma = va ? A.metas[ia + lane] : 0u;
+        const uint32_t mb = vb ? B.metas[ib + lane] : 0u;
+        const uint64_t xa = va ? A.vals[ia + lane] : 0ull;
+        const uint64_t xb = vb ? B.vals[ib + lane] : 0ull;
+        const bool endA = ia + na == A.L, endB = ib + nb == B.L;
+        const uint64_t lastA = na ? shfl64(ka, na - 1) : 0ull;
+        const uint64_t lastB = nb ? shfl64(kb, nb - 1) : 0ull;
+        // everything <= bound is resolvable in this window
+        bool inf = true;
+        uint64_t bound = 0;
+        if (!endA) { bound = lastA; inf = false; }
+        if (!endB) { bound = inf ? lastB : min(bound, lastB); inf = false; }
+        const bool inA = va && (inf || ka <= bound);
+        const bool inB = vb && (inf || kb <= bound);
+        // arena offsets of this window's long values
+        const uint32_t asA = meta_arena(ma), asB = meta_arena(mb);
+        const uint32_t incA = wave_incl_scan(asA), incB = wave_incl_scan(asB);
+        const uint32_t offA = arA + incA - asA, offB = arB + incB - asB;
+        // resolve A keys against the B window
+        const uint32_t jA = tile_lower_bound(ka, kb, nb);
+        const uint64_t kbj = shfl64(kb, min(jA, 63u));
+        const uint32_t mbj = shfl32(mb, min(jA, 63u));
+        const uint64_t xbj = shfl64(xb, min(jA, 63u));
+        const uint32_t obj = shfl32(offB, min(jA, 63u));
+        const bool matchA = inA && jA < nb && kbj == ka;
+        bool differ = matchA && (ma != mbj || xa != xbj);
+        if (matchA && !differ && meta_long(ma))
+            differ = bytes_differ(A.arena + offA, B.arena + obj, ma >> 3);
+        // resolve B keys against the A window
+        const uint32_t iB = tile_lower_bound(kb, ka, na);
+        const uint64_t kai = shfl64(ka, min(iB, 63u));
+        const bool matchB = inB && iB < na && kai == kb;
+        const bool emitA = inA && (!matchA || differ);
+        const bool emitB = inB && !matchB;
+        const uint64_t balA = ballot(emitA), balB = ballot(emitB);
+        if (EMIT) {
+            if (emitA) {
+                const uint32_t pos = popc64(balA & lt) + popc64(balB & mask_lt(jA));
+                out_h[out_base + outpos + pos] = ka;
+                out_k[out_base + outpos + pos] = region_bit | (matchA ? GPUDIFF_PATH_CHANGED : GPUDIFF_PATH_REMOVED);
+            }
+            if (emitB) {
+                const uint32_t pos = popc64(balB & lt) + popc64(balA & mask_lt(iB));
+                out_h[out_base + outpos + pos] = kb;
+                out_k[out_base + outpos + pos] = region_bit | GPUDIFF_PATH_ADDED;
+            }
+        }
+        outpos += popc64(balA) + popc64(balB);
+        const uint32_t ca = popc64(ballot(inA)), cb = popc64(ballot(inB));
+        arA += ca ? shfl32(incA, ca - 1) : 0u;
+        arB += cb ? shfl32(incB, cb - 1) : 0u;
+        ia += ca;
+        ib += cb;
+    }
+    return outpos;
+}
+
+__device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
+    // XXH64 of the 11 path bytes 01 06 00 00 00 's' 't' 'a' 't' 'u' 's'
+    // bytes: [0]=01 [1]=06 [2..4]=00 [5]='s' [6]='t' [7]='a' | [8]='t' [9]='u' [10]='s'
+    uint64_t w[4] = {0, 0, 0, 0};
+    w[0] = 0x01ull | (0x06ull << 8) | ((uint64_t)'s' << 40) | ((uint64_t)'t' << 48) | ((uint64_t)'a' << 56);
+    w[1] = (uint64_t)'t' | ((uint64_t)'u' << 8) | ((uint64_t)'s' << 16);
+    uint64_t h = (uint64_t)seed + XP5 + 11u;
+    h = xxh64_tail(h, w, 11);
+    return xavalanche(h) & mask;
+}
+
+template <bool EMIT>
+__device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
+                              uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane) {
+    if (f & F_ERR) return 0;
+    uint32_t n = 0;
+    if (f & F_SPEC) {
+        RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
+        RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
+        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane);
+    }
+    if (f & F_STATUS) {
+        RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
+        RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
+        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane);
+        if (!(r.flags_b & GPUDIFF_OBJ_HAS_STATUS)) {
+            if (EMIT && lane == 0) {
+                out_h[base + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
+                out_k[base + n] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+            }
+            n += 1;
+        }
+    }
+    return n;
+}
+
+// One wave per dirty pair.  Writes the pair's changed paths into its scratch
+// slot (sized by the cap computed in K2) and its count.
+__global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict__ rows,
+                                              const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
+                                              const uint32_t* __restrict__ dirty_idx,
+                                              const uint32_t* __restrict__ scratch_off, uint32_t* __restrict__ summary,
+                                              uint64_t scratch_cap, uint64_t mask, uint64_t* __restrict__ sh,
+                                              uint8_t* __restrict__ sk, uint32_t* __restrict__ path_count) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t ndirty = summary[2];
+    const bool fits = (uint64_t)summary[3] <= scratch_cap;
+    if (!fits && blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
+    for (uint32_t d = wave; d < ndirty; d += nwaves) {
+        const uint32_t p = dirty_idx[d];
+        const gpudiff_pair_row r = rows[p];
+        const uint32_t f = flags[p];
+        uint32_t n;
+        if (fits) n = join_pair<true>(r, f, pool, mask, sh, sk, scratch_off[d], lane);
+        else n = join_pair<false>(r, f, pool, mask, sh, sk, 0, lane);
+        if (lane == 0) path_count[d] = n;
+    }
+}
+
+// ---------------------------------------------------------------- K5
+// Exclusive scan of path_count[0..summary[2]) into path_off, 3 kernels.
+constexpr uint32_t SCAN_TILE = 4096;  // 256 threads x 16
+
+__global__ __launch_bounds__(256) void k_scan_tiles(const uint32_t* __restrict__ in, const uint32_t* __restrict__ summary,
+                                                    uint32_t* __restrict__ tile_sums) {
+    __shared__ uint32_t red[4];
+    const uint32_t n = summary[2];
+    const uint32_t base = blockIdx.x * SCAN_TILE;
+    if (base >= n) return;
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x; i < SCAN_TILE; i += 256) {
+        const uint32_t k = base + i;
+        if (k < n) s += in[k];
+    }
+    s = wave_sum(s);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(1024) void k_scan_top(uint32_t* __restrict__ tile_sums, uint32_t* __restrict__ summary) {
+    __shared__ uint32_t part[1024];
+    const uint32_t n = summary[2];
+    const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (ntiles + 1023u) / 1024u;
+    const uint32_t b = min(ntiles, t * per), e = min(ntiles, b + per);
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; i++) s += tile_sums[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        uint32_t o = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += o;
+        __syncthreads();
+    }
+    uint32_t run = t ? part[t - 1] : 0u;
+    for (uint32_t i = b; i < e; i++) {
+        const uint32_t v = tile_sums[i];
+        tile_sums[i] = run;
+        run += v;
+    }
+    if (t == 1023) summary[5] = part[1023];  // total paths
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ in, const uint32_t* __restrict__ summary,
+                                                    const uint32_t* __restrict__ tile_base, uint32_t* __restrict__ out) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t n = summary[2];
+    const uint32_t base = blockIdx.x * SCAN_TILE;
+    if (base > n) return;
+    if (base == n) {  // terminal offset
+        if (threadIdx.x == 0) out[n] = summary[5];
+        return;
+    }
+    // each thread owns 16 consecutive elements
+    const uint32_t t = threadIdx.x;
+    uint32_t v[16];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t i = base + t * 16 + k;
+        v[k] = i < n ? in[i] : 0u;
+        s += v[k];
+    }
+    const uint32_t incl = wave_incl_scan(s);
+    if (lane_id() == 63) wsum[t >> 6] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t w = 0; w < (t >> 6); w++) wbase += wsum[w];
+    uint32_t run = tile_base[blockIdx.x] + wbase + incl - s;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t i = base + t * 16 + k;
+        if (i < n) out[i] = run;
+        run += v[k];
+    }
+    if (base + SCAN_TILE >= n && t == 0) out[n] = summary[5];
+}
+
+// ---------------------------------------------------------------- K6
+__global__ __launch_bounds__(256) void k_copy_paths(const uint32_t* __restrict__ summary,
+                                                    const uint32_t* __restrict__ scratch_off,
+                                                    const uint32_t* __restrict__ path_off,
+                                                    const uint32_t* __restrict__ path_count,
+                                                    const uint64_t* __restrict__ sh, const uint8_t* __restrict__ sk,
+                                                    uint64_t* __restrict__ oh, uint8_t* __restrict__ ok) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t ndirty = summary[2];
+    if (summary[4]) return;  // scratch overflow: host re-runs with a larger slot pool
+    for (uint32_t d = wave; d < ndirty; d += nwaves) {
+        const uint32_t so = scratch_off[d], po = path_off[d], c = path_count[d];
+        for (uint32_t i = lane; i < c; i += 64) {
+            oh[po + i] = sh[so + i];
+            ok[po + i] = sk[so + i];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- ingest helper
+__global__ __launch_bounds__(256) void k_rebase_rows(gpudiff_pair_row* __restrict__ rows, uint32_t begin, uint32_t end,
+                                                     uint64_t base, uint32_t* __restrict__ pair_ids) {
+    const uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= end) return;
+    rows[i].off_a += base;
+    rows[i].off_b += base;
+    pair_ids[i] = rows[i].pair_id;
+}
+
+// ---------------------------------------------------------------- launchers
+static inline uint32_t grid_for(uint64_t waves_wanted, uint32_t cap_blocks) {
+    uint64_t blocks = (waves_wanted + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    return (uint32_t)(blocks < cap_blocks ? blocks : cap_blocks);
+}
+
+// 256 CUs x 8 resident 256-thread workgroups
+static constexpr uint32_t kPersistBlocks = 256 * 8;
+
+hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
+                         uint32_t* pair_ids) {
+    if (end <= begin) return hipSuccess;
+    k_rebase_rows<<<(end - begin + 255) / 256, 256, 0, s>>>(rows, begin, end, base, pair_ids);
+    return hipGetLastError();
+}
+
+hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool) {
+    if (end <= begin) return hipSuccess;
+    k_value_hash<<<grid_for((uint64_t)(end - begin) * 4, kPersistBlocks), 256, 0, s>>>(rows, begin, end, pool);
+    return hipGetLastError();
+}
+
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b) {
+    const uint32_t nchunks = (b.n_pairs + 63) / 64;
+    k_compare<<<grid_for(nchunks, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.n_pairs, b.flags, b.caps,
+                                                                 (uint4*)b.chunk_counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(hipStream_t s, const DiffBuffers& b) {
+    const uint32_t nchunks = (b.n_pairs + 63) / 64;
+    k_scan_chunks<<<1, 1024, 0, s>>>((uint4*)b.chunk_counts, nchunks, b.summary);
+    k_compact<<<grid_for(nchunks, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
+                                                                 (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
+                                                                 b.dirty_ids, b.dirty_idx, b.scratch_off);
+    return hipGetLastError();
+}
+
+hipError_t launch_join(hipStream_t s, const DiffBuffers& b) {
+    k_join<<<grid_for(b.n_pairs, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off,
+                                                                b.summary, b.scratch_cap, b.hash_mask, b.scratch_h,
+                                                                b.scratch_k, b.path_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit(hipStream_t s, const DiffBuffers& b) {
+    const uint32_t ntiles = (b.n_pairs + SCAN_TILE - 1) / SCAN_TILE + 1;
+    k_scan_tiles<<<ntiles, 256, 0, s>>>(b.path_count, b.summary, b.tile_sums);
+    k_scan_top<<<1, 1024, 0, s>>>(b.tile_sums, b.summary);
+    k_scan_apply<<<ntiles, 256, 0, s>>>(b.path_count, b.summary, b.tile_sums, b.path_off);
+    k_copy_paths<<<grid_for(b.n_pairs, kPersistBlocks), 256, 0, s>>>(b.summary, b.scratch_off, b.path_off,
+                                                                      b.path_count, b.scratch_h, b.scratch_k,
+                                                                      b.out_h, b.out_k);
+    return hipGetLastError();
+}
+
+}  // namespace gd

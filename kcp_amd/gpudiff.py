@@ -1,0 +1,410 @@
+"""ctypes binding of libgpudiff.so (include/gpudiff.h).
+
+This is the Python host side above the C-ABI.  It holds no diff logic: every
+decision is made by the HIP kernels behind the C-ABI.  If the shared library
+is missing the import fails loudly (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+from dataclasses import dataclass
+from typing import Any, Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgpudiff.so")
+
+OK = 0
+E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUND = range(-1, -9, -1)
+
+SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR = 0x1, 0x2, 0x4
+PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
+PATH_REGION_STATUS = 0x80
+OPT_TIMING, OPT_HOST_VALUE_HASH = 0x1, 0x2
+DEVICE_CURRENT, DEVICE_NONE = -1, -2
+
+OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_SEED_SHIFT = 0x1, 0x2, 8
+
+
+class GpuDiffError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        super().__init__("%s: %s (%d)" % (where, _lib.gpudiff_strerror(code).decode(), code))
+
+
+class Opts(C.Structure):
+    _fields_ = [("device", C.c_int32), ("encode_threads", C.c_uint32), ("stream", C.c_void_p),
+                ("flags", C.c_uint32), ("path_hash_bits", C.c_uint32)]
+
+
+class JsonPair(C.Structure):
+    _fields_ = [("old_json", C.c_void_p), ("old_len", C.c_size_t), ("new_json", C.c_void_p),
+                ("new_len", C.c_size_t), ("pair_id", C.c_uint32), ("cluster_id", C.c_uint32)]
+
+
+class PairRow(C.Structure):
+    _fields_ = [("off_a", C.c_uint64), ("off_b", C.c_uint64),
+                ("spec_l_a", C.c_uint32), ("spec_l_b", C.c_uint32),
+                ("spec_ar_a", C.c_uint32), ("spec_ar_b", C.c_uint32),
+                ("stat_l_a", C.c_uint32), ("stat_l_b", C.c_uint32),
+                ("stat_ar_a", C.c_uint32), ("stat_ar_b", C.c_uint32),
+                ("flags_a", C.c_uint32), ("flags_b", C.c_uint32),
+                ("pair_id", C.c_uint32), ("cluster_id", C.c_uint32)]
+
+
+ROW_DTYPE = np.dtype([("off_a", "<u8"), ("off_b", "<u8"), ("spec_l_a", "<u4"), ("spec_l_b", "<u4"),
+                      ("spec_ar_a", "<u4"), ("spec_ar_b", "<u4"), ("stat_l_a", "<u4"), ("stat_l_b", "<u4"),
+                      ("stat_ar_a", "<u4"), ("stat_ar_b", "<u4"), ("flags_a", "<u4"), ("flags_b", "<u4"),
+                      ("pair_id", "<u4"), ("cluster_id", "<u4")])
+assert ROW_DTYPE.itemsize == 64
+
+
+class HBatchInfo(C.Structure):
+    _fields_ = [("n_pairs", C.c_size_t), ("rows", C.c_void_p), ("pool", C.c_void_p), ("pool_bytes", C.c_uint64),
+                ("total_leaves", C.c_uint64), ("n_decode_errors", C.c_uint64), ("n_reseeded", C.c_uint64)]
+
+
+class Result(C.Structure):
+    _fields_ = [("n_pairs", C.c_size_t), ("pair_flags", C.c_void_p),
+                ("n_spec_dirty", C.c_size_t), ("spec_dirty_ids", C.c_void_p),
+                ("n_status_dirty", C.c_size_t), ("status_dirty_ids", C.c_void_p),
+                ("n_dirty", C.c_size_t), ("dirty_ids", C.c_void_p), ("path_offsets", C.c_void_p),
+                ("n_paths", C.c_size_t), ("path_hashes", C.c_void_p), ("path_kinds", C.c_void_p),
+                ("internal_", C.c_void_p)]
+
+
+class DeviceView(C.Structure):
+    _fields_ = [("pair_flags", C.c_void_p), ("spec_dirty_ids", C.c_void_p), ("status_dirty_ids", C.c_void_p),
+                ("dirty_ids", C.c_void_p), ("counts", C.c_void_p)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("n_pairs", C.c_uint64), ("pool_bytes", C.c_uint64), ("total_leaves", C.c_uint64),
+                ("compare_bytes", C.c_uint64)]
+
+
+class Timings(C.Structure):
+    _fields_ = [("value_hash_ms", C.c_float), ("compare_ms", C.c_float), ("compact_ms", C.c_float),
+                ("join_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float)]
+
+
+# (name, restype, argtypes) for every symbol of include/gpudiff.h
+_P = C.c_void_p
+SIGNATURES = [
+    ("gpudiff_strerror", C.c_char_p, [C.c_int]),
+    ("gpudiff_abi_version", C.c_int, []),
+    ("gpudiff_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("gpudiff_open", C.c_int, [C.POINTER(Opts), C.POINTER(_P)]),
+    ("gpudiff_close", None, [_P]),
+    ("gpudiff_encode_pairs", C.c_int, [_P, C.POINTER(JsonPair), C.c_size_t, C.POINTER(_P)]),
+    ("gpudiff_hbatch_info_get", C.c_int, [_P, C.POINTER(HBatchInfo)]),
+    ("gpudiff_hbatch_free", None, [_P, _P]),
+    ("gpudiff_dbatch_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
+    ("gpudiff_dbatch_append", C.c_int, [_P, _P, _P]),
+    ("gpudiff_dbatch_reset", C.c_int, [_P, _P]),
+    ("gpudiff_dbatch_stats_get", C.c_int, [_P, C.POINTER(BatchStats)]),
+    ("gpudiff_dbatch_device_view", C.c_int, [_P, C.POINTER(DeviceView)]),
+    ("gpudiff_dbatch_read_pool", C.c_int, [_P, _P, C.c_uint64, C.c_void_p, C.c_uint64]),
+    ("gpudiff_dbatch_free", None, [_P, _P]),
+    ("gpudiff_diff", C.c_int, [_P, _P, C.POINTER(C.c_uint64)]),
+    ("gpudiff_wait", C.c_int, [_P, C.c_uint64, C.POINTER(Result)]),
+    ("gpudiff_result_release", None, [_P, C.POINTER(Result)]),
+    ("gpudiff_last_timings", C.c_int, [_P, C.POINTER(Timings)]),
+    ("gpudiff_sync", C.c_int, [_P]),
+    ("gpudiff_submit", C.c_int, [_P, C.POINTER(JsonPair), C.c_size_t, C.POINTER(C.c_uint64)]),
+    ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
+    ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
+    ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
+                                       C.c_uint32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+]
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libgpudiff.so not built (run `python -m kcp_amd.build`); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = _load()
+
+
+def lib() -> C.CDLL:
+    return _lib
+
+
+def _chk(rc: int, where: str):
+    if rc != OK:
+        raise GpuDiffError(rc, where)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _chk(_lib.gpudiff_device_count(C.byref(n)), "gpudiff_device_count")
+    return n.value
+
+
+def to_json_bytes(obj: Union[bytes, bytearray, str, dict]) -> bytes:
+    if isinstance(obj, (bytes, bytearray)):
+        return bytes(obj)
+    if isinstance(obj, str):
+        return obj.encode()
+    return json.dumps(obj, separators=(",", ":")).encode()
+
+
+@dataclass
+class DiffResult:
+    """Host copy of one batch's results (all arrays in batch order)."""
+    pair_flags: np.ndarray          # u8 [n_pairs]
+    spec_dirty_ids: np.ndarray      # u32
+    status_dirty_ids: np.ndarray    # u32
+    dirty_ids: np.ndarray           # u32
+    path_offsets: np.ndarray        # u32 [n_dirty + 1]
+    path_hashes: np.ndarray         # u64
+    path_kinds: np.ndarray          # u8
+
+    def paths_of(self, k: int) -> List[Tuple[int, int]]:
+        """[(hash, kind)] of the k-th dirty pair."""
+        b, e = int(self.path_offsets[k]), int(self.path_offsets[k + 1])
+        return list(zip(self.path_hashes[b:e].tolist(), self.path_kinds[b:e].tolist()))
+
+
+def _arr(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    ct = np.ctypeslib.as_ctypes_type(np.dtype(dtype))
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).copy()
+
+
+class HostBatch:
+    def __init__(self, engine: "Engine", handle: int, keep: Any):
+        self.engine = engine
+        self.h = C.c_void_p(handle)
+        self._keep = keep
+
+    def info(self) -> HBatchInfo:
+        inf = HBatchInfo()
+        _chk(_lib.gpudiff_hbatch_info_get(self.h, C.byref(inf)), "gpudiff_hbatch_info_get")
+        return inf
+
+    def rows(self) -> np.ndarray:
+        inf = self.info()
+        if inf.n_pairs == 0:
+            return np.zeros(0, dtype=ROW_DTYPE)
+        buf = (C.c_uint8 * (inf.n_pairs * 64)).from_address(inf.rows)
+        return np.frombuffer(bytes(buf), dtype=ROW_DTYPE)
+
+    def pool(self) -> bytes:
+        inf = self.info()
+        return C.string_at(inf.pool, inf.pool_bytes) if inf.pool_bytes else b""
+
+    def free(self):
+        if self.h:
+            _lib.gpudiff_hbatch_free(self.engine.ctx, self.h)
+            self.h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceBatch:
+    def __init__(self, engine: "Engine", pool_bytes: int, max_pairs: int):
+        self.engine = engine
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_dbatch_create(engine.ctx, pool_bytes, max_pairs, C.byref(h)), "gpudiff_dbatch_create")
+        self.h = h
+
+    def append(self, hb: HostBatch):
+        _chk(_lib.gpudiff_dbatch_append(self.engine.ctx, self.h, hb.h), "gpudiff_dbatch_append")
+
+    def reset(self):
+        _chk(_lib.gpudiff_dbatch_reset(self.engine.ctx, self.h), "gpudiff_dbatch_reset")
+
+    def stats(self) -> BatchStats:
+        st = BatchStats()
+        _chk(_lib.gpudiff_dbatch_stats_get(self.h, C.byref(st)), "gpudiff_dbatch_stats_get")
+        return st
+
+    def device_view(self) -> DeviceView:
+        v = DeviceView()
+        _chk(_lib.gpudiff_dbatch_device_view(self.h, C.byref(v)), "gpudiff_dbatch_device_view")
+        return v
+
+    def read_pool(self, off: int, nbytes: int) -> bytes:
+        buf = C.create_string_buffer(max(nbytes, 1))
+        _chk(_lib.gpudiff_dbatch_read_pool(self.engine.ctx, self.h, off, buf, nbytes), "gpudiff_dbatch_read_pool")
+        return buf.raw[:nbytes]
+
+    def free(self):
+        if self.h:
+            _lib.gpudiff_dbatch_free(self.engine.ctx, self.h)
+            self.h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One gpudiff context (one GPU, one stream, one submitting thread)."""
+
+    def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
+                 timing: bool = False, path_hash_bits: int = 64, host_value_hash: bool = False):
+        o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
+                 flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0),
+                 path_hash_bits=path_hash_bits)
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_open(C.byref(o), C.byref(h)), "gpudiff_open")
+        self.ctx = h
+        self.path_hash_bits = path_hash_bits
+
+    def close(self):
+        if self.ctx:
+            _lib.gpudiff_close(self.ctx)
+            self.ctx = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- encoding
+    @staticmethod
+    def _pairs(pairs: Sequence[Tuple[Any, Any]], ids: Optional[Sequence[int]] = None,
+               clusters: Optional[Sequence[int]] = None):
+        n = len(pairs)
+        arr = (JsonPair * max(n, 1))()
+        keep = []
+        for i, (a, b) in enumerate(pairs):
+            ab, bb = to_json_bytes(a), to_json_bytes(b)
+            ca = C.create_string_buffer(ab, len(ab)) if ab else C.create_string_buffer(1)
+            cb = C.create_string_buffer(bb, len(bb)) if bb else C.create_string_buffer(1)
+            keep += [ca, cb]
+            arr[i].old_json = C.cast(ca, C.c_void_p)
+            arr[i].old_len = len(ab)
+            arr[i].new_json = C.cast(cb, C.c_void_p)
+            arr[i].new_len = len(bb)
+            arr[i].pair_id = ids[i] if ids is not None else i
+            arr[i].cluster_id = clusters[i] if clusters is not None else 0
+        return arr, n, keep
+
+    def encode(self, pairs, ids=None, clusters=None) -> HostBatch:
+        arr, n, keep = self._pairs(pairs, ids, clusters)
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_encode_pairs(self.ctx, arr, n, C.byref(h)), "gpudiff_encode_pairs")
+        return HostBatch(self, h.value, None)
+
+    # ---- device
+    def device_batch(self, pool_bytes: int, max_pairs: int) -> DeviceBatch:
+        return DeviceBatch(self, pool_bytes, max_pairs)
+
+    def diff(self, db: DeviceBatch) -> int:
+        t = C.c_uint64()
+        _chk(_lib.gpudiff_diff(self.ctx, db.h, C.byref(t)), "gpudiff_diff")
+        return t.value
+
+    def wait(self, ticket: int) -> DiffResult:
+        r = Result()
+        _chk(_lib.gpudiff_wait(self.ctx, ticket, C.byref(r)), "gpudiff_wait")
+        try:
+            out = DiffResult(
+                pair_flags=_arr(r.pair_flags, r.n_pairs, np.uint8),
+                spec_dirty_ids=_arr(r.spec_dirty_ids, r.n_spec_dirty, np.uint32),
+                status_dirty_ids=_arr(r.status_dirty_ids, r.n_status_dirty, np.uint32),
+                dirty_ids=_arr(r.dirty_ids, r.n_dirty, np.uint32),
+                path_offsets=_arr(r.path_offsets, r.n_dirty + 1, np.uint32),
+                path_hashes=_arr(r.path_hashes, r.n_paths, np.uint64),
+                path_kinds=_arr(r.path_kinds, r.n_paths, np.uint8))
+        finally:
+            _lib.gpudiff_result_release(self.ctx, C.byref(r))
+        return out
+
+    def sync(self):
+        _chk(_lib.gpudiff_sync(self.ctx), "gpudiff_sync")
+
+    def timings(self) -> Timings:
+        t = Timings()
+        _chk(_lib.gpudiff_last_timings(self.ctx, C.byref(t)), "gpudiff_last_timings")
+        return t
+
+    def submit(self, pairs, ids=None, clusters=None) -> int:
+        arr, n, keep = self._pairs(pairs, ids, clusters)
+        t = C.c_uint64()
+        _chk(_lib.gpudiff_submit(self.ctx, arr, n, C.byref(t)), "gpudiff_submit")
+        return t.value
+
+    def diff_pairs(self, pairs, ids=None, clusters=None) -> DiffResult:
+        return self.wait(self.submit(pairs, ids, clusters))
+
+    # ---- single pair drop-ins
+    def spec_equal(self, old, new) -> bool:
+        a, b = to_json_bytes(old), to_json_bytes(new)
+        eq = C.c_int()
+        rc = _lib.gpudiff_spec_equal(self.ctx, a, len(a), b, len(b), C.byref(eq))
+        if rc not in (OK, E_DECODE):
+            _chk(rc, "gpudiff_spec_equal")
+        return bool(eq.value)
+
+    def status_equal(self, old, new) -> bool:
+        a, b = to_json_bytes(old), to_json_bytes(new)
+        eq = C.c_int()
+        rc = _lib.gpudiff_status_equal(self.ctx, a, len(a), b, len(b), C.byref(eq))
+        if rc not in (OK, E_DECODE):
+            _chk(rc, "gpudiff_status_equal")
+        return bool(eq.value)
+
+
+def resolve_path(old, new, path_hash: int, path_kind: int, path_hash_bits: int = 64) -> str:
+    a, b = to_json_bytes(old), to_json_bytes(new)
+    buf = C.create_string_buffer(4096)
+    n = C.c_size_t()
+    _chk(_lib.gpudiff_resolve_path(a, len(a), b, len(b), path_hash, path_kind, path_hash_bits, buf, 4096,
+                                   C.byref(n)), "gpudiff_resolve_path")
+    if n.value >= 4096:
+        buf = C.create_string_buffer(n.value + 1)
+        _chk(_lib.gpudiff_resolve_path(a, len(a), b, len(b), path_hash, path_kind, path_hash_bits, buf,
+                                       n.value + 1, C.byref(n)), "gpudiff_resolve_path")
+    return buf.value.decode("utf-8", "replace")
+
+
+# ------------------------------------------------------------------ decoding helpers (tests / tooling)
+
+def decode_segment(pool: bytes, off: int, L: int, arena: int):
+    """Canonical segment -> list of (key, val, meta, value_bytes)."""
+    keys = np.frombuffer(pool, dtype="<u8", count=L, offset=off) if L else np.zeros(0, "<u8")
+    vals = np.frombuffer(pool, dtype="<u8", count=L, offset=off + 8 * L) if L else np.zeros(0, "<u8")
+    metas = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 16 * L) if L else np.zeros(0, "<u4")
+    head = ((20 * L) + 15) & ~15
+    ar = off + head
+    out = []
+    for k, v, m in zip(keys.tolist(), vals.tolist(), metas.tolist()):
+        tag, ln = m & 7, m >> 3
+        if tag == 5 and ln > 8:
+            vb = pool[ar:ar + ln]
+            ar += (ln + 15) & ~15
+        elif tag == 5:
+            vb = int(v).to_bytes(8, "little")[:ln]
+        elif tag in (3, 4):
+            vb = int(v).to_bytes(8, "little")
+        else:
+            vb = b""
+        out.append((k, v, m, vb))
+    assert ar == off + head + arena, (ar, off, head, arena)
+    return out
+
+
+def segment_bytes(L: int, arena: int) -> int:
+    return (((20 * L) + 15) & ~15) + arena

@@ -1,0 +1,166 @@
+"""CPU tests of the host canonical encoder (product code) against the oracle's
+independent restatement of the leaf extraction (oracle/gpudiff_oracle.py).
+
+These run without a GPU: the encoder is host code behind the C-ABI
+(gpudiff_encode_pairs on a GPUDIFF_DEVICE_NONE context)."""
+import json
+import random
+
+import numpy as np
+import pytest
+import xxhash
+from hypothesis import given, settings, strategies as st
+
+from kcp_amd import gpudiff as G
+from oracle import gpudiff_oracle as O
+from tests.golden.kat_cases import BASE, J, cases
+
+CASES = cases()
+
+
+@pytest.fixture(scope="module")
+def host_engine():
+    e = G.Engine(device=G.DEVICE_NONE, encode_threads=4)
+    yield e
+    e.close()
+
+
+def expected_segments(a_json: bytes, b_json: bytes, bits: int = 64):
+    """Oracle view: (seed, [(key, tag, bytes)] for spec/status of A and B, flags)."""
+    try:
+        a = O.go_json_decode(a_json)
+        b = O.go_json_decode(b_json)
+    except O.DecodeError:
+        return None
+    sa, sb, ta, tb = O.spec_leaves(a), O.spec_leaves(b), O.status_leaves(a), O.status_leaves(b)
+    seed = O.pair_seed(sa, sb, ta, tb, bits)
+    if seed < 0:
+        return None
+    mask = (1 << bits) - 1
+
+    def seg(leaves):
+        out = [(O.path_hash(p, seed) & mask, tag, vb) for p, (tag, vb) in leaves.items()]
+        return sorted(out)
+
+    fa = (O.OBJ_HAS_STATUS if False else 0)
+    return dict(seed=seed, spec_a=seg(sa), spec_b=seg(sb), stat_a=seg(ta), stat_b=seg(tb),
+                has_a="status" in a, has_b="status" in b)
+
+
+def actual_segments(hb: G.HostBatch):
+    pool = hb.pool()
+    out = []
+    for r in hb.rows():
+        if r["flags_a"] & G.OBJ_DECODE_ERR:
+            out.append(None)
+            continue
+
+        def segs(off, sl, sar, tl, tar):
+            s = G.decode_segment(pool, off, sl, sar)
+            t = G.decode_segment(pool, off + G.segment_bytes(sl, sar), tl, tar)
+            f = lambda lst: [(k, m & 7, vb) for (k, v, m, vb) in lst]
+            return f(s), f(t)
+
+        sa, ta = segs(int(r["off_a"]), int(r["spec_l_a"]), int(r["spec_ar_a"]), int(r["stat_l_a"]), int(r["stat_ar_a"]))
+        sb, tb = segs(int(r["off_b"]), int(r["spec_l_b"]), int(r["spec_ar_b"]), int(r["stat_l_b"]), int(r["stat_ar_b"]))
+        out.append(dict(seed=int(r["flags_a"]) >> G.OBJ_SEED_SHIFT, spec_a=sa, spec_b=sb, stat_a=ta, stat_b=tb,
+                        has_a=bool(r["flags_a"] & G.OBJ_HAS_STATUS), has_b=bool(r["flags_b"] & G.OBJ_HAS_STATUS)))
+    return out
+
+
+def check_pairs(engine, pairs, bits=64):
+    hb = engine.encode(pairs)
+    got = actual_segments(hb)
+    for (a, b), g in zip(pairs, got):
+        exp = expected_segments(G.to_json_bytes(a), G.to_json_bytes(b), bits)
+        assert g == exp, (a, b)
+    return hb
+
+
+def test_kat_encoding(host_engine):
+    hb = check_pairs(host_engine, [(a, b) for _, a, b, _, _ in CASES])
+    inf = hb.info()
+    assert inf.n_decode_errors == 2  # x11 truncated JSON, x20 trailing garbage
+
+
+def test_rows_layout(host_engine):
+    hb = host_engine.encode([(J(BASE), J(BASE))], ids=[77], clusters=[5])
+    r = hb.rows()[0]
+    assert r["pair_id"] == 77 and r["cluster_id"] == 5
+    assert r["off_a"] % 16 == 0 and r["off_b"] % 16 == 0
+    assert r["spec_ar_a"] % 16 == 0
+    # identical objects -> byte-identical segments
+    pool = hb.pool()
+    la = G.segment_bytes(int(r["spec_l_a"]), int(r["spec_ar_a"])) + G.segment_bytes(int(r["stat_l_a"]),
+                                                                                        int(r["stat_ar_a"]))
+    assert pool[r["off_a"]:r["off_a"] + la] == pool[r["off_b"]:r["off_b"] + la]
+
+
+def test_value_hash_host_matches_xxhash():
+    e = G.Engine(device=G.DEVICE_NONE, host_value_hash=True)
+    hb = e.encode([(J(BASE), J(BASE))])
+    pool = hb.pool()
+    r = hb.rows()[0]
+    n_long = 0
+    for (k, v, m, vb) in G.decode_segment(pool, int(r["off_a"]), int(r["spec_l_a"]), int(r["spec_ar_a"])):
+        if (m & 7) == 5 and (m >> 3) > 8:
+            assert v == xxhash.xxh64_intdigest(vb)
+            n_long += 1
+    assert n_long > 5
+    e.close()
+
+
+def test_multithreaded_matches_single(host_engine):
+    rnd = random.Random(7)
+    pairs = []
+    for i in range(600):
+        o = json.loads(J(BASE))
+        o["spec"]["replicas"] = rnd.randint(0, 5)
+        o["metadata"]["labels"]["k%d" % (i % 7)] = "v" * rnd.randint(0, 20)
+        pairs.append((J(BASE), J(o)))
+    e1 = G.Engine(device=G.DEVICE_NONE, encode_threads=1)
+    h1 = e1.encode(pairs)
+    h4 = host_engine.encode(pairs)
+    assert h1.pool() == h4.pool()
+    assert (h1.rows() == h4.rows()).all()
+    e1.close()
+
+
+def test_collision_reseed_small_hash():
+    e = G.Engine(device=G.DEVICE_NONE, path_hash_bits=8)
+    pairs = [(a, b) for _, a, b, _, _ in CASES[:12]]
+    hb = check_pairs(e, pairs, bits=8)
+    assert hb.info().n_reseeded > 0
+    e.close()
+
+
+_scalar = st.one_of(st.none(), st.booleans(), st.integers(-(1 << 63), (1 << 63) - 1),
+                    st.floats(allow_nan=False, allow_infinity=False),
+                    st.text(max_size=20))
+_tree = st.recursive(_scalar, lambda ch: st.one_of(st.lists(ch, max_size=4),
+                                                   st.dictionaries(st.text(max_size=6), ch, max_size=4)),
+                     max_leaves=20)
+_obj = st.fixed_dictionaries({}, optional={
+    "spec": _tree, "status": _tree, "data": _tree, "kind": _scalar,
+    "metadata": st.fixed_dictionaries({}, optional={
+        "labels": st.one_of(st.none(), st.dictionaries(st.text(max_size=5), st.one_of(st.text(max_size=12),
+                                                                                       st.integers(0, 1)),
+                                                       max_size=3)),
+        "annotations": st.dictionaries(st.text(max_size=5), st.text(max_size=30), max_size=3)})})
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.tuples(_obj, _obj), min_size=1, max_size=6))
+def test_random_encoding(pairs):
+    e = G.Engine(device=G.DEVICE_NONE, encode_threads=1)
+    check_pairs(e, [(json.dumps(a).encode(), json.dumps(b).encode()) for a, b in pairs])
+    e.close()
+
+
+def test_resolve_path():
+    a = J(BASE)
+    o = json.loads(a)
+    o["spec"]["template"]["spec"]["containers"][0]["image"] = "busybox:1.26"
+    r = O.diff_pair(a, J(o))
+    (h, region, kind, p), = r["paths"]
+    assert G.resolve_path(a, J(o), h, kind | (0x80 if region else 0)) == "spec.template.spec.containers[0].image"

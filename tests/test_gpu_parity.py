@@ -1,0 +1,161 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle, bit-exact.
+
+Covers the Appendix A.4 KAT table, mixed synthetic populations (configs 1-4
+shapes, 5% mutated), deep objects (>64 leaves per region -> multi-window
+merge-join, values >32 B -> XXH64 stripes), forced path-hash collisions,
+multi-chunk batches (scan tiles), appends, single-pair drop-ins, and K1's
+device value hashes against the xxhash package."""
+import json
+import random
+
+import numpy as np
+import pytest
+import xxhash
+
+from kcp_amd import gpudiff as G
+from oracle import gpudiff_oracle as O
+from tests.golden.kat_cases import BASE, J, cases
+from tests.parity import assert_matches, oracle_batch
+from tests.workload import make_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    assert G.device_count() > 0, "no GPU visible"
+    e = G.Engine(device=0, encode_threads=8, timing=True)
+    yield e
+    e.close()
+
+
+def test_kat(eng):
+    cs = cases()
+    pairs = [(a, b) for _, a, b, _, _ in cs]
+    res = eng.diff_pairs(pairs)
+    exp = assert_matches(res, pairs)
+    for (name, a, b, se, st), r in zip(cs, exp):
+        if se is not None:
+            assert r["spec_dirty"] == (not se), name
+
+
+def test_empty_batch(eng):
+    res = eng.diff_pairs([])
+    assert res.pair_flags.size == 0 and res.dirty_ids.size == 0 and res.path_offsets.tolist() == [0]
+
+
+def test_mixed_population(eng):
+    pairs, cl, muts = make_pairs(3000, seed=1)
+    ids = [1000 + 3 * i for i in range(len(pairs))]
+    res = eng.diff_pairs(pairs, ids=ids, clusters=cl)
+    assert_matches(res, pairs, ids=ids)
+
+
+def test_all_mutated_many_chunks(eng):
+    # > SCAN_TILE dirty pairs and > 64-pair chunks, every pair dirty
+    pairs, _, _ = make_pairs(5000, seed=2, mix=(("cm", 0.5), ("deploy", 0.5)), mutate_frac=1.0, pretty_frac=0)
+    res = eng.diff_pairs(pairs)
+    assert_matches(res, pairs)
+
+
+def test_deep_objects(eng):
+    pairs, _, _ = make_pairs(300, seed=3, mix=(("crd", 1.0),), mutate_frac=0.5, crd_leaves=1500)
+    res = eng.diff_pairs(pairs)
+    assert_matches(res, pairs)
+
+
+def test_long_values_and_list_shift(eng):
+    rnd = random.Random(4)
+    pairs = []
+    for i in range(200):
+        a = json.loads(J(BASE))
+        a["spec"]["blob"] = "".join(rnd.choice("ab") for _ in range(rnd.randint(9, 300)))
+        a["spec"]["items"] = ["item-%03d-%s" % (k, "x" * rnd.randint(0, 40)) for k in range(rnd.randint(60, 200))]
+        b = json.loads(json.dumps(a))
+        c = i % 4
+        if c == 0:
+            b["spec"]["blob"] = b["spec"]["blob"][:-1] + ("a" if b["spec"]["blob"][-1] == "b" else "b")
+        elif c == 1:
+            del b["spec"]["items"][len(b["spec"]["items"]) // 2]
+        elif c == 2:
+            b["spec"]["items"].insert(3, "new")
+        pairs.append((J(a), J(b)))
+    res = eng.diff_pairs(pairs)
+    assert_matches(res, pairs)
+
+
+def test_forced_collisions():
+    e = G.Engine(device=0, path_hash_bits=8)
+    pairs, _, _ = make_pairs(200, seed=5, mix=(("cm", 0.5), ("deploy", 0.5)), mutate_frac=0.5)
+    res = e.diff_pairs(pairs)
+    assert_matches(res, pairs, hash_bits=8)
+    e.close()
+
+
+def test_host_vs_device_value_hash(eng):
+    pairs, _, _ = make_pairs(400, seed=6, mutate_frac=0.3)
+    e2 = G.Engine(device=0, host_value_hash=True)
+    r1 = eng.diff_pairs(pairs)
+    r2 = e2.diff_pairs(pairs)
+    for f in ("pair_flags", "spec_dirty_ids", "status_dirty_ids", "dirty_ids", "path_offsets", "path_hashes",
+              "path_kinds"):
+        assert np.array_equal(getattr(r1, f), getattr(r2, f)), f
+    e2.close()
+
+
+def test_k1_value_hashes_on_device(eng):
+    pairs, _, _ = make_pairs(100, seed=7)
+    hb = eng.encode(pairs)
+    info = hb.info()
+    db = eng.device_batch(info.pool_bytes + 1024, len(pairs))
+    db.append(hb)
+    eng.sync()
+    pool = db.read_pool(0, info.pool_bytes)
+    rows = hb.rows()
+    checked = 0
+    for r in rows:
+        for off, sl, sar in ((int(r["off_a"]), int(r["spec_l_a"]), int(r["spec_ar_a"])),
+                             (int(r["off_b"]), int(r["spec_l_b"]), int(r["spec_ar_b"]))):
+            for (k, v, m, vb) in G.decode_segment(pool, off, sl, sar):
+                if (m & 7) == 5 and (m >> 3) > 8:
+                    assert v == xxhash.xxh64_intdigest(vb)
+                    checked += 1
+    assert checked > 1000
+    db.free()
+    hb.free()
+
+
+def test_append_chunks_and_rediff(eng):
+    pairs, cl, _ = make_pairs(1500, seed=8, mutate_frac=0.1)
+    chunks = [pairs[0:100], pairs[100:900], pairs[900:]]
+    hbs = [eng.encode(c, ids=list(range(s, s + len(c)))) for c, s in zip(chunks, (0, 100, 900))]
+    total = sum(h.info().pool_bytes for h in hbs)
+    db = eng.device_batch(total + 4096, len(pairs))
+    for h in hbs:
+        db.append(h)
+    st = db.stats()
+    assert st.n_pairs == len(pairs) and st.pool_bytes == total
+    r1 = eng.wait(eng.diff(db))
+    exp = assert_matches(r1, pairs)
+    r2 = eng.wait(eng.diff(db))  # re-diff of the resident batch is identical
+    assert_matches(r2, pairs, exp=exp)
+    t = eng.timings()
+    assert t.compare_ms > 0 and t.total_ms >= t.compare_ms
+    db.free()
+
+
+def test_single_pair_dropins(eng):
+    for name, a, b, se, st in cases():
+        r = O.diff_pair(a, b)
+        assert eng.spec_equal(a, b) == (not r["spec_dirty"]), name
+        assert eng.status_equal(a, b) == (not r["status_dirty"]), name
+
+
+def test_submit_pipelining(eng):
+    # two tickets in flight on the submit ring
+    p1, _, _ = make_pairs(300, seed=9, mutate_frac=0.2)
+    p2, _, _ = make_pairs(500, seed=10, mutate_frac=0.2)
+    t1 = eng.submit(p1)
+    t2 = eng.submit(p2)
+    assert_matches(eng.wait(t2), p2)
+    assert_matches(eng.wait(t1), p1)
