@@ -158,6 +158,11 @@ void gpudiff_close(gpudiff_ctx* ctx);
 int gpudiff_encode_pairs(gpudiff_ctx* ctx, const gpudiff_json_pair* pairs, size_t n,
                          gpudiff_hbatch** out);
 int gpudiff_hbatch_info_get(const gpudiff_hbatch* hb, gpudiff_hbatch_info* info);
+/* empty host batch (pinned on a GPU context) for pairs encoded elsewhere in the
+ * canonical format (pre-encoded replays, synthetic populations); the caller
+ * fills *pool and *rows (row offsets relative to *pool) before appending */
+int gpudiff_hbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, size_t n_pairs, uint64_t total_leaves,
+                          gpudiff_hbatch** out, uint8_t** pool, gpudiff_pair_row** rows);
 void gpudiff_hbatch_free(gpudiff_ctx* ctx, gpudiff_hbatch* hb);
 
 /* ---- device batches ---- */

@@ -1,0 +1,66 @@
+/*
+ * gpudiff_synth.h -- seeded synthetic object populations for bench.py and
+ * the GPU tests (NOT part of the drop-in boundary; libgpudiff_synth.so).
+ *
+ * Shapes follow SURVEY.md §8(d): ConfigMaps/Secrets (8 data keys, 64-512 B
+ * values, 4 labels, 2 annotations, no status), Deployments
+ * (contrib/examples/deployment.yaml of the reference plus server defaults and a
+ * two-condition status), medium CRDs (~200 leaves, nested lists) and deep
+ * list-heavy CRDs (300-3000 leaves, status lists of 64-1024 items).  Pairs are
+ * keyed by logical cluster (rank-frequency Zipf 1.1, offset 10); B = A with
+ * the metadata the predicates ignore rewritten and, for a seeded fraction, one
+ * semantic mutation whose effect (spec / status) the generator records as
+ * ground truth.  Every pair is a pure function of (seed, global pair index),
+ * independent of rank count, chunking and threads.
+ */
+#ifndef GPUDIFF_SYNTH_H
+#define GPUDIFF_SYNTH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gpudiff_format.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gpudiff_synth_cfg {
+    uint64_t seed;
+    uint64_t n_pairs;        /* whole population */
+    uint32_t n_clusters;     /* logical clusters */
+    float mutate_frac;
+    float w_configmap, w_secret, w_deployment, w_crd, w_deep;  /* kind mix */
+    uint32_t crd_leaves;     /* medium CRD target leaves (default 200) */
+} gpudiff_synth_cfg;
+
+/* ground truth bits per pair */
+#define GPUDIFF_SYNTH_SPEC_MUT 0x1u
+#define GPUDIFF_SYNTH_STATUS_MUT 0x2u
+#define GPUDIFF_SYNTH_B_HAS_STATUS 0x4u
+
+typedef struct gpudiff_synth gpudiff_synth;
+
+/* plans the population and the LPT shard of `rank` among `world` ranks */
+int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudiff_synth** out);
+void gpudiff_synth_close(gpudiff_synth* s);
+uint64_t gpudiff_synth_local_pairs(const gpudiff_synth* s);
+uint64_t gpudiff_synth_local_clusters(const gpudiff_synth* s);
+/* global pair index of local pair i */
+uint64_t gpudiff_synth_global_index(const gpudiff_synth* s, uint64_t i);
+
+/* encodes local pairs [first, first+n) with `threads` host threads into
+ * internal buffers; reports the pool bytes and leaves needed */
+int gpudiff_synth_encode(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t threads, uint64_t* pool_bytes,
+                         uint64_t* total_leaves);
+/* copies the last encoded range out (row offsets relative to `pool`) and the
+ * ground truth bits per pair */
+int gpudiff_synth_copy_out(gpudiff_synth* s, uint8_t* pool, gpudiff_pair_row* rows, uint8_t* truth);
+/* JSON text of local pair i (A then B); returns required sizes */
+int gpudiff_synth_json(gpudiff_synth* s, uint64_t i, char* a, size_t acap, size_t* alen, char* b, size_t bcap,
+                       size_t* blen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -14,8 +14,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = ["kernels.hip", "api.cpp", "encoder.cpp", "json.cpp"]
+SYNTH_SOURCES = ["synth.cpp", "encoder.cpp", "json.cpp"]
+SYNTH_LIB = os.path.join(HERE, "libgpudiff_synth.so")
 HEADERS = ["kernels.h", "encoder.h", "json.h", "xxh64.h"]
-INCLUDES = [os.path.join(ROOT, "include", h) for h in ("gpudiff.h", "gpudiff_format.h")]
+INCLUDES = [os.path.join(ROOT, "include", h) for h in ("gpudiff.h", "gpudiff_format.h", "gpudiff_synth.h")]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}",
           "-I" + os.path.join(ROOT, "include")]
 
@@ -42,18 +44,27 @@ def _compile(src, verbose):
     return o
 
 
+def _link(lib, objs, mapfile, verbose):
+    if not _newer(lib, objs + [mapfile]):
+        return
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + [
+        "-lpthread", "-Wl,--version-script=" + mapfile]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n%s%s" % (r.stdout, r.stderr))
+
+
 def build(verbose: bool = False) -> str:
+    """Builds libgpudiff.so (the product) and libgpudiff_synth.so (bench /
+    test workload generator)."""
     os.makedirs(OUT, exist_ok=True)
-    with ThreadPoolExecutor(max_workers=4) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), SOURCES))
-    if _newer(LIB, objs + [os.path.join(CSRC, "gpudiff.map")]):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
-            "-lpthread", "-Wl,--version-script=" + os.path.join(CSRC, "gpudiff.map")]
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError("link failed:\n%s%s" % (r.stdout, r.stderr))
+    srcs = sorted(set(SOURCES) | set(SYNTH_SOURCES))
+    with ThreadPoolExecutor(max_workers=5) as ex:
+        objs = dict(zip(srcs, ex.map(lambda s: _compile(s, verbose), srcs)))
+    _link(LIB, [objs[s] for s in SOURCES], os.path.join(CSRC, "gpudiff.map"), verbose)
+    _link(SYNTH_LIB, [objs[s] for s in SYNTH_SOURCES], os.path.join(CSRC, "synth.map"), verbose)
     return LIB
 
 

@@ -305,13 +305,45 @@ int gpudiff_encode_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t 
     } catch (const std::bad_alloc&) {
         return GPUDIFF_E_NOMEM;
     }
-    std::unique_ptr<gpudiff_hbatch> hb(new (std::nothrow) gpudiff_hbatch());
-    if (!hb) return GPUDIFF_E_NOMEM;
     uint64_t total = 0;
     for (uint32_t t = 0; t < T; t++) total += c->parts[t].pool.size();
+    gpudiff_hbatch* raw = nullptr;
+    uint8_t* pool_p = nullptr;
+    gpudiff_pair_row* rows_p = nullptr;
+    int rc = gpudiff_hbatch_create(c, total, n, 0, &raw, &pool_p, &rows_p);
+    if (rc) return rc;
+    std::unique_ptr<gpudiff_hbatch> hb(raw);
+    uint64_t base = 0;
+    size_t r0 = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        Part& part = c->parts[t];
+        if (!part.pool.empty()) memcpy(hb->pool + base, part.pool.data(), part.pool.size());
+        for (size_t i = 0; i < part.rows.size(); i++) {
+            gpudiff_pair_row r = part.rows[i];
+            r.off_a += base;
+            r.off_b += base;
+            hb->rows[r0 + i] = r;
+        }
+        r0 += part.rows.size();
+        base += part.pool.size();
+        hb->leaves += part.leaves;
+        hb->errors += part.errors;
+        hb->reseeded += part.reseeded;
+    }
+    *out = hb.release();
+    return GPUDIFF_OK;
+}
+
+int gpudiff_hbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, size_t n, uint64_t total_leaves, gpudiff_hbatch** out,
+                          uint8_t** pool, gpudiff_pair_row** rows) {
+    if (!c || !out || !pool || !rows || (pool_bytes & 15)) return GPUDIFF_E_INVAL;
+    *out = nullptr;
+    std::unique_ptr<gpudiff_hbatch> hb(new (std::nothrow) gpudiff_hbatch());
+    if (!hb) return GPUDIFF_E_NOMEM;
     hb->n = n;
-    hb->pool_bytes = total;
-    size_t pool_alloc = (size_t)std::max<uint64_t>(total, 16);
+    hb->pool_bytes = pool_bytes;
+    hb->leaves = total_leaves;
+    size_t pool_alloc = (size_t)std::max<uint64_t>(pool_bytes, 16);
     size_t rows_alloc = std::max<size_t>(n, 1) * sizeof(gpudiff_pair_row);
     if (c->has_device) {
         HIPCHK(hipSetDevice(c->device));
@@ -331,23 +363,8 @@ int gpudiff_encode_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t 
             return GPUDIFF_E_NOMEM;
         }
     }
-    uint64_t base = 0;
-    size_t r0 = 0;
-    for (uint32_t t = 0; t < T; t++) {
-        Part& part = c->parts[t];
-        if (!part.pool.empty()) memcpy(hb->pool + base, part.pool.data(), part.pool.size());
-        for (size_t i = 0; i < part.rows.size(); i++) {
-            gpudiff_pair_row r = part.rows[i];
-            r.off_a += base;
-            r.off_b += base;
-            hb->rows[r0 + i] = r;
-        }
-        r0 += part.rows.size();
-        base += part.pool.size();
-        hb->leaves += part.leaves;
-        hb->errors += part.errors;
-        hb->reseeded += part.reseeded;
-    }
+    *pool = hb->pool;
+    *rows = hb->rows;
     *out = hb.release();
     return GPUDIFF_OK;
 }

@@ -1,0 +1,132 @@
+"""ctypes binding of libgpudiff_synth.so (include/gpudiff_synth.h): seeded
+synthetic populations for bench.py and tests.  Not part of the drop-in."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import gpudiff as G
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SYNTH_PATH = os.path.join(_HERE, "libgpudiff_synth.so")
+
+SPEC_MUT, STATUS_MUT, B_HAS_STATUS = 0x1, 0x2, 0x4
+
+
+class SynthCfg(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_pairs", C.c_uint64), ("n_clusters", C.c_uint32),
+                ("mutate_frac", C.c_float), ("w_configmap", C.c_float), ("w_secret", C.c_float),
+                ("w_deployment", C.c_float), ("w_crd", C.c_float), ("w_deep", C.c_float),
+                ("crd_leaves", C.c_uint32)]
+
+
+_P = C.c_void_p
+_SIGS = [
+    ("gpudiff_synth_open", C.c_int, [C.POINTER(SynthCfg), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("gpudiff_synth_close", None, [_P]),
+    ("gpudiff_synth_local_pairs", C.c_uint64, [_P]),
+    ("gpudiff_synth_local_clusters", C.c_uint64, [_P]),
+    ("gpudiff_synth_global_index", C.c_uint64, [_P, C.c_uint64]),
+    ("gpudiff_synth_encode", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)]),
+    ("gpudiff_synth_copy_out", C.c_int, [_P, _P, _P, _P]),
+    ("gpudiff_synth_json", C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_char_p,
+                                     C.c_size_t, C.POINTER(C.c_size_t)]),
+]
+
+_lib = C.CDLL(SYNTH_PATH)
+for _n, _r, _a in _SIGS:
+    getattr(_lib, _n).restype = _r
+    getattr(_lib, _n).argtypes = _a
+
+# SURVEY.md §8(d) populations
+CONFIGS = {
+    # name: (n_pairs, n_clusters, mix cm/secret/deploy/crd/deep, seed offset)
+    "config1": (10_000, 1, (0, 0, 1, 0, 0), 1),
+    "config2": (1_000_000, 10_000, (0.5, 0.5, 0, 0, 0), 2),
+    "config3": (10_000_000, 100_000, (0.2, 0.2, 0.4, 0.2, 0), 3),
+    "config4": (100_000, 1_000, (0, 0, 0, 0, 1), 4),
+}
+BASE_SEED = 20211004
+
+
+def make_cfg(name: str, n_pairs: int = 0, n_clusters: int = 0, mutate_frac: float = 0.05) -> SynthCfg:
+    n, c, mix, off = CONFIGS[name]
+    return SynthCfg(seed=BASE_SEED + off, n_pairs=n_pairs or n, n_clusters=n_clusters or c,
+                    mutate_frac=mutate_frac, w_configmap=mix[0], w_secret=mix[1], w_deployment=mix[2],
+                    w_crd=mix[3], w_deep=mix[4], crd_leaves=200)
+
+
+@dataclass
+class Chunk:
+    hb: G.HostBatch
+    truth: np.ndarray  # u8 ground-truth bits per pair
+    pool_bytes: int
+    leaves: int
+
+
+class Population:
+    """One rank's shard (LPT by logical cluster) of a synthetic population."""
+
+    def __init__(self, cfg: SynthCfg, world: int = 1, rank: int = 0):
+        h = C.c_void_p()
+        rc = _lib.gpudiff_synth_open(C.byref(cfg), world, rank, C.byref(h))
+        if rc != 0:
+            raise RuntimeError("gpudiff_synth_open failed (%d)" % rc)
+        self.h = h
+        self.cfg = cfg
+        self.n = int(_lib.gpudiff_synth_local_pairs(h))
+        self.n_clusters = int(_lib.gpudiff_synth_local_clusters(h))
+
+    def close(self):
+        if self.h:
+            _lib.gpudiff_synth_close(self.h)
+            self.h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def global_index(self, i: int) -> int:
+        return int(_lib.gpudiff_synth_global_index(self.h, i))
+
+    def chunk(self, engine: G.Engine, first: int, n: int, threads: int = 16) -> Chunk:
+        pb, lv = C.c_uint64(), C.c_uint64()
+        rc = _lib.gpudiff_synth_encode(self.h, first, n, threads, C.byref(pb), C.byref(lv))
+        if rc != 0:
+            raise RuntimeError("gpudiff_synth_encode failed")
+        hbh = C.c_void_p()
+        pool = C.c_void_p()
+        rows = C.c_void_p()
+        G._chk(G._lib.gpudiff_hbatch_create(engine.ctx, pb.value, n, lv.value, C.byref(hbh),
+                                            C.cast(C.byref(pool), C.POINTER(C.POINTER(C.c_uint8))),
+                                            C.cast(C.byref(rows), C.POINTER(C.POINTER(G.PairRow)))),
+               "gpudiff_hbatch_create")
+        truth = np.zeros(n, dtype=np.uint8)
+        _lib.gpudiff_synth_copy_out(self.h, pool, rows, truth.ctypes.data_as(C.c_void_p))
+        return Chunk(G.HostBatch(engine, hbh.value, None), truth, pb.value, lv.value)
+
+    def json_pair(self, i: int):
+        al, bl = C.c_size_t(), C.c_size_t()
+        _lib.gpudiff_synth_json(self.h, i, None, 0, C.byref(al), None, 0, C.byref(bl))
+        a = C.create_string_buffer(al.value + 1)
+        b = C.create_string_buffer(bl.value + 1)
+        rc = _lib.gpudiff_synth_json(self.h, i, a, al.value + 1, C.byref(al), b, bl.value + 1, C.byref(bl))
+        if rc != 0:
+            raise RuntimeError("gpudiff_synth_json failed")
+        return a.raw[:al.value], b.raw[:bl.value]
+
+    def expected_flags(self, truth: np.ndarray) -> np.ndarray:
+        """Ground-truth decision bits: spec dirty iff a spec mutation was
+        applied; status dirty iff B has no status key (statussyncer.go:22-26)
+        or a status mutation was applied."""
+        f = np.zeros(truth.shape, dtype=np.uint8)
+        f |= np.where(truth & SPEC_MUT, G.SPEC_DIRTY, 0).astype(np.uint8)
+        st = ((truth & STATUS_MUT) != 0) | ((truth & B_HAS_STATUS) == 0)
+        f |= np.where(st, G.STATUS_DIRTY, 0).astype(np.uint8)
+        return f
