@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Headline benchmark: object-pair diffs/sec (whole node) + achieved HBM GB/s.
+
+Workload (BASELINE.json configs[2], the metric's own configuration): 10M mixed
+object pairs (40% ConfigMap/Secret, 40% Deployment, 20% medium CRD) across
+100k logical clusters, 5% mutated, synthetic (seed 20211004+3).  The
+population is fixed (strong scaling); each rank holds the LPT shard of whole
+logical clusters assigned to it, encoded on the host with the product encoder
+and resident in HBM before timing.
+
+A step = one diff pass of the hot path (K2 compare, K3 compaction, K4
+changed-path merge-join, K5/K6 path emit) over the rank's resident pairs, plus
+(N > 1) the RCCL all-gather of per-rank dirty counts and dirty pair IDs.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+
+
+def log(*a):
+    print("[bench r%s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4"])
+    ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")
+    ap.add_argument("--clusters", type=int, default=0)
+    ap.add_argument("--chunk", type=int, default=262144)
+    ap.add_argument("--threads", type=int, default=0, help="host encode threads (default min(16, cpus))")
+    ap.add_argument("--sample", type=int, default=600, help="pairs checked bit-exact vs the oracle (JSON path)")
+    ap.add_argument("--cpu-sample", type=int, default=20000, help="pairs in the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*) to attach")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+
+    import torch
+    import torch.distributed as dist
+
+    from kcp_amd import gpudiff as G
+    from kcp_amd import synth as S
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    stream = torch.cuda.current_stream(dev)
+    ncpu = len(os.sched_getaffinity(0))
+    threads = args.threads or max(1, min(16, ncpu))
+
+    eng = G.Engine(device=local_rank, encode_threads=threads, stream=stream.cuda_stream, timing=True)
+    cfg = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=args.clusters)
+    pop = S.Population(cfg, world, rank)
+    n = pop.n
+    log("config %s: %d pairs / %d clusters total; this rank %d pairs / %d clusters; %d host threads" % (
+        args.config, cfg.n_pairs, cfg.n_clusters, n, pop.n_clusters, threads))
+
+    # ---------------- ingest: synthesize + encode on the host, stage, H2D, K1
+    t_gen = time.time()
+    first = pop.chunk(eng, 0, min(args.chunk, n), threads)
+    per_pair = first.pool_bytes / max(1, min(args.chunk, n))
+    margin = 1.15 if args.config != "config4" else 1.4
+    pool_cap = int(per_pair * n * margin) + (64 << 20)
+    db = eng.device_batch(pool_cap, n)
+    truth = np.zeros(n, dtype=np.uint8)
+    stage = [first.hb, None]
+    truth[:first.truth.size] = first.truth
+    db.append(first.hb)
+    pos = first.truth.size
+    leaves = first.leaves
+    k = 1
+    last_log = time.time()
+    while pos < n:
+        m = min(args.chunk, n - pos)
+        ch = pop.chunk(eng, pos, m, threads, reuse=stage[k & 1])
+        stage[k & 1] = ch.hb
+        db.append(ch.hb)
+        truth[pos:pos + m] = ch.truth
+        pos += m
+        leaves += ch.leaves
+        k += 1
+        if time.time() - last_log > 20:
+            log("ingest %d/%d pairs (%.0f s)" % (pos, n, time.time() - t_gen))
+            last_log = time.time()
+    eng.sync()
+    t_gen = time.time() - t_gen
+    st = db.stats()
+    k1_ms = eng.timings().value_hash_ms
+    log("ingest done in %.1f s: %.2f GB resident, %.1f leaves/pair, %.2f GB compared per pass" % (
+        t_gen, st.pool_bytes / 1e9, st.total_leaves / max(1, n), st.compare_bytes / 1e9))
+
+    # ---------------- warmup + full-size correctness (size-independent properties)
+    ticket = eng.diff(db)
+    res = eng.wait(ticket)
+    exp_flags = pop.expected_flags(truth)
+    got = res.pair_flags & (G.SPEC_DIRTY | G.STATUS_DIRTY)
+    n_bad = int((got != exp_flags).sum())
+    offs = res.path_offsets.astype(np.int64)
+    every_dirty_has_path = bool((np.diff(offs) >= 1).all()) if res.dirty_ids.size else True
+    ids_ok = (res.spec_dirty_ids.size == int((got & G.SPEC_DIRTY).astype(bool).sum()) and
+              res.status_dirty_ids.size == int((got & G.STATUS_DIRTY).astype(bool).sum()))
+    full_check = dict(pairs=n, flag_mismatches=n_bad, every_dirty_pair_has_paths=every_dirty_has_path,
+                      id_lists_consistent=ids_ok, spec_dirty=int(res.spec_dirty_ids.size),
+                      status_dirty=int(res.status_dirty_ids.size), paths=int(res.path_hashes.size))
+    log("full-size check:", json.dumps(full_check))
+    if n_bad or not every_dirty_has_path or not ids_ok:
+        log("FULL-SIZE CHECK FAILED")
+    pop_flags = res.pair_flags.copy()
+    del res
+
+    # bit-exact sample through the JSON -> encoder -> GPU path vs the oracle
+    sample_check = None
+    if args.sample and rank == 0:
+        from tests.parity import assert_matches, oracle_batch
+        idx = np.unique(np.linspace(0, n - 1, min(args.sample, n)).astype(np.int64))
+        pairs = [pop.json_pair(int(i)) for i in idx]
+        exp = oracle_batch(pairs)
+        r = eng.diff_pairs(pairs)
+        ok = True
+        try:
+            assert_matches(r, pairs, exp=exp)
+        except AssertionError as e:
+            ok = False
+            log("SAMPLE PARITY FAILED:", str(e)[:500])
+        same = bool((r.pair_flags == pop_flags[idx]).all())
+        sample_check = dict(pairs=int(idx.size), bit_exact_vs_oracle=ok, matches_population_flags=same)
+        log("sample check:", json.dumps(sample_check))
+
+    for _ in range(max(0, args.warmup - 1)):
+        eng.diff(db)
+    eng.sync()
+
+    # ---------------- timed region
+    def gather_step():
+        counts = torch.empty(8, dtype=torch.int32, device=dev)
+        db.export(G.EXPORT_COUNTS, counts.data_ptr(), 8)
+        allc = torch.empty(world * 8, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(allc, counts)
+        cc = allc.view(world, 8).cpu()
+        out = []
+        for col, what in ((0, G.EXPORT_SPEC_IDS), (1, G.EXPORT_STATUS_IDS)):
+            mx = max(1, int(cc[:, col].max()))
+            buf = torch.zeros(mx, dtype=torch.int32, device=dev)
+            db.export(what, buf.data_ptr(), mx, int(cc[rank, col]))
+            allb = torch.empty(world * mx, dtype=torch.int32, device=dev)
+            dist.all_gather_into_tensor(allb, buf)
+            out.append((allb, cc[:, col]))
+        return out
+
+    eng.timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.diff(db)
+        if world > 1:
+            gather_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tm = eng.timings()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tot = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        total_pairs = int(tot.item())
+    else:
+        total_pairs = n
+
+    value = total_pairs * args.steps / dt
+    k2_ms = tm.compare_ms
+    achieved = st.compare_bytes / (k2_ms * 1e-3) / 1e9 if k2_ms > 0 else 0.0
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    # ---------------- CPU baseline (rank 0, N=1 only): the oracle's C++ port
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import cpu_ref
+        idx = np.unique(np.linspace(0, n - 1, min(args.cpu_sample, n)).astype(np.int64))
+        pairs = [pop.json_pair(int(i)) for i in idx]
+        dp = cpu_ref.DecodedPairs(pairs)
+        cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
+        agree = bool((cflags & 3 == pop_flags[idx] & 3).all())
+        _, sweeps1, sec1 = dp.decide(threads=1, min_seconds=args.cpu_seconds / 2)
+        dp.close()
+        cpu = dict(value=len(idx) * sweeps / sec, unit="pairs/s", cores=threads, kind="port",
+                   sample="%d pairs (every %dth of this workload, JSON decoded untimed), %d sweeps in %.1f s; "
+                          "decisions agree with GPU: %s; 1-core: %.0f pairs/s" % (
+                              len(idx), max(1, n // len(idx)), sweeps, sec, agree, len(idx) * sweeps1 / sec1))
+        log("cpu baseline:", json.dumps(cpu))
+
+    if rank == 0:
+        line = {
+            "metric": "object-pair diffs/sec (whole node) + achieved HBM GB/s, 10M objs/100k clusters",
+            "value": value,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded object populations, SURVEY.md 8d; no real cluster data)",
+            "config": {
+                "workload": "%s: %d pairs / %d logical clusters, %.0f%% mutated (%s)" % (
+                    args.config, cfg.n_pairs, cfg.n_clusters, cfg.mutate_frac * 100,
+                    "40% ConfigMap/Secret, 40% Deployment, 20% CRD" if args.config == "config3" else args.config),
+                "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9,
+                "parallelism": "shard-by-logical-cluster x%d (LPT)%s" % (
+                    world, ", RCCL all-gather of dirty counts+IDs per step" if world > 1 else ""),
+            },
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "kernel": "k_compare (K2)", "bytes_per_launch": st.compare_bytes,
+                         "avg_launch_ms": k2_ms},
+            "kernels_ms": {"compare": tm.compare_ms, "compact": tm.compact_ms, "join": tm.join_ms,
+                           "emit": tm.emit_ms, "diff_pass": tm.total_ms, "passes": tm.n_passes,
+                           "value_hash_last_chunk": k1_ms},
+            "cpu_baseline": cpu,
+            "checks": {"full_size": full_check, "sample": sample_check},
+            "ingest_s": t_gen,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -143,6 +143,7 @@ typedef struct gpudiff_timings {
     float join_ms;        /* K4 changed-path merge-join */
     float emit_ms;        /* K5 + K6 path scan and copy */
     float total_ms;       /* first to last event of gpudiff_diff */
+    uint32_t n_passes;    /* diff passes averaged (since gpudiff_timing_reset) */
 } gpudiff_timings;
 
 /* ---- library ---- */
@@ -163,6 +164,10 @@ int gpudiff_hbatch_info_get(const gpudiff_hbatch* hb, gpudiff_hbatch_info* info)
  * fills *pool and *rows (row offsets relative to *pool) before appending */
 int gpudiff_hbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, size_t n_pairs, uint64_t total_leaves,
                           gpudiff_hbatch** out, uint8_t** pool, gpudiff_pair_row** rows);
+/* reuses a host batch (staging ring): waits for its last H2D copy, grows the
+ * buffers only when needed, and returns them for refilling */
+int gpudiff_hbatch_resize(gpudiff_ctx* ctx, gpudiff_hbatch* hb, uint64_t pool_bytes, size_t n_pairs,
+                          uint64_t total_leaves, uint8_t** pool, gpudiff_pair_row** rows);
 void gpudiff_hbatch_free(gpudiff_ctx* ctx, gpudiff_hbatch* hb);
 
 /* ---- device batches ---- */
@@ -173,6 +178,16 @@ int gpudiff_dbatch_append(gpudiff_ctx* ctx, gpudiff_dbatch* db, const gpudiff_hb
 int gpudiff_dbatch_reset(gpudiff_ctx* ctx, gpudiff_dbatch* db);
 int gpudiff_dbatch_stats_get(const gpudiff_dbatch* db, gpudiff_batch_stats* st);
 int gpudiff_dbatch_device_view(const gpudiff_dbatch* db, gpudiff_device_view* v);
+/* async device-to-device copy of a diffed batch's results into caller memory
+ * (e.g. a tensor handed to an RCCL all-gather), ordered on the context
+ * stream; copies min(count, max_elems) elements of `what` */
+#define GPUDIFF_EXPORT_COUNTS 0u      /* 8 x u32: n_spec, n_status, n_dirty, cap, overflow, n_paths, 0, 0 */
+#define GPUDIFF_EXPORT_SPEC_IDS 1u    /* u32 */
+#define GPUDIFF_EXPORT_STATUS_IDS 2u  /* u32 */
+#define GPUDIFF_EXPORT_DIRTY_IDS 3u   /* u32 */
+#define GPUDIFF_EXPORT_FLAGS 4u       /* u8 per pair */
+int gpudiff_dbatch_export(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint32_t what, void* dst_device,
+                          uint64_t max_elems, uint64_t known_count);
 /* synchronous D2H copy of resident pool bytes (inspection / tests) */
 int gpudiff_dbatch_read_pool(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint64_t off, void* dst,
                              uint64_t bytes);
@@ -184,7 +199,10 @@ int gpudiff_diff(gpudiff_ctx* ctx, gpudiff_dbatch* db, gpudiff_ticket* ticket);
 /* block until the ticket's diff finished and copy results to host */
 int gpudiff_wait(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_result* res);
 void gpudiff_result_release(gpudiff_ctx* ctx, gpudiff_result* res);
+/* mean per-kernel times over the passes recorded since the last reset
+ * (GPUDIFF_OPT_TIMING); synchronizes the context stream */
 int gpudiff_last_timings(gpudiff_ctx* ctx, gpudiff_timings* t);
+int gpudiff_timing_reset(gpudiff_ctx* ctx);
 int gpudiff_sync(gpudiff_ctx* ctx);
 
 /* encode + upload into a context-owned batch + diff (the syncer batcher's call) */

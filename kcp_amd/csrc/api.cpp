@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <memory>
 #include <mutex>
@@ -48,6 +49,8 @@ struct gpudiff_hbatch {
     size_t n = 0;
     uint64_t pool_bytes = 0;
     uint64_t leaves = 0, errors = 0, reseeded = 0;
+    uint64_t pool_cap = 0;
+    size_t rows_cap = 0;
     bool pinned = false;
     hipEvent_t used = nullptr;  // last async copy that reads this batch
 };
@@ -100,8 +103,10 @@ struct gpudiff_ctx {
     std::vector<Part> parts;
     gpudiff_ticket next_ticket = 1;
     std::unordered_map<gpudiff_ticket, gpudiff_dbatch*> tickets;
-    hipEvent_t ev[7] = {};
-    bool timing_valid = false;
+    hipEvent_t ev_k1[2] = {};
+    bool k1_recorded = false;
+    std::vector<std::array<hipEvent_t, 5>> pass_ev;
+    size_t n_pass = 0;
     // submit ring
     gpudiff_dbatch* ring[2] = {nullptr, nullptr};
     gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
@@ -245,7 +250,7 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             c->own_stream = true;
         }
-        for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+        for (auto& e : c->ev_k1) HIPCHK(hipEventCreate(&e));
     }
     *out = c.release();
     return GPUDIFF_OK;
@@ -260,8 +265,10 @@ void gpudiff_close(gpudiff_ctx* c) {
             if (c->ring[i]) gpudiff_dbatch_free(c, c->ring[i]);
             if (c->ring_hb[i]) gpudiff_hbatch_free(c, c->ring_hb[i]);
         }
-        for (auto& e : c->ev)
+        for (auto& e : c->ev_k1)
             if (e) (void)hipEventDestroy(e);
+        for (auto& a : c->pass_ev)
+            for (auto& e : a) (void)hipEventDestroy(e);
         if (c->own_stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -334,38 +341,77 @@ int gpudiff_encode_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t 
     return GPUDIFF_OK;
 }
 
+static void hb_release_buffers(gpudiff_hbatch* hb) {
+    if (hb->pinned) {
+        if (hb->pool) (void)hipHostFree(hb->pool);
+        if (hb->rows) (void)hipHostFree(hb->rows);
+    } else {
+        free(hb->pool);
+        free(hb->rows);
+    }
+    hb->pool = nullptr;
+    hb->rows = nullptr;
+    hb->pool_cap = hb->rows_cap = 0;
+}
+
+// (re)allocates hb's buffers for at least pool_bytes / n rows; pinned on GPU contexts
+static int hb_reserve(gpudiff_ctx* c, gpudiff_hbatch* hb, uint64_t pool_bytes, size_t n) {
+    if (hb->used) HIPCHK(hipEventSynchronize(hb->used));  // an in-flight H2D may still read it
+    if (pool_bytes <= hb->pool_cap && n <= hb->rows_cap && hb->pool) return GPUDIFF_OK;
+    hb_release_buffers(hb);
+    size_t pool_alloc = (size_t)std::max<uint64_t>((pool_bytes + 63) & ~63ull, 64);
+    size_t rows_alloc = std::max<size_t>(n, 1) * sizeof(gpudiff_pair_row);
+    if (c->has_device) {
+        HIPCHK(hipSetDevice(c->device));
+        if (hipHostMalloc((void**)&hb->pool, pool_alloc, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void**)&hb->rows, rows_alloc, hipHostMallocDefault) != hipSuccess) {
+            hb_release_buffers(hb);
+            return GPUDIFF_E_NOMEM;
+        }
+        hb->pinned = true;
+        if (!hb->used) HIPCHK(hipEventCreateWithFlags(&hb->used, hipEventDisableTiming));
+    } else {
+        hb->pool = (uint8_t*)aligned_alloc(64, pool_alloc);
+        hb->rows = (gpudiff_pair_row*)aligned_alloc(64, (rows_alloc + 63) & ~(size_t)63);
+        if (!hb->pool || !hb->rows) {
+            hb_release_buffers(hb);
+            return GPUDIFF_E_NOMEM;
+        }
+        hb->pinned = false;
+    }
+    hb->pool_cap = pool_alloc;
+    hb->rows_cap = std::max<size_t>(n, 1);
+    return GPUDIFF_OK;
+}
+
 int gpudiff_hbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, size_t n, uint64_t total_leaves, gpudiff_hbatch** out,
                           uint8_t** pool, gpudiff_pair_row** rows) {
     if (!c || !out || !pool || !rows || (pool_bytes & 15)) return GPUDIFF_E_INVAL;
     *out = nullptr;
     std::unique_ptr<gpudiff_hbatch> hb(new (std::nothrow) gpudiff_hbatch());
     if (!hb) return GPUDIFF_E_NOMEM;
+    int rc = hb_reserve(c, hb.get(), pool_bytes, n);
+    if (rc) return rc;
     hb->n = n;
     hb->pool_bytes = pool_bytes;
     hb->leaves = total_leaves;
-    size_t pool_alloc = (size_t)std::max<uint64_t>(pool_bytes, 16);
-    size_t rows_alloc = std::max<size_t>(n, 1) * sizeof(gpudiff_pair_row);
-    if (c->has_device) {
-        HIPCHK(hipSetDevice(c->device));
-        if (hipHostMalloc((void**)&hb->pool, pool_alloc, hipHostMallocDefault) != hipSuccess ||
-            hipHostMalloc((void**)&hb->rows, rows_alloc, hipHostMallocDefault) != hipSuccess) {
-            if (hb->pool) (void)hipHostFree(hb->pool);
-            return GPUDIFF_E_NOMEM;
-        }
-        hb->pinned = true;
-        HIPCHK(hipEventCreateWithFlags(&hb->used, hipEventDisableTiming));
-    } else {
-        hb->pool = (uint8_t*)aligned_alloc(64, (pool_alloc + 63) & ~(size_t)63);
-        hb->rows = (gpudiff_pair_row*)aligned_alloc(64, (rows_alloc + 63) & ~(size_t)63);
-        if (!hb->pool || !hb->rows) {
-            free(hb->pool);
-            free(hb->rows);
-            return GPUDIFF_E_NOMEM;
-        }
-    }
     *pool = hb->pool;
     *rows = hb->rows;
     *out = hb.release();
+    return GPUDIFF_OK;
+}
+
+int gpudiff_hbatch_resize(gpudiff_ctx* c, gpudiff_hbatch* hb, uint64_t pool_bytes, size_t n, uint64_t total_leaves,
+                          uint8_t** pool, gpudiff_pair_row** rows) {
+    if (!c || !hb || !pool || !rows || (pool_bytes & 15)) return GPUDIFF_E_INVAL;
+    int rc = hb_reserve(c, hb, pool_bytes, n);
+    if (rc) return rc;
+    hb->n = n;
+    hb->pool_bytes = pool_bytes;
+    hb->leaves = total_leaves;
+    hb->errors = hb->reseeded = 0;
+    *pool = hb->pool;
+    *rows = hb->rows;
     return GPUDIFF_OK;
 }
 
@@ -383,18 +429,12 @@ int gpudiff_hbatch_info_get(const gpudiff_hbatch* hb, gpudiff_hbatch_info* info)
 
 void gpudiff_hbatch_free(gpudiff_ctx* c, gpudiff_hbatch* hb) {
     if (!hb) return;
-    if (hb->pinned) {
-        if (c && c->has_device) (void)hipSetDevice(c->device);
-        if (hb->used) {
-            (void)hipEventSynchronize(hb->used);
-            (void)hipEventDestroy(hb->used);
-        }
-        (void)hipHostFree(hb->pool);
-        (void)hipHostFree(hb->rows);
-    } else {
-        free(hb->pool);
-        free(hb->rows);
+    if (c && c->has_device) (void)hipSetDevice(c->device);
+    if (hb->used) {
+        (void)hipEventSynchronize(hb->used);
+        (void)hipEventDestroy(hb->used);
     }
+    hb_release_buffers(hb);
     delete hb;
 }
 
@@ -447,9 +487,12 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
     if (hb->used) HIPCHK(hipEventRecord(hb->used, c->stream));
     HIPCHK(launch_rebase(c->stream, d->rows, begin, end, base, d->pair_ids));
     if (!c->ecfg.host_value_hash) {
-        if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
         HIPCHK(launch_value_hash(c->stream, d->rows, begin, end, d->pool));
-        if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        if (c->flags & GPUDIFF_OPT_TIMING) {
+            HIPCHK(hipEventRecord(c->ev_k1[1], c->stream));
+            c->k1_recorded = true;
+        }
     }
     uint64_t cb = 0;
     for (size_t i = 0; i < hb->n; i++) cb += pair_compare_bytes(hb->rows[i]);
@@ -489,6 +532,27 @@ int gpudiff_dbatch_device_view(const gpudiff_dbatch* d, gpudiff_device_view* v) 
     return GPUDIFF_OK;
 }
 
+int gpudiff_dbatch_export(gpudiff_ctx* c, const gpudiff_dbatch* d, uint32_t what, void* dst, uint64_t max_elems,
+                          uint64_t known_count) {
+    if (!c || !d || (!dst && max_elems)) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const void* src;
+    size_t esz = 4;
+    uint64_t n = std::min<uint64_t>(max_elems, known_count);
+    switch (what) {
+        case GPUDIFF_EXPORT_COUNTS: src = d->summary; n = std::min<uint64_t>(max_elems, 8); break;
+        case GPUDIFF_EXPORT_SPEC_IDS: src = d->spec_ids; break;
+        case GPUDIFF_EXPORT_STATUS_IDS: src = d->status_ids; break;
+        case GPUDIFF_EXPORT_DIRTY_IDS: src = d->dirty_ids; break;
+        case GPUDIFF_EXPORT_FLAGS: src = d->flags; esz = 1; break;
+        default: return GPUDIFF_E_INVAL;
+    }
+    if (what != GPUDIFF_EXPORT_COUNTS && n > d->n_pairs) n = d->n_pairs;
+    if (n) HIPCHK(hipMemcpyAsync(dst, src, n * esz, hipMemcpyDeviceToDevice, c->stream));
+    return GPUDIFF_OK;
+}
+
 int gpudiff_dbatch_read_pool(gpudiff_ctx* c, const gpudiff_dbatch* d, uint64_t off, void* dst, uint64_t bytes) {
     if (!c || !d || (!dst && bytes)) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
@@ -511,12 +575,25 @@ void gpudiff_dbatch_free(gpudiff_ctx* c, gpudiff_dbatch* d) {
 }
 
 // ------------------------------------------------------------------ diff
-static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d, bool timing) {
+// Timing: one set of 5 events per recorded pass ([0] before K2, [1] after K2,
+// [2] after K3, [3] after K4, [4] after K5/K6); gpudiff_last_timings averages
+// every pass recorded since gpudiff_timing_reset.
+static hipEvent_t* pass_events(gpudiff_ctx* c) {
+    if (c->n_pass >= c->pass_ev.size()) {
+        std::array<hipEvent_t, 5> a{};
+        for (auto& e : a)
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->pass_ev.push_back(a);
+    }
+    return c->pass_ev[c->n_pass].data();
+}
+
+static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d, hipEvent_t* ev) {
     DiffBuffers b = buffers_of(c, d);
     HIPCHK(launch_join(c->stream, b));
-    if (timing) HIPCHK(hipEventRecord(c->ev[4], c->stream));
+    if (ev) HIPCHK(hipEventRecord(ev[3], c->stream));
     HIPCHK(launch_emit(c->stream, b));
-    if (timing) HIPCHK(hipEventRecord(c->ev[6], c->stream));
+    if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
     return GPUDIFF_OK;
 }
 
@@ -526,22 +603,25 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     if (rc) return rc;
     // scratch for changed paths: sized from the batch, grown on overflow
     if ((rc = ensure_scratch(d, std::max<uint64_t>(d->n_pairs * 2 + d->leaves / 8, 1u << 16)))) return rc;
-    const bool timing = (c->flags & GPUDIFF_OPT_TIMING) != 0;
+    hipEvent_t* ev = nullptr;
+    if ((c->flags & GPUDIFF_OPT_TIMING) && d->n_pairs) {
+        ev = pass_events(c);
+        if (!ev) return GPUDIFF_E_DEVICE;
+    }
     HIPCHK(hipMemsetAsync(d->summary, 0, 8 * sizeof(uint32_t), c->stream));
-    if (timing) HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    if (ev) HIPCHK(hipEventRecord(ev[0], c->stream));
     DiffBuffers b = buffers_of(c, d);
     if (d->n_pairs) {
         HIPCHK(launch_compare(c->stream, b));
-        if (timing) HIPCHK(hipEventRecord(c->ev[3], c->stream));
+        if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
         HIPCHK(launch_compact(c->stream, b));
-        if (timing) HIPCHK(hipEventRecord(c->ev[5], c->stream));
-        rc = enqueue_join_emit(c, d, timing);
-        if (rc) return rc;
+        if (ev) HIPCHK(hipEventRecord(ev[2], c->stream));
+        if ((rc = enqueue_join_emit(c, d, ev))) return rc;
     } else {
         HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), c->stream));
     }
+    if (ev) c->n_pass++;
     HIPCHK(hipEventRecord(d->done, c->stream));
-    c->timing_valid = timing && d->n_pairs;
     if (d->ticket) c->tickets.erase(d->ticket);
     d->ticket = c->next_ticket++;
     c->tickets[d->ticket] = d;
@@ -557,6 +637,15 @@ int gpudiff_sync(gpudiff_ctx* c) {
     return GPUDIFF_OK;
 }
 
+int gpudiff_timing_reset(gpudiff_ctx* c) {
+    if (!c) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->n_pass = 0;
+    return GPUDIFF_OK;
+}
+
 int gpudiff_last_timings(gpudiff_ctx* c, gpudiff_timings* t) {
     if (!c || !t) return GPUDIFF_E_INVAL;
     memset(t, 0, sizeof(*t));
@@ -564,13 +653,25 @@ int gpudiff_last_timings(gpudiff_ctx* c, gpudiff_timings* t) {
     if (!(c->flags & GPUDIFF_OPT_TIMING)) return GPUDIFF_E_STATE;
     HIPCHK(hipStreamSynchronize(c->stream));
     float ms = 0;
-    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) t->value_hash_ms = ms;
-    if (!c->timing_valid) return GPUDIFF_OK;
-    HIPCHK(hipEventElapsedTime(&t->compare_ms, c->ev[2], c->ev[3]));
-    HIPCHK(hipEventElapsedTime(&t->compact_ms, c->ev[3], c->ev[5]));
-    HIPCHK(hipEventElapsedTime(&t->join_ms, c->ev[5], c->ev[4]));
-    HIPCHK(hipEventElapsedTime(&t->emit_ms, c->ev[4], c->ev[6]));
-    HIPCHK(hipEventElapsedTime(&t->total_ms, c->ev[2], c->ev[6]));
+    if (c->k1_recorded && hipEventElapsedTime(&ms, c->ev_k1[0], c->ev_k1[1]) == hipSuccess) t->value_hash_ms = ms;
+    t->n_passes = (uint32_t)c->n_pass;
+    if (!c->n_pass) return GPUDIFF_OK;
+    double s[5] = {0, 0, 0, 0, 0};
+    for (size_t i = 0; i < c->n_pass; i++) {
+        hipEvent_t* e = c->pass_ev[i].data();
+        float x;
+        HIPCHK(hipEventElapsedTime(&x, e[0], e[1])); s[0] += x;
+        HIPCHK(hipEventElapsedTime(&x, e[1], e[2])); s[1] += x;
+        HIPCHK(hipEventElapsedTime(&x, e[2], e[3])); s[2] += x;
+        HIPCHK(hipEventElapsedTime(&x, e[3], e[4])); s[3] += x;
+        HIPCHK(hipEventElapsedTime(&x, e[0], e[4])); s[4] += x;
+    }
+    const double n = (double)c->n_pass;
+    t->compare_ms = (float)(s[0] / n);
+    t->compact_ms = (float)(s[1] / n);
+    t->join_ms = (float)(s[2] / n);
+    t->emit_ms = (float)(s[3] / n);
+    t->total_ms = (float)(s[4] / n);
     return GPUDIFF_OK;
 }
 
@@ -589,7 +690,7 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
         if ((rc = ensure_scratch(d, sum[3]))) return rc;
         uint32_t zero = 0;
         HIPCHK(hipMemcpyAsync(d->summary + 4, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
-        if ((rc = enqueue_join_emit(c, d, false))) return rc;
+        if ((rc = enqueue_join_emit(c, d, nullptr))) return rc;
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
         if (sum[4]) return GPUDIFF_E_CAPACITY;

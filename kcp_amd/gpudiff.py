@@ -27,6 +27,7 @@ OPT_TIMING, OPT_HOST_VALUE_HASH = 0x1, 0x2
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
 OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_SEED_SHIFT = 0x1, 0x2, 8
+EXPORT_COUNTS, EXPORT_SPEC_IDS, EXPORT_STATUS_IDS, EXPORT_DIRTY_IDS, EXPORT_FLAGS = range(5)
 
 
 class GpuDiffError(RuntimeError):
@@ -88,7 +89,8 @@ class BatchStats(C.Structure):
 
 class Timings(C.Structure):
     _fields_ = [("value_hash_ms", C.c_float), ("compare_ms", C.c_float), ("compact_ms", C.c_float),
-                ("join_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float)]
+                ("join_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float),
+                ("n_passes", C.c_uint32)]
 
 
 # (name, restype, argtypes) for every symbol of include/gpudiff.h
@@ -108,12 +110,18 @@ SIGNATURES = [
     ("gpudiff_dbatch_stats_get", C.c_int, [_P, C.POINTER(BatchStats)]),
     ("gpudiff_dbatch_device_view", C.c_int, [_P, C.POINTER(DeviceView)]),
     ("gpudiff_dbatch_read_pool", C.c_int, [_P, _P, C.c_uint64, C.c_void_p, C.c_uint64]),
+    ("gpudiff_dbatch_export", C.c_int, [_P, _P, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64]),
     ("gpudiff_dbatch_free", None, [_P, _P]),
     ("gpudiff_diff", C.c_int, [_P, _P, C.POINTER(C.c_uint64)]),
     ("gpudiff_wait", C.c_int, [_P, C.c_uint64, C.POINTER(Result)]),
     ("gpudiff_result_release", None, [_P, C.POINTER(Result)]),
     ("gpudiff_last_timings", C.c_int, [_P, C.POINTER(Timings)]),
     ("gpudiff_sync", C.c_int, [_P]),
+    ("gpudiff_timing_reset", C.c_int, [_P]),
+    ("gpudiff_hbatch_create", C.c_int, [_P, C.c_uint64, C.c_size_t, C.c_uint64, C.POINTER(_P), C.POINTER(_P),
+                                        C.POINTER(_P)]),
+    ("gpudiff_hbatch_resize", C.c_int, [_P, _P, C.c_uint64, C.c_size_t, C.c_uint64, C.POINTER(_P),
+                                        C.POINTER(_P)]),
     ("gpudiff_submit", C.c_int, [_P, C.POINTER(JsonPair), C.c_size_t, C.POINTER(C.c_uint64)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
@@ -240,6 +248,11 @@ class DeviceBatch:
         _chk(_lib.gpudiff_dbatch_device_view(self.h, C.byref(v)), "gpudiff_dbatch_device_view")
         return v
 
+    def export(self, what: int, dst_device_ptr: int, max_elems: int, known_count: int = 1 << 62):
+        """Async D2D copy of results into caller device memory (ctx stream)."""
+        _chk(_lib.gpudiff_dbatch_export(self.engine.ctx, self.h, what, dst_device_ptr, max_elems, known_count),
+             "gpudiff_dbatch_export")
+
     def read_pool(self, off: int, nbytes: int) -> bytes:
         buf = C.create_string_buffer(max(nbytes, 1))
         _chk(_lib.gpudiff_dbatch_read_pool(self.engine.ctx, self.h, off, buf, nbytes), "gpudiff_dbatch_read_pool")
@@ -334,6 +347,9 @@ class Engine:
 
     def sync(self):
         _chk(_lib.gpudiff_sync(self.ctx), "gpudiff_sync")
+
+    def timing_reset(self):
+        _chk(_lib.gpudiff_timing_reset(self.ctx), "gpudiff_timing_reset")
 
     def timings(self) -> Timings:
         t = Timings()

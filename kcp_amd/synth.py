@@ -95,21 +95,29 @@ class Population:
     def global_index(self, i: int) -> int:
         return int(_lib.gpudiff_synth_global_index(self.h, i))
 
-    def chunk(self, engine: G.Engine, first: int, n: int, threads: int = 16) -> Chunk:
+    def chunk(self, engine: G.Engine, first: int, n: int, threads: int = 16,
+              reuse: "G.HostBatch | None" = None) -> Chunk:
+        """Encodes local pairs [first, first+n) into a host batch (pinned on a
+        GPU engine).  `reuse` recycles a staging batch (waits for its last H2D
+        copy; reallocates only when it is too small)."""
         pb, lv = C.c_uint64(), C.c_uint64()
         rc = _lib.gpudiff_synth_encode(self.h, first, n, threads, C.byref(pb), C.byref(lv))
         if rc != 0:
             raise RuntimeError("gpudiff_synth_encode failed")
-        hbh = C.c_void_p()
         pool = C.c_void_p()
         rows = C.c_void_p()
-        G._chk(G._lib.gpudiff_hbatch_create(engine.ctx, pb.value, n, lv.value, C.byref(hbh),
-                                            C.cast(C.byref(pool), C.POINTER(C.POINTER(C.c_uint8))),
-                                            C.cast(C.byref(rows), C.POINTER(C.POINTER(G.PairRow)))),
-               "gpudiff_hbatch_create")
+        if reuse is not None:
+            G._chk(G._lib.gpudiff_hbatch_resize(engine.ctx, reuse.h, pb.value, n, lv.value, C.byref(pool),
+                                                C.byref(rows)), "gpudiff_hbatch_resize")
+            hb = reuse
+        else:
+            hbh = C.c_void_p()
+            G._chk(G._lib.gpudiff_hbatch_create(engine.ctx, pb.value, n, lv.value, C.byref(hbh), C.byref(pool),
+                                                C.byref(rows)), "gpudiff_hbatch_create")
+            hb = G.HostBatch(engine, hbh.value, None)
         truth = np.zeros(n, dtype=np.uint8)
         _lib.gpudiff_synth_copy_out(self.h, pool, rows, truth.ctypes.data_as(C.c_void_p))
-        return Chunk(G.HostBatch(engine, hbh.value, None), truth, pb.value, lv.value)
+        return Chunk(hb, truth, pb.value, lv.value)
 
     def json_pair(self, i: int):
         al, bl = C.c_size_t(), C.c_size_t()

@@ -1,0 +1,58 @@
+"""ctypes wrapper of oracle/_build/liboracle.so -- the C++ restatement of the
+reference predicates (TEST INFRASTRUCTURE / CPU BASELINE ONLY)."""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import build as _build
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = _build.LIB if os.path.exists(_build.LIB) else _build.build()
+        l = C.CDLL(path)
+        l.oracle_load.restype = C.c_void_p
+        l.oracle_load.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.POINTER(C.c_char_p),
+                                  C.POINTER(C.c_size_t), C.c_size_t]
+        l.oracle_free.restype = None
+        l.oracle_free.argtypes = [C.c_void_p]
+        l.oracle_decide.restype = C.c_int
+        l.oracle_decide.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double)]
+        _lib = l
+    return _lib
+
+
+class DecodedPairs:
+    """Pairs decoded once (untimed) into the oracle's Go-like value trees."""
+
+    def __init__(self, pairs):
+        n = len(pairs)
+        self.n = n
+        A = (C.c_char_p * n)(*[a for a, _ in pairs])
+        B = (C.c_char_p * n)(*[b for _, b in pairs])
+        AL = (C.c_size_t * n)(*[len(a) for a, _ in pairs])
+        BL = (C.c_size_t * n)(*[len(b) for _, b in pairs])
+        self.h = lib().oracle_load(A, AL, B, BL, n)
+
+    def decide(self, threads=1, min_seconds=0.0):
+        """-> (flags u8[n], sweeps, seconds)"""
+        flags = np.zeros(self.n, dtype=np.uint8)
+        sec = C.c_double()
+        sweeps = lib().oracle_decide(self.h, flags.ctypes.data_as(C.c_void_p), threads, min_seconds,
+                                     C.byref(sec))
+        return flags, sweeps, sec.value
+
+    def close(self):
+        if self.h:
+            lib().oracle_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

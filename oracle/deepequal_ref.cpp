@@ -1,0 +1,393 @@
+// CPU restatement of the kcp syncer change-detection predicates
+// (TEST INFRASTRUCTURE / CPU BASELINE ONLY -- never linked into the product).
+//
+// Follows, line by line:
+//   deepEqualApartFromStatus  pkg/syncer/specsyncer.go:17-41
+//   deepEqualStatus           pkg/syncer/statussyncer.go:15-27
+// over decoded unstructured trees with the value semantics of
+// equality.Semantic.DeepEqual (apimachinery third_party/forked/golang/reflect,
+// module pinned at go.mod:33), Unstructured.GetLabels/GetAnnotations
+// (NestedStringMap: fresh map per call, nil on any non-string value) and the
+// k8s util/json decode rules (int64 if ParseInt accepts the literal else
+// float64; duplicate keys last-wins; Go string unescaping).  Maps are hash maps
+// and every GetLabels/GetAnnotations/StringKeySet/Union call allocates, as the
+// Go code does, so the timing reflects the reference algorithm's structure.
+//
+// This is the "port" CPU baseline of bench.py and the large-sample checker of
+// the bench (decision bits only).  Parity of this restatement is pinned by
+// tests/test_oracle_cpp.py against the Python oracle and the Appendix A.4 KATs;
+// against the Go reference itself it is unpinned (no Go toolchain).
+#include <errno.h>
+#include <locale.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <chrono>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace oracle {
+
+struct Value;
+using Map = std::unordered_map<std::string, Value>;
+using Arr = std::vector<Value>;
+
+struct Value {
+    enum Kind : uint8_t { NIL, BOOL, INT, FLOAT, STR, MAP, ARR } k = NIL;
+    bool b = false;
+    int64_t i = 0;
+    double f = 0;
+    std::string s;
+    std::shared_ptr<Map> m;
+    std::shared_ptr<Arr> a;
+};
+
+// ------------------------------------------------------------ decoder
+struct Dec {
+    const unsigned char* p;
+    const unsigned char* e;
+    bool ok = true;
+    int depth = 0;
+
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++;
+    }
+    static void utf8(std::string& o, uint32_t r) {
+        if (r < 0x80) o += (char)r;
+        else if (r < 0x800) { o += (char)(0xC0 | (r >> 6)); o += (char)(0x80 | (r & 63)); }
+        else if (r < 0x10000) { o += (char)(0xE0 | (r >> 12)); o += (char)(0x80 | ((r >> 6) & 63)); o += (char)(0x80 | (r & 63)); }
+        else { o += (char)(0xF0 | (r >> 18)); o += (char)(0x80 | ((r >> 12) & 63)); o += (char)(0x80 | ((r >> 6) & 63)); o += (char)(0x80 | (r & 63)); }
+    }
+    // Go utf8.DecodeRune: length of a valid rune at q, or 0
+    int rune(const unsigned char* q) {
+        unsigned c = q[0];
+        int n;
+        unsigned lo = 0x80, hi = 0xBF;
+        if (c < 0x80) return 1;
+        if (c >= 0xC2 && c <= 0xDF) n = 2;
+        else if (c == 0xE0) { n = 3; lo = 0xA0; }
+        else if (c >= 0xE1 && c <= 0xEF && c != 0xED) n = 3;
+        else if (c == 0xED) { n = 3; hi = 0x9F; }
+        else if (c == 0xF0) { n = 4; lo = 0x90; }
+        else if (c >= 0xF1 && c <= 0xF3) n = 4;
+        else if (c == 0xF4) { n = 4; hi = 0x8F; }
+        else return 0;
+        if (e - q < n || q[1] < lo || q[1] > hi) return 0;
+        for (int j = 2; j < n; j++)
+            if (q[j] < 0x80 || q[j] > 0xBF) return 0;
+        return n;
+    }
+    int u4(const unsigned char* q) {
+        if (e - q < 6 || q[0] != '\\' || q[1] != 'u') return -1;
+        int v = 0;
+        for (int j = 2; j < 6; j++) {
+            int c = q[j], h;
+            if (c >= '0' && c <= '9') h = c - '0';
+            else if (c >= 'a' && c <= 'f') h = c - 'a' + 10;
+            else if (c >= 'A' && c <= 'F') h = c - 'A' + 10;
+            else return -1;
+            v = v * 16 + h;
+        }
+        return v;
+    }
+    bool str(std::string& o) {
+        p++;
+        for (;;) {
+            if (p >= e) return false;
+            unsigned c = *p;
+            if (c == '"') { p++; return true; }
+            if (c == '\\') {
+                if (e - p < 2) return false;
+                unsigned x = p[1];
+                const char* simple = "\"\\/bfnrt";
+                const char* rep = "\"\\/\b\f\n\r\t";
+                const char* f = x ? strchr(simple, (int)x) : nullptr;
+                if (f) { o += rep[f - simple]; p += 2; continue; }
+                if (x != 'u') return false;
+                int r = u4(p);
+                if (r < 0) return false;
+                p += 6;
+                if (r >= 0xD800 && r < 0xE000) {
+                    int r2 = u4(p);
+                    if (r < 0xDC00 && r2 >= 0xDC00 && r2 < 0xE000) {
+                        utf8(o, 0x10000 + (((uint32_t)r - 0xD800) << 10) + ((uint32_t)r2 - 0xDC00));
+                        p += 6;
+                        continue;
+                    }
+                    r = 0xFFFD;
+                }
+                utf8(o, (uint32_t)r);
+                continue;
+            }
+            if (c < 0x20) return false;
+            int n = rune(p);
+            if (n == 0) { o += "\xEF\xBF\xBD"; p++; }
+            else { o.append((const char*)p, n); p += n; }
+        }
+    }
+    bool num(Value& v) {
+        const unsigned char* s = p;
+        if (*p == '-') p++;
+        if (p >= e) return false;
+        if (*p == '0') p++;
+        else if (*p >= '1' && *p <= '9') { while (p < e && *p >= '0' && *p <= '9') p++; }
+        else return false;
+        bool integer = true;
+        if (p < e && *p == '.') {
+            integer = false;
+            p++;
+            if (p >= e || *p < '0' || *p > '9') return false;
+            while (p < e && *p >= '0' && *p <= '9') p++;
+        }
+        if (p < e && (*p == 'e' || *p == 'E')) {
+            integer = false;
+            p++;
+            if (p < e && (*p == '+' || *p == '-')) p++;
+            if (p >= e || *p < '0' || *p > '9') return false;
+            while (p < e && *p >= '0' && *p <= '9') p++;
+        }
+        std::string t((const char*)s, (size_t)(p - s));
+        if (integer) {  // strconv.ParseInt(t, 10, 64)
+            errno = 0;
+            char* end = nullptr;
+            long long x = strtoll(t.c_str(), &end, 10);
+            if (errno == 0 && end && *end == 0) {
+                v.k = Value::INT;
+                v.i = x;
+                return true;
+            }
+        }
+        static locale_t cl = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+        double d = strtod_l(t.c_str(), nullptr, cl);  // strconv.ParseFloat
+        if (isinf(d)) return false;
+        v.k = Value::FLOAT;
+        v.f = d;
+        return true;
+    }
+    bool val(Value& v) {
+        ws();
+        if (p >= e) return false;
+        unsigned c = *p;
+        if (c == '{') {
+            if (++depth > 10000) return false;
+            p++;
+            v.k = Value::MAP;
+            v.m = std::make_shared<Map>();
+            ws();
+            if (p < e && *p == '}') { p++; depth--; return true; }
+            for (;;) {
+                ws();
+                if (p >= e || *p != '"') return false;
+                std::string key;
+                if (!str(key)) return false;
+                ws();
+                if (p >= e || *p != ':') return false;
+                p++;
+                Value x;
+                if (!val(x)) return false;
+                (*v.m)[key] = std::move(x);  // last one wins
+                ws();
+                if (p >= e) return false;
+                c = *p++;
+                if (c == ',') continue;
+                if (c == '}') { depth--; return true; }
+                return false;
+            }
+        }
+        if (c == '[') {
+            if (++depth > 10000) return false;
+            p++;
+            v.k = Value::ARR;
+            v.a = std::make_shared<Arr>();
+            ws();
+            if (p < e && *p == ']') { p++; depth--; return true; }
+            for (;;) {
+                Value x;
+                if (!val(x)) return false;
+                v.a->push_back(std::move(x));
+                ws();
+                if (p >= e) return false;
+                c = *p++;
+                if (c == ',') continue;
+                if (c == ']') { depth--; return true; }
+                return false;
+            }
+        }
+        if (c == '"') { v.k = Value::STR; return str(v.s); }
+        if (e - p >= 4 && !memcmp(p, "true", 4)) { p += 4; v.k = Value::BOOL; v.b = true; return true; }
+        if (e - p >= 5 && !memcmp(p, "false", 5)) { p += 5; v.k = Value::BOOL; v.b = false; return true; }
+        if (e - p >= 4 && !memcmp(p, "null", 4)) { p += 4; v.k = Value::NIL; return true; }
+        if (c == '-' || (c >= '0' && c <= '9')) return num(v);
+        return false;
+    }
+};
+
+bool decode(const char* data, size_t n, Value& out) {
+    Dec d{(const unsigned char*)data, (const unsigned char*)data + n};
+    d.ws();
+    if (d.p >= d.e || *d.p != '{') return false;
+    if (!d.val(out)) return false;
+    d.ws();
+    return d.p == d.e;
+}
+
+// ------------------------------------------------------------ DeepEqual
+bool deep_equal(const Value& x, const Value& y) {
+    if (x.k == Value::NIL || y.k == Value::NIL) return x.k == Value::NIL && y.k == Value::NIL;
+    if (x.k != y.k) return false;
+    switch (x.k) {
+        case Value::BOOL: return x.b == y.b;
+        case Value::INT: return x.i == y.i;
+        case Value::FLOAT: return x.f == y.f;
+        case Value::STR: return x.s == y.s;
+        case Value::MAP: {
+            if (x.m->empty() || y.m->empty()) return x.m->empty() && y.m->empty();
+            if (x.m->size() != y.m->size()) return false;
+            for (const auto& kv : *x.m) {
+                auto it = y.m->find(kv.first);
+                if (it == y.m->end()) return false;
+                if (!deep_equal(kv.second, it->second)) return false;
+            }
+            return true;
+        }
+        case Value::ARR: {
+            if (x.a->empty() || y.a->empty()) return x.a->empty() && y.a->empty();
+            if (x.a->size() != y.a->size()) return false;
+            for (size_t i = 0; i < x.a->size(); i++)
+                if (!deep_equal((*x.a)[i], (*y.a)[i])) return false;
+            return true;
+        }
+        default: return true;
+    }
+}
+
+using StrMap = std::unordered_map<std::string, std::string>;
+
+// unstructured.NestedStringMap(obj, "metadata", field): a fresh map, or nil
+std::unique_ptr<StrMap> nested_string_map(const Value& obj, const char* field) {
+    auto md = obj.m->find("metadata");
+    if (md == obj.m->end() || md->second.k != Value::MAP) return nullptr;
+    auto f = md->second.m->find(field);
+    if (f == md->second.m->end() || f->second.k != Value::MAP) return nullptr;
+    std::unique_ptr<StrMap> out(new StrMap());
+    out->reserve(f->second.m->size());
+    for (const auto& kv : *f->second.m) {
+        if (kv.second.k != Value::STR) return nullptr;
+        (*out)[kv.first] = kv.second.s;
+    }
+    return out;
+}
+
+bool de_string_map(const StrMap* a, const StrMap* b) {
+    const bool ea = !a || a->empty(), eb = !b || b->empty();
+    if (ea || eb) return ea && eb;
+    if (a->size() != b->size()) return false;
+    for (const auto& kv : *a) {
+        auto it = b->find(kv.first);
+        if (it == b->end() || it->second != kv.second) return false;
+    }
+    return true;
+}
+
+static const Value kNil;
+
+// specsyncer.go:17-41
+bool deep_equal_apart_from_status(const Value& o, const Value& n) {
+    {
+        auto a = nested_string_map(o, "annotations"), b = nested_string_map(n, "annotations");  // :23
+        if (!de_string_map(a.get(), b.get())) return false;
+    }
+    {
+        auto a = nested_string_map(o, "labels"), b = nested_string_map(n, "labels");  // :26
+        if (!de_string_map(a.get(), b.get())) return false;
+    }
+    std::unordered_set<std::string> ok, nk;  // sets.StringKeySet x2 (:30-31)
+    for (const auto& kv : *o.m) ok.insert(kv.first);
+    for (const auto& kv : *n.m) nk.insert(kv.first);
+    std::unordered_set<std::string> uni(ok);  // Union (:32)
+    uni.insert(nk.begin(), nk.end());
+    std::vector<std::string> keys(uni.begin(), uni.end());  // UnsortedList
+    for (const std::string& key : keys) {
+        if (key == "metadata" || key == "status") continue;  // :33-35
+        auto x = o.m->find(key), y = n.m->find(key);
+        const Value& vx = x == o.m->end() ? kNil : x->second;
+        const Value& vy = y == n.m->end() ? kNil : y->second;
+        if (!deep_equal(vx, vy)) return false;  // :36
+    }
+    return true;
+}
+
+// statussyncer.go:15-27
+bool deep_equal_status(const Value& o, const Value& n) {
+    auto ns = n.m->find("status");
+    if (ns != n.m->end()) {  // :22
+        auto os = o.m->find("status");
+        return deep_equal(os == o.m->end() ? kNil : os->second, ns->second);  // :23-24
+    }
+    return false;  // :26
+}
+
+struct Pairs {
+    std::vector<Value> a, b;
+    std::vector<uint8_t> err;
+};
+
+}  // namespace oracle
+
+using namespace oracle;
+
+extern "C" {
+
+// decode n pairs (untimed); returns a handle
+void* oracle_load(const char* const* a, const size_t* alen, const char* const* b, const size_t* blen, size_t n) {
+    Pairs* p = new Pairs();
+    p->a.resize(n);
+    p->b.resize(n);
+    p->err.assign(n, 0);
+    for (size_t i = 0; i < n; i++) {
+        if (!decode(a[i], alen[i], p->a[i]) || !decode(b[i], blen[i], p->b[i])) p->err[i] = 1;
+    }
+    return p;
+}
+
+void oracle_free(void* h) { delete (Pairs*)h; }
+
+// runs both predicates over every pair; flags bit0 spec dirty, bit1 status
+// dirty, bit2 decode error.  Repeats the sweep until min_seconds elapsed;
+// returns the number of sweeps and the wall seconds of the timed region.
+int oracle_decide(void* h, uint8_t* flags, int threads, double min_seconds, double* seconds) {
+    Pairs* p = (Pairs*)h;
+    const size_t n = p->a.size();
+    if (threads < 1) threads = 1;
+    int sweeps = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    double el = 0;
+    do {
+        auto work = [&](int t) {
+            size_t b = n * t / threads, e = n * (t + 1) / threads;
+            for (size_t i = b; i < e; i++) {
+                uint8_t f;
+                if (p->err[i]) f = 7;
+                else f = (deep_equal_apart_from_status(p->a[i], p->b[i]) ? 0 : 1) |
+                         (deep_equal_status(p->a[i], p->b[i]) ? 0 : 2);
+                flags[i] = f;
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < threads; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        sweeps++;
+        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } while (el < min_seconds);
+    if (seconds) *seconds = el;
+    return sweeps;
+}
+
+}  // extern "C"
