@@ -153,21 +153,15 @@ def main():
     eng.sync()
 
     # ---------------- timed region
+    from kcp_amd import shard
+
+    def fill_from_hbm(col, buf, n):
+        db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(), n)
+
     def gather_step():
         counts = torch.empty(8, dtype=torch.int32, device=dev)
         db.export(G.EXPORT_COUNTS, counts.data_ptr(), 8)
-        allc = torch.empty(world * 8, dtype=torch.int32, device=dev)
-        dist.all_gather_into_tensor(allc, counts)
-        cc = allc.view(world, 8).cpu()
-        out = []
-        for col, what in ((0, G.EXPORT_SPEC_IDS), (1, G.EXPORT_STATUS_IDS)):
-            mx = max(1, int(cc[:, col].max()))
-            buf = torch.zeros(mx, dtype=torch.int32, device=dev)
-            db.export(what, buf.data_ptr(), mx, int(cc[rank, col]))
-            allb = torch.empty(world * mx, dtype=torch.int32, device=dev)
-            dist.all_gather_into_tensor(allb, buf)
-            out.append((allb, cc[:, col]))
-        return out
+        return shard.gather_dirty(counts, fill_from_hbm, rank, world, dist, dev, trim=False)
 
     eng.timing_reset()
     if world > 1:

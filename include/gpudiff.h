@@ -68,6 +68,9 @@ enum {
 /* context option flags */
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
 #define GPUDIFF_OPT_HOST_VALUE_HASH 0x2u /* hash long values on the host instead of K1 */
+#define GPUDIFF_OPT_NO_VALUE_HASH 0x4u   /* tests: leave value digests 0 so every equal-length
+                                            long value goes through byte confirmation (the
+                                            path a digest collision would take) */
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */

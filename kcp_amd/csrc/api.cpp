@@ -451,7 +451,7 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
     d->max_pairs = max_pairs;
     const uint64_t np = std::max<uint64_t>(max_pairs, 1);
     const uint64_t nchunks = (np + 63) / 64;
-    const uint64_t ntiles = np / 4096 + 2;
+    const uint64_t ntiles = 4 * (np / 4096 + 2);  // scan tile sums (4 x u32 for the chunk scan)
     uint4* cc = nullptr;
     if ((rc = dalloc(&d->pool, d->pool_cap)) || (rc = dalloc(&d->rows, np)) || (rc = dalloc(&d->pair_ids, np)) ||
         (rc = dalloc(&d->flags, np)) || (rc = dalloc(&d->caps, np)) || (rc = dalloc(&cc, nchunks)) ||
@@ -486,7 +486,7 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
                           c->stream));
     if (hb->used) HIPCHK(hipEventRecord(hb->used, c->stream));
     HIPCHK(launch_rebase(c->stream, d->rows, begin, end, base, d->pair_ids));
-    if (!c->ecfg.host_value_hash) {
+    if (!c->ecfg.host_value_hash && !(c->flags & GPUDIFF_OPT_NO_VALUE_HASH)) {
         if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
         HIPCHK(launch_value_hash(c->stream, d->rows, begin, end, d->pool));
         if (c->flags & GPUDIFF_OPT_TIMING) {
@@ -709,6 +709,7 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
         return GPUDIFF_E_NOMEM;
     }
     if (d->n_pairs) HIPCHK(hipMemcpy(rs->flags.data(), d->flags, d->n_pairs, hipMemcpyDeviceToHost));
+    for (uint8_t& f : rs->flags) f &= (uint8_t)(GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY | GPUDIFF_DECODE_ERROR);
     if (sum[0]) HIPCHK(hipMemcpy(rs->spec.data(), d->spec_ids, sum[0] * 4ull, hipMemcpyDeviceToHost));
     if (sum[1]) HIPCHK(hipMemcpy(rs->status.data(), d->status_ids, sum[1] * 4ull, hipMemcpyDeviceToHost));
     if (sum[2]) HIPCHK(hipMemcpy(rs->dirty.data(), d->dirty_ids, sum[2] * 4ull, hipMemcpyDeviceToHost));

@@ -4,14 +4,14 @@
 //   K2 k_compare      spec/status decision per pair: 16-B-per-lane streaming
 //                     compare of the two canonical segments (one wave per
 //                     pair, 64 pairs per wave-chunk, ballot counts per chunk)
-//   K3 k_scan_chunks  exclusive scan of chunk counts (one workgroup)
+//   K3 k_scan_*<V4>   reduce-then-scan of the per-chunk counts
 //      k_compact      ballot/prefix compaction of dirty pair IDs + scratch
 //                     slots for the changed-path join
-//   K4 k_join         wave-per-dirty-pair merge-join of the sorted leaf keys
-//                     in 64-key windows held in registers (cross-lane binary
-//                     search with ds_bpermute), byte-exact confirmation of
-//                     hash-equal long values, emits changed paths
-//   K5 k_scan_*       exclusive scan of per-pair path counts
+//   K4 k_join         merge-join of the sorted leaf keys, one wave per dirty
+//                     pair, in 64-key windows held in registers (cross-lane
+//                     binary search with ds_bpermute), byte-exact confirmation
+//                     of hash-equal long values; trivial pairs lane-parallel
+//   K5 k_scan_*<u32>  exclusive scan of per-pair path counts
 //   K6 k_copy_paths   compaction of the path scratch into the output CSR
 //
 // Semantics: DESIGN.md "Kernels"; reference predicates
@@ -25,7 +25,13 @@
 
 namespace gd {
 
+// per-pair flag byte written by K2: bits 0-2 are the public GPUDIFF_* result
+// bits; bits 3-6 are internal hints for K4/K6 (masked off on the host)
 constexpr uint32_t F_SPEC = 1u, F_STATUS = 2u, F_ERR = 4u;
+constexpr uint32_t F_SENT = 8u;    // status-absent-in-new sentinel path
+constexpr uint32_t F_JSPEC = 16u;  // spec region needs the merge-join
+constexpr uint32_t F_JSTAT = 32u;  // status region needs the merge-join
+constexpr uint32_t F_SEED = 64u;   // pair path-hash seed != 0
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -191,7 +197,10 @@ __device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, 
     }
     const bool spec_dirty = !spec_sz || ballot(mis1) != 0;
     const bool stat_dirty = !stat_sz || ballot(mis2) != 0;
-    d.flag = (spec_dirty ? F_SPEC : 0u) | (stat_dirty ? F_STATUS : 0u);
+    const bool stat_join = stat_dirty && (r.stat_l_a + r.stat_l_b) != 0u;
+    d.flag = (spec_dirty ? F_SPEC | F_JSPEC : 0u) | (stat_dirty ? F_STATUS : 0u) | (stat_join ? F_JSTAT : 0u) |
+             (stat_dirty && !has_st_b ? F_SENT : 0u) |
+             (((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu) ? F_SEED : 0u);
     d.cap = (spec_dirty ? r.spec_l_a + r.spec_l_b : 0u) +
             (stat_dirty ? r.stat_l_a + r.stat_l_b + (has_st_b ? 0u : 1u) : 0u);
     return d;
@@ -231,46 +240,117 @@ __global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restr
     }
 }
 
-// ---------------------------------------------------------------- K3
-// Exclusive scan of per-chunk uint4 counts by one 1024-thread workgroup.
-// summary[0..3] = totals (n_spec, n_status, n_dirty, total scratch cap).
-__global__ __launch_bounds__(1024) void k_scan_chunks(uint4* __restrict__ cc, uint32_t nchunks,
-                                                      uint32_t* __restrict__ summary) {
-    __shared__ uint4 part[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (nchunks + 1023u) / 1024u;
-    const uint32_t b = min(nchunks, t * per), e = min(nchunks, b + per);
-    uint4 s = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = b; i < e; i++) {
-        uint4 v = cc[i];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+// ---------------------------------------------------------------- scans
+// Reduce-then-scan over u32 or 4 x u32 elements in tiles of 4096 (256 threads
+// x 16), three launches: tile sums -> one-workgroup scan of tile sums ->
+// per-tile exclusive scan + base.  The element count comes from the host
+// (n_host) or from device memory (n_dev, e.g. the dirty count).
+constexpr uint32_t SCAN_TILE = 4096;
+
+struct V4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ uint32_t vadd(uint32_t a, uint32_t b) { return a + b; }
+__device__ __forceinline__ V4 vadd(const V4& a, const V4& b) { return V4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+template <class V> __device__ __forceinline__ V vzero() { return V{}; }
+__device__ __forceinline__ uint32_t vshfl(uint32_t v, uint32_t src) { return shfl32(v, src); }
+__device__ __forceinline__ V4 vshfl(const V4& v, uint32_t src) {
+    return V4{shfl32(v.x, src), shfl32(v.y, src), shfl32(v.z, src), shfl32(v.w, src)};
+}
+template <class V>
+__device__ __forceinline__ V wave_incl_scan_v(V v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        V o = vshfl(v, lane >= d ? lane - d : lane);
+        if (lane >= d) v = vadd(v, o);
     }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t scan_n(const uint32_t* n_dev, uint32_t n_host) { return n_dev ? *n_dev : n_host; }
+
+template <class V>
+__global__ __launch_bounds__(256) void k_scan_tiles(const V* __restrict__ in, const uint32_t* __restrict__ n_dev,
+                                                    uint32_t n_host, V* __restrict__ tile_sums) {
+    __shared__ V red[4];
+    const uint32_t n = scan_n(n_dev, n_host);
+    const uint32_t base = blockIdx.x * SCAN_TILE;
+    if (base >= n) return;
+    V s = vzero<V>();
+    for (uint32_t i = threadIdx.x; i < SCAN_TILE; i += 256)
+        if (base + i < n) s = vadd(s, in[base + i]);
+    s = vshfl(wave_incl_scan_v(s), 63);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = vadd(vadd(red[0], red[1]), vadd(red[2], red[3]));
+}
+
+// exclusive scan of the tile sums in place; total -> *total
+template <class V>
+__global__ __launch_bounds__(1024) void k_scan_top(V* __restrict__ tile_sums, const uint32_t* __restrict__ n_dev,
+                                                   uint32_t n_host, V* __restrict__ total) {
+    __shared__ V part[1024];
+    const uint32_t n = scan_n(n_dev, n_host);
+    const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (ntiles + 1023u) / 1024u;
+    const uint32_t b = min(ntiles, t * per), e = min(ntiles, b + per);
+    V s = vzero<V>();
+    for (uint32_t i = b; i < e; i++) s = vadd(s, tile_sums[i]);
     part[t] = s;
     __syncthreads();
     for (uint32_t d = 1; d < 1024; d <<= 1) {
-        uint4 o = make_uint4(0, 0, 0, 0);
-        if (t >= d) o = part[t - d];
+        V o = t >= d ? part[t - d] : vzero<V>();
         __syncthreads();
-        if (t >= d) {
-            uint4 v = part[t];
-            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
-            part[t] = v;
-        }
+        part[t] = vadd(part[t], o);
         __syncthreads();
     }
-    uint4 run = t ? part[t - 1] : make_uint4(0, 0, 0, 0);
+    V run = t ? part[t - 1] : vzero<V>();
     for (uint32_t i = b; i < e; i++) {
-        uint4 v = cc[i];
-        cc[i] = run;
-        run.x += v.x; run.y += v.y; run.z += v.z; run.w += v.w;
+        const V v = tile_sums[i];
+        tile_sums[i] = run;
+        run = vadd(run, v);
     }
-    if (t == 1023) {
-        uint4 tot = part[1023];
-        summary[0] = tot.x;
-        summary[1] = tot.y;
-        summary[2] = tot.z;
-        summary[3] = tot.w;
+    if (t == 1023) *total = part[1023];
+}
+
+// out[i] = exclusive prefix (may alias in); if out_n != nullptr, out[n] = total
+template <class V>
+__global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t* __restrict__ n_dev, uint32_t n_host,
+                                                    const V* __restrict__ tile_base, const V* __restrict__ total,
+                                                    V* out, bool write_terminal) {
+    __shared__ V wsum[4];
+    const uint32_t n = scan_n(n_dev, n_host);
+    const uint32_t base = blockIdx.x * SCAN_TILE;
+    if (base > n) return;
+    if (base == n) {
+        if (write_terminal && threadIdx.x == 0) out[n] = *total;
+        return;
     }
+    const uint32_t t = threadIdx.x;
+    V v[16];
+    V s = vzero<V>();
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t i = base + t * 16 + k;
+        v[k] = i < n ? in[i] : vzero<V>();
+        s = vadd(s, v[k]);
+    }
+    const V incl = wave_incl_scan_v(s);
+    if (lane_id() == 63) wsum[t >> 6] = incl;
+    __syncthreads();
+    V run = tile_base[blockIdx.x];
+    for (uint32_t w = 0; w < (t >> 6); w++) run = vadd(run, wsum[w]);
+    const V excl_thread = vshfl(incl, lane_id() ? lane_id() - 1 : 0);
+    if (lane_id()) run = vadd(run, excl_thread);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t i = base + t * 16 + k;
+        if (i < n) out[i] = run;
+        run = vadd(run, v[k]);
+    }
+    if (write_terminal && base + SCAN_TILE >= n && t == 0) out[n] = *total;
 }
 
 // One wave per chunk: ballot + prefix compaction into the ID lists.
@@ -339,26 +419,54 @@ __device__ __forceinline__ uint32_t tile_lower_bound(uint64_t x, uint64_t tile, 
     return j;
 }
 
-// byte-exact confirmation of two 16-aligned, zero padded values of equal length
-__device__ __forceinline__ bool bytes_differ(const uint8_t* a, const uint8_t* b, uint32_t len) {
-    const u32x4* pa = (const u32x4*)a;
-    const u32x4* pb = (const u32x4*)b;
-    const uint32_t n16 = (len + 15u) >> 4;
-    for (uint32_t k = 0; k < n16; k += 4) {
+// Byte-exact confirmation of every lane's pending (hash-equal, same length)
+// long value at once.  The lanes' 16-byte chunks are flattened into one index
+// space (prefix sum of chunk counts); each pass the wave compares 256 chunks
+// with 16-B loads (consecutive chunks of a value are consecutive addresses),
+// finding a chunk's owner lane by a cross-lane binary search over the prefix
+// sums.  Returns true in the lanes whose value differs (a hash collision).
+__device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a, const uint8_t* arena_b,
+                               uint32_t off_b, uint32_t len, uint32_t lane) {
+    const uint32_t n16 = need ? (len + 15u) >> 4 : 0u;
+    const uint32_t incl = wave_incl_scan(n16);
+    const uint32_t total = shfl32(incl, 63);
+    uint64_t bad = 0;  // lanes whose value differs (wave-uniform)
+    for (uint32_t base = 0; base < total; base += 256) {
         u32x4 xa[4], xb[4];
+        uint32_t own[4];
+        bool act[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (k + u < n16) {
-                xa[u] = pa[k + u];
-                xb[u] = pb[k + u];
+        for (int u = 0; u < 4; u++) {
+            const uint32_t g = base + u * 64 + lane;
+            act[u] = g < total;
+            // owner = number of lanes whose inclusive chunk prefix is <= g
+            uint32_t o = 0;
+#pragma unroll
+            for (uint32_t s = 64; s >= 1; s >>= 1) {
+                const uint32_t cand = o + s;
+                const uint32_t t = shfl32(incl, min(cand, 64u) - 1u);
+                if (cand <= 64u && t <= g) o = cand;
             }
-        bool ne = false;
+            own[u] = min(o, 63u);
+            const uint32_t oa = shfl32(off_a, own[u]), ob = shfl32(off_b, own[u]);
+            const uint32_t first = shfl32(incl - n16, own[u]);
+            if (act[u]) {
+                const uint32_t k = g - first;
+                xa[u] = *(const u32x4*)(arena_a + oa + 16u * k);
+                xb[u] = *(const u32x4*)(arena_b + ob + 16u * k);
+            }
+        }
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (k + u < n16) ne |= neq16(xa[u], xb[u]);
-        if (ne) return true;
+        for (int u = 0; u < 4; u++) {
+            uint64_t m = ballot(act[u] && neq16(xa[u], xb[u]));
+            while (m) {  // collisions only: practically never taken
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                bad |= 1ull << shfl32(own[u], j);
+            }
+        }
     }
-    return false;
+    return (bad >> lane) & 1ull;
 }
 
 // Merge-join of one region; returns the number of paths emitted.  Emission
@@ -400,8 +508,7 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         const uint32_t obj = shfl32(offB, min(jA, 63u));
         const bool matchA = inA && jA < nb && kbj == ka;
         bool differ = matchA && (ma != mbj || xa != xbj);
-        if (matchA && !differ && meta_long(ma))
-            differ = bytes_differ(A.arena + offA, B.arena + obj, ma >> 3);
+        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, ma >> 3, lane);
         // resolve B keys against the A window
         const uint32_t iB = tile_lower_bound(kb, ka, na);
         const uint64_t kai = shfl64(ka, min(iB, 63u));
@@ -445,30 +552,33 @@ __device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
 template <bool EMIT>
 __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
                               uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane) {
-    if (f & F_ERR) return 0;
     uint32_t n = 0;
-    if (f & F_SPEC) {
+    if (f & F_JSPEC) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
         n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane);
     }
-    if (f & F_STATUS) {
+    if (f & F_JSTAT) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
         n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane);
-        if (!(r.flags_b & GPUDIFF_OBJ_HAS_STATUS)) {
-            if (EMIT && lane == 0) {
-                out_h[base + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
-                out_k[base + n] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
-            }
-            n += 1;
+    }
+    if (f & F_SENT) {
+        if (EMIT && lane == 0) {
+            out_h[base + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
+            out_k[base + n] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
         }
+        n += 1;
     }
     return n;
 }
 
-// One wave per dirty pair.  Writes the pair's changed paths into its scratch
-// slot (sized by the cap computed in K2) and its count.
+// One wave per 64 consecutive dirty pairs.  Pairs that need no merge-join
+// (status dirty only because the new object has no status key, and no
+// status leaves on either side: every ConfigMap/Secret update) are finished
+// lane-parallel; the others are joined one at a time by the whole wave.
+// Paths go to the pair's scratch slot (sized by K2's cap), counts to
+// path_count.
 __global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict__ rows,
                                               const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
                                               const uint32_t* __restrict__ dirty_idx,
@@ -481,100 +591,45 @@ __global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict
     const uint32_t ndirty = summary[2];
     const bool fits = (uint64_t)summary[3] <= scratch_cap;
     if (!fits && blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
-    for (uint32_t d = wave; d < ndirty; d += nwaves) {
-        const uint32_t p = dirty_idx[d];
-        const gpudiff_pair_row r = rows[p];
-        const uint32_t f = flags[p];
-        uint32_t n;
-        if (fits) n = join_pair<true>(r, f, pool, mask, sh, sk, scratch_off[d], lane);
-        else n = join_pair<false>(r, f, pool, mask, sh, sk, 0, lane);
-        if (lane == 0) path_count[d] = n;
+    const uint64_t sent0 = status_sentinel_hash(0, mask);
+    const uint32_t nchunks = (ndirty + 63u) >> 6;
+    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+        const uint32_t d = (c << 6) + lane;
+        const bool valid = d < ndirty;
+        const uint32_t p = valid ? dirty_idx[d] : 0u;
+        const uint32_t f = valid ? flags[p] : 0u;
+        const uint32_t so = valid ? scratch_off[d] : 0u;
+        const bool needj = (f & (F_JSPEC | F_JSTAT)) != 0u;
+        if (valid && !needj) {
+            uint32_t n = 0;
+            if (f & F_SENT) {
+                if (fits) {
+                    sh[so] = (f & F_SEED)
+                                 ? status_sentinel_hash((rows[p].flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
+                                 : sent0;
+                    sk[so] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                }
+                n = 1;
+            }
+            path_count[d] = n;
+        }
+        uint64_t m = ballot(valid && needj);
+        while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t pk = uni(shfl32(p, k)), fk = uni(shfl32(f, k)), sok = uni(shfl32(so, k));
+            const gpudiff_pair_row r = rows[pk];
+            uint32_t n;
+            if (fits) n = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane);
+            else n = join_pair<false>(r, fk, pool, mask, sh, sk, 0, lane);
+            if (lane == 0) path_count[(c << 6) + k] = n;
+        }
     }
-}
-
-// ---------------------------------------------------------------- K5
-// Exclusive scan of path_count[0..summary[2]) into path_off, 3 kernels.
-constexpr uint32_t SCAN_TILE = 4096;  // 256 threads x 16
-
-__global__ __launch_bounds__(256) void k_scan_tiles(const uint32_t* __restrict__ in, const uint32_t* __restrict__ summary,
-                                                    uint32_t* __restrict__ tile_sums) {
-    __shared__ uint32_t red[4];
-    const uint32_t n = summary[2];
-    const uint32_t base = blockIdx.x * SCAN_TILE;
-    if (base >= n) return;
-    uint32_t s = 0;
-    for (uint32_t i = threadIdx.x; i < SCAN_TILE; i += 256) {
-        const uint32_t k = base + i;
-        if (k < n) s += in[k];
-    }
-    s = wave_sum(s);
-    if (lane_id() == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
-__global__ __launch_bounds__(1024) void k_scan_top(uint32_t* __restrict__ tile_sums, uint32_t* __restrict__ summary) {
-    __shared__ uint32_t part[1024];
-    const uint32_t n = summary[2];
-    const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (ntiles + 1023u) / 1024u;
-    const uint32_t b = min(ntiles, t * per), e = min(ntiles, b + per);
-    uint32_t s = 0;
-    for (uint32_t i = b; i < e; i++) s += tile_sums[i];
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        uint32_t o = t >= d ? part[t - d] : 0u;
-        __syncthreads();
-        part[t] += o;
-        __syncthreads();
-    }
-    uint32_t run = t ? part[t - 1] : 0u;
-    for (uint32_t i = b; i < e; i++) {
-        const uint32_t v = tile_sums[i];
-        tile_sums[i] = run;
-        run += v;
-    }
-    if (t == 1023) summary[5] = part[1023];  // total paths
-}
-
-__global__ __launch_bounds__(256) void k_scan_apply(const uint32_t* __restrict__ in, const uint32_t* __restrict__ summary,
-                                                    const uint32_t* __restrict__ tile_base, uint32_t* __restrict__ out) {
-    __shared__ uint32_t wsum[4];
-    const uint32_t n = summary[2];
-    const uint32_t base = blockIdx.x * SCAN_TILE;
-    if (base > n) return;
-    if (base == n) {  // terminal offset
-        if (threadIdx.x == 0) out[n] = summary[5];
-        return;
-    }
-    // each thread owns 16 consecutive elements
-    const uint32_t t = threadIdx.x;
-    uint32_t v[16];
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const uint32_t i = base + t * 16 + k;
-        v[k] = i < n ? in[i] : 0u;
-        s += v[k];
-    }
-    const uint32_t incl = wave_incl_scan(s);
-    if (lane_id() == 63) wsum[t >> 6] = incl;
-    __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t w = 0; w < (t >> 6); w++) wbase += wsum[w];
-    uint32_t run = tile_base[blockIdx.x] + wbase + incl - s;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const uint32_t i = base + t * 16 + k;
-        if (i < n) out[i] = run;
-        run += v[k];
-    }
-    if (base + SCAN_TILE >= n && t == 0) out[n] = summary[5];
 }
 
 // ---------------------------------------------------------------- K6
+// Lane per dirty pair (most pairs have 1-3 paths); pairs with many paths
+// (list shifts in deep objects) are copied by the whole wave.
 __global__ __launch_bounds__(256) void k_copy_paths(const uint32_t* __restrict__ summary,
                                                     const uint32_t* __restrict__ scratch_off,
                                                     const uint32_t* __restrict__ path_off,
@@ -585,12 +640,29 @@ __global__ __launch_bounds__(256) void k_copy_paths(const uint32_t* __restrict__
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t ndirty = summary[2];
-    if (summary[4]) return;  // scratch overflow: host re-runs with a larger slot pool
-    for (uint32_t d = wave; d < ndirty; d += nwaves) {
-        const uint32_t so = scratch_off[d], po = path_off[d], c = path_count[d];
-        for (uint32_t i = lane; i < c; i += 64) {
-            oh[po + i] = sh[so + i];
-            ok[po + i] = sk[so + i];
+    if (summary[4]) return;  // scratch overflow: the host grows the slot pool and re-runs K4-K6
+    const uint32_t nchunks = (ndirty + 63u) >> 6;
+    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+        const uint32_t d = (c << 6) + lane;
+        const bool valid = d < ndirty;
+        const uint32_t so = valid ? scratch_off[d] : 0u;
+        const uint32_t po = valid ? path_off[d] : 0u;
+        const uint32_t cnt = valid ? path_count[d] : 0u;
+        const bool big = cnt > 16u;
+        if (!big)
+            for (uint32_t i = 0; i < cnt; i++) {
+                oh[po + i] = sh[so + i];
+                ok[po + i] = sk[so + i];
+            }
+        uint64_t m = ballot(big);
+        while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t sok = uni(shfl32(so, k)), pok = uni(shfl32(po, k)), ck = uni(shfl32(cnt, k));
+            for (uint32_t i = lane; i < ck; i += 64) {
+                oh[pok + i] = sh[sok + i];
+                ok[pok + i] = sk[sok + i];
+            }
         }
     }
 }
@@ -637,7 +709,13 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b) {
 
 hipError_t launch_compact(hipStream_t s, const DiffBuffers& b) {
     const uint32_t nchunks = (b.n_pairs + 63) / 64;
-    k_scan_chunks<<<1, 1024, 0, s>>>((uint4*)b.chunk_counts, nchunks, b.summary);
+    const uint32_t ntiles = (nchunks + SCAN_TILE - 1) / SCAN_TILE;
+    V4* cc = (V4*)b.chunk_counts;
+    V4* ts = (V4*)b.tile_sums;
+    V4* total = (V4*)b.summary;  // summary[0..3] = n_spec, n_status, n_dirty, scratch cap
+    k_scan_tiles<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, nchunks, ts);
+    k_scan_top<V4><<<1, 1024, 0, s>>>(ts, nullptr, nchunks, total);
+    k_scan_apply<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, nchunks, ts, total, cc, false);
     k_compact<<<grid_for(nchunks, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
                                                                  (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
                                                                  b.dirty_ids, b.dirty_idx, b.scratch_off);
@@ -645,20 +723,20 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b) {
 }
 
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b) {
-    k_join<<<grid_for(b.n_pairs, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off,
-                                                                b.summary, b.scratch_cap, b.hash_mask, b.scratch_h,
-                                                                b.scratch_k, b.path_count);
+    k_join<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
+        b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.summary, b.scratch_cap, b.hash_mask, b.scratch_h,
+        b.scratch_k, b.path_count);
     return hipGetLastError();
 }
 
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b) {
-    const uint32_t ntiles = (b.n_pairs + SCAN_TILE - 1) / SCAN_TILE + 1;
-    k_scan_tiles<<<ntiles, 256, 0, s>>>(b.path_count, b.summary, b.tile_sums);
-    k_scan_top<<<1, 1024, 0, s>>>(b.tile_sums, b.summary);
-    k_scan_apply<<<ntiles, 256, 0, s>>>(b.path_count, b.summary, b.tile_sums, b.path_off);
-    k_copy_paths<<<grid_for(b.n_pairs, kPersistBlocks), 256, 0, s>>>(b.summary, b.scratch_off, b.path_off,
-                                                                      b.path_count, b.scratch_h, b.scratch_k,
-                                                                      b.out_h, b.out_k);
+    const uint32_t ntiles = b.n_pairs / SCAN_TILE + 1;  // covers base == n for the terminal offset
+    const uint32_t* nd = b.summary + 2;
+    k_scan_tiles<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums);
+    k_scan_top<uint32_t><<<1, 1024, 0, s>>>(b.tile_sums, nd, 0, b.summary + 5);
+    k_scan_apply<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums, b.summary + 5, b.path_off, true);
+    k_copy_paths<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
+        b.summary, b.scratch_off, b.path_off, b.path_count, b.scratch_h, b.scratch_k, b.out_h, b.out_k);
     return hipGetLastError();
 }
 

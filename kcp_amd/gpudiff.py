@@ -23,7 +23,7 @@ E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUN
 SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR = 0x1, 0x2, 0x4
 PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
-OPT_TIMING, OPT_HOST_VALUE_HASH = 0x1, 0x2
+OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
 OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_SEED_SHIFT = 0x1, 0x2, 8
@@ -274,9 +274,11 @@ class Engine:
     """One gpudiff context (one GPU, one stream, one submitting thread)."""
 
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
-                 timing: bool = False, path_hash_bits: int = 64, host_value_hash: bool = False):
+                 timing: bool = False, path_hash_bits: int = 64, host_value_hash: bool = False,
+                 no_value_hash: bool = False):
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
-                 flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0),
+                 flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0) |
+                       (OPT_NO_VALUE_HASH if no_value_hash else 0),
                  path_hash_bits=path_hash_bits)
         h = C.c_void_p()
         _chk(_lib.gpudiff_open(C.byref(o), C.byref(h)), "gpudiff_open")

@@ -1,0 +1,76 @@
+"""Multi-GPU layer: logical-cluster sharding and the one collective.
+
+The reference runs one independent syncer per logical cluster
+(pkg/reconciler/cluster/cluster.go:125-138), each with its own informers and
+queue (pkg/syncer/syncer.go:88-132), so pairs shard by logical cluster with no
+data-path exchange.  The north star's single collective -- an all-gather of
+per-rank dirty counts and dirty pair IDs so every rank holds the node-wide
+dirty sets -- is `gather_dirty`, written against torch.distributed so the same
+code runs over RCCL/xGMI ("nccl" backend on ROCm) on GPUs and over gloo on CPU
+in the tests.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+
+def lpt_assign(cluster_weights: Sequence[int], world: int) -> np.ndarray:
+    """Greedy LPT bin-packing of clusters onto `world` ranks: heaviest cluster
+    first onto the least-loaded rank (ties: lower cluster id, lower rank).
+    Returns owner rank per cluster.  Same rule as gpudiff_synth_open."""
+    w = np.asarray(cluster_weights, dtype=np.int64)
+    order = sorted(range(len(w)), key=lambda c: (-int(w[c]), c))
+    load = [0] * world
+    owner = np.zeros(len(w), dtype=np.int32)
+    for c in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        owner[c] = r
+        load[r] += int(w[c])
+    return owner
+
+
+def shard_pairs(cluster_of_pair: Sequence[int], world: int) -> List[np.ndarray]:
+    """Pair indices per rank (batch order kept within a rank)."""
+    cl = np.asarray(cluster_of_pair, dtype=np.int64)
+    ids, counts = np.unique(cl, return_counts=True)
+    owner_of = dict(zip(ids.tolist(), lpt_assign(counts, world).tolist()))
+    owners = np.array([owner_of[c] for c in cl.tolist()], dtype=np.int32)
+    return [np.nonzero(owners == r)[0] for r in range(world)]
+
+
+def gather_dirty(counts, fill, rank: int, world: int, dist, device=None, trim: bool = True):
+    """All-gather of the per-rank dirty counts, then of the spec- and
+    status-dirty pair IDs (padded to the largest count).
+
+    counts: int32 tensor [8] (n_spec, n_status, ...) on `device`;
+    fill(col, buf, n): writes this rank's n IDs of list `col` (0 spec,
+    1 status) into the int32 tensor `buf` (the GPU path copies straight from
+    HBM with gpudiff_dbatch_export).  Returns (spec_all, status_all): 1-D
+    tensors in rank order if `trim`, else the padded [world, max] gathers and
+    the host count matrix."""
+    import torch
+
+    dev = device if device is not None else counts.device
+    allc = torch.empty(world * counts.numel(), dtype=counts.dtype, device=dev)
+    dist.all_gather_into_tensor(allc, counts)
+    cc = allc.view(world, -1).cpu()
+    out = []
+    for col in (0, 1):
+        mx = max(1, int(cc[:, col].max()))
+        buf = torch.zeros(mx, dtype=torch.int32, device=dev)
+        fill(col, buf, int(cc[rank, col]))
+        allb = torch.empty(world * mx, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(allb, buf)
+        allb = allb.view(world, mx)
+        out.append(torch.cat([allb[r, :int(cc[r, col])] for r in range(world)]) if trim else allb)
+    return (out[0], out[1]) if trim else (out[0], out[1], cc)
+
+
+def tensor_fill(spec_ids, status_ids):
+    """fill() for gather_dirty over ID tensors already in memory."""
+    def fill(col, buf, n):
+        if n:
+            buf[:n] = (spec_ids if col == 0 else status_ids)[:n]
+    return fill

@@ -1,0 +1,54 @@
+"""The C-ABI libraries load and export every function the headers declare
+(no compute calls: these run without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    src = open(os.path.join(ROOT, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gpudiff_[a-z0-9_]+)\s*\(", src)) -
+                  {"gpudiff_seg_bytes", "gpudiff_meta", "gpudiff_meta_tag", "gpudiff_meta_len",
+                   "gpudiff_meta_is_long", "gpudiff_meta_arena"})
+
+
+@pytest.mark.parametrize("header,lib", [("gpudiff.h", "kcp_amd/libgpudiff.so"),
+                                        ("gpudiff_synth.h", "kcp_amd/libgpudiff_synth.so")])
+def test_exports(header, lib):
+    names = declared(header)
+    assert len(names) > 5
+    so = ctypes.CDLL(os.path.join(ROOT, lib))
+    missing = [n for n in names if not hasattr(so, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    from kcp_amd import gpudiff as G
+    bound = {n for n, _, _ in G.SIGNATURES}
+    assert set(declared("gpudiff.h")) == bound
+
+
+def test_host_only_context_refuses_device_work():
+    from kcp_amd import gpudiff as G
+    e = G.Engine(device=G.DEVICE_NONE)
+    with pytest.raises(G.GpuDiffError) as ei:
+        e.submit([(b"{}", b"{}")])
+    assert ei.value.code == G.E_NODEVICE
+    assert G.lib().gpudiff_abi_version() == 1
+    e.close()
+
+
+def test_header_compiles_as_c():
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write('#include "gpudiff.h"\n#include "gpudiff_synth.h"\nint main(void){return 0;}\n')
+        r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), c, "-o",
+                            os.path.join(d, "t")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr

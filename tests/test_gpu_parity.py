@@ -103,6 +103,27 @@ def test_host_vs_device_value_hash(eng):
     e2.close()
 
 
+def test_byte_confirmation_without_digests():
+    """With value digests left at 0, every equal-length long value is decided
+    by the byte confirmation alone -- the path a digest collision takes."""
+    rnd = random.Random(12)
+    pairs = []
+    for i in range(300):
+        a = json.loads(J(BASE))
+        a["spec"]["vals"] = ["".join(rnd.choice("xy") for _ in range(rnd.randint(9, 400))) for _ in range(12)]
+        b = json.loads(json.dumps(a))
+        if i % 2:
+            k = rnd.randrange(12)
+            s = b["spec"]["vals"][k]
+            j = rnd.randrange(len(s))
+            b["spec"]["vals"][k] = s[:j] + ("x" if s[j] == "y" else "y") + s[j + 1:]  # same length, one byte
+        pairs.append((J(a), J(b)))
+    e = G.Engine(device=0, no_value_hash=True)
+    res = e.diff_pairs(pairs)
+    assert_matches(res, pairs)
+    e.close()
+
+
 def test_k1_value_hashes_on_device(eng):
     pairs, _, _ = make_pairs(100, seed=7)
     hb = eng.encode(pairs)

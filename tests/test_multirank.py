@@ -1,0 +1,87 @@
+"""World-size-2 coverage of the multi-GPU path on CPU (gloo): logical-cluster
+sharding (LPT, clusters never split, all pairs covered exactly once) and the
+all-gather of dirty counts and IDs, checked against a single-rank view."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kcp_amd import shard
+from kcp_amd import synth as S
+
+
+def test_lpt_assign_balanced():
+    w = [100, 60, 50, 40, 30, 20, 10, 10]
+    owner = shard.lpt_assign(w, 2)
+    loads = [sum(x for x, o in zip(w, owner) if o == r) for r in range(2)]
+    assert abs(loads[0] - loads[1]) <= 10
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_synth_shards_partition_population(world):
+    cfg = S.make_cfg("config2", n_pairs=20000, n_clusters=300)
+    seen = []
+    sizes = []
+    for r in range(world):
+        p = S.Population(cfg, world, r)
+        sizes.append(p.n)
+        seen.append(np.array([p.global_index(i) for i in range(p.n)], dtype=np.int64))
+        p.close()
+    allg = np.concatenate(seen)
+    assert allg.size == cfg.n_pairs and np.unique(allg).size == cfg.n_pairs
+    assert max(sizes) - min(sizes) <= max(sizes) * 0.2  # LPT keeps ranks within a few %
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, flags_all, owners, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = np.nonzero(owners == rank)[0]
+    f = flags_all[mine]
+    spec = torch.tensor(mine[(f & 1) != 0], dtype=torch.int32)
+    stat = torch.tensor(mine[(f & 2) != 0], dtype=torch.int32)
+    counts = torch.zeros(8, dtype=torch.int32)
+    counts[0], counts[1] = spec.numel(), stat.numel()
+    sa, ta = shard.gather_dirty(counts, shard.tensor_fill(spec, stat), rank, world, dist)
+    q.put((rank, sorted(sa.tolist()), sorted(ta.tolist())))
+    dist.destroy_process_group()
+
+
+def test_gather_dirty_gloo_world2():
+    rnd = np.random.default_rng(3)
+    n = 5000
+    clusters = rnd.integers(0, 97, n)
+    flags = rnd.integers(0, 4, n).astype(np.uint8)
+    parts = shard.shard_pairs(clusters, 2)
+    owners = np.zeros(n, dtype=np.int32)
+    for r, idx in enumerate(parts):
+        owners[idx] = r
+    # a cluster never spans ranks
+    for c in np.unique(clusters):
+        assert np.unique(owners[clusters == c]).size == 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, flags, owners, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_s = sorted(np.nonzero(flags & 1)[0].tolist())
+    want_t = sorted(np.nonzero(flags & 2)[0].tolist())
+    for rank, s, t in res:
+        assert s == want_s and t == want_t
