@@ -71,6 +71,10 @@ enum {
 #define GPUDIFF_OPT_NO_VALUE_HASH 0x4u   /* tests: leave value digests 0 so every equal-length
                                             long value goes through byte confirmation (the
                                             path a digest collision would take) */
+/* tuning knobs (A/B measurements; 0 = defaults) */
+#define GPUDIFF_OPT_K2_VARIANT_SHIFT 8u  /* 4 bits: decision-kernel load policy / unroll */
+#define GPUDIFF_OPT_K2_BLOCKS_SHIFT 12u  /* 4 bits: resident blocks per CU for the decision kernel */
+#define GPUDIFF_OPT_SEGMENTS_SHIFT 16u   /* 4 bits: force the number of pipelined batch segments */
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */
@@ -141,12 +145,13 @@ typedef struct gpudiff_batch_stats {
 
 typedef struct gpudiff_timings {
     float value_hash_ms;  /* K1 over the last appended chunk */
-    float compare_ms;     /* K2 */
-    float compact_ms;     /* K3 (scan + compaction) */
-    float join_ms;        /* K4 changed-path merge-join */
+    float compare_ms;     /* K2: all k2_launches launches of a pass (back to back on the stream) */
+    float compact_ms;     /* K3 (scan + compaction); 0 when overlapped with K2 (segmented pass) */
+    float join_ms;        /* K4 merge-join; segmented pass: the part not hidden behind K2 */
     float emit_ms;        /* K5 + K6 path scan and copy */
     float total_ms;       /* first to last event of gpudiff_diff */
     uint32_t n_passes;    /* diff passes averaged (since gpudiff_timing_reset) */
+    uint32_t k2_launches; /* K2 launches per pass (batch segments) */
 } gpudiff_timings;
 
 /* ---- library ---- */

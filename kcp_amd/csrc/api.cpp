@@ -43,6 +43,8 @@ struct Part {
 
 }  // namespace
 
+static constexpr uint32_t kMaxSegments = 8;
+
 struct gpudiff_hbatch {
     uint8_t* pool = nullptr;
     gpudiff_pair_row* rows = nullptr;
@@ -74,6 +76,7 @@ struct gpudiff_dbatch {
     uint32_t* path_count = nullptr;
     uint32_t* path_off = nullptr;
     uint32_t* tile_sums = nullptr;
+    uint4* seg_tot = nullptr;  // running totals after each diff segment
     uint64_t scratch_cap = 0;
     uint64_t* scratch_h = nullptr;
     uint8_t* scratch_k = nullptr;
@@ -107,6 +110,11 @@ struct gpudiff_ctx {
     bool k1_recorded = false;
     std::vector<std::array<hipEvent_t, 5>> pass_ev;
     size_t n_pass = 0;
+    uint32_t pass_k2_launches = 1;
+    // segmented diff pass: side stream for K3/K4, one event per segment
+    hipStream_t side = nullptr;
+    hipEvent_t seg_ev[kMaxSegments] = {};
+    hipEvent_t side_done = nullptr;
     // submit ring
     gpudiff_dbatch* ring[2] = {nullptr, nullptr};
     gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
@@ -131,7 +139,7 @@ static int dalloc(T** p, uint64_t count) {
 static void dfree_all(gpudiff_dbatch* d) {
     void* ps[] = {d->pool, d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
-                  d->tile_sums, d->scratch_h, d->scratch_k, d->out_h, d->out_k};
+                  d->tile_sums, d->seg_tot, d->scratch_h, d->scratch_k, d->out_h, d->out_k};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);
@@ -178,6 +186,8 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.out_h = d->out_h;
     b.out_k = d->out_k;
     b.hash_mask = c->hash_mask;
+    b.k2_variant = (c->flags >> GPUDIFF_OPT_K2_VARIANT_SHIFT) & 0xFu;
+    b.k2_blocks_per_cu = (c->flags >> GPUDIFF_OPT_K2_BLOCKS_SHIFT) & 0xFu;
     return b;
 }
 
@@ -251,6 +261,9 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
             c->own_stream = true;
         }
         for (auto& e : c->ev_k1) HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        for (auto& e : c->seg_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming));
     }
     *out = c.release();
     return GPUDIFF_OK;
@@ -269,6 +282,13 @@ void gpudiff_close(gpudiff_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         for (auto& a : c->pass_ev)
             for (auto& e : a) (void)hipEventDestroy(e);
+        for (auto& e : c->seg_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (c->side_done) (void)hipEventDestroy(c->side_done);
+        if (c->side) {
+            (void)hipStreamSynchronize(c->side);
+            (void)hipStreamDestroy(c->side);
+        }
         if (c->own_stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -458,7 +478,7 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
         (rc = dalloc(&d->summary, 8)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
         (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
-        (rc = dalloc(&d->tile_sums, ntiles))) {
+        (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments))) {
         d->chunk_counts = cc;
         dfree_all(d.get());
         return rc;
@@ -588,13 +608,25 @@ static hipEvent_t* pass_events(gpudiff_ctx* c) {
     return c->pass_ev[c->n_pass].data();
 }
 
-static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d, hipEvent_t* ev) {
+// K4 over every dirty pair + K5/K6 on the main stream (overflow re-run)
+static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d) {
     DiffBuffers b = buffers_of(c, d);
-    HIPCHK(launch_join(c->stream, b));
-    if (ev) HIPCHK(hipEventRecord(ev[3], c->stream));
+    const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);
+    HIPCHK(launch_join(c->stream, b, 0, nchunks, nullptr, (const uint4*)d->summary));
     HIPCHK(launch_emit(c->stream, b));
-    if (ev) HIPCHK(hipEventRecord(ev[4], c->stream));
     return GPUDIFF_OK;
+}
+
+// Segments of the diff pass.  K2 is HBM-bound and K3/K4 latency-bound, so a
+// large batch is cut into segments: K2 of segment s+1 streams on the main
+// stream while K3 (compaction) and K4 (merge-join) of segment s run on the
+// side stream; only the last segment's K3/K4 and the global K5/K6 are exposed.
+static uint32_t choose_segments(uint64_t n_pairs, uint32_t flags) {
+    const uint64_t nchunks = (n_pairs + 63) / 64;
+    const uint32_t forced = (flags >> GPUDIFF_OPT_SEGMENTS_SHIFT) & 0xFu;  // tests / tuning
+    if (forced) return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({forced, kMaxSegments, nchunks}));
+    if (n_pairs < (1u << 20)) return 1;
+    return (uint32_t)std::min<uint64_t>(kMaxSegments, n_pairs >> 19);
 }
 
 int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
@@ -608,19 +640,52 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         ev = pass_events(c);
         if (!ev) return GPUDIFF_E_DEVICE;
     }
-    HIPCHK(hipMemsetAsync(d->summary, 0, 8 * sizeof(uint32_t), c->stream));
-    if (ev) HIPCHK(hipEventRecord(ev[0], c->stream));
+    hipStream_t ms = c->stream;
+    HIPCHK(hipMemsetAsync(d->summary, 0, 8 * sizeof(uint32_t), ms));
+    if (ev) HIPCHK(hipEventRecord(ev[0], ms));
     DiffBuffers b = buffers_of(c, d);
-    if (d->n_pairs) {
-        HIPCHK(launch_compare(c->stream, b));
-        if (ev) HIPCHK(hipEventRecord(ev[1], c->stream));
-        HIPCHK(launch_compact(c->stream, b));
-        if (ev) HIPCHK(hipEventRecord(ev[2], c->stream));
-        if ((rc = enqueue_join_emit(c, d, ev))) return rc;
+    const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);
+    const uint32_t S = choose_segments(d->n_pairs, c->flags);
+    uint4* total = (uint4*)d->summary;  // summary[0..3]: n_spec, n_status, n_dirty, scratch cap
+    if (d->n_pairs == 0) {
+        HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), ms));
+    } else if (S == 1) {
+        HIPCHK(launch_compare(ms, b, 0, nchunks));
+        if (ev) HIPCHK(hipEventRecord(ev[1], ms));
+        HIPCHK(launch_compact(ms, b, 0, nchunks, nullptr, total));
+        if (ev) HIPCHK(hipEventRecord(ev[2], ms));
+        HIPCHK(launch_join(ms, b, 0, nchunks, nullptr, total));
+        if (ev) HIPCHK(hipEventRecord(ev[3], ms));
+        HIPCHK(launch_emit(ms, b));
+        if (ev) HIPCHK(hipEventRecord(ev[4], ms));
     } else {
-        HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), c->stream));
+        const uint32_t per = (nchunks + S - 1) / S;
+        uint32_t last = 0;
+        for (uint32_t s = 0; s < S && s * per < nchunks; s++) last = s;
+        for (uint32_t s = 0; s <= last; s++) {
+            const uint32_t c0 = s * per, c1 = std::min(nchunks, c0 + per);
+            HIPCHK(launch_compare(ms, b, c0, c1));
+            HIPCHK(hipEventRecord(c->seg_ev[s], ms));
+            HIPCHK(hipStreamWaitEvent(c->side, c->seg_ev[s], 0));
+            const uint4* before = s ? d->seg_tot + (s - 1) : nullptr;
+            uint4* after = s == last ? total : d->seg_tot + s;
+            HIPCHK(launch_compact(c->side, b, c0, c1, before, after));
+            HIPCHK(launch_join(c->side, b, c0, c1, before, after));
+        }
+        if (ev) {
+            HIPCHK(hipEventRecord(ev[1], ms));
+            HIPCHK(hipEventRecord(ev[2], ms));
+            HIPCHK(hipEventRecord(ev[3], c->side));
+        }
+        HIPCHK(hipEventRecord(c->side_done, c->side));
+        HIPCHK(hipStreamWaitEvent(ms, c->side_done, 0));
+        HIPCHK(launch_emit(ms, b));
+        if (ev) HIPCHK(hipEventRecord(ev[4], ms));
     }
-    if (ev) c->n_pass++;
+    if (ev) {
+        c->pass_k2_launches = S;
+        c->n_pass++;
+    }
     HIPCHK(hipEventRecord(d->done, c->stream));
     if (d->ticket) c->tickets.erase(d->ticket);
     d->ticket = c->next_ticket++;
@@ -655,6 +720,7 @@ int gpudiff_last_timings(gpudiff_ctx* c, gpudiff_timings* t) {
     float ms = 0;
     if (c->k1_recorded && hipEventElapsedTime(&ms, c->ev_k1[0], c->ev_k1[1]) == hipSuccess) t->value_hash_ms = ms;
     t->n_passes = (uint32_t)c->n_pass;
+    t->k2_launches = c->pass_k2_launches;
     if (!c->n_pass) return GPUDIFF_OK;
     double s[5] = {0, 0, 0, 0, 0};
     for (size_t i = 0; i < c->n_pass; i++) {
@@ -690,7 +756,7 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
         if ((rc = ensure_scratch(d, sum[3]))) return rc;
         uint32_t zero = 0;
         HIPCHK(hipMemcpyAsync(d->summary + 4, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
-        if ((rc = enqueue_join_emit(c, d, nullptr))) return rc;
+        if ((rc = enqueue_join_emit(c, d))) return rc;
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
         if (sum[4]) return GPUDIFF_E_CAPACITY;

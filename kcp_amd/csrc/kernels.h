@@ -32,14 +32,21 @@ struct DiffBuffers {
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
+    uint32_t k2_variant;        // tuning: 0 default (NT loads, 4 chunks in flight per lane per object)
+    uint32_t k2_blocks_per_cu;  // tuning: 0 = 8 resident 256-thread blocks per CU
 };
 
 hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
                          uint32_t* pair_ids);
 hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool);
-hipError_t launch_compare(hipStream_t s, const DiffBuffers& b);
-hipError_t launch_compact(hipStream_t s, const DiffBuffers& b);
-hipError_t launch_join(hipStream_t s, const DiffBuffers& b);
+// K2 over the 64-pair chunks [c0, c1)
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1);
+// K3 over chunks [c0, c1): running (n_spec, n_status, n_dirty, cap) totals before -> after
+hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
+                          uint4* after);
+// K4 over the dirty pairs the segment added (before.z .. after.z)
+hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
+                       const uint4* after);
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
 
 }  // namespace gd

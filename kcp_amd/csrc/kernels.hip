@@ -152,6 +152,13 @@ struct PairDecision {
     uint32_t cap;
 };
 
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+template <bool NT, int U>
 __device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, const uint8_t* __restrict__ pool,
                                                      uint32_t lane) {
     PairDecision d{0u, 0u};
@@ -172,21 +179,21 @@ __device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, 
     const u32x4* b2 = (const u32x4*)(pool + r.off_b + seg_b);
     const uint32_t ntot = n1 + n2;
     bool mis1 = false, mis2 = false;
-    for (uint32_t base = 0; base < ntot; base += 256) {
-        u32x4 va[4], vb[4];
+    for (uint32_t base = 0; base < ntot; base += 64 * U) {
+        u32x4 va[U], vb[U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             const uint32_t i = base + u * 64 + lane;
             if (i < ntot) {
                 const bool in1 = i < n1;
                 const u32x4* pa = in1 ? a1 + i : a2 + (i - n1);
                 const u32x4* pb = in1 ? b1 + i : b2 + (i - n1);
-                va[u] = __builtin_nontemporal_load(pa);
-                vb[u] = __builtin_nontemporal_load(pb);
+                va[u] = ld16<NT>(pa);
+                vb[u] = ld16<NT>(pb);
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < U; u++) {
             const uint32_t i = base + u * 64 + lane;
             if (i < ntot) {
                 const bool ne = neq16(va[u], vb[u]);
@@ -207,22 +214,24 @@ __device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, 
 }
 
 // One wave per chunk of 64 consecutive pairs; the wave walks its pairs in
-// order, all 64 lanes streaming both objects of a pair with 16-byte loads.
+// order, all 64 lanes streaming both objects of a pair with 16-byte loads
+// (NT: non-temporal; U: 16-B chunks in flight per lane per object).
+template <bool NT, int U>
 __global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restrict__ rows,
                                                  const uint8_t* __restrict__ pool, uint32_t n,
                                                  uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
-                                                 uint4* __restrict__ chunk_counts) {
+                                                 uint4* __restrict__ chunk_counts, uint32_t c_begin,
+                                                 uint32_t c_end) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t nchunks = (n + 63u) >> 6;
-    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
         const uint32_t p0 = c << 6;
         const uint32_t cnt = min(64u, n - p0);
         uint32_t myflag = 0, mycap = 0;
         for (uint32_t k = 0; k < cnt; k++) {
             const gpudiff_pair_row r = rows[p0 + k];
-            const PairDecision d = compare_pair(r, pool, lane);
+            const PairDecision d = compare_pair<NT, U>(r, pool, lane);
             if (lane == k) {
                 myflag = d.flag;
                 mycap = d.cap;
@@ -286,11 +295,13 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const V* __restrict__ in, co
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = vadd(vadd(red[0], red[1]), vadd(red[2], red[3]));
 }
 
-// exclusive scan of the tile sums in place; total -> *total
+// exclusive scan of the tile sums in place, offset by *base_in (the running
+// total of earlier batch segments, nullptr = 0); *total = base + sum
 template <class V>
 __global__ __launch_bounds__(1024) void k_scan_top(V* __restrict__ tile_sums, const uint32_t* __restrict__ n_dev,
-                                                   uint32_t n_host, V* __restrict__ total) {
+                                                   uint32_t n_host, const V* base_in, V* total) {
     __shared__ V part[1024];
+    const V base = base_in ? *base_in : vzero<V>();
     const uint32_t n = scan_n(n_dev, n_host);
     const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     const uint32_t t = threadIdx.x;
@@ -306,13 +317,14 @@ __global__ __launch_bounds__(1024) void k_scan_top(V* __restrict__ tile_sums, co
         part[t] = vadd(part[t], o);
         __syncthreads();
     }
-    V run = t ? part[t - 1] : vzero<V>();
+    V run = vadd(base, t ? part[t - 1] : vzero<V>());
     for (uint32_t i = b; i < e; i++) {
         const V v = tile_sums[i];
         tile_sums[i] = run;
         run = vadd(run, v);
     }
-    if (t == 1023) *total = part[1023];
+    __syncthreads();  // every thread has read base_in before it may be overwritten (total may alias it)
+    if (t == 1023) *total = vadd(base, part[1023]);
 }
 
 // out[i] = exclusive prefix (may alias in); if out_n != nullptr, out[n] = total
@@ -358,13 +370,13 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                                                  const uint32_t* __restrict__ pair_ids, uint32_t n,
                                                  const uint4* __restrict__ cbase, uint32_t* __restrict__ spec_ids,
                                                  uint32_t* __restrict__ status_ids, uint32_t* __restrict__ dirty_ids,
-                                                 uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off) {
+                                                 uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off,
+                                                 uint32_t c_begin, uint32_t c_end) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t nchunks = (n + 63u) >> 6;
     const uint64_t lt = mask_lt(lane);
-    for (uint32_t c = wave; c < nchunks; c += nwaves) {
+    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
         const uint32_t p = (c << 6) + lane;
         const bool valid = p < n;
         const uint32_t f = valid ? flags[p] : 0u;
@@ -578,23 +590,27 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
 // status leaves on either side: every ConfigMap/Secret update) are finished
 // lane-parallel; the others are joined one at a time by the whole wave.
 // Paths go to the pair's scratch slot (sized by K2's cap), counts to
-// path_count.
+// path_count.  Works on the dirty pairs of one batch segment: indices
+// [before.z, after.z) of the running (n_spec, n_status, n_dirty, cap) totals.
 __global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict__ rows,
                                               const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
                                               const uint32_t* __restrict__ dirty_idx,
                                               const uint32_t* __restrict__ scratch_off, uint32_t* __restrict__ summary,
+                                              const uint4* __restrict__ tot_before, const uint4* __restrict__ tot_after,
                                               uint64_t scratch_cap, uint64_t mask, uint64_t* __restrict__ sh,
                                               uint8_t* __restrict__ sk, uint32_t* __restrict__ path_count) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t ndirty = summary[2];
-    const bool fits = (uint64_t)summary[3] <= scratch_cap;
+    const uint32_t d_begin = tot_before ? tot_before->z : 0u;
+    const uint4 after = *tot_after;
+    const uint32_t ndirty = after.z;
+    const bool fits = (uint64_t)after.w <= scratch_cap;
     if (!fits && blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
-    const uint32_t nchunks = (ndirty + 63u) >> 6;
+    const uint32_t nchunks = (ndirty - d_begin + 63u) >> 6;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
-        const uint32_t d = (c << 6) + lane;
+        const uint32_t d = d_begin + (c << 6) + lane;
         const bool valid = d < ndirty;
         const uint32_t p = valid ? dirty_idx[d] : 0u;
         const uint32_t f = valid ? flags[p] : 0u;
@@ -622,7 +638,7 @@ __global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict
             uint32_t n;
             if (fits) n = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane);
             else n = join_pair<false>(r, fk, pool, mask, sh, sk, 0, lane);
-            if (lane == 0) path_count[(c << 6) + k] = n;
+            if (lane == 0) path_count[d_begin + (c << 6) + k] = n;
         }
     }
 }
@@ -700,32 +716,46 @@ hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_compare(hipStream_t s, const DiffBuffers& b) {
-    const uint32_t nchunks = (b.n_pairs + 63) / 64;
-    k_compare<<<grid_for(nchunks, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.n_pairs, b.flags, b.caps,
-                                                                 (uint4*)b.chunk_counts);
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1) {
+    // 4 resident 256-thread blocks per CU (16 waves/CU) streamed faster than 8 in
+    // the interleaved A/B (tools/ab_k2.py) and leave wave slots for K3/K4 of the
+    // previous segment running concurrently on the side stream
+    const uint32_t cap = 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 4u);
+    const dim3 grid(grid_for(c1 - c0, cap));
+    uint4* cc = (uint4*)b.chunk_counts;
+#define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1
+    switch (b.k2_variant) {  // tuning variants (GPUDIFF_OPT_K2_VARIANT_SHIFT); 0 is the default
+        case 1: k_compare<false, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 2: k_compare<true, 8><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 3: k_compare<false, 8><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 4: k_compare<true, 2><<<grid, 256, 0, s>>>(K2ARGS); break;
+        default: k_compare<true, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
+    }
+#undef K2ARGS
     return hipGetLastError();
 }
 
-hipError_t launch_compact(hipStream_t s, const DiffBuffers& b) {
-    const uint32_t nchunks = (b.n_pairs + 63) / 64;
-    const uint32_t ntiles = (nchunks + SCAN_TILE - 1) / SCAN_TILE;
-    V4* cc = (V4*)b.chunk_counts;
+// K3 over the chunks [c0, c1) of one segment: running totals before -> after
+hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
+                          uint4* after) {
+    const uint32_t n = c1 - c0;
+    const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+    V4* cc = (V4*)b.chunk_counts + c0;
     V4* ts = (V4*)b.tile_sums;
-    V4* total = (V4*)b.summary;  // summary[0..3] = n_spec, n_status, n_dirty, scratch cap
-    k_scan_tiles<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, nchunks, ts);
-    k_scan_top<V4><<<1, 1024, 0, s>>>(ts, nullptr, nchunks, total);
-    k_scan_apply<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, nchunks, ts, total, cc, false);
-    k_compact<<<grid_for(nchunks, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
-                                                                 (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
-                                                                 b.dirty_ids, b.dirty_idx, b.scratch_off);
+    if (ntiles) k_scan_tiles<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts);
+    k_scan_top<V4><<<1, 1024, 0, s>>>(ts, nullptr, n, (const V4*)before, (V4*)after);
+    if (ntiles) k_scan_apply<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts, (const V4*)after, cc, false);
+    k_compact<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
+                                                           (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
+                                                           b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1);
     return hipGetLastError();
 }
 
-hipError_t launch_join(hipStream_t s, const DiffBuffers& b) {
-    k_join<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
-        b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.summary, b.scratch_cap, b.hash_mask, b.scratch_h,
-        b.scratch_k, b.path_count);
+hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
+                       const uint4* after) {
+    k_join<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off,
+                                                              b.summary, before, after, b.scratch_cap, b.hash_mask,
+                                                              b.scratch_h, b.scratch_k, b.path_count);
     return hipGetLastError();
 }
 
@@ -733,7 +763,7 @@ hipError_t launch_emit(hipStream_t s, const DiffBuffers& b) {
     const uint32_t ntiles = b.n_pairs / SCAN_TILE + 1;  // covers base == n for the terminal offset
     const uint32_t* nd = b.summary + 2;
     k_scan_tiles<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums);
-    k_scan_top<uint32_t><<<1, 1024, 0, s>>>(b.tile_sums, nd, 0, b.summary + 5);
+    k_scan_top<uint32_t><<<1, 1024, 0, s>>>(b.tile_sums, nd, 0, nullptr, b.summary + 5);
     k_scan_apply<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums, b.summary + 5, b.path_off, true);
     k_copy_paths<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
         b.summary, b.scratch_off, b.path_off, b.path_count, b.scratch_h, b.scratch_k, b.out_h, b.out_k);

@@ -90,7 +90,7 @@ class BatchStats(C.Structure):
 class Timings(C.Structure):
     _fields_ = [("value_hash_ms", C.c_float), ("compare_ms", C.c_float), ("compact_ms", C.c_float),
                 ("join_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float),
-                ("n_passes", C.c_uint32)]
+                ("n_passes", C.c_uint32), ("k2_launches", C.c_uint32)]
 
 
 # (name, restype, argtypes) for every symbol of include/gpudiff.h
@@ -275,10 +275,10 @@ class Engine:
 
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
                  timing: bool = False, path_hash_bits: int = 64, host_value_hash: bool = False,
-                 no_value_hash: bool = False):
+                 no_value_hash: bool = False, flags: int = 0):
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
                  flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0) |
-                       (OPT_NO_VALUE_HASH if no_value_hash else 0),
+                       (OPT_NO_VALUE_HASH if no_value_hash else 0) | flags,
                  path_hash_bits=path_hash_bits)
         h = C.c_void_p()
         _chk(_lib.gpudiff_open(C.byref(o), C.byref(h)), "gpudiff_open")

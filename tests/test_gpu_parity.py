@@ -84,6 +84,25 @@ def test_long_values_and_list_shift(eng):
     assert_matches(res, pairs)
 
 
+@pytest.mark.parametrize("segments", [2, 3, 8])
+def test_segmented_pipeline(segments):
+    """K2 of segment s+1 overlapped with K3/K4 of segment s on the side stream:
+    identical results to the single-segment pass."""
+    pairs, cl, _ = make_pairs(2600, seed=13, mutate_frac=0.3, pretty_frac=0)
+    e = G.Engine(device=0, flags=segments << 16, timing=True)
+    hb = e.encode(pairs)
+    db = e.device_batch(hb.info().pool_bytes + 4096, len(pairs))
+    db.append(hb)
+    res = e.wait(e.diff(db))
+    assert_matches(res, pairs)
+    assert e.timings().k2_launches == segments
+    res2 = e.wait(e.diff(db))
+    assert np.array_equal(res.path_hashes, res2.path_hashes)
+    db.free()
+    hb.free()
+    e.close()
+
+
 def test_forced_collisions():
     e = G.Engine(device=0, path_hash_bits=8)
     pairs, _, _ = make_pairs(200, seed=5, mix=(("cm", 0.5), ("deploy", 0.5)), mutate_frac=0.5)

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output into profiles/: per-kernel average duration from
+the --kernel-trace --stats pass, and HBM bytes per launch from separate
+--pmc FETCH_SIZE / WRITE_SIZE passes, corrected as MI355X_MICROARCH.md §HBM
+prescribes (counters in KiB; gfx950 FETCH_SIZE reports 1/2 of wide coalesced
+reads, so it is doubled).
+
+usage: pmc_summary.py KT_DIR FETCH_DIR WRITE_DIR BENCH_JSON OUT_JSON
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def load_stats(d):
+    out = {}
+    with open(os.path.join(d, "run_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            out[r["Name"]] = dict(calls=int(r["Calls"]), avg_ms=float(r["AverageNs"]) / 1e6,
+                                  pct=float(r["Percentage"]))
+    return out
+
+
+def load_counter(d, name):
+    agg = collections.defaultdict(list)
+    with open(os.path.join(d, "run_counter_collection.csv")) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == name:
+                agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def short(name):
+    return name.split("(")[0].replace("gd::", "")
+
+
+def main():
+    kt, fd, wd, bench_json, out = sys.argv[1:6]
+    stats = load_stats(kt)
+    fetch = load_counter(fd, "FETCH_SIZE")
+    write = load_counter(wd, "WRITE_SIZE")
+    bench = json.load(open(bench_json))
+    kernels = {}
+    for name, s in stats.items():
+        k = dict(s)
+        if name in fetch:
+            k["fetch_bytes_corrected"] = fetch[name] * 1024 * 2
+        if name in write:
+            k["write_bytes"] = write[name] * 1024
+        if "fetch_bytes_corrected" in k and "write_bytes" in k:
+            k["hbm_bytes"] = k["fetch_bytes_corrected"] + k["write_bytes"]
+        kernels[short(name)] = k
+    k2 = kernels.get("k_compare", {})
+    alg = bench["roofline"]["bytes_per_launch"]
+    summary = dict(
+        workload=bench["config"]["workload"],
+        kernel="k_compare",
+        algorithmic_bytes_per_launch=alg,
+        hbm_bytes_per_launch=k2.get("hbm_bytes"),
+        traffic_over_algorithmic=(k2["hbm_bytes"] / alg) if k2.get("hbm_bytes") else None,
+        rocprof_avg_ms=k2.get("avg_ms"),
+        bench_hip_event_avg_ms=bench["roofline"]["avg_launch_ms"],
+        note="FETCH_SIZE x2 (gfx950 half-count of 16-B/lane reads) + WRITE_SIZE, KiB -> bytes; "
+             "separate --pmc passes; scalar row loads are counted at the doubled rate too",
+        kernels=kernels,
+    )
+    with open(out, "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: v for k, v in summary.items() if k != "kernels"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
