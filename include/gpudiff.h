@@ -75,6 +75,9 @@ enum {
 #define GPUDIFF_OPT_K2_VARIANT_SHIFT 8u  /* 4 bits: decision-kernel load policy / unroll */
 #define GPUDIFF_OPT_K2_BLOCKS_SHIFT 12u  /* 4 bits: resident blocks per CU for the decision kernel */
 #define GPUDIFF_OPT_SEGMENTS_SHIFT 16u   /* 4 bits: force the number of pipelined batch segments */
+#define GPUDIFF_OPT_NO_K2_ALT 0x100000u  /* keep every K2 segment on the main stream */
+#define GPUDIFF_OPT_ARENA_SHIFT 21u      /* 4 bits: shrink the per-wave path arena 2^k-fold
+                                            (tests: forces pairs through the deferred K4 path) */
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */

@@ -44,6 +44,9 @@ struct Part {
 }  // namespace
 
 static constexpr uint32_t kMaxSegments = 8;
+// changed-path arena entries per K2 wave (a pair whose worst case does not
+// fit the wave's remaining arena is deferred to K4)
+static constexpr uint32_t kArenaPerWave = 16384;
 
 struct gpudiff_hbatch {
     uint8_t* pool = nullptr;
@@ -77,6 +80,11 @@ struct gpudiff_dbatch {
     uint32_t* path_off = nullptr;
     uint32_t* tile_sums = nullptr;
     uint4* seg_tot = nullptr;  // running totals after each diff segment
+    uint32_t* path_src = nullptr;
+    uint32_t* path_cnt = nullptr;
+    uint64_t arena_cap = 0;
+    uint64_t* arena_h = nullptr;
+    uint8_t* arena_k = nullptr;
     uint64_t scratch_cap = 0;
     uint64_t* scratch_h = nullptr;
     uint8_t* scratch_k = nullptr;
@@ -113,8 +121,10 @@ struct gpudiff_ctx {
     uint32_t pass_k2_launches = 1;
     // segmented diff pass: side stream for K3/K4, one event per segment
     hipStream_t side = nullptr;
+    hipStream_t k2alt = nullptr;  // second K2 stream (odd segments)
     hipEvent_t seg_ev[kMaxSegments] = {};
     hipEvent_t side_done = nullptr;
+    hipEvent_t alt_start = nullptr;
     // submit ring
     gpudiff_dbatch* ring[2] = {nullptr, nullptr};
     gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
@@ -139,26 +149,35 @@ static int dalloc(T** p, uint64_t count) {
 static void dfree_all(gpudiff_dbatch* d) {
     void* ps[] = {d->pool, d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
-                  d->tile_sums, d->seg_tot, d->scratch_h, d->scratch_k, d->out_h, d->out_k};
+                  d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
+                  d->scratch_h, d->scratch_k, d->out_h, d->out_k};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);
 }
 
-static int ensure_scratch(gpudiff_dbatch* d, uint64_t need) {
-    if (need <= d->scratch_cap && d->scratch_h) return GPUDIFF_OK;
-    uint64_t cap = std::max<uint64_t>(need + need / 8, 1u << 16);
-    if (d->scratch_h) (void)hipFree(d->scratch_h);
-    if (d->scratch_k) (void)hipFree(d->scratch_k);
-    if (d->out_h) (void)hipFree(d->out_h);
-    if (d->out_k) (void)hipFree(d->out_k);
-    d->scratch_h = d->out_h = nullptr;
-    d->scratch_k = d->out_k = nullptr;
+// Changed-path buffers: the K2 wave arenas (arena entries), the K4 scratch for
+// deferred pairs (scratch entries) and the compacted output, which can never
+// hold more than both together.
+static int ensure_paths(gpudiff_dbatch* d, uint64_t arena, uint64_t scratch) {
+    const bool ok_a = arena <= d->arena_cap && d->arena_h;
+    const bool ok_s = scratch <= d->scratch_cap && d->scratch_h;
+    if (ok_a && ok_s) return GPUDIFF_OK;
+    arena = std::max(arena, d->arena_cap);
+    scratch = std::max<uint64_t>({scratch + scratch / 8, d->scratch_cap, 1u << 16});
+    void* ps[] = {d->arena_h, d->arena_k, d->scratch_h, d->scratch_k, d->out_h, d->out_k};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    d->arena_h = d->scratch_h = d->out_h = nullptr;
+    d->arena_k = d->scratch_k = d->out_k = nullptr;
+    d->arena_cap = d->scratch_cap = 0;
     int rc;
-    if ((rc = dalloc(&d->scratch_h, cap)) || (rc = dalloc(&d->scratch_k, cap)) || (rc = dalloc(&d->out_h, cap)) ||
-        (rc = dalloc(&d->out_k, cap)))
+    if ((rc = dalloc(&d->arena_h, arena)) || (rc = dalloc(&d->arena_k, arena)) ||
+        (rc = dalloc(&d->scratch_h, scratch)) || (rc = dalloc(&d->scratch_k, scratch)) ||
+        (rc = dalloc(&d->out_h, arena + scratch)) || (rc = dalloc(&d->out_k, arena + scratch)))
         return rc;
-    d->scratch_cap = cap;
+    d->arena_cap = arena;
+    d->scratch_cap = scratch;
     return GPUDIFF_OK;
 }
 
@@ -180,6 +199,11 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.path_count = d->path_count;
     b.path_off = d->path_off;
     b.tile_sums = d->tile_sums;
+    b.path_src = d->path_src;
+    b.path_cnt = d->path_cnt;
+    b.arena_h = d->arena_h;
+    b.arena_k = d->arena_k;
+    b.arena_per_wave = kArenaPerWave >> ((c->flags >> GPUDIFF_OPT_ARENA_SHIFT) & 0xFu);
     b.scratch_h = d->scratch_h;
     b.scratch_k = d->scratch_k;
     b.scratch_cap = d->scratch_cap;
@@ -262,8 +286,10 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
         }
         for (auto& e : c->ev_k1) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->k2alt, hipStreamNonBlocking));
         for (auto& e : c->seg_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->alt_start, hipEventDisableTiming));
     }
     *out = c.release();
     return GPUDIFF_OK;
@@ -285,10 +311,12 @@ void gpudiff_close(gpudiff_ctx* c) {
         for (auto& e : c->seg_ev)
             if (e) (void)hipEventDestroy(e);
         if (c->side_done) (void)hipEventDestroy(c->side_done);
-        if (c->side) {
-            (void)hipStreamSynchronize(c->side);
-            (void)hipStreamDestroy(c->side);
-        }
+        if (c->alt_start) (void)hipEventDestroy(c->alt_start);
+        for (hipStream_t s : {c->side, c->k2alt})
+            if (s) {
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamDestroy(s);
+            }
         if (c->own_stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -478,6 +506,7 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
         (rc = dalloc(&d->summary, 8)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
         (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
+        (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) ||
         (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments))) {
         d->chunk_counts = cc;
         dfree_all(d.get());
@@ -625,8 +654,11 @@ static uint32_t choose_segments(uint64_t n_pairs, uint32_t flags) {
     const uint64_t nchunks = (n_pairs + 63) / 64;
     const uint32_t forced = (flags >> GPUDIFF_OPT_SEGMENTS_SHIFT) & 0xFu;  // tests / tuning
     if (forced) return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({forced, kMaxSegments, nchunks}));
-    if (n_pairs < (1u << 20)) return 1;
-    return (uint32_t)std::min<uint64_t>(kMaxSegments, n_pairs >> 19);
+    // Measured (tools/ab_k2.py, config3 10M pairs): the overlapped K3/K4 take as
+    // much HBM/issue time from K2 as they hide at 5% dirty pairs, so one
+    // segment is the default; segmenting pays off when dirty pairs dominate.
+    (void)n_pairs;
+    return 1;
 }
 
 int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
@@ -634,7 +666,12 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     int rc = set_device(c);
     if (rc) return rc;
     // scratch for changed paths: sized from the batch, grown on overflow
-    if ((rc = ensure_scratch(d, std::max<uint64_t>(d->n_pairs * 2 + d->leaves / 8, 1u << 16)))) return rc;
+    {
+        const uint32_t nch = (uint32_t)((d->n_pairs + 63) / 64);
+        DiffBuffers b0 = buffers_of(c, d);
+        const uint64_t arena = (uint64_t)k2_grid_waves(b0, std::max(nch, 1u)) * kArenaPerWave;
+        if ((rc = ensure_paths(d, arena, std::max<uint64_t>(d->n_pairs / 64, 1u << 16)))) return rc;
+    }
     hipEvent_t* ev = nullptr;
     if ((c->flags & GPUDIFF_OPT_TIMING) && d->n_pairs) {
         ev = pass_events(c);
@@ -650,7 +687,7 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     if (d->n_pairs == 0) {
         HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), ms));
     } else if (S == 1) {
-        HIPCHK(launch_compare(ms, b, 0, nchunks));
+        HIPCHK(launch_compare(ms, b, 0, nchunks, 0, 1));
         if (ev) HIPCHK(hipEventRecord(ev[1], ms));
         HIPCHK(launch_compact(ms, b, 0, nchunks, nullptr, total));
         if (ev) HIPCHK(hipEventRecord(ev[2], ms));
@@ -662,19 +699,29 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         const uint32_t per = (nchunks + S - 1) / S;
         uint32_t last = 0;
         for (uint32_t s = 0; s < S && s * per < nchunks; s++) last = s;
+        // K2 segments alternate between the main stream and k2alt so a segment's
+        // waves fill the CUs while the previous segment's last waves drain
+        const bool alt = !(c->flags & GPUDIFF_OPT_NO_K2_ALT);
+        if (alt) {
+            HIPCHK(hipEventRecord(c->alt_start, ms));
+            HIPCHK(hipStreamWaitEvent(c->k2alt, c->alt_start, 0));
+        }
+        hipStream_t k2s = ms;
         for (uint32_t s = 0; s <= last; s++) {
             const uint32_t c0 = s * per, c1 = std::min(nchunks, c0 + per);
-            HIPCHK(launch_compare(ms, b, c0, c1));
-            HIPCHK(hipEventRecord(c->seg_ev[s], ms));
+            k2s = (alt && (s & 1)) ? c->k2alt : ms;
+            HIPCHK(launch_compare(k2s, b, c0, c1, s, last + 1));
+            HIPCHK(hipEventRecord(c->seg_ev[s], k2s));
             HIPCHK(hipStreamWaitEvent(c->side, c->seg_ev[s], 0));
             const uint4* before = s ? d->seg_tot + (s - 1) : nullptr;
             uint4* after = s == last ? total : d->seg_tot + s;
             HIPCHK(launch_compact(c->side, b, c0, c1, before, after));
             HIPCHK(launch_join(c->side, b, c0, c1, before, after));
         }
-        if (ev) {
-            HIPCHK(hipEventRecord(ev[1], ms));
-            HIPCHK(hipEventRecord(ev[2], ms));
+        if (ev) {  // ev[1] after both K2 streams' last segments
+            if (alt && last > 0) HIPCHK(hipStreamWaitEvent(k2s, c->seg_ev[last - 1], 0));
+            HIPCHK(hipEventRecord(ev[1], k2s));
+            HIPCHK(hipEventRecord(ev[2], k2s));
             HIPCHK(hipEventRecord(ev[3], c->side));
         }
         HIPCHK(hipEventRecord(c->side_done, c->side));
@@ -753,7 +800,7 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
     uint32_t sum[8];
     HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
     if (sum[4]) {  // path scratch overflow: grow to the exact need and redo the join
-        if ((rc = ensure_scratch(d, sum[3]))) return rc;
+        if ((rc = ensure_paths(d, d->arena_cap, sum[3]))) return rc;
         uint32_t zero = 0;
         HIPCHK(hipMemcpyAsync(d->summary + 4, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
         if ((rc = enqueue_join_emit(c, d))) return rc;

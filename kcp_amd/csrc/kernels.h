@@ -8,7 +8,7 @@
 namespace gd {
 
 // Device buffers of one diff pass.  summary[]: 0 n_spec, 1 n_status,
-// 2 n_dirty, 3 total scratch cap, 4 overflow, 5 n_paths, 6..7 reserved.
+// 2 n_dirty, 3 K4 scratch cap, 4 overflow, 5 n_paths, 6 deferred pairs, 7 -.
 struct DiffBuffers {
     const gpudiff_pair_row* rows;
     const uint8_t* pool;
@@ -16,35 +16,44 @@ struct DiffBuffers {
     uint32_t n_pairs;
     uint8_t* flags;
     uint32_t* caps;
-    void* chunk_counts;  // uint4 per 64 pairs
+    uint32_t* path_src;   // per pair: arena index of the paths K2 wrote
+    uint32_t* path_cnt;   // per pair: number of those paths
+    void* chunk_counts;   // uint4 per 64 pairs
     uint32_t* summary;
     uint32_t* spec_ids;
     uint32_t* status_ids;
     uint32_t* dirty_ids;
     uint32_t* dirty_idx;
-    uint32_t* scratch_off;
+    uint32_t* scratch_off;  // per dirty pair: K4 scratch slot, or ARENA_BIT | arena index
     uint32_t* path_count;
-    uint32_t* path_off;   // n_pairs + 1
+    uint32_t* path_off;     // n_dirty + 1
     uint32_t* tile_sums;
-    uint64_t* scratch_h;
+    uint64_t* arena_h;      // K2 wave arenas (arena_per_wave entries per K2 wave)
+    uint8_t* arena_k;
+    uint32_t arena_per_wave;
+    uint64_t* scratch_h;    // K4 scratch for deferred pairs
     uint8_t* scratch_k;
     uint64_t scratch_cap;
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
     uint32_t k2_variant;        // tuning: 0 default (NT loads, 4 chunks in flight per lane per object)
-    uint32_t k2_blocks_per_cu;  // tuning: 0 = 8 resident 256-thread blocks per CU
+    uint32_t k2_blocks_per_cu;  // tuning: 0 = 4 resident 256-thread blocks per CU
 };
+
+// waves of a K2 launch over nchunks 64-pair chunks (sizes the wave arenas)
+uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks);
 
 hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
                          uint32_t* pair_ids);
 hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool);
-// K2 over the 64-pair chunks [c0, c1)
-hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1);
+// K2 (+ fused join) over the 64-pair chunks [c0, c1), batch segment seg of nsegs
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
+                          uint32_t nsegs);
 // K3 over chunks [c0, c1): running (n_spec, n_status, n_dirty, cap) totals before -> after
 hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                           uint4* after);
-// K4 over the dirty pairs the segment added (before.z .. after.z)
+// K4 over the deferred dirty pairs the segment added (before.z .. after.z)
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after);
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);

@@ -32,6 +32,8 @@ constexpr uint32_t F_SENT = 8u;    // status-absent-in-new sentinel path
 constexpr uint32_t F_JSPEC = 16u;  // spec region needs the merge-join
 constexpr uint32_t F_JSTAT = 32u;  // status region needs the merge-join
 constexpr uint32_t F_SEED = 64u;   // pair path-hash seed != 0
+constexpr uint32_t F_DEFER = 128u; // paths not produced by K2 (wave arena full): K4 joins it
+constexpr uint32_t ARENA_BIT = 0x80000000u;  // scratch_off[d]: paths live in the K2 wave arenas
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -213,41 +215,6 @@ __device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, 
     return d;
 }
 
-// One wave per chunk of 64 consecutive pairs; the wave walks its pairs in
-// order, all 64 lanes streaming both objects of a pair with 16-byte loads
-// (NT: non-temporal; U: 16-B chunks in flight per lane per object).
-template <bool NT, int U>
-__global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restrict__ rows,
-                                                 const uint8_t* __restrict__ pool, uint32_t n,
-                                                 uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
-                                                 uint4* __restrict__ chunk_counts, uint32_t c_begin,
-                                                 uint32_t c_end) {
-    const uint32_t lane = lane_id();
-    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
-        const uint32_t p0 = c << 6;
-        const uint32_t cnt = min(64u, n - p0);
-        uint32_t myflag = 0, mycap = 0;
-        for (uint32_t k = 0; k < cnt; k++) {
-            const gpudiff_pair_row r = rows[p0 + k];
-            const PairDecision d = compare_pair<NT, U>(r, pool, lane);
-            if (lane == k) {
-                myflag = d.flag;
-                mycap = d.cap;
-            }
-        }
-        if (lane < cnt) {
-            flags[p0 + lane] = (uint8_t)myflag;
-            if (myflag & (F_SPEC | F_STATUS)) caps[p0 + lane] = mycap;
-        }
-        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
-        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
-        const uint32_t nd = popc64(ballot(myflag & (F_SPEC | F_STATUS)));
-        const uint32_t cs = wave_sum((myflag & (F_SPEC | F_STATUS)) ? mycap : 0u);
-        if (lane == 0) chunk_counts[c] = make_uint4(ns, nt, nd, cs);
-    }
-}
 
 // ---------------------------------------------------------------- scans
 // Reduce-then-scan over u32 or 4 x u32 elements in tiles of 4096 (256 threads
@@ -371,7 +338,9 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                                                  const uint4* __restrict__ cbase, uint32_t* __restrict__ spec_ids,
                                                  uint32_t* __restrict__ status_ids, uint32_t* __restrict__ dirty_ids,
                                                  uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off,
-                                                 uint32_t c_begin, uint32_t c_end) {
+                                                 uint32_t c_begin, uint32_t c_end, const uint32_t* __restrict__ path_src,
+                                                 const uint32_t* __restrict__ path_cnt,
+                                                 uint32_t* __restrict__ path_count) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -393,7 +362,12 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
             const uint32_t d = base.z + popc64(bd & lt);
             dirty_ids[d] = id;
             dirty_idx[d] = p;
-            scratch_off[d] = base.w + cincl - cap;
+            if (f & F_DEFER) {  // K4 joins it into its scratch slot and writes the count
+                scratch_off[d] = base.w + cincl - cap;
+            } else {            // K2 already wrote its paths into a wave arena
+                scratch_off[d] = path_src[p] | ARENA_BIT;
+                path_count[d] = path_cnt[p];
+            }
         }
     }
 }
@@ -592,7 +566,7 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
 // Paths go to the pair's scratch slot (sized by K2's cap), counts to
 // path_count.  Works on the dirty pairs of one batch segment: indices
 // [before.z, after.z) of the running (n_spec, n_status, n_dirty, cap) totals.
-__global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict__ rows,
+__global__ __launch_bounds__(256, 6) void k_join(const gpudiff_pair_row* __restrict__ rows,
                                               const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
                                               const uint32_t* __restrict__ dirty_idx,
                                               const uint32_t* __restrict__ scratch_off, uint32_t* __restrict__ summary,
@@ -607,7 +581,7 @@ __global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict
     const uint32_t ndirty = after.z;
     const bool fits = (uint64_t)after.w <= scratch_cap;
     if (!fits && blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
-    const uint64_t sent0 = status_sentinel_hash(0, mask);
+    if (summary[6] == 0u) return;  // K2 produced every pair's paths (no F_DEFER)
     const uint32_t nchunks = (ndirty - d_begin + 63u) >> 6;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
         const uint32_t d = d_begin + (c << 6) + lane;
@@ -615,31 +589,98 @@ __global__ __launch_bounds__(256) void k_join(const gpudiff_pair_row* __restrict
         const uint32_t p = valid ? dirty_idx[d] : 0u;
         const uint32_t f = valid ? flags[p] : 0u;
         const uint32_t so = valid ? scratch_off[d] : 0u;
-        const bool needj = (f & (F_JSPEC | F_JSTAT)) != 0u;
-        if (valid && !needj) {
-            uint32_t n = 0;
-            if (f & F_SENT) {
-                if (fits) {
-                    sh[so] = (f & F_SEED)
-                                 ? status_sentinel_hash((rows[p].flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
-                                 : sent0;
-                    sk[so] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
-                }
-                n = 1;
-            }
-            path_count[d] = n;
-        }
+        const bool needj = (f & F_DEFER) != 0u;
         uint64_t m = ballot(valid && needj);
+        gpudiff_pair_row rnext;
+        if (m) rnext = rows[uni(shfl32(p, (uint32_t)__builtin_ctzll(m)))];
         while (m) {
             const uint32_t k = (uint32_t)__builtin_ctzll(m);
             m &= m - 1;
             const uint32_t pk = uni(shfl32(p, k)), fk = uni(shfl32(f, k)), sok = uni(shfl32(so, k));
-            const gpudiff_pair_row r = rows[pk];
+            (void)pk;
+            const gpudiff_pair_row r = rnext;
+            if (m) rnext = rows[uni(shfl32(p, (uint32_t)__builtin_ctzll(m)))];  // prefetch the next join's row
             uint32_t n;
             if (fits) n = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane);
             else n = join_pair<false>(r, fk, pool, mask, sh, sk, 0, lane);
             if (lane == 0) path_count[d_begin + (c << 6) + k] = n;
         }
+    }
+}
+
+// ---------------------------------------------------------------- K2 (+ fused K4)
+// One wave per chunk of 64 consecutive pairs; the wave walks its pairs in
+// order, all 64 lanes streaming both objects of a pair with 16-byte loads
+// (NT: non-temporal; U: 16-B chunks in flight per lane per object).  A dirty
+// pair is merge-joined right away by the same wave while its bytes are hot in
+// the XCD's L2, its changed paths appended to this wave's private arena (no
+// atomics, no second HBM read of dirty pairs); a pair whose worst case does
+// not fit the arena's remaining space is flagged F_DEFER for K4.
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restrict__ rows,
+                                                 const uint8_t* __restrict__ pool, uint32_t n,
+                                                 uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
+                                                 uint4* __restrict__ chunk_counts, uint32_t c_begin,
+                                                 uint32_t c_end, uint64_t* __restrict__ ah, uint8_t* __restrict__ ak,
+                                                 uint32_t arena_off, uint32_t arena_per_wave, uint32_t arena_stride,
+                                                 uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
+                                                 uint64_t mask, uint32_t* __restrict__ summary) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wbase = arena_off + wave * arena_stride;
+    uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
+    const uint64_t sent0 = status_sentinel_hash(0, mask);
+    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
+        const uint32_t p0 = c << 6;
+        const uint32_t cnt = min(64u, n - p0);
+        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0;
+        for (uint32_t k = 0; k < cnt; k++) {
+            const gpudiff_pair_row r = rows[p0 + k];
+            PairDecision d = compare_pair<NT, U>(r, pool, lane);
+            uint32_t src = 0, pc = 0;
+            if (d.flag & (F_SPEC | F_STATUS)) {
+                if (used + d.cap <= arena_per_wave) {
+                    src = wbase + used;
+                    if (d.flag & (F_JSPEC | F_JSTAT)) {
+                        pc = join_pair<true>(r, d.flag, pool, mask, ah, ak, src, lane);
+                    } else if (d.flag & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
+                        if (lane == 0) {
+                            ah[src] = (d.flag & F_SEED)
+                                          ? status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
+                                          : sent0;
+                            ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                        }
+                        pc = 1;
+                    }
+                    used += pc;
+                    d.cap = 0;  // no K4 scratch slot needed
+                } else {
+                    d.flag |= F_DEFER;
+                    if (lane == 0) atomicAdd(summary + 6, 1u);
+                }
+            }
+            if (lane == k) {
+                myflag = d.flag;
+                mycap = d.cap;
+                mysrc = src;
+                mycnt = pc;
+            }
+        }
+        const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
+        if (lane < cnt) {
+            flags[p0 + lane] = (uint8_t)myflag;
+            if (dirty) {
+                caps[p0 + lane] = mycap;
+                path_src[p0 + lane] = mysrc;
+                path_cnt[p0 + lane] = mycnt;
+            }
+        }
+        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
+        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
+        const uint32_t nd = popc64(ballot(dirty));
+        const uint32_t cs = wave_sum(dirty ? mycap : 0u);
+        if (lane == 0) chunk_counts[c] = make_uint4(ns, nt, nd, cs);
     }
 }
 
@@ -651,6 +692,7 @@ __global__ __launch_bounds__(256) void k_copy_paths(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ path_off,
                                                     const uint32_t* __restrict__ path_count,
                                                     const uint64_t* __restrict__ sh, const uint8_t* __restrict__ sk,
+                                                    const uint64_t* __restrict__ ah, const uint8_t* __restrict__ ak,
                                                     uint64_t* __restrict__ oh, uint8_t* __restrict__ ok) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -661,23 +703,30 @@ __global__ __launch_bounds__(256) void k_copy_paths(const uint32_t* __restrict__
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
         const uint32_t d = (c << 6) + lane;
         const bool valid = d < ndirty;
-        const uint32_t so = valid ? scratch_off[d] : 0u;
+        const uint32_t sraw = valid ? scratch_off[d] : 0u;
+        const bool arena = (sraw & ARENA_BIT) != 0u;  // written by K2 (else K4's scratch)
+        const uint32_t so = sraw & ~ARENA_BIT;
         const uint32_t po = valid ? path_off[d] : 0u;
         const uint32_t cnt = valid ? path_count[d] : 0u;
+        const uint64_t* srch = arena ? ah : sh;
+        const uint8_t* srck = arena ? ak : sk;
         const bool big = cnt > 16u;
         if (!big)
             for (uint32_t i = 0; i < cnt; i++) {
-                oh[po + i] = sh[so + i];
-                ok[po + i] = sk[so + i];
+                oh[po + i] = srch[so + i];
+                ok[po + i] = srck[so + i];
             }
         uint64_t m = ballot(big);
         while (m) {
             const uint32_t k = (uint32_t)__builtin_ctzll(m);
             m &= m - 1;
             const uint32_t sok = uni(shfl32(so, k)), pok = uni(shfl32(po, k)), ck = uni(shfl32(cnt, k));
+            const bool ak_ = uni(shfl32(arena ? 1u : 0u, k)) != 0u;
+            const uint64_t* bh = ak_ ? ah : sh;
+            const uint8_t* bk = ak_ ? ak : sk;
             for (uint32_t i = lane; i < ck; i += 64) {
-                oh[pok + i] = sh[sok + i];
-                ok[pok + i] = sk[sok + i];
+                oh[pok + i] = bh[sok + i];
+                ok[pok + i] = bk[sok + i];
             }
         }
     }
@@ -716,14 +765,21 @@ hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32
     return hipGetLastError();
 }
 
-hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1) {
+uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks) {
     // 4 resident 256-thread blocks per CU (16 waves/CU) streamed faster than 8 in
-    // the interleaved A/B (tools/ab_k2.py) and leave wave slots for K3/K4 of the
-    // previous segment running concurrently on the side stream
+    // the interleaved A/B (tools/ab_k2.py)
     const uint32_t cap = 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 4u);
-    const dim3 grid(grid_for(c1 - c0, cap));
+    return grid_for(nchunks, cap) * 4u;
+}
+
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
+                          uint32_t nsegs) {
+    const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
     uint4* cc = (uint4*)b.chunk_counts;
-#define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1
+    // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
+    const uint32_t slice = b.arena_per_wave / nsegs;
+#define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
+               b.arena_per_wave, b.path_src, b.path_cnt, b.hash_mask, b.summary
     switch (b.k2_variant) {  // tuning variants (GPUDIFF_OPT_K2_VARIANT_SHIFT); 0 is the default
         case 1: k_compare<false, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
         case 2: k_compare<true, 8><<<grid, 256, 0, s>>>(K2ARGS); break;
@@ -747,7 +803,8 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     if (ntiles) k_scan_apply<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts, (const V4*)after, cc, false);
     k_compact<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
                                                            (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
-                                                           b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1);
+                                                           b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1,
+                                                           b.path_src, b.path_cnt, b.path_count);
     return hipGetLastError();
 }
 
@@ -766,7 +823,8 @@ hipError_t launch_emit(hipStream_t s, const DiffBuffers& b) {
     k_scan_top<uint32_t><<<1, 1024, 0, s>>>(b.tile_sums, nd, 0, nullptr, b.summary + 5);
     k_scan_apply<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums, b.summary + 5, b.path_off, true);
     k_copy_paths<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
-        b.summary, b.scratch_off, b.path_off, b.path_count, b.scratch_h, b.scratch_k, b.out_h, b.out_k);
+        b.summary, b.scratch_off, b.path_off, b.path_count, b.scratch_h, b.scratch_k, b.arena_h, b.arena_k, b.out_h,
+        b.out_k);
     return hipGetLastError();
 }
 

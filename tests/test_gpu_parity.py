@@ -103,6 +103,18 @@ def test_segmented_pipeline(segments):
     e.close()
 
 
+@pytest.mark.parametrize("shrink,segments", [(10, 1), (12, 1), (9, 3), (14, 2)])
+def test_deferred_join_path(shrink, segments):
+    """Wave arenas shrunk until most dirty pairs do not fit: those pairs take the
+    deferred K4 path (and with shrink 14 every pair with a path does);
+    results must not change."""
+    pairs, _, _ = make_pairs(1500, seed=14, mutate_frac=0.4, crd_leaves=300, pretty_frac=0)
+    e = G.Engine(device=0, flags=(shrink << 21) | (segments << 16))
+    res = e.diff_pairs(pairs)
+    assert_matches(res, pairs)
+    e.close()
+
+
 def test_forced_collisions():
     e = G.Engine(device=0, path_hash_bits=8)
     pairs, _, _ = make_pairs(200, seed=5, mix=(("cm", 0.5), ("deploy", 0.5)), mutate_frac=0.5)

@@ -1,30 +1,35 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of decision-kernel (K2) variants on one resident
-population, in one process (cdna_hip_programming.md §5.4 rule 24).
+"""Interleaved A/B of diff-pass variants on one resident population, in one
+process (cdna_hip_programming.md §5.4 rule 24).  Each variant is an engine
+opened with different tuning flags (include/gpudiff.h GPUDIFF_OPT_*); all
+variants must produce identical results.
 
-usage: python tools/ab_k2.py [--pairs N] [--rounds R] [--variants v:b,...]
-  variant v = GPUDIFF_OPT_K2_VARIANT (0 NT x4, 1 plain x4, 2 NT x8, 3 plain x8, 4 NT x2)
-  b = resident blocks per CU (0 = 8)
+usage: python tools/ab_k2.py [--pairs N] [--rounds R] [--variants name=flags,...]
+  flags bits: 8-11 K2 variant (0 NT x4, 1 plain x4, 2 NT x8, 3 plain x8, 4 NT x2),
+              12-15 K2 blocks/CU (0 = default 4), 16-19 forced segments,
+              0x100000 no alternate K2 stream
 """
 import argparse
 import json
 import os
 import statistics
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+DEFAULT = ("seg1=0x10000,seg2=0x20000,seg4=0x40000,seg8=0x80000,seg8noalt=0x180000,"
+           "seg4noalt=0x140000,seg1b8=0x18000,seg4b6=0x46000")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="config3")
-    ap.add_argument("--pairs", type=int, default=4_000_000)
-    ap.add_argument("--clusters", type=int, default=40_000)
-    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--pairs", type=int, default=10_000_000)
+    ap.add_argument("--clusters", type=int, default=100_000)
+    ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--passes", type=int, default=3)
-    ap.add_argument("--variants", default="0:0,1:0,2:0,3:0,4:0,0:6,0:4")
+    ap.add_argument("--variants", default=DEFAULT)
     args = ap.parse_args()
     from kcp_amd import gpudiff as G
     from kcp_amd import synth as S
@@ -46,27 +51,30 @@ def main():
     st = db.stats()
     variants = []
     for spec in args.variants.split(","):
-        v, b = (int(x) for x in spec.split(":"))
-        flags = (v << 8) | (b << 12)
-        variants.append((spec, G.Engine(device=0, timing=True, flags=flags)))
-    res = {spec: [] for spec, _ in variants}
+        name, flags = spec.split("=")
+        variants.append((name, G.Engine(device=0, timing=True, flags=int(flags, 0))))
+    res = {name: [] for name, _ in variants}
     ref = None
     for r in range(args.rounds):
-        for spec, e in variants:
+        for name, e in variants:
             e.timing_reset()
             for _ in range(args.passes):
                 e.diff(db)
             t = e.timings()
-            res[spec].append(t.compare_ms)
+            res[name].append((t.total_ms, t.compare_ms, t.join_ms, t.emit_ms, t.k2_launches))
             if r == 0:
                 out = e.wait(e.diff(db))
                 sig = (out.spec_dirty_ids.tobytes(), out.status_dirty_ids.tobytes(), out.path_hashes.tobytes())
                 ref = ref or sig
-                assert sig == ref, "variant %s changed the results" % spec
+                assert sig == ref, "variant %s changed the results" % name
     summary = {}
-    for spec, xs in res.items():
-        summary[spec] = dict(median_ms=statistics.median(xs), min_ms=min(xs),
-                             gbps=st.compare_bytes / (statistics.median(xs) * 1e-3) / 1e9)
+    for name, xs in res.items():
+        tot = [x[0] for x in xs]
+        summary[name] = dict(pass_ms_median=statistics.median(tot), pass_ms_min=min(tot),
+                             k2_span_ms=statistics.median(x[1] for x in xs),
+                             join_exposed_ms=statistics.median(x[2] for x in xs),
+                             emit_ms=statistics.median(x[3] for x in xs), k2_launches=xs[0][4],
+                             k2_gbps=st.compare_bytes / (statistics.median(x[1] for x in xs) * 1e-3) / 1e9)
     print(json.dumps(dict(pairs=pop.n, compare_bytes=st.compare_bytes, variants=summary), indent=1))
 
 
