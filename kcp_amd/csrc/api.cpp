@@ -163,21 +163,32 @@ static int ensure_paths(gpudiff_dbatch* d, uint64_t arena, uint64_t scratch) {
     const bool ok_a = arena <= d->arena_cap && d->arena_h;
     const bool ok_s = scratch <= d->scratch_cap && d->scratch_h;
     if (ok_a && ok_s) return GPUDIFF_OK;
-    arena = std::max(arena, d->arena_cap);
-    scratch = std::max<uint64_t>({scratch + scratch / 8, d->scratch_cap, 1u << 16});
-    void* ps[] = {d->arena_h, d->arena_k, d->scratch_h, d->scratch_k, d->out_h, d->out_k};
-    for (void* p : ps)
+    // Only the short buffers are replaced: the overflow re-run of the join grows
+    // the scratch while the wave arenas still hold the paths K2 joined in place.
+    auto drop = [](auto*& p) {
         if (p) (void)hipFree(p);
-    d->arena_h = d->scratch_h = d->out_h = nullptr;
-    d->arena_k = d->scratch_k = d->out_k = nullptr;
-    d->arena_cap = d->scratch_cap = 0;
+        p = nullptr;
+    };
+    drop(d->out_h);
+    drop(d->out_k);
     int rc;
-    if ((rc = dalloc(&d->arena_h, arena)) || (rc = dalloc(&d->arena_k, arena)) ||
-        (rc = dalloc(&d->scratch_h, scratch)) || (rc = dalloc(&d->scratch_k, scratch)) ||
-        (rc = dalloc(&d->out_h, arena + scratch)) || (rc = dalloc(&d->out_k, arena + scratch)))
-        return rc;
-    d->arena_cap = arena;
-    d->scratch_cap = scratch;
+    if (!ok_a) {
+        drop(d->arena_h);
+        drop(d->arena_k);
+        d->arena_cap = 0;
+        if ((rc = dalloc(&d->arena_h, arena)) || (rc = dalloc(&d->arena_k, arena))) return rc;
+        d->arena_cap = arena;
+    }
+    if (!ok_s) {
+        scratch = std::max<uint64_t>({scratch + scratch / 8, d->scratch_cap, 1u << 16});
+        drop(d->scratch_h);
+        drop(d->scratch_k);
+        d->scratch_cap = 0;
+        if ((rc = dalloc(&d->scratch_h, scratch)) || (rc = dalloc(&d->scratch_k, scratch))) return rc;
+        d->scratch_cap = scratch;
+    }
+    const uint64_t out = d->arena_cap + d->scratch_cap;
+    if ((rc = dalloc(&d->out_h, out)) || (rc = dalloc(&d->out_k, out))) return rc;
     return GPUDIFF_OK;
 }
 

@@ -8,7 +8,7 @@
 namespace gd {
 
 // Device buffers of one diff pass.  summary[]: 0 n_spec, 1 n_status,
-// 2 n_dirty, 3 K4 scratch cap, 4 overflow, 5 n_paths, 6 deferred pairs, 7 -.
+// 2 n_dirty, 3 K4 scratch cap, 4 overflow, 5 n_paths, 6 any pair deferred to K4, 7 -.
 struct DiffBuffers {
     const gpudiff_pair_row* rows;
     const uint8_t* pool;
@@ -38,7 +38,7 @@ struct DiffBuffers {
     uint8_t* out_k;
     uint64_t hash_mask;
     uint32_t k2_variant;        // tuning: 0 default (NT loads, 4 chunks in flight per lane per object)
-    uint32_t k2_blocks_per_cu;  // tuning: 0 = 4 resident 256-thread blocks per CU
+    uint32_t k2_blocks_per_cu;  // tuning: 0 = 5 resident 256-thread blocks per CU
 };
 
 // waves of a K2 launch over nchunks 64-pair chunks (sizes the wave arenas)

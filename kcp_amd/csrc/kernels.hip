@@ -63,6 +63,16 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
     return v;
 }
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return v;
+}
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
@@ -616,8 +626,8 @@ __global__ __launch_bounds__(256, 6) void k_join(const gpudiff_pair_row* __restr
 // the XCD's L2, its changed paths appended to this wave's private arena (no
 // atomics, no second HBM read of dirty pairs); a pair whose worst case does
 // not fit the arena's remaining space is flagged F_DEFER for K4.
-template <bool NT, int U>
-__global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restrict__ rows,
+template <bool NT, int U, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* __restrict__ rows,
                                                  const uint8_t* __restrict__ pool, uint32_t n,
                                                  uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
                                                  uint4* __restrict__ chunk_counts, uint32_t c_begin,
@@ -630,6 +640,7 @@ __global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restr
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
+    bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
     for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
         const uint32_t p0 = c << 6;
@@ -657,7 +668,7 @@ __global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restr
                     d.cap = 0;  // no K4 scratch slot needed
                 } else {
                     d.flag |= F_DEFER;
-                    if (lane == 0) atomicAdd(summary + 6, 1u);
+                    deferred = true;
                 }
             }
             if (lane == k) {
@@ -682,6 +693,9 @@ __global__ __launch_bounds__(256) void k_compare(const gpudiff_pair_row* __restr
         const uint32_t cs = wave_sum(dirty ? mycap : 0u);
         if (lane == 0) chunk_counts[c] = make_uint4(ns, nt, nd, cs);
     }
+    // one plain store per wave (a same-address atomic per deferred pair
+    // serialises across the XCDs)
+    if (deferred && lane == 0) summary[6] = 1u;
 }
 
 // ---------------------------------------------------------------- K6
@@ -766,9 +780,10 @@ hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32
 }
 
 uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks) {
-    // 4 resident 256-thread blocks per CU (16 waves/CU) streamed faster than 8 in
-    // the interleaved A/B (tools/ab_k2.py)
-    const uint32_t cap = 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 4u);
+    // 5 resident 256-thread blocks per CU (20 waves/CU, the occupancy the fused
+    // kernel's 90 VGPRs allow): with joins inside K2 the extra waves keep HBM
+    // streaming while others join (tools/ab_k2.py: 11.18 vs 11.59 ms at 4)
+    const uint32_t cap = 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 5u);
     return grid_for(nchunks, cap) * 4u;
 }
 
@@ -781,11 +796,14 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.hash_mask, b.summary
     switch (b.k2_variant) {  // tuning variants (GPUDIFF_OPT_K2_VARIANT_SHIFT); 0 is the default
-        case 1: k_compare<false, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 2: k_compare<true, 8><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 3: k_compare<false, 8><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 4: k_compare<true, 2><<<grid, 256, 0, s>>>(K2ARGS); break;
-        default: k_compare<true, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 1: k_compare<false, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 2: k_compare<true, 8, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 3: k_compare<false, 8, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 4: k_compare<true, 2, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 5: k_compare<true, 4, 6><<<grid, 256, 0, s>>>(K2ARGS); break;  // <= 80 VGPRs
+        case 6: k_compare<true, 2, 8><<<grid, 256, 0, s>>>(K2ARGS); break;  // <= 64 VGPRs
+        case 7: k_compare<true, 2, 6><<<grid, 256, 0, s>>>(K2ARGS); break;
+        default: k_compare<true, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
     }
 #undef K2ARGS
     return hipGetLastError();

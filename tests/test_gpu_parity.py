@@ -115,6 +115,28 @@ def test_deferred_join_path(shrink, segments):
     e.close()
 
 
+def test_scratch_overflow_keeps_arena_paths():
+    """Deferred pairs whose paths overflow the initial K4 scratch (64Ki entries)
+    force the grow-and-rejoin path in gpudiff_wait, while the small pairs' paths
+    already sit in the K2 wave arenas: both sets must survive the re-run."""
+    rnd = random.Random(15)
+    pairs = []
+    for i in range(800):
+        a = json.loads(J(BASE))
+        a["spec"]["m"] = {"k%04d" % k: rnd.randint(0, 1 << 40) for k in range(260)}
+        b = json.loads(json.dumps(a))
+        if i % 2:  # ~260 changed paths: deferred to K4
+            b["spec"]["m"] = {k: v + 1 for k, v in b["spec"]["m"].items()}
+        else:  # one changed path: joined inside K2
+            b["spec"]["m"]["k0007"] += 1
+        pairs.append((J(a), J(b)))
+    e = G.Engine(device=0, flags=10 << 21)
+    res = e.diff_pairs(pairs)
+    assert res.path_hashes.size > 65536 + 65536 // 8
+    assert_matches(res, pairs)
+    e.close()
+
+
 def test_forced_collisions():
     e = G.Engine(device=0, path_hash_bits=8)
     pairs, _, _ = make_pairs(200, seed=5, mix=(("cm", 0.5), ("deploy", 0.5)), mutate_frac=0.5)
@@ -134,9 +156,11 @@ def test_host_vs_device_value_hash(eng):
     e2.close()
 
 
-def test_byte_confirmation_without_digests():
+@pytest.mark.parametrize("shrink", [0, 14])
+def test_byte_confirmation_without_digests(shrink):
     """With value digests left at 0, every equal-length long value is decided
-    by the byte confirmation alone -- the path a digest collision takes."""
+    by the byte confirmation alone -- the path a digest collision takes -- both
+    for joins inside K2 (shrink 0) and in K4 (shrink 14: every pair deferred)."""
     rnd = random.Random(12)
     pairs = []
     for i in range(300):
@@ -149,7 +173,7 @@ def test_byte_confirmation_without_digests():
             j = rnd.randrange(len(s))
             b["spec"]["vals"][k] = s[:j] + ("x" if s[j] == "y" else "y") + s[j + 1:]  # same length, one byte
         pairs.append((J(a), J(b)))
-    e = G.Engine(device=0, no_value_hash=True)
+    e = G.Engine(device=0, no_value_hash=True, flags=shrink << 21)
     res = e.diff_pairs(pairs)
     assert_matches(res, pairs)
     e.close()
