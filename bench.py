@@ -47,7 +47,10 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=20000, help="pairs in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default="", help="PMC traffic summary (profiles/*) to attach")
+    ap.add_argument("--traffic-json", default="latest",
+                    help="PMC traffic summary to attach as roofline.traffic (default: the newest committed "
+                         "profiles/r*_pmc_summary.json, used only if it was measured on this same workload; "
+                         "'none' to skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -194,10 +197,18 @@ def main():
     k2_ms = tm.compare_ms / launches
     bytes_per_launch = st.compare_bytes / launches
     achieved = bytes_per_launch / (k2_ms * 1e-3) / 1e9 if k2_ms > 0 else 0.0
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    traffic, traffic_src = None, None
+    tj = args.traffic_json
+    if tj == "latest":
+        import glob
+        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+        tj = found[-1] if found else ""
+    if tj and tj != "none" and os.path.exists(tj):
+        with open(tj) as f:
+            pmc = json.load(f)
+        # per-launch bytes are only comparable on the same workload and launch split
+        if pmc.get("algorithmic_bytes_per_launch") == bytes_per_launch:
+            traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
 
     # ---------------- CPU baseline (rank 0, N=1 only): the oracle's C++ port
     cpu = None
@@ -239,7 +250,7 @@ def main():
                     world, ", RCCL all-gather of dirty counts+IDs per step" if world > 1 else ""),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_compare (K2)", "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": k2_ms, "launches_per_step": launches},
             "kernels_ms": {"compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,

@@ -33,7 +33,8 @@ def load_counter(d, name):
 
 
 def short(name):
-    return name.split("(")[0].replace("gd::", "")
+    n = name.split("(")[0].split("<")[0].replace("gd::", "")
+    return n[5:] if n.startswith("void ") else n
 
 
 def main():
