@@ -220,6 +220,60 @@ int gpudiff_sync(gpudiff_ctx* ctx);
 int gpudiff_submit(gpudiff_ctx* ctx, const gpudiff_json_pair* pairs, size_t n,
                    gpudiff_ticket* ticket);
 
+/* ---- device-resident object store (watch replay) ----
+ * The informer cache's "old" objects stay resident in HBM, one per caller
+ * slot (the shim maps (cluster, gvr, namespace, name) to a slot, as the
+ * indexer at pkg/syncer/syncer.go:318 keys its cache).  An Update event
+ * uploads only its new version: the engine diffs it against the slot's
+ * resident version -- UpdateFunc(old, new), specsyncer.go:47-51 and
+ * statussyncer.go:32-36 -- and the new version becomes the resident one.
+ * Events of one batch apply in order, so two events on one slot chain.
+ * Exactness: the host keeps a second, independent 64-bit hash of every
+ * resident path; a path-hash collision between versions (or within the new
+ * one) re-encodes the pair with a fresh seed from old_json.  Blobs are
+ * appended to the current space and the live ones are packed into the other
+ * space (K7 k_move_blobs) when it fills. */
+typedef struct gpudiff_store gpudiff_store;
+
+typedef struct gpudiff_event {
+    uint32_t slot;            /* < max_slots */
+    uint32_t pair_id;         /* echoed in the result id lists */
+    uint32_t cluster_id;      /* logical cluster */
+    uint32_t reserved;        /* 0 */
+    const uint8_t* new_json;  /* the event's object (required) */
+    size_t new_len;
+    /* optional: the informer's old object, read only when the slot is empty
+     * (a first sighting diffs against it) or a collision forces a re-seed.
+     * An empty slot without old_json diffs against the empty object {};
+     * a collision without old_json reports the event dirty with
+     * GPUDIFF_DECODE_ERROR (conservative) and stores the new version. */
+    const uint8_t* old_json;
+    size_t old_len;
+} gpudiff_event;
+
+typedef struct gpudiff_store_stats {
+    uint64_t max_slots, live_slots;
+    uint64_t space_bytes;      /* per space (two are allocated) */
+    uint64_t used_bytes;       /* appended to the current space */
+    uint64_t live_bytes;       /* resident blobs */
+    uint64_t compactions;
+    uint64_t events, old_encoded, reseeded, collisions_unresolved;
+    uint64_t last_batch_bytes; /* blob bytes uploaded by the last submit */
+} gpudiff_store_stats;
+
+int gpudiff_store_create(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,
+                         gpudiff_store** out);
+/* encode (host threads), H2D into the current space, K1 on the new blobs,
+ * K2..K6 over the batch's (resident, new) pairs; results via gpudiff_wait.
+ * Two submits may be in flight (the next batch encodes while the GPU diffs
+ * the previous one); wait on a ticket before its slot in the ring is reused. */
+int gpudiff_store_submit(gpudiff_ctx* ctx, gpudiff_store* st, const gpudiff_event* events, size_t n,
+                         gpudiff_ticket* ticket);
+/* Delete event: the slot is empty again */
+int gpudiff_store_forget(gpudiff_ctx* ctx, gpudiff_store* st, uint32_t slot);
+int gpudiff_store_stats_get(const gpudiff_store* st, gpudiff_store_stats* out);
+void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
+
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,
                        const uint8_t* new_json, size_t new_len, int* equal);

@@ -39,6 +39,8 @@
 /* object flags (PairRow.flags_a / flags_b) */
 #define GPUDIFF_OBJ_HAS_STATUS 0x1u   /* top-level "status" key present (even null) */
 #define GPUDIFF_OBJ_DECODE_ERR 0x2u   /* JSON failed the Go decode rules */
+#define GPUDIFF_OBJ_FRESH 0x4u        /* object store: blob uploaded with this batch (K1 hashes
+                                         its long values; resident blobs were hashed on arrival) */
 /* bits 8..15 of flags_a: per-pair path-hash seed */
 #define GPUDIFF_OBJ_SEED_SHIFT 8u
 

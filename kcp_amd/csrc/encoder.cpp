@@ -297,6 +297,48 @@ void PairEncoder::encode_json(const uint8_t* a, size_t alen, const uint8_t* b, s
     encode_nodes(oka ? &na : nullptr, okb ? &nb : nullptr, pair_id, cluster_id, pool, row);
 }
 
+// ------------------------------------------------------------------ object store helpers
+static constexpr uint64_t kFingerprintSeed = 0x9FB21C651E98DF25ull;
+
+bool PairEncoder::flatten_json(const uint8_t* json, size_t len, Arena& arena, FlatObject& o) {
+    arena.reset();
+    Node n;
+    if (!json || !parser.parse_object(json, len, arena, &n)) return false;
+    flatten_object(n, o);
+    return true;
+}
+
+static void fingerprints(FlatObject& o) {
+    for (std::vector<LeafRec>* v : {&o.spec, &o.stat})
+        for (LeafRec& r : *v) r.fp = xxh64_host(o.paths.data() + r.path_off, r.path_len, kFingerprintSeed);
+}
+
+bool PairEncoder::hash_single(FlatObject& o, uint32_t seed) {
+    const uint64_t mask = cfg_.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg_.hash_bits) - 1);
+    auto by_h = [](const LeafRec& x, const LeafRec& y) { return x.h < y.h; };
+    for (std::vector<LeafRec>* v : {&o.spec, &o.stat}) {
+        for (LeafRec& r : *v) r.h = xxh64_host(o.paths.data() + r.path_off, r.path_len, seed) & mask;
+        std::sort(v->begin(), v->end(), by_h);
+        for (size_t i = 1; i < v->size(); i++)
+            if ((*v)[i].h == (*v)[i - 1].h) return false;
+    }
+    const std::string& sp = status_path_bytes();
+    if (!sentinel_check(o, o.stat, xxh64_host(sp.data(), sp.size(), seed) & mask)) return false;
+    fingerprints(o);
+    return true;
+}
+
+bool PairEncoder::pair_seed(FlatObject& a, FlatObject& b, uint32_t* seed) {
+    if (!assign_seed(a, b, seed)) return false;
+    fingerprints(b);
+    return true;
+}
+
+void PairEncoder::write_object(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
+                               uint32_t* sar, uint32_t* tl, uint32_t* tar) {
+    write_blob(o, pool, off, sl, sar, tl, tar);
+}
+
 std::string render_path(const char* p, size_t n) {
     std::string s;
     size_t i = 0;

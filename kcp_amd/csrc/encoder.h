@@ -24,6 +24,7 @@ namespace gd {
 
 struct LeafRec {
     uint64_t h;
+    uint64_t fp;  // object store: second, independent 64-bit path hash (collision detection)
     uint64_t val;
     uint32_t meta;
     uint32_t path_off;
@@ -64,6 +65,19 @@ class PairEncoder {
     // Assigns the pair seed, sorts, and writes both blobs.
     void encode_flat(FlatObject* fa, FlatObject* fb, uint32_t pair_id, uint32_t cluster_id,
                      std::vector<uint8_t>& pool, gpudiff_pair_row& row);
+    // ---- object store (single objects against a resident version)
+    // Parses and flattens one object into `o` (false on a decode error).
+    bool flatten_json(const uint8_t* json, size_t len, Arena& arena, FlatObject& o);
+    // Path hashes under `seed` (sorted) plus fingerprints; true iff the hashes
+    // are unique within the object and the status sentinel is unambiguous.
+    bool hash_single(FlatObject& o, uint32_t seed);
+    // Smallest seed valid for the pair (a, b) as encode_json would pick it;
+    // fills b's fingerprints too.  False if no seed <= 255 works.
+    bool pair_seed(FlatObject& a, FlatObject& b, uint32_t* seed);
+    // Appends o's blob (16-B aligned) and reports its layout.
+    void write_object(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl, uint32_t* sar,
+                      uint32_t* tl, uint32_t* tar);
+
     uint64_t leaves_written = 0;
     uint64_t reseeded = 0;
     uint64_t decode_errors = 0;

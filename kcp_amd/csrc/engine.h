@@ -1,0 +1,164 @@
+// Internal engine state shared by the C-ABI translation units (api.cpp,
+// store.cpp).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/gpudiff.h"
+#include "encoder.h"
+#include "kernels.h"
+
+using gd::PairEncoder;
+using gd::EncodeConfig;
+
+namespace gd {
+extern thread_local std::string g_last_hip_error;
+}
+
+#define HIPCHK(x)                                             \
+    do {                                                      \
+        hipError_t e_ = (x);                                  \
+        if (e_ != hipSuccess) {                               \
+            gd::g_last_hip_error = hipGetErrorString(e_);     \
+            return GPUDIFF_E_DEVICE;                          \
+        }                                                     \
+    } while (0)
+
+namespace gd {
+struct Part {
+    std::vector<uint8_t> pool;
+    std::vector<gpudiff_pair_row> rows;
+    uint64_t leaves = 0, errors = 0, reseeded = 0;
+};
+}  // namespace gd
+
+inline constexpr uint32_t kMaxSegments = 8;
+// changed-path arena entries per K2 wave (a pair whose worst case does not
+// fit the wave's remaining arena is deferred to K4)
+inline constexpr uint32_t kArenaPerWave = 16384;
+
+struct gpudiff_hbatch {
+    uint8_t* pool = nullptr;
+    gpudiff_pair_row* rows = nullptr;
+    size_t n = 0;
+    uint64_t pool_bytes = 0;
+    uint64_t leaves = 0, errors = 0, reseeded = 0;
+    uint64_t pool_cap = 0;
+    size_t rows_cap = 0;
+    bool pinned = false;
+    hipEvent_t used = nullptr;  // last async copy that reads this batch
+};
+
+struct gpudiff_dbatch {
+    uint64_t pool_cap = 0, pool_used = 0;
+    uint64_t max_pairs = 0, n_pairs = 0;
+    uint64_t leaves = 0, compare_bytes = 0;
+    uint8_t* pool = nullptr;
+    bool pool_borrowed = false;  // pool owned by a gpudiff_store (its current space)
+    gpudiff_pair_row* rows = nullptr;
+    uint32_t* pair_ids = nullptr;
+    uint8_t* flags = nullptr;
+    uint32_t* caps = nullptr;
+    void* chunk_counts = nullptr;
+    uint32_t* summary = nullptr;
+    uint32_t* spec_ids = nullptr;
+    uint32_t* status_ids = nullptr;
+    uint32_t* dirty_ids = nullptr;
+    uint32_t* dirty_idx = nullptr;
+    uint32_t* scratch_off = nullptr;
+    uint32_t* path_count = nullptr;
+    uint32_t* path_off = nullptr;
+    uint32_t* tile_sums = nullptr;
+    uint4* seg_tot = nullptr;  // running totals after each diff segment
+    uint32_t* path_src = nullptr;
+    uint32_t* path_cnt = nullptr;
+    uint64_t arena_cap = 0;
+    uint64_t* arena_h = nullptr;
+    uint8_t* arena_k = nullptr;
+    uint64_t scratch_cap = 0;
+    uint64_t* scratch_h = nullptr;
+    uint8_t* scratch_k = nullptr;
+    uint64_t* out_h = nullptr;
+    uint8_t* out_k = nullptr;
+    hipEvent_t done = nullptr;
+    gpudiff_ticket ticket = 0;
+};
+
+struct ResultStore {
+    std::vector<uint8_t> flags;
+    std::vector<uint32_t> spec, status, dirty, off;
+    std::vector<uint64_t> hashes;
+    std::vector<uint8_t> kinds;
+};
+
+struct gpudiff_ctx {
+    int device = GPUDIFF_DEVICE_NONE;
+    bool has_device = false;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    uint32_t threads = 1;
+    uint32_t flags = 0;
+    EncodeConfig ecfg;
+    uint64_t hash_mask = ~0ULL;
+    std::vector<std::unique_ptr<PairEncoder>> encoders;
+    std::vector<gd::Part> parts;
+    gpudiff_ticket next_ticket = 1;
+    std::unordered_map<gpudiff_ticket, gpudiff_dbatch*> tickets;
+    hipEvent_t ev_k1[2] = {};
+    bool k1_recorded = false;
+    std::vector<std::array<hipEvent_t, 5>> pass_ev;
+    size_t n_pass = 0;
+    uint32_t pass_k2_launches = 1;
+    // segmented diff pass: side stream for K3/K4, one event per segment
+    hipStream_t side = nullptr;
+    hipStream_t k2alt = nullptr;  // second K2 stream (odd segments)
+    hipEvent_t seg_ev[kMaxSegments] = {};
+    hipEvent_t side_done = nullptr;
+    hipEvent_t alt_start = nullptr;
+    // submit ring
+    gpudiff_dbatch* ring[2] = {nullptr, nullptr};
+    gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
+    uint32_t ring_next = 0;
+};
+
+// ------------------------------------------------------------------ helpers
+inline int set_device(gpudiff_ctx* c) {
+    if (!c->has_device) return GPUDIFF_E_NODEVICE;
+    HIPCHK(hipSetDevice(c->device));
+    return GPUDIFF_OK;
+}
+
+template <class T>
+inline int dalloc(T** p, uint64_t count) {
+    *p = nullptr;
+    size_t bytes = (size_t)std::max<uint64_t>(count, 1) * sizeof(T);
+    HIPCHK(hipMalloc((void**)p, bytes));
+    return GPUDIFF_OK;
+}
+
+inline void dfree_all(gpudiff_dbatch* d) {
+    if (d->pool && !d->pool_borrowed) (void)hipFree(d->pool);
+    void* ps[] = {d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
+                  d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
+                  d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
+                  d->scratch_h, d->scratch_k, d->out_h, d->out_k};
+    for (void* p : ps)
+        if (p) (void)hipFree(p);
+    if (d->done) (void)hipEventDestroy(d->done);
+}
+
+// bytes the decision kernel must read for this pair (DESIGN.md "Roofline")
+inline uint64_t pair_compare_bytes(const gpudiff_pair_row& r) {
+    uint64_t b = sizeof(gpudiff_pair_row) + 1;
+    if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) return b;
+    if (r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b) b += 2 * gpudiff_seg_bytes(r.spec_l_a, r.spec_ar_a);
+    if ((r.flags_b & GPUDIFF_OBJ_HAS_STATUS) && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b)
+        b += 2 * gpudiff_seg_bytes(r.stat_l_a, r.stat_ar_a);
+    return b;
+}

@@ -46,7 +46,13 @@ uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks);
 
 hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
                          uint32_t* pair_ids);
-hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool);
+hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool,
+                             bool fresh_only = false);
+// object-store compaction: blob copies between the two spaces
+struct BlobMove {
+    uint64_t src, dst, bytes;
+};
+hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, const BlobMove* moves, uint32_t n);
 // K2 (+ fused join) over the 64-pair chunks [c0, c1), batch segment seg of nsegs
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
                           uint32_t nsegs);

@@ -127,9 +127,11 @@ __device__ uint64_t xxh64_a16(const uint4* p, uint32_t len, uint64_t seed) {
     return xavalanche(h);
 }
 
-// One wave per (row, object, region) item.
+// One wave per (row, object, region) item.  fresh_only: only the objects
+// flagged GPUDIFF_OBJ_FRESH (the object store's newly uploaded blobs; the
+// resident ones were hashed when they arrived).
 __global__ __launch_bounds__(256) void k_value_hash(const gpudiff_pair_row* __restrict__ rows, uint32_t row_begin,
-                                                    uint32_t row_end, uint8_t* __restrict__ pool) {
+                                                    uint32_t row_end, uint8_t* __restrict__ pool, bool fresh_only) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -137,6 +139,7 @@ __global__ __launch_bounds__(256) void k_value_hash(const gpudiff_pair_row* __re
     for (uint32_t it = wave; it < nitems; it += nwaves) {
         const gpudiff_pair_row& r = rows[row_begin + (it >> 2)];
         const bool b = it & 1u, st = it & 2u;
+        if (fresh_only && !((b ? r.flags_b : r.flags_a) & GPUDIFF_OBJ_FRESH)) continue;
         const uint64_t off = b ? r.off_b : r.off_a;
         const uint32_t sl = b ? r.spec_l_b : r.spec_l_a, sar = b ? r.spec_ar_b : r.spec_ar_a;
         const uint32_t L = st ? (b ? r.stat_l_b : r.stat_l_a) : sl;
@@ -746,6 +749,23 @@ __global__ __launch_bounds__(256) void k_copy_paths(const uint32_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------- object store compaction
+// Wave per live blob: copies it from the old space to its packed offset in
+// the new one with 16-B loads/stores (blobs are 16-B aligned and sized).
+__global__ __launch_bounds__(256) void k_move_blobs(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    const BlobMove* __restrict__ moves, uint32_t n) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t i = wave; i < n; i += nwaves) {
+        const BlobMove m = moves[i];
+        const u32x4* s4 = (const u32x4*)(src + m.src);
+        u32x4* d4 = (u32x4*)(dst + m.dst);
+        const uint64_t n16 = m.bytes >> 4;
+        for (uint64_t k = lane; k < n16; k += 64) d4[k] = __builtin_nontemporal_load(s4 + k);
+    }
+}
+
 // ---------------------------------------------------------------- ingest helper
 __global__ __launch_bounds__(256) void k_rebase_rows(gpudiff_pair_row* __restrict__ rows, uint32_t begin, uint32_t end,
                                                      uint64_t base, uint32_t* __restrict__ pair_ids) {
@@ -773,9 +793,17 @@ hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, 
     return hipGetLastError();
 }
 
-hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool) {
+hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool,
+                             bool fresh_only) {
     if (end <= begin) return hipSuccess;
-    k_value_hash<<<grid_for((uint64_t)(end - begin) * 4, kPersistBlocks), 256, 0, s>>>(rows, begin, end, pool);
+    k_value_hash<<<grid_for((uint64_t)(end - begin) * 4, kPersistBlocks), 256, 0, s>>>(rows, begin, end, pool,
+                                                                                        fresh_only);
+    return hipGetLastError();
+}
+
+hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, const BlobMove* moves, uint32_t n) {
+    if (!n) return hipSuccess;
+    k_move_blobs<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(src, dst, moves, n);
     return hipGetLastError();
 }
 

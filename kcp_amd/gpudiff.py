@@ -26,7 +26,7 @@ PATH_REGION_STATUS = 0x80
 OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
-OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_SEED_SHIFT = 0x1, 0x2, 8
+OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_FRESH, OBJ_SEED_SHIFT = 0x1, 0x2, 0x4, 8
 EXPORT_COUNTS, EXPORT_SPEC_IDS, EXPORT_STATUS_IDS, EXPORT_DIRTY_IDS, EXPORT_FLAGS = range(5)
 
 
@@ -61,6 +61,18 @@ ROW_DTYPE = np.dtype([("off_a", "<u8"), ("off_b", "<u8"), ("spec_l_a", "<u4"), (
                       ("stat_ar_a", "<u4"), ("stat_ar_b", "<u4"), ("flags_a", "<u4"), ("flags_b", "<u4"),
                       ("pair_id", "<u4"), ("cluster_id", "<u4")])
 assert ROW_DTYPE.itemsize == 64
+
+
+class Event(C.Structure):
+    _fields_ = [("slot", C.c_uint32), ("pair_id", C.c_uint32), ("cluster_id", C.c_uint32), ("reserved", C.c_uint32),
+                ("new_json", C.c_void_p), ("new_len", C.c_size_t), ("old_json", C.c_void_p), ("old_len", C.c_size_t)]
+
+
+class StoreStats(C.Structure):
+    _fields_ = [("max_slots", C.c_uint64), ("live_slots", C.c_uint64), ("space_bytes", C.c_uint64),
+                ("used_bytes", C.c_uint64), ("live_bytes", C.c_uint64), ("compactions", C.c_uint64),
+                ("events", C.c_uint64), ("old_encoded", C.c_uint64), ("reseeded", C.c_uint64),
+                ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64)]
 
 
 class HBatchInfo(C.Structure):
@@ -123,6 +135,11 @@ SIGNATURES = [
     ("gpudiff_hbatch_resize", C.c_int, [_P, _P, C.c_uint64, C.c_size_t, C.c_uint64, C.POINTER(_P),
                                         C.POINTER(_P)]),
     ("gpudiff_submit", C.c_int, [_P, C.POINTER(JsonPair), C.c_size_t, C.POINTER(C.c_uint64)]),
+    ("gpudiff_store_create", C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(_P)]),
+    ("gpudiff_store_submit", C.c_int, [_P, _P, C.POINTER(Event), C.c_size_t, C.POINTER(C.c_uint64)]),
+    ("gpudiff_store_forget", C.c_int, [_P, _P, C.c_uint32]),
+    ("gpudiff_store_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
+    ("gpudiff_store_free", None, [_P, _P]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
@@ -270,6 +287,75 @@ class DeviceBatch:
             pass
 
 
+class ObjectStore:
+    """Device-resident informer snapshot (gpudiff_store_*): submit(events)
+    diffs each event's new object against its slot's resident version and
+    makes it resident; results come back through Engine.wait(ticket)."""
+
+    def __init__(self, engine: "Engine", max_slots: int, space_bytes: int, max_events: int):
+        self.engine = engine
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_store_create(engine.ctx, max_slots, space_bytes, max_events, C.byref(h)),
+             "gpudiff_store_create")
+        self.h = h
+        self._keep = [None, None]  # inputs of the (at most two) submits in flight
+        self._k = 0
+
+    @staticmethod
+    def events(items):
+        """items: [(slot, new_json, old_json_or_None, pair_id, cluster_id)] -> (Event array, n, keepalive)."""
+        n = len(items)
+        arr = (Event * max(n, 1))()
+        keep = []
+        for i, it in enumerate(items):
+            slot, new, old = it[0], it[1], it[2]
+            nb = to_json_bytes(new)
+            cn = C.create_string_buffer(nb, len(nb)) if nb else C.create_string_buffer(1)
+            keep.append(cn)
+            arr[i].slot = slot
+            arr[i].pair_id = it[3] if len(it) > 3 else i
+            arr[i].cluster_id = it[4] if len(it) > 4 else 0
+            arr[i].new_json = C.cast(cn, C.c_void_p)
+            arr[i].new_len = len(nb)
+            if old is not None:
+                ob = to_json_bytes(old)
+                co = C.create_string_buffer(ob, len(ob)) if ob else C.create_string_buffer(1)
+                keep.append(co)
+                arr[i].old_json = C.cast(co, C.c_void_p)
+                arr[i].old_len = len(ob)
+        return arr, n, keep
+
+    def submit(self, items) -> int:
+        arr, n, keep = self.events(items)
+        return self.submit_raw(arr, n, keep)
+
+    def submit_raw(self, arr, n, keep=None) -> int:
+        t = C.c_uint64()
+        _chk(_lib.gpudiff_store_submit(self.engine.ctx, self.h, arr, n, C.byref(t)), "gpudiff_store_submit")
+        self._keep[self._k] = (arr, keep)
+        self._k ^= 1
+        return t.value
+
+    def forget(self, slot: int):
+        _chk(_lib.gpudiff_store_forget(self.engine.ctx, self.h, slot), "gpudiff_store_forget")
+
+    def stats(self) -> StoreStats:
+        s = StoreStats()
+        _chk(_lib.gpudiff_store_stats_get(self.h, C.byref(s)), "gpudiff_store_stats_get")
+        return s
+
+    def free(self):
+        if self.h:
+            _lib.gpudiff_store_free(self.engine.ctx, self.h)
+            self.h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Engine:
     """One gpudiff context (one GPU, one stream, one submitting thread)."""
 
@@ -366,6 +452,9 @@ class Engine:
 
     def diff_pairs(self, pairs, ids=None, clusters=None) -> DiffResult:
         return self.wait(self.submit(pairs, ids, clusters))
+
+    def object_store(self, max_slots: int, space_bytes: int, max_events: int) -> ObjectStore:
+        return ObjectStore(self, max_slots, space_bytes, max_events)
 
     # ---- single pair drop-ins
     def spec_equal(self, old, new) -> bool:
