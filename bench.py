@@ -38,7 +38,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4"])
+    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5"],
+                    help="config5 = watch replay through the device-resident object store (bench_replay.py)")
+    ap.add_argument("--batch", type=int, default=65536, help="config5: events per batch")
+    ap.add_argument("--batches", type=int, default=40, help="config5: timed batches")
+    ap.add_argument("--warmup-batches", type=int, default=4, help="config5: untimed batches")
     ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")
     ap.add_argument("--clusters", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=262144)
@@ -52,6 +56,11 @@ def main():
                          "profiles/r*_pmc_summary.json, used only if it was measured on this same workload; "
                          "'none' to skip)")
     args = ap.parse_args()
+
+    if args.config == "config5":
+        import bench_replay
+        args.sample = min(args.sample, 300)
+        return bench_replay.run(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,23 +142,7 @@ def main():
     pop_flags = res.pair_flags.copy()
     del res
 
-    # bit-exact sample through the JSON -> encoder -> GPU path vs the oracle
     sample_check = None
-    if args.sample and rank == 0:
-        from tests.parity import assert_matches, oracle_batch
-        idx = np.unique(np.linspace(0, n - 1, min(args.sample, n)).astype(np.int64))
-        pairs = [pop.json_pair(int(i)) for i in idx]
-        exp = oracle_batch(pairs)
-        r = eng.diff_pairs(pairs)
-        ok = True
-        try:
-            assert_matches(r, pairs, exp=exp)
-        except AssertionError as e:
-            ok = False
-            log("SAMPLE PARITY FAILED:", str(e)[:500])
-        same = bool((r.pair_flags == pop_flags[idx]).all())
-        sample_check = dict(pairs=int(idx.size), bit_exact_vs_oracle=ok, matches_population_flags=same)
-        log("sample check:", json.dumps(sample_check))
 
     for _ in range(max(0, args.warmup - 1)):
         eng.diff(db)
@@ -210,9 +203,26 @@ def main():
         if pmc.get("algorithmic_bytes_per_launch") == bytes_per_launch:
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
 
-    # ---------------- CPU baseline (rank 0, N=1 only): the oracle's C++ port
+    # ---------------- CPU baseline leg (rank 0, N=1 only): the oracle's C++ port
+    # timed on the host, and -- the oracle as checker -- a bit-exact sample
+    # through the JSON -> encoder -> GPU path vs the Python oracle
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if args.sample:
+            from tests.parity import assert_matches, oracle_batch
+            idx = np.unique(np.linspace(0, n - 1, min(args.sample, n)).astype(np.int64))
+            pairs = [pop.json_pair(int(i)) for i in idx]
+            exp = oracle_batch(pairs)
+            r = eng.diff_pairs(pairs)
+            ok = True
+            try:
+                assert_matches(r, pairs, exp=exp)
+            except AssertionError as e:
+                ok = False
+                log("SAMPLE PARITY FAILED:", str(e)[:500])
+            same = bool((r.pair_flags == pop_flags[idx]).all())
+            sample_check = dict(pairs=int(idx.size), bit_exact_vs_oracle=ok, matches_population_flags=same)
+            log("sample check:", json.dumps(sample_check))
         from oracle import cpu_ref
         idx = np.unique(np.linspace(0, n - 1, min(args.cpu_sample, n)).astype(np.int64))
         pairs = [pop.json_pair(int(i)) for i in idx]

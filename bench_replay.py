@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Watch-replay benchmark: sustained Update
+events/s through the device-resident object store, with end-to-end batch
+latency.
+
+M objects (config3 mix: ConfigMap/Secret/Deployment/CRD, synthetic, seed
+20211004+3) are loaded into a gpudiff_store (initial list, untimed).  Each
+timed event is the next version of one resident object -- the population's
+(A, B) versions of that object alternate, so every event is a real Update with
+the same 5% spec/status mutation rate as the headline workload -- delivered as
+JSON bytes together with the informer's old object (read only on a collision).
+Per event the host encodes only the new version; H2D, K1 (fresh blobs only) and
+the diff pass run on the GPU while the host encodes the next batch (two
+batches in flight).  The timed region therefore includes host encoding and the
+PCIe upload: streaming is the point of this configuration.
+
+Reported: events/s over the timed batches, per-batch latency p50/p99 (submit
+call -> results on the host), H2D GB/s, the GPU time per batch, and checks:
+every timed event's decisions against the generator's ground truth and a
+sample bit-exact against the oracle (flags and changed paths).
+
+usage: python bench.py --config config5 [--pairs M] [--batch B] [--seconds S]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+EVENT_DTYPE = np.dtype([("slot", "<u4"), ("pair_id", "<u4"), ("cluster_id", "<u4"), ("reserved", "<u4"),
+                        ("new_json", "<u8"), ("new_len", "<u8"), ("old_json", "<u8"), ("old_len", "<u8")])
+assert EVENT_DTYPE.itemsize == 48
+
+
+def log(*a):
+    print("[replay]", *a, file=sys.stderr, flush=True)
+
+
+def run(args):
+    import ctypes as C
+
+    import torch
+
+    from kcp_amd import gpudiff as G
+    from kcp_amd import synth as S
+
+    assert G.Event.__sizeof__ is not None and C.sizeof(G.Event) == EVENT_DTYPE.itemsize
+    torch.cuda.set_device(0)
+    ncpu = len(os.sched_getaffinity(0))
+    threads = args.threads or max(1, min(16, ncpu))
+    M = args.pairs or 1_000_000
+    B = args.batch
+    cfg = S.make_cfg("config3", n_pairs=M, n_clusters=args.clusters or max(1, M // 100))
+    pop = S.Population(cfg)
+    t0 = time.time()
+    buf, offs, truth = pop.json_range(0, M, threads)
+    log("generated %d objects x 2 versions: %.2f GB JSON in %.1f s" % (M, buf.size / 1e9, time.time() - t0))
+    base = buf.ctypes.data
+    starts = offs[:-1].astype(np.uint64) + np.uint64(base)
+    lens = np.diff(offs).astype(np.uint64)
+    a_ptr, b_ptr = starts[0::2], starts[1::2]
+    a_len, b_len = lens[0::2], lens[1::2]
+    exp_ab = pop.expected_flags(truth)  # decisions of A -> B (and, by symmetry, of B -> A)
+    cluster = np.arange(M, dtype=np.uint32) % np.uint32(cfg.n_clusters)
+
+    eng = G.Engine(device=0, encode_threads=threads, timing=True)
+    per_obj = float(lens.mean()) * 1.3 + 256
+    space = int(per_obj * M * 2.5) + (B * int(per_obj) * 4) + (256 << 20)
+    st = eng.object_store(M, space, B)
+    log("store: %d slots, 2 x %.2f GB spaces, batches of %d events, %d host threads" % (M, space / 1e9, B, threads))
+
+    def events(slots, new_is_b, with_old=True):
+        ev = np.zeros(slots.size, dtype=EVENT_DTYPE)
+        ev["slot"] = slots
+        ev["pair_id"] = np.arange(slots.size, dtype=np.uint32)
+        ev["cluster_id"] = cluster[slots]
+        ev["new_json"] = np.where(new_is_b, b_ptr[slots], a_ptr[slots])
+        ev["new_len"] = np.where(new_is_b, b_len[slots], a_len[slots])
+        if with_old:
+            ev["old_json"] = np.where(new_is_b, a_ptr[slots], b_ptr[slots])
+            ev["old_len"] = np.where(new_is_b, a_len[slots], b_len[slots])
+        return ev
+
+    def submit(ev):
+        arr = (G.Event * ev.size).from_buffer(ev)
+        return st.submit_raw(arr, ev.size, ev)
+
+    # ---- initial list: every object's A version (diffed against {}; untimed)
+    t0 = time.time()
+    pend = None
+    for s0 in range(0, M, B):
+        sl = np.arange(s0, min(M, s0 + B), dtype=np.uint32)
+        t = submit(events(sl, np.zeros(sl.size, bool), with_old=False))
+        if pend is not None:
+            eng.wait(pend)
+        pend = t
+    eng.wait(pend)
+    t_load = time.time() - t0
+    ss = st.stats()
+    log("initial list: %d objects in %.1f s (%.0f objects/s), %.2f GB resident" % (
+        M, t_load, M / t_load, ss.live_bytes / 1e9))
+
+    # ---- timed replay: each batch = B distinct objects, each advanced one version
+    rng = np.random.default_rng(20211004 + 5)
+    on_b = np.zeros(M, dtype=bool)  # current version of each object
+    n_batches = args.batches
+    batches = []
+    for k in range(args.warmup_batches + n_batches):
+        sl = rng.choice(M, size=B, replace=False).astype(np.uint32)
+        new_is_b = ~on_b[sl]
+        on_b[sl] = new_is_b
+        batches.append((sl, new_is_b, events(sl, new_is_b)))
+    lat, gpu_ms, bytes_up = [], [], 0
+    mism = 0
+    checked = 0
+    sample_ok = None
+    first_res = None
+    inflight = []  # (ticket, t_submit, batch index)
+    eng.timing_reset()
+    t_start = None
+    for k, (sl, new_is_b, ev) in enumerate(batches):
+        if k == args.warmup_batches:
+            # drain the warmup batches, then start the clock
+            while inflight:
+                tk, ts, kk = inflight.pop(0)
+                eng.wait(tk)
+            eng.timing_reset()
+            t_start = time.time()
+        ts = time.time()
+        tk = submit(ev)
+        if k >= args.warmup_batches:
+            bytes_up += st.stats().last_batch_bytes
+        inflight.append((tk, ts, k))
+        if len(inflight) == 2:
+            tk0, ts0, k0 = inflight.pop(0)
+            r = eng.wait(tk0)
+            if k0 >= args.warmup_batches:
+                lat.append(time.time() - ts0)
+                f = r.pair_flags & 3
+                mism += int((f != (exp_ab[batches[k0][0]] & 3)).sum())
+                checked += f.size
+                if first_res is None:
+                    first_res = (r, batches[k0])
+    while inflight:
+        tk0, ts0, k0 = inflight.pop(0)
+        r = eng.wait(tk0)
+        lat.append(time.time() - ts0)
+        f = r.pair_flags & 3
+        mism += int((f != (exp_ab[batches[k0][0]] & 3)).sum())
+        checked += f.size
+    t_end = time.time()
+    el = t_end - t_start
+    tm = eng.timings()
+    ev_total = n_batches * B
+    ss = st.stats()
+    lat_ms = np.array(lat) * 1e3
+
+    # ---- CPU baseline leg: the oracle's C++ port on a sample of the timed events
+    # (decoded trees; JSON decode untimed) and, as checker, the Python oracle on
+    # the first timed batch (flags + changed paths bit-exact)
+    cpu = None
+    if not args.no_cpu_baseline:
+        if args.sample and first_res is not None:
+            sample_ok = _sample_check(first_res[0], first_res[1], buf, offs, args.sample)
+            log("sample bit-exact vs oracle:", sample_ok)
+        from oracle import cpu_ref
+        sl, new_is_b, _ = batches[args.warmup_batches]
+        m = min(args.cpu_sample, sl.size)
+        pairs = []
+        for i in range(m):
+            s_ = int(sl[i])
+            a = bytes(buf[offs[2 * s_]:offs[2 * s_ + 1]])
+            b = bytes(buf[offs[2 * s_ + 1]:offs[2 * s_ + 2]])
+            pairs.append((a, b) if new_is_b[i] else (b, a))
+        dp = cpu_ref.DecodedPairs(pairs)
+        cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
+        dp.close()
+        agree = bool(((cflags & 3) == (first_res[0].pair_flags[:m] & 3)).all()) if first_res else None
+        cpu = dict(value=m * sweeps / sec, unit="events/s", cores=threads, kind="port",
+                   sample="%d events of the first timed batch, old+new JSON decoded untimed (the informer "
+                          "decodes them), predicates only, %d sweeps in %.1f s; decisions agree with GPU: %s" % (
+                              m, sweeps, sec, agree))
+        log("cpu baseline:", json.dumps(cpu))
+    line = {
+        "metric": "watch-replay Update events/s (device-resident old objects, JSON in, decisions + changed paths out)",
+        "value": ev_total / el,
+        "unit": "events/s",
+        "n_gpus": 1,
+        "steps": n_batches,
+        "warmup": args.warmup_batches,
+        "ms_per_step": el / n_batches * 1e3,
+        "higher_is_better": True,
+        "scaling": "replicas only",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (config3 object mix; each event alternates an object's two seeded versions)",
+        "config": {"workload": "config5: %d resident objects, batches of %d events, 2 in flight" % (M, B),
+                   "host_encode_threads": threads},
+        "latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p99": float(np.percentile(lat_ms, 99)),
+                       "max": float(lat_ms.max())},
+        "h2d_gbps": bytes_up / el / 1e9,
+        "gpu_ms_per_batch": {"diff_pass": tm.total_ms, "k2": tm.compare_ms},
+        "store": {"resident_gb": ss.live_bytes / 1e9, "compactions": ss.compactions, "reseeded": ss.reseeded,
+                  "old_objects_encoded": ss.old_encoded},
+        "initial_list_objects_per_s": M / t_load,
+        "checks": {"events_checked": checked, "decision_mismatches_vs_ground_truth": mism,
+                   "sample_bit_exact_vs_oracle": sample_ok},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    st.free()
+    eng.close()
+
+
+def _sample_check(r, batch, buf, offs, n):
+    """First n events of a batch: flags + changed paths bit-exact vs the oracle."""
+    from oracle import gpudiff_oracle as O
+    from tests.parity import expected_flags, expected_paths
+
+    sl, new_is_b, _ = batch
+    n = min(n, sl.size)
+    pos = {int(d): k for k, d in enumerate(r.dirty_ids.tolist())}
+    for i in range(n):
+        s = int(sl[i])
+        a = bytes(buf[offs[2 * s]:offs[2 * s + 1]])
+        b = bytes(buf[offs[2 * s + 1]:offs[2 * s + 2]])
+        old, new = (a, b) if new_is_b[i] else (b, a)
+        e = O.diff_pair(old, new)
+        if int(r.pair_flags[i]) != expected_flags(e):
+            return False
+        if i in pos:
+            if r.paths_of(pos[i]) != expected_paths(e):
+                return False
+        elif e["paths"]:
+            return False
+    return True

@@ -57,6 +57,12 @@ int gpudiff_synth_encode(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t 
  * ground truth bits per pair */
 int gpudiff_synth_copy_out(gpudiff_synth* s, uint8_t* pool, gpudiff_pair_row* rows, uint8_t* truth);
 /* JSON text of local pair i (A then B); returns required sizes */
+/* JSON of local pairs [first, first+n): A_i, B_i concatenated into one malloc'ed
+ * buffer (free with gpudiff_synth_free_buf); offs[2n+1] byte offsets; truth[n]
+ * optional ground-truth bits */
+int gpudiff_synth_json_range(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t threads, uint8_t** buf,
+                             uint64_t* offs, uint8_t* truth);
+void gpudiff_synth_free_buf(uint8_t* buf);
 int gpudiff_synth_json(gpudiff_synth* s, uint64_t i, char* a, size_t acap, size_t* alen, char* b, size_t bcap,
                        size_t* blen);
 

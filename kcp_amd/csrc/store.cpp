@@ -66,6 +66,7 @@ struct Worker {
     std::vector<uint32_t> touched;                         // slots set to batch-local offsets
     std::vector<std::pair<uint64_t, uint32_t>> pre;        // batch-start resident blobs of touched slots
     uint64_t old_encoded = 0, reseeded = 0, unresolved = 0, leaves = 0;
+    int64_t live_delta = 0, bytes_delta = 0;  // resident slot count / bytes changes of this batch
 };
 
 inline uint64_t local_tag(uint32_t part, uint64_t off) { return kLocal | ((uint64_t)part << kLocalPartShift) | off; }
@@ -172,6 +173,10 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
             S.epoch = epoch;
             if (S.live && !(S.off & kLocal)) w.pre.emplace_back(S.off, S.bytes);
         }
+        if (S.live) {  // its contribution is re-added below if it stays resident
+            w.live_delta--;
+            w.bytes_delta -= S.bytes;
+        }
         gpudiff_pair_row& r = rows[i];
         memset(&r, 0, sizeof(r));
         r.pair_id = e.pair_id;
@@ -273,6 +278,8 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
         S.stat_l = tl;
         S.stat_ar = tar;
         S.oflags = w.fn.flags & GPUDIFF_OBJ_HAS_STATUS;
+        w.live_delta++;
+        w.bytes_delta += S.bytes;
         S.spec.resize(w.fn.spec.size());
         for (size_t k = 0; k < w.fn.spec.size(); k++) S.spec[k] = HF{w.fn.spec[k].h, w.fn.spec[k].fp};
         S.stat.resize(w.fn.stat.size());
@@ -398,6 +405,9 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
         }
         leaves += w.leaves;
         w.leaves = 0;
+        s->st.live_slots += w.live_delta;
+        s->st.live_bytes += w.bytes_delta;
+        w.live_delta = w.bytes_delta = 0;
         s->st.old_encoded += w.old_encoded;
         s->st.reseeded += w.reseeded;
         s->st.collisions_unresolved += w.unresolved;
@@ -445,6 +455,10 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
 int gpudiff_store_forget(gpudiff_ctx* c, gpudiff_store* s, uint32_t slot) {
     if (!c || !s || slot >= s->max_slots) return GPUDIFF_E_INVAL;
     Slot& S = s->slots[slot];
+    if (S.live) {
+        s->st.live_slots--;
+        s->st.live_bytes -= S.bytes;
+    }
     S.live = false;
     S.seed = 0;
     S.spec.clear();
@@ -457,14 +471,6 @@ int gpudiff_store_forget(gpudiff_ctx* c, gpudiff_store* s, uint32_t slot) {
 int gpudiff_store_stats_get(const gpudiff_store* s, gpudiff_store_stats* out) {
     if (!s || !out) return GPUDIFF_E_INVAL;
     *out = s->st;
-    uint64_t live = 0, bytes = 0;
-    for (const Slot& S : s->slots)
-        if (S.live) {
-            live++;
-            bytes += S.bytes;
-        }
-    out->live_slots = live;
-    out->live_bytes = bytes;
     out->used_bytes = s->used;
     return GPUDIFF_OK;
 }

@@ -5,6 +5,7 @@
 #include "../../include/gpudiff_synth.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -816,5 +817,59 @@ int gpudiff_synth_json(gpudiff_synth* s, uint64_t i, char* a, size_t acap, size_
     if (b && bcap >= jb.size()) memcpy(b, jb.data(), jb.size());
     return (acap >= ja.size() && bcap >= jb.size()) ? 0 : 1;
 }
+
+// JSON of pairs [first, first+n): A_i then B_i for every pair, concatenated
+// into one buffer (watch-replay inputs); offs[2n+1] are byte offsets.
+int gpudiff_synth_json_range(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t threads, uint8_t** buf,
+                             uint64_t* offs, uint8_t* truth) {
+    if (!s || !buf || !offs || first + n > s->n_local) return -1;
+    *buf = nullptr;
+    const uint32_t T = std::max<uint32_t>(1, std::min<uint64_t>(threads ? threads : 1, std::max<uint64_t>(1, n / 64)));
+    while (s->workers.size() < T) s->workers.emplace_back(new Worker());
+    std::vector<std::string> parts(T);
+    std::vector<std::vector<uint64_t>> lens(T);
+    auto work = [&](uint32_t t) {
+        Worker& w = *s->workers[t];
+        const uint64_t b = first + n * t / T, e = first + n * (t + 1) / T;
+        std::string ja, jb;
+        for (uint64_t i = b; i < e; i++) {
+            const PairSpec ps = s->spec_of(i);
+            Node na, nb;
+            bool same;
+            const uint32_t tr = s->build(w, ps, &na, &nb, &same, true);
+            if (truth) truth[i - first] = (uint8_t)tr;
+            ja.clear();
+            jb.clear();
+            to_json(ja, na);
+            to_json(jb, nb);
+            parts[t] += ja;
+            parts[t] += jb;
+            lens[t].push_back(ja.size());
+            lens[t].push_back(jb.size());
+        }
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    uint64_t total = 0;
+    for (auto& p : parts) total += p.size();
+    uint8_t* out = (uint8_t*)malloc(std::max<uint64_t>(total, 1));
+    if (!out) return -2;
+    uint64_t pos = 0, k = 0;
+    offs[0] = 0;
+    for (uint32_t t = 0; t < T; t++) {
+        memcpy(out + pos, parts[t].data(), parts[t].size());
+        pos += parts[t].size();
+        for (uint64_t l : lens[t]) {
+            offs[k + 1] = offs[k] + l;
+            k++;
+        }
+    }
+    *buf = out;
+    return 0;
+}
+
+void gpudiff_synth_free_buf(uint8_t* buf) { free(buf); }
 
 }  // extern "C"

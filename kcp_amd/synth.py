@@ -33,6 +33,8 @@ _SIGS = [
     ("gpudiff_synth_encode", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)]),
     ("gpudiff_synth_copy_out", C.c_int, [_P, _P, _P, _P]),
+    ("gpudiff_synth_json_range", C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(_P), _P, _P]),
+    ("gpudiff_synth_free_buf", None, [_P]),
     ("gpudiff_synth_json", C.c_int, [_P, C.c_uint64, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_char_p,
                                      C.c_size_t, C.POINTER(C.c_size_t)]),
 ]
@@ -118,6 +120,26 @@ class Population:
         truth = np.zeros(n, dtype=np.uint8)
         _lib.gpudiff_synth_copy_out(self.h, pool, rows, truth.ctypes.data_as(C.c_void_p))
         return Chunk(hb, truth, pb.value, lv.value)
+
+    def json_range(self, first: int, n: int, threads: int = 16):
+        """JSON of local pairs [first, first+n) in one buffer: (u8 buffer, u64
+        offsets [2n+1] with A_i at [offs[2i], offs[2i+1]) and B_i after it,
+        u8 ground-truth bits [n])."""
+        offs = np.zeros(2 * n + 1, dtype=np.uint64)
+        truth = np.zeros(max(n, 1), dtype=np.uint8)
+        p = C.c_void_p()
+        rc = _lib.gpudiff_synth_json_range(self.h, first, n, threads, C.byref(p), offs.ctypes.data,
+                                           truth.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("gpudiff_synth_json_range failed (%d)" % rc)
+        try:
+            total = int(offs[-1])
+            buf = np.empty(max(total, 1), dtype=np.uint8)
+            if total:
+                C.memmove(buf.ctypes.data, p, total)
+        finally:
+            _lib.gpudiff_synth_free_buf(p)
+        return buf, offs, truth[:n]
 
     def json_pair(self, i: int):
         al, bl = C.c_size_t(), C.c_size_t()
