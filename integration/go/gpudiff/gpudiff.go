@@ -78,6 +78,15 @@ func cbytes(b []byte) (*C.uint8_t, C.size_t) {
 	return (*C.uint8_t)(unsafe.Pointer(&b[0])), C.size_t(len(b))
 }
 
+// cmem copies b into C memory: pointers stored inside C-allocated arrays
+// (gpudiff_json_pair, gpudiff_event) must not be Go pointers (cgo rules).
+func cmem(b []byte) (*C.uint8_t, C.size_t) {
+	if len(b) == 0 {
+		return nil, 0
+	}
+	return (*C.uint8_t)(C.CBytes(b)), C.size_t(len(b))
+}
+
 // DeepEqualApartFromStatus is the drop-in for specsyncer.go:17-41.
 func (e *Engine) DeepEqualApartFromStatus(oldObj, newObj interface{}) bool {
 	a, ok1 := jsonOf(oldObj)
@@ -126,6 +135,7 @@ type event struct {
 	old, new interface{}
 	which    Which
 	enqueue  func(obj interface{})
+	slot     int64 // >= 0: decided against the Store's resident version of this slot
 }
 
 // Batcher collects UpdateFunc events from all informers (MPSC) and decides
@@ -133,6 +143,7 @@ type event struct {
 // (Controller.AddToQueue, syncer.go:222-224) in arrival order.
 type Batcher struct {
 	e        *Engine
+	store    *Store
 	ch       chan event
 	maxBatch int
 	window   time.Duration
@@ -146,7 +157,14 @@ func NewBatcher(e *Engine, maxBatch int, window time.Duration) *Batcher {
 
 // Update replaces `if !deepEqual...(old, new) { c.AddToQueue(gvr, new) }`.
 func (b *Batcher) Update(oldObj, newObj interface{}, which Which, enqueue func(obj interface{})) {
-	b.ch <- event{oldObj, newObj, which, enqueue}
+	b.ch <- event{oldObj, newObj, which, enqueue, -1}
+}
+
+// UpdateStored is Update against the batcher's Store: only the new object is
+// uploaded; oldObj is read only if the slot is empty or a path-hash collision
+// needs a re-seed.  All events of one Batcher go either here or to Update.
+func (b *Batcher) UpdateStored(slot uint32, oldObj, newObj interface{}, which Which, enqueue func(obj interface{})) {
+	b.ch <- event{oldObj, newObj, which, enqueue, int64(slot)}
 }
 
 func (b *Batcher) loop() {
@@ -170,10 +188,13 @@ func (b *Batcher) loop() {
 }
 
 func (b *Batcher) flush(evs []event) {
+	if b.store != nil {
+		b.flushStored(evs)
+		return
+	}
 	n := len(evs)
 	pairs := (*[1 << 28]C.gpudiff_json_pair)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_json_pair{}))))[:n:n]
 	defer C.free(unsafe.Pointer(&pairs[0]))
-	keep := make([][]byte, 0, 2*n)
 	bad := make([]bool, n)
 	for i, ev := range evs {
 		a, ok1 := jsonOf(ev.old)
@@ -182,12 +203,17 @@ func (b *Batcher) flush(evs []event) {
 			bad[i] = true
 			a, c = []byte("{}"), []byte("{}")
 		}
-		keep = append(keep, a, c)
-		pa, la := cbytes(a)
-		pc, lc := cbytes(c)
+		pa, la := cmem(a)
+		pc, lc := cmem(c)
 		pairs[i] = C.gpudiff_json_pair{old_json: pa, old_len: la, new_json: pc, new_len: lc,
 			pair_id: C.uint32_t(i)}
 	}
+	defer func() {
+		for i := range pairs {
+			C.free(unsafe.Pointer(pairs[i].old_json))
+			C.free(unsafe.Pointer(pairs[i].new_json))
+		}
+	}()
 	b.e.mu.Lock()
 	var ticket C.gpudiff_ticket
 	rc := C.gpudiff_submit(b.e.ctx, &pairs[0], C.size_t(n), &ticket)
@@ -208,7 +234,97 @@ func (b *Batcher) flush(evs []event) {
 			ev.enqueue(ev.new)
 		}
 	}
-	_ = keep
+}
+
+// Store is the device-resident informer snapshot (gpudiff_store_*): the old
+// versions stay in HBM, one per slot ((cluster, gvr, namespace, name) -> slot,
+// the indexer's key, pkg/syncer/syncer.go:318).
+type Store struct {
+	e *Engine
+	s *C.gpudiff_store
+}
+
+func (e *Engine) NewStore(maxSlots uint32, spaceBytes uint64, maxEvents uint32) (*Store, error) {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	var s *C.gpudiff_store
+	if err := errOf(C.gpudiff_store_create(e.ctx, C.uint32_t(maxSlots), C.uint64_t(spaceBytes),
+		C.uint32_t(maxEvents), &s)); err != nil {
+		return nil, err
+	}
+	return &Store{e: e, s: s}, nil
+}
+
+// Forget is the DeleteFunc side: the slot is empty again.
+func (s *Store) Forget(slot uint32) error {
+	s.e.mu.Lock()
+	defer s.e.mu.Unlock()
+	return errOf(C.gpudiff_store_forget(s.e.ctx, s.s, C.uint32_t(slot)))
+}
+
+// WithStore routes the batcher's UpdateStored events through st.
+func (b *Batcher) WithStore(st *Store) *Batcher {
+	b.store = st
+	return b
+}
+
+func (b *Batcher) flushStored(evs []event) {
+	// events whose objects are not Unstructured never reach the store (its slot
+	// state must only see real versions); they are enqueued, as the reference's
+	// failed type assertion would (specsyncer.go:20-22)
+	good := make([]int, 0, len(evs))
+	for i, ev := range evs {
+		if _, ok := ev.new.(*unstructured.Unstructured); ok && ev.slot >= 0 {
+			good = append(good, i)
+		} else {
+			ev.enqueue(ev.new)
+		}
+	}
+	n := len(good)
+	if n == 0 {
+		return
+	}
+	ce := (*[1 << 27]C.gpudiff_event)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_event{}))))[:n:n]
+	defer C.free(unsafe.Pointer(&ce[0]))
+	ok := make([]bool, n)
+	for k, i := range good {
+		ev := evs[i]
+		ce[k] = C.gpudiff_event{slot: C.uint32_t(ev.slot), pair_id: C.uint32_t(k)}
+		if nb, okn := jsonOf(ev.new); okn {
+			ce[k].new_json, ce[k].new_len = cmem(nb)
+			ok[k] = true
+		} else {
+			ce[k].new_json, ce[k].new_len = cmem([]byte("{"))  // undecodable: reported dirty, slot emptied
+		}
+		if ob, oko := jsonOf(ev.old); oko {
+			ce[k].old_json, ce[k].old_len = cmem(ob)
+		}
+	}
+	defer func() {
+		for k := range ce {
+			C.free(unsafe.Pointer(ce[k].new_json))
+			C.free(unsafe.Pointer(ce[k].old_json))
+		}
+	}()
+	b.e.mu.Lock()
+	var ticket C.gpudiff_ticket
+	rc := C.gpudiff_store_submit(b.e.ctx, b.store.s, &ce[0], C.size_t(n), &ticket)
+	var res C.gpudiff_result
+	if rc == C.GPUDIFF_OK {
+		rc = C.gpudiff_wait(b.e.ctx, ticket, &res)
+	}
+	flags := make([]uint8, n)
+	if rc == C.GPUDIFF_OK {
+		copy(flags, (*[1 << 30]uint8)(unsafe.Pointer(res.pair_flags))[:n:n])
+		C.gpudiff_result_release(b.e.ctx, &res)
+	}
+	b.e.mu.Unlock()
+	for k, i := range good {
+		ev := evs[i]
+		if rc != C.GPUDIFF_OK || !ok[k] || flags[k]&uint8(ev.which) != 0 {
+			ev.enqueue(ev.new)
+		}
+	}
 }
 
 var errNoEngine = errors.New("gpudiff: engine not initialised")
