@@ -149,7 +149,7 @@ SIGNATURES = [
 
 def _load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
-        raise ImportError("libgpudiff.so not built (run `python -m kcp_amd.build`); there is no CPU fallback")
+        raise ImportError("libgpudiff.so not built (run `python kcp_amd/build.py`); there is no CPU fallback")
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         f = getattr(lib, name)
