@@ -814,7 +814,7 @@ int gpudiff_resolve_path(const uint8_t* a, size_t al, const uint8_t* b, size_t b
         const uint64_t mask = cfg.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg.hash_bits) - 1);
         const uint32_t seed = (row.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFF;
         const std::string& sp = status_path_bytes();
-        if ((xxh64_host(sp.data(), sp.size(), seed) & mask) == h) {
+        if ((chain_hash(sp.data(), sp.size(), seed) & mask) == h) {
             s = "status";
             found = true;
         }

@@ -33,6 +33,22 @@ static inline void push_idx(std::string& p, uint32_t i) {
     p.append(hdr, 5);
 }
 
+uint64_t chain_hash(const char* p, size_t n, uint64_t seed) {
+    uint64_t h = seed;
+    size_t i = 0;
+    while (i + 5 <= n) {
+        uint32_t len = 5;
+        if (p[i] == 0x01) {
+            uint32_t k;
+            memcpy(&k, p + i + 1, 4);
+            len += k;
+        }
+        h = xxh64_host(p + i, len, h);
+        i += len;
+    }
+    return h;
+}
+
 const std::string& status_path_bytes() {
     static const std::string s = [] {
         std::string p;
@@ -189,7 +205,7 @@ bool PairEncoder::assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed_out) 
     for (uint32_t seed = 0; seed <= 255; seed++) {
         for (FlatObject* o : {&a, &b})
             for (std::vector<LeafRec>* v : {&o->spec, &o->stat}) {
-                for (LeafRec& r : *v) r.h = xxh64_host(o->paths.data() + r.path_off, r.path_len, seed) & mask;
+                for (LeafRec& r : *v) r.h = chain_hash(o->paths.data() + r.path_off, r.path_len, seed) & mask;
                 std::sort(v->begin(), v->end(), by_h);
             }
         bool ok = true;
@@ -200,7 +216,7 @@ bool PairEncoder::assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed_out) 
         ok = ok && merge_check(a, a.spec, b, b.spec) && merge_check(a, a.stat, b, b.stat);
         if (ok) {
             const std::string& sp = status_path_bytes();
-            uint64_t hs = xxh64_host(sp.data(), sp.size(), seed) & mask;
+            uint64_t hs = chain_hash(sp.data(), sp.size(), seed) & mask;
             ok = sentinel_check(a, a.stat, hs) && sentinel_check(b, b.stat, hs);
         }
         if (ok) {
@@ -298,7 +314,6 @@ void PairEncoder::encode_json(const uint8_t* a, size_t alen, const uint8_t* b, s
 }
 
 // ------------------------------------------------------------------ object store helpers
-static constexpr uint64_t kFingerprintSeed = 0x9FB21C651E98DF25ull;
 
 bool PairEncoder::flatten_json(const uint8_t* json, size_t len, Arena& arena, FlatObject& o) {
     arena.reset();
@@ -310,20 +325,20 @@ bool PairEncoder::flatten_json(const uint8_t* json, size_t len, Arena& arena, Fl
 
 static void fingerprints(FlatObject& o) {
     for (std::vector<LeafRec>* v : {&o.spec, &o.stat})
-        for (LeafRec& r : *v) r.fp = xxh64_host(o.paths.data() + r.path_off, r.path_len, kFingerprintSeed);
+        for (LeafRec& r : *v) r.fp = chain_hash(o.paths.data() + r.path_off, r.path_len, kFingerprintSeed);
 }
 
 bool PairEncoder::hash_single(FlatObject& o, uint32_t seed) {
     const uint64_t mask = cfg_.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg_.hash_bits) - 1);
     auto by_h = [](const LeafRec& x, const LeafRec& y) { return x.h < y.h; };
     for (std::vector<LeafRec>* v : {&o.spec, &o.stat}) {
-        for (LeafRec& r : *v) r.h = xxh64_host(o.paths.data() + r.path_off, r.path_len, seed) & mask;
+        for (LeafRec& r : *v) r.h = chain_hash(o.paths.data() + r.path_off, r.path_len, seed) & mask;
         std::sort(v->begin(), v->end(), by_h);
         for (size_t i = 1; i < v->size(); i++)
             if ((*v)[i].h == (*v)[i - 1].h) return false;
     }
     const std::string& sp = status_path_bytes();
-    if (!sentinel_check(o, o.stat, xxh64_host(sp.data(), sp.size(), seed) & mask)) return false;
+    if (!sentinel_check(o, o.stat, chain_hash(sp.data(), sp.size(), seed) & mask)) return false;
     fingerprints(o);
     return true;
 }

@@ -10,7 +10,8 @@
 //   status region = the "status" subtree (statussyncer.go:22-24), a top-level
 //                   `status: null` contributes no leaves but sets HAS_STATUS.
 // Leaves are scalars and empty containers; paths are encoded component by
-// component (0x01 u32le(len) key | 0x02 u32le(index)) and hashed with XXH64.
+// component (0x01 u32le(len) key | 0x02 u32le(index)) and hashed with the
+// chained XXH64 below.
 #pragma once
 #include <stdint.h>
 
@@ -92,6 +93,14 @@ class PairEncoder {
                     uint32_t* sar, uint32_t* tl, uint32_t* tar);
     EncodeConfig cfg_;
 };
+
+// Chained path hash over encoded path bytes: h(empty) = seed,
+// h(p + c) = XXH64(enc(c), seed = h(p)).  A child's hash depends only on its
+// parent's hash and its own component, so the device tokenizer hashes a tree
+// level by level (kernels K0*).  Masking to hash_bits happens on the result.
+uint64_t chain_hash(const char* p, size_t n, uint64_t seed);
+// Root of the object store's fingerprint chain (an independent second path hash)
+constexpr uint64_t kFingerprintSeed = 0x9FB21C651E98DF25ull;
 
 // Status-region sentinel path bytes: [Key "status"]
 const std::string& status_path_bytes();

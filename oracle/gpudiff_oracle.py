@@ -417,7 +417,15 @@ def encode_path(path: Path) -> bytes:
 
 
 def path_hash(path: Path, seed: int = 0) -> int:
-    return xxhash.xxh64_intdigest(encode_path(path), seed=seed)
+    """Chained XXH64 over the path's encoded components (build-defined, as the
+    whole field-path diff is): h(()) = seed and
+    h(p + (c,)) = XXH64(encode_path((c,)), seed=h(p)).  A child's hash is a
+    function of its parent's hash and its own component only, which is what
+    lets the device tokenizer hash a document tree level by level."""
+    h = seed
+    for comp in path:
+        h = xxhash.xxh64_intdigest(encode_path((comp,)), seed=h)
+    return h
 
 
 def render_path(path: Path) -> str:
