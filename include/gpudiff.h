@@ -58,6 +58,18 @@ enum {
 #define GPUDIFF_STATUS_DIRTY 0x2u
 #define GPUDIFF_DECODE_ERROR 0x4u
 
+/* device encoder (K0) per-object status: 0 = encoded on the device; otherwise
+ * the reason the object was handed to the host encoder (the Go-exact path) */
+#define GPUDIFF_TOK_OK 0
+#define GPUDIFF_TOK_SYNTAX 1  /* not in the device's JSON subset: the host decides (usually a Go decode error) */
+#define GPUDIFF_TOK_NUMBER 2  /* number outside the exact fast path (float needing full strtod, int64 overflow) */
+#define GPUDIFF_TOK_KEY 3     /* object key that needs unescaping or UTF-8 repair */
+#define GPUDIFF_TOK_STRING 4  /* control character or invalid escape in a string */
+#define GPUDIFF_TOK_HASH 5    /* equal path hashes: duplicate key, or a collision under the seed */
+#define GPUDIFF_TOK_DEPTH 6   /* nesting deeper than 255 */
+#define GPUDIFF_TOK_SIZE 7    /* document larger than 16 MiB */
+#define GPUDIFF_TOK_SPACE 8   /* output space exhausted */
+
 /* changed-path kinds (low 2 bits); bit 7 = status region */
 #define GPUDIFF_PATH_CHANGED 0u        /* present in both, value differs */
 #define GPUDIFF_PATH_ADDED 1u          /* only in new (B) */
@@ -273,6 +285,24 @@ int gpudiff_store_submit(gpudiff_ctx* ctx, gpudiff_store* st, const gpudiff_even
 int gpudiff_store_forget(gpudiff_ctx* ctx, gpudiff_store* st, uint32_t slot);
 int gpudiff_store_stats_get(const gpudiff_store* st, gpudiff_store_stats* out);
 void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
+
+/* ---- object encoding in the device-store format (inspection / parity) ----
+ * An object's blob followed by its fingerprint trailer.  gpudiff_encode_objects
+ * runs kernel K0 (the device JSON tokenizer + encoder) over n documents;
+ * gpudiff_encode_object_host runs the host encoder (the Go-exact path) over
+ * one.  Where K0 reports GPUDIFF_TOK_OK the two are byte-identical. */
+typedef struct gpudiff_obj_info {
+    int32_t status;          /* GPUDIFF_TOK_*: 0 = encoded */
+    uint32_t oflags;         /* GPUDIFF_OBJ_HAS_STATUS */
+    uint32_t spec_l, spec_ar, stat_l, stat_ar;
+    uint64_t off;            /* blob offset in out */
+    uint64_t bytes;          /* blob + trailer bytes */
+} gpudiff_obj_info;
+
+int gpudiff_encode_objects(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, const uint32_t* seeds,
+                           size_t n, uint8_t* out, uint64_t out_cap, gpudiff_obj_info* info);
+int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, uint32_t path_hash_bits, uint8_t* out,
+                               uint64_t out_cap, gpudiff_obj_info* info);
 
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,

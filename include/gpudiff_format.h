@@ -41,6 +41,10 @@
 #define GPUDIFF_OBJ_DECODE_ERR 0x2u   /* JSON failed the Go decode rules */
 #define GPUDIFF_OBJ_FRESH 0x4u        /* object store: blob uploaded with this batch (K1 hashes
                                          its long values; resident blobs were hashed on arrival) */
+/* object store: root of the fingerprint chain, an independent second path hash
+ * (fp(p + c) = XXH64(enc(c), fp(p))) kept after a resident blob's segments */
+#define GPUDIFF_FP_ROOT 0x9FB21C651E98DF25ull
+
 /* bits 8..15 of flags_a: per-pair path-hash seed */
 #define GPUDIFF_OBJ_SEED_SHIFT 8u
 

@@ -354,6 +354,21 @@ void PairEncoder::write_object(const FlatObject& o, std::vector<uint8_t>& pool, 
     write_blob(o, pool, off, sl, sar, tl, tar);
 }
 
+void PairEncoder::write_object_fp(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
+                                  uint32_t* sar, uint32_t* tl, uint32_t* tar, uint32_t* bytes) {
+    write_blob(o, pool, off, sl, sar, tl, tar);
+    const size_t n = o.spec.size() + o.stat.size();
+    const size_t base = pool.size();
+    pool.resize(base + ((8 * n + 15) & ~(size_t)15), 0);
+    uint8_t* f = pool.data() + base;
+    for (const std::vector<LeafRec>* v : {&o.spec, &o.stat})
+        for (const LeafRec& r : *v) {
+            memcpy(f, &r.fp, 8);
+            f += 8;
+        }
+    *bytes = (uint32_t)(pool.size() - *off);
+}
+
 std::string render_path(const char* p, size_t n) {
     std::string s;
     size_t i = 0;

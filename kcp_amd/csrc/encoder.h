@@ -78,6 +78,11 @@ class PairEncoder {
     // Appends o's blob (16-B aligned) and reports its layout.
     void write_object(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl, uint32_t* sar,
                       uint32_t* tl, uint32_t* tar);
+    // Device object store format: the blob followed by the fingerprint trailer
+    // (fp of the spec leaves, then of the status leaves, in key order; padded
+    // to 16 B) -- the bytes kernel K0 writes for the same object.
+    void write_object_fp(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl, uint32_t* sar,
+                         uint32_t* tl, uint32_t* tar, uint32_t* bytes);
 
     uint64_t leaves_written = 0;
     uint64_t reseeded = 0;
@@ -100,7 +105,7 @@ class PairEncoder {
 // level by level (kernels K0*).  Masking to hash_bits happens on the result.
 uint64_t chain_hash(const char* p, size_t n, uint64_t seed);
 // Root of the object store's fingerprint chain (an independent second path hash)
-constexpr uint64_t kFingerprintSeed = 0x9FB21C651E98DF25ull;
+constexpr uint64_t kFingerprintSeed = GPUDIFF_FP_ROOT;
 
 // Status-region sentinel path bytes: [Key "status"]
 const std::string& status_path_bytes();

@@ -1,0 +1,80 @@
+// K0: device JSON tokenizer + canonical encoder (tokenize.hip) and the
+// device object-store kernels around it.  Internal, not part of the ABI.
+//
+// One wave turns one raw JSON object (an informer event body) into the same
+// blob the host encoder writes (include/gpudiff_format.h), followed by the
+// fingerprint trailer the object store checks collisions with:
+//
+//   blob = [spec segment][status segment][fp(spec leaves) u64][fp(status leaves) u64]
+//
+// Anything outside the device's exact subset -- a Go decode error of any kind,
+// a float literal beyond the exact fast path, a key that needs unescaping, a
+// duplicate key or path-hash collision, nesting deeper than 255 -- is not
+// guessed at: the object is reported with a nonzero status and the host
+// encoder (json.cpp + encoder.cpp, the Go-exact path) takes it over.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpudiff_format.h"
+
+namespace gd {
+
+struct TokDoc {
+    uint64_t json_off;     // document bytes in the staged JSON buffer (16-B aligned, kTokSlack readable after)
+    uint64_t scratch_off;  // per-document working area (tok_scratch_bytes(json_len) bytes)
+    uint32_t json_len;
+    uint32_t seed;         // path-hash seed (the slot's)
+    uint32_t pad[2];
+};
+
+struct TokOut {
+    uint64_t off;          // blob offset in the output space
+    uint32_t bytes;        // blob bytes incl. fingerprint trailer (multiple of 16)
+    uint32_t spec_l, spec_ar, stat_l, stat_ar;
+    uint32_t oflags;       // GPUDIFF_OBJ_HAS_STATUS
+    uint32_t status;       // GPUDIFF_TOK_*
+    uint32_t n_nodes;
+    uint32_t pad;
+};
+static_assert(sizeof(TokDoc) == 32, "TokDoc");
+static_assert(sizeof(TokOut) == 48, "TokOut");
+
+__host__ __device__ inline uint64_t tok_align(uint64_t x) { return (x + 255u) & ~(uint64_t)255u; }
+__host__ __device__ inline uint32_t tok_cap(uint32_t len) { return len + 2u; }
+__host__ __device__ inline uint32_t node_cap(uint32_t len) { return len / 2u + 2u; }
+
+// Per-document working area: tokens, node records, hashes, values, sort keys,
+// decoded strings.  Bounded by the JSON length (a node needs >= 2 bytes).
+struct TokLayout {
+    uint64_t tok, rec, h, fp, val, skey, meta, order, sidx, str, total;
+};
+__host__ __device__ inline TokLayout tok_layout(uint32_t len) {
+    TokLayout L;
+    const uint64_t nc = node_cap(len);
+    L.tok = 0;
+    L.rec = tok_align(4ull * tok_cap(len));
+    L.h = L.rec + tok_align(16ull * nc);
+    L.fp = L.h + tok_align(8ull * nc);
+    L.val = L.fp + tok_align(8ull * nc);
+    L.skey = L.val + tok_align(8ull * nc);
+    L.meta = L.skey + tok_align(8ull * nc);
+    L.order = L.meta + tok_align(4ull * nc);
+    L.sidx = L.order + tok_align(4ull * nc);
+    L.str = L.sidx + tok_align(4ull * nc);
+    L.total = L.str + tok_align((uint64_t)len + 32u);
+    return L;
+}
+__host__ __device__ inline uint64_t tok_scratch_bytes(uint32_t len) { return tok_layout(len).total; }
+// upper bound of a document's blob (leaf >= 2 JSON bytes -> 28 B; segment pads)
+__host__ __device__ inline uint64_t tok_blob_bound(uint32_t len) { return 14ull * len + 64u; }
+
+constexpr uint32_t kTokMaxLen = (1u << 24) - 64u;  // token words hold 24-bit positions
+constexpr uint32_t kTokSlack = 32u;                 // readable bytes K0 needs after each staged document
+
+// K0 over docs [0, n): blobs appended to space at atomic offsets (*used).
+hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                              uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
+                              TokOut* out);
+
+}  // namespace gd

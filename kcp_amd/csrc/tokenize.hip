@@ -1,0 +1,957 @@
+// K0 k_encode_docs: device JSON tokenizer + canonical encoder (gfx950, wave64).
+//
+// One wave per document (a raw informer event body).  The output is the blob
+// the host encoder writes for the same object (encoder.cpp write_blob with
+// value digests filled) plus the fingerprint trailer of the object store:
+// byte-identical, so the diff kernels cannot tell the two producers apart.
+//
+// Phases (all inside one wave, working set in a per-document scratch area):
+//   1 structural scan, 64 bytes per step: ballots give 64-bit masks of
+//     backslashes, quotes, structural characters and whitespace; escapes and
+//     in-string state are resolved on the masks (prefix-xor of the unescaped
+//     quotes), and every token start (structural, open/close quote, atom
+//     start) is appended with its position in one coalesced store per step
+//   2 tree building: the wave walks the token list (64 tokens per vector
+//     load, readlane per token) as a uniform state machine that checks the
+//     JSON grammar, creates one node per value (parent, key token or array
+//     index) and assigns the reference's regions -- S (top-level keys except
+//     metadata/status, top-level null dropped), L/N (metadata.labels /
+//     metadata.annotations children, kept only if every value is a string),
+//     T (status subtree) -- specsyncer.go:17-41, statussyncer.go:15-27
+//   3 per node, lane-parallel: chained path hash and fingerprint level by
+//     level (h(child) = XXH64(component, h(parent))), value decoding (Go
+//     escapes / UTF-8 repair, int64 or exact-fast-path float64, literals)
+//   4 bitonic sort of the node keys; equal neighbours (a duplicate key or a
+//     collision) hand the document to the host
+//   5 ballot/prefix compaction of the spec / status leaves in key order into
+//     the blob, allocated with one atomic on the space's append point
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpudiff.h"
+#include "decfloat.h"
+#include "tokenize.h"
+#include "xxh64.h"
+
+namespace gd {
+
+namespace {
+
+constexpr uint32_t TK_CLOSEQ = 0x01u;     // token code of a closing quote
+constexpr uint32_t TK_OPENQ_SLOW = 0x02u; // opening quote of a string that needs decoding
+constexpr uint32_t POS_MASK = 0xFFFFFFu;
+
+// node info word
+constexpr uint32_t NI_TAG = 7u;
+constexpr uint32_t NI_LEAF = 1u << 3;
+constexpr uint32_t NI_ATOM = 1u << 4;
+constexpr uint32_t NI_SLOW = 1u << 5;
+constexpr uint32_t NI_STR = 1u << 6;
+constexpr uint32_t NI_REG_SHIFT = 8;
+constexpr uint32_t NI_DEPTH_SHIFT = 16;
+constexpr uint32_t KEYBIT = 0x80000000u;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+enum : uint32_t { R_NONE = 0, R_SPEC = 1, R_META = 2, R_LABELS = 3, R_ANNOT = 4, R_STATUS = 5 };
+enum : uint32_t { E_ROOT, E_KEY, E_KEYCLOSE, E_COLON, E_VALUE, E_STRCLOSE, E_NEXT, E_END };
+
+constexpr uint32_t kMaxDepth = 255;
+constexpr uint32_t kWavesPerBlock = 4;
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+__device__ __forceinline__ uint64_t mask_lt(uint32_t n) { return n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL); }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
+    return ((uint64_t)rdlane((uint32_t)(v >> 32), l) << 32) | rdlane((uint32_t)v, l);
+}
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        uint32_t o = shfl32(v, lane >= d ? lane - d : lane);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return v;
+}
+// the wave's own global writes become visible to its other lanes
+__device__ __forceinline__ void wave_sync() { __threadfence_block(); }
+
+// unaligned 8-byte read; up to 15 bytes past p must be readable
+__device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint64_t lo = q[0];
+    if (!sh) return lo;
+    return (lo >> sh) | (q[1] << (64u - sh));
+}
+
+// XXH64 over a virtual byte stream given as 8-byte little-endian words
+template <class F>
+__device__ __forceinline__ uint64_t xxh64_words(uint64_t seed, uint32_t len, F word) {
+    uint64_t h;
+    const uint32_t stripes = len >> 5;
+    if (stripes) {
+        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+        for (uint32_t s = 0; s < stripes; s++) {
+            v1 = xround(v1, word(4 * s));
+            v2 = xround(v2, word(4 * s + 1));
+            v3 = xround(v3, word(4 * s + 2));
+            v4 = xround(v4, word(4 * s + 3));
+        }
+        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = seed + XP5;
+    }
+    h += len;
+    const uint32_t rem = len & 31u;
+    uint64_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+        if (8 * j < rem) w[j] = word(4 * stripes + j);
+    h = xxh64_tail(h, w, rem);
+    return xavalanche(h);
+}
+
+// path component hashes: 0x01 u32le(len) key | 0x02 u32le(index)
+__device__ __forceinline__ uint64_t hash_key(uint64_t seed, const uint8_t* k, uint32_t klen) {
+    return xxh64_words(seed, klen + 5u, [&](uint32_t i) -> uint64_t {
+        if (i == 0) return 0x01ull | ((uint64_t)klen << 8) | (ld8u(k) << 40);
+        return ld8u(k + 8u * i - 5u);
+    });
+}
+__device__ __forceinline__ uint64_t hash_index(uint64_t seed, uint32_t idx) {
+    return xxh64_words(seed, 5u, [&](uint32_t) -> uint64_t { return 0x02ull | ((uint64_t)idx << 8); });
+}
+__device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, uint32_t len) {
+    return xxh64_words(0, len, [&](uint32_t i) -> uint64_t { return ld8u(p + 8u * i); });
+}
+
+__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
+    return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
+}
+__device__ __forceinline__ uint32_t meta_arena(uint32_t m) {
+    return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) + 15u) & ~15u) : 0u;
+}
+
+__device__ __forceinline__ bool is_ws(uint32_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool is_delim(uint32_t c) {
+    return is_ws(c) || c == ',' || c == '}' || c == ']' || c == ':' || c == '"' || c == '{' || c == '[';
+}
+__device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
+
+// utf8.DecodeRune validity (json.cpp go_rune_len): sequence size, 0 if invalid
+__device__ int rune_len(const uint8_t* p, const uint8_t* end) {
+    const uint32_t c0 = p[0];
+    int size;
+    uint32_t lo = 0x80, hi = 0xBF;
+    if (c0 < 0x80) return 1;
+    if (c0 >= 0xC2 && c0 <= 0xDF) size = 2;
+    else if (c0 == 0xE0) { size = 3; lo = 0xA0; }
+    else if ((c0 >= 0xE1 && c0 <= 0xEC) || c0 == 0xEE || c0 == 0xEF) size = 3;
+    else if (c0 == 0xED) { size = 3; hi = 0x9F; }
+    else if (c0 == 0xF0) { size = 4; lo = 0x90; }
+    else if (c0 >= 0xF1 && c0 <= 0xF3) size = 4;
+    else if (c0 == 0xF4) { size = 4; hi = 0x8F; }
+    else return 0;
+    if (end - p < size) return 0;
+    if (p[1] < lo || p[1] > hi) return 0;
+    for (int k = 2; k < size; k++)
+        if (p[k] < 0x80 || p[k] > 0xBF) return 0;
+    return size;
+}
+__device__ __forceinline__ int hexv(uint32_t c) {
+    if (c - '0' < 10u) return (int)(c - '0');
+    if (c - 'a' < 6u) return (int)(c - 'a' + 10);
+    if (c - 'A' < 6u) return (int)(c - 'A' + 10);
+    return -1;
+}
+__device__ int getu4(const uint8_t* p, const uint8_t* end) {
+    if (end - p < 6 || p[0] != '\\' || p[1] != 'u') return -1;
+    int v = 0;
+    for (int k = 2; k < 6; k++) {
+        const int h = hexv(p[k]);
+        if (h < 0) return -1;
+        v = (v << 4) | h;
+    }
+    return v;
+}
+__device__ __forceinline__ uint8_t* put_utf8(uint8_t* o, uint32_t r) {
+    if (r < 0x80) {
+        *o++ = (uint8_t)r;
+    } else if (r < 0x800) {
+        *o++ = (uint8_t)(0xC0 | (r >> 6));
+        *o++ = (uint8_t)(0x80 | (r & 0x3F));
+    } else if (r < 0x10000) {
+        *o++ = (uint8_t)(0xE0 | (r >> 12));
+        *o++ = (uint8_t)(0x80 | ((r >> 6) & 0x3F));
+        *o++ = (uint8_t)(0x80 | (r & 0x3F));
+    } else {
+        *o++ = (uint8_t)(0xF0 | (r >> 18));
+        *o++ = (uint8_t)(0x80 | ((r >> 12) & 0x3F));
+        *o++ = (uint8_t)(0x80 | ((r >> 6) & 0x3F));
+        *o++ = (uint8_t)(0x80 | (r & 0x3F));
+    }
+    return o;
+}
+
+// Go string decoding (encoding/json unquote, json.cpp JsonParser::string):
+// raw bytes [p, q) between the quotes -> dst (never longer than the raw
+// bytes); returns the decoded length, or -1 for the host to decide (invalid
+// escape or control character: a Go error; invalid UTF-8: U+FFFD repair)
+__device__ int decode_string(const uint8_t* p, const uint8_t* q, const uint8_t* end, uint8_t* dst) {
+    uint8_t* o = dst;
+    while (p < q) {
+        const uint32_t c = *p;
+        if (c == '\\') {
+            if (end - p < 2) return -1;
+            const uint32_t e = p[1];
+            uint32_t b = 0;
+            switch (e) {
+                case '"': b = '"'; break;
+                case '\\': b = '\\'; break;
+                case '/': b = '/'; break;
+                case 'b': b = '\b'; break;
+                case 'f': b = '\f'; break;
+                case 'n': b = '\n'; break;
+                case 'r': b = '\r'; break;
+                case 't': b = '\t'; break;
+                case 'u': {
+                    int rr = getu4(p, end);
+                    if (rr < 0) return -1;
+                    p += 6;
+                    if (rr >= 0xD800 && rr < 0xE000) {
+                        const int rr1 = getu4(p, end);
+                        if (rr < 0xDC00 && rr1 >= 0xDC00 && rr1 < 0xE000) {
+                            const uint32_t dec = (((uint32_t)(rr - 0xD800) << 10) | (uint32_t)(rr1 - 0xDC00)) + 0x10000u;
+                            o = put_utf8(o, dec);
+                            p += 6;
+                            continue;
+                        }
+                        rr = 0xFFFD;
+                    }
+                    o = put_utf8(o, (uint32_t)rr);
+                    continue;
+                }
+                default: return -1;
+            }
+            *o++ = (uint8_t)b;
+            p += 2;
+            continue;
+        }
+        if (c < 0x20) return -1;
+        if (c < 0x80) {
+            *o++ = (uint8_t)c;
+            p++;
+            continue;
+        }
+        const int l = rune_len(p, end);
+        if (l == 0) return -1;  // U+FFFD repair would outgrow the in-place area: host encoder
+        for (int k = 0; k < l; k++) *o++ = p[k];
+        p += l;
+    }
+    return (int)(o - dst);
+}
+
+// literal / number at p (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error
+__device__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+    const uint32_t c = *p;
+    *val = 0;
+    if (c == 't' || c == 'f' || c == 'n') {
+        const uint32_t n = c == 'f' ? 5u : 4u;
+        if ((uint64_t)(end - p) < n) return GPUDIFF_TOK_SYNTAX;
+        const uint64_t w = ld8u(p) & ((1ull << (8 * n)) - 1ull);
+        const uint64_t want = c == 't' ? 0x65757274ull : c == 'f' ? 0x65736c6166ull : 0x6c6c756eull;
+        if (w != want) return GPUDIFF_TOK_SYNTAX;
+        if (p + n < end && !is_delim(p[n])) return GPUDIFF_TOK_SYNTAX;
+        *tag = c == 't' ? GPUDIFF_TAG_TRUE : c == 'f' ? GPUDIFF_TAG_FALSE : GPUDIFF_TAG_NULL;
+        return GPUDIFF_TOK_OK;
+    }
+    // number grammar: -? (0 | [1-9][0-9]*) (. [0-9]+)? ([eE] [+-]? [0-9]+)?
+    const uint8_t* q = p;
+    const bool neg = c == '-';
+    if (neg) q++;
+    if (q >= end) return GPUDIFF_TOK_SYNTAX;
+    if (*q == '0') {
+        q++;
+    } else if (*q >= '1' && *q <= '9') {
+        while (q < end && is_digit(*q)) q++;
+    } else {
+        return GPUDIFF_TOK_SYNTAX;
+    }
+    const uint8_t* int_end = q;
+    const uint8_t* frac_beg = q;
+    const uint8_t* frac_end = q;
+    bool is_int = true;
+    if (q < end && *q == '.') {
+        is_int = false;
+        q++;
+        frac_beg = q;
+        if (q >= end || !is_digit(*q)) return GPUDIFF_TOK_SYNTAX;
+        while (q < end && is_digit(*q)) q++;
+        frac_end = q;
+    }
+    int64_t ex = 0;
+    if (q < end && (*q == 'e' || *q == 'E')) {
+        is_int = false;
+        q++;
+        bool eneg = false;
+        if (q < end && (*q == '+' || *q == '-')) {
+            eneg = *q == '-';
+            q++;
+        }
+        if (q >= end || !is_digit(*q)) return GPUDIFF_TOK_SYNTAX;
+        while (q < end && is_digit(*q)) {
+            if (ex < 100000) ex = ex * 10 + (*q - '0');
+            q++;
+        }
+        if (eneg) ex = -ex;
+    }
+    if (q < end && !is_delim(*q)) return GPUDIFF_TOK_SYNTAX;
+    const uint8_t* d0 = p + (neg ? 1 : 0);
+    if (is_int) {  // strconv.ParseInt(s, 10, 64)
+        const uint64_t lim = neg ? (1ull << 63) : ((1ull << 63) - 1ull);
+        uint64_t v = 0;
+        bool ovf = false;
+        for (const uint8_t* d = d0; d < int_end; d++) {
+            const uint64_t dig = (uint64_t)(*d - '0');
+            if (v > (lim - dig) / 10) {
+                ovf = true;
+                break;
+            }
+            v = v * 10 + dig;
+        }
+        if (!ovf) {
+            *tag = GPUDIFF_TAG_INT;
+            *val = neg ? (0ull - v) : v;
+            return GPUDIFF_TOK_OK;
+        }
+        // beyond int64: convertNumber falls back to float64
+    }
+    // strconv.ParseFloat on the significant digits (first to last nonzero),
+    // <= 19 of them: decfloat.h (Clinger's exact path, else Eisel-Lemire)
+    const uint32_t n_int = (uint32_t)(int_end - d0), n_frac = (uint32_t)(frac_end - frac_beg);
+    const uint32_t n_all = n_int + n_frac;
+    auto digit = [&](uint32_t k) -> uint32_t { return (k < n_int ? d0[k] : frac_beg[k - n_int]) - '0'; };
+    uint32_t first = n_all, last = 0;
+    for (uint32_t k = 0; k < n_all; k++)
+        if (digit(k)) {
+            if (first == n_all) first = k;
+            last = k;
+        }
+    *tag = GPUDIFF_TAG_FLOAT;
+    if (first == n_all) {
+        *val = 0;  // +-0.0 -> +0.0 (Go ==)
+        return GPUDIFF_TOK_OK;
+    }
+    if (last - first + 1 > 19) return GPUDIFF_TOK_NUMBER;
+    uint64_t w = 0;
+    for (uint32_t k = first; k <= last; k++) w = w * 10 + digit(k);
+    const int64_t e10 = ex - (int64_t)n_frac + (int64_t)(n_all - 1 - last);
+    uint64_t bits;
+    if (!decimal_to_double(w, e10, neg, &bits)) return GPUDIFF_TOK_NUMBER;
+    *val = bits;
+    return GPUDIFF_TOK_OK;
+}
+
+struct Scratch {
+    uint32_t* tok;
+    uint4* rec;
+    uint64_t *h, *fp, *val, *skey;
+    uint32_t *meta, *order, *sidx;
+    uint8_t* str;
+};
+
+// 8-byte constants of the region keys
+constexpr uint64_t KW_METADATA = 0x617461646174656dull;   // "metadata"
+constexpr uint64_t KW_STATUS = 0x737574617473ull;         // "status"
+constexpr uint64_t KW_LABELS = 0x736c6562616cull;         // "labels"
+constexpr uint64_t KW_ANNOT8 = 0x697461746f6e6e61ull;     // "annotati"
+constexpr uint64_t KW_ANNOT3 = 0x736e6full;               // "ons"
+
+__device__ __forceinline__ bool key_is(const uint8_t* k, uint32_t klen, uint64_t w, uint32_t n) {
+    return klen == n && (ld8u(k) & (n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull))) == w;
+}
+__device__ __forceinline__ bool key_is_annotations(const uint8_t* k, uint32_t klen) {
+    return klen == 11 && ld8u(k) == KW_ANNOT8 && (ld8u(k + 8) & 0xFFFFFFull) == KW_ANNOT3;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ docs, uint32_t n_docs,
+                                                     const uint8_t* __restrict__ json, uint8_t* __restrict__ scratch,
+                                                     uint8_t* __restrict__ space, uint64_t space_cap,
+                                                     unsigned long long* __restrict__ used, uint64_t mask,
+                                                     TokOut* __restrict__ out) {
+    __shared__ uint32_t s_stk_node[kWavesPerBlock][kMaxDepth + 1];
+    __shared__ uint32_t s_stk_meta[kWavesPerBlock][kMaxDepth + 1];
+    __shared__ uint32_t s_hist[kWavesPerBlock][kMaxDepth + 1];
+    __shared__ uint32_t s_cur[kWavesPerBlock][kMaxDepth + 1];
+
+    const uint32_t lane = lane_id();
+    const uint32_t wib = threadIdx.x >> 6;
+    const uint32_t doc_i = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wib);
+    if (doc_i >= n_docs) return;
+    uint32_t* stk_node = s_stk_node[wib];
+    uint32_t* stk_meta = s_stk_meta[wib];
+    uint32_t* hist = s_hist[wib];
+    uint32_t* cur = s_cur[wib];
+
+    const TokDoc D = docs[doc_i];
+    const uint8_t* d = json + D.json_off;
+    const uint32_t len = D.json_len;
+    TokOut o{};
+    if (len > kTokMaxLen) {
+        if (lane == 0) {
+            o.status = GPUDIFF_TOK_SIZE;
+            out[doc_i] = o;
+        }
+        return;
+    }
+    const TokLayout LY = tok_layout(len);
+    uint8_t* base = scratch + D.scratch_off;
+    Scratch S;
+    S.tok = (uint32_t*)(base + LY.tok);
+    S.rec = (uint4*)(base + LY.rec);
+    S.h = (uint64_t*)(base + LY.h);
+    S.fp = (uint64_t*)(base + LY.fp);
+    S.val = (uint64_t*)(base + LY.val);
+    S.skey = (uint64_t*)(base + LY.skey);
+    S.meta = (uint32_t*)(base + LY.meta);
+    S.order = (uint32_t*)(base + LY.order);
+    S.sidx = (uint32_t*)(base + LY.sidx);
+    S.str = base + LY.str;
+    const uint32_t ncap = node_cap(len);
+    uint32_t status = GPUDIFF_TOK_OK;
+
+    // ------------------------------------------------------------ phase 1: structural scan
+    uint32_t ntok = 0;
+    uint64_t esc_carry = 0, str_carry = 0, atom_carry = 0;
+    uint32_t last_open_idx = NONE, last_open_pos = 0, last_marked = NONE;
+    bool ctl_in_string = false;
+    for (uint32_t b = 0; b < len; b += 64) {
+        const uint32_t pos = b + lane;
+        const uint32_t c = pos < len ? d[pos] : 0x20u;
+        const uint64_t bs = ballot(c == '\\');
+        const uint64_t qt = ballot(c == '"');
+        const uint64_t st = ballot(c == '{' || c == '}' || c == '[' || c == ']' || c == ':' || c == ',');
+        const uint64_t wsm = ballot(is_ws(c));
+        const uint64_t ctl = ballot(c < 0x20u);  // inside a string every control byte is an error
+        const uint64_t hi = ballot(c >= 0x80u);
+        // escaped characters: an unescaped backslash escapes the next byte
+        uint64_t esc = esc_carry;
+        esc_carry = 0;
+        for (uint64_t m = bs; m;) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            if ((esc >> i) & 1ull) continue;
+            if (i == 63) esc_carry = 1;
+            else esc |= 1ull << (i + 1);
+        }
+        const uint64_t q = qt & ~esc;
+        uint64_t x = q;
+        x ^= x << 1;
+        x ^= x << 2;
+        x ^= x << 4;
+        x ^= x << 8;
+        x ^= x << 16;
+        x ^= x << 32;
+        const uint64_t instr = x ^ str_carry;  // opening quote + string body
+        str_carry = (instr >> 63) ? ~0ull : 0ull;
+        const uint64_t valid = mask_lt(len - b);
+        const uint64_t opens = q & instr, closes = q & ~instr;
+        const uint64_t structural = st & ~instr & valid;
+        const uint64_t atom = ~instr & ~q & ~st & ~wsm & valid;
+        const uint64_t astart = atom & ~((atom << 1) | atom_carry);
+        atom_carry = atom >> 63;
+        if (ctl & valid & instr & ~opens) ctl_in_string = true;
+        const uint64_t tokens = structural | opens | closes | astart;
+        // strings that need decoding (a backslash or a non-ASCII byte inside)
+        uint64_t slow_opens = 0;
+        for (uint64_t marks = (bs | hi) & instr & ~opens; marks;) {
+            const uint32_t mb = (uint32_t)__builtin_ctzll(marks);
+            const uint64_t ob = opens & mask_lt(mb);
+            if (ob) {
+                slow_opens |= 1ull << (63 - __builtin_clzll(ob));
+            } else if (last_open_idx != NONE && last_open_idx != last_marked) {
+                // the string opened in an earlier step: rewrite its token
+                wave_sync();
+                if (lane == 0) S.tok[last_open_idx] = (TK_OPENQ_SLOW << 24) | last_open_pos;
+                last_marked = last_open_idx;
+            }
+            const uint64_t nx = opens & ~mask_lt(mb + 1);
+            marks = nx ? (marks & ~mask_lt((uint32_t)__builtin_ctzll(nx))) : 0ull;
+        }
+        if ((tokens >> lane) & 1ull) {
+            const uint32_t idx = ntok + popc64(tokens & mask_lt(lane));
+            uint32_t code = c;
+            if ((closes >> lane) & 1ull) code = TK_CLOSEQ;
+            else if ((slow_opens >> lane) & 1ull) code = TK_OPENQ_SLOW;
+            S.tok[idx] = (code << 24) | pos;
+        }
+        if (opens) {
+            const uint32_t ob = 63u - (uint32_t)__builtin_clzll(opens);
+            last_open_idx = ntok + popc64(tokens & mask_lt(ob));
+            last_open_pos = b + ob;
+            if ((slow_opens >> ob) & 1ull) last_marked = last_open_idx;
+        }
+        ntok += popc64(tokens);
+    }
+    if (str_carry) status = GPUDIFF_TOK_SYNTAX;  // unterminated string
+    if (ctl_in_string && status == GPUDIFF_TOK_OK) status = GPUDIFF_TOK_STRING;
+    wave_sync();
+
+    // ------------------------------------------------------------ phase 2: tree building
+    for (uint32_t i = lane; i <= kMaxDepth; i += 64) hist[i] = 0;
+    uint32_t nn = 0, sp = 0, expect = E_ROOT;
+    bool skip = false;
+    uint32_t key_tok = 0, key_pos = 0, key_len = 0;
+    uint32_t meta_node = NONE, labels_node = NONE, annot_node = NONE;
+    bool labels_ok = true, annot_ok = true, has_status = false;
+    uint32_t max_depth = 0;
+    uint32_t rx = 0, ry = 0, rz = 0, rw = 0;  // pending node records, node k in lane k % 64
+    auto add_node = [&](uint32_t parent, uint32_t comp, uint32_t vtok, uint32_t info, uint32_t depth) -> uint32_t {
+        const uint32_t id = nn;
+        if (lane == (id & 63u)) {
+            rx = parent;
+            ry = comp;
+            rz = vtok;
+            rw = info | (depth << NI_DEPTH_SHIFT);
+        }
+        if (depth) {
+            if (lane == 0) hist[depth]++;
+            max_depth = max(max_depth, depth);
+        }
+        nn++;
+        if ((nn & 63u) == 0) S.rec[nn - 64 + lane] = make_uint4(rx, ry, rz, rw);
+        return id;
+    };
+    if (status == GPUDIFF_TOK_OK) {
+        for (uint32_t tb = 0; tb < ntok && status == GPUDIFF_TOK_OK; tb += 64) {
+            const uint32_t tv = tb + lane < ntok ? S.tok[tb + lane] : 0u;
+            const uint32_t tnext = tb + 64 < ntok ? S.tok[tb + 64] : 0u;
+            const uint32_t kend = min(64u, ntok - tb);
+            for (uint32_t k = 0; k < kend; k++) {
+                if (skip) {  // the close of an empty container, consumed by its opener's peek
+                    skip = false;
+                    continue;
+                }
+                const uint32_t t = rdlane(tv, k);
+                const uint32_t code = t >> 24, pos = t & POS_MASK, ti = tb + k;
+                if (expect == E_KEY) {
+                    if (code == '"') {
+                        key_tok = ti;
+                        key_pos = pos;
+                        expect = E_KEYCLOSE;
+                    } else {
+                        status = code == TK_OPENQ_SLOW ? GPUDIFF_TOK_KEY : GPUDIFF_TOK_SYNTAX;
+                        break;
+                    }
+                } else if (expect == E_KEYCLOSE) {
+                    key_len = pos - key_pos - 1u;  // the token after an open quote is its close
+                    expect = E_COLON;
+                } else if (expect == E_COLON) {
+                    if (code != ':') {
+                        status = GPUDIFF_TOK_SYNTAX;
+                        break;
+                    }
+                    expect = E_VALUE;
+                } else if (expect == E_STRCLOSE) {
+                    expect = E_NEXT;
+                } else if (expect == E_NEXT) {
+                    const uint32_t top = sp - 1u;
+                    const bool is_arr = stk_meta[top] & 1u;
+                    if (code == ',') {
+                        expect = is_arr ? E_VALUE : E_KEY;
+                    } else if (code == (is_arr ? (uint32_t)']' : (uint32_t)'}')) {
+                        sp--;
+                        expect = sp ? E_NEXT : E_END;
+                    } else {
+                        status = GPUDIFF_TOK_SYNTAX;
+                        break;
+                    }
+                } else if (expect == E_ROOT) {
+                    if (code != '{') {
+                        status = GPUDIFF_TOK_SYNTAX;
+                        break;
+                    }
+                    add_node(NONE, 0, ti, R_NONE << NI_REG_SHIFT, 0);
+                    const uint32_t pk = k + 1 < kend ? rdlane(tv, k + 1) : tnext;
+                    if (ti + 1 < ntok && (pk >> 24) == '}') {
+                        skip = true;  // {}: no leaves
+                        expect = E_END;
+                    } else {
+                        stk_node[0] = 0;
+                        stk_meta[0] = R_NONE << 1;
+                        sp = 1;
+                        expect = E_KEY;
+                    }
+                } else if (expect == E_VALUE) {
+                    const uint32_t top = sp - 1u;
+                    const uint32_t parent = stk_node[top];
+                    const uint32_t pm = stk_meta[top];
+                    const bool in_arr = pm & 1u;
+                    const uint32_t preg = (pm >> 1) & 7u;
+                    const uint32_t depth = sp;
+                    uint32_t comp;
+                    if (in_arr) {
+                        comp = pm >> 4;
+                        stk_meta[top] = pm + 16u;
+                    } else {
+                        comp = key_tok | KEYBIT;
+                    }
+                    const bool is_str = code == '"' || code == TK_OPENQ_SLOW;
+                    uint32_t reg = preg;
+                    bool is_lab = false, is_ann = false, is_meta = false;
+                    if (depth == 1) {
+                        const uint8_t* kp = d + key_pos + 1;
+                        if (key_is(kp, key_len, KW_METADATA, 8)) {
+                            reg = R_META;
+                            is_meta = true;
+                        } else if (key_is(kp, key_len, KW_STATUS, 6)) {
+                            has_status = true;
+                            reg = code == 'n' ? R_NONE : R_STATUS;
+                        } else {
+                            reg = code == 'n' ? R_NONE : R_SPEC;
+                        }
+                    } else if (depth == 2 && !in_arr && parent == meta_node) {
+                        const uint8_t* kp = d + key_pos + 1;
+                        is_lab = key_is(kp, key_len, KW_LABELS, 6);
+                        is_ann = key_is_annotations(kp, key_len);
+                    } else if (depth == 3 && parent == labels_node) {
+                        reg = R_LABELS;
+                        if (!is_str) labels_ok = false;
+                    } else if (depth == 3 && parent == annot_node) {
+                        reg = R_ANNOT;
+                        if (!is_str) annot_ok = false;
+                    } else if (preg == R_LABELS || preg == R_ANNOT) {
+                        reg = R_META;
+                    }
+                    const uint32_t rinfo = reg << NI_REG_SHIFT;
+                    if (code == '{' || code == '[') {
+                        const uint32_t closer = code == '{' ? '}' : ']';
+                        const uint32_t pk = k + 1 < kend ? rdlane(tv, k + 1) : tnext;
+                        if (ti + 1 < ntok && (pk >> 24) == closer) {
+                            add_node(parent, comp, ti,
+                                     rinfo | NI_LEAF | (code == '{' ? GPUDIFF_TAG_EOBJ : GPUDIFF_TAG_EARR), depth);
+                            skip = true;
+                            expect = E_NEXT;
+                        } else {
+                            if (sp > kMaxDepth - 1) {
+                                status = GPUDIFF_TOK_DEPTH;
+                                break;
+                            }
+                            const uint32_t id = add_node(parent, comp, ti, rinfo, depth);
+                            if (code == '{') {
+                                if (is_meta) meta_node = id;
+                                if (is_lab) labels_node = id;
+                                if (is_ann) annot_node = id;
+                            }
+                            stk_node[sp] = id;
+                            stk_meta[sp] = (code == '[' ? 1u : 0u) | (reg << 1);
+                            sp++;
+                            expect = code == '{' ? E_KEY : E_VALUE;
+                        }
+                    } else if (is_str) {
+                        add_node(parent, comp, ti,
+                                 rinfo | NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u),
+                                 depth);
+                        expect = E_STRCLOSE;
+                    } else if (code == '}' || code == ']' || code == ',' || code == ':' || code == TK_CLOSEQ) {
+                        status = GPUDIFF_TOK_SYNTAX;
+                        break;
+                    } else {
+                        add_node(parent, comp, ti, rinfo | NI_LEAF | NI_ATOM, depth);
+                        expect = E_NEXT;
+                    }
+                    if (nn + 2 > ncap) {
+                        status = GPUDIFF_TOK_SIZE;
+                        break;
+                    }
+                } else {  // E_END: trailing data
+                    status = GPUDIFF_TOK_SYNTAX;
+                    break;
+                }
+            }
+        }
+        if (status == GPUDIFF_TOK_OK && expect != E_END) status = GPUDIFF_TOK_SYNTAX;
+        if ((nn & 63u) && lane < (nn & 63u)) S.rec[(nn & ~63u) + lane] = make_uint4(rx, ry, rz, rw);
+    }
+    wave_sync();
+
+    const uint64_t seed = D.seed;
+    // ------------------------------------------------------------ phase 3a: values (lane per node)
+    if (status == GPUDIFF_TOK_OK) {
+        uint32_t err = GPUDIFF_TOK_OK;
+        for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            if (i >= nn) break;
+            const uint4 r = S.rec[i];
+            if (!(r.w & NI_LEAF)) continue;
+            uint32_t tag = r.w & NI_TAG, mlen = 0;
+            uint64_t v = 0;
+            if (r.w & NI_STR) {
+                const uint32_t op = S.tok[r.z] & POS_MASK, cp = S.tok[r.z + 1] & POS_MASK;
+                const uint8_t* src = d + op + 1;
+                uint32_t sl = cp - op - 1;
+                if (r.w & NI_SLOW) {
+                    uint8_t* dst = S.str + op + 1;
+                    const int dl = decode_string(src, d + cp, d + len, dst);
+                    if (dl < 0) {
+                        err = GPUDIFF_TOK_STRING;
+                        continue;
+                    }
+                    src = dst;
+                    sl = (uint32_t)dl;
+                }
+                mlen = sl;
+                if (sl <= GPUDIFF_INLINE_MAX) v = sl ? (ld8u(src) & (~0ull >> (64u - 8u * sl))) : 0ull;
+                else v = hash_bytes(src, sl);
+            } else if (r.w & NI_ATOM) {
+                const uint32_t ap = S.tok[r.z] & POS_MASK;
+                const uint32_t e = parse_atom(d + ap, d + len, &tag, &v);
+                if (e) {
+                    err = e;
+                    continue;
+                }
+                mlen = (tag == GPUDIFF_TAG_INT || tag == GPUDIFF_TAG_FLOAT) ? 8u : 0u;
+            }
+            S.val[i] = v;
+            S.meta[i] = (mlen << 3) | tag;
+        }
+        const uint32_t e = wave_max(err);  // any error: SYNTAX < NUMBER < ... all nonzero
+        if (e) status = e;
+    }
+
+    // ------------------------------------------------------------ phase 3b: path hashes by depth
+    if (status == GPUDIFF_TOK_OK && nn > 1) {
+        // counting sort of nodes by depth (hist filled in phase 2)
+        uint32_t run = 0;
+        for (uint32_t d0 = 0; d0 <= kMaxDepth; d0 += 64) {
+            const uint32_t dd = d0 + lane;
+            const uint32_t cnt = dd <= kMaxDepth ? hist[dd] : 0u;
+            const uint32_t inc = wave_incl_scan(cnt);
+            if (dd <= kMaxDepth) cur[dd] = run + inc - cnt;
+            run += rdlane(inc, 63);
+        }
+        wave_sync();
+        for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            if (i < nn) {
+                const uint32_t dep = (S.rec[i].w >> NI_DEPTH_SHIFT) & 0xFFu;
+                const uint32_t p = atomicAdd(&cur[dep], 1u);
+                S.order[p] = i;
+            }
+        }
+        wave_sync();
+        uint32_t beg = 0;
+        for (uint32_t dep = 1; dep <= max_depth; dep++) {
+            const uint32_t cnt = hist[dep];
+            for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+                if (j0 + lane < cnt) {
+                    const uint32_t i = S.order[beg + j0 + lane];
+                    const uint4 r = S.rec[i];
+                    const uint64_t ph = r.x == 0 ? seed : S.h[r.x];
+                    const uint64_t pf = r.x == 0 ? GPUDIFF_FP_ROOT : S.fp[r.x];
+                    uint64_t hh, ff;
+                    if (r.y & KEYBIT) {
+                        const uint32_t kt = r.y & ~KEYBIT;
+                        const uint32_t op = S.tok[kt] & POS_MASK, cp = S.tok[kt + 1] & POS_MASK;
+                        hh = hash_key(ph, d + op + 1, cp - op - 1);
+                        ff = hash_key(pf, d + op + 1, cp - op - 1);
+                    } else {
+                        hh = hash_index(ph, r.y);
+                        ff = hash_index(pf, r.y);
+                    }
+                    S.h[i] = hh;
+                    S.fp[i] = ff;
+                }
+            }
+            beg += cnt;
+            wave_sync();
+        }
+    }
+
+    // ------------------------------------------------------------ phase 4: sort keys, uniqueness
+    const uint32_t ns = nn > 1 ? nn - 1 : 0;  // every node but the root
+    if (status == GPUDIFF_TOK_OK && ns) {
+        for (uint32_t j = lane; j < ns; j += 64) {
+            S.skey[j] = S.h[j + 1] & mask;
+            S.sidx[j] = j + 1;
+        }
+        wave_sync();
+        // bitonic sort, all comparators ascending (flip + half-cleaners):
+        // indices >= ns act as +inf and never move
+        for (uint32_t kk = 2; (kk >> 1) < ns; kk <<= 1) {
+            for (uint32_t dd = kk; dd >= 2; dd >>= 1) {
+                const bool flip = dd == kk;
+                for (uint32_t i = lane; i < ns; i += 64) {
+                    const uint32_t j = flip ? (i ^ (kk - 1u)) : (i ^ (dd >> 1));
+                    if (j > i && j < ns) {
+                        const uint64_t a = S.skey[i], b = S.skey[j];
+                        if (a > b) {
+                            const uint32_t ia = S.sidx[i], ib = S.sidx[j];
+                            S.skey[i] = b;
+                            S.skey[j] = a;
+                            S.sidx[i] = ib;
+                            S.sidx[j] = ia;
+                        }
+                    }
+                }
+                wave_sync();
+            }
+        }
+        bool dup = false;
+        for (uint32_t j = lane + 1; j < ns; j += 64)
+            if (S.skey[j] == S.skey[j - 1]) dup = true;
+        if (ballot(dup)) status = GPUDIFF_TOK_HASH;
+    }
+
+    // ------------------------------------------------------------ phase 5: blob
+    o.n_nodes = nn;
+    o.oflags = has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
+    if (status == GPUDIFF_TOK_OK) {
+        auto region_of = [&](uint32_t w) -> uint32_t {  // 1 spec, 2 status, 0 not encoded
+            if (!(w & NI_LEAF)) return 0u;
+            const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
+            if (reg == R_SPEC || (reg == R_LABELS && labels_ok) || (reg == R_ANNOT && annot_ok)) return 1u;
+            return reg == R_STATUS ? 2u : 0u;
+        };
+        uint32_t Ls = 0, Lt = 0, ARs = 0, ARt = 0;
+        for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            uint32_t rg = 0, ar = 0;
+            if (j < ns) {
+                const uint32_t i = S.sidx[j];
+                rg = region_of(S.rec[i].w);
+                if (rg) ar = meta_arena(S.meta[i]);
+            }
+            Ls += popc64(ballot(rg == 1));
+            Lt += popc64(ballot(rg == 2));
+            ARs += wave_sum(rg == 1 ? ar : 0u);
+            ARt += wave_sum(rg == 2 ? ar : 0u);
+        }
+        const uint64_t seg_s = seg_bytes(Ls, ARs), seg_t = seg_bytes(Lt, ARt);
+        const uint64_t bytes = (seg_s + seg_t + 8ull * (Ls + Lt) + 15ull) & ~15ull;
+        uint64_t off = 0;
+        if (lane == 0) off = atomicAdd(used, (unsigned long long)bytes);
+        off = rdlane64(off, 0);
+        if (off + bytes > space_cap) {
+            status = GPUDIFF_TOK_SPACE;
+        } else {
+            uint8_t* blob = space + off;
+            uint8_t* segp[2] = {blob, blob + seg_s};
+            const uint32_t Lr[2] = {Ls, Lt};
+            uint64_t* fpt[2] = {(uint64_t*)(blob + seg_s + seg_t), (uint64_t*)(blob + seg_s + seg_t) + Ls};
+            // zero the pad between metas and arena, and the trailer pad
+            for (uint32_t g = 0; g < 2; g++) {
+                const uint32_t L = Lr[g];
+                const uint32_t pad_beg = 20u * L, pad_end = (20u * L + 15u) & ~15u;
+                if (lane < (pad_end - pad_beg) / 4u) ((uint32_t*)(segp[g] + pad_beg))[lane] = 0u;
+            }
+            if (lane == 0 && ((Ls + Lt) & 1u)) *(uint64_t*)(blob + seg_s + seg_t + 8ull * (Ls + Lt)) = 0ull;
+            uint32_t rank[2] = {0, 0}, aoff[2] = {0, 0};
+            for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                uint32_t rg = 0, i = 0, m = 0, ar = 0;
+                if (j < ns) {
+                    i = S.sidx[j];
+                    const uint32_t w = S.rec[i].w;
+                    rg = region_of(w);
+                    if (rg) {
+                        m = S.meta[i];
+                        ar = meta_arena(m);
+                    }
+                }
+                uint32_t my_rank = 0, my_aoff = 0;
+                for (uint32_t g = 0; g < 2; g++) {
+                    const uint64_t bal = ballot(rg == g + 1);
+                    const uint32_t inc = wave_incl_scan(rg == g + 1 ? ar : 0u);
+                    if (rg == g + 1) {
+                        my_rank = rank[g] + popc64(bal & mask_lt(lane));
+                        my_aoff = aoff[g] + inc - ar;
+                    }
+                    rank[g] += popc64(bal);
+                    aoff[g] += rdlane(inc, 63);
+                }
+                if (rg) {
+                    const uint32_t g = rg - 1;
+                    const uint32_t L = Lr[g];
+                    uint8_t* sp8 = segp[g];
+                    ((uint64_t*)sp8)[my_rank] = S.skey[j];
+                    ((uint64_t*)(sp8 + 8ull * L))[my_rank] = S.val[i];
+                    ((uint32_t*)(sp8 + 16ull * L))[my_rank] = m;
+                    fpt[g][my_rank] = S.fp[i];
+                }
+                // long strings: wave-cooperative 16-B copies into the arena
+                for (uint64_t bl = ballot(ar != 0); bl; bl &= bl - 1) {
+                    const uint32_t src_lane = (uint32_t)__builtin_ctzll(bl);
+                    const uint32_t si = rdlane(i, src_lane);
+                    const uint32_t sm = rdlane(m, src_lane);
+                    const uint32_t sg = rdlane(rg, src_lane) - 1u;
+                    const uint32_t sa = rdlane(my_aoff, src_lane);
+                    const uint4 r = S.rec[si];
+                    const uint32_t op = S.tok[r.z] & POS_MASK;
+                    const uint8_t* src = (r.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1);
+                    const uint32_t slen = sm >> 3;
+                    uint8_t* dst = segp[sg] + ((20ull * Lr[sg] + 15ull) & ~15ull) + sa;
+                    for (uint32_t c16 = lane; c16 * 16u < slen; c16 += 64) {
+                        const uint32_t b0 = c16 * 16u;
+                        uint64_t w0 = ld8u(src + b0), w1 = ld8u(src + b0 + 8);
+                        const uint32_t rem = slen - b0;
+                        if (rem < 16) {
+                            if (rem <= 8) {
+                                w0 &= rem == 8 ? ~0ull : ((1ull << (8 * rem)) - 1ull);
+                                w1 = 0;
+                            } else {
+                                w1 &= (1ull << (8 * (rem - 8))) - 1ull;
+                            }
+                        }
+                        ((uint64_t*)(dst + b0))[0] = w0;
+                        ((uint64_t*)(dst + b0))[1] = w1;
+                    }
+                }
+            }
+            o.off = off;
+            o.bytes = (uint32_t)bytes;
+            o.spec_l = Ls;
+            o.spec_ar = ARs;
+            o.stat_l = Lt;
+            o.stat_ar = ARt;
+        }
+    }
+    o.status = status;
+    if (lane == 0) out[doc_i] = o;
+}
+
+hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                              uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
+                              TokOut* out) {
+    if (!n) return hipSuccess;
+    const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    k_encode_docs<<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask, out);
+    return hipGetLastError();
+}
+
+}  // namespace gd

@@ -75,6 +75,17 @@ class StoreStats(C.Structure):
                 ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64)]
 
 
+class ObjInfo(C.Structure):
+    _fields_ = [("status", C.c_int32), ("oflags", C.c_uint32), ("spec_l", C.c_uint32), ("spec_ar", C.c_uint32),
+                ("stat_l", C.c_uint32), ("stat_ar", C.c_uint32), ("off", C.c_uint64), ("bytes", C.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SIZE, TOK_SPACE = range(9)
+
+
 class HBatchInfo(C.Structure):
     _fields_ = [("n_pairs", C.c_size_t), ("rows", C.c_void_p), ("pool", C.c_void_p), ("pool_bytes", C.c_uint64),
                 ("total_leaves", C.c_uint64), ("n_decode_errors", C.c_uint64), ("n_reseeded", C.c_uint64)]
@@ -140,6 +151,10 @@ SIGNATURES = [
     ("gpudiff_store_forget", C.c_int, [_P, _P, C.c_uint32]),
     ("gpudiff_store_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
     ("gpudiff_store_free", None, [_P, _P]),
+    ("gpudiff_encode_objects", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
+                                         C.c_size_t, C.c_void_p, C.c_uint64, C.POINTER(ObjInfo)]),
+    ("gpudiff_encode_object_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
+                                             C.POINTER(ObjInfo)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
@@ -456,6 +471,27 @@ class Engine:
     def object_store(self, max_slots: int, space_bytes: int, max_events: int) -> ObjectStore:
         return ObjectStore(self, max_slots, space_bytes, max_events)
 
+    # ---- object encoding (device-store format: blob + fingerprint trailer)
+    def encode_objects(self, docs, seeds=None, out_cap: int = 0):
+        """Kernel K0 over the documents: [(ObjInfo dict, blob bytes or None)]."""
+        docs = [to_json_bytes(x) for x in docs]
+        n = len(docs)
+        bufs = [C.create_string_buffer(x, len(x)) if x else C.create_string_buffer(1) for x in docs]
+        ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p) for b in bufs])
+        lens = (C.c_size_t * max(n, 1))(*[len(x) for x in docs])
+        sd = (C.c_uint32 * max(n, 1))(*(list(seeds) if seeds is not None else [0] * n))
+        cap = out_cap or sum(14 * len(x) + 64 for x in docs) + 16
+        out = C.create_string_buffer(cap)
+        info = (ObjInfo * max(n, 1))()
+        _chk(_lib.gpudiff_encode_objects(self.ctx, ptrs, lens, sd, n, C.cast(out, C.c_void_p), cap, info),
+             "gpudiff_encode_objects")
+        raw = out.raw
+        res = []
+        for i in range(n):
+            f = info[i]
+            res.append((f.as_dict(), raw[f.off:f.off + f.bytes] if f.status == TOK_OK else None))
+        return res
+
     # ---- single pair drop-ins
     def spec_equal(self, old, new) -> bool:
         a, b = to_json_bytes(old), to_json_bytes(new)
@@ -485,6 +521,20 @@ def resolve_path(old, new, path_hash: int, path_kind: int, path_hash_bits: int =
         _chk(_lib.gpudiff_resolve_path(a, len(a), b, len(b), path_hash, path_kind, path_hash_bits, buf,
                                        n.value + 1, C.byref(n)), "gpudiff_resolve_path")
     return buf.value.decode("utf-8", "replace")
+
+
+def encode_object_host(doc, seed: int = 0, path_hash_bits: int = 64):
+    """Host encoder (the Go-exact path) in the device-store format: (ObjInfo dict, blob bytes or None)."""
+    b = to_json_bytes(doc)
+    info = ObjInfo()
+    _chk(_lib.gpudiff_encode_object_host(b, len(b), seed, path_hash_bits, None, 0, C.byref(info)),
+         "gpudiff_encode_object_host")
+    if info.status != TOK_OK:
+        return info.as_dict(), None
+    out = C.create_string_buffer(max(1, info.bytes))
+    _chk(_lib.gpudiff_encode_object_host(b, len(b), seed, path_hash_bits, C.cast(out, C.c_void_p), info.bytes,
+                                         C.byref(info)), "gpudiff_encode_object_host")
+    return info.as_dict(), out.raw[:info.bytes]
 
 
 # ------------------------------------------------------------------ decoding helpers (tests / tooling)
