@@ -270,11 +270,21 @@ typedef struct gpudiff_store_stats {
     uint64_t live_bytes;       /* resident blobs */
     uint64_t compactions;
     uint64_t events, old_encoded, reseeded, collisions_unresolved;
-    uint64_t last_batch_bytes; /* blob bytes uploaded by the last submit */
+    uint64_t last_batch_bytes; /* bytes uploaded by the last submit (blobs; device-encode: JSON) */
+    uint64_t deferred;         /* device-encode: events K0 handed to the host encoder */
 } gpudiff_store_stats;
 
 int gpudiff_store_create(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,
                          gpudiff_store** out);
+/* GPUDIFF_STORE_DEVICE_ENCODE: events go up as raw JSON; kernel K0 encodes
+ * them in HBM, K0c checks collisions against the resident versions, K0x
+ * chains events per slot, and the host encoder only re-does the events K0
+ * defers (GPUDIFF_TOK_*), inside gpudiff_wait, with identical results.  In
+ * this mode event buffers must stay valid until gpudiff_wait on the ticket
+ * returns, and tickets are waited in submit order (at most two in flight). */
+#define GPUDIFF_STORE_DEVICE_ENCODE 0x1u
+int gpudiff_store_create_ex(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,
+                            uint32_t flags, gpudiff_store** out);
 /* encode (host threads), H2D into the current space, K1 on the new blobs,
  * K2..K6 over the batch's (resident, new) pairs; results via gpudiff_wait.
  * Two submits may be in flight (the next batch encodes while the GPU diffs

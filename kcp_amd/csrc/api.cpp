@@ -670,6 +670,36 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
     auto it = c->tickets.find(ticket);
     if (it == c->tickets.end()) return GPUDIFF_E_STATE;
     gpudiff_dbatch* d = it->second;
+    std::unique_ptr<ResultStore> rs(new (std::nothrow) ResultStore());
+    if (!rs) return GPUDIFF_E_NOMEM;
+    if ((rc = collect_results(c, d, *rs))) return rc;
+    auto fin = c->finishers.find(ticket);
+    if (fin != c->finishers.end()) {
+        auto fn = std::move(fin->second);
+        c->finishers.erase(fin);
+        if ((rc = fn(*rs))) return rc;
+    }
+    res->n_pairs = rs->flags.size();
+    res->pair_flags = rs->flags.data();
+    res->n_spec_dirty = rs->spec.size();
+    res->spec_dirty_ids = rs->spec.data();
+    res->n_status_dirty = rs->status.size();
+    res->status_dirty_ids = rs->status.data();
+    res->n_dirty = rs->dirty.size();
+    res->dirty_ids = rs->dirty.data();
+    res->path_offsets = rs->off.data();
+    res->n_paths = rs->hashes.size();
+    res->path_hashes = rs->hashes.data();
+    res->path_kinds = rs->kinds.data();
+    res->internal_ = rs.release();
+    return GPUDIFF_OK;
+}
+
+}  // extern "C"
+
+int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rsr) {
+    ResultStore* rs = &rsr;
+    int rc;
     HIPCHK(hipEventSynchronize(d->done));
     uint32_t sum[8];
     HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
@@ -682,8 +712,6 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
         HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
         if (sum[4]) return GPUDIFF_E_CAPACITY;
     }
-    std::unique_ptr<ResultStore> rs(new (std::nothrow) ResultStore());
-    if (!rs) return GPUDIFF_E_NOMEM;
     try {
         rs->flags.resize(d->n_pairs);
         rs->spec.resize(sum[0]);
@@ -705,21 +733,10 @@ int gpudiff_wait(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_result* res) {
         HIPCHK(hipMemcpy(rs->hashes.data(), d->out_h, sum[5] * 8ull, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(rs->kinds.data(), d->out_k, sum[5], hipMemcpyDeviceToHost));
     }
-    res->n_pairs = d->n_pairs;
-    res->pair_flags = rs->flags.data();
-    res->n_spec_dirty = sum[0];
-    res->spec_dirty_ids = rs->spec.data();
-    res->n_status_dirty = sum[1];
-    res->status_dirty_ids = rs->status.data();
-    res->n_dirty = sum[2];
-    res->dirty_ids = rs->dirty.data();
-    res->path_offsets = rs->off.data();
-    res->n_paths = sum[5];
-    res->path_hashes = rs->hashes.data();
-    res->path_kinds = rs->kinds.data();
-    res->internal_ = rs.release();
     return GPUDIFF_OK;
 }
+
+extern "C" {
 
 void gpudiff_result_release(gpudiff_ctx* c, gpudiff_result* res) {
     (void)c;

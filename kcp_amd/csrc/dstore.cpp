@@ -1,0 +1,720 @@
+// Device-encode mode of the object store (gpudiff_store_create_ex with
+// GPUDIFF_STORE_DEVICE_ENCODE; include/gpudiff.h): the informer's events go
+// up as raw JSON and the GPU does the rest.
+//
+// submit (host work is a memcpy into pinned staging plus O(1) per event):
+//   1. documents: each event's new object, plus its old object when the slot
+//      has never been seen (the first sighting diffs against it); per slot a
+//      chain of the batch's documents (prev/next) so events on one slot apply
+//      in order;
+//   2. one H2D of the JSON and the document table;
+//   3. K0 (tokenize.hip) encodes every document into the current space; K0c
+//      checks each event against its old side for path-hash collisions; K0x
+//      walks the chains, writes the (old, new) rows and the slots' new resident
+//      blobs; then the ordinary diff pass (K2..K6).
+// Everything K0 does not take (a Go decode error, a float beyond its exact
+// conversion, an escaped key, a duplicate key or a collision, ...) is
+// deferred: its row is conservative in the device pass, the slot is marked
+// pending, and gpudiff_wait re-does those events on the host with the
+// Go-exact encoder (the same decisions store.cpp makes), places the blobs,
+// diffs them and patches the results -- so every result equals the host
+// store's, and later batches defer events of pending slots until then.
+//
+// Contract of this mode: event buffers stay valid until gpudiff_wait on the
+// ticket returns (deferred events are re-read), and batches are waited in
+// submit order, at most two in flight.
+#include "dstore.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "tokenize.h"
+
+using namespace gd;
+
+namespace {
+
+constexpr uint64_t kScratchCap = 2ull << 30;  // K0 working area, reused across launches
+
+struct Ring {
+    gpudiff_dbatch* d = nullptr;  // rows, pair_ids, results; pool = the store's current space
+    uint8_t* hjson = nullptr;     // pinned staging
+    uint64_t hjson_cap = 0;
+    uint8_t* hmeta = nullptr;     // pinned: TokDoc[] | DocLink[] | heads[]
+    uint64_t hmeta_cap = 0;
+    uint8_t* djson = nullptr;
+    uint64_t djson_cap = 0;
+    uint8_t* dmeta = nullptr;
+    uint64_t dmeta_cap = 0;
+    TokOut* douts = nullptr;
+    uint8_t* dcoll = nullptr;
+    uint8_t* ddef = nullptr;
+    uint64_t docs_cap = 0, coll_cap = 0, def_cap = 0;
+    uint32_t* dcnt = nullptr;     // deferred events of the batch
+    hipEvent_t staged = nullptr;  // its H2D copies finished (pinned buffers reusable)
+    std::vector<gpudiff_event> events;
+    uint32_t batch = 0, nev = 0;
+    uint64_t bound = 0;
+    gpudiff_ticket ticket = 0;
+    bool outstanding = false;
+};
+
+struct HF {
+    uint64_t h, fp;
+};
+
+bool no_collision(const std::vector<HF>& old, const std::vector<LeafRec>& nw) {
+    size_t i = 0, j = 0;
+    while (i < old.size() && j < nw.size()) {
+        if (old[i].h < nw[j].h) i++;
+        else if (old[i].h > nw[j].h) j++;
+        else {
+            if (old[i].fp != nw[j].fp) return false;
+            i++;
+            j++;
+        }
+    }
+    return true;
+}
+
+}  // namespace
+
+struct DStore {
+    gpudiff_ctx* c = nullptr;
+    uint32_t max_slots = 0, max_events = 0;
+    uint64_t space_bytes = 0;
+    uint8_t* space[2] = {nullptr, nullptr};
+    uint32_t cur = 0;
+    unsigned long long* used_dev = nullptr;
+    uint64_t used_ub = 0;  // host upper bound of *used_dev
+    DSlot* slots = nullptr;
+    uint32_t* ctr = nullptr;  // kCtrLive, kCtrLiveBytes
+    uint64_t* sizes = nullptr;
+    uint64_t* tile_sums = nullptr;
+    uint8_t* scratch = nullptr;
+    uint64_t scratch_cap = 0;
+    Ring ring[2];
+    uint32_t ring_next = 0;
+    uint32_t batch_seq = 0;
+    uint32_t next_wait = 1;  // batches are waited in submit order
+    std::vector<uint32_t> stamp;
+    std::vector<int32_t> last;
+    std::vector<uint8_t> seen;  // slot submitted before (its resident version may exist)
+    std::unordered_map<uint32_t, uint32_t> forgotten;  // slot -> batch_seq at forget
+    // resolution
+    std::unique_ptr<PairEncoder> enc;
+    gpudiff_dbatch* res_d = nullptr;
+    uint8_t* res_stage = nullptr;
+    uint64_t res_stage_cap = 0;
+    SlotUpdate* res_ups = nullptr;
+    uint64_t res_ups_cap = 0;
+    uint32_t* res_err = nullptr;
+    bool broken = false;
+    gpudiff_store_stats st{};
+    uint64_t deferred_total = 0;
+};
+
+namespace {
+
+int grow_pinned(uint8_t** p, uint64_t* cap, uint64_t need) {
+    if (need <= *cap) return GPUDIFF_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const uint64_t n = std::max<uint64_t>(need + need / 4, 1 << 16);
+    HIPCHK(hipHostMalloc((void**)p, n, hipHostMallocDefault));
+    *cap = n;
+    return GPUDIFF_OK;
+}
+
+template <class T>
+int grow_dev(T** p, uint64_t* cap, uint64_t need) {
+    if (need <= *cap) return GPUDIFF_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const uint64_t n = std::max<uint64_t>(need + need / 4, 256);
+    int rc = dalloc(p, n);
+    if (rc) return rc;
+    *cap = n;
+    return GPUDIFF_OK;
+}
+
+// packs the live blobs into the other space (stream-ordered), then reads the
+// exact append point back
+int compact(DStore* s) {
+    gpudiff_ctx* c = s->c;
+    HIPCHK(launch_compact_store(c->stream, s->slots, s->max_slots, s->space[s->cur], s->space[1 - s->cur], s->sizes,
+                                s->tile_sums, s->used_dev));
+    s->cur = 1 - s->cur;
+    uint64_t used = 0;
+    HIPCHK(hipMemcpyAsync(&used, s->used_dev, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    s->used_ub = used;
+    s->st.compactions++;
+    return GPUDIFF_OK;
+}
+
+int ensure_space(DStore* s, uint64_t bytes) {
+    if (s->used_ub + bytes <= s->space_bytes) return GPUDIFF_OK;
+    int rc = compact(s);
+    if (rc) return rc;
+    return s->used_ub + bytes <= s->space_bytes ? GPUDIFF_OK : GPUDIFF_E_CAPACITY;
+}
+
+// ------------------------------------------------------------------ host resolution
+struct HostSlot {
+    bool fetched = false;
+    bool live = false, has_status = false;
+    uint32_t seed = 0;
+    uint64_t off = 0;  // absolute, or kRelTag | offset in the resolution pool
+    uint32_t sl = 0, sar = 0, tl = 0, tar = 0, bytes = 0;
+    bool hf_loaded = false;
+    std::vector<HF> spec, stat;
+};
+
+int fetch_slot(DStore* s, uint32_t slot, HostSlot& H) {
+    DSlot d;
+    HIPCHK(hipMemcpy(&d, s->slots + slot, sizeof(DSlot), hipMemcpyDeviceToHost));
+    H.fetched = true;
+    H.live = d.flags & DS_LIVE;
+    H.has_status = d.flags & DS_HAS_STATUS;
+    H.seed = (d.flags >> 8) & 0xFF;
+    H.off = d.off;
+    H.sl = d.spec_l;
+    H.sar = d.spec_ar;
+    H.tl = d.stat_l;
+    H.tar = d.stat_ar;
+    H.bytes = d.bytes;
+    H.hf_loaded = false;
+    return GPUDIFF_OK;
+}
+
+// (pathHash, fingerprint) lists of a device-resident blob: its keys + trailer
+int load_hf(DStore* s, HostSlot& H) {
+    if (H.hf_loaded) return GPUDIFF_OK;
+    const uint64_t seg_s = gpudiff_seg_bytes(H.sl, H.sar), seg_t = gpudiff_seg_bytes(H.tl, H.tar);
+    std::vector<uint64_t> ks(H.sl), kt(H.tl), fp(H.sl + H.tl);
+    const uint8_t* b = s->space[s->cur] + H.off;
+    if (H.sl) HIPCHK(hipMemcpy(ks.data(), b, 8ull * H.sl, hipMemcpyDeviceToHost));
+    if (H.tl) HIPCHK(hipMemcpy(kt.data(), b + seg_s, 8ull * H.tl, hipMemcpyDeviceToHost));
+    if (H.sl + H.tl) HIPCHK(hipMemcpy(fp.data(), b + seg_s + seg_t, 8ull * (H.sl + H.tl), hipMemcpyDeviceToHost));
+    H.spec.resize(H.sl);
+    H.stat.resize(H.tl);
+    for (uint32_t i = 0; i < H.sl; i++) H.spec[i] = HF{ks[i], fp[i]};
+    for (uint32_t i = 0; i < H.tl; i++) H.stat[i] = HF{kt[i], fp[H.sl + i]};
+    H.hf_loaded = true;
+    return GPUDIFF_OK;
+}
+
+void set_hf(HostSlot& H, const FlatObject& o) {
+    H.spec.resize(o.spec.size());
+    for (size_t k = 0; k < o.spec.size(); k++) H.spec[k] = HF{o.spec[k].h, o.spec[k].fp};
+    H.stat.resize(o.stat.size());
+    for (size_t k = 0; k < o.stat.size(); k++) H.stat[k] = HF{o.stat[k].h, o.stat[k].fp};
+    H.hf_loaded = true;
+}
+
+// Re-does the batch's deferred events on the host (store.cpp's decisions),
+// diffs them on the device and patches rs.
+int resolve(DStore* s, Ring& R, ResultStore& rs) {
+    gpudiff_ctx* c = s->c;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<uint8_t> def(R.nev);
+    if (R.nev) HIPCHK(hipMemcpy(def.data(), R.ddef, R.nev, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> drows;
+    for (uint32_t i = 0; i < R.nev; i++)
+        if (def[i]) drows.push_back(i);
+    if (drows.empty()) return GPUDIFF_OK;
+    s->deferred_total += drows.size();
+    int rc;
+    PairEncoder& enc = *s->enc;
+    Arena arena_new, arena_old;
+    FlatObject fn, fo;
+    std::vector<uint8_t> pool;
+    std::vector<gpudiff_pair_row> rows(drows.size());
+    std::unordered_map<uint32_t, HostSlot> hs;
+    std::vector<uint32_t> touched;
+    for (size_t k = 0; k < drows.size(); k++) {
+        const gpudiff_event& e = R.events[drows[k]];
+        HostSlot& S = hs[e.slot];
+        if (!S.fetched) {
+            if ((rc = fetch_slot(s, e.slot, S))) return rc;
+            touched.push_back(e.slot);
+        }
+        gpudiff_pair_row& r = rows[k];
+        memset(&r, 0, sizeof(r));
+        r.pair_id = e.pair_id;
+        r.cluster_id = e.cluster_id;
+        auto conservative = [&]() { r.flags_a = r.flags_b = GPUDIFF_OBJ_DECODE_ERR; };
+        if (!enc.flatten_json(e.new_json, e.new_len, arena_new, fn)) {
+            conservative();
+            S.live = false;
+            S.hf_loaded = false;
+            continue;
+        }
+        bool ok = false, pair_error = false, a_live = false;
+        uint32_t seed = 0;
+        uint64_t a_off = 0;
+        uint32_t a_sl = 0, a_sar = 0, a_tl = 0, a_tar = 0, a_of = 0;
+        auto a_is_slot = [&]() {
+            a_live = true;
+            // the slot's blob as it is when k_place runs (a compaction may move it)
+            a_off = (S.off & kRelTag) ? S.off : (kSlotTag | e.slot);
+            a_sl = S.sl;
+            a_sar = S.sar;
+            a_tl = S.tl;
+            a_tar = S.tar;
+            a_of = S.has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
+        };
+        if (S.live && S.seed == 0) {
+            if ((rc = load_hf(s, S))) return rc;
+            if (enc.hash_single(fn, 0) && no_collision(S.spec, fn.spec) && no_collision(S.stat, fn.stat)) {
+                ok = true;
+                a_is_slot();
+            }
+        }
+        if (!ok && e.old_json) {
+            if (enc.flatten_json(e.old_json, e.old_len, arena_old, fo) && enc.pair_seed(fo, fn, &seed)) {
+                uint64_t off;
+                enc.write_object(fo, pool, &off, &a_sl, &a_sar, &a_tl, &a_tar);
+                a_live = true;
+                a_off = kRelTag | off;
+                a_of = fo.flags & GPUDIFF_OBJ_HAS_STATUS;
+                s->st.old_encoded++;
+                if (S.live) s->st.reseeded++;
+                ok = true;
+            } else {
+                pair_error = true;
+            }
+        } else if (!ok && S.live && S.seed) {
+            if ((rc = load_hf(s, S))) return rc;
+            if (enc.hash_single(fn, S.seed) && no_collision(S.spec, fn.spec) && no_collision(S.stat, fn.stat)) {
+                ok = true;
+                seed = S.seed;
+                a_is_slot();
+            } else {
+                pair_error = true;
+                s->st.collisions_unresolved++;
+            }
+        } else if (!ok && !S.live) {
+            for (seed = 0; seed <= 255 && !ok; seed++) ok = enc.hash_single(fn, seed);
+            seed--;
+            pair_error = !ok;
+        } else if (!ok) {
+            pair_error = true;
+            s->st.collisions_unresolved++;
+        }
+        if (pair_error) {
+            conservative();
+            bool self = false;
+            for (seed = 0; seed <= 255 && !self; seed++) self = enc.hash_single(fn, seed);
+            seed--;
+            if (!self) {
+                S.live = false;
+                S.hf_loaded = false;
+                continue;
+            }
+        }
+        uint64_t off;
+        uint32_t sl, sar, tl, tar, bytes;
+        enc.write_object_fp(fn, pool, &off, &sl, &sar, &tl, &tar, &bytes);
+        if (!pair_error) {
+            r.off_a = a_live ? a_off : 0;
+            r.spec_l_a = a_sl;
+            r.spec_ar_a = a_sar;
+            r.stat_l_a = a_tl;
+            r.stat_ar_a = a_tar;
+            r.flags_a = a_of | (seed << GPUDIFF_OBJ_SEED_SHIFT);
+            r.off_b = kRelTag | off;
+            r.spec_l_b = sl;
+            r.spec_ar_b = sar;
+            r.stat_l_b = tl;
+            r.stat_ar_b = tar;
+            r.flags_b = (fn.flags & GPUDIFF_OBJ_HAS_STATUS) | (seed << GPUDIFF_OBJ_SEED_SHIFT);
+        }
+        S.live = true;
+        S.seed = seed;
+        S.has_status = fn.flags & GPUDIFF_OBJ_HAS_STATUS;
+        S.off = kRelTag | off;
+        S.sl = sl;
+        S.sar = sar;
+        S.tl = tl;
+        S.tar = tar;
+        S.bytes = bytes;
+        set_hf(S, fn);
+    }
+    // slot states (forgotten-since slots keep their forget)
+    std::vector<SlotUpdate> ups;
+    for (uint32_t slot : touched) {
+        auto f = s->forgotten.find(slot);
+        if (f != s->forgotten.end() && f->second >= R.batch) continue;
+        const HostSlot& S = hs[slot];
+        SlotUpdate u{};
+        u.slot = slot;
+        u.batch = R.batch;
+        if (S.live) {
+            u.entry.off = S.off;
+            u.entry.spec_l = S.sl;
+            u.entry.spec_ar = S.sar;
+            u.entry.stat_l = S.tl;
+            u.entry.stat_ar = S.tar;
+            u.entry.bytes = S.bytes;
+            u.entry.flags = DS_LIVE | (S.has_status ? DS_HAS_STATUS : 0u) | (S.seed << 8);
+        } else {
+            s->seen[slot] = 0;  // the next event stages its old object again
+        }
+        ups.push_back(u);
+    }
+    // place: blobs behind the append point, rows, slot states
+    const uint64_t pbytes = (pool.size() + 15) & ~15ull;
+    pool.resize(pbytes, 0);
+    if ((rc = ensure_space(s, pbytes))) return rc;
+    if ((rc = grow_dev(&s->res_stage, &s->res_stage_cap, std::max<uint64_t>(pbytes, 16)))) return rc;
+    if ((rc = grow_dev(&s->res_ups, &s->res_ups_cap, std::max<size_t>(ups.size(), 1)))) return rc;
+    gpudiff_dbatch* d = s->res_d;
+    if (d->max_pairs < rows.size()) {
+        gpudiff_dbatch_free(c, d);
+        s->res_d = nullptr;
+        if ((rc = gpudiff_dbatch_create(c, 16, rows.size() + rows.size() / 2, &s->res_d))) return rc;
+        d = s->res_d;
+        (void)hipFree(d->pool);
+        d->pool = nullptr;
+        d->pool_borrowed = true;
+    }
+    if (pbytes) HIPCHK(hipMemcpy(s->res_stage, pool.data(), pbytes, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->rows, rows.data(), rows.size() * sizeof(gpudiff_pair_row), hipMemcpyHostToDevice));
+    if (!ups.empty()) HIPCHK(hipMemcpy(s->res_ups, ups.data(), ups.size() * sizeof(SlotUpdate), hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(s->res_err, 0, 4, c->stream));
+    HIPCHK(launch_place(c->stream, s->res_stage, pbytes, s->space[s->cur], s->used_dev, s->space_bytes, d->rows,
+                        d->pair_ids, (uint32_t)rows.size(), s->res_ups, (uint32_t)ups.size(), s->slots, s->ctr,
+                        s->res_err));
+    s->used_ub += pbytes;
+    d->pool = s->space[s->cur];
+    d->pool_cap = s->space_bytes;
+    d->n_pairs = rows.size();
+    gpudiff_ticket t2;
+    if ((rc = gpudiff_diff(c, d, &t2))) return rc;
+    ResultStore r2;
+    if ((rc = collect_results(c, d, r2))) return rc;
+    c->tickets.erase(t2);
+    d->ticket = 0;
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, s->res_err, 4, hipMemcpyDeviceToHost));
+    if (err) return GPUDIFF_E_CAPACITY;
+
+    // patch: deferred rows take r2's results, the rest keep rs's
+    ResultStore out;
+    out.flags.resize(R.nev);
+    out.off.push_back(0);
+    size_t jr = 0, j2 = 0, k = 0;
+    for (uint32_t i = 0; i < R.nev; i++) {
+        const bool d_in = (rs.flags[i] & (GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY)) != 0;
+        uint32_t lo = 0, hi = 0;
+        const ResultStore* src = &rs;
+        if (d_in) {
+            lo = rs.off[jr];
+            hi = rs.off[jr + 1];
+            jr++;
+        }
+        uint8_t f = rs.flags[i];
+        if (def[i]) {
+            f = r2.flags[k++];
+            src = &r2;
+            lo = hi = 0;
+            if (f & (GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY)) {
+                lo = r2.off[j2];
+                hi = r2.off[j2 + 1];
+                j2++;
+            }
+        }
+        out.flags[i] = f;
+        const uint32_t pid = R.events[i].pair_id;
+        if (f & GPUDIFF_SPEC_DIRTY) out.spec.push_back(pid);
+        if (f & GPUDIFF_STATUS_DIRTY) out.status.push_back(pid);
+        if (f & (GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY)) {
+            out.dirty.push_back(pid);
+            for (uint32_t q = lo; q < hi; q++) {
+                out.hashes.push_back(src->hashes[q]);
+                out.kinds.push_back(src->kinds[q]);
+            }
+            out.off.push_back((uint32_t)out.hashes.size());
+        }
+    }
+    rs = std::move(out);
+    return GPUDIFF_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ API
+DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events, int* rc_out) {
+    std::unique_ptr<DStore> s(new (std::nothrow) DStore());
+    int rc = GPUDIFF_E_NOMEM;
+    if (!s) {
+        *rc_out = rc;
+        return nullptr;
+    }
+    s->c = c;
+    s->max_slots = max_slots;
+    s->max_events = max_events;
+    s->space_bytes = (space_bytes + 15) & ~15ull;
+    auto fail = [&](int e) {
+        dstore_free(c, s.release());
+        *rc_out = e;
+        return (DStore*)nullptr;
+    };
+    try {
+        s->stamp.assign(max_slots, 0);
+        s->last.assign(max_slots, -1);
+        s->seen.assign(max_slots, 0);
+    } catch (const std::bad_alloc&) {
+        return fail(GPUDIFF_E_NOMEM);
+    }
+    EncodeConfig cfg = c->ecfg;
+    cfg.host_value_hash = true;  // resolved blobs carry their digests like K0's
+    s->enc.reset(new (std::nothrow) PairEncoder(cfg));
+    if (!s->enc) return fail(GPUDIFF_E_NOMEM);
+    for (auto& sp : s->space)
+        if ((rc = dalloc(&sp, s->space_bytes))) return fail(rc);
+    if ((rc = dalloc(&s->used_dev, 1)) || (rc = dalloc(&s->slots, max_slots)) || (rc = dalloc(&s->ctr, 4)) ||
+        (rc = dalloc(&s->sizes, max_slots)) || (rc = dalloc(&s->tile_sums, (max_slots + 1023) / 1024 + 1)) ||
+        (rc = dalloc(&s->res_err, 1)))
+        return fail(rc);
+    if (hipMemset(s->used_dev, 0, 8) != hipSuccess || hipMemset(s->slots, 0, sizeof(DSlot) * (size_t)max_slots) ||
+        hipMemset(s->ctr, 0, 16) != hipSuccess)
+        return fail(GPUDIFF_E_DEVICE);
+    for (Ring& R : s->ring) {
+        if ((rc = gpudiff_dbatch_create(c, 16, max_events, &R.d))) return fail(rc);
+        (void)hipFree(R.d->pool);
+        R.d->pool = nullptr;
+        R.d->pool_borrowed = true;
+        if ((rc = dalloc(&R.dcnt, 1))) return fail(rc);
+        if (hipEventCreateWithFlags(&R.staged, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+    }
+    if ((rc = gpudiff_dbatch_create(c, 16, 1024, &s->res_d))) return fail(rc);
+    (void)hipFree(s->res_d->pool);
+    s->res_d->pool = nullptr;
+    s->res_d->pool_borrowed = true;
+    s->st.max_slots = max_slots;
+    s->st.space_bytes = s->space_bytes;
+    *rc_out = GPUDIFF_OK;
+    return s.release();
+}
+
+int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, gpudiff_ticket* ticket) {
+    if (s->broken) return GPUDIFF_E_STATE;
+    if (n > s->max_events) return GPUDIFF_E_INVAL;
+    Ring& R = s->ring[s->ring_next];
+    if (R.outstanding) return GPUDIFF_E_STATE;  // wait on the batch two submits back first
+    int rc;
+    if (R.staged) HIPCHK(hipEventSynchronize(R.staged));
+    const uint32_t batch = ++s->batch_seq;
+
+    // 1. documents and slot chains
+    const uint64_t max_docs = 2 * (uint64_t)n;
+    const uint64_t meta_bytes = max_docs * (sizeof(TokDoc) + sizeof(DocLink)) + 4 * (uint64_t)n + 64;
+    if ((rc = grow_pinned(&R.hmeta, &R.hmeta_cap, meta_bytes))) return rc;
+    TokDoc* docs = (TokDoc*)R.hmeta;
+    DocLink* links = (DocLink*)(R.hmeta + max_docs * sizeof(TokDoc));
+    uint32_t* heads = (uint32_t*)(R.hmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
+    std::vector<const uint8_t*> src;
+    src.reserve(max_docs);
+    uint32_t nd = 0, nh = 0;
+    uint64_t jbytes = 0, bound = 0;
+    auto add_doc = [&](const uint8_t* p, size_t len, uint32_t slot, uint32_t row, const gpudiff_event& e) {
+        TokDoc& D = docs[nd];
+        memset(&D, 0, sizeof(D));
+        D.json_off = jbytes;
+        D.json_len = (uint32_t)len;
+        jbytes = (jbytes + len + kTokSlack + 15) & ~15ull;
+        bound += len + len / 2 + 64;  // typical blob <= JSON; K0 defers what does not fit (SPACE)
+        DocLink& L = links[nd];
+        memset(&L, 0, sizeof(L));
+        L.slot = slot;
+        L.row = row;
+        L.pair_id = e.pair_id;
+        L.cluster_id = e.cluster_id;
+        L.next = -1;
+        if (s->stamp[slot] == batch) {
+            L.prev = s->last[slot];
+            links[L.prev].next = (int32_t)nd;
+        } else {
+            L.prev = -1;
+            s->stamp[slot] = batch;
+            heads[nh++] = nd;
+        }
+        s->last[slot] = (int32_t)nd;
+        src.push_back(p);
+        nd++;
+    };
+    for (size_t i = 0; i < n; i++) {
+        const gpudiff_event& e = ev[i];
+        if (e.slot >= s->max_slots || !e.new_json || e.new_len > kTokMaxLen || e.old_len > kTokMaxLen)
+            return GPUDIFF_E_INVAL;
+        if (!s->seen[e.slot] && e.old_json) {  // first sighting: its old object is the old side
+            add_doc(e.old_json, e.old_len, e.slot, kNoRow, e);
+            s->st.old_encoded++;
+        }
+        s->seen[e.slot] = 1;
+        add_doc(e.new_json, e.new_len, e.slot, (uint32_t)i, e);
+    }
+    jbytes += kTokSlack;
+    if ((rc = grow_pinned(&R.hjson, &R.hjson_cap, jbytes))) return rc;
+    {  // JSON into pinned staging, split over the host threads by bytes
+        const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(1u, c->threads), std::max<uint64_t>(1, jbytes >> 22));
+        auto copy = [&](uint32_t t) {
+            const uint64_t b0 = jbytes * t / T, b1 = jbytes * (t + 1) / T;
+            for (uint32_t k = 0; k < nd; k++) {
+                const uint64_t o = docs[k].json_off;
+                if (o < b0 || o >= b1) continue;
+                const uint64_t end = k + 1 < nd ? docs[k + 1].json_off : jbytes;
+                memcpy(R.hjson + o, src[k], docs[k].json_len);
+                memset(R.hjson + o + docs[k].json_len, 0, end - o - docs[k].json_len);
+            }
+        };
+        if (T == 1) {
+            copy(0);
+        } else {
+            std::vector<std::thread> th;
+            for (uint32_t t = 0; t < T; t++) th.emplace_back(copy, t);
+            for (auto& x : th) x.join();
+        }
+        if (!nd) memset(R.hjson, 0, jbytes);
+    }
+    // K0 scratch: per-document areas within launches of at most kScratchCap
+    std::vector<std::pair<uint32_t, uint32_t>> launches;
+    {
+        uint64_t sb = 0;
+        uint32_t first = 0;
+        for (uint32_t k = 0; k < nd; k++) {
+            const uint64_t need = tok_scratch_bytes(docs[k].json_len);
+            if (sb && sb + need > std::max(kScratchCap, need)) {
+                launches.emplace_back(first, k);
+                first = k;
+                sb = 0;
+            }
+            docs[k].scratch_off = sb;
+            sb += need;
+            if ((rc = grow_dev(&s->scratch, &s->scratch_cap, sb))) return rc;
+        }
+        if (nd) launches.emplace_back(first, nd);
+    }
+    // 2. capacity (compaction is stream-ordered after every earlier batch)
+    if ((rc = ensure_space(s, bound))) return rc;
+    // 3. upload + kernels
+    if ((rc = grow_dev(&R.djson, &R.djson_cap, jbytes)) ||
+        (rc = grow_dev(&R.dmeta, &R.dmeta_cap, meta_bytes)) || (rc = grow_dev(&R.douts, &R.docs_cap, nd + 1)))
+        return rc;
+    if ((rc = grow_dev(&R.dcoll, &R.coll_cap, nd + 1)) || (rc = grow_dev(&R.ddef, &R.def_cap, n + 1))) return rc;
+    hipStream_t st = c->stream;
+    HIPCHK(hipMemcpyAsync(R.djson, R.hjson, jbytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, meta_bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(R.staged, st));
+    const TokDoc* ddocs = (const TokDoc*)R.dmeta;
+    const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
+    const uint32_t* dheads = (const uint32_t*)(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
+    uint8_t* space = s->space[s->cur];
+    for (auto& L : launches)
+        HIPCHK(launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
+                                  s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first));
+    HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
+    HIPCHK(hipMemsetAsync(R.dcnt, 0, 4, st));
+    gpudiff_dbatch* d = R.d;
+    HIPCHK(launch_link(st, dheads, nh, dlinks, R.douts, R.dcoll, s->slots, d->rows, d->pair_ids, R.ddef, batch,
+                       R.dcnt, s->ctr));
+    s->used_ub += bound;
+    // 4. the diff pass over the batch's rows
+    d->pool = space;
+    d->pool_cap = s->space_bytes;
+    d->pool_used = s->used_ub;
+    d->n_pairs = n;
+    d->leaves = 0;
+    d->compare_bytes = 0;
+    if ((rc = gpudiff_diff(c, d, ticket))) {
+        s->broken = true;
+        return rc;
+    }
+    R.events.assign(ev, ev + n);
+    R.batch = batch;
+    R.nev = (uint32_t)n;
+    R.bound = bound;
+    R.ticket = *ticket;
+    R.outstanding = true;
+    Ring* Rp = &R;
+    c->finishers[*ticket] = [s, Rp](ResultStore& rs) -> int {
+        Ring& RR = *Rp;
+        RR.outstanding = false;
+        if (RR.batch != s->next_wait) return GPUDIFF_E_STATE;  // waits follow submit order
+        s->next_wait++;
+        uint32_t ndef = 0;
+        uint64_t used = 0;
+        HIPCHK(hipMemcpy(&ndef, RR.dcnt, 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&used, s->used_dev, 8, hipMemcpyDeviceToHost));
+        // exact append point + what the other batch in flight may still add
+        const Ring& other = s->ring[(Rp - s->ring) ^ 1];
+        s->used_ub = std::max<uint64_t>(used, used + (other.outstanding ? other.bound : 0));
+        int r2 = ndef ? resolve(s, RR, rs) : GPUDIFF_OK;
+        if (r2) s->broken = true;
+        // forgets older than every outstanding batch are settled
+        for (auto it = s->forgotten.begin(); it != s->forgotten.end();)
+            it = it->second < s->next_wait ? s->forgotten.erase(it) : std::next(it);
+        return r2;
+    };
+    s->ring_next ^= 1u;
+    s->st.events += n;
+    s->st.last_batch_bytes = jbytes;
+    return GPUDIFF_OK;
+}
+
+int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot) {
+    HIPCHK(launch_forget(c->stream, s->slots, slot, s->ctr));
+    s->seen[slot] = 0;
+    s->forgotten[slot] = s->batch_seq;
+    return GPUDIFF_OK;
+}
+
+int dstore_stats(const DStore* s, gpudiff_store_stats* out) {
+    *out = s->st;
+    uint32_t ctr[4] = {0, 0, 0, 0};
+    uint64_t used = 0;
+    HIPCHK(hipSetDevice(s->c->device));
+    HIPCHK(hipStreamSynchronize(s->c->stream));
+    HIPCHK(hipMemcpy(ctr, s->ctr, 16, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&used, s->used_dev, 8, hipMemcpyDeviceToHost));
+    out->live_slots = ctr[kCtrLive];
+    uint64_t lb;
+    memcpy(&lb, ctr + kCtrLiveBytes, 8);
+    out->live_bytes = lb;
+    out->used_bytes = used;
+    out->deferred = s->deferred_total;
+    return GPUDIFF_OK;
+}
+
+void dstore_free(gpudiff_ctx* c, DStore* s) {
+    if (!s) return;
+    if (c && c->has_device) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    for (Ring& R : s->ring) {
+        if (R.d) gpudiff_dbatch_free(c, R.d);
+        if (R.ticket) c->finishers.erase(R.ticket);
+        for (void* p : {(void*)R.djson, (void*)R.dmeta, (void*)R.douts, (void*)R.dcoll, (void*)R.ddef, (void*)R.dcnt})
+            if (p) (void)hipFree(p);
+        for (void* p : {(void*)R.hjson, (void*)R.hmeta})
+            if (p) (void)hipHostFree(p);
+        if (R.staged) (void)hipEventDestroy(R.staged);
+    }
+    if (s->res_d) gpudiff_dbatch_free(c, s->res_d);
+    for (void* p : {(void*)s->space[0], (void*)s->space[1], (void*)s->used_dev, (void*)s->slots, (void*)s->ctr,
+                    (void*)s->sizes, (void*)s->tile_sums, (void*)s->scratch, (void*)s->res_stage, (void*)s->res_ups,
+                    (void*)s->res_err})
+        if (p) (void)hipFree(p);
+    delete s;
+}

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <array>
+#include <functional>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -121,6 +122,9 @@ struct gpudiff_ctx {
     hipEvent_t seg_ev[kMaxSegments] = {};
     hipEvent_t side_done = nullptr;
     hipEvent_t alt_start = nullptr;
+    // per-ticket completion hooks run by gpudiff_wait before results are
+    // published (the device-encode store resolves its host-deferred events)
+    std::unordered_map<gpudiff_ticket, std::function<int(ResultStore&)>> finishers;
     // submit ring
     gpudiff_dbatch* ring[2] = {nullptr, nullptr};
     gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
@@ -152,6 +156,9 @@ inline void dfree_all(gpudiff_dbatch* d) {
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);
 }
+
+// copies a finished diff pass's results to host memory (gpudiff_wait's body)
+int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rs);
 
 // bytes the decision kernel must read for this pair (DESIGN.md "Roofline")
 inline uint64_t pair_compare_bytes(const gpudiff_pair_row& r) {

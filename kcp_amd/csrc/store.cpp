@@ -28,6 +28,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "dstore.h"
 #include "engine.h"
 #include "xxh64.h"
 
@@ -92,6 +93,7 @@ uint32_t blob_bytes(uint32_t sl, uint32_t sar, uint32_t tl, uint32_t tar) {
 }  // namespace
 
 struct gpudiff_store {
+    DStore* dev = nullptr;  // device-encode mode (dstore.cpp)
     uint32_t max_slots = 0, max_events = 0;
     uint64_t space_bytes = 0;
     uint8_t* space[2] = {nullptr, nullptr};
@@ -294,10 +296,24 @@ extern "C" {
 
 int gpudiff_store_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,
                          gpudiff_store** out) {
+    return gpudiff_store_create_ex(c, max_slots, space_bytes, max_events, 0, out);
+}
+
+int gpudiff_store_create_ex(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,
+                            uint32_t flags, gpudiff_store** out) {
     if (!c || !out || !max_slots || !max_events || space_bytes < 4096) return GPUDIFF_E_INVAL;
+    if (flags & ~GPUDIFF_STORE_DEVICE_ENCODE) return GPUDIFF_E_INVAL;
     *out = nullptr;
     int rc = set_device(c);
     if (rc) return rc;
+    if (flags & GPUDIFF_STORE_DEVICE_ENCODE) {
+        std::unique_ptr<gpudiff_store> s(new (std::nothrow) gpudiff_store());
+        if (!s) return GPUDIFF_E_NOMEM;
+        s->dev = dstore_create(c, max_slots, space_bytes, max_events, &rc);
+        if (!s->dev) return rc;
+        *out = s.release();
+        return GPUDIFF_OK;
+    }
     std::unique_ptr<gpudiff_store> s(new (std::nothrow) gpudiff_store());
     if (!s) return GPUDIFF_E_NOMEM;
     try {
@@ -334,10 +350,12 @@ int gpudiff_store_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_byte
 }
 
 int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* ev, size_t n, gpudiff_ticket* ticket) {
-    if (!c || !s || (n && !ev) || n > s->max_events) return GPUDIFF_E_INVAL;
-    if (s->broken) return GPUDIFF_E_STATE;
+    if (!c || !s || (n && !ev)) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
+    if (s->dev) return dstore_submit(c, s->dev, ev, n, ticket);
+    if (n > s->max_events) return GPUDIFF_E_INVAL;
+    if (s->broken) return GPUDIFF_E_STATE;
     for (size_t i = 0; i < n; i++)
         if (ev[i].slot >= s->max_slots || !ev[i].new_json) return GPUDIFF_E_INVAL;
     const uint32_t slot_ring = s->ring_next;
@@ -453,7 +471,13 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
 }
 
 int gpudiff_store_forget(gpudiff_ctx* c, gpudiff_store* s, uint32_t slot) {
-    if (!c || !s || slot >= s->max_slots) return GPUDIFF_E_INVAL;
+    if (!c || !s) return GPUDIFF_E_INVAL;
+    if (s->dev) {
+        int rc = set_device(c);
+        if (rc) return rc;
+        return dstore_forget(c, s->dev, slot);
+    }
+    if (slot >= s->max_slots) return GPUDIFF_E_INVAL;
     Slot& S = s->slots[slot];
     if (S.live) {
         s->st.live_slots--;
@@ -470,6 +494,7 @@ int gpudiff_store_forget(gpudiff_ctx* c, gpudiff_store* s, uint32_t slot) {
 
 int gpudiff_store_stats_get(const gpudiff_store* s, gpudiff_store_stats* out) {
     if (!s || !out) return GPUDIFF_E_INVAL;
+    if (s->dev) return dstore_stats(s->dev, out);
     *out = s->st;
     out->used_bytes = s->used;
     return GPUDIFF_OK;
@@ -477,6 +502,11 @@ int gpudiff_store_stats_get(const gpudiff_store* s, gpudiff_store_stats* out) {
 
 void gpudiff_store_free(gpudiff_ctx* c, gpudiff_store* s) {
     if (!s) return;
+    if (s->dev) {
+        dstore_free(c, s->dev);
+        delete s;
+        return;
+    }
     if (c && c->has_device) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);

@@ -72,9 +72,65 @@ __host__ __device__ inline uint64_t tok_blob_bound(uint32_t len) { return 14ull 
 constexpr uint32_t kTokMaxLen = (1u << 24) - 64u;  // token words hold 24-bit positions
 constexpr uint32_t kTokSlack = 32u;                 // readable bytes K0 needs after each staged document
 
+// ------------------------------------------------------------ device object store
+// One slot per informer-cache object: its resident blob (K0 format, with the
+// fingerprint trailer) in the current space.
+struct DSlot {
+    uint64_t off;
+    uint32_t spec_l, spec_ar, stat_l, stat_ar;
+    uint32_t bytes;   // blob + trailer
+    uint32_t flags;   // DS_* | seed << 8
+    uint32_t pend;    // last batch that deferred an event of this slot to the host
+    uint32_t pad;
+};
+static_assert(sizeof(DSlot) == 40, "DSlot");
+constexpr uint32_t DS_LIVE = 1u, DS_HAS_STATUS = 2u, DS_PENDING = 4u;
+
+// Per staged document of a store batch: its slot chain inside the batch.
+struct DocLink {
+    uint32_t slot;
+    int32_t prev;       // previous document of the slot in this batch, -1
+    int32_t next;       // next one, -1
+    uint32_t row;       // result row (event index); kNoRow for an old_json first-sighting document
+    uint32_t pair_id, cluster_id;
+    uint32_t pad[2];
+};
+static_assert(sizeof(DocLink) == 32, "DocLink");
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+
+// counters[] of a store (device): 1 live slots, 2-3 live bytes (u64)
+constexpr uint32_t kCtrLive = 1, kCtrLiveBytes = 2;
+
+// host-resolved state of one slot (kernel k_place applies it)
+struct SlotUpdate {
+    DSlot entry;        // off tagged with kRelTag = relative to the placed bytes
+    uint32_t slot;
+    uint32_t batch;     // the batch whose deferred events produced it
+};
+constexpr uint64_t kRelTag = 1ull << 63;   // offset relative to the placed bytes
+constexpr uint64_t kSlotTag = 1ull << 62;  // the resident blob of slot (off & 0xFFFFFFFF)
+
 // K0 over docs [0, n): blobs appended to space at atomic offsets (*used).
+// slots/links (optional): the seed is the slot's (DSlot.flags >> 8).
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
-                              TokOut* out);
+                              TokOut* out, const DSlot* slots = nullptr, const DocLink* links = nullptr);
+// K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)
+hipError_t launch_collide(hipStream_t s, const DocLink* links, const TokOut* outs, const DSlot* slots, uint32_t n,
+                          const uint8_t* space, uint8_t* coll);
+// K0x: walk each slot's chain: rows for K2, deferrals, the slot's new resident blob
+hipError_t launch_link(hipStream_t s, const uint32_t* heads, uint32_t n_heads, const DocLink* links,
+                       const TokOut* outs, const uint8_t* coll, DSlot* slots, gpudiff_pair_row* rows,
+                       uint32_t* pair_ids, uint8_t* deferred, uint32_t batch, uint32_t* n_deferred,
+                       uint32_t* counters);
+// compaction: pack every live slot's blob into dst, rewrite the offsets, *used = total
+hipError_t launch_compact_store(hipStream_t s, DSlot* slots, uint32_t n, const uint8_t* src, uint8_t* dst,
+                                uint64_t* sizes, uint64_t* block_sums, unsigned long long* used);
+// place host-resolved blobs, rows and slot states
+hipError_t launch_place(hipStream_t s, const uint8_t* stage, uint64_t bytes, uint8_t* space,
+                        unsigned long long* used, uint64_t cap, gpudiff_pair_row* rows, uint32_t* pair_ids,
+                        uint32_t n_rows, const SlotUpdate* ups, uint32_t n_ups, DSlot* slots, uint32_t* counters,
+                        uint32_t* err);
+hipError_t launch_forget(hipStream_t s, DSlot* slots, uint32_t slot, uint32_t* counters);
 
 }  // namespace gd

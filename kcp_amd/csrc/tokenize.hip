@@ -403,7 +403,8 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                                                      const uint8_t* __restrict__ json, uint8_t* __restrict__ scratch,
                                                      uint8_t* __restrict__ space, uint64_t space_cap,
                                                      unsigned long long* __restrict__ used, uint64_t mask,
-                                                     TokOut* __restrict__ out) {
+                                                     TokOut* __restrict__ out, const DSlot* __restrict__ slots,
+                                                     const DocLink* __restrict__ links) {
     __shared__ uint32_t s_stk_node[kWavesPerBlock][kMaxDepth + 1];
     __shared__ uint32_t s_stk_meta[kWavesPerBlock][kMaxDepth + 1];
     __shared__ uint32_t s_hist[kWavesPerBlock][kMaxDepth + 1];
@@ -700,7 +701,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     }
     wave_sync();
 
-    const uint64_t seed = D.seed;
+    const uint64_t seed = slots ? ((slots[links[doc_i].slot].flags >> 8) & 0xFFu) : D.seed;
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
         uint32_t err = GPUDIFF_TOK_OK;
@@ -947,10 +948,11 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
 
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
-                              TokOut* out) {
+                              TokOut* out, const DSlot* slots, const DocLink* links) {
     if (!n) return hipSuccess;
     const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    k_encode_docs<<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask, out);
+    k_encode_docs<<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask, out,
+                                                         slots, links);
     return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
 OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_FRESH, OBJ_SEED_SHIFT = 0x1, 0x2, 0x4, 8
+STORE_DEVICE_ENCODE = 0x1
 EXPORT_COUNTS, EXPORT_SPEC_IDS, EXPORT_STATUS_IDS, EXPORT_DIRTY_IDS, EXPORT_FLAGS = range(5)
 
 
@@ -72,7 +73,7 @@ class StoreStats(C.Structure):
     _fields_ = [("max_slots", C.c_uint64), ("live_slots", C.c_uint64), ("space_bytes", C.c_uint64),
                 ("used_bytes", C.c_uint64), ("live_bytes", C.c_uint64), ("compactions", C.c_uint64),
                 ("events", C.c_uint64), ("old_encoded", C.c_uint64), ("reseeded", C.c_uint64),
-                ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64)]
+                ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64), ("deferred", C.c_uint64)]
 
 
 class ObjInfo(C.Structure):
@@ -147,6 +148,7 @@ SIGNATURES = [
                                         C.POINTER(_P)]),
     ("gpudiff_submit", C.c_int, [_P, C.POINTER(JsonPair), C.c_size_t, C.POINTER(C.c_uint64)]),
     ("gpudiff_store_create", C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint32, C.POINTER(_P)]),
+    ("gpudiff_store_create_ex", C.c_int, [_P, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     ("gpudiff_store_submit", C.c_int, [_P, _P, C.POINTER(Event), C.c_size_t, C.POINTER(C.c_uint64)]),
     ("gpudiff_store_forget", C.c_int, [_P, _P, C.c_uint32]),
     ("gpudiff_store_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
@@ -307,11 +309,14 @@ class ObjectStore:
     diffs each event's new object against its slot's resident version and
     makes it resident; results come back through Engine.wait(ticket)."""
 
-    def __init__(self, engine: "Engine", max_slots: int, space_bytes: int, max_events: int):
+    def __init__(self, engine: "Engine", max_slots: int, space_bytes: int, max_events: int,
+                 device_encode: bool = False):
         self.engine = engine
+        self.device_encode = device_encode
         h = C.c_void_p()
-        _chk(_lib.gpudiff_store_create(engine.ctx, max_slots, space_bytes, max_events, C.byref(h)),
-             "gpudiff_store_create")
+        _chk(_lib.gpudiff_store_create_ex(engine.ctx, max_slots, space_bytes, max_events,
+                                          STORE_DEVICE_ENCODE if device_encode else 0, C.byref(h)),
+             "gpudiff_store_create_ex")
         self.h = h
         self._keep = [None, None]  # inputs of the (at most two) submits in flight
         self._k = 0
@@ -468,8 +473,9 @@ class Engine:
     def diff_pairs(self, pairs, ids=None, clusters=None) -> DiffResult:
         return self.wait(self.submit(pairs, ids, clusters))
 
-    def object_store(self, max_slots: int, space_bytes: int, max_events: int) -> ObjectStore:
-        return ObjectStore(self, max_slots, space_bytes, max_events)
+    def object_store(self, max_slots: int, space_bytes: int, max_events: int,
+                     device_encode: bool = False) -> ObjectStore:
+        return ObjectStore(self, max_slots, space_bytes, max_events, device_encode)
 
     # ---- object encoding (device-store format: blob + fingerprint trailer)
     def encode_objects(self, docs, seeds=None, out_cap: int = 0):

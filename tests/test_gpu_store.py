@@ -4,7 +4,9 @@ oracle's diff_pair(previous version, new version) -- previous = the empty
 object {} on a first sighting without an old object -- including chained
 events on one slot inside a batch, forced path-hash collisions (8-bit
 hashes: re-seeds through old_json), compactions of the two spaces, Delete
-events (forget) and undecodable new objects."""
+events (forget) and undecodable new objects.  Every test runs in both modes:
+host encoding, and device encoding (raw JSON up, kernel K0 encodes, the host
+re-does only the events K0 defers)."""
 import copy
 import json
 import random
@@ -17,6 +19,8 @@ from tests.parity import assert_matches
 from tests.workload import _noise, configmap, crd, deployment, mutate
 
 pytestmark = pytest.mark.gpu
+
+MODES = pytest.mark.parametrize("dev", [False, True], ids=["host_encode", "device_encode"])
 
 
 def _obj(rnd, i):
@@ -75,12 +79,13 @@ def _run(eng, st, stream, drop_old=False):
         assert_matches(res, pairs, hash_bits=eng.path_hash_bits)
 
 
+@MODES
 @pytest.mark.parametrize("drop_old", [False, True])
-def test_replay_matches_oracle(drop_old):
+def test_replay_matches_oracle(drop_old, dev):
     """Events on 60 slots, 6 batches of 150 (many slots get several events
     per batch: they chain)."""
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=60, space_bytes=64 << 20, max_events=256)
+    st = e.object_store(max_slots=60, space_bytes=64 << 20, max_events=256, device_encode=dev)
     _run(e, st, _stream(1, 60, 6, 150), drop_old)
     s = st.stats()
     assert s.events == 900 and s.live_slots == 60 and s.collisions_unresolved == 0
@@ -88,11 +93,12 @@ def test_replay_matches_oracle(drop_old):
     e.close()
 
 
-def test_compaction_keeps_results_exact():
+@MODES
+def test_compaction_keeps_results_exact(dev):
     """A space of 512 KiB forces compactions while batches still read blobs of
     the previous versions."""
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=40, space_bytes=512 << 10, max_events=128)
+    st = e.object_store(max_slots=40, space_bytes=512 << 10, max_events=128, device_encode=dev)
     _run(e, st, _stream(2, 40, 12, 60))
     s = st.stats()
     assert s.compactions >= 3, s.compactions
@@ -101,9 +107,10 @@ def test_compaction_keeps_results_exact():
     e.close()
 
 
-def test_forced_collisions_reseed_through_old_json():
+@MODES
+def test_forced_collisions_reseed_through_old_json(dev):
     e = G.Engine(device=0, encode_threads=2, path_hash_bits=8)
-    st = e.object_store(max_slots=30, space_bytes=64 << 20, max_events=128)
+    st = e.object_store(max_slots=30, space_bytes=64 << 20, max_events=128, device_encode=dev)
     _run(e, st, _stream(3, 30, 5, 80))
     s = st.stats()
     assert s.reseeded > 0 and s.collisions_unresolved == 0
@@ -111,9 +118,10 @@ def test_forced_collisions_reseed_through_old_json():
     e.close()
 
 
-def test_forget_and_decode_error():
+@MODES
+def test_forget_and_decode_error(dev):
     e = G.Engine(device=0, encode_threads=1)
-    st = e.object_store(max_slots=4, space_bytes=1 << 20, max_events=16)
+    st = e.object_store(max_slots=4, space_bytes=1 << 20, max_events=16, device_encode=dev)
     rnd = random.Random(4)
     a = deployment(rnd, 0, 0)
     aj = json.dumps(a).encode()
@@ -139,9 +147,10 @@ def test_forget_and_decode_error():
     e.close()
 
 
-def test_two_submits_in_flight():
+@MODES
+def test_two_submits_in_flight(dev):
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=50, space_bytes=32 << 20, max_events=200)
+    st = e.object_store(max_slots=50, space_bytes=32 << 20, max_events=200, device_encode=dev)
     stream = _stream(5, 50, 4, 120)
     tickets = []
     for k, (evs, pairs) in enumerate(stream):
@@ -152,3 +161,60 @@ def test_two_submits_in_flight():
     assert_matches(e.wait(tickets[-1]), stream[-1][1])
     st.free()
     e.close()
+
+
+_IRREGULAR = [
+    b',"zz":1,"zz":2}',                      # duplicate key (last wins): K0 defers (HASH)
+    b',"k\\u0065y":"v"}',                   # escaped key: K0 defers (KEY)
+    b',"bad":"\xff\xfe x"}',                 # invalid UTF-8 (U+FFFD repair): K0 defers (STRING)
+    b',"big":123456789012345678901234567}',  # > 19 significant digits: K0 defers (NUMBER)
+    b',"f":0.30886104750414978,"g":-1.5e-7}',  # floats K0 converts itself (Eisel-Lemire)
+    b',"spec":',                             # Go decode error (truncated)
+]
+
+
+def _raw_stream(seed, n_slots, n_batches, per_batch):
+    """Like _stream, but ~1 in 6 new versions gets an irregular tail spliced
+    into its JSON bytes; the next event's old object is those exact bytes."""
+    rnd = random.Random(seed)
+    cur, cur_b = {}, {}
+    out = []
+    for _b in range(n_batches):
+        evs, pairs = [], []
+        for _ in range(per_batch):
+            s = rnd.randrange(n_slots)
+            old = cur.get(s)
+            new = _obj(rnd, s) if old is None else _next_version(rnd, old)
+            nj = json.dumps(new, separators=(",", ":")).encode()
+            if rnd.random() < 0.17:
+                nj = nj[:-1] + rnd.choice(_IRREGULAR)
+            oj = cur_b.get(s)
+            # without old objects, a slot emptied by an undecodable version diffs against {}
+            prev_bad = oj is not None and oj.endswith(b',"spec":')
+            evs.append((s, nj, oj))
+            pairs.append((oj if oj is not None else b"{}", nj, b"{}" if (oj is None or prev_bad) else oj))
+            cur[s] = new
+            cur_b[s] = nj
+        out.append((evs, pairs))
+    return out
+
+
+@pytest.mark.parametrize("drop_old", [False, True])
+def test_device_encode_deferrals_exact(drop_old):
+    """Host encoding and device encoding on the same stream with irregular
+    objects spliced in: both bit-exact with the oracle, and the device mode
+    really deferred events to the host."""
+    stream = _raw_stream(11, 40, 6, 120)
+    for dev in (False, True):
+        e = G.Engine(device=0, encode_threads=4)
+        st = e.object_store(max_slots=40, space_bytes=32 << 20, max_events=256, device_encode=dev)
+        for evs, pairs in stream:
+            items = [(s, nj, None if drop_old else oj, i, s % 5) for i, (s, nj, oj) in enumerate(evs)]
+            res = e.wait(st.submit(items))
+            pairs = [(p[2] if drop_old else p[0], p[1]) for p in pairs]
+            assert_matches(res, pairs)
+        s = st.stats()
+        if dev:
+            assert s.deferred > 0
+        st.free()
+        e.close()

@@ -92,7 +92,7 @@ EDGE_OK = [
     b'{"spec":{"u":"\\u00e9\\u20ac\\ud83d\\ude00 \\ud800 x \\udc00"}}',
     '{"spec":{"utf":"héllo wörld ✓ 日本語 \U0001F600"}}'.encode(),
     b'{"spec":{"n":[0,-0,1,-1,9223372036854775807,-9223372036854775808,1.5,-0.0,0.0,1e3,1E-5,0.1,2.5e+2,'
-    b'123456789.123,1e22,1e-22,9007199254740992,4.9e-1,100000000000000000000.0,1e23,1.7976931348623157e308,'
+    b'123456789.123,1e22,1e-22,9007199254740992,4.9e-1,100000000000000000000.0,1.7976931348623157e308,'
     b'9223372036854775808,-9223372036854775809,0.30886104750414978,2.2250738585072014e-308,'
     b'0.1e-300,123456789012345678e-5,7.0e0,-1.5E+10]}}',
     b'{"spec":{"t":true,"f":false,"z":null,"a":[true,false,null]}}',
@@ -111,6 +111,7 @@ EDGE_OK = [
 ]
 # (doc, K0 status, host decides Go error?)
 EDGE_DEFER = [
+    (b'{"spec":{"f":1e23}}', G.TOK_NUMBER),  # Eisel-Lemire cannot decide it: strconv's slow path
     (b'{"spec":{"f":5e-324}}', G.TOK_NUMBER), (b'{"spec":{"f":2.2250738585072011e-308}}', G.TOK_NUMBER),
     (b'{"spec":{"i":123456789012345678901}}', G.TOK_NUMBER), (b'{"i":18446744073709551615}', G.TOK_NUMBER),
     (b'{"spec":{"f":1e400}}', G.TOK_NUMBER), (b'{"spec":{"f":0.12345678901234567890123}}', G.TOK_NUMBER),
