@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="config5: events per batch")
     ap.add_argument("--batches", type=int, default=40, help="config5: timed batches")
     ap.add_argument("--warmup-batches", type=int, default=4, help="config5: untimed batches")
+    ap.add_argument("--encode", default="device", choices=["device", "host"],
+                    help="config5: encode events on the GPU (K0, raw JSON up) or on the host")
     ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")
     ap.add_argument("--clusters", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=262144)

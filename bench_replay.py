@@ -19,7 +19,10 @@ call -> results on the host), H2D GB/s, the GPU time per batch, and checks:
 every timed event's decisions against the generator's ground truth and a
 sample bit-exact against the oracle (flags and changed paths).
 
-usage: python bench.py --config config5 [--pairs M] [--batch B] [--seconds S]
+With --encode device (the default) the events go up as raw JSON and kernel K0
+encodes them in HBM; --encode host is the host-encoder mode.
+
+usage: python bench.py --config config5 [--pairs M] [--batch B] [--encode device|host]
 """
 import json
 import os
@@ -70,8 +73,10 @@ def run(args):
     eng = G.Engine(device=0, encode_threads=threads, timing=True)
     per_obj = float(lens.mean()) * 1.3 + 256
     space = int(per_obj * M * 2.5) + (B * int(per_obj) * 4) + (256 << 20)
-    st = eng.object_store(M, space, B)
-    log("store: %d slots, 2 x %.2f GB spaces, batches of %d events, %d host threads" % (M, space / 1e9, B, threads))
+    dev_enc = args.encode == "device"
+    st = eng.object_store(M, space, B, device_encode=dev_enc)
+    log("store: %d slots, 2 x %.2f GB spaces, batches of %d events, %d host threads, %s encoding" % (
+        M, space / 1e9, B, threads, args.encode))
 
     def events(slots, new_is_b, with_old=True):
         ev = np.zeros(slots.size, dtype=EVENT_DTYPE)
@@ -133,7 +138,8 @@ def run(args):
         ts = time.time()
         tk = submit(ev)
         if k >= args.warmup_batches:
-            bytes_up += st.stats().last_batch_bytes
+            # device encoding uploads the events' JSON; host encoding the encoded blobs
+            bytes_up += int(ev["new_len"].sum()) if dev_enc else st.stats().last_batch_bytes
         inflight.append((tk, ts, k))
         if len(inflight) == 2:
             tk0, ts0, k0 = inflight.pop(0)
@@ -199,13 +205,14 @@ def run(args):
         "dtype": "u8",
         "data": "synthetic (config3 object mix; each event alternates an object's two seeded versions)",
         "config": {"workload": "config5: %d resident objects, batches of %d events, 2 in flight" % (M, B),
-                   "host_encode_threads": threads},
+                   "encode": "device (K0 JSON tokenizer/encoder in HBM)" if dev_enc else "host (%d threads)" % threads,
+                   "host_threads": threads},
         "latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p99": float(np.percentile(lat_ms, 99)),
                        "max": float(lat_ms.max())},
         "h2d_gbps": bytes_up / el / 1e9,
         "gpu_ms_per_batch": {"diff_pass": tm.total_ms, "k2": tm.compare_ms},
         "store": {"resident_gb": ss.live_bytes / 1e9, "compactions": ss.compactions, "reseeded": ss.reseeded,
-                  "old_objects_encoded": ss.old_encoded},
+                  "old_objects_encoded": ss.old_encoded, "deferred_to_host": ss.deferred},
         "initial_list_objects_per_s": M / t_load,
         "checks": {"events_checked": checked, "decision_mismatches_vs_ground_truth": mism,
                    "sample_bit_exact_vs_oracle": sample_ok},

@@ -313,6 +313,10 @@ int gpudiff_encode_objects(gpudiff_ctx* ctx, const uint8_t* const* docs, const s
                            size_t n, uint8_t* out, uint64_t out_cap, gpudiff_obj_info* info);
 int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, uint32_t path_hash_bits, uint8_t* out,
                                uint64_t out_cap, gpudiff_obj_info* info);
+/* tuning: K0 per-phase wall-clock ticks (100 MHz, summed over waves) since the
+ * previous call (scan, tree, values, hashes, sort, blob, -, -); enable != 0
+ * keeps recording */
+int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
 
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,

@@ -111,4 +111,13 @@ int gpudiff_encode_objects(gpudiff_ctx* c, const uint8_t* const* docs, const siz
     return GPUDIFF_OK;
 }
 
+int gpudiff_k0_profile(gpudiff_ctx* c, int enable, uint64_t* ticks8) {
+    if (!c) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(k0_profile(enable, ticks8));
+    return GPUDIFF_OK;
+}
+
 }  // extern "C"

@@ -110,6 +110,10 @@ struct SlotUpdate {
 constexpr uint64_t kRelTag = 1ull << 63;   // offset relative to the placed bytes
 constexpr uint64_t kSlotTag = 1ull << 62;  // the resident blob of slot (off & 0xFFFFFFFF)
 
+// tuning: per-phase wall-clock ticks (100 MHz) of K0 summed over waves since the
+// last call; enable = record from now on
+hipError_t k0_profile(int enable, uint64_t* out8);
+
 // K0 over docs [0, n): blobs appended to space at atomic offsets (*used).
 // slots/links (optional): the seed is the slot's (DSlot.flags >> 8).
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,

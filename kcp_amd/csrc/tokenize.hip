@@ -39,6 +39,8 @@ namespace {
 
 constexpr uint32_t TK_CLOSEQ = 0x01u;     // token code of a closing quote
 constexpr uint32_t TK_OPENQ_SLOW = 0x02u; // opening quote of a string that needs decoding
+// opening quotes of the exact strings "metadata", "status", "labels", "annotations"
+constexpr uint32_t TK_KEY_META = 0x03u, TK_KEY_STATUS = 0x04u, TK_KEY_LABELS = 0x05u, TK_KEY_ANNOT = 0x06u;
 constexpr uint32_t POS_MASK = 0xFFFFFFu;
 
 // node info word
@@ -57,6 +59,8 @@ enum : uint32_t { E_ROOT, E_KEY, E_KEYCLOSE, E_COLON, E_VALUE, E_STRCLOSE, E_NEX
 
 constexpr uint32_t kMaxDepth = 255;
 constexpr uint32_t kWavesPerBlock = 4;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
@@ -383,21 +387,11 @@ struct Scratch {
     uint8_t* str;
 };
 
-// 8-byte constants of the region keys
-constexpr uint64_t KW_METADATA = 0x617461646174656dull;   // "metadata"
-constexpr uint64_t KW_STATUS = 0x737574617473ull;         // "status"
-constexpr uint64_t KW_LABELS = 0x736c6562616cull;         // "labels"
-constexpr uint64_t KW_ANNOT8 = 0x697461746f6e6e61ull;     // "annotati"
-constexpr uint64_t KW_ANNOT3 = 0x736e6full;               // "ons"
-
-__device__ __forceinline__ bool key_is(const uint8_t* k, uint32_t klen, uint64_t w, uint32_t n) {
-    return klen == n && (ld8u(k) & (n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull))) == w;
-}
-__device__ __forceinline__ bool key_is_annotations(const uint8_t* k, uint32_t klen) {
-    return klen == 11 && ld8u(k) == KW_ANNOT8 && (ld8u(k + 8) & 0xFFFFFFull) == KW_ANNOT3;
-}
-
 }  // namespace
+
+// tuning hook (gpudiff_k0_profile): per-phase wall-clock ticks summed over waves
+__device__ unsigned long long g_k0_prof[8];
+__device__ int g_k0_prof_on;
 
 __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ docs, uint32_t n_docs,
                                                      const uint8_t* __restrict__ json, uint8_t* __restrict__ scratch,
@@ -409,6 +403,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     __shared__ uint32_t s_stk_meta[kWavesPerBlock][kMaxDepth + 1];
     __shared__ uint32_t s_hist[kWavesPerBlock][kMaxDepth + 1];
     __shared__ uint32_t s_cur[kWavesPerBlock][kMaxDepth + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_ring[kWavesPerBlock][2048];
 
     const uint32_t lane = lane_id();
     const uint32_t wib = threadIdx.x >> 6;
@@ -446,88 +441,155 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     const uint32_t ncap = node_cap(len);
     uint32_t status = GPUDIFF_TOK_OK;
 
+    const bool prof = g_k0_prof_on != 0;
+    uint64_t t_prev = prof ? wall_clock64() : 0;
+    auto mark = [&](int ph) {
+        if (prof) {
+            const uint64_t t = wall_clock64();
+            if (lane == 0) atomicAdd(&g_k0_prof[ph], (unsigned long long)(t - t_prev));
+            t_prev = t;
+        }
+    };
     // ------------------------------------------------------------ phase 1: structural scan
+    // The document streams through a 2 x 1 KiB LDS ring (one 16-B load per
+    // lane per KiB, the next KiB staged before the current one is scanned, so
+    // an opening quote can look 12 bytes ahead for the region keywords).
+    uint8_t* ring = s_ring[wib];
     uint32_t ntok = 0;
     uint64_t esc_carry = 0, str_carry = 0, atom_carry = 0;
     uint32_t last_open_idx = NONE, last_open_pos = 0, last_marked = NONE;
     bool ctl_in_string = false;
-    for (uint32_t b = 0; b < len; b += 64) {
-        const uint32_t pos = b + lane;
-        const uint32_t c = pos < len ? d[pos] : 0x20u;
-        const uint64_t bs = ballot(c == '\\');
-        const uint64_t qt = ballot(c == '"');
-        const uint64_t st = ballot(c == '{' || c == '}' || c == '[' || c == ']' || c == ':' || c == ',');
-        const uint64_t wsm = ballot(is_ws(c));
-        const uint64_t ctl = ballot(c < 0x20u);  // inside a string every control byte is an error
-        const uint64_t hi = ballot(c >= 0x80u);
-        // escaped characters: an unescaped backslash escapes the next byte
-        uint64_t esc = esc_carry;
-        esc_carry = 0;
-        for (uint64_t m = bs; m;) {
-            const uint32_t i = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            if ((esc >> i) & 1ull) continue;
-            if (i == 63) esc_carry = 1;
-            else esc |= 1ull << (i + 1);
-        }
-        const uint64_t q = qt & ~esc;
-        uint64_t x = q;
-        x ^= x << 1;
-        x ^= x << 2;
-        x ^= x << 4;
-        x ^= x << 8;
-        x ^= x << 16;
-        x ^= x << 32;
-        const uint64_t instr = x ^ str_carry;  // opening quote + string body
-        str_carry = (instr >> 63) ? ~0ull : 0ull;
-        const uint64_t valid = mask_lt(len - b);
-        const uint64_t opens = q & instr, closes = q & ~instr;
-        const uint64_t structural = st & ~instr & valid;
-        const uint64_t atom = ~instr & ~q & ~st & ~wsm & valid;
-        const uint64_t astart = atom & ~((atom << 1) | atom_carry);
-        atom_carry = atom >> 63;
-        if (ctl & valid & instr & ~opens) ctl_in_string = true;
-        const uint64_t tokens = structural | opens | closes | astart;
-        // strings that need decoding (a backslash or a non-ASCII byte inside)
-        uint64_t slow_opens = 0;
-        for (uint64_t marks = (bs | hi) & instr & ~opens; marks;) {
-            const uint32_t mb = (uint32_t)__builtin_ctzll(marks);
-            const uint64_t ob = opens & mask_lt(mb);
-            if (ob) {
-                slow_opens |= 1ull << (63 - __builtin_clzll(ob));
-            } else if (last_open_idx != NONE && last_open_idx != last_marked) {
-                // the string opened in an earlier step: rewrite its token
-                wave_sync();
-                if (lane == 0) S.tok[last_open_idx] = (TK_OPENQ_SLOW << 24) | last_open_pos;
-                last_marked = last_open_idx;
+    const uint32_t nchunks = (len + 1023u) >> 10;
+    auto stage = [&](uint32_t ch) {
+        const uint32_t o = (ch << 10) + lane * 16u;
+        u32x4 v = {0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u};
+        if (o < len) v = *(const u32x4*)(d + o);  // d is 16-B aligned, kTokSlack readable past len
+        *(u32x4*)(ring + ((ch & 1u) << 10) + lane * 16u) = v;
+    };
+    auto rb = [&](uint32_t p) -> uint32_t { return p < len ? (uint32_t)ring[p & 2047u] : 0x20u; };
+    if (nchunks) stage(0);
+    for (uint32_t ch = 0; ch < nchunks; ch++) {
+        if (ch + 1 < nchunks) stage(ch + 1);
+        wave_sync();
+        const uint32_t bend = min(len, (ch + 1) << 10);
+        for (uint32_t b = ch << 10; b < bend; b += 64) {
+            const uint32_t pos = b + lane;
+            const uint32_t c = rb(pos);
+            const uint64_t bs = ballot(c == '\\');
+            const uint64_t qt = ballot(c == '"');
+            const uint64_t st = ballot(c == '{' || c == '}' || c == '[' || c == ']' || c == ':' || c == ',');
+            const uint64_t wsm = ballot(is_ws(c));
+            const uint64_t ctl = ballot(c < 0x20u);  // inside a string every control byte is an error
+            const uint64_t hi = ballot(c >= 0x80u);
+            // escaped characters: an unescaped backslash escapes the next byte
+            uint64_t esc = esc_carry;
+            esc_carry = 0;
+            for (uint64_t m = bs; m;) {
+                const uint32_t i = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                if ((esc >> i) & 1ull) continue;
+                if (i == 63) esc_carry = 1;
+                else esc |= 1ull << (i + 1);
             }
-            const uint64_t nx = opens & ~mask_lt(mb + 1);
-            marks = nx ? (marks & ~mask_lt((uint32_t)__builtin_ctzll(nx))) : 0ull;
+            const uint64_t q = qt & ~esc;
+            uint64_t x = q;
+            x ^= x << 1;
+            x ^= x << 2;
+            x ^= x << 4;
+            x ^= x << 8;
+            x ^= x << 16;
+            x ^= x << 32;
+            const uint64_t instr = x ^ str_carry;  // opening quote + string body
+            str_carry = (instr >> 63) ? ~0ull : 0ull;
+            const uint64_t valid = mask_lt(len - b);
+            const uint64_t opens = q & instr, closes = q & ~instr;
+            const uint64_t structural = st & ~instr & valid;
+            const uint64_t atom = ~instr & ~q & ~st & ~wsm & valid;
+            const uint64_t astart = atom & ~((atom << 1) | atom_carry);
+            atom_carry = atom >> 63;
+            if (ctl & valid & instr & ~opens) ctl_in_string = true;
+            const uint64_t tokens = structural | opens | closes | astart;
+            // strings that need decoding (a backslash or a non-ASCII byte inside)
+            uint64_t slow_opens = 0;
+            for (uint64_t marks = (bs | hi) & instr & ~opens; marks;) {
+                const uint32_t mb = (uint32_t)__builtin_ctzll(marks);
+                const uint64_t ob = opens & mask_lt(mb);
+                if (ob) {
+                    slow_opens |= 1ull << (63 - __builtin_clzll(ob));
+                } else if (last_open_idx != NONE && last_open_idx != last_marked) {
+                    // the string opened in an earlier step: rewrite its token
+                    wave_sync();
+                    if (lane == 0) S.tok[last_open_idx] = (TK_OPENQ_SLOW << 24) | last_open_pos;
+                    last_marked = last_open_idx;
+                }
+                const uint64_t nx = opens & ~mask_lt(mb + 1);
+                marks = nx ? (marks & ~mask_lt((uint32_t)__builtin_ctzll(nx))) : 0ull;
+            }
+            if ((tokens >> lane) & 1ull) {
+                const uint32_t idx = ntok + popc64(tokens & mask_lt(lane));
+                uint32_t code = c;
+                if ((closes >> lane) & 1ull) {
+                    code = TK_CLOSEQ;
+                } else if ((slow_opens >> lane) & 1ull) {
+                    code = TK_OPENQ_SLOW;
+                } else if ((opens >> lane) & 1ull) {
+                    // region keywords (an exact string: its closing quote follows the word);
+                    // the 13 bytes after the quote come from three aligned LDS words
+                    const uint32_t a = (pos + 1u) & ~7u, sh = ((pos + 1u) & 7u) * 8u;
+                    const uint64_t w0 = *(const uint64_t*)(ring + (a & 2047u));
+                    const uint64_t w1 = *(const uint64_t*)(ring + ((a + 8u) & 2047u));
+                    const uint64_t w2 = *(const uint64_t*)(ring + ((a + 16u) & 2047u));
+                    const uint64_t k0 = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
+                    const uint64_t k1 = sh ? (w1 >> sh) | (w2 << (64u - sh)) : w1;
+                    if (pos + 13u < len) {  // all compared bytes inside the document
+                        if (k0 == 0x617461646174656dull && (k1 & 0xFF) == '"') code = TK_KEY_META;
+                        else if ((k0 & 0xFFFFFFFFFFFFFFull) == 0x22737574617473ull) code = TK_KEY_STATUS;
+                        else if ((k0 & 0xFFFFFFFFFFFFFFull) == 0x22736c6562616cull) code = TK_KEY_LABELS;
+                        else if (k0 == 0x697461746f6e6e61ull && (k1 & 0xFFFFFFFFull) == 0x22736e6full)
+                            code = TK_KEY_ANNOT;
+                    } else {
+                        const uint32_t c1 = rb(pos + 1);
+                        if (c1 == 's' && rb(pos + 2) == 't' && rb(pos + 3) == 'a' && rb(pos + 4) == 't' &&
+                            rb(pos + 5) == 'u' && rb(pos + 6) == 's' && rb(pos + 7) == '"')
+                            code = TK_KEY_STATUS;
+                        else if (c1 == 'm' && rb(pos + 2) == 'e' && rb(pos + 3) == 't' && rb(pos + 4) == 'a' &&
+                                 rb(pos + 5) == 'd' && rb(pos + 6) == 'a' && rb(pos + 7) == 't' &&
+                                 rb(pos + 8) == 'a' && rb(pos + 9) == '"')
+                            code = TK_KEY_META;
+                        else if (c1 == 'l' && rb(pos + 2) == 'a' && rb(pos + 3) == 'b' && rb(pos + 4) == 'e' &&
+                                 rb(pos + 5) == 'l' && rb(pos + 6) == 's' && rb(pos + 7) == '"')
+                            code = TK_KEY_LABELS;
+                        else if (c1 == 'a' && rb(pos + 2) == 'n' && rb(pos + 3) == 'n' && rb(pos + 4) == 'o' &&
+                                 rb(pos + 5) == 't' && rb(pos + 6) == 'a' && rb(pos + 7) == 't' &&
+                                 rb(pos + 8) == 'i' && rb(pos + 9) == 'o' && rb(pos + 10) == 'n' &&
+                                 rb(pos + 11) == 's' && rb(pos + 12) == '"')
+                            code = TK_KEY_ANNOT;
+                    }
+                }
+                S.tok[idx] = (code << 24) | pos;
+            }
+            if (opens) {
+                const uint32_t ob = 63u - (uint32_t)__builtin_clzll(opens);
+                last_open_idx = ntok + popc64(tokens & mask_lt(ob));
+                last_open_pos = b + ob;
+                if ((slow_opens >> ob) & 1ull) last_marked = last_open_idx;
+            }
+            ntok += popc64(tokens);
         }
-        if ((tokens >> lane) & 1ull) {
-            const uint32_t idx = ntok + popc64(tokens & mask_lt(lane));
-            uint32_t code = c;
-            if ((closes >> lane) & 1ull) code = TK_CLOSEQ;
-            else if ((slow_opens >> lane) & 1ull) code = TK_OPENQ_SLOW;
-            S.tok[idx] = (code << 24) | pos;
-        }
-        if (opens) {
-            const uint32_t ob = 63u - (uint32_t)__builtin_clzll(opens);
-            last_open_idx = ntok + popc64(tokens & mask_lt(ob));
-            last_open_pos = b + ob;
-            if ((slow_opens >> ob) & 1ull) last_marked = last_open_idx;
-        }
-        ntok += popc64(tokens);
     }
     if (str_carry) status = GPUDIFF_TOK_SYNTAX;  // unterminated string
     if (ctl_in_string && status == GPUDIFF_TOK_OK) status = GPUDIFF_TOK_STRING;
     wave_sync();
 
+    mark(0);
     // ------------------------------------------------------------ phase 2: tree building
-    for (uint32_t i = lane; i <= kMaxDepth; i += 64) hist[i] = 0;
+    // Uniform state machine over the token list: everything lives in scalar
+    // registers (state, the innermost open container, region bookkeeping);
+    // outer containers go to an LDS stack on push and come back on pop.
     uint32_t nn = 0, sp = 0, expect = E_ROOT;
     bool skip = false;
-    uint32_t key_tok = 0, key_pos = 0, key_len = 0;
+    uint32_t top_node = 0, top_meta = 0;  // innermost open container: is_arr | region << 1 | count << 4
+    uint32_t key_tok = 0, key_code = 0;
     uint32_t meta_node = NONE, labels_node = NONE, annot_node = NONE;
     bool labels_ok = true, annot_ok = true, has_status = false;
     uint32_t max_depth = 0;
@@ -540,10 +602,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
             rz = vtok;
             rw = info | (depth << NI_DEPTH_SHIFT);
         }
-        if (depth) {
-            if (lane == 0) hist[depth]++;
-            max_depth = max(max_depth, depth);
-        }
+        max_depth = max(max_depth, depth);
         nn++;
         if ((nn & 63u) == 0) S.rec[nn - 64 + lane] = make_uint4(rx, ry, rz, rw);
         return id;
@@ -551,7 +610,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     if (status == GPUDIFF_TOK_OK) {
         for (uint32_t tb = 0; tb < ntok && status == GPUDIFF_TOK_OK; tb += 64) {
             const uint32_t tv = tb + lane < ntok ? S.tok[tb + lane] : 0u;
-            const uint32_t tnext = tb + 64 < ntok ? S.tok[tb + 64] : 0u;
+            const uint32_t tnext = __builtin_amdgcn_readfirstlane(tb + 64 < ntok ? S.tok[tb + 64] : 0u);
             const uint32_t kend = min(64u, ntok - tb);
             for (uint32_t k = 0; k < kend; k++) {
                 if (skip) {  // the close of an empty container, consumed by its opener's peek
@@ -559,19 +618,23 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                     continue;
                 }
                 const uint32_t t = rdlane(tv, k);
-                const uint32_t code = t >> 24, pos = t & POS_MASK, ti = tb + k;
+                const uint32_t code = t >> 24, ti = tb + k;
                 if (expect == E_KEY) {
-                    if (code == '"') {
+                    if (code == '"' || (code >= TK_KEY_META && code <= TK_KEY_ANNOT)) {
                         key_tok = ti;
-                        key_pos = pos;
+                        key_code = code;
                         expect = E_KEYCLOSE;
+                        // common case: close quote and ':' in this batch -> consume all three
+                        if (k + 2 < kend && (rdlane(tv, k + 2) >> 24) == ':') {
+                            k += 2;
+                            expect = E_VALUE;
+                        }
                     } else {
                         status = code == TK_OPENQ_SLOW ? GPUDIFF_TOK_KEY : GPUDIFF_TOK_SYNTAX;
                         break;
                     }
                 } else if (expect == E_KEYCLOSE) {
-                    key_len = pos - key_pos - 1u;  // the token after an open quote is its close
-                    expect = E_COLON;
+                    expect = E_COLON;  // the token after an open quote is its close
                 } else if (expect == E_COLON) {
                     if (code != ':') {
                         status = GPUDIFF_TOK_SYNTAX;
@@ -581,65 +644,50 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                 } else if (expect == E_STRCLOSE) {
                     expect = E_NEXT;
                 } else if (expect == E_NEXT) {
-                    const uint32_t top = sp - 1u;
-                    const bool is_arr = stk_meta[top] & 1u;
+                    const bool is_arr = top_meta & 1u;
                     if (code == ',') {
                         expect = is_arr ? E_VALUE : E_KEY;
                     } else if (code == (is_arr ? (uint32_t)']' : (uint32_t)'}')) {
                         sp--;
-                        expect = sp ? E_NEXT : E_END;
+                        if (sp) {
+                            top_node = __builtin_amdgcn_readfirstlane(stk_node[sp - 1]);
+                            top_meta = __builtin_amdgcn_readfirstlane(stk_meta[sp - 1]);
+                            expect = E_NEXT;
+                        } else {
+                            expect = E_END;
+                        }
                     } else {
                         status = GPUDIFF_TOK_SYNTAX;
                         break;
-                    }
-                } else if (expect == E_ROOT) {
-                    if (code != '{') {
-                        status = GPUDIFF_TOK_SYNTAX;
-                        break;
-                    }
-                    add_node(NONE, 0, ti, R_NONE << NI_REG_SHIFT, 0);
-                    const uint32_t pk = k + 1 < kend ? rdlane(tv, k + 1) : tnext;
-                    if (ti + 1 < ntok && (pk >> 24) == '}') {
-                        skip = true;  // {}: no leaves
-                        expect = E_END;
-                    } else {
-                        stk_node[0] = 0;
-                        stk_meta[0] = R_NONE << 1;
-                        sp = 1;
-                        expect = E_KEY;
                     }
                 } else if (expect == E_VALUE) {
-                    const uint32_t top = sp - 1u;
-                    const uint32_t parent = stk_node[top];
-                    const uint32_t pm = stk_meta[top];
-                    const bool in_arr = pm & 1u;
-                    const uint32_t preg = (pm >> 1) & 7u;
+                    const uint32_t parent = top_node;
+                    const bool in_arr = top_meta & 1u;
+                    const uint32_t preg = (top_meta >> 1) & 7u;
                     const uint32_t depth = sp;
                     uint32_t comp;
                     if (in_arr) {
-                        comp = pm >> 4;
-                        stk_meta[top] = pm + 16u;
+                        comp = top_meta >> 4;
+                        top_meta += 16u;
                     } else {
                         comp = key_tok | KEYBIT;
                     }
-                    const bool is_str = code == '"' || code == TK_OPENQ_SLOW;
+                    const bool is_str = code == '"' || (code >= TK_OPENQ_SLOW && code <= TK_KEY_ANNOT);
                     uint32_t reg = preg;
                     bool is_lab = false, is_ann = false, is_meta = false;
                     if (depth == 1) {
-                        const uint8_t* kp = d + key_pos + 1;
-                        if (key_is(kp, key_len, KW_METADATA, 8)) {
+                        if (key_code == TK_KEY_META) {
                             reg = R_META;
                             is_meta = true;
-                        } else if (key_is(kp, key_len, KW_STATUS, 6)) {
+                        } else if (key_code == TK_KEY_STATUS) {
                             has_status = true;
                             reg = code == 'n' ? R_NONE : R_STATUS;
                         } else {
                             reg = code == 'n' ? R_NONE : R_SPEC;
                         }
                     } else if (depth == 2 && !in_arr && parent == meta_node) {
-                        const uint8_t* kp = d + key_pos + 1;
-                        is_lab = key_is(kp, key_len, KW_LABELS, 6);
-                        is_ann = key_is_annotations(kp, key_len);
+                        is_lab = key_code == TK_KEY_LABELS;
+                        is_ann = key_code == TK_KEY_ANNOT;
                     } else if (depth == 3 && parent == labels_node) {
                         reg = R_LABELS;
                         if (!is_str) labels_ok = false;
@@ -669,8 +717,12 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                                 if (is_lab) labels_node = id;
                                 if (is_ann) annot_node = id;
                             }
-                            stk_node[sp] = id;
-                            stk_meta[sp] = (code == '[' ? 1u : 0u) | (reg << 1);
+                            if (lane == 0) {  // push: the current innermost container goes to LDS
+                                stk_node[sp - 1] = top_node;
+                                stk_meta[sp - 1] = top_meta;
+                            }
+                            top_node = id;
+                            top_meta = (code == '[' ? 1u : 0u) | (reg << 1);
                             sp++;
                             expect = code == '{' ? E_KEY : E_VALUE;
                         }
@@ -679,6 +731,10 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                                  rinfo | NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u),
                                  depth);
                         expect = E_STRCLOSE;
+                        if (k + 1 < kend) {  // its close quote is the next token
+                            k++;
+                            expect = E_NEXT;
+                        }
                     } else if (code == '}' || code == ']' || code == ',' || code == ':' || code == TK_CLOSEQ) {
                         status = GPUDIFF_TOK_SYNTAX;
                         break;
@@ -689,6 +745,22 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                     if (nn + 2 > ncap) {
                         status = GPUDIFF_TOK_SIZE;
                         break;
+                    }
+                } else if (expect == E_ROOT) {
+                    if (code != '{') {
+                        status = GPUDIFF_TOK_SYNTAX;
+                        break;
+                    }
+                    add_node(NONE, 0, ti, R_NONE << NI_REG_SHIFT, 0);
+                    const uint32_t pk = k + 1 < kend ? rdlane(tv, k + 1) : tnext;
+                    if (ti + 1 < ntok && (pk >> 24) == '}') {
+                        skip = true;  // {}: no leaves
+                        expect = E_END;
+                    } else {
+                        top_node = 0;
+                        top_meta = R_NONE << 1;
+                        sp = 1;
+                        expect = E_KEY;
                     }
                 } else {  // E_END: trailing data
                     status = GPUDIFF_TOK_SYNTAX;
@@ -702,6 +774,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     wave_sync();
 
     const uint64_t seed = slots ? ((slots[links[doc_i].slot].flags >> 8) & 0xFFu) : D.seed;
+    mark(1);
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
         uint32_t err = GPUDIFF_TOK_OK;
@@ -745,9 +818,17 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
         if (e) status = e;
     }
 
+    mark(2);
     // ------------------------------------------------------------ phase 3b: path hashes by depth
     if (status == GPUDIFF_TOK_OK && nn > 1) {
-        // counting sort of nodes by depth (hist filled in phase 2)
+        // counting sort of nodes by depth
+        for (uint32_t i = lane; i <= kMaxDepth; i += 64) hist[i] = 0;
+        wave_sync();
+        for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            if (i < nn) atomicAdd(&hist[(S.rec[i].w >> NI_DEPTH_SHIFT) & 0xFFu], 1u);
+        }
+        wave_sync();
         uint32_t run = 0;
         for (uint32_t d0 = 0; d0 <= kMaxDepth; d0 += 64) {
             const uint32_t dd = d0 + lane;
@@ -794,6 +875,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
         }
     }
 
+    mark(3);
     // ------------------------------------------------------------ phase 4: sort keys, uniqueness
     const uint32_t ns = nn > 1 ? nn - 1 : 0;  // every node but the root
     if (status == GPUDIFF_TOK_OK && ns) {
@@ -829,6 +911,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
         if (ballot(dup)) status = GPUDIFF_TOK_HASH;
     }
 
+    mark(4);
     // ------------------------------------------------------------ phase 5: blob
     o.n_nodes = nn;
     o.oflags = has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
@@ -944,6 +1027,18 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     }
     o.status = status;
     if (lane == 0) out[doc_i] = o;
+    mark(5);
+}
+
+hipError_t k0_profile(int enable, uint64_t* out8) {
+    if (out8) {
+        hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_k0_prof), 8 * sizeof(unsigned long long));
+        if (e != hipSuccess) return e;
+    }
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_k0_prof), z, sizeof(z));
+    if (e != hipSuccess) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_k0_prof_on), &enable, sizeof(int));
 }
 
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,

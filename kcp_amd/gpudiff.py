@@ -157,6 +157,7 @@ SIGNATURES = [
                                          C.c_size_t, C.c_void_p, C.c_uint64, C.POINTER(ObjInfo)]),
     ("gpudiff_encode_object_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
                                              C.POINTER(ObjInfo)]),
+    ("gpudiff_k0_profile", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
@@ -497,6 +498,12 @@ class Engine:
             f = info[i]
             res.append((f.as_dict(), raw[f.off:f.off + f.bytes] if f.status == TOK_OK else None))
         return res
+
+    def k0_profile(self, enable: bool = True):
+        """K0 per-phase wall-clock ticks (100 MHz) summed over waves since the last call."""
+        out = (C.c_uint64 * 8)()
+        _chk(_lib.gpudiff_k0_profile(self.ctx, 1 if enable else 0, out), "gpudiff_k0_profile")
+        return list(out)
 
     # ---- single pair drop-ins
     def spec_equal(self, old, new) -> bool:
