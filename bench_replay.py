@@ -213,6 +213,8 @@ def run(args):
         "gpu_ms_per_batch": {"diff_pass": tm.total_ms, "k2": tm.compare_ms},
         "store": {"resident_gb": ss.live_bytes / 1e9, "compactions": ss.compactions, "reseeded": ss.reseeded,
                   "old_objects_encoded": ss.old_encoded, "deferred_to_host": ss.deferred},
+        "batch_ms": {"host_submit": ss.host_submit_ms, "h2d": ss.h2d_ms, "k0_encode": ss.encode_ms,
+                     "k0c_k0x_link": ss.link_ms, "diff_pass": tm.total_ms} if dev_enc else None,
         "initial_list_objects_per_s": M / t_load,
         "checks": {"events_checked": checked, "decision_mismatches_vs_ground_truth": mism,
                    "sample_bit_exact_vs_oracle": sample_ok},

@@ -90,6 +90,9 @@ enum {
 #define GPUDIFF_OPT_NO_K2_ALT 0x100000u  /* keep every K2 segment on the main stream */
 #define GPUDIFF_OPT_ARENA_SHIFT 21u      /* 4 bits: shrink the per-wave path arena 2^k-fold
                                             (tests: forces pairs through the deferred K4 path) */
+#define GPUDIFF_OPT_DEVICE_ENCODE 0x2000000u /* gpudiff_submit / single-pair helpers: raw JSON up, kernel K0
+                                                encodes (as GPUDIFF_STORE_DEVICE_ENCODE does for the store) */
+#define GPUDIFF_OPT_K0_VARIANT_SHIFT 26u /* 2 bits: K0 occupancy variant (0: 8 waves/SIMD, 1: unconstrained) */
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */
@@ -272,6 +275,9 @@ typedef struct gpudiff_store_stats {
     uint64_t events, old_encoded, reseeded, collisions_unresolved;
     uint64_t last_batch_bytes; /* bytes uploaded by the last submit (blobs; device-encode: JSON) */
     uint64_t deferred;         /* device-encode: events K0 handed to the host encoder */
+    /* device-encode with GPUDIFF_OPT_TIMING: per-batch means (ms) of the host side of submit,
+     * the H2D copy, K0 and K0c+K0x */
+    float host_submit_ms, h2d_ms, encode_ms, link_ms;
 } gpudiff_store_stats;
 
 int gpudiff_store_create(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,

@@ -17,6 +17,7 @@
 
 #include "../../include/gpudiff.h"
 #include "encoder.h"
+#include "dstore.h"
 #include "engine.h"
 #include "kernels.h"
 #include "xxh64.h"
@@ -174,6 +175,7 @@ void gpudiff_close(gpudiff_ctx* c) {
     if (c->has_device) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
+        if (c->pair_store) dstore_free(c, c->pair_store);
         for (int i = 0; i < 2; i++) {
             if (c->ring[i]) gpudiff_dbatch_free(c, c->ring[i]);
             if (c->ring_hb[i]) gpudiff_hbatch_free(c, c->ring_hb[i]);
@@ -749,6 +751,10 @@ int gpudiff_submit(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpu
     if (!c || (n && !pairs)) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
+    if ((c->flags & GPUDIFF_OPT_DEVICE_ENCODE) && n) {
+        rc = dstore_submit_pairs(c, pairs, n, ticket);
+        if (rc != GPUDIFF_E_CAPACITY) return rc;
+    }
     gpudiff_hbatch* hb = nullptr;
     if ((rc = gpudiff_encode_pairs(c, pairs, n, &hb))) return rc;
     const uint32_t slot = c->ring_next;

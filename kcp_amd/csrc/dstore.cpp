@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <thread>
 #include <unordered_map>
@@ -57,6 +58,7 @@ struct Ring {
     uint64_t docs_cap = 0, coll_cap = 0, def_cap = 0;
     uint32_t* dcnt = nullptr;     // deferred events of the batch
     hipEvent_t staged = nullptr;  // its H2D copies finished (pinned buffers reusable)
+    hipEvent_t t_ev[4] = {};      // GPUDIFF_OPT_TIMING: before H2D, after H2D, after K0, after K0c/K0x
     std::vector<gpudiff_event> events;
     uint32_t batch = 0, nev = 0;
     uint64_t bound = 0;
@@ -115,8 +117,12 @@ struct DStore {
     uint64_t res_ups_cap = 0;
     uint32_t* res_err = nullptr;
     bool broken = false;
+    bool pair_mode = false;  // gpudiff_submit with GPUDIFF_OPT_DEVICE_ENCODE: slot i = pair i, no state kept
     gpudiff_store_stats st{};
     uint64_t deferred_total = 0;
+    // GPUDIFF_OPT_TIMING: per-batch sums (ms) of host submit, H2D, K0, K0c+K0x
+    double t_sum[4] = {0, 0, 0, 0};
+    uint64_t t_n = 0;
 };
 
 namespace {
@@ -242,6 +248,26 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
     std::vector<uint32_t> touched;
     for (size_t k = 0; k < drows.size(); k++) {
         const gpudiff_event& e = R.events[drows[k]];
+        if (s->pair_mode) {  // gpudiff_encode_pairs' decisions on (old_json, new_json)
+            gpudiff_pair_row& r = rows[k];
+            memset(&r, 0, sizeof(r));
+            r.pair_id = e.pair_id;
+            r.cluster_id = e.cluster_id;
+            uint32_t seed = 0;
+            if (e.old_json && enc.flatten_json(e.old_json, e.old_len, arena_old, fo) &&
+                enc.flatten_json(e.new_json, e.new_len, arena_new, fn) && enc.pair_seed(fo, fn, &seed)) {
+                uint64_t oa, ob;
+                enc.write_object(fo, pool, &oa, &r.spec_l_a, &r.spec_ar_a, &r.stat_l_a, &r.stat_ar_a);
+                enc.write_object(fn, pool, &ob, &r.spec_l_b, &r.spec_ar_b, &r.stat_l_b, &r.stat_ar_b);
+                r.off_a = kRelTag | oa;
+                r.off_b = kRelTag | ob;
+                r.flags_a = (fo.flags & GPUDIFF_OBJ_HAS_STATUS) | (seed << GPUDIFF_OBJ_SEED_SHIFT);
+                r.flags_b = (fn.flags & GPUDIFF_OBJ_HAS_STATUS) | (seed << GPUDIFF_OBJ_SEED_SHIFT);
+            } else {
+                r.flags_a = r.flags_b = GPUDIFF_OBJ_DECODE_ERR;
+            }
+            continue;
+        }
         HostSlot& S = hs[e.slot];
         if (!S.fetched) {
             if ((rc = fetch_slot(s, e.slot, S))) return rc;
@@ -510,8 +536,15 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
 int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, gpudiff_ticket* ticket) {
     if (s->broken) return GPUDIFF_E_STATE;
     if (n > s->max_events) return GPUDIFF_E_INVAL;
+    const auto t_host0 = std::chrono::steady_clock::now();
+    const bool timing = (c->flags & GPUDIFF_OPT_TIMING) != 0;
     Ring& R = s->ring[s->ring_next];
-    if (R.outstanding) return GPUDIFF_E_STATE;  // wait on the batch two submits back first
+    if (R.outstanding) {
+        if (!s->pair_mode) return GPUDIFF_E_STATE;  // wait on the batch two submits back first
+        // pair mode keeps gpudiff_submit's ring rule: the ticket two submits back is dropped
+        c->finishers.erase(R.ticket);
+        R.outstanding = false;
+    }
     int rc;
     if (R.staged) HIPCHK(hipEventSynchronize(R.staged));
     const uint32_t batch = ++s->batch_seq;
@@ -557,11 +590,16 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         const gpudiff_event& e = ev[i];
         if (e.slot >= s->max_slots || !e.new_json || e.new_len > kTokMaxLen || e.old_len > kTokMaxLen)
             return GPUDIFF_E_INVAL;
-        if (!s->seen[e.slot] && e.old_json) {  // first sighting: its old object is the old side
-            add_doc(e.old_json, e.old_len, e.slot, kNoRow, e);
-            s->st.old_encoded++;
+        if (s->pair_mode) {  // every pair: its old object, then its new one (an absent old object: decode error)
+            static const uint8_t kNone[1] = {0};
+            add_doc(e.old_json ? e.old_json : kNone, e.old_json ? e.old_len : 0, e.slot, kNoRow, e);
+        } else {
+            if (!s->seen[e.slot] && e.old_json) {  // first sighting: its old object is the old side
+                add_doc(e.old_json, e.old_len, e.slot, kNoRow, e);
+                s->st.old_encoded++;
+            }
+            s->seen[e.slot] = 1;
         }
-        s->seen[e.slot] = 1;
         add_doc(e.new_json, e.new_len, e.slot, (uint32_t)i, e);
     }
     jbytes += kTokSlack;
@@ -613,21 +651,29 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         return rc;
     if ((rc = grow_dev(&R.dcoll, &R.coll_cap, nd + 1)) || (rc = grow_dev(&R.ddef, &R.def_cap, n + 1))) return rc;
     hipStream_t st = c->stream;
+    if (timing && !R.t_ev[0])
+        for (auto& e : R.t_ev) HIPCHK(hipEventCreate(&e));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[0], st));
     HIPCHK(hipMemcpyAsync(R.djson, R.hjson, jbytes, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, meta_bytes, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(R.staged, st));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[1], st));
+    if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
     const TokDoc* ddocs = (const TokDoc*)R.dmeta;
     const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
     const uint32_t* dheads = (const uint32_t*)(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
     uint8_t* space = s->space[s->cur];
     for (auto& L : launches)
         HIPCHK(launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
-                                  s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first));
+                                  s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
+                                  (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[2], st));
     HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
     HIPCHK(hipMemsetAsync(R.dcnt, 0, 4, st));
     gpudiff_dbatch* d = R.d;
     HIPCHK(launch_link(st, dheads, nh, dlinks, R.douts, R.dcoll, s->slots, d->rows, d->pair_ids, R.ddef, batch,
                        R.dcnt, s->ctr));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
     s->used_ub += bound;
     // 4. the diff pass over the batch's rows
     d->pool = space;
@@ -650,8 +696,10 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     c->finishers[*ticket] = [s, Rp](ResultStore& rs) -> int {
         Ring& RR = *Rp;
         RR.outstanding = false;
-        if (RR.batch != s->next_wait) return GPUDIFF_E_STATE;  // waits follow submit order
-        s->next_wait++;
+        if (!s->pair_mode) {
+            if (RR.batch != s->next_wait) return GPUDIFF_E_STATE;  // waits follow submit order
+            s->next_wait++;
+        }
         uint32_t ndef = 0;
         uint64_t used = 0;
         HIPCHK(hipMemcpy(&ndef, RR.dcnt, 4, hipMemcpyDeviceToHost));
@@ -659,6 +707,12 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         // exact append point + what the other batch in flight may still add
         const Ring& other = s->ring[(Rp - s->ring) ^ 1];
         s->used_ub = std::max<uint64_t>(used, used + (other.outstanding ? other.bound : 0));
+        if (RR.t_ev[0] && (s->c->flags & GPUDIFF_OPT_TIMING)) {
+            float ms[3];
+            for (int k = 0; k < 3; k++) HIPCHK(hipEventElapsedTime(&ms[k], RR.t_ev[k], RR.t_ev[k + 1]));
+            for (int k = 0; k < 3; k++) s->t_sum[1 + k] += ms[k];
+            s->t_n++;
+        }
         int r2 = ndef ? resolve(s, RR, rs) : GPUDIFF_OK;
         if (r2) s->broken = true;
         // forgets older than every outstanding batch are settled
@@ -667,9 +721,40 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         return r2;
     };
     s->ring_next ^= 1u;
+    if (timing)
+        s->t_sum[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
     s->st.events += n;
     s->st.last_batch_bytes = jbytes;
     return GPUDIFF_OK;
+}
+
+int dstore_submit_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpudiff_ticket* ticket) {
+    DStore*& s = c->pair_store;
+    uint64_t json = 0;
+    for (size_t i = 0; i < n; i++) json += pairs[i].old_len + pairs[i].new_len;
+    const uint64_t space = std::max<uint64_t>(512ull << 20, 4 * (json + json / 2 + 128 * n));
+    if (!s || s->max_events < n || s->space_bytes < space / 2) {
+        if (s && (s->ring[0].outstanding || s->ring[1].outstanding))
+            return GPUDIFF_E_CAPACITY;  // grows only between batches: gpudiff_submit encodes this one on the host
+        if (s) dstore_free(c, s);
+        s = nullptr;
+        const uint32_t cap = (uint32_t)std::max<size_t>(65536, n + n / 2);
+        int rc;
+        s = dstore_create(c, cap, space, cap, &rc);
+        if (!s) return rc;
+        s->pair_mode = true;
+    }
+    std::vector<gpudiff_event> ev(n);
+    for (size_t i = 0; i < n; i++) {
+        const gpudiff_json_pair& p = pairs[i];
+        ev[i] = gpudiff_event{(uint32_t)i, p.pair_id, p.cluster_id, 0, p.new_json, p.new_len, p.old_json, p.old_len};
+        if (!p.new_json) {  // as gpudiff_encode_pairs: an absent object is a decode error
+            static const uint8_t kNone[1] = {0};
+            ev[i].new_json = kNone;
+            ev[i].new_len = 0;
+        }
+    }
+    return dstore_submit(c, s, ev.data(), n, ticket);
 }
 
 int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot) {
@@ -693,6 +778,12 @@ int dstore_stats(const DStore* s, gpudiff_store_stats* out) {
     out->live_bytes = lb;
     out->used_bytes = used;
     out->deferred = s->deferred_total;
+    if (s->t_n) {
+        out->host_submit_ms = (float)(s->t_sum[0] / s->t_n);
+        out->h2d_ms = (float)(s->t_sum[1] / s->t_n);
+        out->encode_ms = (float)(s->t_sum[2] / s->t_n);
+        out->link_ms = (float)(s->t_sum[3] / s->t_n);
+    }
     return GPUDIFF_OK;
 }
 
@@ -710,6 +801,8 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         for (void* p : {(void*)R.hjson, (void*)R.hmeta})
             if (p) (void)hipHostFree(p);
         if (R.staged) (void)hipEventDestroy(R.staged);
+        for (auto& e : R.t_ev)
+            if (e) (void)hipEventDestroy(e);
     }
     if (s->res_d) gpudiff_dbatch_free(c, s->res_d);
     for (void* p : {(void*)s->space[0], (void*)s->space[1], (void*)s->used_dev, (void*)s->slots, (void*)s->ctr,

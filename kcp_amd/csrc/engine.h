@@ -91,6 +91,8 @@ struct gpudiff_dbatch {
     gpudiff_ticket ticket = 0;
 };
 
+struct DStore;
+
 struct ResultStore {
     std::vector<uint8_t> flags;
     std::vector<uint32_t> spec, status, dirty, off;
@@ -125,6 +127,8 @@ struct gpudiff_ctx {
     // per-ticket completion hooks run by gpudiff_wait before results are
     // published (the device-encode store resolves its host-deferred events)
     std::unordered_map<gpudiff_ticket, std::function<int(ResultStore&)>> finishers;
+    // GPUDIFF_OPT_DEVICE_ENCODE: gpudiff_submit's pairs go through K0 (dstore.cpp, pair mode)
+    DStore* pair_store = nullptr;
     // submit ring
     gpudiff_dbatch* ring[2] = {nullptr, nullptr};
     gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};

@@ -118,7 +118,8 @@ hipError_t k0_profile(int enable, uint64_t* out8);
 // slots/links (optional): the seed is the slot's (DSlot.flags >> 8).
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
-                              TokOut* out, const DSlot* slots = nullptr, const DocLink* links = nullptr);
+                              TokOut* out, const DSlot* slots = nullptr, const DocLink* links = nullptr,
+                              uint32_t variant = 0);
 // K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)
 hipError_t launch_collide(hipStream_t s, const DocLink* links, const TokOut* outs, const DSlot* slots, uint32_t n,
                           const uint8_t* space, uint8_t* coll);

@@ -59,6 +59,8 @@ enum : uint32_t { E_ROOT, E_KEY, E_KEYCLOSE, E_COLON, E_VALUE, E_STRCLOSE, E_NEX
 
 constexpr uint32_t kMaxDepth = 255;
 constexpr uint32_t kWavesPerBlock = 4;
+constexpr uint32_t kLdsPerWave = 5120;
+constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -114,6 +116,7 @@ __device__ __forceinline__ uint64_t xxh64_words(uint64_t seed, uint32_t len, F w
     const uint32_t stripes = len >> 5;
     if (stripes) {
         uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+#pragma unroll 2
         for (uint32_t s = 0; s < stripes; s++) {
             v1 = xround(v1, word(4 * s));
             v2 = xround(v2, word(4 * s + 1));
@@ -393,26 +396,27 @@ struct Scratch {
 __device__ unsigned long long g_k0_prof[8];
 __device__ int g_k0_prof_on;
 
-__global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ docs, uint32_t n_docs,
+template <int MINW>
+__global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restrict__ docs, uint32_t n_docs,
                                                      const uint8_t* __restrict__ json, uint8_t* __restrict__ scratch,
                                                      uint8_t* __restrict__ space, uint64_t space_cap,
                                                      unsigned long long* __restrict__ used, uint64_t mask,
                                                      TokOut* __restrict__ out, const DSlot* __restrict__ slots,
                                                      const DocLink* __restrict__ links) {
-    __shared__ uint32_t s_stk_node[kWavesPerBlock][kMaxDepth + 1];
-    __shared__ uint32_t s_stk_meta[kWavesPerBlock][kMaxDepth + 1];
-    __shared__ uint32_t s_hist[kWavesPerBlock][kMaxDepth + 1];
-    __shared__ uint32_t s_cur[kWavesPerBlock][kMaxDepth + 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_ring[kWavesPerBlock][2048];
+    // per wave, one LDS area reused phase by phase (5 KiB -> 8 workgroups of 4 waves per CU):
+    //   phase 1: [0, 2048) byte ring; phase 2: [2048, 4096) container stack;
+    //   phase 3b: [0, 2048) depth histogram + cursors; phase 4: [0, 4608) sort (ns <= kLdsSort)
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[kWavesPerBlock][kLdsPerWave];
 
     const uint32_t lane = lane_id();
     const uint32_t wib = threadIdx.x >> 6;
     const uint32_t doc_i = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wib);
     if (doc_i >= n_docs) return;
-    uint32_t* stk_node = s_stk_node[wib];
-    uint32_t* stk_meta = s_stk_meta[wib];
-    uint32_t* hist = s_hist[wib];
-    uint32_t* cur = s_cur[wib];
+    uint8_t* lds = s_lds[wib];
+    uint32_t* stk_node = (uint32_t*)(lds + 2048);
+    uint32_t* stk_meta = (uint32_t*)(lds + 3072);
+    uint32_t* hist = (uint32_t*)lds;
+    uint32_t* cur = (uint32_t*)(lds + 1024);
 
     const TokDoc D = docs[doc_i];
     const uint8_t* d = json + D.json_off;
@@ -454,7 +458,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     // The document streams through a 2 x 1 KiB LDS ring (one 16-B load per
     // lane per KiB, the next KiB staged before the current one is scanned, so
     // an opening quote can look 12 bytes ahead for the region keywords).
-    uint8_t* ring = s_ring[wib];
+    uint8_t* ring = lds;
     uint32_t ntok = 0;
     uint64_t esc_carry = 0, str_carry = 0, atom_carry = 0;
     uint32_t last_open_idx = NONE, last_open_pos = 0, last_marked = NONE;
@@ -878,10 +882,12 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
     mark(3);
     // ------------------------------------------------------------ phase 4: sort keys, uniqueness
     const uint32_t ns = nn > 1 ? nn - 1 : 0;  // every node but the root
+    uint64_t* skey = ns <= kLdsSort ? (uint64_t*)lds : S.skey;
+    uint32_t* sidx = ns <= kLdsSort ? (uint32_t*)(lds + 8 * kLdsSort) : S.sidx;
     if (status == GPUDIFF_TOK_OK && ns) {
         for (uint32_t j = lane; j < ns; j += 64) {
-            S.skey[j] = S.h[j + 1] & mask;
-            S.sidx[j] = j + 1;
+            skey[j] = S.h[j + 1] & mask;
+            sidx[j] = j + 1;
         }
         wave_sync();
         // bitonic sort, all comparators ascending (flip + half-cleaners):
@@ -892,13 +898,13 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                 for (uint32_t i = lane; i < ns; i += 64) {
                     const uint32_t j = flip ? (i ^ (kk - 1u)) : (i ^ (dd >> 1));
                     if (j > i && j < ns) {
-                        const uint64_t a = S.skey[i], b = S.skey[j];
+                        const uint64_t a = skey[i], b = skey[j];
                         if (a > b) {
-                            const uint32_t ia = S.sidx[i], ib = S.sidx[j];
-                            S.skey[i] = b;
-                            S.skey[j] = a;
-                            S.sidx[i] = ib;
-                            S.sidx[j] = ia;
+                            const uint32_t ia = sidx[i], ib = sidx[j];
+                            skey[i] = b;
+                            skey[j] = a;
+                            sidx[i] = ib;
+                            sidx[j] = ia;
                         }
                     }
                 }
@@ -907,7 +913,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
         }
         bool dup = false;
         for (uint32_t j = lane + 1; j < ns; j += 64)
-            if (S.skey[j] == S.skey[j - 1]) dup = true;
+            if (skey[j] == skey[j - 1]) dup = true;
         if (ballot(dup)) status = GPUDIFF_TOK_HASH;
     }
 
@@ -927,7 +933,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
             const uint32_t j = j0 + lane;
             uint32_t rg = 0, ar = 0;
             if (j < ns) {
-                const uint32_t i = S.sidx[j];
+                const uint32_t i = sidx[j];
                 rg = region_of(S.rec[i].w);
                 if (rg) ar = meta_arena(S.meta[i]);
             }
@@ -960,7 +966,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                 const uint32_t j = j0 + lane;
                 uint32_t rg = 0, i = 0, m = 0, ar = 0;
                 if (j < ns) {
-                    i = S.sidx[j];
+                    i = sidx[j];
                     const uint32_t w = S.rec[i].w;
                     rg = region_of(w);
                     if (rg) {
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(256) void k_encode_docs(const TokDoc* __restrict__ 
                     const uint32_t g = rg - 1;
                     const uint32_t L = Lr[g];
                     uint8_t* sp8 = segp[g];
-                    ((uint64_t*)sp8)[my_rank] = S.skey[j];
+                    ((uint64_t*)sp8)[my_rank] = skey[j];
                     ((uint64_t*)(sp8 + 8ull * L))[my_rank] = S.val[i];
                     ((uint32_t*)(sp8 + 16ull * L))[my_rank] = m;
                     fpt[g][my_rank] = S.fp[i];
@@ -1043,11 +1049,16 @@ hipError_t k0_profile(int enable, uint64_t* out8) {
 
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
-                              TokOut* out, const DSlot* slots, const DocLink* links) {
+                              TokOut* out, const DSlot* slots, const DocLink* links, uint32_t variant) {
     if (!n) return hipSuccess;
     const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    k_encode_docs<<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask, out,
-                                                         slots, links);
+    // variant (tuning, GPUDIFF_OPT_K0_VARIANT_SHIFT): 0 = 8 waves/SIMD (<= 64 VGPRs), 1 = unconstrained
+    if (variant == 1)
+        k_encode_docs<1><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask,
+                                                                out, slots, links);
+    else
+        k_encode_docs<8><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask,
+                                                                out, slots, links);
     return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR = 0x1, 0x2, 0x4
 PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
 OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
+OPT_DEVICE_ENCODE = 0x2000000
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
 OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_FRESH, OBJ_SEED_SHIFT = 0x1, 0x2, 0x4, 8
@@ -73,7 +74,9 @@ class StoreStats(C.Structure):
     _fields_ = [("max_slots", C.c_uint64), ("live_slots", C.c_uint64), ("space_bytes", C.c_uint64),
                 ("used_bytes", C.c_uint64), ("live_bytes", C.c_uint64), ("compactions", C.c_uint64),
                 ("events", C.c_uint64), ("old_encoded", C.c_uint64), ("reseeded", C.c_uint64),
-                ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64), ("deferred", C.c_uint64)]
+                ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64), ("deferred", C.c_uint64),
+                ("host_submit_ms", C.c_float), ("h2d_ms", C.c_float), ("encode_ms", C.c_float),
+                ("link_ms", C.c_float)]
 
 
 class ObjInfo(C.Structure):
@@ -382,10 +385,11 @@ class Engine:
 
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
                  timing: bool = False, path_hash_bits: int = 64, host_value_hash: bool = False,
-                 no_value_hash: bool = False, flags: int = 0):
+                 no_value_hash: bool = False, flags: int = 0, device_encode: bool = False):
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
                  flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0) |
-                       (OPT_NO_VALUE_HASH if no_value_hash else 0) | flags,
+                       (OPT_NO_VALUE_HASH if no_value_hash else 0) | (OPT_DEVICE_ENCODE if device_encode else 0) |
+                       flags,
                  path_hash_bits=path_hash_bits)
         h = C.c_void_p()
         _chk(_lib.gpudiff_open(C.byref(o), C.byref(h)), "gpudiff_open")

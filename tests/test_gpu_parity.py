@@ -21,10 +21,12 @@ from tests.workload import make_pairs
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def eng():
+@pytest.fixture(scope="module", params=[False, True], ids=["host_encode", "device_encode"])
+def eng(request):
+    """Both submit paths: host encoding, and device encoding (raw JSON up,
+    kernel K0 encodes, the host re-does only what K0 defers)."""
     assert G.device_count() > 0, "no GPU visible"
-    e = G.Engine(device=0, encode_threads=8, timing=True)
+    e = G.Engine(device=0, encode_threads=8, timing=True, device_encode=request.param)
     yield e
     e.close()
 
@@ -137,8 +139,9 @@ def test_scratch_overflow_keeps_arena_paths():
     e.close()
 
 
-def test_forced_collisions():
-    e = G.Engine(device=0, path_hash_bits=8)
+@pytest.mark.parametrize("dev", [False, True], ids=["host_encode", "device_encode"])
+def test_forced_collisions(dev):
+    e = G.Engine(device=0, path_hash_bits=8, device_encode=dev)
     pairs, _, _ = make_pairs(200, seed=5, mix=(("cm", 0.5), ("deploy", 0.5)), mutate_frac=0.5)
     res = e.diff_pairs(pairs)
     assert_matches(res, pairs, hash_bits=8)

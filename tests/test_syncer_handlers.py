@@ -64,9 +64,10 @@ def test_batched_update_gate_matches_reference_order():
 
 
 @pytest.mark.gpu
-def test_gpu_handlers_match_reference():
+@pytest.mark.parametrize("dev", [False, True], ids=["host_encode", "device_encode"])
+def test_gpu_handlers_match_reference(dev):
     events = _events()
-    eng = G.Engine(device=0)
+    eng = G.Engine(device=0, device_encode=dev)
     spec_c, stat_c = Y.Controller(), Y.Controller()
     b = Y.UpdateBatcher(engine=eng, max_batch=16)
     hs = Y.spec_handlers(spec_c, "deployments.apps", b)

@@ -18,17 +18,20 @@ pop = S.Population(cfg)
 buf, offs, _ = pop.json_range(0, n, 8)
 docs = [bytes(buf[offs[2 * i + 1]:offs[2 * i + 2]]) for i in range(n)]
 print("docs %d, mean %.0f B" % (n, np.mean([len(d) for d in docs])))
-eng = G.Engine(device=0)
-eng.encode_objects(docs[:256])  # warm
-for on in (False, True):
-    eng.k0_profile(on)
-    t = time.time()
-    res = eng.encode_objects(docs)
-    dt = time.time() - t
-    prof = eng.k0_profile(False)
-    bad = sum(1 for i, _ in res if i["status"] != 0)
-    print("profile=%s: %.1f ms incl. staging, %d deferred" % (on, dt * 1e3, bad))
-names = ["scan", "tree", "values", "hashes", "sort", "blob"]
-tot = sum(prof[:6])
-for k, nm in enumerate(names):
-    print("  %-7s %6.1f%%  %.2f us/doc-wave" % (nm, 100.0 * prof[k] / max(1, tot), prof[k] / 100.0 / n))
+variants = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0"])]
+for var in variants:
+    eng = G.Engine(device=0, flags=var << 26)
+    eng.encode_objects(docs[:256])  # warm
+    for on in (False, True):
+        eng.k0_profile(on)
+        t = time.time()
+        res = eng.encode_objects(docs)
+        dt = time.time() - t
+        prof = eng.k0_profile(False)
+        bad = sum(1 for i, _ in res if i["status"] != 0)
+        print("variant %d profile=%s: %.1f ms incl. staging, %d deferred" % (var, on, dt * 1e3, bad))
+    names = ["scan", "tree", "values", "hashes", "sort", "blob"]
+    tot = sum(prof[:6])
+    for k, nm in enumerate(names):
+        print("  %-7s %6.1f%%  %.2f us/doc-wave" % (nm, 100.0 * prof[k] / max(1, tot), prof[k] / 100.0 / n))
+    eng.close()
