@@ -58,7 +58,9 @@ struct Ring {
     uint64_t docs_cap = 0, coll_cap = 0, def_cap = 0;
     uint32_t* dcnt = nullptr;     // deferred events of the batch
     hipEvent_t staged = nullptr;  // its H2D copies finished (pinned buffers reusable)
-    hipEvent_t t_ev[4] = {};      // GPUDIFF_OPT_TIMING: before H2D, after H2D, after K0, after K0c/K0x
+    hipEvent_t k0_done = nullptr;  // its K0..K0x finished reading the device JSON / document table
+    bool k0_recorded = false;
+    hipEvent_t t_ev[5] = {};      // GPUDIFF_OPT_TIMING: H2D begin/end (copy stream), K0 begin/end, K0c+K0x end
     std::vector<gpudiff_event> events;
     uint32_t batch = 0, nev = 0;
     uint64_t bound = 0;
@@ -96,6 +98,7 @@ struct DStore {
     uint64_t used_ub = 0;  // host upper bound of *used_dev
     DSlot* slots = nullptr;
     uint32_t* ctr = nullptr;  // kCtrLive, kCtrLiveBytes
+    hipStream_t cs = nullptr;  // H2D of the next batch overlaps K0 of the current one
     uint64_t* sizes = nullptr;
     uint64_t* tile_sums = nullptr;
     uint8_t* scratch = nullptr;
@@ -521,8 +524,11 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
         R.d->pool = nullptr;
         R.d->pool_borrowed = true;
         if ((rc = dalloc(&R.dcnt, 1))) return fail(rc);
-        if (hipEventCreateWithFlags(&R.staged, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+        if (hipEventCreateWithFlags(&R.staged, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&R.k0_done, hipEventDisableTiming) != hipSuccess)
+            return fail(GPUDIFF_E_DEVICE);
     }
+    if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
     if ((rc = gpudiff_dbatch_create(c, 16, 1024, &s->res_d))) return fail(rc);
     (void)hipFree(s->res_d->pool);
     s->res_d->pool = nullptr;
@@ -650,14 +656,19 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         (rc = grow_dev(&R.dmeta, &R.dmeta_cap, meta_bytes)) || (rc = grow_dev(&R.douts, &R.docs_cap, nd + 1)))
         return rc;
     if ((rc = grow_dev(&R.dcoll, &R.coll_cap, nd + 1)) || (rc = grow_dev(&R.ddef, &R.def_cap, n + 1))) return rc;
-    hipStream_t st = c->stream;
+    hipStream_t st = c->stream, cs = s->cs;
     if (timing && !R.t_ev[0])
         for (auto& e : R.t_ev) HIPCHK(hipEventCreate(&e));
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[0], st));
-    HIPCHK(hipMemcpyAsync(R.djson, R.hjson, jbytes, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, meta_bytes, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(R.staged, st));
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[1], st));
+    // the upload runs on the copy stream, behind this ring slot's previous K0 (which read the
+    // same device buffers), so it overlaps the other batch's K0 / diff pass
+    if (R.k0_recorded) HIPCHK(hipStreamWaitEvent(cs, R.k0_done, 0));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[0], cs));
+    HIPCHK(hipMemcpyAsync(R.djson, R.hjson, jbytes, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, meta_bytes, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipEventRecord(R.staged, cs));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[1], cs));
+    HIPCHK(hipStreamWaitEvent(st, R.staged, 0));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[2], st));
     if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
     const TokDoc* ddocs = (const TokDoc*)R.dmeta;
     const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
@@ -667,13 +678,15 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         HIPCHK(launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
                                   s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
                                   (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[2], st));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
     HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
     HIPCHK(hipMemsetAsync(R.dcnt, 0, 4, st));
     gpudiff_dbatch* d = R.d;
     HIPCHK(launch_link(st, dheads, nh, dlinks, R.douts, R.dcoll, s->slots, d->rows, d->pair_ids, R.ddef, batch,
                        R.dcnt, s->ctr));
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
+    HIPCHK(hipEventRecord(R.k0_done, st));
+    R.k0_recorded = true;
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[4], st));
     s->used_ub += bound;
     // 4. the diff pass over the batch's rows
     d->pool = space;
@@ -709,7 +722,9 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         s->used_ub = std::max<uint64_t>(used, used + (other.outstanding ? other.bound : 0));
         if (RR.t_ev[0] && (s->c->flags & GPUDIFF_OPT_TIMING)) {
             float ms[3];
-            for (int k = 0; k < 3; k++) HIPCHK(hipEventElapsedTime(&ms[k], RR.t_ev[k], RR.t_ev[k + 1]));
+            HIPCHK(hipEventElapsedTime(&ms[0], RR.t_ev[0], RR.t_ev[1]));  // H2D
+            HIPCHK(hipEventElapsedTime(&ms[1], RR.t_ev[2], RR.t_ev[3]));  // K0
+            HIPCHK(hipEventElapsedTime(&ms[2], RR.t_ev[3], RR.t_ev[4]));  // K0c + K0x
             for (int k = 0; k < 3; k++) s->t_sum[1 + k] += ms[k];
             s->t_n++;
         }
@@ -792,6 +807,7 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
     if (c && c->has_device) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
+        if (s->cs) (void)hipStreamSynchronize(s->cs);
     }
     for (Ring& R : s->ring) {
         if (R.d) gpudiff_dbatch_free(c, R.d);
@@ -801,10 +817,15 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         for (void* p : {(void*)R.hjson, (void*)R.hmeta})
             if (p) (void)hipHostFree(p);
         if (R.staged) (void)hipEventDestroy(R.staged);
+        if (R.k0_done) (void)hipEventDestroy(R.k0_done);
         for (auto& e : R.t_ev)
             if (e) (void)hipEventDestroy(e);
     }
     if (s->res_d) gpudiff_dbatch_free(c, s->res_d);
+    if (s->cs) {
+        (void)hipStreamSynchronize(s->cs);
+        (void)hipStreamDestroy(s->cs);
+    }
     for (void* p : {(void*)s->space[0], (void*)s->space[1], (void*)s->used_dev, (void*)s->slots, (void*)s->ctr,
                     (void*)s->sizes, (void*)s->tile_sums, (void*)s->scratch, (void*)s->res_stage, (void*)s->res_ups,
                     (void*)s->res_err})
