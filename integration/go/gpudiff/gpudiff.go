@@ -41,8 +41,15 @@ func errOf(rc C.int) error {
 
 // Open creates an engine on HIP device `device` (-1 = current).
 func Open(device int) (*Engine, error) {
+	return OpenWith(device, 0)
+}
+
+// OpenWith is Open with GPUDIFF_OPT_* flags, e.g. C.GPUDIFF_OPT_DEVICE_ENCODE to send the
+// batcher's JSON pairs to the GPU tokenizer (kernel K0) instead of the host encoder.
+func OpenWith(device int, flags uint32) (*Engine, error) {
 	var opts C.gpudiff_opts
 	opts.device = C.int32_t(device)
+	opts.flags = C.uint32_t(flags)
 	var ctx *C.gpudiff_ctx
 	if err := errOf(C.gpudiff_open(&opts, &ctx)); err != nil {
 		return nil, err
@@ -245,11 +252,22 @@ type Store struct {
 }
 
 func (e *Engine) NewStore(maxSlots uint32, spaceBytes uint64, maxEvents uint32) (*Store, error) {
+	return e.NewStoreEx(maxSlots, spaceBytes, maxEvents, false)
+}
+
+// NewStoreEx with deviceEncode uploads raw JSON and encodes it on the GPU (kernel K0); the
+// batcher already keeps each batch's buffers until gpudiff_wait returns and waits in order,
+// which is what that mode requires.
+func (e *Engine) NewStoreEx(maxSlots uint32, spaceBytes uint64, maxEvents uint32, deviceEncode bool) (*Store, error) {
 	e.mu.Lock()
 	defer e.mu.Unlock()
+	var flags C.uint32_t
+	if deviceEncode {
+		flags = C.GPUDIFF_STORE_DEVICE_ENCODE
+	}
 	var s *C.gpudiff_store
-	if err := errOf(C.gpudiff_store_create(e.ctx, C.uint32_t(maxSlots), C.uint64_t(spaceBytes),
-		C.uint32_t(maxEvents), &s)); err != nil {
+	if err := errOf(C.gpudiff_store_create_ex(e.ctx, C.uint32_t(maxSlots), C.uint64_t(spaceBytes),
+		C.uint32_t(maxEvents), flags, &s)); err != nil {
 		return nil, err
 	}
 	return &Store{e: e, s: s}, nil
