@@ -637,7 +637,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                                                  uint32_t c_end, uint64_t* __restrict__ ah, uint8_t* __restrict__ ak,
                                                  uint32_t arena_off, uint32_t arena_per_wave, uint32_t arena_stride,
                                                  uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
-                                                 uint64_t mask, uint32_t* __restrict__ summary) {
+                                                 uint64_t mask, uint32_t* __restrict__ summary,
+                                                 uint32_t sub_shift) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -645,9 +646,15 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
-    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
-        const uint32_t p0 = c << 6;
-        const uint32_t cnt = min(64u, n - p0);
+    // work item = 1/2^sub_shift of a 64-pair chunk: small batches of large pairs spread over
+    // the whole grid; items of one chunk add their counts into chunk_counts atomically
+    const uint32_t per = 64u >> sub_shift;
+    const uint32_t nitems = (c_end - c_begin) << sub_shift;
+    for (uint32_t it = wave; it < nitems; it += nwaves) {
+        const uint32_t c = c_begin + (it >> sub_shift);
+        const uint32_t p0 = (c << 6) + (it & ((1u << sub_shift) - 1u)) * per;
+        if (p0 >= n) continue;
+        const uint32_t cnt = min(per, n - p0);
         uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0;
         for (uint32_t k = 0; k < cnt; k++) {
             const gpudiff_pair_row r = rows[p0 + k];
@@ -694,7 +701,17 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
         const uint32_t nt = popc64(ballot(myflag & F_STATUS));
         const uint32_t nd = popc64(ballot(dirty));
         const uint32_t cs = wave_sum(dirty ? mycap : 0u);
-        if (lane == 0) chunk_counts[c] = make_uint4(ns, nt, nd, cs);
+        if (lane == 0) {
+            if (!sub_shift) {
+                chunk_counts[c] = make_uint4(ns, nt, nd, cs);
+            } else if (ns | nt | nd | cs) {
+                uint32_t* cc = (uint32_t*)(chunk_counts + c);
+                atomicAdd(cc + 0, ns);
+                atomicAdd(cc + 1, nt);
+                atomicAdd(cc + 2, nd);
+                atomicAdd(cc + 3, cs);
+            }
+        }
     }
     // one plain store per wave (a same-address atomic per deferred pair
     // serialises across the XCDs)
@@ -807,22 +824,40 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
     return hipGetLastError();
 }
 
-uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks) {
+static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     // 5 resident 256-thread blocks per CU (20 waves/CU, the occupancy the fused
     // kernel's 90 VGPRs allow): with joins inside K2 the extra waves keep HBM
     // streaming while others join (tools/ab_k2.py: 11.18 vs 11.59 ms at 4)
-    const uint32_t cap = 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 5u);
-    return grid_for(nchunks, cap) * 4u;
+    return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 5u);
+}
+
+// 64-pair chunks split into 2^k items until there are >= 4 items per resident
+// wave (config3's 156k chunks: k = 0; config4's 1.6k chunks of deep pairs: k = 4)
+static uint32_t k2_sub_shift(const DiffBuffers& b, uint32_t nchunks) {
+    const uint64_t want = 4ull * 4u * k2_cap_blocks(b);
+    uint32_t k = 0;
+    while (k < 6 && (uint64_t)nchunks << k < want) k++;
+    return k;
+}
+
+uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks) {
+    const uint64_t items = (uint64_t)nchunks << k2_sub_shift(b, nchunks);
+    return grid_for(items, k2_cap_blocks(b)) * 4u;
 }
 
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
                           uint32_t nsegs) {
     const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
     uint4* cc = (uint4*)b.chunk_counts;
+    const uint32_t sub = k2_sub_shift(b, c1 - c0);
+    if (sub) {
+        hipError_t e = hipMemsetAsync(cc + c0, 0, (size_t)(c1 - c0) * sizeof(uint4), s);
+        if (e != hipSuccess) return e;
+    }
     // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
-               b.arena_per_wave, b.path_src, b.path_cnt, b.hash_mask, b.summary
+               b.arena_per_wave, b.path_src, b.path_cnt, b.hash_mask, b.summary, sub
     switch (b.k2_variant) {  // tuning variants (GPUDIFF_OPT_K2_VARIANT_SHIFT); 0 is the default
         case 1: k_compare<false, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
         case 2: k_compare<true, 8, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
