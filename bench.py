@@ -3,10 +3,16 @@
 
 Workload (BASELINE.json configs[2], the metric's own configuration): 10M mixed
 object pairs (40% ConfigMap/Secret, 40% Deployment, 20% medium CRD) across
-100k logical clusters, 5% mutated, synthetic (seed 20211004+3).  The
-population is fixed (strong scaling); each rank holds the LPT shard of whole
-logical clusters assigned to it, encoded on the host with the product encoder
-and resident in HBM before timing.
+100k logical clusters, 5% mutated, synthetic (seed 20211004+3).
+
+Scaling (--scaling, default weak): pairs are independent and shard by logical
+cluster with no data-path exchange, so per-GPU work is fixed -- at N GPUs the
+node-wide population is N x the config (N x 10M pairs over N x 100k logical
+clusters, same seed and mix) and each rank holds the LPT shard of whole
+logical clusters assigned to it (~10M pairs, one config3-sized population per
+GPU).  --scaling strong keeps the population fixed at the config's size and
+splits it N ways instead.  Either way the pairs are encoded on the host with
+the product encoder and are resident in HBM before timing.
 
 A step = one diff pass of the hot path (K2 compare, K3 compaction, K4
 changed-path merge-join, K5/K6 path emit) over the rank's resident pairs, plus
@@ -47,6 +53,9 @@ def main():
                     help="config5: encode events on the GPU (K0, raw JSON up) or on the host")
     ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")
     ap.add_argument("--clusters", type=int, default=0)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: per-GPU work fixed (node population = N x the config); "
+                         "strong: the config's population split N ways")
     ap.add_argument("--chunk", type=int, default=262144)
     ap.add_argument("--threads", type=int, default=0, help="host encode threads (default min(16, cpus))")
     ap.add_argument("--sample", type=int, default=600, help="pairs checked bit-exact vs the oracle (JSON path)")
@@ -85,7 +94,9 @@ def main():
     threads = args.threads or max(1, min(16, ncpu))
 
     eng = G.Engine(device=local_rank, encode_threads=threads, stream=stream.cuda_stream, timing=True)
-    cfg = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=args.clusters)
+    base = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=args.clusters)
+    mult = world if args.scaling == "weak" else 1
+    cfg = S.make_cfg(args.config, n_pairs=base.n_pairs * mult, n_clusters=base.n_clusters * mult)
     pop = S.Population(cfg, world, rank)
     n = pop.n
     log("config %s: %d pairs / %d clusters total; this rank %d pairs / %d clusters; %d host threads" % (
@@ -249,13 +260,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded object populations, SURVEY.md 8d; no real cluster data)",
             "config": {
-                "workload": "%s: %d pairs / %d logical clusters, %.0f%% mutated (%s)" % (
-                    args.config, cfg.n_pairs, cfg.n_clusters, cfg.mutate_frac * 100,
+                "workload": "%s: %d pairs / %d logical clusters node-wide%s, %.0f%% mutated (%s)" % (
+                    args.config, cfg.n_pairs, cfg.n_clusters,
+                    " (%d x %d pairs / %d clusters, one per GPU)" % (world, base.n_pairs, base.n_clusters)
+                    if mult > 1 else "", cfg.mutate_frac * 100,
                     "40% ConfigMap/Secret, 40% Deployment, 20% CRD" if args.config == "config3" else args.config),
                 "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9,
                 "parallelism": "shard-by-logical-cluster x%d (LPT)%s" % (

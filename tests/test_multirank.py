@@ -36,6 +36,23 @@ def test_synth_shards_partition_population(world):
     assert max(sizes) - min(sizes) <= max(sizes) * 0.2  # LPT keeps ranks within a few %
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_weak_scaling_shards_are_one_config_each(world):
+    """bench.py --scaling weak: the node population is world x config3 and the
+    LPT shard every rank holds is one config3-sized population (per-GPU work
+    fixed as N grows)."""
+    base = S.make_cfg("config3")
+    cfg = S.make_cfg("config3", n_pairs=base.n_pairs * world, n_clusters=base.n_clusters * world)
+    sizes, clusters = [], []
+    for r in range(world):
+        p = S.Population(cfg, world, r)
+        sizes.append(p.n)
+        clusters.append(p.n_clusters)
+        p.close()
+    assert sum(sizes) == base.n_pairs * world and sum(clusters) <= base.n_clusters * world
+    assert max(abs(x - base.n_pairs) for x in sizes) <= base.n_pairs * 0.001
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
