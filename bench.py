@@ -44,8 +44,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5"],
-                    help="config5 = watch replay through the device-resident object store (bench_replay.py)")
+    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5", "upsert"],
+                    help="config5 = watch replay through the device-resident object store (bench_replay.py); "
+                         "upsert = the write path's request bodies, kernel K10 (bench_upsert.py)")
+    ap.add_argument("--docs", type=int, default=131072, help="upsert: documents resident in HBM")
     ap.add_argument("--batch", type=int, default=65536, help="config5: events per batch")
     ap.add_argument("--batches", type=int, default=40, help="config5: timed batches")
     ap.add_argument("--warmup-batches", type=int, default=4, help="config5: untimed batches")
@@ -67,6 +69,11 @@ def main():
                          "profiles/r*_pmc_summary.json, used only if it was measured on this same workload; "
                          "'none' to skip)")
     args = ap.parse_args()
+
+    if args.config == "upsert":
+        import bench_upsert
+        args.sample = min(args.sample, 300)
+        return bench_upsert.run(args)
 
     if args.config == "config5":
         import bench_replay

@@ -69,6 +69,8 @@ enum {
 #define GPUDIFF_TOK_DEPTH 6   /* nesting deeper than 255 */
 #define GPUDIFF_TOK_SIZE 7    /* document larger than 16 MiB */
 #define GPUDIFF_TOK_SPACE 8   /* output space exhausted */
+#define GPUDIFF_TOK_FLOAT 9   /* K10 (write path): a float64 value (Go's shortest formatting is done on the host) */
+#define GPUDIFF_TOK_WIDE 10   /* K10: an object with more than 2048 members (quadratic key ranking) */
 
 /* changed-path kinds (low 2 bits); bit 7 = status region */
 #define GPUDIFF_PATH_CHANGED 0u        /* present in both, value differs */
@@ -323,6 +325,67 @@ int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, ui
  * previous call (scan, tree, values, hashes, sort, blob, -, -); enable != 0
  * keeps recording */
 int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
+
+/* ---- write path: the request body for a dirty object ----
+ * GPUDIFF_UPSERT_SPEC: what upsertIntoDownstream hands to client.Create
+ *   (pkg/syncer/specsyncer.go:86-110): the object with metadata.uid and
+ *   metadata.resourceVersion removed and every owner reference whose name equals
+ *   the kcp.dev/owned-by label dropped (the rest normalized as
+ *   Unstructured.SetOwnerReferences writes them; the field removed when none
+ *   remain).
+ * GPUDIFF_UPSERT_STATUS: updateStatusInUpstream's object (statussyncer.go:41-48)
+ *   before the live resourceVersion is set: uid and resourceVersion removed.
+ * Bytes are exactly json.NewEncoder(w).Encode(obj.Object) of Go 1.16 -- what the
+ * dynamic client sends (UnstructuredJSONScheme): keys sorted, HTML-safe string
+ * escaping, shortest floats, trailing newline.  Kernel K10 emits the bodies in
+ * HBM; documents outside its subset (floats, duplicate keys, undecodable input,
+ * ...) are marshalled by the host path, with identical bytes. */
+#define GPUDIFF_UPSERT_SPEC 0u
+#define GPUDIFF_UPSERT_STATUS 1u
+
+typedef struct gpudiff_bodies {
+    size_t n;
+    const uint64_t* offsets;  /* n + 1: body i = bytes[offsets[i], offsets[i + 1]) */
+    const uint8_t* bytes;
+    const int32_t* status;    /* 0 = body; GPUDIFF_E_DECODE = Go could not decode the object (empty body) */
+    const uint8_t* source;    /* GPUDIFF_BODY_DEVICE / GPUDIFF_BODY_HOST per document */
+    const int32_t* k10_status; /* K10's GPUDIFF_TOK_* per document (why the host took it over) */
+    size_t n_host;            /* documents the host marshalled */
+    void* internal;
+} gpudiff_bodies;
+#define GPUDIFF_BODY_DEVICE 0u
+#define GPUDIFF_BODY_HOST 1u
+
+/* n documents (JSON objects) -> n bodies; synchronous.  Release with
+ * gpudiff_bodies_release. */
+int gpudiff_upsert_bodies(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, size_t n, uint32_t mode,
+                          gpudiff_bodies* out);
+void gpudiff_bodies_release(gpudiff_ctx* ctx, gpudiff_bodies* b);
+
+/* The staged form: documents uploaded once into HBM (gpudiff_wbatch_create),
+ * K10 launched on the context's stream (gpudiff_wbatch_run, asynchronous; with
+ * GPUDIFF_OPT_TIMING each launch is bracketed by HIP events and
+ * gpudiff_wbatch_stats.k10_ms is the mean), bodies read back and host-completed
+ * (gpudiff_wbatch_fetch). */
+typedef struct gpudiff_wbatch gpudiff_wbatch;
+typedef struct gpudiff_wbatch_stats {
+    uint64_t n_docs, json_bytes, body_bytes;  /* body_bytes: K10's output (valid after a fetch) */
+    uint64_t scratch_bytes, out_cap_bytes;
+    double k10_ms;                            /* mean K10 duration over the timed runs */
+    uint64_t runs;                            /* timed runs (GPUDIFF_OPT_TIMING) */
+} gpudiff_wbatch_stats;
+int gpudiff_wbatch_create(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, size_t n, uint32_t mode,
+                          gpudiff_wbatch** out);
+int gpudiff_wbatch_run(gpudiff_ctx* ctx, gpudiff_wbatch* wb);
+int gpudiff_wbatch_fetch(gpudiff_ctx* ctx, gpudiff_wbatch* wb, gpudiff_bodies* out);
+int gpudiff_wbatch_stats_get(const gpudiff_wbatch* wb, gpudiff_wbatch_stats* st);
+void gpudiff_wbatch_free(gpudiff_ctx* ctx, gpudiff_wbatch* wb);
+
+/* The host path (Go-exact restatement; also what completes K10's deferrals):
+ * one body into out[0, cap).  *out_len = the body length (also when it does not
+ * fit: then GPUDIFF_E_CAPACITY).  GPUDIFF_E_DECODE if Go cannot decode doc. */
+int gpudiff_upsert_body_host(const uint8_t* doc, size_t len, uint32_t mode, uint8_t* out, size_t cap,
+                             size_t* out_len);
 
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,

@@ -1,0 +1,471 @@
+// Device helpers shared by K0 (tokenize.hip) and K10 (marshal.hip): wave
+// primitives, Go string/number decoding, XXH64 over virtual word streams.
+// Internal; each including TU gets its own copy (anonymous namespace).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpudiff.h"
+#include "decfloat.h"
+#include "tokenize.h"
+#include "xxh64.h"
+
+namespace gd {
+
+namespace {
+
+constexpr uint32_t TK_CLOSEQ = 0x01u;     // token code of a closing quote
+constexpr uint32_t TK_OPENQ_SLOW = 0x02u; // opening quote of a string that needs decoding
+// opening quotes of the exact strings "metadata", "status", "labels", "annotations"
+constexpr uint32_t TK_KEY_META = 0x03u, TK_KEY_STATUS = 0x04u, TK_KEY_LABELS = 0x05u, TK_KEY_ANNOT = 0x06u;
+constexpr uint32_t POS_MASK = 0xFFFFFFu;
+
+// node info word
+constexpr uint32_t NI_TAG = 7u;
+constexpr uint32_t NI_LEAF = 1u << 3;
+constexpr uint32_t NI_ATOM = 1u << 4;
+constexpr uint32_t NI_SLOW = 1u << 5;
+constexpr uint32_t NI_STR = 1u << 6;
+constexpr uint32_t NI_REG_SHIFT = 8;
+constexpr uint32_t NI_DEPTH_SHIFT = 16;
+constexpr uint32_t KEYBIT = 0x80000000u;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+enum : uint32_t { R_NONE = 0, R_SPEC = 1, R_META = 2, R_LABELS = 3, R_ANNOT = 4, R_STATUS = 5 };
+enum : uint32_t { E_ROOT, E_KEY, E_KEYCLOSE, E_COLON, E_VALUE, E_STRCLOSE, E_NEXT, E_END };
+
+constexpr uint32_t kMaxDepth = 255;
+constexpr uint32_t kWavesPerBlock = 4;
+constexpr uint32_t kLdsPerWave = 5120;
+constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+__device__ __forceinline__ uint64_t mask_lt(uint32_t n) { return n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL); }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
+    return ((uint64_t)rdlane((uint32_t)(v >> 32), l) << 32) | rdlane((uint32_t)v, l);
+}
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        uint32_t o = shfl32(v, lane >= d ? lane - d : lane);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return v;
+}
+// the wave's own global writes become visible to its other lanes
+__device__ __forceinline__ void wave_sync() { __threadfence_block(); }
+
+// unaligned 8-byte read; up to 15 bytes past p must be readable
+__device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint64_t lo = q[0];
+    if (!sh) return lo;
+    return (lo >> sh) | (q[1] << (64u - sh));
+}
+
+// XXH64 over a virtual byte stream given as 8-byte little-endian words
+template <class F>
+__device__ __forceinline__ uint64_t xxh64_words(uint64_t seed, uint32_t len, F word) {
+    uint64_t h;
+    const uint32_t stripes = len >> 5;
+    if (stripes) {
+        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+#pragma unroll 2
+        for (uint32_t s = 0; s < stripes; s++) {
+            v1 = xround(v1, word(4 * s));
+            v2 = xround(v2, word(4 * s + 1));
+            v3 = xround(v3, word(4 * s + 2));
+            v4 = xround(v4, word(4 * s + 3));
+        }
+        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = seed + XP5;
+    }
+    h += len;
+    const uint32_t rem = len & 31u;
+    uint64_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+        if (8 * j < rem) w[j] = word(4 * stripes + j);
+    h = xxh64_tail(h, w, rem);
+    return xavalanche(h);
+}
+
+// path component hashes: 0x01 u32le(len) key | 0x02 u32le(index)
+__device__ __forceinline__ uint64_t hash_key(uint64_t seed, const uint8_t* k, uint32_t klen) {
+    return xxh64_words(seed, klen + 5u, [&](uint32_t i) -> uint64_t {
+        if (i == 0) return 0x01ull | ((uint64_t)klen << 8) | (ld8u(k) << 40);
+        return ld8u(k + 8u * i - 5u);
+    });
+}
+__device__ __forceinline__ uint64_t hash_index(uint64_t seed, uint32_t idx) {
+    return xxh64_words(seed, 5u, [&](uint32_t) -> uint64_t { return 0x02ull | ((uint64_t)idx << 8); });
+}
+__device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, uint32_t len) {
+    return xxh64_words(0, len, [&](uint32_t i) -> uint64_t { return ld8u(p + 8u * i); });
+}
+
+__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
+    return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
+}
+__device__ __forceinline__ uint32_t meta_arena(uint32_t m) {
+    return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) + 15u) & ~15u) : 0u;
+}
+
+__device__ __forceinline__ bool is_ws(uint32_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool is_delim(uint32_t c) {
+    return is_ws(c) || c == ',' || c == '}' || c == ']' || c == ':' || c == '"' || c == '{' || c == '[';
+}
+__device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
+
+// utf8.DecodeRune validity (json.cpp go_rune_len): sequence size, 0 if invalid
+__device__ int rune_len(const uint8_t* p, const uint8_t* end) {
+    const uint32_t c0 = p[0];
+    int size;
+    uint32_t lo = 0x80, hi = 0xBF;
+    if (c0 < 0x80) return 1;
+    if (c0 >= 0xC2 && c0 <= 0xDF) size = 2;
+    else if (c0 == 0xE0) { size = 3; lo = 0xA0; }
+    else if ((c0 >= 0xE1 && c0 <= 0xEC) || c0 == 0xEE || c0 == 0xEF) size = 3;
+    else if (c0 == 0xED) { size = 3; hi = 0x9F; }
+    else if (c0 == 0xF0) { size = 4; lo = 0x90; }
+    else if (c0 >= 0xF1 && c0 <= 0xF3) size = 4;
+    else if (c0 == 0xF4) { size = 4; hi = 0x8F; }
+    else return 0;
+    if (end - p < size) return 0;
+    if (p[1] < lo || p[1] > hi) return 0;
+    for (int k = 2; k < size; k++)
+        if (p[k] < 0x80 || p[k] > 0xBF) return 0;
+    return size;
+}
+__device__ __forceinline__ int hexv(uint32_t c) {
+    if (c - '0' < 10u) return (int)(c - '0');
+    if (c - 'a' < 6u) return (int)(c - 'a' + 10);
+    if (c - 'A' < 6u) return (int)(c - 'A' + 10);
+    return -1;
+}
+__device__ int getu4(const uint8_t* p, const uint8_t* end) {
+    if (end - p < 6 || p[0] != '\\' || p[1] != 'u') return -1;
+    int v = 0;
+    for (int k = 2; k < 6; k++) {
+        const int h = hexv(p[k]);
+        if (h < 0) return -1;
+        v = (v << 4) | h;
+    }
+    return v;
+}
+__device__ __forceinline__ uint8_t* put_utf8(uint8_t* o, uint32_t r) {
+    if (r < 0x80) {
+        *o++ = (uint8_t)r;
+    } else if (r < 0x800) {
+        *o++ = (uint8_t)(0xC0 | (r >> 6));
+        *o++ = (uint8_t)(0x80 | (r & 0x3F));
+    } else if (r < 0x10000) {
+        *o++ = (uint8_t)(0xE0 | (r >> 12));
+        *o++ = (uint8_t)(0x80 | ((r >> 6) & 0x3F));
+        *o++ = (uint8_t)(0x80 | (r & 0x3F));
+    } else {
+        *o++ = (uint8_t)(0xF0 | (r >> 18));
+        *o++ = (uint8_t)(0x80 | ((r >> 12) & 0x3F));
+        *o++ = (uint8_t)(0x80 | ((r >> 6) & 0x3F));
+        *o++ = (uint8_t)(0x80 | (r & 0x3F));
+    }
+    return o;
+}
+
+// Go string decoding (encoding/json unquote, json.cpp JsonParser::string):
+// raw bytes [p, q) between the quotes -> dst (never longer than the raw
+// bytes); returns the decoded length, or -1 for the host to decide (invalid
+// escape or control character: a Go error; invalid UTF-8: U+FFFD repair)
+__device__ int decode_string(const uint8_t* p, const uint8_t* q, const uint8_t* end, uint8_t* dst) {
+    uint8_t* o = dst;
+    while (p < q) {
+        const uint32_t c = *p;
+        if (c == '\\') {
+            if (end - p < 2) return -1;
+            const uint32_t e = p[1];
+            uint32_t b = 0;
+            switch (e) {
+                case '"': b = '"'; break;
+                case '\\': b = '\\'; break;
+                case '/': b = '/'; break;
+                case 'b': b = '\b'; break;
+                case 'f': b = '\f'; break;
+                case 'n': b = '\n'; break;
+                case 'r': b = '\r'; break;
+                case 't': b = '\t'; break;
+                case 'u': {
+                    int rr = getu4(p, end);
+                    if (rr < 0) return -1;
+                    p += 6;
+                    if (rr >= 0xD800 && rr < 0xE000) {
+                        const int rr1 = getu4(p, end);
+                        if (rr < 0xDC00 && rr1 >= 0xDC00 && rr1 < 0xE000) {
+                            const uint32_t dec = (((uint32_t)(rr - 0xD800) << 10) | (uint32_t)(rr1 - 0xDC00)) + 0x10000u;
+                            o = put_utf8(o, dec);
+                            p += 6;
+                            continue;
+                        }
+                        rr = 0xFFFD;
+                    }
+                    o = put_utf8(o, (uint32_t)rr);
+                    continue;
+                }
+                default: return -1;
+            }
+            *o++ = (uint8_t)b;
+            p += 2;
+            continue;
+        }
+        if (c < 0x20) return -1;
+        if (c < 0x80) {
+            *o++ = (uint8_t)c;
+            p++;
+            continue;
+        }
+        const int l = rune_len(p, end);
+        if (l == 0) return -1;  // U+FFFD repair would outgrow the in-place area: host encoder
+        for (int k = 0; k < l; k++) *o++ = p[k];
+        p += l;
+    }
+    return (int)(o - dst);
+}
+
+// literal / number at p (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error
+__device__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+    const uint32_t c = *p;
+    *val = 0;
+    if (c == 't' || c == 'f' || c == 'n') {
+        const uint32_t n = c == 'f' ? 5u : 4u;
+        if ((uint64_t)(end - p) < n) return GPUDIFF_TOK_SYNTAX;
+        const uint64_t w = ld8u(p) & ((1ull << (8 * n)) - 1ull);
+        const uint64_t want = c == 't' ? 0x65757274ull : c == 'f' ? 0x65736c6166ull : 0x6c6c756eull;
+        if (w != want) return GPUDIFF_TOK_SYNTAX;
+        if (p + n < end && !is_delim(p[n])) return GPUDIFF_TOK_SYNTAX;
+        *tag = c == 't' ? GPUDIFF_TAG_TRUE : c == 'f' ? GPUDIFF_TAG_FALSE : GPUDIFF_TAG_NULL;
+        return GPUDIFF_TOK_OK;
+    }
+    // number grammar: -? (0 | [1-9][0-9]*) (. [0-9]+)? ([eE] [+-]? [0-9]+)?
+    const uint8_t* q = p;
+    const bool neg = c == '-';
+    if (neg) q++;
+    if (q >= end) return GPUDIFF_TOK_SYNTAX;
+    if (*q == '0') {
+        q++;
+    } else if (*q >= '1' && *q <= '9') {
+        while (q < end && is_digit(*q)) q++;
+    } else {
+        return GPUDIFF_TOK_SYNTAX;
+    }
+    const uint8_t* int_end = q;
+    const uint8_t* frac_beg = q;
+    const uint8_t* frac_end = q;
+    bool is_int = true;
+    if (q < end && *q == '.') {
+        is_int = false;
+        q++;
+        frac_beg = q;
+        if (q >= end || !is_digit(*q)) return GPUDIFF_TOK_SYNTAX;
+        while (q < end && is_digit(*q)) q++;
+        frac_end = q;
+    }
+    int64_t ex = 0;
+    if (q < end && (*q == 'e' || *q == 'E')) {
+        is_int = false;
+        q++;
+        bool eneg = false;
+        if (q < end && (*q == '+' || *q == '-')) {
+            eneg = *q == '-';
+            q++;
+        }
+        if (q >= end || !is_digit(*q)) return GPUDIFF_TOK_SYNTAX;
+        while (q < end && is_digit(*q)) {
+            if (ex < 100000) ex = ex * 10 + (*q - '0');
+            q++;
+        }
+        if (eneg) ex = -ex;
+    }
+    if (q < end && !is_delim(*q)) return GPUDIFF_TOK_SYNTAX;
+    const uint8_t* d0 = p + (neg ? 1 : 0);
+    if (is_int) {  // strconv.ParseInt(s, 10, 64)
+        const uint64_t lim = neg ? (1ull << 63) : ((1ull << 63) - 1ull);
+        uint64_t v = 0;
+        bool ovf = false;
+        for (const uint8_t* d = d0; d < int_end; d++) {
+            const uint64_t dig = (uint64_t)(*d - '0');
+            if (v > (lim - dig) / 10) {
+                ovf = true;
+                break;
+            }
+            v = v * 10 + dig;
+        }
+        if (!ovf) {
+            *tag = GPUDIFF_TAG_INT;
+            *val = neg ? (0ull - v) : v;
+            return GPUDIFF_TOK_OK;
+        }
+        // beyond int64: convertNumber falls back to float64
+    }
+    // strconv.ParseFloat on the significant digits (first to last nonzero),
+    // <= 19 of them: decfloat.h (Clinger's exact path, else Eisel-Lemire)
+    const uint32_t n_int = (uint32_t)(int_end - d0), n_frac = (uint32_t)(frac_end - frac_beg);
+    const uint32_t n_all = n_int + n_frac;
+    auto digit = [&](uint32_t k) -> uint32_t { return (k < n_int ? d0[k] : frac_beg[k - n_int]) - '0'; };
+    uint32_t first = n_all, last = 0;
+    for (uint32_t k = 0; k < n_all; k++)
+        if (digit(k)) {
+            if (first == n_all) first = k;
+            last = k;
+        }
+    *tag = GPUDIFF_TAG_FLOAT;
+    if (first == n_all) {
+        *val = 0;  // +-0.0 -> +0.0 (Go ==)
+        return GPUDIFF_TOK_OK;
+    }
+    if (last - first + 1 > 19) return GPUDIFF_TOK_NUMBER;
+    uint64_t w = 0;
+    for (uint32_t k = first; k <= last; k++) w = w * 10 + digit(k);
+    const int64_t e10 = ex - (int64_t)n_frac + (int64_t)(n_all - 1 - last);
+    uint64_t bits;
+    if (!decimal_to_double(w, e10, neg, &bits)) return GPUDIFF_TOK_NUMBER;
+    *val = bits;
+    return GPUDIFF_TOK_OK;
+}
+
+// ---- K10 (write path) helpers: Go 1.16 encodeState.string(s, escapeHTML=true)
+// over decoded (valid UTF-8) bytes; strconv.AppendInt
+__device__ __forceinline__ uint32_t go_esc_len(const uint8_t* s, uint32_t n) {
+    uint32_t out = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t c = s[i];
+        if (c < 0x80u) {
+            if (c == '"' || c == '\\' || c == '\n' || c == '\r' || c == '\t') out += 2;
+            else if (c < 0x20u || c == '<' || c == '>' || c == '&') out += 6;
+            else out += 1;
+        } else if (c == 0xE2u && i + 2 < n && s[i + 1] == 0x80u && (s[i + 2] == 0xA8u || s[i + 2] == 0xA9u)) {
+            out += 6;  // U+2028 / U+2029
+            i += 2;
+        } else {
+            out += 1;
+        }
+    }
+    return out;
+}
+__device__ __forceinline__ uint8_t* go_esc_put(uint8_t* o, const uint8_t* s, uint32_t n) {
+    const char* hx = "0123456789abcdef";
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t c = s[i];
+        if (c < 0x80u) {
+            if (c == '"' || c == '\\') {
+                *o++ = '\\';
+                *o++ = (uint8_t)c;
+            } else if (c == '\n' || c == '\r' || c == '\t') {
+                *o++ = '\\';
+                *o++ = c == '\n' ? 'n' : c == '\r' ? 'r' : 't';
+            } else if (c < 0x20u || c == '<' || c == '>' || c == '&') {
+                *o++ = '\\';
+                *o++ = 'u';
+                *o++ = '0';
+                *o++ = '0';
+                *o++ = (uint8_t)hx[c >> 4];
+                *o++ = (uint8_t)hx[c & 15u];
+            } else {
+                *o++ = (uint8_t)c;
+            }
+        } else if (c == 0xE2u && i + 2 < n && s[i + 1] == 0x80u && (s[i + 2] == 0xA8u || s[i + 2] == 0xA9u)) {
+            *o++ = '\\';
+            *o++ = 'u';
+            *o++ = '2';
+            *o++ = '0';
+            *o++ = '2';
+            *o++ = s[i + 2] == 0xA8u ? '8' : '9';
+            i += 2;
+        } else {
+            *o++ = (uint8_t)c;
+        }
+    }
+    return o;
+}
+__device__ __forceinline__ uint32_t i64_len(int64_t v) {
+    uint64_t u = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
+    uint32_t n = v < 0 ? 2u : 1u;
+    while (u >= 10u) {
+        u /= 10u;
+        n++;
+    }
+    return n;
+}
+__device__ __forceinline__ void i64_put(uint8_t* o, int64_t v, uint32_t n) {
+    uint64_t u = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
+    for (uint32_t k = n; k-- > (v < 0 ? 1u : 0u);) {
+        o[k] = (uint8_t)('0' + u % 10u);
+        u /= 10u;
+    }
+    if (v < 0) o[0] = '-';
+}
+template <class T>
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, uint32_t al, const T* b, uint32_t bl) {
+    if (al != bl) return false;
+    for (uint32_t i = 0; i < al; i++)
+        if (a[i] != (uint8_t)b[i]) return false;
+    return true;
+}
+// Go string order (bytes, then length)
+__device__ __forceinline__ int bytes_cmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+    const uint32_t n = al < bl ? al : bl;
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint64_t x = __builtin_bswap64(ld8u(a + i)), y = __builtin_bswap64(ld8u(b + i));
+        if (x != y) return x < y ? -1 : 1;
+    }
+    for (; i < n; i++)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return al < bl ? -1 : al > bl ? 1 : 0;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return v;
+}
+constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u;
+constexpr uint32_t kMarshalMaxMembers = 2048;
+constexpr int kModeEncode = 0, kModeMarshal = 1;
+
+struct Scratch {
+    uint32_t* tok;
+    uint4* rec;
+    uint64_t *h, *fp, *val, *skey;
+    uint32_t *meta, *order, *sidx;
+    uint8_t* str;
+};
+
+}  // namespace
+
+}  // namespace gd

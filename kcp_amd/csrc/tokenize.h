@@ -69,6 +69,40 @@ __host__ __device__ inline uint64_t tok_scratch_bytes(uint32_t len) { return tok
 // upper bound of a document's blob (leaf >= 2 JSON bytes -> 28 B; segment pads)
 __host__ __device__ inline uint64_t tok_blob_bound(uint32_t len) { return 14ull * len + 64u; }
 
+// K10 (k_encode_docs in marshal mode, the write path): per-document working
+// area.  tok/rec/str are laid out as phases 1-2 of K0 expect; the rest holds
+// one word per node (own text size, key size, subtree size, flags, child
+// count, child-list base, child list, sibling prefix sums, rank, value start,
+// depth order) and the decoded int64 / string location.
+struct MarshalLayout {
+    uint64_t tok, rec, str, val, vsz, ksz, sz, fl, nch, base, kids, pre, rank, vst, order, total;
+};
+__host__ __device__ inline MarshalLayout marshal_layout(uint32_t len) {
+    MarshalLayout L;
+    const uint64_t nc = node_cap(len);
+    L.tok = 0;
+    L.rec = tok_align(4ull * tok_cap(len));
+    L.str = L.rec + tok_align(16ull * nc);
+    L.val = L.str + tok_align((uint64_t)len + 32u);
+    L.vsz = L.val + tok_align(8ull * nc);
+    L.ksz = L.vsz + tok_align(4ull * nc);
+    L.sz = L.ksz + tok_align(4ull * nc);
+    L.fl = L.sz + tok_align(4ull * nc);
+    L.nch = L.fl + tok_align(4ull * nc);
+    L.base = L.nch + tok_align(4ull * nc);
+    L.kids = L.base + tok_align(4ull * nc);
+    L.pre = L.kids + tok_align(4ull * nc);
+    L.rank = L.pre + tok_align(4ull * nc);
+    L.vst = L.rank + tok_align(4ull * nc);
+    L.order = L.vst + tok_align(4ull * nc);
+    L.total = L.order + tok_align(4ull * nc);
+    return L;
+}
+__host__ __device__ inline uint64_t marshal_scratch_bytes(uint32_t len) { return marshal_layout(len).total; }
+// output room per document: a body longer than this is left to the host
+// (escaping can grow a string 6-fold, owner references gain their fixed keys)
+__host__ __device__ inline uint64_t marshal_out_cap(uint32_t len) { return ((2ull * len + 512u) + 15u) & ~15ull; }
+
 constexpr uint32_t kTokMaxLen = (1u << 24) - 64u;  // token words hold 24-bit positions
 constexpr uint32_t kTokSlack = 32u;                 // readable bytes K0 needs after each staged document
 
@@ -120,6 +154,11 @@ hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, con
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
                               TokOut* out, const DSlot* slots = nullptr, const DocLink* links = nullptr,
                               uint32_t variant = 0);
+// K10: the write path's request bodies (GPUDIFF_UPSERT_*): docs[i].pad holds
+// the body's u64 offset in `bodies` (room: marshal_out_cap(json_len)); out[i]
+// gets {off, bytes, status}.  A nonzero status leaves the document to the host.
+hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                               uint8_t* bodies, uint32_t mode, TokOut* out);
 // K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)
 hipError_t launch_collide(hipStream_t s, const DocLink* links, const TokOut* outs, const DSlot* slots, uint32_t n,
                           const uint8_t* space, uint8_t* coll);

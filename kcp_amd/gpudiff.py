@@ -87,7 +87,23 @@ class ObjInfo(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
-TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SIZE, TOK_SPACE = range(9)
+TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SIZE, TOK_SPACE, TOK_FLOAT, TOK_WIDE = \
+    range(11)
+
+UPSERT_SPEC, UPSERT_STATUS = 0, 1
+BODY_DEVICE, BODY_HOST = 0, 1
+
+
+class Bodies(C.Structure):
+    _fields_ = [("n", C.c_size_t), ("offsets", C.c_void_p), ("bytes", C.c_void_p), ("status", C.c_void_p),
+                ("source", C.c_void_p), ("k10_status", C.c_void_p), ("n_host", C.c_size_t),
+                ("internal", C.c_void_p)]
+
+
+class WBatchStats(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("json_bytes", C.c_uint64), ("body_bytes", C.c_uint64),
+                ("scratch_bytes", C.c_uint64), ("out_cap_bytes", C.c_uint64), ("k10_ms", C.c_double),
+                ("runs", C.c_uint64)]
 
 
 class HBatchInfo(C.Structure):
@@ -161,6 +177,17 @@ SIGNATURES = [
     ("gpudiff_encode_object_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64,
                                              C.POINTER(ObjInfo)]),
     ("gpudiff_k0_profile", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
+    ("gpudiff_upsert_bodies", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
+                                        C.POINTER(Bodies)]),
+    ("gpudiff_bodies_release", None, [_P, C.POINTER(Bodies)]),
+    ("gpudiff_wbatch_create", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
+                                        C.POINTER(_P)]),
+    ("gpudiff_wbatch_run", C.c_int, [_P, _P]),
+    ("gpudiff_wbatch_fetch", C.c_int, [_P, _P, C.POINTER(Bodies)]),
+    ("gpudiff_wbatch_stats_get", C.c_int, [_P, C.POINTER(WBatchStats)]),
+    ("gpudiff_wbatch_free", None, [_P, _P]),
+    ("gpudiff_upsert_body_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_size_t,
+                                           C.POINTER(C.c_size_t)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
@@ -503,6 +530,19 @@ class Engine:
             res.append((f.as_dict(), raw[f.off:f.off + f.bytes] if f.status == TOK_OK else None))
         return res
 
+    # ---- write path: request bodies of dirty objects
+    def upsert_bodies(self, docs, mode: int = UPSERT_SPEC):
+        """Kernel K10 (host-completed) over the documents: BodyList."""
+        wb = self.wbatch(docs, mode)
+        try:
+            wb.run()
+            return wb.fetch()
+        finally:
+            wb.close()
+
+    def wbatch(self, docs, mode: int = UPSERT_SPEC) -> "WBatch":
+        return WBatch(self, docs, mode)
+
     def k0_profile(self, enable: bool = True):
         """K0 per-phase wall-clock ticks (100 MHz) summed over waves since the last call."""
         out = (C.c_uint64 * 8)()
@@ -525,6 +565,85 @@ class Engine:
         if rc not in (OK, E_DECODE):
             _chk(rc, "gpudiff_status_equal")
         return bool(eq.value)
+
+
+def _doc_arrays(docs):
+    docs = [to_json_bytes(x) for x in docs]
+    n = len(docs)
+    bufs = [C.create_string_buffer(x, len(x)) if x else C.create_string_buffer(1) for x in docs]
+    ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p) for b in bufs])
+    lens = (C.c_size_t * max(n, 1))(*[len(x) for x in docs])
+    return docs, bufs, ptrs, lens
+
+
+@dataclass
+class BodyList:
+    bodies: List[Optional[bytes]]  # None = Go decode error (no write)
+    source: np.ndarray             # BODY_DEVICE / BODY_HOST
+    k10_status: np.ndarray         # K10's TOK_* per document
+    n_host: int
+
+
+class WBatch:
+    """Documents resident in HBM for K10 (gpudiff_wbatch_*)."""
+
+    def __init__(self, eng: "Engine", docs, mode: int = UPSERT_SPEC):
+        self.eng = eng
+        self.docs, self._bufs, ptrs, lens = _doc_arrays(docs)
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_wbatch_create(eng.ctx, ptrs, lens, len(self.docs), mode, C.byref(h)),
+             "gpudiff_wbatch_create")
+        self.h = h
+
+    def run(self):
+        _chk(_lib.gpudiff_wbatch_run(self.eng.ctx, self.h), "gpudiff_wbatch_run")
+
+    def fetch(self) -> BodyList:
+        b = Bodies()
+        _chk(_lib.gpudiff_wbatch_fetch(self.eng.ctx, self.h, C.byref(b)), "gpudiff_wbatch_fetch")
+        try:
+            n = b.n
+            offs = np.ctypeslib.as_array(C.cast(b.offsets, C.POINTER(C.c_uint64)), (n + 1,)).copy()
+            st = np.ctypeslib.as_array(C.cast(b.status, C.POINTER(C.c_int32)), (max(n, 1),))[:n].copy()
+            src = np.ctypeslib.as_array(C.cast(b.source, C.POINTER(C.c_uint8)), (max(n, 1),))[:n].copy()
+            k10 = np.ctypeslib.as_array(C.cast(b.k10_status, C.POINTER(C.c_int32)), (max(n, 1),))[:n].copy()
+            total = int(offs[-1]) if n else 0
+            raw = C.string_at(b.bytes, total) if total else b""
+            bodies = [None if st[i] != OK else raw[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+            return BodyList(bodies, src, k10, int(b.n_host))
+        finally:
+            _lib.gpudiff_bodies_release(self.eng.ctx, C.byref(b))
+
+    def stats(self) -> WBatchStats:
+        st = WBatchStats()
+        _chk(_lib.gpudiff_wbatch_stats_get(self.h, C.byref(st)), "gpudiff_wbatch_stats_get")
+        return st
+
+    def close(self):
+        if self.h:
+            _lib.gpudiff_wbatch_free(self.eng.ctx, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def upsert_body_host(doc, mode: int = UPSERT_SPEC) -> Optional[bytes]:
+    """The host path (Go-exact): the request body, or None on a Go decode error."""
+    b = to_json_bytes(doc)
+    n = C.c_size_t()
+    rc = _lib.gpudiff_upsert_body_host(b, len(b), mode, None, 0, C.byref(n))
+    if rc == E_DECODE:
+        return None
+    if rc not in (OK, E_CAPACITY):
+        _chk(rc, "gpudiff_upsert_body_host")
+    out = C.create_string_buffer(max(1, n.value))
+    _chk(_lib.gpudiff_upsert_body_host(b, len(b), mode, C.cast(out, C.c_void_p), n.value, C.byref(n)),
+         "gpudiff_upsert_body_host")
+    return out.raw[:n.value]
 
 
 def resolve_path(old, new, path_hash: int, path_kind: int, path_hash_bits: int = 64) -> str:

@@ -22,6 +22,15 @@ def lib():
         l.oracle_free.argtypes = [C.c_void_p]
         l.oracle_decide.restype = C.c_int
         l.oracle_decide.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double)]
+        l.oracle_docs_load.restype = C.c_void_p
+        l.oracle_docs_load.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t]
+        l.oracle_docs_free.restype = None
+        l.oracle_docs_free.argtypes = [C.c_void_p]
+        l.oracle_upsert_body.restype = C.c_long
+        l.oracle_upsert_body.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_char_p, C.c_size_t]
+        l.oracle_upsert_run.restype = C.c_int
+        l.oracle_upsert_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double),
+                                        C.POINTER(C.c_uint64)]
         _lib = l
     return _lib
 
@@ -49,6 +58,44 @@ class DecodedPairs:
     def close(self):
         if self.h:
             lib().oracle_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DecodedDocs:
+    """Documents decoded once (untimed) for the write-path restatement
+    (DeepCopy + upsert transform + json.Marshal)."""
+
+    def __init__(self, docs):
+        n = len(docs)
+        self.n = n
+        D = (C.c_char_p * max(n, 1))(*docs)
+        L = (C.c_size_t * max(n, 1))(*[len(d) for d in docs])
+        self.h = lib().oracle_docs_load(D, L, n)
+
+    def body(self, i, mode=0):
+        n = lib().oracle_upsert_body(self.h, i, mode, None, 0)
+        if n < 0:
+            return None
+        buf = C.create_string_buffer(n)
+        lib().oracle_upsert_body(self.h, i, mode, buf, n)
+        return buf.raw[:n]
+
+    def run(self, mode=0, threads=1, min_seconds=0.0):
+        """-> (sweeps, seconds, body bytes per sweep)"""
+        sec = C.c_double()
+        nb = C.c_uint64()
+        sw = lib().oracle_upsert_run(self.h, mode, threads, min_seconds, C.byref(sec), C.byref(nb))
+        return sw, sec.value, nb.value
+
+    def close(self):
+        if self.h:
+            lib().oracle_docs_free(self.h)
             self.h = None
 
     def __del__(self):

@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <charconv>
 #include <chrono>
 #include <memory>
 #include <string>
@@ -387,6 +389,251 @@ int oracle_decide(void* h, uint8_t* flags, int threads, double min_seconds, doub
         el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     } while (el < min_seconds);
     if (seconds) *seconds = el;
+    return sweeps;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ write path
+// upsertIntoDownstream (pkg/syncer/specsyncer.go:94-110): unstrob.DeepCopy(),
+// SetUID(""), SetResourceVersion(""), owner references whose Name equals the
+// kcp.dev/owned-by label (GetLabels: NestedStringMap) dropped, the rest written
+// back as ToUnstructured(&OwnerReference) maps; the field removed when none are
+// kept.  updateStatusInUpstream (statussyncer.go:44-48): DeepCopy, SetUID(""),
+// SetResourceVersion("").  Then the dynamic client's body,
+// json.NewEncoder(w).Encode(obj.Object) (Go 1.16): sorted keys, HTML-safe
+// escaping, shortest floats, trailing newline.  Like the Go code, the
+// transform works on a deep copy of the decoded (cached) object.
+namespace oracle {
+
+Value deep_copy(const Value& v) {
+    Value o;
+    o.k = v.k;
+    o.b = v.b;
+    o.i = v.i;
+    o.f = v.f;
+    o.s = v.s;
+    if (v.k == Value::MAP) {
+        o.m = std::make_shared<Map>();
+        o.m->reserve(v.m->size());
+        for (const auto& kv : *v.m) (*o.m)[kv.first] = deep_copy(kv.second);
+    } else if (v.k == Value::ARR) {
+        o.a = std::make_shared<Arr>();
+        o.a->reserve(v.a->size());
+        for (const auto& x : *v.a) o.a->push_back(deep_copy(x));
+    }
+    return o;
+}
+
+static Value str_value(const std::string& s) {
+    Value v;
+    v.k = Value::STR;
+    v.s = s;
+    return v;
+}
+
+void transform(Value& obj, int mode) {
+    auto md = obj.m->find("metadata");
+    if (md == obj.m->end() || md->second.k != Value::MAP) return;  // RemoveNestedField: no-op
+    Map& m = *md->second.m;
+    m.erase("uid");
+    m.erase("resourceVersion");
+    if (mode != 0) return;
+    auto labels = nested_string_map(obj, "labels");
+    std::string owned;
+    if (labels) {
+        auto it = labels->find("kcp.dev/owned-by");
+        if (it != labels->end()) owned = it->second;
+    }
+    // GetOwnerReferences: nil unless a list of maps
+    std::vector<Value> kept;
+    auto refs = m.find("ownerReferences");
+    if (refs != m.end() && refs->second.k == Value::ARR) {
+        bool all_maps = true;
+        for (const auto& e : *refs->second.a)
+            if (e.k != Value::MAP) all_maps = false;
+        if (all_maps) {
+            for (const auto& e : *refs->second.a) {
+                auto gs = [&](const char* k) {
+                    auto it = e.m->find(k);
+                    return it != e.m->end() && it->second.k == Value::STR ? it->second.s : std::string();
+                };
+                if (gs("name") == owned) continue;
+                Value r;
+                r.k = Value::MAP;
+                r.m = std::make_shared<Map>();
+                (*r.m)["apiVersion"] = str_value(gs("apiVersion"));
+                (*r.m)["kind"] = str_value(gs("kind"));
+                (*r.m)["name"] = str_value(gs("name"));
+                (*r.m)["uid"] = str_value(gs("uid"));
+                for (const char* k : {"controller", "blockOwnerDeletion"}) {
+                    auto it = e.m->find(k);
+                    if (it != e.m->end() && it->second.k == Value::BOOL) (*r.m)[k] = it->second;
+                }
+                kept.push_back(std::move(r));
+            }
+        }
+    }
+    if (kept.empty()) {
+        m.erase("ownerReferences");
+    } else {
+        Value l;
+        l.k = Value::ARR;
+        l.a = std::make_shared<Arr>(std::move(kept));
+        m["ownerReferences"] = std::move(l);
+    }
+}
+
+static void m_str(std::string& o, const std::string& s) {
+    static const char hx[] = "0123456789abcdef";
+    o.push_back('"');
+    for (size_t i = 0; i < s.size(); i++) {
+        const unsigned char c = (unsigned char)s[i];
+        if (c == '"' || c == '\\') { o.push_back('\\'); o.push_back((char)c); }
+        else if (c == '\n') o += "\\n";
+        else if (c == '\r') o += "\\r";
+        else if (c == '\t') o += "\\t";
+        else if (c < 0x20 || c == '<' || c == '>' || c == '&') { o += "\\u00"; o.push_back(hx[c >> 4]); o.push_back(hx[c & 15]); }
+        else if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+                 ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+            o += (unsigned char)s[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";
+            i += 2;
+        } else o.push_back((char)c);
+    }
+    o.push_back('"');
+}
+
+// strconv.AppendFloat(f, 'f'|'e', -1, 64): the shortest digits laid out
+static void m_float(std::string& o, double f) {
+    char b[64];
+    auto r = std::to_chars(b, b + 63, f, std::chars_format::scientific);
+    *r.ptr = 0;
+    std::string s(b);
+    const double a = fabs(f);
+    if (a != 0 && (a < 1e-6 || a >= 1e21)) {
+        const size_t n = s.size();
+        if (n >= 4 && s[n - 4] == 'e' && s[n - 3] == '-' && s[n - 2] == '0') s.erase(n - 2, 1);
+        o += s;
+        return;
+    }
+    const size_t e = s.find('e');
+    std::string mant = s.substr(0, e);
+    const int x = atoi(s.c_str() + e + 1);
+    bool neg = mant[0] == '-';
+    std::string dig;
+    for (char c : mant) if (c >= '0' && c <= '9') dig.push_back(c);
+    const int nd = (int)dig.size();
+    if (neg) o.push_back('-');
+    if (x >= nd - 1) o += dig + std::string((size_t)(x - nd + 1), '0');
+    else if (x >= 0) o += dig.substr(0, (size_t)x + 1) + "." + dig.substr((size_t)x + 1);
+    else o += "0." + std::string((size_t)(-x - 1), '0') + dig;
+}
+
+void marshal(std::string& o, const Value& v) {
+    switch (v.k) {
+        case Value::NIL: o += "null"; break;
+        case Value::BOOL: o += v.b ? "true" : "false"; break;
+        case Value::INT: o += std::to_string(v.i); break;
+        case Value::FLOAT: m_float(o, v.f); break;
+        case Value::STR: m_str(o, v.s); break;
+        case Value::ARR:
+            o.push_back('[');
+            for (size_t i = 0; i < v.a->size(); i++) {
+                if (i) o.push_back(',');
+                marshal(o, (*v.a)[i]);
+            }
+            o.push_back(']');
+            break;
+        case Value::MAP: {
+            std::vector<const std::pair<const std::string, Value>*> kv;  // encoding/json sorts map keys
+            kv.reserve(v.m->size());
+            for (const auto& x : *v.m) kv.push_back(&x);
+            std::sort(kv.begin(), kv.end(), [](auto* a, auto* b) { return a->first < b->first; });
+            o.push_back('{');
+            for (size_t i = 0; i < kv.size(); i++) {
+                if (i) o.push_back(',');
+                m_str(o, kv[i]->first);
+                o.push_back(':');
+                marshal(o, kv[i]->second);
+            }
+            o.push_back('}');
+            break;
+        }
+    }
+}
+
+struct Docs {
+    std::vector<Value> v;
+    std::vector<uint8_t> err;
+};
+
+}  // namespace oracle
+
+extern "C" {
+
+void* oracle_docs_load(const char* const* d, const size_t* len, size_t n) {
+    Docs* p = new Docs();
+    p->v.resize(n);
+    p->err.assign(n, 0);
+    for (size_t i = 0; i < n; i++)
+        if (!decode(d[i], len[i], p->v[i])) p->err[i] = 1;
+    return p;
+}
+
+void oracle_docs_free(void* h) { delete (Docs*)h; }
+
+// body of doc i (DeepCopy + transform + marshal); returns its length, -1 on a
+// decode error; writes min(len, cap) bytes
+long oracle_upsert_body(void* h, size_t i, int mode, char* out, size_t cap) {
+    Docs* p = (Docs*)h;
+    if (p->err[i]) return -1;
+    Value c = deep_copy(p->v[i]);
+    transform(c, mode);
+    std::string o;
+    marshal(o, c);
+    o.push_back('\n');
+    memcpy(out, o.data(), std::min(cap, o.size()));
+    return (long)o.size();
+}
+
+// the timed CPU baseline: every document's body, sweeps until min_seconds;
+// returns sweeps, *bytes = body bytes of one sweep
+int oracle_upsert_run(void* h, int mode, int threads, double min_seconds, double* seconds, uint64_t* bytes) {
+    Docs* p = (Docs*)h;
+    const size_t n = p->v.size();
+    if (threads < 1) threads = 1;
+    std::vector<uint64_t> tb(threads, 0);
+    int sweeps = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    double el = 0;
+    do {
+        auto work = [&](int t) {
+            size_t b = n * t / threads, e = n * (t + 1) / threads;
+            uint64_t acc = 0;
+            std::string o;
+            for (size_t i = b; i < e; i++) {
+                if (p->err[i]) continue;
+                Value c = deep_copy(p->v[i]);
+                transform(c, mode);
+                o.clear();
+                marshal(o, c);
+                o.push_back('\n');
+                acc += o.size();
+            }
+            tb[t] = acc;
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < threads; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        sweeps++;
+        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } while (el < min_seconds);
+    if (seconds) *seconds = el;
+    if (bytes) {
+        *bytes = 0;
+        for (auto x : tb) *bytes += x;
+    }
     return sweeps;
 }
 
