@@ -413,6 +413,64 @@ __device__ __forceinline__ uint8_t* go_esc_put(uint8_t* o, const uint8_t* s, uin
     }
     return o;
 }
+// wave-cooperative escaping of long strings: the output length of byte i
+// (1, 2 or 6; the three bytes of U+2028 / U+2029 give 6, 0, 0 -- E2 is a lead
+// byte, so a 0x80 / 0xA8 after it is that sequence's continuation)
+__device__ __forceinline__ uint32_t esc_unit(const uint8_t* s, uint32_t n, uint32_t i) {
+    const uint32_t c = s[i];
+    if (c < 0x80u) {
+        if (c == '"' || c == '\\' || c == '\n' || c == '\r' || c == '\t') return 2;
+        return (c < 0x20u || c == '<' || c == '>' || c == '&') ? 6u : 1u;
+    }
+    if (c == 0xE2u) return (i + 2 < n && s[i + 1] == 0x80u && (s[i + 2] == 0xA8u || s[i + 2] == 0xA9u)) ? 6u : 1u;
+    if (c == 0x80u) return (i >= 1 && s[i - 1] == 0xE2u && i + 1 < n && (s[i + 1] == 0xA8u || s[i + 1] == 0xA9u)) ? 0u : 1u;
+    if (c == 0xA8u || c == 0xA9u) return (i >= 2 && s[i - 1] == 0x80u && s[i - 2] == 0xE2u) ? 0u : 1u;
+    return 1u;
+}
+__device__ __forceinline__ uint32_t wave_esc_len(const uint8_t* s, uint32_t n) {
+    uint32_t acc = 0;
+    for (uint32_t b = 0; b < n; b += 64) {
+        const uint32_t i = b + __lane_id();
+        acc += i < n ? esc_unit(s, n, i) : 0u;
+    }
+    return wave_sum(acc);
+}
+// writes the escaped bytes of s[0, n) at o (the whole wave)
+__device__ __forceinline__ void wave_esc_put(uint8_t* o, const uint8_t* s, uint32_t n) {
+    const char* hx = "0123456789abcdef";
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < n; b += 64) {
+        const uint32_t i = b + __lane_id();
+        const uint32_t u = i < n ? esc_unit(s, n, i) : 0u;
+        const uint32_t inc = wave_incl_scan(u);
+        uint8_t* q = o + run + inc - u;
+        if (u == 1) {
+            q[0] = s[i];
+        } else if (u == 2) {
+            const uint32_t c = s[i];
+            q[0] = '\\';
+            q[1] = c == '\n' ? 'n' : c == '\r' ? 'r' : c == '\t' ? 't' : (uint8_t)c;
+        } else if (u == 6) {
+            const uint32_t c = s[i];
+            q[0] = '\\';
+            q[1] = 'u';
+            if (c == 0xE2u) {
+                q[2] = '2';
+                q[3] = '0';
+                q[4] = '2';
+                q[5] = s[i + 2] == 0xA8u ? '8' : '9';
+            } else {
+                q[2] = '0';
+                q[3] = '0';
+                q[4] = (uint8_t)hx[c >> 4];
+                q[5] = (uint8_t)hx[c & 15u];
+            }
+        }
+        run += __builtin_amdgcn_readlane((int)inc, 63);
+    }
+}
+constexpr uint32_t kLongString = 16;  // strings longer than this are escaped by the whole wave
+
 __device__ __forceinline__ uint32_t i64_len(int64_t v) {
     uint64_t u = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
     uint32_t n = v < 0 ? 2u : 1u;

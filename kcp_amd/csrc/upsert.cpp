@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <charconv>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -465,9 +466,24 @@ int gpudiff_wbatch_fetch(gpudiff_ctx* c, gpudiff_wbatch* wb, gpudiff_bodies* out
     bs->status.assign(n, 0);
     bs->k10.resize(n);
     bs->source.assign(n, GPUDIFF_BODY_DEVICE);
-    size_t n_host = 0;
+    // documents K10 left: the host path, on the context's encode threads
+    std::vector<uint32_t> def;
+    for (size_t i = 0; i < n; i++)
+        if (to[i].status != GPUDIFF_TOK_OK) def.push_back((uint32_t)i);
+    std::vector<std::string> hb(def.size());
+    std::vector<uint8_t> hok(def.size(), 0);
+    const uint32_t T = std::max<uint32_t>(1, std::min<uint32_t>(c->threads, (uint32_t)((def.size() + 63) / 64)));
+    auto work = [&](uint32_t t) {
+        for (size_t k = t; k < def.size(); k += T)
+            hok[k] = host_body(wb->src[def[k]], wb->lens[def[k]], wb->mode, hb[k]) ? 1 : 0;
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    const size_t n_host = def.size();
     uint64_t dev_bytes = 0;
-    std::string tmp;
+    size_t k = 0;
     for (size_t i = 0; i < n; i++) {
         bs->offsets[i] = bs->bytes.size();
         bs->k10[i] = (int32_t)to[i].status;
@@ -476,10 +492,10 @@ int gpudiff_wbatch_fetch(gpudiff_ctx* c, gpudiff_wbatch* wb, gpudiff_bodies* out
             bs->bytes.insert(bs->bytes.end(), p, p + to[i].bytes);
             dev_bytes += to[i].bytes;
         } else {
-            n_host++;
             bs->source[i] = GPUDIFF_BODY_HOST;
-            if (host_body(wb->src[i], wb->lens[i], wb->mode, tmp)) bs->bytes.insert(bs->bytes.end(), tmp.begin(), tmp.end());
+            if (hok[k]) bs->bytes.insert(bs->bytes.end(), hb[k].begin(), hb[k].end());
             else bs->status[i] = GPUDIFF_E_DECODE;
+            k++;
         }
     }
     bs->offsets[n] = bs->bytes.size();
