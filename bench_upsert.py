@@ -150,7 +150,7 @@ def run(args):
                      "bytes_per_launch": alg, "avg_launch_ms": k10_ms, "launches_per_step": 1},
         "host_completion": {"docs": int(res.n_host), "fetch_s": t_host_docs,
                             "note": "deferred documents marshalled by the host path inside gpudiff_wbatch_fetch "
-                                    "(1 thread); fetch_s includes the D2H copy of all bodies"},
+                                    "(the context's encode threads); fetch_s includes the D2H copy of all bodies"},
         "cpu_baseline": cpu,
         "checks": {"full_size": full, "sample": dict(docs=len(idx), bit_exact_vs_oracle=sample_ok)},
     }

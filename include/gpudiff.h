@@ -94,7 +94,8 @@ enum {
                                             (tests: forces pairs through the deferred K4 path) */
 #define GPUDIFF_OPT_DEVICE_ENCODE 0x2000000u /* gpudiff_submit / single-pair helpers: raw JSON up, kernel K0
                                                 encodes (as GPUDIFF_STORE_DEVICE_ENCODE does for the store) */
-#define GPUDIFF_OPT_K0_VARIANT_SHIFT 26u /* 2 bits: K0 occupancy variant (0: 8 waves/SIMD, 1: unconstrained) */
+#define GPUDIFF_OPT_K0_VARIANT_SHIFT 26u /* 2 bits: K0 / K10 occupancy variant (0: 8 waves/SIMD, 1: unconstrained;
+                                           K10 also 2: 5 waves, 3: 6 waves) */
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */

@@ -7,6 +7,7 @@
 
 #include "../../include/gpudiff.h"
 #include "decfloat.h"
+#include "ryu_tables.h"
 #include "tokenize.h"
 #include "xxh64.h"
 
@@ -469,7 +470,179 @@ __device__ __forceinline__ void wave_esc_put(uint8_t* o, const uint8_t* s, uint3
         run += __builtin_amdgcn_readlane((int)inc, 63);
     }
 }
-constexpr uint32_t kLongString = 16;  // strings longer than this are escaped by the whole wave
+constexpr uint32_t kLongString = 16;
+
+// ---- float64 -> Go text (floatEncoder(64): strconv.AppendFloat(f, 'f'|'e', -1, 64)
+// with the 1e-6 / 1e21 switch and the e-09 -> e-9 clean-up).  The shortest,
+// closest (ties to even) digit string is Ryu's (Adams, PLDI 2018): this is
+// tools/gen_ryu_table.py d2d_model restated over the same 125-bit tables.
+__device__ __forceinline__ uint32_t ryu_pow5bits(int32_t e) { return (uint32_t)(((uint32_t)e * 1217359u) >> 19) + 1u; }
+__device__ __forceinline__ uint64_t ryu_mulshift(uint64_t m, const uint64_t* mul, int32_t j) {
+    // (m * mul) >> j over the 192-bit product; j >= 64
+    const uint64_t b0_hi = __umul64hi(m, mul[0]);
+    const uint64_t b2_lo = m * mul[1], b2_hi = __umul64hi(m, mul[1]);
+    const uint64_t s_lo = b2_lo + b0_hi, s_hi = b2_hi + (s_lo < b2_lo ? 1ull : 0ull);
+    const int32_t sh = j - 64;
+    if (sh == 0) return s_lo;
+    if (sh >= 64) return s_hi >> (sh - 64);
+    return (s_lo >> sh) | (s_hi << (64 - sh));
+}
+__device__ __forceinline__ bool ryu_pow5_multiple(uint64_t v, int32_t p) {
+    int32_t c = 0;
+    while (v % 5u == 0u) {
+        v /= 5u;
+        if (++c >= p) return true;
+    }
+    return c >= p;
+}
+// finite nonzero double -> (digits, decimal exponent of the last digit)
+__device__ inline void ryu_d2d(uint64_t bits, uint64_t* digits, int32_t* exp10) {
+    const uint64_t ieee_m = bits & ((1ull << 52) - 1ull);
+    const uint32_t ieee_e = (uint32_t)((bits >> 52) & 0x7FFu);
+    int32_t e2;
+    uint64_t m2;
+    if (ieee_e == 0) {
+        e2 = 1 - 1023 - 52 - 2;
+        m2 = ieee_m;
+    } else {
+        e2 = (int32_t)ieee_e - 1023 - 52 - 2;
+        m2 = (1ull << 52) | ieee_m;
+    }
+    const bool accept = (m2 & 1u) == 0;
+    const uint64_t mv = 4u * m2;
+    const uint32_t mm_shift = (ieee_m != 0 || ieee_e <= 1) ? 1u : 0u;
+    bool vm_tz = false, vr_tz = false;
+    uint64_t vr, vp, vm;
+    int32_t e10;
+    if (e2 >= 0) {
+        const int32_t q = (int32_t)(((uint32_t)e2 * 78913u) >> 18) - (e2 > 3 ? 1 : 0);
+        e10 = q;
+        const int32_t k = kRyuPow5InvBits + (int32_t)ryu_pow5bits(q) - 1;
+        const int32_t i = -e2 + q + k;
+        const uint64_t* mul = kRyuPow5InvSplit[q];
+        vr = ryu_mulshift(4u * m2, mul, i);
+        vp = ryu_mulshift(4u * m2 + 2u, mul, i);
+        vm = ryu_mulshift(4u * m2 - 1u - mm_shift, mul, i);
+        if (q <= 21) {
+            if (mv % 5u == 0u) vr_tz = ryu_pow5_multiple(mv, q);
+            else if (accept) vm_tz = ryu_pow5_multiple(mv - 1u - mm_shift, q);
+            else vp -= ryu_pow5_multiple(mv + 2u, q) ? 1u : 0u;
+        }
+    } else {
+        const int32_t q = (int32_t)(((uint32_t)(-e2) * 732923u) >> 20) - (-e2 > 1 ? 1 : 0);
+        e10 = q + e2;
+        const int32_t i = -e2 - q;
+        const int32_t k = (int32_t)ryu_pow5bits(i) - kRyuPow5Bits;
+        const int32_t j = q - k;
+        const uint64_t* mul = kRyuPow5Split[i];
+        vr = ryu_mulshift(4u * m2, mul, j);
+        vp = ryu_mulshift(4u * m2 + 2u, mul, j);
+        vm = ryu_mulshift(4u * m2 - 1u - mm_shift, mul, j);
+        if (q <= 1) {
+            vr_tz = true;
+            if (accept) vm_tz = mm_shift == 1;
+            else vp--;
+        } else if (q < 63) {
+            vr_tz = (mv & ((1ull << q) - 1ull)) == 0;
+        }
+    }
+    int32_t removed = 0;
+    uint64_t out;
+    if (vm_tz || vr_tz) {
+        uint32_t last = 0;
+        while (vp / 10u > vm / 10u) {
+            vm_tz = vm_tz && vm % 10u == 0;
+            vr_tz = vr_tz && last == 0;
+            last = (uint32_t)(vr % 10u);
+            vr /= 10u;
+            vp /= 10u;
+            vm /= 10u;
+            removed++;
+        }
+        if (vm_tz) {
+            while (vm % 10u == 0) {
+                vr_tz = vr_tz && last == 0;
+                last = (uint32_t)(vr % 10u);
+                vr /= 10u;
+                vp /= 10u;
+                vm /= 10u;
+                removed++;
+            }
+        }
+        if (vr_tz && last == 5 && vr % 2u == 0) last = 4;
+        out = vr + (((vr == vm && (!accept || !vm_tz)) || last >= 5) ? 1u : 0u);
+    } else {
+        bool round_up = false;
+        if (vp / 100u > vm / 100u) {
+            round_up = vr % 100u >= 50u;
+            vr /= 100u;
+            vp /= 100u;
+            vm /= 100u;
+            removed += 2;
+        }
+        while (vp / 10u > vm / 10u) {
+            round_up = vr % 10u >= 5u;
+            vr /= 10u;
+            vp /= 10u;
+            vm /= 10u;
+            removed++;
+        }
+        out = vr + ((vr == vm || round_up) ? 1u : 0u);
+    }
+    *digits = out;
+    *exp10 = e10 + removed;
+}
+// Go's text of a decoded float64 (bits; neg_zero: the literal was a negative
+// zero, which the canonical value does not keep); o == nullptr: length only
+__device__ inline uint32_t go_float_put(uint64_t bits, bool neg_zero, uint8_t* o) {
+    uint32_t n = 0;
+    auto put = [&](uint32_t c) {
+        if (o) o[n] = (uint8_t)c;
+        n++;
+    };
+    if ((bits & ~(1ull << 63)) == 0) {
+        if (neg_zero || (bits >> 63)) put('-');
+        put('0');
+        return n;
+    }
+    if (bits >> 63) put('-');
+    uint64_t dg;
+    int32_t e;
+    ryu_d2d(bits, &dg, &e);
+    char buf[20];
+    uint32_t nd = 0;
+    for (uint64_t t = dg; t; t /= 10u) buf[nd++] = (char)('0' + t % 10u);  // reversed
+    const int32_t x = e + (int32_t)nd - 1;  // exponent of the first digit
+    const double a = __longlong_as_double((long long)(bits & ~(1ull << 63)));
+    if (a < 1e-6 || a >= 1e21) {
+        put(buf[nd - 1]);
+        if (nd > 1) {
+            put('.');
+            for (int32_t k = (int32_t)nd - 2; k >= 0; k--) put(buf[k]);
+        }
+        put('e');
+        put(x < 0 ? '-' : '+');
+        uint32_t ax = (uint32_t)(x < 0 ? -x : x);
+        if (x >= 0 && ax < 10) put('0');
+        if (ax >= 100) put('0' + ax / 100u);
+        if (ax >= 10) put('0' + (ax / 10u) % 10u);
+        put('0' + ax % 10u);
+    } else if (x >= (int32_t)nd - 1) {
+        for (int32_t k = (int32_t)nd - 1; k >= 0; k--) put(buf[k]);
+        for (int32_t k = 0; k < x - ((int32_t)nd - 1); k++) put('0');
+    } else if (x >= 0) {
+        for (int32_t k = (int32_t)nd - 1, c = 0; k >= 0; k--, c++) {
+            if (c == x + 1) put('.');
+            put(buf[k]);
+        }
+    } else {
+        put('0');
+        put('.');
+        for (int32_t k = 0; k < -x - 1; k++) put('0');
+        for (int32_t k = (int32_t)nd - 1; k >= 0; k--) put(buf[k]);
+    }
+    return n;
+}  // strings longer than this are escaped by the whole wave
 
 __device__ __forceinline__ uint32_t i64_len(int64_t v) {
     uint64_t u = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
@@ -512,7 +685,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     for (uint32_t d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
     return v;
 }
-constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u;
+constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u, MF_FLOAT = 16u;
 constexpr uint32_t kMarshalMaxMembers = 2048;
 constexpr int kModeEncode = 0, kModeMarshal = 1;
 

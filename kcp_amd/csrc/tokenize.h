@@ -158,7 +158,7 @@ hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, con
 // the body's u64 offset in `bodies` (room: marshal_out_cap(json_len)); out[i]
 // gets {off, bytes, status}.  A nonzero status leaves the document to the host.
 hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
-                               uint8_t* bodies, uint32_t mode, TokOut* out);
+                               uint8_t* bodies, uint32_t mode, TokOut* out, uint32_t variant = 0);
 // K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)
 hipError_t launch_collide(hipStream_t s, const DocLink* links, const TokOut* outs, const DSlot* slots, uint32_t n,
                           const uint8_t* space, uint8_t* coll);

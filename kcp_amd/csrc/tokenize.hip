@@ -720,11 +720,20 @@ hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, con
 }
 
 hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
-                               uint8_t* bodies, uint32_t mode, TokOut* out) {
+                               uint8_t* bodies, uint32_t mode, TokOut* out, uint32_t variant) {
     if (!n) return hipSuccess;
     const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    k_encode_docs<1, kModeMarshal><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, bodies, 0, nullptr,
-                                                                          (uint64_t)mode, out, nullptr, nullptr);
+    // variant (tuning, GPUDIFF_OPT_K0_VARIANT_SHIFT): 0 = 8 waves/SIMD (<= 64 VGPRs, a few spills:
+    // fastest, A/B on config3 documents), 1 = unconstrained (4 waves), 2 = 5 waves (no spills), 3 = 6 waves
+#define K10_LAUNCH(W)                                                                                   \
+    k_encode_docs<W, kModeMarshal><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, bodies, 0, \
+                                                                          nullptr, (uint64_t)mode, out,      \
+                                                                          nullptr, nullptr)
+    if (variant == 1) K10_LAUNCH(1);
+    else if (variant == 2) K10_LAUNCH(5);
+    else if (variant == 3) K10_LAUNCH(6);
+    else K10_LAUNCH(8);
+#undef K10_LAUNCH
     return hipGetLastError();
 }
 

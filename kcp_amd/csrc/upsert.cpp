@@ -434,7 +434,8 @@ int gpudiff_wbatch_run(gpudiff_ctx* c, gpudiff_wbatch* wb) {
     }
     if (wb->ev[0]) HIPCHK(hipEventRecord(wb->ev[0], c->stream));
     HIPCHK(launch_marshal_docs(c->stream, (const TokDoc*)wb->d_docs, wb->n, (const uint8_t*)wb->d_json,
-                               (uint8_t*)wb->d_scratch, (uint8_t*)wb->d_out, wb->mode, (TokOut*)wb->d_res));
+                               (uint8_t*)wb->d_scratch, (uint8_t*)wb->d_out, wb->mode, (TokOut*)wb->d_res,
+                               (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
     if (wb->ev[1]) {
         HIPCHK(hipEventRecord(wb->ev[1], c->stream));
         wb->pending_timing = true;

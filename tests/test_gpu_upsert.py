@@ -54,15 +54,14 @@ def test_kat_device_subset():
     docs = [k[1] for k in UC.KAT if k[2] == UC.SPEC]
     codes = _check(eng, docs, UC.SPEC, must_device=False)
     by_name = {k[0]: c for k, c in zip([k for k in UC.KAT if k[2] == UC.SPEC], codes)}
-    assert by_name["floats"] == G.TOK_FLOAT
+    assert by_name["floats"] == G.TOK_NUMBER  # 5e-324: a subnormal, outside the device's exact float parse
     assert by_name["duplicate keys last wins"] == G.TOK_HASH
     assert by_name["surrogates and invalid UTF-8"] == G.TOK_STRING
-    assert by_name["ints"] == G.TOK_FLOAT  # 9223372036854775808 decodes to a float64
     assert by_name["key byte order"] == G.TOK_KEY  # a non-ASCII key
     for name in ("uid+rv removed", "kept ref normalized", "owned ref dropped, field removed", "refs not a list",
                  "refs with a non-map element", "non-string label collapses owned-by", "html-safe escaping",
                  "raw U+2028 in input", "escaped key", "whitespace", "empty object", "refs empty list",
-                 "empty ref object kept", "non-bool controller omitted", "nested metadata untouched"):
+                 "empty ref object kept", "non-bool controller omitted", "nested metadata untouched", "ints"):
         assert by_name[name] == G.TOK_OK, name
     eng.close()
 
@@ -72,19 +71,17 @@ def test_fixtures_and_synthetic(mode):
     eng = G.Engine(device=0)
     # the KAT pairs hold floats, duplicate keys, escaped keys and invalid UTF-8 on purpose, the
     # reference's manifests a few floats; the config populations none of these
-    codes = _check(eng, UC.fixture_docs(), mode, allowed=(G.TOK_FLOAT, G.TOK_NUMBER, G.TOK_KEY, G.TOK_HASH,
-                                                           G.TOK_STRING))
-    assert sum(c == G.TOK_OK for c in codes) >= 0.85 * len(codes)  # config3/4 CRDs carry random floats
+    codes = _check(eng, UC.fixture_docs(), mode, allowed=(G.TOK_NUMBER, G.TOK_KEY, G.TOK_HASH, G.TOK_STRING))
+    assert sum(c == G.TOK_OK for c in codes) >= 0.95 * len(codes)
     _check(eng, UC.synthetic_docs(floats=False), mode)
-    codes = _check(eng, UC.synthetic_docs(seed=12), mode, allowed=(G.TOK_FLOAT,))
-    assert G.TOK_OK in codes and G.TOK_FLOAT in codes
+    _check(eng, UC.synthetic_docs(seed=12), mode, allowed=(G.TOK_NUMBER,))
     eng.close()
 
 
 def test_edges_and_scan_boundaries():
     eng = G.Engine(device=0)
     _check(eng, UC.boundary_docs(), UC.SPEC)
-    _check(eng, list(EDGE_OK), UC.SPEC, allowed=(G.TOK_FLOAT,))
+    _check(eng, list(EDGE_OK), UC.SPEC, allowed=(G.TOK_NUMBER,))
     _check(eng, [d for d, _ in EDGE_DEFER], UC.SPEC, must_device=False)
     eng.close()
 
@@ -116,4 +113,30 @@ def test_staged_batch_reruns_identical():
     wb.close()
     assert a.bodies == b.bodies and a.n_host == 0
     assert st.runs == 4 and st.k10_ms > 0 and st.body_bytes == sum(len(x) for x in a.bodies)
+    eng.close()
+
+
+def test_float_text_matches_host():
+    """Go's shortest float64 text (Ryu on the device, std::to_chars on the
+    host): random doubles of every magnitude, %.17g and repr literals, the
+    'e' switch boundaries and negative zeros."""
+    import struct
+    eng = G.Engine(device=0)
+    rnd = random.Random(17)
+    vals = [rnd.uniform(-1, 1) * 10 ** rnd.randint(-300, 300) for _ in range(6000)]
+    vals += [struct.unpack("<d", struct.pack("<Q", rnd.getrandbits(64)))[0] for _ in range(6000)]
+    vals += [1e-6, 9.999999999999999e-7, 1e21, 9.999999999999999e20, 1.7976931348623157e308, 0.1, 0.5,
+             2.0 ** 63, 2.0 ** 53 + 2, 123456789012345680000.0, 1e22, 1e23, 4.35e-5]
+    vals += [float(k) for k in range(-70, 70)] + [2.0 ** k for k in range(-80, 80)]  # exact integers / powers of 2
+    vals = [v for v in vals if v == v and abs(v) != float("inf")]
+    lits = [repr(v).encode() for v in vals] + [b"%.17g" % v for v in vals[:3000]] + \
+        [b"-0.0", b"-0e5", b"0.000", b"-1e-400", b"1E+2", b"-12.50"]
+    docs = [b'{"f":[' + b",".join(lits[i:i + 40]) + b']}' for i in range(0, len(lits), 40)]
+    codes = _check(eng, docs, UC.SPEC, must_device=False)
+    # only literals the device cannot parse exactly (subnormals, undecidable halfway cases) go to the host
+    assert sum(c == G.TOK_OK for c in codes) >= 0.5 * len(codes)
+    assert set(codes) <= {G.TOK_OK, G.TOK_NUMBER}
+    single = [b'{"f":%s}' % x for x in lits[:4000]]
+    codes = _check(eng, single, UC.SPEC, must_device=False)
+    assert sum(c == G.TOK_OK for c in codes) >= 0.95 * len(codes), sum(c == G.TOK_OK for c in codes)
     eng.close()

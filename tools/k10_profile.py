@@ -22,7 +22,9 @@ for d in docs:
     k = d[d.find(b'"kind":"') + 8:][:12].split(b'"')[0].decode()
     kinds[k] = kinds.get(k, 0) + 1
 print("docs %d, mean %.0f B, kinds %s" % (n, np.mean([len(d) for d in docs]), kinds))
-eng = G.Engine(device=0, timing=True)
+variant = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+eng = G.Engine(device=0, timing=True, flags=variant << 26)
+print("K10 variant", variant)
 wb = eng.wbatch(docs)
 wb.run()
 r = wb.fetch()
