@@ -346,3 +346,65 @@ func (b *Batcher) flushStored(evs []event) {
 }
 
 var errNoEngine = errors.New("gpudiff: engine not initialised")
+
+// Mode selects which of the syncer's two write-path transforms UpsertBodies applies.
+type Mode uint32
+
+const (
+	// UpsertSpec is upsertIntoDownstream's object (specsyncer.go:94-108).
+	UpsertSpec Mode = C.GPUDIFF_UPSERT_SPEC
+	// UpsertStatus is updateStatusInUpstream's object (statussyncer.go:44-48).
+	UpsertStatus Mode = C.GPUDIFF_UPSERT_STATUS
+)
+
+// UpsertBodies returns, for each dirty object, the request body the dynamic
+// client would send after the syncer's DeepCopy + SetUID("") +
+// SetResourceVersion("") (+ owner-reference filter in UpsertSpec mode): the
+// bytes of json.NewEncoder(w).Encode(obj.Object), built by kernel K10 (the
+// host path completes what K10 leaves).  bodies[i] is nil when objs[i] is not
+// an *unstructured.Unstructured or does not decode; the caller then takes the
+// reference path for that object.  The caller splices the live
+// resourceVersion in before client.Update (specsyncer.go:122,
+// statussyncer.go:56) exactly as today.
+func (e *Engine) UpsertBodies(objs []interface{}, mode Mode) ([][]byte, error) {
+	n := len(objs)
+	if n == 0 {
+		return nil, nil
+	}
+	docs := C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	lens := C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.size_t(0))))
+	defer C.free(docs)
+	defer C.free(lens)
+	dp := (*[1 << 30]*C.uint8_t)(docs)[:n:n]
+	lp := (*[1 << 30]C.size_t)(lens)[:n:n]
+	for i, o := range objs {
+		dp[i], lp[i] = nil, 0
+		if b, ok := jsonOf(o); ok {
+			dp[i], lp[i] = cmem(b)
+		}
+	}
+	defer func() {
+		for i := range dp {
+			C.free(unsafe.Pointer(dp[i]))
+		}
+	}()
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	var out C.gpudiff_bodies
+	if err := errOf(C.gpudiff_upsert_bodies(e.ctx, (**C.uint8_t)(docs), (*C.size_t)(lens), C.size_t(n),
+		C.uint32_t(mode), &out)); err != nil {
+		return nil, err
+	}
+	defer C.gpudiff_bodies_release(e.ctx, &out)
+	offs := (*[1 << 30]C.uint64_t)(unsafe.Pointer(out.offsets))[: n+1 : n+1]
+	st := (*[1 << 30]C.int32_t)(unsafe.Pointer(out.status))[:n:n]
+	res := make([][]byte, n)
+	for i := 0; i < n; i++ {
+		if lp[i] == 0 || st[i] != 0 {
+			continue
+		}
+		res[i] = C.GoBytes(unsafe.Pointer(uintptr(unsafe.Pointer(out.bytes))+uintptr(offs[i])),
+			C.int(offs[i+1]-offs[i]))
+	}
+	return res, nil
+}
