@@ -44,10 +44,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5", "upsert"],
+    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5", "upsert", "rollup"],
                     help="config5 = watch replay through the device-resident object store (bench_replay.py); "
-                         "upsert = the write path's request bodies, kernel K10 (bench_upsert.py)")
+                         "upsert = the write path's request bodies, kernel K10 (bench_upsert.py); "
+                         "rollup = the Deployment splitter's status roll-up, K11 + K12 (bench_rollup.py)")
     ap.add_argument("--docs", type=int, default=131072, help="upsert: documents resident in HBM")
+    ap.add_argument("--roots", type=int, default=250000, help="rollup: root Deployments")
+    ap.add_argument("--leaves", type=int, default=4, help="rollup: leaf Deployments per root")
     ap.add_argument("--batch", type=int, default=65536, help="config5: events per batch")
     ap.add_argument("--batches", type=int, default=40, help="config5: timed batches")
     ap.add_argument("--warmup-batches", type=int, default=4, help="config5: untimed batches")
@@ -75,6 +78,10 @@ def main():
         args.sample = min(args.sample, 300)
         return bench_upsert.run(args)
 
+    if args.config == "rollup":
+        import bench_rollup
+
+        return bench_rollup.run(args)
     if args.config == "config5":
         import bench_replay
         args.sample = min(args.sample, 300)

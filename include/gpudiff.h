@@ -71,6 +71,8 @@ enum {
 #define GPUDIFF_TOK_SPACE 8   /* output space exhausted */
 #define GPUDIFF_TOK_FLOAT 9   /* K10 (write path): a float64 value (Go's shortest formatting is done on the host) */
 #define GPUDIFF_TOK_WIDE 10   /* K10: an object with more than 2048 members (quadratic key ranking) */
+#define GPUDIFF_TOK_FIELD 11  /* K11 (roll-up): a field the typed decode must judge on the host (duplicate,
+                                 case-folded key, type mismatch, counter not an int32 literal, escaped label) */
 
 /* changed-path kinds (low 2 bits); bit 7 = status region */
 #define GPUDIFF_PATH_CHANGED 0u        /* present in both, value differs */
@@ -387,6 +389,70 @@ void gpudiff_wbatch_free(gpudiff_ctx* ctx, gpudiff_wbatch* wb);
  * fit: then GPUDIFF_E_CAPACITY).  GPUDIFF_E_DECODE if Go cannot decode doc. */
 int gpudiff_upsert_body_host(const uint8_t* doc, size_t len, uint32_t mode, uint8_t* out, size_t cap,
                              size_t* out_len);
+
+/* ---- Deployment splitter status roll-up ----
+ * pkg/reconciler/deployment/deployment.go:41-91: when a leaf Deployment
+ * changes, the splitter lists every cached Deployment labelled
+ * kcp.dev/owned-by=<root> (:44-51; all namespaces, all logical clusters), sums
+ * their status.{replicas, updatedReplicas, readyReplicas, availableReplicas,
+ * unavailableReplicas} into the root's status (:74-85, int32: Go wrap-around)
+ * and copies others[0].status.conditions (:89-91).  Batch form: n cached
+ * Deployments (JSON) -> one group per distinct owned-by value, ordered by first
+ * appearance; others[0] is the member with the lowest index (the lister's order
+ * is unspecified).  The objects are typed appsv1.Deployments: Go 1.16
+ * encoding/json rules apply to the fields read (case-insensitive field names,
+ * repeated keys merge, null is a no-op, counters must be int32 literals); a
+ * document Go cannot decode gets GPUDIFF_ROLLUP_DECODE.  Kernel K11 extracts
+ * the fields (roll-up mode of k_encode_docs), K12 groups by label on the device;
+ * documents outside K11's subset (GPUDIFF_TOK_*) are decided by the host path
+ * (gpudiff_rollup_doc_host), which then regroups the batch with identical
+ * results. */
+typedef struct gpudiff_rollup_group {
+    uint32_t first_doc;  /* others[0]: its status.conditions become the root's */
+    uint32_t n_members;
+    int32_t sums[5];     /* replicas, updatedReplicas, readyReplicas, availableReplicas, unavailableReplicas */
+    uint32_t reserved;
+} gpudiff_rollup_group;
+#define GPUDIFF_ROLLUP_NONE (-1)    /* no kcp.dev/owned-by label: not a leaf */
+#define GPUDIFF_ROLLUP_DECODE (-2)  /* Go cannot decode the document into an appsv1.Deployment */
+
+typedef struct gpudiff_rollup {
+    size_t n_docs;
+    const int32_t* doc_group;              /* [n_docs]: group index or GPUDIFF_ROLLUP_* */
+    size_t n_groups;
+    const gpudiff_rollup_group* groups;    /* ascending first_doc */
+    const int32_t* k11_status;             /* [n_docs]: K11's GPUDIFF_TOK_* (why the host took it) */
+    size_t n_host;                         /* documents the host path decided */
+    uint32_t host_grouped;                 /* 1: the host regrouped (deferrals or a label-hash collision) */
+    void* internal;
+} gpudiff_rollup;
+
+typedef struct gpudiff_rbatch gpudiff_rbatch;
+typedef struct gpudiff_rbatch_stats {
+    uint64_t n_docs, json_bytes, scratch_bytes;
+    double k11_ms, k12_ms;  /* mean durations over the timed runs (GPUDIFF_OPT_TIMING) */
+    uint64_t runs;
+} gpudiff_rbatch_stats;
+/* documents uploaded once into HBM; run = K11 + K12 on the context stream
+ * (asynchronous); fetch = results to the host, host path for deferrals.  The
+ * caller's document buffers must stay valid until gpudiff_rbatch_free (the
+ * host path and regrouping read them). */
+int gpudiff_rbatch_create(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, size_t n,
+                          gpudiff_rbatch** out);
+int gpudiff_rbatch_run(gpudiff_ctx* ctx, gpudiff_rbatch* rb);
+int gpudiff_rbatch_fetch(gpudiff_ctx* ctx, gpudiff_rbatch* rb, gpudiff_rollup* out);
+int gpudiff_rbatch_stats_get(const gpudiff_rbatch* rb, gpudiff_rbatch_stats* st);
+void gpudiff_rbatch_free(gpudiff_ctx* ctx, gpudiff_rbatch* rb);
+/* create + run + fetch + free */
+int gpudiff_rollup_status(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, size_t n,
+                          gpudiff_rollup* out);
+void gpudiff_rollup_release(gpudiff_ctx* ctx, gpudiff_rollup* r);
+/* the host path for one document (Go-exact typed decode of the fields read):
+ * counters into v[5]; the owned-by value into label[0, cap) with *label_len
+ * its length, or SIZE_MAX when the label is absent (GPUDIFF_E_CAPACITY when it
+ * does not fit); GPUDIFF_E_DECODE when Go rejects the document. */
+int gpudiff_rollup_doc_host(const uint8_t* doc, size_t len, int32_t* v, uint8_t* label, size_t cap,
+                            size_t* label_len);
 
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,

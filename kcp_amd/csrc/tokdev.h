@@ -687,7 +687,30 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 }
 constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u, MF_FLOAT = 16u;
 constexpr uint32_t kMarshalMaxMembers = 2048;
-constexpr int kModeEncode = 0, kModeMarshal = 1;
+constexpr int kModeEncode = 0, kModeMarshal = 1, kModeRollup = 2;
+
+// K11 (roll-up mode): Go's struct field lookup for an ASCII key -- 0 no
+// match, 1 exact, 2 equal only under ASCII case folding (encoding/json
+// fold.go; the device never sees non-ASCII keys: they are slow strings)
+__device__ __forceinline__ uint32_t field_fold(const uint8_t* k, uint32_t kl, const char* name, uint32_t nl) {
+    if (kl != nl) return 0u;
+    bool exact = true;
+    for (uint32_t i = 0; i < nl; i++) {
+        const uint32_t a = k[i], b = (uint8_t)name[i];
+        if (a == b) continue;
+        exact = false;
+        if ((a ^ b) != 0x20u || (a | 0x20u) - 'a' > 25u) return 0u;
+    }
+    return exact ? 1u : 2u;
+}
+// appsv1.DeploymentStatus counters summed by deployment.go:79-85, in RollOut.v order
+__device__ __forceinline__ const char* roll_field(uint32_t k) {
+    return k == 0 ? "replicas" : k == 1 ? "updatedReplicas" : k == 2 ? "readyReplicas"
+         : k == 3 ? "availableReplicas" : "unavailableReplicas";
+}
+__device__ __forceinline__ uint32_t roll_field_len(uint32_t k) {
+    return k == 0 ? 8u : k == 1 ? 15u : k == 2 ? 13u : k == 3 ? 17u : 19u;
+}
 
 struct Scratch {
     uint32_t* tok;

@@ -103,6 +103,23 @@ __host__ __device__ inline uint64_t marshal_scratch_bytes(uint32_t len) { return
 // (escaping can grow a string 6-fold, owner references gain their fixed keys)
 __host__ __device__ inline uint64_t marshal_out_cap(uint32_t len) { return ((2ull * len + 512u) + 15u) & ~15ull; }
 
+// K11 (k_encode_docs in roll-up mode, the Deployment splitter's status
+// aggregation): per document, the five status counters and the owned-by label
+// span; a nonzero status leaves the document to the host path.
+struct RollOut {
+    int32_t v[5];        // replicas, updatedReplicas, readyReplicas, availableReplicas, unavailableReplicas
+    uint32_t label_off;  // kcp.dev/owned-by value bytes in the document (no escapes)
+    uint32_t label_len;
+    uint16_t status;     // GPUDIFF_TOK_*
+    uint16_t flags;      // kRollHasLabel
+};
+static_assert(sizeof(RollOut) == 32, "RollOut");
+constexpr uint16_t kRollHasLabel = 1u;
+// phases 1-2 only: tokens, node records, decoded-string room
+__host__ __device__ inline uint64_t rollup_scratch_bytes(uint32_t len) {
+    return tok_align(4ull * tok_cap(len)) + tok_align(16ull * node_cap(len)) + tok_align((uint64_t)len + 32u);
+}
+
 constexpr uint32_t kTokMaxLen = (1u << 24) - 64u;  // token words hold 24-bit positions
 constexpr uint32_t kTokSlack = 32u;                 // readable bytes K0 needs after each staged document
 
@@ -159,6 +176,11 @@ hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, con
 // gets {off, bytes, status}.  A nonzero status leaves the document to the host.
 hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                                uint8_t* bodies, uint32_t mode, TokOut* out, uint32_t variant = 0);
+// K11: roll-up fields per document into outs (RollOut[n]); scratch per document at docs[i].scratch_off
+hipError_t launch_rollup_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                              RollOut* outs);
+// K12: group the documents by owned-by label (xxh64 radix sort + byte check),
+// int32 sums per group; see rollup.hip
 // K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)
 hipError_t launch_collide(hipStream_t s, const DocLink* links, const TokOut* outs, const DSlot* slots, uint32_t n,
                           const uint8_t* space, uint8_t* coll);

@@ -69,14 +69,25 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     TokOut o{};
     if (len > kTokMaxLen) {
         if (lane == 0) {
-            o.status = GPUDIFF_TOK_SIZE;
-            out[doc_i] = o;
+            if constexpr (MODE == kModeRollup) {
+                RollOut R{};
+                R.status = GPUDIFF_TOK_SIZE;
+                ((RollOut*)space)[doc_i] = R;
+            } else {
+                o.status = GPUDIFF_TOK_SIZE;
+                out[doc_i] = o;
+            }
         }
         return;
     }
     uint8_t* base = scratch + D.scratch_off;
     Scratch S;
-    if constexpr (MODE == kModeMarshal) {
+    if constexpr (MODE == kModeRollup) {
+        S = Scratch{};
+        S.tok = (uint32_t*)base;
+        S.rec = (uint4*)(base + tok_align(4ull * tok_cap(len)));
+        S.str = base + tok_align(4ull * tok_cap(len)) + tok_align(16ull * node_cap(len));
+    } else if constexpr (MODE == kModeMarshal) {
         const MarshalLayout ML = marshal_layout(len);
         S = Scratch{};
         S.tok = (uint32_t*)(base + ML.tok);
@@ -433,6 +444,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     if constexpr (MODE == kModeMarshal) {
 #include "marshal_phases.inc"
     }
+    if constexpr (MODE == kModeRollup) {
+#include "rollup_phases.inc"
+    }
 
     const uint64_t seed = slots ? ((slots[links[doc_i].slot].flags >> 8) & 0xFFu) : D.seed;
     mark(1);
@@ -734,6 +748,15 @@ hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, co
     else if (variant == 3) K10_LAUNCH(6);
     else K10_LAUNCH(8);
 #undef K10_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_rollup_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                              RollOut* outs) {
+    if (!n) return hipSuccess;
+    const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    k_encode_docs<8, kModeRollup><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, (uint8_t*)outs, 0,
+                                                                        nullptr, 0, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

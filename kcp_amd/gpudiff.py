@@ -87,8 +87,9 @@ class ObjInfo(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
-TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SIZE, TOK_SPACE, TOK_FLOAT, TOK_WIDE = \
-    range(11)
+TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SIZE, TOK_SPACE, TOK_FLOAT, TOK_WIDE, \
+    TOK_FIELD = range(12)
+ROLLUP_NONE, ROLLUP_DECODE = -1, -2
 
 UPSERT_SPEC, UPSERT_STATUS = 0, 1
 BODY_DEVICE, BODY_HOST = 0, 1
@@ -104,6 +105,22 @@ class WBatchStats(C.Structure):
     _fields_ = [("n_docs", C.c_uint64), ("json_bytes", C.c_uint64), ("body_bytes", C.c_uint64),
                 ("scratch_bytes", C.c_uint64), ("out_cap_bytes", C.c_uint64), ("k10_ms", C.c_double),
                 ("runs", C.c_uint64)]
+
+
+class RollupGroup(C.Structure):
+    _fields_ = [("first_doc", C.c_uint32), ("n_members", C.c_uint32), ("sums", C.c_int32 * 5),
+                ("reserved", C.c_uint32)]
+
+
+class Rollup(C.Structure):
+    _fields_ = [("n_docs", C.c_size_t), ("doc_group", C.c_void_p), ("n_groups", C.c_size_t), ("groups", C.c_void_p),
+                ("k11_status", C.c_void_p), ("n_host", C.c_size_t), ("host_grouped", C.c_uint32),
+                ("internal", C.c_void_p)]
+
+
+class RBatchStats(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("json_bytes", C.c_uint64), ("scratch_bytes", C.c_uint64),
+                ("k11_ms", C.c_double), ("k12_ms", C.c_double), ("runs", C.c_uint64)]
 
 
 class HBatchInfo(C.Structure):
@@ -188,6 +205,17 @@ SIGNATURES = [
     ("gpudiff_wbatch_free", None, [_P, _P]),
     ("gpudiff_upsert_body_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_size_t,
                                            C.POINTER(C.c_size_t)]),
+    ("gpudiff_rbatch_create", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                        C.POINTER(_P)]),
+    ("gpudiff_rbatch_run", C.c_int, [_P, _P]),
+    ("gpudiff_rbatch_fetch", C.c_int, [_P, _P, C.POINTER(Rollup)]),
+    ("gpudiff_rbatch_stats_get", C.c_int, [_P, C.POINTER(RBatchStats)]),
+    ("gpudiff_rbatch_free", None, [_P, _P]),
+    ("gpudiff_rollup_status", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                        C.POINTER(Rollup)]),
+    ("gpudiff_rollup_release", None, [_P, C.POINTER(Rollup)]),
+    ("gpudiff_rollup_doc_host", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int32), C.c_void_p, C.c_size_t,
+                                          C.POINTER(C.c_size_t)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
@@ -543,6 +571,19 @@ class Engine:
     def wbatch(self, docs, mode: int = UPSERT_SPEC) -> "WBatch":
         return WBatch(self, docs, mode)
 
+    # ---- Deployment splitter status roll-up
+    def rollup_status(self, docs) -> "RollupResult":
+        """Kernels K11 + K12 (host path for K11's deferrals) over cached Deployments."""
+        rb = self.rbatch(docs)
+        try:
+            rb.run()
+            return rb.fetch()
+        finally:
+            rb.close()
+
+    def rbatch(self, docs) -> "RBatch":
+        return RBatch(self, docs)
+
     def k0_profile(self, enable: bool = True):
         """K0 per-phase wall-clock ticks (100 MHz) summed over waves since the last call."""
         out = (C.c_uint64 * 8)()
@@ -629,6 +670,92 @@ class WBatch:
             self.close()
         except Exception:
             pass
+
+
+@dataclass
+class RollupResult:
+    """deployment.go:41-91 over a batch: per document its group (or ROLLUP_NONE /
+    ROLLUP_DECODE); per group (ascending first_doc) the int32 status sums."""
+    doc_group: np.ndarray          # int32 [n]
+    first_doc: np.ndarray          # uint32 [groups]: others[0]
+    n_members: np.ndarray          # uint32 [groups]
+    sums: np.ndarray               # int32 [groups, 5]
+    k11_status: np.ndarray         # K11's TOK_* per document
+    n_host: int
+    host_grouped: bool
+
+    def as_dict(self):
+        return {"doc_group": self.doc_group.tolist(),
+                "groups": [{"first_doc": int(f), "n_members": int(m), "sums": [int(x) for x in s]}
+                           for f, m, s in zip(self.first_doc, self.n_members, self.sums)]}
+
+
+class RBatch:
+    """Cached Deployments resident in HBM for K11/K12 (gpudiff_rbatch_*)."""
+
+    def __init__(self, eng: "Engine", docs):
+        self.eng = eng
+        self.docs, self._bufs, ptrs, lens = _doc_arrays(docs)
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_rbatch_create(eng.ctx, ptrs, lens, len(self.docs), C.byref(h)), "gpudiff_rbatch_create")
+        self.h = h
+
+    def run(self):
+        _chk(_lib.gpudiff_rbatch_run(self.eng.ctx, self.h), "gpudiff_rbatch_run")
+
+    def fetch(self) -> RollupResult:
+        r = Rollup()
+        _chk(_lib.gpudiff_rbatch_fetch(self.eng.ctx, self.h, C.byref(r)), "gpudiff_rbatch_fetch")
+        try:
+            n, g = r.n_docs, r.n_groups
+            if n:
+                dg = np.ctypeslib.as_array(C.cast(r.doc_group, C.POINTER(C.c_int32)), (n,)).copy()
+                k11 = np.ctypeslib.as_array(C.cast(r.k11_status, C.POINTER(C.c_int32)), (n,)).copy()
+            else:
+                dg = np.zeros(0, np.int32)
+                k11 = np.zeros(0, np.int32)
+            if g:
+                raw = np.frombuffer(C.string_at(r.groups, 32 * g), dtype=np.uint32).reshape(g, 8)
+            else:
+                raw = np.zeros((0, 8), np.uint32)
+            return RollupResult(dg, raw[:, 0].copy(), raw[:, 1].copy(), raw[:, 2:7].view(np.int32).copy(), k11,
+                                int(r.n_host), bool(r.host_grouped))
+        finally:
+            _lib.gpudiff_rollup_release(self.eng.ctx, C.byref(r))
+
+    def stats(self) -> RBatchStats:
+        st = RBatchStats()
+        _chk(_lib.gpudiff_rbatch_stats_get(self.h, C.byref(st)), "gpudiff_rbatch_stats_get")
+        return st
+
+    def close(self):
+        if self.h:
+            _lib.gpudiff_rbatch_free(self.eng.ctx, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rollup_doc_host(doc):
+    """The roll-up host path for one document: ([5 x int32], owned-by bytes or None), or None when Go
+    cannot decode it."""
+    b = to_json_bytes(doc)
+    v = (C.c_int32 * 5)()
+    n = C.c_size_t()
+    buf = C.create_string_buffer(max(1, len(b)))
+    rc = _lib.gpudiff_rollup_doc_host(b, len(b), v, C.cast(buf, C.c_void_p), len(b) + 1, C.byref(n))
+    if rc == E_DECODE:
+        return None
+    if rc == E_CAPACITY:  # a decoded label never outgrows ~3x its JSON text
+        buf = C.create_string_buffer(n.value)
+        rc = _lib.gpudiff_rollup_doc_host(b, len(b), v, C.cast(buf, C.c_void_p), n.value, C.byref(n))
+    _chk(rc, "gpudiff_rollup_doc_host")
+    label = None if n.value == C.c_size_t(-1).value else buf.raw[:n.value]
+    return list(v), label
 
 
 def upsert_body_host(doc, mode: int = UPSERT_SPEC) -> Optional[bytes]:

@@ -160,3 +160,57 @@ class Population:
         st = ((truth & STATUS_MUT) != 0) | ((truth & B_HAS_STATUS) == 0)
         f |= np.where(st, G.STATUS_DIRTY, 0).astype(np.uint8)
         return f
+
+
+# ------------------------------------------------------------------ roll-up population
+
+_DEP_TMPL = ('{"apiVersion":"apps/v1","kind":"Deployment","metadata":{"annotations":{"deployment.kubernetes.io/'
+             'revision":"1"},"clusterName":"%s","creationTimestamp":"2021-10-04T15:09:37Z","generation":%d,'
+             '"labels":{%s},"name":"%s","namespace":"%s","resourceVersion":"%d","uid":"%08x-5ac9-4f5e-9d3e-'
+             '%012x"},"spec":{"progressDeadlineSeconds":600,"replicas":%d,"revisionHistoryLimit":10,"selector":'
+             '{"matchLabels":{"app":"%s"}},"strategy":{"rollingUpdate":{"maxSurge":"25%%","maxUnavailable":"25%%"},'
+             '"type":"RollingUpdate"},"template":{"metadata":{"creationTimestamp":null,"labels":{"app":"%s"}},'
+             '"spec":{"containers":[{"image":"quay.io/kcp-dev/%s:v%d","imagePullPolicy":"IfNotPresent","name":'
+             '"%s","resources":{},"terminationMessagePath":"/dev/termination-log","terminationMessagePolicy":'
+             '"File"}],"dnsPolicy":"ClusterFirst","restartPolicy":"Always","schedulerName":"default-scheduler",'
+             '"securityContext":{},"terminationGracePeriodSeconds":30}}},"status":{"availableReplicas":%d,'
+             '"conditions":[{"lastTransitionTime":"2021-10-04T15:09:51Z","lastUpdateTime":"2021-10-04T15:09:51Z",'
+             '"message":"Deployment has minimum availability.","reason":"MinimumReplicasAvailable","status":"True",'
+             '"type":"Available"},{"lastTransitionTime":"2021-10-04T15:09:37Z","lastUpdateTime":'
+             '"2021-10-04T15:09:51Z","message":"ReplicaSet \\"%s-66b6c48dd5\\" has successfully progressed.",'
+             '"reason":"NewReplicaSetAvailable","status":"True","type":"Progressing"}],"observedGeneration":%d,'
+             '"readyReplicas":%d,"replicas":%d,"unavailableReplicas":%d,"updatedReplicas":%d}}')
+
+
+def rollup_population(n_roots: int, leaves_per_root: int = 4, seed: int = 20211004 + 6, shuffle: bool = True):
+    """Cached Deployments as the splitter's informer holds them: per root one
+    Deployment without an owned-by label and `leaves_per_root` leaves labelled
+    kcp.dev/cluster=<cluster>, kcp.dev/owned-by=<root> (deployment.go:127-160),
+    with seeded status counters; API-server JSON (sorted keys, no whitespace).
+    Returns (docs, roots): roots[i] = index of root i's own document."""
+    rng = np.random.default_rng(seed)
+    n = n_roots * (1 + leaves_per_root)
+    st = rng.integers(0, 50, size=(n, 5)).tolist()
+    order = rng.permutation(n).tolist() if shuffle else list(range(n))
+    docs = [b""] * n
+    roots = [0] * n_roots
+    k = 0
+    for r in range(n_roots):
+        name = "web-%07d" % r
+        ns = "ns-%04d" % (r % 997)
+        lc = "lc-%05d" % (r % 100000)
+        for j in range(1 + leaves_per_root):
+            idx = order[k]
+            s = st[k]
+            k += 1
+            if j == 0:
+                labels = '"app":"%s"' % name
+                dname = name
+                roots[r] = idx
+            else:
+                labels = '"app":"%s","kcp.dev/cluster":"cluster-%d","kcp.dev/owned-by":"%s"' % (name, j, name)
+                dname = "%s--cluster-%d" % (name, j)
+            docs[idx] = (_DEP_TMPL % (lc, 1 + (r & 3), labels, dname, ns, 1000 + idx, idx, r, s[0], name, name,
+                                      name, 1 + (r & 7), name, s[3], name, 1 + (r & 3), s[2], s[0], s[4],
+                                      s[1])).encode()
+    return docs, roots

@@ -6,14 +6,14 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "liboracle.so")
-SRC = os.path.join(HERE, "deepequal_ref.cpp")
+SRCS = [os.path.join(HERE, "deepequal_ref.cpp"), os.path.join(HERE, "rollup_ref.cpp")]
 
 
 def build() -> str:
     os.makedirs(OUT, exist_ok=True)
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(SRC):
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in SRCS):
         return LIB
-    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", SRC, "-o", LIB]
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread"] + SRCS + ["-o", LIB]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("oracle build failed:\n" + r.stdout + r.stderr)

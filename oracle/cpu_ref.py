@@ -31,6 +31,13 @@ def lib():
         l.oracle_upsert_run.restype = C.c_int
         l.oracle_upsert_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double),
                                         C.POINTER(C.c_uint64)]
+        l.oracle_rollup_load.restype = C.c_void_p
+        l.oracle_rollup_load.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t]
+        l.oracle_rollup_free.restype = None
+        l.oracle_rollup_free.argtypes = [C.c_void_p]
+        l.oracle_rollup_run.restype = C.c_int
+        l.oracle_rollup_run.argtypes = [C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double), C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t)]
         _lib = l
     return _lib
 
@@ -96,6 +103,46 @@ class DecodedDocs:
     def close(self):
         if self.h:
             lib().oracle_docs_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RollupDocs:
+    """Cached Deployments (JSON) for the roll-up restatement (oracle/rollup_ref.cpp):
+    typed-field decode + group by owned-by + int32 sums, decode timed."""
+
+    def __init__(self, docs):
+        n = len(docs)
+        self.n = n
+        D = (C.c_char_p * max(n, 1))(*docs)
+        L = (C.c_size_t * max(n, 1))(*[len(d) for d in docs])
+        self.h = lib().oracle_rollup_load(D, L, n)
+
+    def run(self, threads=1, min_seconds=0.0):
+        """-> (sweeps, seconds, result dict like rollup_oracle.rollup without owned_by)"""
+        n = self.n
+        dg = np.zeros(max(n, 1), np.int32)
+        first = np.zeros(max(n, 1), np.uint32)
+        cnt = np.zeros(max(n, 1), np.uint32)
+        sums = np.zeros(max(5 * n, 1), np.int32)
+        ng = C.c_size_t()
+        sec = C.c_double()
+        sw = lib().oracle_rollup_run(self.h, threads, min_seconds, C.byref(sec), dg.ctypes.data, first.ctypes.data,
+                                     cnt.ctypes.data, sums.ctypes.data, C.byref(ng))
+        g = ng.value
+        res = {"doc_group": dg[:n].tolist(),
+               "groups": [{"first_doc": int(first[i]), "n_members": int(cnt[i]), "sums": sums[5 * i:5 * i + 5].tolist()}
+                          for i in range(g)]}
+        return sw, sec.value, res
+
+    def close(self):
+        if self.h:
+            lib().oracle_rollup_free(self.h)
             self.h = None
 
     def __del__(self):
