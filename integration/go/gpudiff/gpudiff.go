@@ -408,3 +408,75 @@ func (e *Engine) UpsertBodies(objs []interface{}, mode Mode) ([][]byte, error) {
 	}
 	return res, nil
 }
+
+// RollupGroup is the status roll-up of one root Deployment
+// (pkg/reconciler/deployment/deployment.go:71-91): the int32 sums of its
+// leaves' status counters and the index of others[0] (whose
+// status.conditions the root copies).
+type RollupGroup struct {
+	FirstDoc            int
+	Members             int
+	Replicas            int32
+	UpdatedReplicas     int32
+	ReadyReplicas       int32
+	AvailableReplicas   int32
+	UnavailableReplicas int32
+}
+
+// Rollup groups are keyed by doc index: DocGroup[i] is the group of docs[i],
+// or RollupNone (no kcp.dev/owned-by label) / RollupDecode (Go cannot decode
+// the document into an appsv1.Deployment).
+const (
+	RollupNone   = int(C.GPUDIFF_ROLLUP_NONE)
+	RollupDecode = int(C.GPUDIFF_ROLLUP_DECODE)
+)
+
+// RollupStatus aggregates every root's status at once from the JSON of the
+// cached Deployments (kernels K11 + K12; the host path decides what K11
+// leaves): the answer of the splitter's reconcile loop for each root, with
+// others[0] fixed to the lowest document index.  Groups are in order of first
+// appearance.
+func (e *Engine) RollupStatus(docs [][]byte) ([]RollupGroup, []int, error) {
+	n := len(docs)
+	if n == 0 {
+		return nil, nil, nil
+	}
+	dptr := C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	lens := C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.size_t(0))))
+	defer C.free(dptr)
+	defer C.free(lens)
+	dp := (*[1 << 30]*C.uint8_t)(dptr)[:n:n]
+	lp := (*[1 << 30]C.size_t)(lens)[:n:n]
+	for i, b := range docs {
+		dp[i], lp[i] = cmem(b)
+	}
+	defer func() {
+		for i := range dp {
+			C.free(unsafe.Pointer(dp[i]))
+		}
+	}()
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	var out C.gpudiff_rollup
+	if err := errOf(C.gpudiff_rollup_status(e.ctx, (**C.uint8_t)(dptr), (*C.size_t)(lens), C.size_t(n),
+		&out)); err != nil {
+		return nil, nil, err
+	}
+	defer C.gpudiff_rollup_release(e.ctx, &out)
+	dg := (*[1 << 30]C.int32_t)(unsafe.Pointer(out.doc_group))[:n:n]
+	docGroup := make([]int, n)
+	for i := range dg {
+		docGroup[i] = int(dg[i])
+	}
+	ng := int(out.n_groups)
+	groups := make([]RollupGroup, ng)
+	if ng > 0 {
+		gs := (*[1 << 28]C.gpudiff_rollup_group)(unsafe.Pointer(out.groups))[:ng:ng]
+		for i, g := range gs {
+			groups[i] = RollupGroup{FirstDoc: int(g.first_doc), Members: int(g.n_members),
+				Replicas: int32(g.sums[0]), UpdatedReplicas: int32(g.sums[1]), ReadyReplicas: int32(g.sums[2]),
+				AvailableReplicas: int32(g.sums[3]), UnavailableReplicas: int32(g.sums[4])}
+		}
+	}
+	return groups, docGroup, nil
+}
