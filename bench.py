@@ -44,10 +44,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5", "upsert", "rollup"],
+    ap.add_argument("--config", default="config3", choices=["config1", "config2", "config3", "config4", "config5", "upsert", "rollup", "negotiate"],
                     help="config5 = watch replay through the device-resident object store (bench_replay.py); "
                          "upsert = the write path's request bodies, kernel K10 (bench_upsert.py); "
-                         "rollup = the Deployment splitter's status roll-up, K11 + K12 (bench_rollup.py)")
+                         "rollup = the Deployment splitter's status roll-up, K11 + K12 (bench_rollup.py); "
+                         "negotiate = the API-negotiation update classifier, K13 + K14 (bench_negotiate.py)")
     ap.add_argument("--docs", type=int, default=131072, help="upsert: documents resident in HBM")
     ap.add_argument("--roots", type=int, default=250000, help="rollup: root Deployments")
     ap.add_argument("--leaves", type=int, default=4, help="rollup: leaf Deployments per root")
@@ -82,6 +83,11 @@ def main():
         import bench_rollup
 
         return bench_rollup.run(args)
+    if args.config == "negotiate":
+        import bench_negotiate
+        args.pairs = args.pairs or 500000
+        args.cpu_sample = min(args.cpu_sample, 10000)
+        return bench_negotiate.run(args)
     if args.config == "config5":
         import bench_replay
         args.sample = min(args.sample, 300)

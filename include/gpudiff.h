@@ -454,6 +454,49 @@ void gpudiff_rollup_release(gpudiff_ctx* ctx, gpudiff_rollup* r);
 int gpudiff_rollup_doc_host(const uint8_t* doc, size_t len, int32_t* v, uint8_t* label, size_t cap,
                             size_t* label_len);
 
+/* ---- API-negotiation update classifier (second half) ----
+ * Replaces the "Update" branch of Controller.enqueue,
+ * pkg/reconciler/apiresource/controller.go:253-283, for APIResourceImport and
+ * NegotiatedAPIResource objects (both have status {conditions: [{type, status,
+ * lastTransitionTime, reason, message}]}).  Per (old, new) pair: no old object
+ * -> CREATED; equal resourceVersion -> IGNORE; different generation -> SPEC;
+ * status not Semantic.DeepEqual (nil == empty, metav1.Time by instant) ->
+ * STATUS; annotations differ OR labels EQUAL (the reference's missing `!` at
+ * :278, reproduced) -> META; else IGNORE.  Objects are decoded with Go 1.16
+ * encoding/json typed rules; a pair with a side Go cannot decode -> DECODE.
+ * Kernel K13 (negotiation mode of k_encode_docs) extracts each document's
+ * fields, K14 classifies each pair on the device; pairs with a document outside
+ * K13's subset are classified by the host path (gpudiff_negotiate_pair_host). */
+#define GPUDIFF_NEG_IGNORE 0
+#define GPUDIFF_NEG_SPEC 1     /* SpecChanged */
+#define GPUDIFF_NEG_STATUS 2   /* StatusOnlyChanged */
+#define GPUDIFF_NEG_META 3     /* AnnotationOrLabelsOnlyChanged */
+#define GPUDIFF_NEG_CREATED 4  /* no old object */
+#define GPUDIFF_NEG_DECODE (-1)
+
+typedef struct gpudiff_nbatch gpudiff_nbatch;
+typedef struct gpudiff_nbatch_stats {
+    uint64_t n_pairs, json_bytes, scratch_bytes, n_host;
+    double k13_ms, k14_ms;  /* mean durations over the timed runs (GPUDIFF_OPT_TIMING) */
+    uint64_t runs;
+} gpudiff_nbatch_stats;
+/* olds[i] == NULL: no old object.  The documents are uploaded once into HBM;
+ * run = K13 + K14 on the context stream (asynchronous); fetch = actions[n] to
+ * the host, host path for the deferred pairs.  The caller's buffers must stay
+ * valid until gpudiff_nbatch_free. */
+int gpudiff_nbatch_create(gpudiff_ctx* ctx, const uint8_t* const* olds, const size_t* old_lens,
+                          const uint8_t* const* news, const size_t* new_lens, size_t n, gpudiff_nbatch** out);
+int gpudiff_nbatch_run(gpudiff_ctx* ctx, gpudiff_nbatch* nb);
+int gpudiff_nbatch_fetch(gpudiff_ctx* ctx, gpudiff_nbatch* nb, int32_t* actions);
+int gpudiff_nbatch_stats_get(const gpudiff_nbatch* nb, gpudiff_nbatch_stats* st);
+void gpudiff_nbatch_free(gpudiff_ctx* ctx, gpudiff_nbatch* nb);
+/* create + run + fetch + free */
+int gpudiff_classify_updates(gpudiff_ctx* ctx, const uint8_t* const* olds, const size_t* old_lens,
+                             const uint8_t* const* news, const size_t* new_lens, size_t n, int32_t* actions);
+/* the host path for one pair (old == NULL: no old object) */
+int gpudiff_negotiate_pair_host(const uint8_t* old_json, size_t old_len, const uint8_t* new_json, size_t new_len,
+                                int32_t* action);
+
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,
                        const uint8_t* new_json, size_t new_len, int* equal);

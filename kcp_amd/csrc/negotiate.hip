@@ -1,0 +1,91 @@
+// K14: the API-negotiation update classifier over K13's per-document fields
+// (pkg/reconciler/apiresource/controller.go:253-283).
+// One lane per (old, new) pair: documents 2i (old) and 2i+1 (new) of the batch.
+// The work per pair is a handful of short span compares on 2 x 944-byte NegOut
+// records; like K12 it is latency-bound and tiny next to K13.
+#include <hip/hip_runtime.h>
+
+#include "../../include/gpudiff.h"
+#include "tokenize.h"
+
+namespace gd {
+
+namespace {
+
+__device__ __forceinline__ bool span_eq(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_t bl) {
+    if (al != bl) return false;
+    for (uint32_t i = 0; i < al; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// Semantic.DeepEqual of two map[string]string (nil == empty; K13 left no repeated keys)
+__device__ bool map_eq(const NegMember* a, uint32_t na, const uint8_t* da, const NegMember* b, uint32_t nb,
+                       const uint8_t* db) {
+    if (na != nb) return false;
+    for (uint32_t i = 0; i < na; i++) {
+        const NegMember x = a[i];
+        bool found = false;
+        for (uint32_t j = 0; j < nb && !found; j++) {
+            const NegMember y = b[j];
+            if (span_eq(da + x.koff, x.klen, db + y.koff, y.klen)) {
+                if (!span_eq(da + x.voff, x.vlen, db + y.voff, y.vlen)) return false;
+                found = true;
+            }
+        }
+        if (!found) return false;
+    }
+    return true;
+}
+
+// Semantic.DeepEqual of the two statuses: conditions element-wise (nil == empty),
+// strings by bytes, metav1.Time by instant (a.UTC() == b.UTC())
+__device__ bool status_eq(const NegOut& A, const uint8_t* da, const NegOut& B, const uint8_t* db) {
+    if (A.n_cond != B.n_cond) return false;
+    for (uint32_t c = 0; c < A.n_cond; c++) {
+        const NegCond& x = A.cond[c];
+        const NegCond& y = B.cond[c];
+        if (x.sec != y.sec || x.nsec != y.nsec) return false;
+        for (uint32_t f = 0; f < 4; f++)
+            if (!span_eq(da + x.off[f], x.len[f], db + y.off[f], y.len[f])) return false;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_negotiate_pairs(const NegOut* __restrict__ outs, const uint8_t* __restrict__ absent,
+                                                         const TokDoc* __restrict__ docs, const uint8_t* __restrict__ json,
+                                                         uint32_t n, int32_t* __restrict__ actions) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NegOut& B = outs[2u * i + 1u];
+    int32_t act;
+    if (B.status != GPUDIFF_TOK_OK) {
+        act = kNegDefer;
+    } else if (absent[i]) {
+        act = GPUDIFF_NEG_CREATED;  // controller.go:258-261
+    } else {
+        const NegOut& A = outs[2u * i];
+        const uint8_t* da = json + docs[2u * i].json_off;
+        const uint8_t* db = json + docs[2u * i + 1u].json_off;
+        if (A.status != GPUDIFF_TOK_OK) act = kNegDefer;
+        else if (span_eq(da + A.rv_off, A.rv_len, db + B.rv_off, B.rv_len)) act = GPUDIFF_NEG_IGNORE;  // :263-265
+        else if (A.gen != B.gen) act = GPUDIFF_NEG_SPEC;                                                 // :267-270
+        else if (!status_eq(A, da, B, db)) act = GPUDIFF_NEG_STATUS;                                     // :272-275
+        else if (!map_eq(A.ann, A.n_ann, da, B.ann, B.n_ann, db) || map_eq(A.lab, A.n_lab, da, B.lab, B.n_lab, db))
+            act = GPUDIFF_NEG_META;  // :277-281, the missing `!` before the labels term kept
+        else
+            act = GPUDIFF_NEG_IGNORE;  // :282-283
+    }
+    actions[i] = act;
+}
+
+}  // namespace
+
+hipError_t launch_negotiate_pairs(hipStream_t s, const NegOut* outs, const uint8_t* absent, const TokDoc* docs,
+                                  const uint8_t* json, uint32_t n_pairs, int32_t* actions) {
+    if (!n_pairs) return hipSuccess;
+    k_negotiate_pairs<<<(n_pairs + 255u) / 256u, 256, 0, s>>>(outs, absent, docs, json, n_pairs, actions);
+    return hipGetLastError();
+}
+
+}  // namespace gd

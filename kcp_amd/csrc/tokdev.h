@@ -687,7 +687,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 }
 constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u, MF_FLOAT = 16u;
 constexpr uint32_t kMarshalMaxMembers = 2048;
-constexpr int kModeEncode = 0, kModeMarshal = 1, kModeRollup = 2;
+constexpr int kModeEncode = 0, kModeMarshal = 1, kModeRollup = 2, kModeNegotiate = 3;
 
 // K11 (roll-up mode): Go's struct field lookup for an ASCII key -- 0 no
 // match, 1 exact, 2 equal only under ASCII case folding (encoding/json
@@ -710,6 +710,72 @@ __device__ __forceinline__ const char* roll_field(uint32_t k) {
 }
 __device__ __forceinline__ uint32_t roll_field_len(uint32_t k) {
     return k == 0 ? 8u : k == 1 ? 15u : k == 2 ? 13u : k == 3 ? 17u : 19u;
+}
+
+// K13 (negotiation mode): metav1.Time's time.Parse(time.RFC3339, s) for the
+// strict shape "YYYY-MM-DDTHH:MM:SS[.f{1,9}](Z|+hh:mm|-hh:mm)" (2-digit hour);
+// false = not certain (other shapes Go may accept, range errors): the host decides
+__device__ __forceinline__ int64_t neg_days_from_civil(int64_t y, uint32_t m, uint32_t d) {
+    y -= m <= 2u;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * (int64_t)(m + (m > 2u ? -3 : 9)) + 2) / 5 + (int64_t)d - 1;
+    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+__device__ __forceinline__ bool neg_parse_time(const uint8_t* s, uint32_t l, int64_t* sec, int32_t* nsec) {
+    if (l < 20u) return false;
+    auto dg = [&](uint32_t i) -> uint32_t { return (uint32_t)s[i] - '0'; };
+    const uint32_t dpos[14] = {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18};
+#pragma unroll
+    for (uint32_t k = 0; k < 14; k++)
+        if (dg(dpos[k]) > 9u) return false;
+    if (s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':' || s[16] != ':') return false;
+    const uint32_t year = dg(0) * 1000u + dg(1) * 100u + dg(2) * 10u + dg(3);
+    const uint32_t mon = dg(5) * 10u + dg(6), day = dg(8) * 10u + dg(9);
+    const uint32_t hh = dg(11) * 10u + dg(12), mi = dg(14) * 10u + dg(15), ss = dg(17) * 10u + dg(18);
+    if (mon < 1u || mon > 12u || hh >= 24u || mi >= 60u || ss >= 60u || day < 1u) return false;
+    const bool leap = (year % 4u == 0u) && (year % 100u != 0u || year % 400u == 0u);
+    const uint32_t dim = mon == 2u ? (leap ? 29u : 28u) : (mon == 4u || mon == 6u || mon == 9u || mon == 11u) ? 30u : 31u;
+    if (day > dim) return false;
+    uint32_t p = 19u;
+    int32_t ns = 0;
+    if (s[p] == '.' && p + 1u < l && dg(p + 1u) <= 9u) {
+        uint32_t n = 0;
+        p++;
+        while (p < l && dg(p) <= 9u) {
+            if (++n > 9u) return false;
+            ns = ns * 10 + (int32_t)dg(p);
+            p++;
+        }
+        for (uint32_t k = n; k < 9u; k++) ns *= 10;
+    }
+    int64_t off = 0;
+    if (p < l && s[p] == 'Z') {
+        p++;
+    } else {
+        if (p + 6u != l || (s[p] != '+' && s[p] != '-') || s[p + 3u] != ':' || dg(p + 1u) > 9u || dg(p + 2u) > 9u ||
+            dg(p + 4u) > 9u || dg(p + 5u) > 9u)
+            return false;
+        off = ((int64_t)(dg(p + 1u) * 10u + dg(p + 2u)) * 60 + (int64_t)(dg(p + 4u) * 10u + dg(p + 5u))) * 60;
+        if (s[p] == '-') off = -off;
+        p += 6u;
+    }
+    if (p != l) return false;
+    *sec = neg_days_from_civil((int64_t)year, mon, day) * 86400 + (int64_t)(hh * 3600u + mi * 60u + ss) - off;
+    *nsec = ns;
+    return true;
+}
+__device__ __forceinline__ const char* neg_meta_field(uint32_t k) {
+    return k == 0 ? "resourceVersion" : k == 1 ? "generation" : k == 2 ? "labels" : "annotations";
+}
+__device__ __forceinline__ uint32_t neg_meta_field_len(uint32_t k) { return k == 0 ? 15u : k == 1 ? 10u : k == 2 ? 6u : 11u; }
+// APIResourceImportCondition / NegotiatedAPIResourceCondition json names, NegCond order + time last
+__device__ __forceinline__ const char* neg_cond_field(uint32_t k) {
+    return k == 0 ? "type" : k == 1 ? "status" : k == 2 ? "reason" : k == 3 ? "message" : "lastTransitionTime";
+}
+__device__ __forceinline__ uint32_t neg_cond_field_len(uint32_t k) {
+    return k == 0 ? 4u : k == 1 ? 6u : k == 2 ? 6u : k == 3 ? 7u : 18u;
 }
 
 struct Scratch {

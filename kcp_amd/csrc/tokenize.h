@@ -120,6 +120,33 @@ __host__ __device__ inline uint64_t rollup_scratch_bytes(uint32_t len) {
     return tok_align(4ull * tok_cap(len)) + tok_align(16ull * node_cap(len)) + tok_align((uint64_t)len + 32u);
 }
 
+// K13 (k_encode_docs in negotiation mode, the API-negotiation update
+// classifier): per document, the fields controller.go:253-283 reads, as spans
+// into the document (no escapes) and parsed values; a nonzero status leaves
+// every pair holding the document to the host path.
+constexpr uint32_t kNegMaxMembers = 16;  // labels / annotations entries on the device
+constexpr uint32_t kNegMaxConds = 8;     // status.conditions elements on the device
+struct NegMember {
+    uint32_t koff, klen, voff, vlen;
+};
+struct NegCond {
+    uint32_t off[4], len[4];  // type, status, reason, message
+    int64_t sec;              // lastTransitionTime: unix seconds (zero Time: -62135596800)
+    int32_t nsec;
+    uint32_t pad;
+};
+struct NegOut {
+    uint32_t status;          // GPUDIFF_TOK_*
+    uint32_t n_lab, n_ann, n_cond;
+    uint32_t rv_off, rv_len, pad0, pad1;
+    int64_t gen;
+    int64_t pad2;
+    NegMember lab[kNegMaxMembers], ann[kNegMaxMembers];
+    NegCond cond[kNegMaxConds];
+};
+static_assert(sizeof(NegCond) == 48 && sizeof(NegOut) == 944, "NegOut");
+constexpr int64_t kZeroTimeSec = -62135596800ll;
+
 constexpr uint32_t kTokMaxLen = (1u << 24) - 64u;  // token words hold 24-bit positions
 constexpr uint32_t kTokSlack = 32u;                 // readable bytes K0 needs after each staged document
 
@@ -179,6 +206,14 @@ hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, co
 // K11: roll-up fields per document into outs (RollOut[n]); scratch per document at docs[i].scratch_off
 hipError_t launch_rollup_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               RollOut* outs);
+// K13: negotiation fields per document into outs (NegOut[n]); scratch as K11's
+hipError_t launch_negotiate_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                                 NegOut* outs);
+// K14: one action per pair (old doc 2i, new doc 2i+1; absent[i]: no old object);
+// kNegDefer = the host decides the pair
+constexpr int32_t kNegDefer = -2;
+hipError_t launch_negotiate_pairs(hipStream_t s, const NegOut* outs, const uint8_t* absent, const TokDoc* docs,
+                                  const uint8_t* json, uint32_t n_pairs, int32_t* actions);
 // K12: group the documents by owned-by label (xxh64 radix sort + byte check),
 // int32 sums per group; see rollup.hip
 // K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)

@@ -73,6 +73,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 RollOut R{};
                 R.status = GPUDIFF_TOK_SIZE;
                 ((RollOut*)space)[doc_i] = R;
+            } else if constexpr (MODE == kModeNegotiate) {
+                ((NegOut*)space)[doc_i].status = GPUDIFF_TOK_SIZE;
             } else {
                 o.status = GPUDIFF_TOK_SIZE;
                 out[doc_i] = o;
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     }
     uint8_t* base = scratch + D.scratch_off;
     Scratch S;
-    if constexpr (MODE == kModeRollup) {
+    if constexpr (MODE == kModeRollup || MODE == kModeNegotiate) {
         S = Scratch{};
         S.tok = (uint32_t*)base;
         S.rec = (uint4*)(base + tok_align(4ull * tok_cap(len)));
@@ -447,6 +449,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     if constexpr (MODE == kModeRollup) {
 #include "rollup_phases.inc"
     }
+    if constexpr (MODE == kModeNegotiate) {
+#include "negotiate_phases.inc"
+    }
 
     const uint64_t seed = slots ? ((slots[links[doc_i].slot].flags >> 8) & 0xFFu) : D.seed;
     mark(1);
@@ -757,6 +762,15 @@ hipError_t launch_rollup_docs(hipStream_t s, const TokDoc* docs, uint32_t n, con
     const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     k_encode_docs<8, kModeRollup><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, (uint8_t*)outs, 0,
                                                                         nullptr, 0, nullptr, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_negotiate_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
+                                 NegOut* outs) {
+    if (!n) return hipSuccess;
+    const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    k_encode_docs<8, kModeNegotiate><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, (uint8_t*)outs, 0,
+                                                                           nullptr, 0, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -123,6 +123,11 @@ class RBatchStats(C.Structure):
                 ("k11_ms", C.c_double), ("k12_ms", C.c_double), ("runs", C.c_uint64)]
 
 
+class NBatchStats(C.Structure):
+    _fields_ = [("n_pairs", C.c_uint64), ("json_bytes", C.c_uint64), ("scratch_bytes", C.c_uint64),
+                ("n_host", C.c_uint64), ("k13_ms", C.c_double), ("k14_ms", C.c_double), ("runs", C.c_uint64)]
+
+
 class HBatchInfo(C.Structure):
     _fields_ = [("n_pairs", C.c_size_t), ("rows", C.c_void_p), ("pool", C.c_void_p), ("pool_bytes", C.c_uint64),
                 ("total_leaves", C.c_uint64), ("n_decode_errors", C.c_uint64), ("n_reseeded", C.c_uint64)]
@@ -216,6 +221,16 @@ SIGNATURES = [
     ("gpudiff_rollup_release", None, [_P, C.POINTER(Rollup)]),
     ("gpudiff_rollup_doc_host", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int32), C.c_void_p, C.c_size_t,
                                           C.POINTER(C.c_size_t)]),
+    ("gpudiff_nbatch_create", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(_P)]),
+    ("gpudiff_nbatch_run", C.c_int, [_P, _P]),
+    ("gpudiff_nbatch_fetch", C.c_int, [_P, _P, C.POINTER(C.c_int32)]),
+    ("gpudiff_nbatch_stats_get", C.c_int, [_P, C.POINTER(NBatchStats)]),
+    ("gpudiff_nbatch_free", None, [_P, _P]),
+    ("gpudiff_classify_updates", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
+                                           C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(C.c_int32)]),
+    ("gpudiff_negotiate_pair_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                              C.POINTER(C.c_int32)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_status_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
     ("gpudiff_resolve_path", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_uint64, C.c_uint8,
@@ -584,6 +599,19 @@ class Engine:
     def rbatch(self, docs) -> "RBatch":
         return RBatch(self, docs)
 
+    # ---- API-negotiation update classifier
+    def classify_updates(self, pairs) -> np.ndarray:
+        """Kernels K13 + K14 (host path for K13's deferrals): one NEG_* action per (old or None, new) pair."""
+        nb = self.nbatch(pairs)
+        try:
+            nb.run()
+            return nb.fetch()
+        finally:
+            nb.close()
+
+    def nbatch(self, pairs) -> "NBatch":
+        return NBatch(self, pairs)
+
     def k0_profile(self, enable: bool = True):
         """K0 per-phase wall-clock ticks (100 MHz) summed over waves since the last call."""
         out = (C.c_uint64 * 8)()
@@ -738,6 +766,64 @@ class RBatch:
             self.close()
         except Exception:
             pass
+
+
+NEG_IGNORE, NEG_SPEC, NEG_STATUS, NEG_META, NEG_CREATED, NEG_DECODE = 0, 1, 2, 3, 4, -1
+
+
+class NBatch:
+    """(old, new) pairs of APIResourceImport / NegotiatedAPIResource JSON resident in HBM for K13/K14
+    (gpudiff_nbatch_*); old None = no old object."""
+
+    def __init__(self, eng: "Engine", pairs):
+        self.eng = eng
+        pairs = list(pairs)
+        self.n = len(pairs)
+        olds = [None if a is None else to_json_bytes(a) for a, _ in pairs]
+        _, self._nb, nptrs, nlens = _doc_arrays([b for _, b in pairs])
+        _, self._ob, optrs, olens = _doc_arrays([a if a is not None else b"" for a in olds])
+        for i, a in enumerate(olds):
+            if a is None:
+                optrs[i] = None
+        h = C.c_void_p()
+        _chk(_lib.gpudiff_nbatch_create(eng.ctx, optrs, olens, nptrs, nlens, self.n, C.byref(h)),
+             "gpudiff_nbatch_create")
+        self.h = h
+
+    def run(self):
+        _chk(_lib.gpudiff_nbatch_run(self.eng.ctx, self.h), "gpudiff_nbatch_run")
+
+    def fetch(self) -> np.ndarray:
+        out = np.zeros(max(self.n, 1), np.int32)
+        _chk(_lib.gpudiff_nbatch_fetch(self.eng.ctx, self.h, out.ctypes.data_as(C.POINTER(C.c_int32))),
+             "gpudiff_nbatch_fetch")
+        return out[:self.n]
+
+    def stats(self) -> NBatchStats:
+        st = NBatchStats()
+        _chk(_lib.gpudiff_nbatch_stats_get(self.h, C.byref(st)), "gpudiff_nbatch_stats_get")
+        return st
+
+    def close(self):
+        if self.h:
+            _lib.gpudiff_nbatch_free(self.eng.ctx, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def negotiate_pair_host(old, new) -> int:
+    """The classifier's host path (Go-exact) for one pair; old None = no old object."""
+    a = None if old is None else to_json_bytes(old)
+    b = to_json_bytes(new)
+    act = C.c_int32()
+    _chk(_lib.gpudiff_negotiate_pair_host(a, 0 if a is None else len(a), b, len(b), C.byref(act)),
+         "gpudiff_negotiate_pair_host")
+    return int(act.value)
 
 
 def rollup_doc_host(doc):

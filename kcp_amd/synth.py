@@ -214,3 +214,87 @@ def rollup_population(n_roots: int, leaves_per_root: int = 4, seed: int = 202110
                                       name, 1 + (r & 7), name, s[3], name, 1 + (r & 3), s[2], s[0], s[4],
                                       s[1])).encode()
     return docs, roots
+
+
+def negotiate_population(n_pairs: int, seed: int = 20211004 + 7, variants: bool = True):
+    """(old, new) Update pairs of APIResourceImport / NegotiatedAPIResource JSON
+    for the API-negotiation classifier (pkg/reconciler/apiresource/controller.go:
+    238-295), API-server shaped (~1.3 KB: metadata with the kcp labels, a spec
+    with the columnDefinitions of a CommonAPIResourceSpec, 1-3 status
+    conditions).  Event mix: 15% resync (same resourceVersion), 20% generation
+    bump, 25% status change (condition status / reason / time / added), 15%
+    annotation change, 15% label change only, 10% nothing but resourceVersion.
+    With `variants`, 2% of the new objects carry a condition time written in
+    another zone (the same instant) and 0.5% a fold-case metadata key (a
+    document the device leaves to the host path).  Returns (pairs, expected
+    actions as designed by the generator)."""
+    rng = np.random.default_rng(seed)
+    kinds = ("APIResourceImport", "NegotiatedAPIResource")
+    cols = ",".join('{"name":"%s","type":"string","format":"","description":"%s column","priority":0,'
+                    '"jsonPath":".spec.%s"}' % (c, c, c) for c in ("Ready", "Phase", "Location", "Age"))
+
+    def doc(kind, name, rv, gen, labels, ann, conds, meta_key="metadata"):
+        lab = ",".join('"%s":"%s"' % kv for kv in labels)
+        an = ",".join('"%s":"%s"' % kv for kv in ann)
+        cs = ",".join('{"type":"%s","status":"%s","lastTransitionTime":"%s","reason":"%s","message":"%s"}' % c
+                      for c in conds)
+        return ('{"apiVersion":"apiresource.kcp.dev/v1alpha1","kind":"%s","%s":{"name":"%s","clusterName":"admin",'
+                '"uid":"5f0c%08x-8d1e-4c1b-9a61-0d1f2e3c4b5a","resourceVersion":"%d","generation":%d,'
+                '"creationTimestamp":"2021-10-04T15:09:37Z","labels":{%s},"annotations":{%s}},'
+                '"spec":{"groupVersion":{"group":"apps","version":"v1"},"plural":"%ss","singular":"%s",'
+                '"kind":"Widget","scope":"Namespaced","location":"us-east1","schemaUpdateStrategy":"UpdateUnpublished",'
+                '"columnDefinitions":[%s]},"status":{"conditions":[%s]}}' % (
+                    kind, meta_key, name, rv & 0xFFFFFFFF, rv, gen, lab, an, name, name, cols, cs)).encode()
+
+    pairs, want = [], []
+    u = rng.random(n_pairs)
+    v = rng.random(n_pairs)
+    for i in range(n_pairs):
+        kind = kinds[i & 1]
+        name = "widget%07d" % i
+        rv = 1000 + 7 * i
+        gen = 1 + (i % 5)
+        labels = [("kcp.dev/cluster", "lc-%05d" % (i % 10000)), ("app", "w%d" % (i % 97))]
+        ann = [("kcp.dev/schema", "v%d" % (i % 3))]
+        ts = "2021-10-%02dT%02d:%02d:%02dZ" % (1 + i % 28, i % 24, i % 60, (7 * i) % 60)
+        conds = [("Compatible", "True", ts, "Compatible", "schema is compatible")]
+        if i % 3:
+            conds.append(("Available", "True", ts, "Published", "negotiated"))
+        old = doc(kind, name, rv, gen, labels, ann, conds)
+        x = u[i]
+        nrv, ngen, nlab, nann, ncond = rv + 1, gen, labels, ann, list(conds)
+        if x < 0.15:
+            nrv, exp = rv, 0
+        elif x < 0.35:
+            ngen, exp = gen + 1, 1
+        elif x < 0.60:
+            c = ncond[0]
+            y = v[i]
+            if y < 0.4:
+                ncond[0] = (c[0], "False", c[2], "Incompatible", c[4])
+            elif y < 0.7:
+                ncond[0] = (c[0], c[1], "2021-11-01T00:00:00Z", c[3], c[4])
+            else:
+                ncond.append(("Enforced", "True", ts, "Enforced", "enforced"))
+            exp = 2
+        elif x < 0.75:
+            nann, exp = [("kcp.dev/schema", "v%d" % (i % 3 + 10))], 3
+        elif x < 0.90:
+            nlab, exp = labels[:1] + [("app", "moved")], 0   # the missing `!`: differing labels are ignored
+        else:
+            exp = 3                                           # equal labels: AnnotationOrLabelsOnlyChanged
+        meta_key = "metadata"
+        if variants and exp in (0, 3) and nrv != rv:
+            y = v[i]
+            if y < 0.02:  # the same instant, another zone
+                c = ncond[0]
+                hh = int(c[2][11:13])
+                day = int(c[2][8:10])
+                ncond[0] = (c[0], c[1], "2021-10-%02dT%02d:%s+01:00" % (day + (hh + 1) // 24, (hh + 1) % 24, c[2][14:19]),
+                            c[3], c[4])
+            elif y > 0.995:
+                meta_key = "Metadata"
+        new = doc(kind, name, nrv, ngen, nlab, nann, ncond, meta_key)
+        pairs.append((old, new))
+        want.append(exp)
+    return pairs, np.asarray(want, np.int32)

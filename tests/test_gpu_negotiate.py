@@ -1,0 +1,83 @@
+"""Kernels K13 (negotiation fields, negotiation mode of k_encode_docs) and K14
+(per-pair classification) on the GPU -- SURVEY.md §8(f) row 4,
+pkg/reconciler/apiresource/controller.go:238-295.  Every batch's actions must
+equal the oracle's (oracle/negotiate_oracle.py, pinned by
+tests/negotiate_cases.py); API-server-shaped populations must be classified
+entirely on the device."""
+import pytest
+
+from kcp_amd import gpudiff as G
+from kcp_amd import synth as S
+from oracle import negotiate_oracle as N
+from tests import negotiate_cases as C
+from tests.test_negotiate import fuzz_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(eng, pairs):
+    nb = eng.nbatch(pairs)
+    try:
+        nb.run()
+        got = nb.fetch().tolist()
+        st = nb.stats()
+    finally:
+        nb.close()
+    want = [N.classify(a, b) for a, b in pairs]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, (len(bad), bad[:5], [(got[i], want[i], pairs[i]) for i in bad[:2]])
+    return st
+
+
+def test_kat_batch():
+    eng = G.Engine(device=0)
+    pairs = [(a, b) for _, a, b, _ in C.cases()]
+    _check(eng, pairs)
+    eng.close()
+
+
+def test_clean_population_all_on_device():
+    eng = G.Engine(device=0)
+    pairs, want = S.negotiate_population(20000, seed=5, variants=False)
+    st = _check(eng, pairs)
+    assert st.n_host == 0
+    got = eng.classify_updates(pairs)
+    assert got.tolist() == want.tolist()
+    eng.close()
+
+
+def test_population_with_variants():
+    eng = G.Engine(device=0)
+    pairs, want = S.negotiate_population(20000, seed=6)
+    st = _check(eng, pairs)
+    # the fold-case metadata keys (0.5% of the ignorable events) are the only deferrals
+    assert 0 < st.n_host < 200
+    eng.close()
+
+
+def test_fuzz():
+    eng = G.Engine(device=0)
+    _check(eng, fuzz_pairs(4000, 20211004 + 72))
+    eng.close()
+
+
+def test_empty_and_repeated_runs():
+    eng = G.Engine(device=0)
+    assert eng.classify_updates([]).tolist() == []
+    pairs, want = S.negotiate_population(3000, seed=8, variants=False)
+    nb = eng.nbatch(pairs)
+    for _ in range(3):
+        nb.run()
+        assert nb.fetch().tolist() == want.tolist()
+    nb.close()
+    eng.close()
+
+
+def test_many_members_and_conditions_defer():
+    eng = G.Engine(device=0)
+    base = C.obj(rv="1", labels={"k%d" % i: "v" for i in range(20)}, conds=[C.cond(t="T%d" % i) for i in range(10)])
+    new = C.obj(rv="2", labels={"k%d" % i: "v" for i in range(20)}, conds=[C.cond(t="T%d" % i) for i in range(10)])
+    new2 = C.obj(rv="2", labels={"k%d" % i: "v" for i in range(20)}, conds=[C.cond(t="T%d" % i) for i in range(9)])
+    st = _check(eng, [(base, new), (base, new2), (new, base)])
+    assert st.n_host == 3
+    eng.close()
