@@ -480,3 +480,62 @@ func (e *Engine) RollupStatus(docs [][]byte) ([]RollupGroup, []int, error) {
 	}
 	return groups, docGroup, nil
 }
+
+// Update classification actions (GPUDIFF_NEG_*), the queue actions of
+// pkg/reconciler/apiresource/controller.go:159-166.
+const (
+	NegIgnore  = int32(C.GPUDIFF_NEG_IGNORE)  // dropped (:264, :283)
+	NegSpec    = int32(C.GPUDIFF_NEG_SPEC)    // SpecChanged
+	NegStatus  = int32(C.GPUDIFF_NEG_STATUS)  // StatusOnlyChanged
+	NegMeta    = int32(C.GPUDIFF_NEG_META)    // AnnotationOrLabelsOnlyChanged
+	NegCreated = int32(C.GPUDIFF_NEG_CREATED) // Created (no old object)
+	NegDecode  = int32(C.GPUDIFF_NEG_DECODE)  // a side Go cannot decode
+)
+
+// ClassifyUpdates is the batch form of the "Update" branch of
+// Controller.enqueue (controller.go:253-283) for APIResourceImport /
+// NegotiatedAPIResource JSON: one action per (olds[i], news[i]); olds[i] == nil
+// means no old object.  Kernels K13 + K14, host path for K13's deferrals.
+func (e *Engine) ClassifyUpdates(olds, news [][]byte) ([]int32, error) {
+	n := len(news)
+	if n == 0 {
+		return nil, nil
+	}
+	if len(olds) != n {
+		return nil, errOf(C.GPUDIFF_E_INVAL)
+	}
+	ptrSz := C.size_t(unsafe.Sizeof(uintptr(0)))
+	lenSz := C.size_t(unsafe.Sizeof(C.size_t(0)))
+	optr, olen := C.malloc(C.size_t(n)*ptrSz), C.malloc(C.size_t(n)*lenSz)
+	nptr, nlen := C.malloc(C.size_t(n)*ptrSz), C.malloc(C.size_t(n)*lenSz)
+	defer C.free(optr)
+	defer C.free(olen)
+	defer C.free(nptr)
+	defer C.free(nlen)
+	op := (*[1 << 30]*C.uint8_t)(optr)[:n:n]
+	ol := (*[1 << 30]C.size_t)(olen)[:n:n]
+	np := (*[1 << 30]*C.uint8_t)(nptr)[:n:n]
+	nl := (*[1 << 30]C.size_t)(nlen)[:n:n]
+	for i := 0; i < n; i++ {
+		op[i], ol[i] = nil, 0
+		if olds[i] != nil { // present, even when empty: a non-NULL pointer
+			op[i], ol[i] = (*C.uint8_t)(C.CBytes(append(olds[i][:len(olds[i]):len(olds[i])], 0))), C.size_t(len(olds[i]))
+		}
+		np[i], nl[i] = cmem(news[i])
+	}
+	defer func() {
+		for i := 0; i < n; i++ {
+			C.free(unsafe.Pointer(op[i]))
+			C.free(unsafe.Pointer(np[i]))
+		}
+	}()
+	actions := make([]int32, n)
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	rc := C.gpudiff_classify_updates(e.ctx, (**C.uint8_t)(optr), (*C.size_t)(olen), (**C.uint8_t)(nptr),
+		(*C.size_t)(nlen), C.size_t(n), (*C.int32_t)(unsafe.Pointer(&actions[0])))
+	if err := errOf(rc); err != nil {
+		return nil, err
+	}
+	return actions, nil
+}
