@@ -81,3 +81,19 @@ def test_many_members_and_conditions_defer():
     st = _check(eng, [(base, new), (base, new2), (new, base)])
     assert st.n_host == 3
     eng.close()
+
+
+def test_condition_times_vs_oracle():
+    """K13's strict-shape RFC3339 parser (or its deferral) against the oracle over random time strings."""
+    from tests.test_negotiate import random_times
+    eng = G.Engine(device=0)
+    times = random_times(3000, 4)
+    pairs = []
+    for i, t in enumerate(times):
+        a = C.obj(rv="1", conds=[C.cond(ltt=times[i - 1])])
+        b = C.obj(rv="2", conds=[C.cond(ltt=t)])
+        pairs.append((a, b))
+        pairs.append((b, C.obj(rv="3", conds=[C.cond(ltt=t.replace("Z", "+00:00"))])))
+    st = _check(eng, pairs)
+    assert st.n_host < len(pairs) // 3  # most shapes are parsed on the device, not deferred
+    eng.close()

@@ -86,3 +86,66 @@ def test_host_matches_oracle_fuzz():
     pairs = fuzz_pairs(3000, 20211004 + 71)
     bad = [i for i, (a, b) in enumerate(pairs) if G.negotiate_pair_host(a, b) != N.classify(a, b)]
     assert not bad, (len(bad), pairs[bad[0]], G.negotiate_pair_host(*pairs[bad[0]]), N.classify(*pairs[bad[0]]))
+
+
+def random_times(n, seed):
+    """RFC3339 strings across the whole range: valid ones in every zone/fraction shape, plus near misses."""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        y, mo, d = rng.randint(1, 9999), rng.randint(1, 12), rng.randint(1, 28)
+        h, mi, s = rng.randint(0, 23), rng.randint(0, 59), rng.randint(0, 59)
+        t = "%04d-%02d-%02dT%02d:%02d:%02d" % (y, mo, d, h, mi, s)
+        r = rng.random()
+        if r < 0.3:
+            t += "." + "".join(rng.choice("0123456789") for _ in range(rng.randint(1, 9)))
+        z = rng.random()
+        if z < 0.5:
+            t += "Z"
+        else:
+            t += "%s%02d:%02d" % (rng.choice("+-"), rng.randint(0, 23), rng.randint(0, 59))
+        m = rng.random()
+        if m < 0.05:
+            t = t.replace("T%02d" % h, "T%d" % h, 1)  # 1-digit hour (Go accepts)
+        elif m < 0.08:
+            t = t[:8] + "31" + t[10:]                  # day 31: out of range in short months
+        elif m < 0.10:
+            t = t[:5] + "02-29" + t[10:]                # leap days
+        elif m < 0.12:
+            t = t.replace(":", "", 1)                   # malformed
+        out.append(t)
+    return out
+
+
+def test_time_parse_vs_datetime():
+    import datetime as D
+    for t in random_times(4000, 3):
+        try:
+            got = N.parse_rfc3339(t)
+        except N.DecodeError:
+            got = None
+        want = None
+        try:
+            core, frac = t[:19], 0
+            rest = t[19:]
+            if len(t) >= 11 and t[10] == "T" and len(t[11:].split(":")[0]) == 1:
+                core = t[:11] + "0" + t[11:18]
+                rest = t[18:]
+            dt = D.datetime.strptime(core, "%Y-%m-%dT%H:%M:%S")
+            if rest.startswith("."):
+                k = 1
+                while k < len(rest) and rest[k].isdigit():
+                    k += 1
+                frac = int(rest[1:k].ljust(9, "0"))
+                rest = rest[k:]
+            if rest == "Z":
+                off = 0
+            elif len(rest) == 6 and rest[0] in "+-" and rest[3] == ":":
+                off = (int(rest[1:3]) * 60 + int(rest[4:6])) * 60 * (1 if rest[0] == "+" else -1)
+            else:
+                raise ValueError(rest)
+            secs = (dt - D.datetime(1970, 1, 1)) // D.timedelta(seconds=1) - off
+            want = (secs, frac)
+        except ValueError:
+            want = None
+        assert got == want, (t, got, want)
