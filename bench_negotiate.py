@@ -35,18 +35,47 @@ def log(*a):
     print("[negotiate]", *a, file=sys.stderr, flush=True)
 
 
+_POOL_PAIRS = None
+
+
+def _pool_work(k_T):
+    from oracle import negotiate_oracle as NO
+    k, T, n = k_T
+    return [NO.classify(a, b) for a, b in _POOL_PAIRS[k:n:T]]
+
+
+def _pool_baseline(pairs, n):
+    """The oracle on every host thread (min(16, affinity) forked processes), wall-clock over n pairs."""
+    import multiprocessing as mp
+    global _POOL_PAIRS
+    _POOL_PAIRS = pairs
+    T = max(1, min(16, len(os.sched_getaffinity(0))))
+    with mp.get_context("fork").Pool(T) as pool:
+        pool.map(_pool_work, [(k, T, k + 1) for k in range(T)])  # workers up, oracle imported
+        t = time.perf_counter()
+        pool.map(_pool_work, [(k, T, n) for k in range(T)])
+        dt = time.perf_counter() - t
+    return n / dt, T, n
+
+
 def run(args):
     import torch
 
     from kcp_amd import gpudiff as G
     from kcp_amd import synth as S
 
-    torch.cuda.set_device(0)
     t0 = time.time()
     pairs, want = S.negotiate_population(args.pairs)
     N = len(pairs)
     json_bytes = sum(len(a) + len(b) for a, b in pairs)
     log("%d Update pairs, %.2f GB of JSON, generated in %.1f s" % (N, json_bytes / 1e9, time.time() - t0))
+    # CPU baseline on all host threads first: forked workers share the population, and the fork happens
+    # before this process touches the GPU
+    pool_cpu = None
+    if not args.no_cpu_baseline:
+        pool_cpu = _pool_baseline(pairs, min(N, 16 * args.cpu_sample))
+        log("cpu baseline (pool): %.0f pairs/s on %d processes over %d pairs" % pool_cpu)
+    torch.cuda.set_device(0)
     eng = G.Engine(device=0, timing=True)
     nb = eng.nbatch(pairs)
     st0 = nb.stats()
@@ -89,9 +118,11 @@ def run(args):
 
     cpu = None
     if not args.no_cpu_baseline:
-        cpu = dict(value=n_s / t_or, unit="pairs/s", cores=1, kind="port",
+        v, T, n_p = pool_cpu
+        cpu = dict(value=v, unit="pairs/s", cores=T, kind="port",
                    sample="first %d pairs of this population through oracle/negotiate_oracle.py (typed decode of "
-                          "both sides + classification, decode timed), %.1f s" % (n_s, t_or))
+                          "both sides + classification, decode timed) on %d forked processes, wall clock; "
+                          "1-core: %.0f pairs/s over the first %d pairs" % (n_p, T, n_s / t_or, n_s))
         log("cpu baseline:", json.dumps(cpu))
 
     line = {
