@@ -5,23 +5,31 @@ Workload (BASELINE.json configs[2], the metric's own configuration): 10M mixed
 object pairs (40% ConfigMap/Secret, 40% Deployment, 20% medium CRD) across
 100k logical clusters, 5% mutated, synthetic (seed 20211004+3).
 
-Scaling (--scaling, default weak): pairs are independent and shard by logical
-cluster with no data-path exchange, so per-GPU work is fixed -- at N GPUs the
-node-wide population is N x the config (N x 10M pairs over N x 100k logical
-clusters, same seed and mix) and each rank holds the LPT shard of whole
-logical clusters assigned to it (~10M pairs, one config3-sized population per
-GPU).  --scaling strong keeps the population fixed at the config's size and
-splits it N ways instead.  Either way the pairs are encoded on the host with
-the product encoder and are resident in HBM before timing.
+Scaling (--scaling; default weak at N = 1, strong at N > 1): the metric is
+quoted on 10M objects / 100k clusters, so at N > 1 that population is split N
+ways by whole logical cluster (LPT; the reference runs one syncer per cluster,
+pkg/reconciler/cluster/cluster.go:125-138) -- strong scaling.  --scaling weak
+keeps per-GPU work fixed instead (the node holds N x the config).  Either way
+the pairs are encoded on the host with the product encoder and are resident
+in HBM before timing.
 
-A step = one diff pass of the hot path (K2 compare, K3 compaction, K4
-changed-path merge-join, K5/K6 path emit) over the rank's resident pairs, plus
-(N > 1) the RCCL all-gather of per-rank dirty counts and dirty pair IDs.
+A step = one diff pass of the hot path (K2 compare + fused merge-join, K3
+compaction, K4 deferred joins, K5/K6 path emit) over the rank's resident
+pairs, plus (N > 1) the RCCL all-gather of per-rank dirty counts and dirty
+pair IDs (shard.DirtyGather: preallocated, no host sync in the step).
+
+Beside the timed line (rank 0, N = 1): the roofline on both byte definitions
+(this build's format bytes, and SURVEY.md §8(d)'s B_pair = sum(24 L + V + 8) +
+O), end-to-end JSON-in rates (host-encoded and device-encoded, K0), the CPU
+baselines on all host cores (the C++ tree-walk restatement of the predicates
+and the CPU merge over the CSR encoding) and a three-way parity check of
+decisions and changed paths (GPU, tree-walk, CSR merge) on the CPU sample.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU).  Rank 0 prints one JSON line.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -33,10 +41,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
+# the sources K2's code and launch come from: a PMC summary is attached as roofline.traffic only when it
+# was measured on these same bytes
+K2_SOURCES = ["kcp_amd/csrc/kernels.hip", "kcp_amd/csrc/kernels.h", "kcp_amd/csrc/engine.h", "kcp_amd/csrc/api.cpp",
+              "include/gpudiff_format.h"]
 
 
 def log(*a):
     print("[bench r%s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
+
+
+def k2_source_hash():
+    h = hashlib.sha256()
+    for f in K2_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def host_cores():
+    """(threads for the CPU baseline = every CPU this process may run on, nproc, cgroup CPU quota or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return aff, os.cpu_count(), quota
 
 
 def main():
@@ -59,19 +93,21 @@ def main():
                     help="config5: encode events on the GPU (K0, raw JSON up) or on the host")
     ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")
     ap.add_argument("--clusters", type=int, default=0)
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: per-GPU work fixed (node population = N x the config); "
-                         "strong: the config's population split N ways")
+    ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
+                    help="strong: the config's population split N ways (the metric's 10M/100k node-wide; "
+                         "default for N > 1); weak: per-GPU work fixed (node population = N x the config)")
     ap.add_argument("--chunk", type=int, default=262144)
     ap.add_argument("--threads", type=int, default=0, help="host encode threads (default min(16, cpus))")
     ap.add_argument("--sample", type=int, default=600, help="pairs checked bit-exact vs the oracle (JSON path)")
     ap.add_argument("--cpu-sample", type=int, default=20000, help="pairs in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--json-in-pairs", type=int, default=131072,
+                    help="pairs of the end-to-end JSON-in measurement (0 = skip)")
     ap.add_argument("--traffic-json", default="latest",
                     help="PMC traffic summary to attach as roofline.traffic (default: the newest committed "
-                         "profiles/r*_pmc_summary.json, used only if it was measured on this same workload; "
-                         "'none' to skip)")
+                         "profiles/**/pmc_summary.json, used only if it was measured on this workload with the "
+                         "same K2 sources; 'none' to skip)")
     args = ap.parse_args()
 
     if args.config == "upsert":
@@ -98,11 +134,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    scaling = args.scaling if args.scaling != "auto" else ("strong" if world > 1 else "weak")
 
     import torch
     import torch.distributed as dist
 
     from kcp_amd import gpudiff as G
+    from kcp_amd import shard
     from kcp_amd import synth as S
 
     torch.cuda.set_device(local_rank)
@@ -110,17 +148,17 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     stream = torch.cuda.current_stream(dev)
-    ncpu = len(os.sched_getaffinity(0))
-    threads = args.threads or max(1, min(16, ncpu))
+    aff, nproc, quota = host_cores()
+    threads = args.threads or max(1, min(16, aff))
 
     eng = G.Engine(device=local_rank, encode_threads=threads, stream=stream.cuda_stream, timing=True)
     base = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=args.clusters)
-    mult = world if args.scaling == "weak" else 1
+    mult = world if scaling == "weak" else 1
     cfg = S.make_cfg(args.config, n_pairs=base.n_pairs * mult, n_clusters=base.n_clusters * mult)
     pop = S.Population(cfg, world, rank)
     n = pop.n
-    log("config %s: %d pairs / %d clusters total; this rank %d pairs / %d clusters; %d host threads" % (
-        args.config, cfg.n_pairs, cfg.n_clusters, n, pop.n_clusters, threads))
+    log("config %s (%s scaling): %d pairs / %d clusters node-wide; this rank %d pairs / %d clusters; %d host threads"
+        % (args.config, scaling, cfg.n_pairs, cfg.n_clusters, n, pop.n_clusters, threads))
 
     # ---------------- ingest: synthesize + encode on the host, stage, H2D, K1
     t_gen = time.time()
@@ -134,7 +172,6 @@ def main():
     truth[:first.truth.size] = first.truth
     db.append(first.hb)
     pos = first.truth.size
-    leaves = first.leaves
     k = 1
     last_log = time.time()
     while pos < n:
@@ -144,7 +181,6 @@ def main():
         db.append(ch.hb)
         truth[pos:pos + m] = ch.truth
         pos += m
-        leaves += ch.leaves
         k += 1
         if time.time() - last_log > 20:
             log("ingest %d/%d pairs (%.0f s)" % (pos, n, time.time() - t_gen))
@@ -166,32 +202,38 @@ def main():
     every_dirty_has_path = bool((np.diff(offs) >= 1).all()) if res.dirty_ids.size else True
     ids_ok = (res.spec_dirty_ids.size == int((got & G.SPEC_DIRTY).astype(bool).sum()) and
               res.status_dirty_ids.size == int((got & G.STATUS_DIRTY).astype(bool).sum()))
+    n_spec, n_status, n_paths = int(res.spec_dirty_ids.size), int(res.status_dirty_ids.size), int(res.path_hashes.size)
     full_check = dict(pairs=n, flag_mismatches=n_bad, every_dirty_pair_has_paths=every_dirty_has_path,
-                      id_lists_consistent=ids_ok, spec_dirty=int(res.spec_dirty_ids.size),
-                      status_dirty=int(res.status_dirty_ids.size), paths=int(res.path_hashes.size))
+                      id_lists_consistent=ids_ok, spec_dirty=n_spec, status_dirty=n_status, paths=n_paths)
     log("full-size check:", json.dumps(full_check))
     if n_bad or not every_dirty_has_path or not ids_ok:
         log("FULL-SIZE CHECK FAILED")
     pop_flags = res.pair_flags.copy()
     del res
 
-    sample_check = None
-
     for _ in range(max(0, args.warmup - 1)):
         eng.diff(db)
     eng.sync()
 
-    # ---------------- timed region
-    from kcp_amd import shard
-
-    def fill_from_hbm(col, buf, n):
-        db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(), n)
-
-    def gather_step():
-        counts = torch.empty(8, dtype=torch.int32, device=dev)
+    # ---------------- the collective (N > 1): capacities agreed once, untimed
+    gather = None
+    if world > 1:
+        counts = torch.zeros(8, dtype=torch.int32, device=dev)
         db.export(G.EXPORT_COUNTS, counts.data_ptr(), 8)
-        return shard.gather_dirty(counts, fill_from_hbm, rank, world, dist, dev, trim=False)
+        torch.cuda.synchronize()
+        cap_s, cap_t = shard.DirtyGather.agree_capacity(counts, world, dist)
+        gather = shard.DirtyGather(world, cap_s, cap_t, dev, dist)
 
+        def fill_counts(t):
+            db.export(G.EXPORT_COUNTS, t.data_ptr(), 8)
+
+        def fill_ids(col, buf):
+            db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
+                      buf.numel())
+        gather.step(fill_counts, fill_ids)  # warm the communicator
+        torch.cuda.synchronize()
+
+    # ---------------- timed region
     eng.timing_reset()
     if world > 1:
         dist.barrier()
@@ -199,14 +241,20 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.diff(db)
-        if world > 1:
-            gather_step()
+        if gather is not None:
+            gather.step(fill_counts, fill_ids)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     tm = eng.timings()
+    gather_check = None
     if world > 1:
+        ok, cc = gather.check()
+        sa, ta = gather.result() if ok else (None, None)
+        gather_check = dict(capacity_ok=ok, node_spec_dirty=int(cc[:, 0].sum()), node_status_dirty=int(cc[:, 1].sum()),
+                            gathered_spec=None if sa is None else int(sa.numel()),
+                            gathered_status=None if ta is None else int(ta.numel()))
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -218,29 +266,48 @@ def main():
 
     value = total_pairs * args.steps / dt
     # K2 runs as k2_launches back-to-back launches per pass (pipelined batch
-    # segments); per launch: bytes = compare_bytes / launches, time = span / launches
+    # segments); per launch: bytes = bytes / launches, time = span / launches
     launches = max(1, tm.k2_launches)
     k2_ms = tm.compare_ms / launches
-    bytes_per_launch = st.compare_bytes / launches
-    achieved = bytes_per_launch / (k2_ms * 1e-3) / 1e9 if k2_ms > 0 else 0.0
+    pass_ms = tm.total_ms
+    # B_pair = sum over A, B of (24 L + V + 8) + O, O = 4 B per dirty ID (x2 decisions) + 8 B per path
+    survey_bytes = 24 * st.total_leaves + st.value_bytes + 16 * n + 4 * (n_spec + n_status) + 8 * n_paths
+    fmt_bytes = st.compare_bytes
+    achieved = survey_bytes / launches / (k2_ms * 1e-3) / 1e9 if k2_ms > 0 else 0.0
+    achieved_fmt = fmt_bytes / launches / (k2_ms * 1e-3) / 1e9 if k2_ms > 0 else 0.0
+    achieved_pass = survey_bytes / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     traffic, traffic_src = None, None
+    src_hash = k2_source_hash()
     tj = args.traffic_json
     if tj == "latest":
         import glob
-        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
-        tj = found[-1] if found else ""
+        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_summary.json"), recursive=True),
+                       key=os.path.getmtime)
+        cand = []
+        for f in found:
+            try:
+                with open(f) as fh:
+                    pm = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if pm.get("k2_source_hash") == src_hash:
+                cand.append(f)
+        tj = cand[-1] if cand else ""
     if tj and tj != "none" and os.path.exists(tj):
         with open(tj) as f:
             pmc = json.load(f)
-        # per-launch bytes are only comparable on the same workload and launch split
-        if pmc.get("algorithmic_bytes_per_launch") == bytes_per_launch:
+        # comparable only on the same K2 sources and the same workload (format bytes per launch)
+        if pmc.get("k2_source_hash") == src_hash and pmc.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
 
-    # ---------------- CPU baseline leg (rank 0, N=1 only): the oracle's C++ port
-    # timed on the host, and -- the oracle as checker -- a bit-exact sample
-    # through the JSON -> encoder -> GPU path vs the Python oracle
-    cpu = None
+    db.free()  # the JSON-in and CPU legs below need no resident population
+
+    # ---------------- rank 0, N = 1: end-to-end JSON-in, CPU baselines, three-way parity
+    json_in = cpu = sample_check = three_way = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if args.json_in_pairs:
+            json_in = json_in_rates(G, pop, min(args.json_in_pairs, n), threads, local_rank)
+            log("json-in:", json.dumps(json_in))
         if args.sample:
             from tests.parity import assert_matches, oracle_batch
             idx = np.unique(np.linspace(0, n - 1, min(args.sample, n)).astype(np.int64))
@@ -256,19 +323,9 @@ def main():
             same = bool((r.pair_flags == pop_flags[idx]).all())
             sample_check = dict(pairs=int(idx.size), bit_exact_vs_oracle=ok, matches_population_flags=same)
             log("sample check:", json.dumps(sample_check))
-        from oracle import cpu_ref
-        idx = np.unique(np.linspace(0, n - 1, min(args.cpu_sample, n)).astype(np.int64))
-        pairs = [pop.json_pair(int(i)) for i in idx]
-        dp = cpu_ref.DecodedPairs(pairs)
-        cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
-        agree = bool((cflags & 3 == pop_flags[idx] & 3).all())
-        _, sweeps1, sec1 = dp.decide(threads=1, min_seconds=args.cpu_seconds / 2)
-        dp.close()
-        cpu = dict(value=len(idx) * sweeps / sec, unit="pairs/s", cores=threads, kind="port",
-                   sample="%d pairs (every %dth of this workload, JSON decoded untimed), %d sweeps in %.1f s; "
-                          "decisions agree with GPU: %s; 1-core: %.0f pairs/s" % (
-                              len(idx), max(1, n // len(idx)), sweeps, sec, agree, len(idx) * sweeps1 / sec1))
+        cpu, three_way = cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota)
         log("cpu baseline:", json.dumps(cpu))
+        log("three-way parity:", json.dumps(three_way))
 
     if rank == 0:
         line = {
@@ -280,7 +337,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": args.scaling,
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded object populations, SURVEY.md 8d; no real cluster data)",
@@ -288,7 +345,8 @@ def main():
                 "workload": "%s: %d pairs / %d logical clusters node-wide%s, %.0f%% mutated (%s)" % (
                     args.config, cfg.n_pairs, cfg.n_clusters,
                     " (%d x %d pairs / %d clusters, one per GPU)" % (world, base.n_pairs, base.n_clusters)
-                    if mult > 1 else "", cfg.mutate_frac * 100,
+                    if mult > 1 else (" split %d ways by logical cluster" % world if world > 1 else ""),
+                    cfg.mutate_frac * 100,
                     "40% ConfigMap/Secret, 40% Deployment, 20% CRD" if args.config == "config3" else args.config),
                 "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9,
                 "parallelism": "shard-by-logical-cluster x%d (LPT)%s" % (
@@ -296,18 +354,102 @@ def main():
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_compare (K2)", "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": k2_ms, "launches_per_step": launches},
+                         "kernel": "k_compare (K2)", "avg_launch_ms": k2_ms, "launches_per_step": launches,
+                         "bytes_def": "SURVEY.md 8(d) / BASELINE.md:52: sum over A,B of (24 L + V + 8) + O",
+                         "bytes_per_launch": survey_bytes / launches,
+                         "format": {"bytes_per_launch": fmt_bytes / launches, "achieved": achieved_fmt,
+                                    "frac": achieved_fmt / HBM_PEAK_GBPS,
+                                    "def": "bytes K2 reads in this build's CSR format: 64-B row + flag + both "
+                                           "size-matched segments (20 B/leaf + 16-B padded arena)"},
+                         "diff_pass": {"ms": pass_ms, "achieved": achieved_pass, "frac": achieved_pass / HBM_PEAK_GBPS,
+                                       "def": "SURVEY bytes over the whole diff pass (K2..K6)"},
+                         "k2_source_hash": src_hash},
             "kernels_ms": {"compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,
                            "join_exposed": tm.join_ms, "emit": tm.emit_ms, "diff_pass": tm.total_ms,
                            "passes": tm.n_passes, "value_hash_last_chunk": k1_ms},
             "cpu_baseline": cpu,
-            "checks": {"full_size": full_check, "sample": sample_check},
+            "json_in": json_in,
+            "checks": {"full_size": full_check, "sample": sample_check, "three_way": three_way,
+                       "gather": gather_check},
             "ingest_s": t_gen,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def json_in_rates(G, pop, m, threads, device):
+    """End-to-end JSON-in pairs/s on the first m pairs of this workload: JSON in
+    host memory -> gpudiff_submit -> gpudiff_wait (results on the host),
+    once with host encoding (16 encode threads, pinned H2D, K1, diff pass) and
+    once with device encoding (pinned staging, H2D, K0, diff pass).  Includes
+    PCIe; the timed headline (`value`) does not."""
+    buf, offs, _truth = pop.json_range(0, m, threads)
+    arr = G.json_pair_array(buf, offs)
+    out = dict(sample_pairs=m, json_bytes=int(offs[-1]), threads=threads)
+    flags = {}
+    for mode in ("host_encode", "device_encode"):
+        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode == "device_encode"))
+        r = e.wait(e.submit_array(arr))  # warm: staging and scratch allocations
+        times = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = e.wait(e.submit_array(arr))
+            times.append(time.perf_counter() - t0)
+        flags[mode] = r.pair_flags
+        best = min(times)
+        out[mode] = dict(pairs_per_s=m / best, ms=best * 1e3, json_gb_per_s=int(offs[-1]) / best / 1e9)
+        e.close()
+    out["modes_agree"] = bool(np.array_equal(flags["host_encode"], flags["device_encode"]))
+    return out
+
+
+def cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota):
+    """CPU baselines on every core this process may use: the C++ tree-walk
+    restatement of the predicates over decoded trees (cpu-ref, primary) and the
+    CPU merge over the canonical CSR encoding (cpu-csr), each also on one core;
+    then the three-way parity of flags and changed paths on the same sample
+    (GPU vs tree-walk vs CSR merge)."""
+    from oracle import cpu_ref
+    idx = np.unique(np.linspace(0, n - 1, min(args.cpu_sample, n)).astype(np.int64))
+    pairs = [pop.json_pair(int(i)) for i in idx]
+    threads = aff
+    dp = cpu_ref.DecodedPairs(pairs)
+    cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
+    _, sweeps1, sec1 = dp.decide(threads=1, min_seconds=args.cpu_seconds / 3)
+    hb = eng.encode(pairs)
+    rows = hb.rows()
+    csr = cpu_ref.CsrPairs(hb.pool(), rows)
+    fcsr, csw, csec, _ = csr.run(threads=threads, min_seconds=args.cpu_seconds / 2)
+    _, csw1, csec1, _ = csr.run(threads=1, min_seconds=args.cpu_seconds / 4)
+    ref_rate, csr_rate = len(idx) * sweeps / sec, len(idx) * csw / csec
+    cpu = dict(value=ref_rate, unit="pairs/s", cores=threads, kind="port",
+               sample="%d pairs (every %dth of this workload, JSON decoded untimed), %d sweeps in %.1f s; "
+                      "C++ tree-walk restatement of specsyncer.go:17-41 + statussyncer.go:15-27" % (
+                          len(idx), max(1, n // len(idx)), sweeps, sec),
+               one_core=len(idx) * sweeps1 / sec1, nproc=nproc, affinity_cpus=aff, cgroup_cpu_quota=quota,
+               cpu_csr=dict(value=csr_rate, unit="pairs/s", cores=threads, one_core=len(idx) * csw1 / csec1,
+                            what="the build's CPU merge over the canonical CSR encoding (oracle/csr_ref.cpp), "
+                                 "decisions + changed paths"))
+    # three-way parity on the sample: GPU vs tree-walk vs CSR merge (flags and paths)
+    r = eng.diff_pairs(pairs)
+    seeds = (rows["flags_a"] >> G.OBJ_SEED_SHIFT) & 0xFF
+    t_offs, t_h, t_k = dp.paths(seeds)
+    c_flags, c_offs, c_h, c_k = csr.paths()
+    gflags = r.pair_flags & 7
+    three = dict(pairs=len(idx),
+                 flags_gpu_eq_tree=bool(np.array_equal(gflags, cflags)),
+                 flags_gpu_eq_csr=bool(np.array_equal(gflags, c_flags)),
+                 flags_gpu_eq_population=bool(np.array_equal(r.pair_flags, pop_flags[idx])),
+                 paths_gpu_eq_tree=bool(np.array_equal(r.path_offsets, t_offs) and np.array_equal(r.path_hashes, t_h)
+                                        and np.array_equal(r.path_kinds, t_k)),
+                 paths_gpu_eq_csr=bool(np.array_equal(r.path_offsets, c_offs) and np.array_equal(r.path_hashes, c_h)
+                                       and np.array_equal(r.path_kinds, c_k)),
+                 csr_timed_flags_eq=bool(np.array_equal(fcsr, c_flags)),
+                 dirty=int(r.dirty_ids.size), paths=int(r.path_hashes.size))
+    dp.close()
+    hb.free()
+    return cpu, three
 
 
 if __name__ == "__main__":

@@ -11,10 +11,13 @@ event mix of kcp_amd.synth.negotiate_population.  The documents are uploaded
 once (gpudiff_nbatch_create); a step is one K13 + K14 pass over all of them,
 resident in HBM.
 
-Reported: pairs/s (value), K13's HBM GB/s (JSON read + 944 B per document
-written) against the roofline, K14 time, checks (every action vs the
-generator's designed outcome, a sample vs the Python oracle), CPU baseline: the
-Python oracle (one core) on a bounded sample.
+Reported: pairs/s (value: a step = K13 + K14 + the actions' copy-back + the
+host path for K13's deferrals, i.e. every pair classified inside the timed
+step), the device-only rate beside it, K13's HBM GB/s (JSON read + 944 B per
+document written) against the roofline, K14 time, checks (every action vs the
+generator's designed outcome, a sample vs the Python oracle), and the CPU
+baseline: the product's Go-exact C++ host path (gpudiff_classify_updates_host,
+typed decode of both sides + classification, decode timed) on every host CPU.
 
 usage: python bench.py --config negotiate [--pairs N] [--steps K]
 """
@@ -35,29 +38,6 @@ def log(*a):
     print("[negotiate]", *a, file=sys.stderr, flush=True)
 
 
-_POOL_PAIRS = None
-
-
-def _pool_work(k_T):
-    from oracle import negotiate_oracle as NO
-    k, T, n = k_T
-    return [NO.classify(a, b) for a, b in _POOL_PAIRS[k:n:T]]
-
-
-def _pool_baseline(pairs, n):
-    """The oracle on every host thread (min(16, affinity) forked processes), wall-clock over n pairs."""
-    import multiprocessing as mp
-    global _POOL_PAIRS
-    _POOL_PAIRS = pairs
-    T = max(1, min(16, len(os.sched_getaffinity(0))))
-    with mp.get_context("fork").Pool(T) as pool:
-        pool.map(_pool_work, [(k, T, k + 1) for k in range(T)])  # workers up, oracle imported
-        t = time.perf_counter()
-        pool.map(_pool_work, [(k, T, n) for k in range(T)])
-        dt = time.perf_counter() - t
-    return n / dt, T, n
-
-
 def run(args):
     import torch
 
@@ -69,12 +49,6 @@ def run(args):
     N = len(pairs)
     json_bytes = sum(len(a) + len(b) for a, b in pairs)
     log("%d Update pairs, %.2f GB of JSON, generated in %.1f s" % (N, json_bytes / 1e9, time.time() - t0))
-    # CPU baseline on all host threads first: forked workers share the population, and the fork happens
-    # before this process touches the GPU
-    pool_cpu = None
-    if not args.no_cpu_baseline:
-        pool_cpu = _pool_baseline(pairs, min(N, 16 * args.cpu_sample))
-        log("cpu baseline (pool): %.0f pairs/s on %d processes over %d pairs" % pool_cpu)
     torch.cuda.set_device(0)
     eng = G.Engine(device=0, timing=True)
     nb = eng.nbatch(pairs)
@@ -98,15 +72,22 @@ def run(args):
 
     for _ in range(max(0, args.warmup - 1)):
         nb.run()
-    eng.sync()
-    nb.fetch()
+        nb.fetch()
     s_before = nb.stats()
     torch.cuda.synchronize()
+    # end to end: every step classifies every pair (K13 + K14, actions to the host, host path for deferrals)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         nb.run()
-    eng.sync()
+        acts = nb.fetch()
     dt = time.perf_counter() - t0
+    steps_ok = bool(np.array_equal(acts, got))
+    # device only: K13 + K14 back to back (deferred pairs left to a later fetch)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        nb.run()
+    eng.sync()
+    dt_dev = time.perf_counter() - t1
     nb.fetch()
     s_after = nb.stats()
     runs = s_after.runs - s_before.runs
@@ -118,11 +99,31 @@ def run(args):
 
     cpu = None
     if not args.no_cpu_baseline:
-        v, T, n_p = pool_cpu
-        cpu = dict(value=v, unit="pairs/s", cores=T, kind="port",
-                   sample="first %d pairs of this population through oracle/negotiate_oracle.py (typed decode of "
-                          "both sides + classification, decode timed) on %d forked processes, wall clock; "
-                          "1-core: %.0f pairs/s over the first %d pairs" % (n_p, T, n_s / t_or, n_s))
+        T = len(os.sched_getaffinity(0))
+        n_c = min(N, 20 * args.cpu_sample)
+        hp = G.HostPairs(pairs[:n_c])
+        hp.classify(threads=T)  # warm
+        reps, t_c = 0, time.perf_counter()
+        while True:
+            ha = hp.classify(threads=T)
+            reps += 1
+            el = time.perf_counter() - t_c
+            if el >= args.cpu_seconds:
+                break
+        reps1, t_c = 0, time.perf_counter()
+        while True:
+            hp.classify(threads=1)
+            reps1 += 1
+            el1 = time.perf_counter() - t_c
+            if el1 >= args.cpu_seconds / 3:
+                break
+        cpu = dict(value=n_c * reps / el, unit="pairs/s", cores=T, kind="port",
+                   sample="first %d pairs of this population through the product's Go-exact host path "
+                          "(gpudiff_classify_updates_host: typed decode of both sides + classification, decode "
+                          "timed), %d sweeps in %.1f s; agrees with the device: %s" % (
+                              n_c, reps, el, bool(np.array_equal(ha, got[:n_c]))),
+                   one_core=n_c * reps1 / el1, nproc=os.cpu_count(),
+                   python_oracle_one_core=n_s / t_or)
         log("cpu baseline:", json.dumps(cpu))
 
     line = {
@@ -135,10 +136,16 @@ def run(args):
                                % (N, json_bytes / 1e9)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_encode_docs<negotiate> (K13)",
-                     "bytes_per_launch": alg, "avg_launch_ms": k13_ms, "launches_per_step": 1},
+                     "bytes_per_launch": alg, "avg_launch_ms": k13_ms, "launches_per_step": 1,
+                     "limiter": "issue (a wave's scalar scan/tree state machine per document, DESIGN.md 6e); "
+                                "the HBM fraction is informational"},
         "kernels_ms": {"k13": k13_ms, "k14_classify": k14_ms},
+        "device_only": {"pairs_per_s": N * args.steps / dt_dev, "ms_per_step": dt_dev / args.steps * 1e3,
+                        "what": "K13 + K14 only; the deferred pairs' host path is outside this rate"},
+        "n_host": int(s_after.n_host),
         "cpu_baseline": cpu,
-        "checks": {"full_size": full, "sample": dict(pairs=n_s, bit_exact_vs_oracle=sample_ok)},
+        "checks": {"full_size": full, "sample": dict(pairs=n_s, bit_exact_vs_oracle=sample_ok),
+                   "timed_steps_equal_first_run": steps_ok},
     }
     nb.close()
     eng.close()

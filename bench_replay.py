@@ -183,10 +183,10 @@ def run(args):
             b = bytes(buf[offs[2 * s_ + 1]:offs[2 * s_ + 2]])
             pairs.append((a, b) if new_is_b[i] else (b, a))
         dp = cpu_ref.DecodedPairs(pairs)
-        cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
+        cflags, sweeps, sec = dp.decide(threads=ncpu, min_seconds=args.cpu_seconds)
         dp.close()
         agree = bool(((cflags & 3) == (first_res[0].pair_flags[:m] & 3)).all()) if first_res else None
-        cpu = dict(value=m * sweeps / sec, unit="events/s", cores=threads, kind="port",
+        cpu = dict(value=m * sweeps / sec, unit="events/s", cores=ncpu, kind="port",
                    sample="%d events of the first timed batch, old+new JSON decoded untimed (the informer "
                           "decodes them), predicates only, %d sweeps in %.1f s; decisions agree with GPU: %s" % (
                               m, sweeps, sec, agree))

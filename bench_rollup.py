@@ -104,10 +104,10 @@ def run(args):
         n_s = min(args.cpu_sample, N)
         sdocs = docs[:n_s]
         rd = cpu_ref.RollupDocs(sdocs)
-        sw_, sec, _ = rd.run(threads=threads, min_seconds=args.cpu_seconds)
+        sw_, sec, _ = rd.run(threads=ncpu, min_seconds=args.cpu_seconds)
         sw1, sec1, _ = rd.run(threads=1, min_seconds=args.cpu_seconds / 2)
         rd.close()
-        cpu = dict(value=n_s * sw_ / sec, unit="docs/s", cores=threads, kind="port",
+        cpu = dict(value=n_s * sw_ / sec, unit="docs/s", cores=ncpu, kind="port",
                    sample="first %d documents of this population (decode + group-by + int32 sums, decode timed), "
                           "%d sweeps in %.1f s; 1-core: %.0f docs/s; full population on %d threads: %.2f s" % (
                               n_s, sw_, sec, n_s * sw1 / sec1, threads, t_ref))

@@ -128,10 +128,10 @@ def run(args):
         sidx = np.unique(np.linspace(0, N - 1, min(args.cpu_sample, N)).astype(np.int64)).tolist()
         dd = cpu_ref.DecodedDocs([docs[i] for i in sidx])
         agree = all(dd.body(j) == res.bodies[i] for j, i in enumerate(sidx[:2000]))
-        sw, sec, _ = dd.run(0, threads, args.cpu_seconds)
+        sw, sec, _ = dd.run(0, ncpu, args.cpu_seconds)
         sw1, sec1, _ = dd.run(0, 1, args.cpu_seconds / 2)
         dd.close()
-        cpu = dict(value=len(sidx) * sw / sec, unit="bodies/s", cores=threads, kind="port",
+        cpu = dict(value=len(sidx) * sw / sec, unit="bodies/s", cores=ncpu, kind="port",
                    sample="%d documents (every %dth, decoded untimed; DeepCopy + transform + json.Marshal), "
                           "%d sweeps in %.1f s; bodies agree with GPU: %s; 1-core: %.0f bodies/s" % (
                               len(sidx), max(1, N // len(sidx)), sw, sec, agree, len(sidx) * sw1 / sec1))

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GPUDIFF_ABI_VERSION 1
+#define GPUDIFF_ABI_VERSION 2
 
 enum {
     GPUDIFF_OK = 0,
@@ -73,6 +73,9 @@ enum {
 #define GPUDIFF_TOK_WIDE 10   /* K10: an object with more than 2048 members (quadratic key ranking) */
 #define GPUDIFF_TOK_FIELD 11  /* K11 (roll-up): a field the typed decode must judge on the host (duplicate,
                                  case-folded key, type mismatch, counter not an int32 literal, escaped label) */
+#define GPUDIFF_TOK_LIST 12   /* K0: a top-level key the informer decoder's list probe matches ("items" under
+                                 Go's case folding): the host decides (the object is an UnstructuredList, the
+                                 pair is dirty -- specsyncer.go:18-22) */
 
 /* changed-path kinds (low 2 bits); bit 7 = status region */
 #define GPUDIFF_PATH_CHANGED 0u        /* present in both, value differs */
@@ -163,7 +166,9 @@ typedef struct gpudiff_batch_stats {
     uint64_t n_pairs;
     uint64_t pool_bytes;       /* bytes of object blobs resident */
     uint64_t total_leaves;
-    uint64_t compare_bytes;    /* algorithmic bytes of one diff pass */
+    uint64_t compare_bytes;    /* format bytes one diff pass reads */
+    uint64_t value_bytes;      /* canonical bytes of the long (non-inline) string values of every object:
+                                  V of SURVEY.md §8(d)'s B_pair = sum over A, B of (24 L + V + 8) + O */
 } gpudiff_batch_stats;
 
 typedef struct gpudiff_timings {
@@ -463,7 +468,12 @@ int gpudiff_rollup_doc_host(const uint8_t* doc, size_t len, int32_t* v, uint8_t*
  * status not Semantic.DeepEqual (nil == empty, metav1.Time by instant) ->
  * STATUS; annotations differ OR labels EQUAL (the reference's missing `!` at
  * :278, reproduced) -> META; else IGNORE.  Objects are decoded with Go 1.16
- * encoding/json typed rules; a pair with a side Go cannot decode -> DECODE.
+ * encoding/json typed rules; DECODE when a side is not valid JSON, is not an
+ * object, or a field the classifier reads (metadata.resourceVersion /
+ * generation / labels / annotations, status.conditions and their elements)
+ * fails Go's typed decode.  Type errors in fields the classifier does not read
+ * (spec, metadata.name, ...) are not checked: such an object cannot reach the
+ * reference's informer at all, so no reference outcome exists for it.
  * Kernel K13 (negotiation mode of k_encode_docs) extracts each document's
  * fields, K14 classifies each pair on the device; pairs with a document outside
  * K13's subset are classified by the host path (gpudiff_negotiate_pair_host). */
@@ -482,7 +492,8 @@ typedef struct gpudiff_nbatch_stats {
 } gpudiff_nbatch_stats;
 /* olds[i] == NULL: no old object.  The documents are uploaded once into HBM;
  * run = K13 + K14 on the context stream (asynchronous); fetch = actions[n] to
- * the host, host path for the deferred pairs.  The caller's buffers must stay
+ * the host, host path for the deferred pairs (GPUDIFF_E_STATE before the first
+ * run).  The caller's buffers must stay
  * valid until gpudiff_nbatch_free. */
 int gpudiff_nbatch_create(gpudiff_ctx* ctx, const uint8_t* const* olds, const size_t* old_lens,
                           const uint8_t* const* news, const size_t* new_lens, size_t n, gpudiff_nbatch** out);
@@ -490,6 +501,11 @@ int gpudiff_nbatch_run(gpudiff_ctx* ctx, gpudiff_nbatch* nb);
 int gpudiff_nbatch_fetch(gpudiff_ctx* ctx, gpudiff_nbatch* nb, int32_t* actions);
 int gpudiff_nbatch_stats_get(const gpudiff_nbatch* nb, gpudiff_nbatch_stats* st);
 void gpudiff_nbatch_free(gpudiff_ctx* ctx, gpudiff_nbatch* nb);
+/* The host path (Go-exact typed decode + classification) over n pairs on
+ * `threads` host threads -- no device needed; what the batch falls back to for
+ * K13's deferrals, exposed for CPU baselines and callers without a GPU. */
+int gpudiff_classify_updates_host(const uint8_t* const* olds, const size_t* old_lens, const uint8_t* const* news,
+                                  const size_t* new_lens, size_t n, uint32_t threads, int32_t* actions);
 /* create + run + fetch + free */
 int gpudiff_classify_updates(gpudiff_ctx* ctx, const uint8_t* const* olds, const size_t* old_lens,
                              const uint8_t* const* news, const size_t* new_lens, size_t n, int32_t* actions);

@@ -489,7 +489,7 @@ const (
 	NegStatus  = int32(C.GPUDIFF_NEG_STATUS)  // StatusOnlyChanged
 	NegMeta    = int32(C.GPUDIFF_NEG_META)    // AnnotationOrLabelsOnlyChanged
 	NegCreated = int32(C.GPUDIFF_NEG_CREATED) // Created (no old object)
-	NegDecode  = int32(C.GPUDIFF_NEG_DECODE)  // a side Go cannot decode
+	NegDecode  = int32(C.GPUDIFF_NEG_DECODE)  // a side not valid JSON / not an object, or a field read that fails Go's typed decode
 )
 
 // ClassifyUpdates is the batch form of the "Update" branch of

@@ -694,7 +694,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     d->pool_used = s->used_ub;
     d->n_pairs = n;
     d->leaves = 0;
-    d->compare_bytes = 0;
+    d->compare_bytes = d->value_bytes = 0;
     if ((rc = gpudiff_diff(c, d, ticket))) {
         s->broken = true;
         return rc;

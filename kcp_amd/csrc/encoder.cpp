@@ -308,8 +308,8 @@ void PairEncoder::encode_json(const uint8_t* a, size_t alen, const uint8_t* b, s
     arena_a.reset();
     arena_b.reset();
     Node na, nb;
-    bool oka = a && parser.parse_object(a, alen, arena_a, &na);
-    bool okb = oka && b && parser.parse_object(b, blen, arena_b, &nb);
+    bool oka = a && parser.parse_object(a, alen, arena_a, &na) && !decodes_as_list(na);
+    bool okb = oka && b && parser.parse_object(b, blen, arena_b, &nb) && !decodes_as_list(nb);
     encode_nodes(oka ? &na : nullptr, okb ? &nb : nullptr, pair_id, cluster_id, pool, row);
 }
 
@@ -318,7 +318,7 @@ void PairEncoder::encode_json(const uint8_t* a, size_t alen, const uint8_t* b, s
 bool PairEncoder::flatten_json(const uint8_t* json, size_t len, Arena& arena, FlatObject& o) {
     arena.reset();
     Node n;
-    if (!json || !parser.parse_object(json, len, arena, &n)) return false;
+    if (!json || !parser.parse_object(json, len, arena, &n) || decodes_as_list(n)) return false;
     flatten_object(n, o);
     return true;
 }

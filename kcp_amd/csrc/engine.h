@@ -59,7 +59,7 @@ struct gpudiff_hbatch {
 struct gpudiff_dbatch {
     uint64_t pool_cap = 0, pool_used = 0;
     uint64_t max_pairs = 0, n_pairs = 0;
-    uint64_t leaves = 0, compare_bytes = 0;
+    uint64_t leaves = 0, compare_bytes = 0, value_bytes = 0;
     uint8_t* pool = nullptr;
     bool pool_borrowed = false;  // pool owned by a gpudiff_store (its current space)
     gpudiff_pair_row* rows = nullptr;
@@ -163,6 +163,18 @@ inline void dfree_all(gpudiff_dbatch* d) {
 
 // copies a finished diff pass's results to host memory (gpudiff_wait's body)
 int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rs);
+
+// canonical bytes of one object's long string values (V of SURVEY §8(d)); blob at pool + off
+inline uint64_t blob_value_bytes(const uint8_t* blob, uint32_t spec_l, uint32_t spec_ar, uint32_t stat_l) {
+    uint64_t v = 0;
+    const uint32_t* m = (const uint32_t*)(blob + 16ull * spec_l);
+    for (uint32_t i = 0; i < spec_l; i++)
+        if (gpudiff_meta_is_long(m[i])) v += gpudiff_meta_len(m[i]);
+    m = (const uint32_t*)(blob + gpudiff_seg_bytes(spec_l, spec_ar) + 16ull * stat_l);
+    for (uint32_t i = 0; i < stat_l; i++)
+        if (gpudiff_meta_is_long(m[i])) v += gpudiff_meta_len(m[i]);
+    return v;
+}
 
 // bytes the decision kernel must read for this pair (DESIGN.md "Roofline")
 inline uint64_t pair_compare_bytes(const gpudiff_pair_row& r) {

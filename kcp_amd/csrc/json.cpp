@@ -396,3 +396,43 @@ bool JsonParser::array(Node* out, int depth) {
 }
 
 }  // namespace gd
+
+namespace gd {
+
+// encoding/json fold.go equalFoldRight (Go 1.16) for an ASCII field name
+// against a decoded (valid UTF-8) key: ASCII case folding, plus U+017F (long
+// s) for s/S and U+212A (Kelvin sign) for k/K
+static bool go_equal_fold_right(const char* name, const char* k, size_t klen) {
+    size_t i = 0;
+    for (const char* s = name; *s; s++) {
+        const uint8_t sb = (uint8_t)*s;
+        if (i >= klen) return false;
+        const uint8_t tb = (uint8_t)k[i];
+        if (tb < 0x80) {
+            if (sb != tb) {
+                const uint8_t up = sb & 0xDF;
+                if (up < 'A' || up > 'Z' || up != (tb & 0xDF)) return false;
+            }
+            i++;
+            continue;
+        }
+        if ((sb == 's' || sb == 'S') && i + 1 < klen && tb == 0xC5 && (uint8_t)k[i + 1] == 0xBF) {
+            i += 2;
+        } else if ((sb == 'k' || sb == 'K') && i + 2 < klen && tb == 0xE2 && (uint8_t)k[i + 1] == 0x84 &&
+                   (uint8_t)k[i + 2] == 0xAA) {
+            i += 3;
+        } else {
+            return false;
+        }
+    }
+    return i == klen;
+}
+
+bool decodes_as_list(const Node& root) {
+    if (root.t != J_OBJ) return false;
+    for (uint32_t m = 0; m < root.n; m++)
+        if (go_equal_fold_right("Items", root.u.mem[m].k, root.u.mem[m].klen)) return true;
+    return false;
+}
+
+}  // namespace gd

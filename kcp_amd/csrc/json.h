@@ -85,4 +85,13 @@ class JsonParser {
     std::string tmp_;
 };
 
+// The list probe of apimachinery's unstructuredJSONScheme.decode [3P]: the
+// informer's decoder first unmarshals the bytes into struct{ Items
+// json.RawMessage }; a top-level key equal to "Items" under encoding/json's
+// case folding (any value, null included) makes the object an
+// UnstructuredList.  The predicates' type assertions then fail
+// (specsyncer.go:18-22, statussyncer.go:16-20): the pair is dirty, like a
+// decode error.
+bool decodes_as_list(const Node& root);
+
 }  // namespace gd

@@ -35,6 +35,7 @@ struct gpudiff_nbatch {
     std::vector<const uint8_t*> olds, news;
     std::vector<size_t> old_lens, new_lens;
     uint64_t json_bytes = 0, scratch_bytes = 0, n_host = 0;
+    bool ran = false;  // a run was issued (fetch before any run: GPUDIFF_E_STATE)
     void *d_json = nullptr, *d_scratch = nullptr, *d_docs = nullptr, *d_no = nullptr, *d_absent = nullptr,
          *d_act = nullptr;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -357,10 +358,29 @@ int gpudiff_negotiate_pair_host(const uint8_t* old_json, size_t old_len, const u
     return GPUDIFF_OK;
 }
 
+int gpudiff_classify_updates_host(const uint8_t* const* olds, const size_t* old_lens, const uint8_t* const* news,
+                                  const size_t* new_lens, size_t n, uint32_t threads, int32_t* actions) {
+    if (n && (!olds || !old_lens || !news || !new_lens || !actions)) return GPUDIFF_E_INVAL;
+    for (size_t i = 0; i < n; i++)
+        if (!news[i] && new_lens[i]) return GPUDIFF_E_INVAL;
+    const uint32_t T = (uint32_t)std::max<size_t>(1, std::min<size_t>(threads ? threads : 1, n ? n : 1));
+    auto work = [&](uint32_t t) {
+        for (size_t i = n * t / T, e = n * (t + 1) / T; i < e; i++)
+            actions[i] = classify_host(olds[i], olds[i] ? old_lens[i] : 0, news[i], new_lens[i]);
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    return GPUDIFF_OK;
+}
+
 int gpudiff_nbatch_create(gpudiff_ctx* c, const uint8_t* const* olds, const size_t* old_lens,
                           const uint8_t* const* news, const size_t* new_lens, size_t n, gpudiff_nbatch** out) {
     if (!c || !out || (n && (!olds || !old_lens || !news || !new_lens)) || n > 0x3FFFFFFFu) return GPUDIFF_E_INVAL;
     *out = nullptr;
+    for (size_t i = 0; i < n; i++)
+        if (!news[i] && new_lens[i]) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
     gpudiff_nbatch* nb = new (std::nothrow) gpudiff_nbatch();
@@ -445,11 +465,13 @@ int gpudiff_nbatch_run(gpudiff_ctx* c, gpudiff_nbatch* nb) {
         HIPCHK(hipEventRecord(nb->ev[2], c->stream));
         nb->pending_timing = true;
     }
+    nb->ran = true;
     return GPUDIFF_OK;
 }
 
 int gpudiff_nbatch_fetch(gpudiff_ctx* c, gpudiff_nbatch* nb, int32_t* actions) {
     if (!c || !nb || (nb->n && !actions)) return GPUDIFF_E_INVAL;
+    if (!nb->ran) return GPUDIFF_E_STATE;  // nothing classified yet: d_act holds no actions
     int rc = set_device(c);
     if (rc) return rc;
     const size_t n = nb->n;

@@ -461,6 +461,7 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
     d->n_pairs = n;
     d->leaves = leaves;
     d->compare_bytes = cb;
+    d->value_bytes = 0;
     if ((rc = gpudiff_diff(c, d, ticket))) {
         s->broken = true;
         return rc;

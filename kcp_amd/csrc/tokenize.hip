@@ -462,6 +462,16 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint32_t i = i0 + lane;
             if (i >= nn) break;
             const uint4 r = S.rec[i];
+            if (r.x == 0 && (r.y & KEYBIT)) {
+                // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key
+                // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
+                const uint32_t kt = r.y & ~KEYBIT;
+                const uint32_t op = S.tok[kt] & POS_MASK, cp = S.tok[kt + 1] & POS_MASK;
+                if (cp - op - 1 == 5u && (ld8u(d + op + 1) & 0xDFDFDFDFDFull) == 0x534D455449ull) {
+                    err = GPUDIFF_TOK_LIST;
+                    continue;
+                }
+            }
             if (!(r.w & NI_LEAF)) continue;
             uint32_t tag = r.w & NI_TAG, mlen = 0;
             uint64_t v = 0;

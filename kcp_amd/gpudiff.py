@@ -48,6 +48,29 @@ class JsonPair(C.Structure):
                 ("new_len", C.c_size_t), ("pair_id", C.c_uint32), ("cluster_id", C.c_uint32)]
 
 
+# numpy mirror of gpudiff_json_pair (zero-copy pair tables over one JSON buffer)
+JSON_PAIR_DTYPE = np.dtype([("old_json", "<u8"), ("old_len", "<u8"), ("new_json", "<u8"), ("new_len", "<u8"),
+                            ("pair_id", "<u4"), ("cluster_id", "<u4")])
+assert JSON_PAIR_DTYPE.itemsize == C.sizeof(JsonPair)
+
+
+def json_pair_array(buf: np.ndarray, offs: np.ndarray, ids=None, clusters=None) -> np.ndarray:
+    """Pair table over one contiguous JSON buffer: pair i's old object is
+    buf[offs[2i]:offs[2i+1]], its new one buf[offs[2i+1]:offs[2i+2]].  The
+    buffer must outlive every submit of the table."""
+    n = (len(offs) - 1) // 2
+    base = buf.ctypes.data
+    o = offs.astype(np.uint64)
+    arr = np.zeros(n, dtype=JSON_PAIR_DTYPE)
+    arr["old_json"] = base + o[0:2 * n:2]
+    arr["old_len"] = o[1:2 * n + 1:2] - o[0:2 * n:2]
+    arr["new_json"] = base + o[1:2 * n + 1:2]
+    arr["new_len"] = o[2:2 * n + 2:2] - o[1:2 * n + 1:2]
+    arr["pair_id"] = np.arange(n, dtype=np.uint32) if ids is None else ids
+    arr["cluster_id"] = 0 if clusters is None else clusters
+    return arr
+
+
 class PairRow(C.Structure):
     _fields_ = [("off_a", C.c_uint64), ("off_b", C.c_uint64),
                 ("spec_l_a", C.c_uint32), ("spec_l_b", C.c_uint32),
@@ -88,7 +111,7 @@ class ObjInfo(C.Structure):
 
 
 TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SIZE, TOK_SPACE, TOK_FLOAT, TOK_WIDE, \
-    TOK_FIELD = range(12)
+    TOK_FIELD, TOK_LIST = range(13)
 ROLLUP_NONE, ROLLUP_DECODE = -1, -2
 
 UPSERT_SPEC, UPSERT_STATUS = 0, 1
@@ -149,7 +172,7 @@ class DeviceView(C.Structure):
 
 class BatchStats(C.Structure):
     _fields_ = [("n_pairs", C.c_uint64), ("pool_bytes", C.c_uint64), ("total_leaves", C.c_uint64),
-                ("compare_bytes", C.c_uint64)]
+                ("compare_bytes", C.c_uint64), ("value_bytes", C.c_uint64)]
 
 
 class Timings(C.Structure):
@@ -229,6 +252,8 @@ SIGNATURES = [
     ("gpudiff_nbatch_free", None, [_P, _P]),
     ("gpudiff_classify_updates", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
                                            C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(C.c_int32)]),
+    ("gpudiff_classify_updates_host", C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
+                                                C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32, C.POINTER(C.c_int32)]),
     ("gpudiff_negotiate_pair_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
                                               C.POINTER(C.c_int32)]),
     ("gpudiff_spec_equal", C.c_int, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]),
@@ -545,6 +570,14 @@ class Engine:
         _chk(_lib.gpudiff_submit(self.ctx, arr, n, C.byref(t)), "gpudiff_submit")
         return t.value
 
+    def submit_array(self, arr: np.ndarray) -> int:
+        """gpudiff_submit over a JSON_PAIR_DTYPE table (json_pair_array)."""
+        assert arr.dtype == JSON_PAIR_DTYPE and arr.flags["C_CONTIGUOUS"]
+        t = C.c_uint64()
+        _chk(_lib.gpudiff_submit(self.ctx, arr.ctypes.data_as(C.POINTER(JsonPair)), arr.size, C.byref(t)),
+             "gpudiff_submit")
+        return t.value
+
     def diff_pairs(self, pairs, ids=None, clusters=None) -> DiffResult:
         return self.wait(self.submit(pairs, ids, clusters))
 
@@ -824,6 +857,28 @@ def negotiate_pair_host(old, new) -> int:
     _chk(_lib.gpudiff_negotiate_pair_host(a, 0 if a is None else len(a), b, len(b), C.byref(act)),
          "gpudiff_negotiate_pair_host")
     return int(act.value)
+
+
+class HostPairs:
+    """(old, new) JSON pairs held in C memory for the classifier's host path
+    (gpudiff_classify_updates_host); old None = no old object."""
+
+    def __init__(self, pairs):
+        pairs = list(pairs)
+        self.n = len(pairs)
+        olds = [None if a is None else to_json_bytes(a) for a, _ in pairs]
+        _, self._nb, self.nptrs, self.nlens = _doc_arrays([b for _, b in pairs])
+        _, self._ob, self.optrs, self.olens = _doc_arrays([a if a is not None else b"" for a in olds])
+        for i, a in enumerate(olds):
+            if a is None:
+                self.optrs[i] = None
+
+    def classify(self, threads: int = 1) -> np.ndarray:
+        out = np.zeros(max(self.n, 1), np.int32)
+        _chk(_lib.gpudiff_classify_updates_host(self.optrs, self.olens, self.nptrs, self.nlens, self.n, threads,
+                                                out.ctypes.data_as(C.POINTER(C.c_int32))),
+             "gpudiff_classify_updates_host")
+        return out[:self.n]
 
 
 def rollup_doc_host(doc):

@@ -74,3 +74,61 @@ def tensor_fill(spec_ids, status_ids):
         if n:
             buf[:n] = (spec_ids if col == 0 else status_ids)[:n]
     return fill
+
+
+class DirtyGather:
+    """The per-step collective with no host synchronisation: preallocated
+    buffers of a fixed capacity per list, one all-gather of the per-rank
+    counts (int32 [8]: n_spec, n_status, ...) and one of each ID list, padded
+    to the capacity.  The capacities are agreed once, before the timed steps
+    (`agree_capacity`: the all-gathered maximum of a first pass's counts); the
+    gathered counts say how many IDs of each rank's slot are real, and
+    `check()` -- called after the timed region -- reports a rank whose count
+    exceeded the capacity (its IDs were truncated: the step must be redone
+    with larger buffers, never silently accepted)."""
+
+    def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist):
+        import torch
+        self.world, self.dist = world, dist
+        self.cap = (max(1, int(cap_spec)), max(1, int(cap_status)))
+        self.counts = torch.zeros(8, dtype=torch.int32, device=device)
+        self.all_counts = torch.zeros(world * 8, dtype=torch.int32, device=device)
+        self.buf = [torch.zeros(c, dtype=torch.int32, device=device) for c in self.cap]
+        self.all_ids = [torch.zeros(world * c, dtype=torch.int32, device=device) for c in self.cap]
+
+    @staticmethod
+    def agree_capacity(counts, world: int, dist, slack: float = 1.0):
+        """All-gathered max of (n_spec, n_status) over ranks (host values; untimed)."""
+        import torch
+        allc = torch.empty(world * counts.numel(), dtype=counts.dtype, device=counts.device)
+        dist.all_gather_into_tensor(allc, counts)
+        cc = allc.view(world, -1).cpu()
+        return int(cc[:, 0].max() * slack) + 1, int(cc[:, 1].max() * slack) + 1
+
+    def step(self, fill_counts, fill_ids):
+        """fill_counts(tensor[8]) and fill_ids(col, tensor[cap]) write this
+        rank's values on the device (the GPU path: gpudiff_dbatch_export
+        straight from HBM, ordered on the stream before the collectives)."""
+        fill_counts(self.counts)
+        self.dist.all_gather_into_tensor(self.all_counts, self.counts)
+        for col in (0, 1):
+            fill_ids(col, self.buf[col])
+            self.dist.all_gather_into_tensor(self.all_ids[col], self.buf[col])
+
+    def check(self):
+        """-> (ok, host count matrix [world, 8])"""
+        cc = self.all_counts.view(self.world, -1).cpu()
+        ok = bool((cc[:, 0] <= self.cap[0]).all() and (cc[:, 1] <= self.cap[1]).all())
+        return ok, cc
+
+    def result(self):
+        """Node-wide (spec IDs, status IDs) in rank order (host sync; after the timed steps)."""
+        import torch
+        ok, cc = self.check()
+        if not ok:
+            raise RuntimeError("dirty-ID capacity exceeded: %s > %s" % (cc[:, :2].tolist(), self.cap))
+        out = []
+        for col in (0, 1):
+            v = self.all_ids[col].view(self.world, self.cap[col])
+            out.append(torch.cat([v[r, :int(cc[r, col])] for r in range(self.world)]))
+        return out[0], out[1]

@@ -20,6 +20,14 @@ def lib():
                                   C.POINTER(C.c_size_t), C.c_size_t]
         l.oracle_free.restype = None
         l.oracle_free.argtypes = [C.c_void_p]
+        l.oracle_tree_paths.restype = C.c_long
+        l.oracle_tree_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        l.oracle_csr_run.restype = C.c_int
+        l.oracle_csr_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.c_void_p,
+                                     C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+        l.oracle_csr_paths.restype = C.c_long
+        l.oracle_csr_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_size_t]
         l.oracle_decide.restype = C.c_int
         l.oracle_decide.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double)]
         l.oracle_docs_load.restype = C.c_void_p
@@ -61,6 +69,24 @@ class DecodedPairs:
         sweeps = lib().oracle_decide(self.h, flags.ctypes.data_as(C.c_void_p), threads, min_seconds,
                                      C.byref(sec))
         return flags, sweeps, sec.value
+
+    def paths(self, seeds, cap=None):
+        """Field-path diff over the decoded trees (checker, untimed): (offsets
+        u32[n_dirty + 1], hashes u64, kinds u8) in gpudiff_result layout; pair i
+        hashed under seeds[i] (the encoder's per-pair seed)."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+        cap = cap or max(1024, 64 * self.n)
+        while True:
+            offs = np.zeros(self.n + 1, np.uint32)
+            hs = np.zeros(cap, np.uint64)
+            ks = np.zeros(cap, np.uint8)
+            m = lib().oracle_tree_paths(self.h, seeds.ctypes.data, offs.ctypes.data, hs.ctypes.data, ks.ctypes.data,
+                                        cap)
+            if m >= 0:
+                flags, _, _ = self.decide()
+                nd = int(np.count_nonzero(flags & 3))
+                return offs[:nd + 1], hs[:m], ks[:m]
+            cap *= 4
 
     def close(self):
         if self.h:
@@ -150,3 +176,37 @@ class RollupDocs:
             self.close()
         except Exception:
             pass
+
+
+class CsrPairs:
+    """The build's canonical CSR encoding of a batch (a host batch's pool and
+    rows) for the CPU merge over CSR ("cpu-csr", oracle/csr_ref.cpp)."""
+
+    def __init__(self, pool: bytes, rows: np.ndarray):
+        self.pool = np.frombuffer(pool, dtype=np.uint8) if pool else np.zeros(16, np.uint8)
+        self.rows = np.ascontiguousarray(rows)
+        self.n = len(rows)
+
+    def run(self, threads=1, min_seconds=0.0):
+        """-> (flags u8[n], sweeps, seconds, paths per sweep); decisions and changed paths timed"""
+        flags = np.zeros(max(self.n, 1), np.uint8)
+        sec = C.c_double()
+        npth = C.c_uint64()
+        sw = lib().oracle_csr_run(self.pool.ctypes.data, self.rows.ctypes.data, self.n, threads, min_seconds,
+                                  flags.ctypes.data, C.byref(sec), C.byref(npth))
+        return flags[:self.n], sw, sec.value, npth.value
+
+    def paths(self, cap=None):
+        """-> (flags u8[n], offsets u32[n_dirty + 1], hashes u64, kinds u8)"""
+        cap = cap or max(1024, 64 * self.n)
+        while True:
+            flags = np.zeros(max(self.n, 1), np.uint8)
+            offs = np.zeros(self.n + 1, np.uint32)
+            hs = np.zeros(cap, np.uint64)
+            ks = np.zeros(cap, np.uint8)
+            m = lib().oracle_csr_paths(self.pool.ctypes.data, self.rows.ctypes.data, self.n, flags.ctypes.data,
+                                       offs.ctypes.data, hs.ctypes.data, ks.ctypes.data, cap)
+            if m >= 0:
+                nd = int(np.count_nonzero(flags[:self.n] & 3))
+                return flags[:self.n], offs[:nd + 1], hs[:m], ks[:m]
+            cap *= 4

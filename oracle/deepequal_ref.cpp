@@ -34,6 +34,8 @@
 #include <unordered_set>
 #include <vector>
 
+#include "xxh64_ref.h"
+
 namespace oracle {
 
 struct Value;
@@ -335,6 +337,142 @@ bool deep_equal_status(const Value& o, const Value& n) {
     return false;  // :26
 }
 
+// apimachinery unstructuredJSONScheme.decode [3P] probes the bytes with
+// encoding/json into struct{ Items json.RawMessage } first: a top-level key
+// equal to "Items" under fold.go's equalFoldRight (ASCII case folding, U+017F
+// for s) decodes as an UnstructuredList, and the predicates' type assertions
+// (specsyncer.go:18-22, statussyncer.go:16-20) fail
+static bool list_probe(const Value& root) {
+    for (const auto& kv : *root.m) {
+        const std::string& k = kv.first;
+        const char* name = "Items";
+        size_t i = 0;
+        bool ok = true;
+        for (const char* s = name; *s && ok; s++) {
+            if (i >= k.size()) { ok = false; break; }
+            const unsigned char t = (unsigned char)k[i];
+            if (t < 0x80) {
+                ok = (unsigned char)(*s | 0x20) == (t | 0x20) && ((t | 0x20) >= 'a' && (t | 0x20) <= 'z');
+                i++;
+            } else if ((*s == 's' || *s == 'S') && t == 0xC5 && i + 1 < k.size() && (unsigned char)k[i + 1] == 0xBF) {
+                i += 2;
+            } else {
+                ok = false;
+            }
+        }
+        if (ok && i == k.size()) return true;
+    }
+    return false;
+}
+
+// ------------------------------------------------------------ field-path diff (build-defined)
+// The same definition as the Python oracle (oracle/gpudiff_oracle.py spec_leaves /
+// status_leaves / _region_diff), over the decoded trees: leaves keyed by their encoded
+// path (0x01 u32le(len) key | 0x02 u32le(index)), chained path hash under the pair's seed.
+struct Leaf {
+    uint8_t tag;
+    std::string bytes;
+    bool operator==(const Leaf& o) const { return tag == o.tag && bytes == o.bytes; }
+};
+using LeafMap = std::unordered_map<std::string, std::pair<uint64_t, Leaf>>;  // path bytes -> (hash, leaf)
+
+static void put_comp(std::string& p, uint8_t kind, const void* data, uint32_t n) {
+    p.push_back((char)kind);
+    if (kind == 0x01) {
+        p.append((const char*)&n, 4);
+        p.append((const char*)data, n);
+    } else {
+        p.append((const char*)data, 4);
+    }
+}
+
+static void flatten(const Value& v, std::string& path, uint64_t h, LeafMap& out) {
+    if (v.k == Value::MAP && !v.m->empty()) {
+        for (const auto& kv : *v.m) {
+            const size_t mark = path.size();
+            put_comp(path, 0x01, kv.first.data(), (uint32_t)kv.first.size());
+            flatten(kv.second, path, xxh64_ref(path.data() + mark, path.size() - mark, h), out);
+            path.resize(mark);
+        }
+        return;
+    }
+    if (v.k == Value::ARR && !v.a->empty()) {
+        for (uint32_t i = 0; i < v.a->size(); i++) {
+            const size_t mark = path.size();
+            put_comp(path, 0x02, &i, 4);
+            flatten((*v.a)[i], path, xxh64_ref(path.data() + mark, path.size() - mark, h), out);
+            path.resize(mark);
+        }
+        return;
+    }
+    Leaf l;
+    switch (v.k) {
+        case Value::NIL: l.tag = 0; break;
+        case Value::BOOL: l.tag = v.b ? 2 : 1; break;
+        case Value::INT: l.tag = 3; l.bytes.assign((const char*)&v.i, 8); break;
+        case Value::FLOAT: {
+            const double d = v.f == 0.0 ? 0.0 : v.f;
+            l.tag = 4;
+            l.bytes.assign((const char*)&d, 8);
+            break;
+        }
+        case Value::STR: l.tag = 5; l.bytes = v.s; break;
+        case Value::MAP: l.tag = 6; break;
+        default: l.tag = 7; break;
+    }
+    out[path] = {h, std::move(l)};
+}
+
+static uint64_t key_hash(uint64_t h, const char* k, std::string& path) {
+    const size_t mark = path.size();
+    put_comp(path, 0x01, k, (uint32_t)strlen(k));
+    return xxh64_ref(path.data() + mark, path.size() - mark, h);
+}
+
+static void spec_leaves(const Value& o, uint64_t seed, LeafMap& out) {
+    for (const auto& kv : *o.m) {
+        if (kv.first == "metadata" || kv.first == "status" || kv.second.k == Value::NIL) continue;
+        std::string path;
+        put_comp(path, 0x01, kv.first.data(), (uint32_t)kv.first.size());
+        flatten(kv.second, path, xxh64_ref(path.data(), path.size(), seed), out);
+    }
+    for (const char* field : {"labels", "annotations"}) {
+        auto m = nested_string_map(o, field);
+        if (!m || m->empty()) continue;
+        std::string path;
+        uint64_t h = key_hash(seed, "metadata", path);
+        h = key_hash(h, field, path);
+        for (const auto& kv : *m) {
+            const size_t mark = path.size();
+            put_comp(path, 0x01, kv.first.data(), (uint32_t)kv.first.size());
+            out[path] = {xxh64_ref(path.data() + mark, path.size() - mark, h), Leaf{5, kv.second}};
+            path.resize(mark);
+        }
+    }
+}
+
+static void status_leaves(const Value& o, uint64_t seed, LeafMap& out) {
+    auto s = o.m->find("status");
+    if (s == o.m->end() || s->second.k == Value::NIL) return;
+    std::string path;
+    const uint64_t h = key_hash(seed, "status", path);
+    flatten(s->second, path, h, out);
+}
+
+// entries (hash, kind | region bit) of one region, ascending hash
+static void region_diff(const LeafMap& a, const LeafMap& b, uint8_t region_bit,
+                        std::vector<std::pair<uint64_t, uint8_t>>& out) {
+    const size_t base = out.size();
+    for (const auto& kv : a) {
+        auto it = b.find(kv.first);
+        if (it == b.end()) out.push_back({kv.second.first, (uint8_t)(2 | region_bit)});  // removed
+        else if (!(it->second.second == kv.second.second)) out.push_back({kv.second.first, (uint8_t)(0 | region_bit)});
+    }
+    for (const auto& kv : b)
+        if (!a.count(kv.first)) out.push_back({kv.second.first, (uint8_t)(1 | region_bit)});  // added
+    std::sort(out.begin() + base, out.end());
+}
+
 struct Pairs {
     std::vector<Value> a, b;
     std::vector<uint8_t> err;
@@ -353,9 +491,56 @@ void* oracle_load(const char* const* a, const size_t* alen, const char* const* b
     p->b.resize(n);
     p->err.assign(n, 0);
     for (size_t i = 0; i < n; i++) {
-        if (!decode(a[i], alen[i], p->a[i]) || !decode(b[i], blen[i], p->b[i])) p->err[i] = 1;
+        if (!decode(a[i], alen[i], p->a[i]) || !decode(b[i], blen[i], p->b[i]) || list_probe(p->a[i]) ||
+            list_probe(p->b[i]))
+            p->err[i] = 1;
     }
     return p;
+}
+
+// changed paths of every pair (checker, untimed): pair i under path-hash seed
+// seeds[i]; for each dirty pair, offsets[k] .. offsets[k+1] of (hashes, kinds)
+// in output order -- spec entries by ascending hash, then (status dirty only)
+// status entries, then the status-absent sentinel.  Returns the number of
+// entries, or -1 if cap is too small.
+long oracle_tree_paths(void* h, const uint8_t* seeds, uint32_t* offsets, uint64_t* hashes, uint8_t* kinds,
+                       size_t cap) {
+    Pairs* p = (Pairs*)h;
+    size_t k = 0, total = 0;
+    offsets[0] = 0;
+    std::vector<std::pair<uint64_t, uint8_t>> ent;
+    for (size_t i = 0; i < p->a.size(); i++) {
+        if (p->err[i]) {
+            offsets[++k] = (uint32_t)total;  // decode error: dirty, no paths
+            continue;
+        }
+        const bool sd = !deep_equal_apart_from_status(p->a[i], p->b[i]);
+        const bool td = !deep_equal_status(p->a[i], p->b[i]);
+        if (!sd && !td) continue;
+        ent.clear();
+        LeafMap la, lb;
+        spec_leaves(p->a[i], seeds[i], la);
+        spec_leaves(p->b[i], seeds[i], lb);
+        region_diff(la, lb, 0, ent);
+        if (td) {
+            LeafMap ta, tb;
+            status_leaves(p->a[i], seeds[i], ta);
+            status_leaves(p->b[i], seeds[i], tb);
+            region_diff(ta, tb, 0x80, ent);
+            if (!p->b[i].m->count("status")) {
+                std::string path;
+                ent.push_back({key_hash(seeds[i], "status", path), (uint8_t)(3 | 0x80)});
+            }
+        }
+        if (total + ent.size() > cap) return -1;
+        for (const auto& e : ent) {
+            hashes[total] = e.first;
+            kinds[total] = e.second;
+            total++;
+        }
+        offsets[++k] = (uint32_t)total;
+    }
+    return (long)total;
 }
 
 void oracle_free(void* h) { delete (Pairs*)h; }

@@ -47,8 +47,14 @@ What it restates (reference paths relative to /root/reference):
   slices are equal; metav1.Time compares ``a.UTC() == b.UTC()``, i.e. the
   instant to the nanosecond.
 
-A pair one of whose sides Go cannot decode is reported as DECODE (-1): the
-reference's informer would never deliver such an object.  CustomResource-
+DECODE (-1) means: a side is not valid JSON, is not an object, or one of the
+fields read above fails Go's typed decode (the reference's informer would
+never deliver such an object).  Type errors in fields the classifier does not
+read (spec, metadata.name, creationTimestamp, ...) are not checked: Go's typed
+Unmarshal would reject those objects too, so no reference outcome exists for
+them, and the classification here follows the fields read (KAT
+"outside-domain-spec-type-error").  A root ``null`` (a zero object to Go's
+Unmarshal; never a watch event body) is reported as DECODE.  CustomResource-
 Definition events (the third kind, :186-199) are not covered.
 
 PARITY STATUS: no reference tests exist for the controller and Go is absent,

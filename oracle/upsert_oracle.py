@@ -49,7 +49,7 @@ from typing import Any, Dict, List, Optional
 
 import numpy as np
 
-from .gpudiff_oracle import DecodeError, go_json_decode, nested_string_map
+from .gpudiff_oracle import DecodeError, _nesting_bound, _on_big_stack, go_json_decode, nested_string_map
 
 MODE_SPEC = 0    # upsertIntoDownstream (specsyncer.go:86-110): the Create body
 MODE_STATUS = 1  # updateStatusInUpstream (statussyncer.go:41-48)
@@ -198,6 +198,12 @@ def upsert_body(json_bytes: bytes, mode: int = MODE_SPEC) -> Optional[bytes]:
     json.NewEncoder(w).Encode(transform(decode(json))) -- Marshal plus '\\n'.
     None if the informer could never have delivered the object (Go decode
     error)."""
+    if _nesting_bound(json_bytes) > 1000:  # recursion as deep as Go's 10000-level limit
+        return _on_big_stack(_upsert_body, json_bytes, mode)
+    return _upsert_body(json_bytes, mode)
+
+
+def _upsert_body(json_bytes: bytes, mode: int) -> Optional[bytes]:
     try:
         obj = go_json_decode(json_bytes)
     except DecodeError:

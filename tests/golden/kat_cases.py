@@ -241,4 +241,25 @@ def cases():
     add("x19_deep_nesting", mod(_set(["spec", "x"], {"a": [[[{"b": [1, {"c": None}]}]]]})),
         mod(_set(["spec", "x"], {"a": [[[{"b": [1, {"c": False}]}]]]})), False, True)
     add("x20_trailing_garbage", B, J(B) + b" x", False, False)
+
+    # ---- the informer decoder's list probe (apimachinery unstructuredJSONScheme.decode, reached from
+    # pkg/syncer/syncer.go:105-108): a top-level key equal to "Items" under encoding/json's case folding
+    # (any value, null included) decodes as an UnstructuredList, which fails the type assertions of
+    # specsyncer.go:18-22 / statussyncer.go:16-20 -> both predicates false, even for identical objects
+    items = mod(_set(["items"], []))
+    add("x21_list_probe_items", items, items, False, False)
+    add("x22_list_probe_items_null_in_new", B, mod(_set(["items"], None)), False, False)
+    add("x23_list_probe_case_folded", J(B), J(B)[:-1] + b',"iTEMs":{"a":1}}', False, False)
+    add("x24_list_probe_long_s", J(B)[:-1] + b',"item\xc5\xbf":1}', J(B), False, False)
+    add("x25_list_probe_escaped_key", J(B)[:-1] + b',"\\u0069tems":1}', J(B)[:-1] + b',"\\u0069tems":1}',
+        False, False)
+    add("x26_not_list_nested_items", mod(_set(["spec", "items"], [1])), mod(_set(["spec", "items"], [1])), True, True)
+    add("x27_not_list_near_misses", J(B)[:-1] + b',"itemz":1,"item":2,"itemss":3,"\xc4\xb1tems":4}',
+        J(B)[:-1] + b',"itemz":1,"item":2,"itemss":3,"\xc4\xb1tems":4}', True, True)
+    # ---- encoding/json's maxNestingDepth (10000): a document nested 10000 containers deep decodes,
+    # 10001 is a decode error (the pair is dirty); spec.x sits at depth 2, so n arrays reach depth n + 2
+    deep = lambda n: J(a25).replace(b'"x":1', b'"x":' + b'[' * n + b']' * n)
+    add("x28_depth_10000", deep(9998), deep(9998), True, True)
+    add("x29_depth_10001", deep(9998), deep(9999), False, False)
+    add("x30_depth_10000_changed", deep(9998), deep(9997) + b'', False, True)
     return out

@@ -105,6 +105,11 @@ def cases():
         ("label-number", obj(rv="1"), obj(rv="2", labels={"a": 1}), DECODE),
         ("status-string", obj(rv="1"), obj(rv="2").replace(b'"status": {}', b'"status": "x"'), DECODE),
         ("bad-json", obj(rv="1"), b'{"metadata": {', DECODE),
+        # outside the reference's domain (Go's typed Unmarshal would reject the object, so the informer never
+        # delivers it): the build's documented answers -- classified by the fields read; a root null is DECODE
+        ("outside-domain-spec-type-error", obj(rv="1", gen=1),
+         obj(rv="2", gen=2).replace(b'"plural": "deployments"', b'"plural": 5'), SPEC),
+        ("outside-domain-root-null", obj(rv="1"), b'null', DECODE),
         ("negotiated-kind", obj(rv="1", kind="NegotiatedAPIResource", conds=C),
          obj(rv="2", kind="NegotiatedAPIResource", conds=[cond(s="False")]), STATUS),
     ]

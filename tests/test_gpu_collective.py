@@ -1,0 +1,71 @@
+"""The multi-GPU step's collective over RCCL ("nccl" backend = RCCL on ROCm) on
+real hardware at world_size 1: shard.DirtyGather (the bench's host-sync-free
+per-step all-gather, IDs exported straight from HBM with
+gpudiff_dbatch_export) and shard.gather_dirty return the node-wide dirty sets
+of a diffed device batch.  World size 2 of the same code runs on CPU (gloo) in
+tests/test_multirank.py."""
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from kcp_amd import gpudiff as G
+from kcp_amd import shard
+from tests.workload import make_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_dirty_gather_over_rccl_world1():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        stream = torch.cuda.current_stream(dev)
+        eng = G.Engine(device=0, stream=stream.cuda_stream)
+        pairs, _, _ = make_pairs(3000, seed=21, mutate_frac=0.3, pretty_frac=0)
+        hb = eng.encode(pairs)
+        db = eng.device_batch(hb.info().pool_bytes + 4096, len(pairs))
+        db.append(hb)
+        want = eng.wait(eng.diff(db))
+        counts = torch.zeros(8, dtype=torch.int32, device=dev)
+        db.export(G.EXPORT_COUNTS, counts.data_ptr(), 8)
+        torch.cuda.synchronize()
+        cap_s, cap_t = shard.DirtyGather.agree_capacity(counts, 1, dist)
+        assert (cap_s, cap_t) == (want.spec_dirty_ids.size + 1, want.status_dirty_ids.size + 1)
+        g = shard.DirtyGather(1, cap_s, cap_t, dev, dist)
+
+        def fill_counts(t):
+            db.export(G.EXPORT_COUNTS, t.data_ptr(), 8)
+
+        def fill_ids(col, buf):
+            db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
+                      buf.numel())
+        for _ in range(3):  # diff + collective, no host sync in between
+            eng.diff(db)
+            g.step(fill_counts, fill_ids)
+        torch.cuda.synchronize()
+        sa, ta = g.result()
+        assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+        assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        # the general (trimmed) form
+        s2, t2 = shard.gather_dirty(counts, lambda col, buf, k: db.export(
+            G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(), k), 0, 1, dist, dev)
+        assert np.array_equal(s2.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+        assert np.array_equal(t2.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        db.free()
+        hb.free()
+        eng.close()
+    finally:
+        dist.destroy_process_group()

@@ -108,6 +108,8 @@ EDGE_OK = [
     b'{"spec":' + b'[' * 200 + b'1' + b']' * 200 + b'}',
     b'{"spec":{"obj":{' + b",".join(b'"k%03d":{"v":"val%d","n":%d}' % (i, i, i) for i in range(150)) + b'}}}',
     b'\n\t {"spec" : { "a" : [ 1 , 2 ] , "b" : "c" } , "status" : { "ok" : true } }\r\n',
+    # near misses of the informer decoder's list probe (only a root key equal to "items" under case folding)
+    b'{"spec":{"items":[1]}}', b'{"itemz":1}', b'{"item":1}', b'{"itemss":1}', b'{"xitems":1,"Item":2}',
 ]
 # (doc, K0 status, host decides Go error?)
 EDGE_DEFER = [
@@ -128,6 +130,9 @@ EDGE_DEFER = [
     (b'{"a":[1 2]}', G.TOK_SYNTAX), (b'{"a":{"b":1]}', G.TOK_SYNTAX), (b'{a:1}', G.TOK_SYNTAX),
     (b'{"a":1', G.TOK_SYNTAX), (b'{"a":truex}', G.TOK_SYNTAX), (b'{"a":"b"c}', G.TOK_SYNTAX),
     (b'\xef\xbb\xbf{"a":1}', G.TOK_SYNTAX), (b'{"a":\\"b"}', G.TOK_SYNTAX), (b'{"a":1}}', G.TOK_SYNTAX),
+    # the list probe: the host decides (an UnstructuredList, json.cpp decodes_as_list)
+    (b'{"items":[]}', G.TOK_LIST), (b'{"a":1,"ITEMS":null}', G.TOK_LIST), (b'{"iTeMs":{"x":[1]},"b":2}', G.TOK_LIST),
+    ('{"item\u017f":1}'.encode(), G.TOK_KEY), (b'{"\\u0069tems":1}', G.TOK_KEY),
 ]
 
 
@@ -138,6 +143,21 @@ def test_edge_cases_exact_or_deferred():
     codes = _check(eng, docs, must_encode=False)
     for (d, want), got in zip(EDGE_DEFER, codes):
         assert got == want, (d[:80], got, want)
+    eng.close()
+
+
+def test_edge_corpus_through_submit_vs_oracle():
+    """The edge corpus through the device-encode submit path (K0, the host
+    re-doing K0's deferrals) against the oracle's decisions and paths: every
+    edge document paired with itself, with an empty object, and with a
+    neighbour."""
+    from tests.parity import assert_matches
+    eng = G.Engine(device=0, device_encode=True)
+    docs = list(EDGE_OK) + [d for d, _ in EDGE_DEFER]
+    pairs = [(d, d) for d in docs] + [(b'{}', d) for d in docs] + [(d, b'{"status":{}}') for d in docs]
+    pairs += [(docs[i], docs[i + 1]) for i in range(len(docs) - 1)]
+    res = eng.diff_pairs(pairs)
+    assert_matches(res, pairs)
     eng.close()
 
 

@@ -1,6 +1,7 @@
 """Kernel K10 (the write path's request bodies) on the
-GPU: every body K10 emits is byte-identical to the host path's (itself pinned
-to the oracle and the known-answer bodies by tests/test_upsert.py), and the
+GPU: every body is byte-identical to the oracle's (oracle/upsert_oracle.py,
+test_k10_bodies_equal_oracle) and to the product's host path (itself pinned to
+the oracle and the known-answer bodies by tests/test_upsert.py), and the
 documents K10 leaves to the host carry one of the documented reasons."""
 import json
 import random
@@ -8,6 +9,7 @@ import random
 import pytest
 
 from kcp_amd import gpudiff as G
+from oracle import upsert_oracle as U
 from tests import upsert_cases as UC
 from tests.test_gpu_tokenize import EDGE_DEFER, EDGE_OK
 
@@ -139,4 +141,24 @@ def test_float_text_matches_host():
     single = [b'{"f":%s}' % x for x in lits[:4000]]
     codes = _check(eng, single, UC.SPEC, must_device=False)
     assert sum(c == G.TOK_OK for c in codes) >= 0.95 * len(codes), sum(c == G.TOK_OK for c in codes)
+    eng.close()
+
+
+@pytest.mark.parametrize("mode", [UC.SPEC, UC.STATUS])
+def test_k10_bodies_equal_oracle(mode):
+    """K10 (with its host completion) against the Python oracle directly, not the
+    product's host path: the known-answer documents, the reference's fixtures,
+    synthetic kcp-shaped objects with and without floats, K0's edge corpus and
+    the 64-byte scan boundaries; the synthetic populations must come from the
+    device."""
+    eng = G.Engine(device=0)
+    groups = [([k[1] for k in UC.KAT], False), (UC.fixture_docs(), False), (UC.synthetic_docs(floats=False), True),
+              (UC.synthetic_docs(seed=12), False), (UC.boundary_docs(), True),
+              (list(EDGE_OK) + [d for d, _ in EDGE_DEFER], False)]
+    for docs, all_device in groups:
+        res = eng.upsert_bodies(docs, mode)
+        for i, d in enumerate(docs):
+            assert res.bodies[i] == U.upsert_body(d, mode), (i, d[:300])
+        if all_device:
+            assert res.n_host == 0 and all(int(s) == G.BODY_DEVICE for s in res.source)
     eng.close()

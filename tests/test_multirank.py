@@ -102,3 +102,81 @@ def test_gather_dirty_gloo_world2():
     want_t = sorted(np.nonzero(flags & 2)[0].tolist())
     for rank, s, t in res:
         assert s == want_s and t == want_t
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_strong_scaling_shards_split_one_config(world):
+    """bench.py default for N > 1 (--scaling strong): the metric's population
+    (config3: 10M pairs / 100k logical clusters) split N ways by whole logical
+    cluster (pkg/reconciler/cluster/cluster.go:125-138: one syncer per cluster)."""
+    cfg = S.make_cfg("config3")
+    sizes, clusters = [], []
+    for r in range(world):
+        p = S.Population(cfg, world, r)
+        sizes.append(p.n)
+        clusters.append(p.n_clusters)
+        p.close()
+    assert sum(sizes) == cfg.n_pairs and sum(clusters) == cfg.n_clusters
+    assert max(sizes) - min(sizes) <= cfg.n_pairs // world * 0.002
+
+
+def _worker_fixed(rank, world, port, flags_all, owners, shrink, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = np.nonzero(owners == rank)[0]
+    f = flags_all[mine]
+    spec = torch.tensor(mine[(f & 1) != 0], dtype=torch.int32)
+    stat = torch.tensor(mine[(f & 2) != 0], dtype=torch.int32)
+    counts = torch.zeros(8, dtype=torch.int32)
+    counts[0], counts[1] = spec.numel(), stat.numel()
+    cs, ct = shard.DirtyGather.agree_capacity(counts, world, dist)
+    g = shard.DirtyGather(world, cs - shrink, ct, "cpu", dist)
+
+    def fill_counts(t):
+        t.copy_(counts)
+
+    def fill_ids(col, buf):
+        src = spec if col == 0 else stat
+        k = min(buf.numel(), src.numel())
+        buf[:k] = src[:k]
+    for _ in range(3):  # repeated steps reuse the buffers
+        g.step(fill_counts, fill_ids)
+    ok, _ = g.check()
+    if ok:
+        sa, ta = g.result()
+        q.put((rank, True, sorted(sa.tolist()), sorted(ta.tolist())))
+    else:
+        q.put((rank, False, None, None))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shrink", [0, 5])
+def test_dirty_gather_fixed_capacity_gloo_world2(shrink):
+    """The bench's per-step collective (shard.DirtyGather: no host sync, fixed
+    capacity): node-wide dirty sets equal the single-rank view; a capacity
+    below a rank's count is reported, never truncated silently."""
+    rnd = np.random.default_rng(4)
+    n = 4000
+    clusters = rnd.integers(0, 61, n)
+    flags = rnd.integers(0, 4, n).astype(np.uint8)
+    owners = np.zeros(n, dtype=np.int32)
+    for r, idx in enumerate(shard.shard_pairs(clusters, 2)):
+        owners[idx] = r
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_fixed, args=(r, 2, port, flags, owners, shrink, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_s = sorted(np.nonzero(flags & 1)[0].tolist())
+    want_t = sorted(np.nonzero(flags & 2)[0].tolist())
+    for rank, ok, s, t in res:
+        if shrink:
+            assert not ok
+        else:
+            assert ok and s == want_s and t == want_t

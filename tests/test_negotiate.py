@@ -149,3 +149,14 @@ def test_time_parse_vs_datetime():
         except ValueError:
             want = None
         assert got == want, (t, got, want)
+
+
+def test_host_batch_entry_point_matches_oracle():
+    """gpudiff_classify_updates_host (the host path over a batch, on several
+    threads; the negotiation bench's CPU baseline) equals the oracle."""
+    from kcp_amd import gpudiff as G
+    cs = C.cases()
+    pairs = [(a, b) for _, a, b, _ in cs] * 7
+    hp = G.HostPairs(pairs)
+    got = hp.classify(threads=4).tolist()
+    assert got == [N.classify(a, b) for a, b in pairs]

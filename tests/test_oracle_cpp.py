@@ -1,19 +1,50 @@
-"""Pins the C++ restatement of the predicates (CPU baseline) to the Python
-oracle and the Appendix A.4 table."""
-import numpy as np
+"""Pins the C++ restatements (CPU baselines) to the Python oracle and the
+Appendix A.4 table: the tree-walk restatement of the predicates (decisions and
+its field-path diff), the CPU merge over the canonical CSR encoding
+("cpu-csr", oracle/csr_ref.cpp) and the oracle's own XXH64."""
+import random
 
+import numpy as np
+import xxhash
+
+from kcp_amd import gpudiff as G
 from oracle import cpu_ref
 from tests.golden.kat_cases import cases
-from tests.parity import expected_flags, oracle_batch
+from tests.parity import expected_flags, expected_paths, oracle_batch
 from tests.workload import make_pairs
 
 
-def _check(pairs, threads=1):
+def _paths_of(offs, hs, ks, k):
+    b, e = int(offs[k]), int(offs[k + 1])
+    return list(zip(hs[b:e].tolist(), ks[b:e].tolist()))
+
+
+def _check(pairs, threads=1, paths=True):
+    exp = oracle_batch(pairs)
+    want = np.array([expected_flags(r) for r in exp], dtype=np.uint8)
     d = cpu_ref.DecodedPairs(pairs)
     flags, sweeps, sec = d.decide(threads)
-    exp = np.array([expected_flags(r) for r in oracle_batch(pairs)], dtype=np.uint8)
-    assert (flags == exp).all(), np.nonzero(flags != exp)[0][:10]
+    assert (flags == want).all(), np.nonzero(flags != want)[0][:10]
+    if not paths:
+        d.close()
+        return
+    dirty = np.nonzero(want & 3)[0].tolist()
+    offs, hs, ks = d.paths([r["seed"] for r in exp])
+    assert offs.size == len(dirty) + 1
+    for k, i in enumerate(dirty):
+        assert _paths_of(offs, hs, ks, k) == expected_paths(exp[i]), i
     d.close()
+    # the CPU merge over the encoder's CSR blobs
+    eng = G.Engine(device=G.DEVICE_NONE, encode_threads=2)
+    hb = eng.encode(pairs)
+    csr = cpu_ref.CsrPairs(hb.pool(), hb.rows())
+    f2, offs2, hs2, ks2 = csr.paths()
+    assert (f2 == want).all(), np.nonzero(f2 != want)[0][:10]
+    for k, i in enumerate(dirty):
+        assert _paths_of(offs2, hs2, ks2, k) == expected_paths(exp[i]), i
+    f3, sweeps, sec, npaths = csr.run(threads=threads)
+    assert (f3 == want).all() and sweeps >= 1 and npaths == hs2.size
+    eng.close()
 
 
 def test_kat():
@@ -23,3 +54,27 @@ def test_kat():
 def test_population_threads():
     pairs, _, _ = make_pairs(1500, seed=11, mutate_frac=0.2)
     _check(pairs, threads=4)
+
+
+def test_deep_objects_and_short_hashes():
+    pairs, _, _ = make_pairs(120, seed=16, mix=(("crd", 1.0),), mutate_frac=0.6, crd_leaves=800)
+    _check(pairs, threads=2)
+
+
+def test_xxh64_ref_matches_xxhash():
+    """The oracle's independent XXH64 (via the chained path hash of the tree
+    restatement) against the xxhash package: a one-component path's hash is
+    XXH64(0x01 u32le(len) key, seed)."""
+    rnd = random.Random(5)
+    for n in list(range(0, 70)) + [127, 128, 1000]:
+        key = "".join(rnd.choice("abcxyz") for _ in range(n))
+        seed = rnd.randrange(256)
+        a = b'{"k":1,"status":{}}'
+        b = ('{"k":1,"%s":2,"status":{}}' % key).encode() if key not in ("k", "metadata", "status") else a
+        if a == b:
+            continue
+        d = cpu_ref.DecodedPairs([(a, b)])
+        offs, hs, ks = d.paths([seed])
+        comp = b"\x01" + len(key.encode()).to_bytes(4, "little") + key.encode()
+        assert hs.tolist() == [xxhash.xxh64_intdigest(comp, seed=seed)], key
+        d.close()

@@ -54,11 +54,14 @@ def main():
             k["hbm_bytes"] = k["fetch_bytes_corrected"] + k["write_bytes"]
         kernels[short(name)] = k
     k2 = kernels.get("k_compare", {})
-    alg = bench["roofline"]["bytes_per_launch"]
+    rl = bench["roofline"]
+    alg = rl["format"]["bytes_per_launch"] if "format" in rl else rl["bytes_per_launch"]
     summary = dict(
         workload=bench["config"]["workload"],
         kernel="k_compare",
+        k2_source_hash=rl.get("k2_source_hash"),
         algorithmic_bytes_per_launch=alg,
+        survey_bytes_per_launch=rl.get("bytes_per_launch") if "format" in rl else None,
         hbm_bytes_per_launch=k2.get("hbm_bytes"),
         traffic_over_algorithmic=(k2["hbm_bytes"] / alg) if k2.get("hbm_bytes") else None,
         rocprof_avg_ms=k2.get("avg_ms"),
