@@ -266,6 +266,8 @@ SIGNATURES = [
 def _load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError("libgpudiff.so not built (run `python kcp_amd/build.py`); there is no CPU fallback")
+    from . import _hiprt
+    _hiprt.preload()  # share torch's HIP runtime instead of mapping a second one
     lib = C.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         f = getattr(lib, name)

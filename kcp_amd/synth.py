@@ -39,6 +39,9 @@ _SIGS = [
                                      C.c_size_t, C.POINTER(C.c_size_t)]),
 ]
 
+from . import _hiprt  # noqa: E402
+
+_hiprt.preload()
 _lib = C.CDLL(SYNTH_PATH)
 for _n, _r, _a in _SIGS:
     getattr(_lib, _n).restype = _r

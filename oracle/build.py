@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "liboracle.so")
 SRCS = [os.path.join(HERE, "deepequal_ref.cpp"), os.path.join(HERE, "rollup_ref.cpp"), os.path.join(HERE, "csr_ref.cpp")]
-DEPS = SRCS + [os.path.join(HERE, "xxh64_ref.h"), os.path.join(os.path.dirname(HERE), "include", "gpudiff_format.h"),
+DEPS = SRCS + [os.path.join(HERE, "xxh64_ref.h"), os.path.join(HERE, "timed_threads.h"), os.path.join(os.path.dirname(HERE), "include", "gpudiff_format.h"),
                 os.path.join(os.path.dirname(HERE), "include", "gpudiff.h")]
 
 

@@ -22,13 +22,13 @@ def lib():
         l.oracle_free.argtypes = [C.c_void_p]
         l.oracle_tree_paths.restype = C.c_long
         l.oracle_tree_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
-        l.oracle_csr_run.restype = C.c_int
+        l.oracle_csr_run.restype = C.c_double
         l.oracle_csr_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.c_void_p,
                                      C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
         l.oracle_csr_paths.restype = C.c_long
         l.oracle_csr_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p, C.c_size_t]
-        l.oracle_decide.restype = C.c_int
+        l.oracle_decide.restype = C.c_double
         l.oracle_decide.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double)]
         l.oracle_docs_load.restype = C.c_void_p
         l.oracle_docs_load.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t]
@@ -36,7 +36,7 @@ def lib():
         l.oracle_docs_free.argtypes = [C.c_void_p]
         l.oracle_upsert_body.restype = C.c_long
         l.oracle_upsert_body.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_char_p, C.c_size_t]
-        l.oracle_upsert_run.restype = C.c_int
+        l.oracle_upsert_run.restype = C.c_double
         l.oracle_upsert_run.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.POINTER(C.c_double),
                                         C.POINTER(C.c_uint64)]
         l.oracle_rollup_load.restype = C.c_void_p

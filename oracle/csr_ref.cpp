@@ -23,6 +23,7 @@
 
 #include "../include/gpudiff.h"
 #include "../include/gpudiff_format.h"
+#include "timed_threads.h"
 #include "xxh64_ref.h"
 
 namespace {
@@ -104,34 +105,22 @@ uint8_t diff_pair(const uint8_t* pool, const gpudiff_pair_row& r, Emit&& emit) {
 extern "C" {
 
 // Timed: decisions + changed paths of every pair (paths counted, not kept),
-// repeated until min_seconds; returns sweeps, *seconds = wall time,
-// *n_paths = paths per sweep.
-int oracle_csr_run(const uint8_t* pool, const gpudiff_pair_row* rows, size_t n, int threads, double min_seconds,
-                   uint8_t* flags, double* seconds, uint64_t* n_paths) {
+// threads repeating their slices until min_seconds; returns sweeps
+// (fractional), *seconds = wall time, *n_paths = paths per sweep.
+double oracle_csr_run(const uint8_t* pool, const gpudiff_pair_row* rows, size_t n, int threads, double min_seconds,
+                      uint8_t* flags, double* seconds, uint64_t* n_paths) {
     if (threads < 1) threads = 1;
-    int sweeps = 0;
     std::vector<uint64_t> per(threads, 0), sink(threads, 0);
-    auto t0 = std::chrono::steady_clock::now();
-    double el = 0;
-    do {
-        auto work = [&](int t) {
-            uint64_t cnt = 0, x = 0;
-            auto emit = [&](uint64_t h, uint8_t k) {
-                cnt++;
-                x ^= h + k;
-            };
-            for (size_t i = n * t / threads, e = n * (t + 1) / threads; i < e; i++)
-                flags[i] = diff_pair(pool, rows[i], emit);
-            per[t] = cnt;
-            sink[t] = x;  // keeps the emitted paths live
+    const double sw = oracle::timed_sweeps(n, threads, min_seconds, seconds, [&](int t, size_t b, size_t e) {
+        uint64_t cnt = 0, x = 0;
+        auto emit = [&](uint64_t h, uint8_t k) {
+            cnt++;
+            x ^= h + k;
         };
-        std::vector<std::thread> th;
-        for (int t = 1; t < threads; t++) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-        sweeps++;
-        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    } while (el < min_seconds);
+        for (size_t i = b; i < e; i++) flags[i] = diff_pair(pool, rows[i], emit);
+        per[t] = cnt;
+        sink[t] ^= x;  // keeps the emitted paths live
+    });
     uint64_t tot = 0, xs = 0;
     for (int t = 0; t < threads; t++) {
         tot += per[t];
@@ -139,9 +128,8 @@ int oracle_csr_run(const uint8_t* pool, const gpudiff_pair_row* rows, size_t n, 
     }
     static volatile uint64_t g_sink;
     g_sink = xs;
-    if (seconds) *seconds = el;
     if (n_paths) *n_paths = tot;
-    return sweeps;
+    return sw;
 }
 
 // Checker: the changed-path CSR of the dirty pairs (gpudiff_result layout:

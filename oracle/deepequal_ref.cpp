@@ -34,6 +34,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "timed_threads.h"
 #include "xxh64_ref.h"
 
 namespace oracle {
@@ -546,35 +547,19 @@ long oracle_tree_paths(void* h, const uint8_t* seeds, uint32_t* offsets, uint64_
 void oracle_free(void* h) { delete (Pairs*)h; }
 
 // runs both predicates over every pair; flags bit0 spec dirty, bit1 status
-// dirty, bit2 decode error.  Repeats the sweep until min_seconds elapsed;
-// returns the number of sweeps and the wall seconds of the timed region.
-int oracle_decide(void* h, uint8_t* flags, int threads, double min_seconds, double* seconds) {
+// dirty, bit2 decode error.  Threads repeat their slices until min_seconds
+// elapsed; returns the sweeps done (fractional) and the wall seconds.
+double oracle_decide(void* h, uint8_t* flags, int threads, double min_seconds, double* seconds) {
     Pairs* p = (Pairs*)h;
-    const size_t n = p->a.size();
-    if (threads < 1) threads = 1;
-    int sweeps = 0;
-    auto t0 = std::chrono::steady_clock::now();
-    double el = 0;
-    do {
-        auto work = [&](int t) {
-            size_t b = n * t / threads, e = n * (t + 1) / threads;
-            for (size_t i = b; i < e; i++) {
-                uint8_t f;
-                if (p->err[i]) f = 7;
-                else f = (deep_equal_apart_from_status(p->a[i], p->b[i]) ? 0 : 1) |
-                         (deep_equal_status(p->a[i], p->b[i]) ? 0 : 2);
-                flags[i] = f;
-            }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < threads; t++) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-        sweeps++;
-        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    } while (el < min_seconds);
-    if (seconds) *seconds = el;
-    return sweeps;
+    return timed_sweeps(p->a.size(), threads, min_seconds, seconds, [&](int, size_t b, size_t e) {
+        for (size_t i = b; i < e; i++) {
+            uint8_t f;
+            if (p->err[i]) f = 7;
+            else f = (deep_equal_apart_from_status(p->a[i], p->b[i]) ? 0 : 1) |
+                     (deep_equal_status(p->a[i], p->b[i]) ? 0 : 2);
+            flags[i] = f;
+        }
+    });
 }
 
 }  // extern "C"
@@ -781,45 +766,32 @@ long oracle_upsert_body(void* h, size_t i, int mode, char* out, size_t cap) {
     return (long)o.size();
 }
 
-// the timed CPU baseline: every document's body, sweeps until min_seconds;
-// returns sweeps, *bytes = body bytes of one sweep
-int oracle_upsert_run(void* h, int mode, int threads, double min_seconds, double* seconds, uint64_t* bytes) {
+// the timed CPU baseline: every document's body, threads repeating their
+// slices until min_seconds; returns sweeps (fractional), *bytes = body bytes of
+// one sweep
+double oracle_upsert_run(void* h, int mode, int threads, double min_seconds, double* seconds, uint64_t* bytes) {
     Docs* p = (Docs*)h;
-    const size_t n = p->v.size();
     if (threads < 1) threads = 1;
     std::vector<uint64_t> tb(threads, 0);
-    int sweeps = 0;
-    auto t0 = std::chrono::steady_clock::now();
-    double el = 0;
-    do {
-        auto work = [&](int t) {
-            size_t b = n * t / threads, e = n * (t + 1) / threads;
-            uint64_t acc = 0;
-            std::string o;
-            for (size_t i = b; i < e; i++) {
-                if (p->err[i]) continue;
-                Value c = deep_copy(p->v[i]);
-                transform(c, mode);
-                o.clear();
-                marshal(o, c);
-                o.push_back('\n');
-                acc += o.size();
-            }
-            tb[t] = acc;
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < threads; t++) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-        sweeps++;
-        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    } while (el < min_seconds);
-    if (seconds) *seconds = el;
+    const double sw = timed_sweeps(p->v.size(), threads, min_seconds, seconds, [&](int t, size_t b, size_t e) {
+        uint64_t acc = 0;
+        std::string o;
+        for (size_t i = b; i < e; i++) {
+            if (p->err[i]) continue;
+            Value c = deep_copy(p->v[i]);
+            transform(c, mode);
+            o.clear();
+            marshal(o, c);
+            o.push_back('\n');
+            acc += o.size();
+        }
+        tb[t] = acc;
+    });
     if (bytes) {
         *bytes = 0;
         for (auto x : tb) *bytes += x;
     }
-    return sweeps;
+    return sw;
 }
 
 }  // extern "C"
