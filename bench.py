@@ -354,7 +354,7 @@ def main():
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_compare (K2)", "avg_launch_ms": k2_ms, "launches_per_step": launches,
+                         "kernel": "k_compare_flat (K2)", "avg_launch_ms": k2_ms, "launches_per_step": launches,
                          "bytes_def": "SURVEY.md 8(d) / BASELINE.md:52: sum over A,B of (24 L + V + 8) + O",
                          "bytes_per_launch": survey_bytes / launches,
                          "format": {"bytes_per_launch": fmt_bytes / launches, "achieved": achieved_fmt,

@@ -37,8 +37,8 @@ struct DiffBuffers {
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
-    uint32_t k2_variant;        // tuning: 0 default (NT loads, 4 chunks in flight per lane per object)
-    uint32_t k2_blocks_per_cu;  // tuning: 0 = 5 resident 256-thread blocks per CU
+    uint32_t k2_variant;        // tuning: 0 default = k_compare_flat, 4 x 16-B chunks in flight per lane per object
+    uint32_t k2_blocks_per_cu;  // tuning: 0 = the variant's occupancy (4 resident 256-thread blocks per CU)
 };
 
 // waves of a K2 launch over nchunks 64-pair chunks (sizes the wave arenas)

@@ -718,6 +718,184 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
     if (deferred && lane == 0) summary[6] = 1u;
 }
 
+// ---------------------------------------------------------------- K2, flattened stream
+// One wave per work item of P = 64 >> sub_shift consecutive pairs.  Lane k
+// loads pair k's 64-B row with four coalesced 16-B loads (one 4 KiB read per
+// item instead of a scalar row load per pair).  The item's compared segments
+// form one flattened index space of 16-B chunks (a wave prefix sum of the
+// per-pair chunk counts); each pass the wave issues U x 64 chunk loads of A
+// and of B with non-temporal 16-B loads, a chunk's owner pair found by a
+// cross-lane binary search over the prefix sums.  So the HBM stream never
+// waits at a pair boundary and no lane idles on a small pair (config3's pairs
+// average ~200 chunks a side: a wave-per-pair pass leaves 1/5 of its loads
+// unused and pays a row + data latency per pair).  A mismatching chunk marks
+// its pair (spec or status region); then the wave merge-joins its dirty pairs
+// one at a time into its arena, exactly as k_compare does (same flags, caps,
+// arena order and F_DEFER rule).
+template <int U, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
+                                                      const uint8_t* __restrict__ pool, uint32_t n,
+                                                      uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
+                                                      uint4* __restrict__ chunk_counts, uint32_t c_begin,
+                                                      uint32_t c_end, uint64_t* __restrict__ ah,
+                                                      uint8_t* __restrict__ ak, uint32_t arena_off,
+                                                      uint32_t arena_per_wave, uint32_t arena_stride,
+                                                      uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
+                                                      uint64_t mask, uint32_t* __restrict__ summary,
+                                                      uint32_t sub_shift) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t wbase = arena_off + wave * arena_stride;
+    uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
+    bool deferred = false;
+    const uint64_t sent0 = status_sentinel_hash(0, mask);
+    const uint32_t per = 64u >> sub_shift;
+    const uint32_t nitems = (c_end - c_begin) << sub_shift;
+    for (uint32_t it = wave; it < nitems; it += nwaves) {
+        const uint32_t c = c_begin + (it >> sub_shift);
+        const uint32_t p0 = (c << 6) + (it & ((1u << sub_shift) - 1u)) * per;
+        if (p0 >= n) continue;
+        const uint32_t cnt = min(per, n - p0);
+        const bool valid = lane < cnt;
+        // ---- rows: lane k holds pair p0 + k
+        u32x4 v0 = {0, 0, 0, 0}, v1 = v0, v2 = v0, v3 = v0;
+        if (valid) {
+            const u32x4* rp = (const u32x4*)(rows + p0 + lane);
+            v0 = rp[0];  // off_a, off_b
+            v1 = rp[1];  // spec_l_a, spec_l_b, spec_ar_a, spec_ar_b
+            v2 = rp[2];  // stat_l_a, stat_l_b, stat_ar_a, stat_ar_b
+            v3 = rp[3];  // flags_a, flags_b, pair_id, cluster_id
+        }
+        const uint64_t off_a = ((uint64_t)v0.y << 32) | v0.x, off_b = ((uint64_t)v0.w << 32) | v0.z;
+        const bool err = valid && ((v3.x | v3.y) & GPUDIFF_OBJ_DECODE_ERR) != 0u;
+        const bool ok = valid && !err;
+        const bool spec_sz = v1.x == v1.y && v1.z == v1.w;
+        const bool has_st_b = (v3.y & GPUDIFF_OBJ_HAS_STATUS) != 0u;
+        const bool stat_sz = has_st_b && v2.x == v2.y && v2.z == v2.w;
+        const uint32_t seg_a = (uint32_t)seg_bytes(v1.x, v1.z), seg_b = (uint32_t)seg_bytes(v1.y, v1.w);
+        const uint32_t n1 = (ok && spec_sz) ? seg_a >> 4 : 0u;
+        const uint32_t n2 = (ok && stat_sz) ? (uint32_t)(seg_bytes(v2.x, v2.z) >> 4) : 0u;
+        const uint32_t tot = n1 + n2;
+        const uint32_t incl = wave_incl_scan(tot);
+        const uint32_t total = uni(shfl32(incl, 63));
+        const uint32_t first = incl - tot;
+        // chunk k of a pair: spec chunk at off + 16k (k < n1), status chunk at off + seg + 16 (k - n1)
+        const uint32_t adj_a = seg_a - 16u * n1, adj_b = seg_b - 16u * n1;
+        uint64_t mis_s = 0, mis_t = 0;  // pairs with a differing spec / status chunk (wave-uniform)
+        for (uint32_t base = 0; base < total; base += 64u * U) {
+            u32x4 va[U], vb[U];
+            uint32_t own[U];
+            bool st[U], act[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t g = base + (uint32_t)u * 64u + lane;
+                act[u] = g < total;
+                uint32_t o = 0;  // owner = number of lanes whose inclusive prefix is <= g
+#pragma unroll
+                for (uint32_t s = 32; s >= 1; s >>= 1)
+                    if (shfl32(incl, o + s - 1u) <= g) o += s;
+                own[u] = o;
+                const uint32_t k = g - shfl32(first, o);
+                st[u] = k >= shfl32(n1, o);
+                const uint32_t xa = shfl32(adj_a, o), xb = shfl32(adj_b, o);
+                const uint64_t oa = shfl64(off_a, o), ob = shfl64(off_b, o);
+                const uint64_t rel = 16ull * k;
+                if (act[u]) {
+                    va[u] = __builtin_nontemporal_load((const u32x4*)(pool + oa + rel + (st[u] ? xa : 0u)));
+                    vb[u] = __builtin_nontemporal_load((const u32x4*)(pool + ob + rel + (st[u] ? xb : 0u)));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                uint64_t m = ballot(act[u] && neq16(va[u], vb[u]));
+                while (m) {  // differing chunks: only in dirty pairs
+                    const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint64_t bit = 1ull << (uint32_t)__builtin_amdgcn_readlane((int)own[u], (int)j);
+                    if (__builtin_amdgcn_readlane((int)(st[u] ? 1 : 0), (int)j)) mis_t |= bit;
+                    else mis_s |= bit;
+                }
+            }
+        }
+        // ---- decisions (compare_pair's rules)
+        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0;
+        if (err) {
+            myflag = F_SPEC | F_STATUS | F_ERR;
+        } else if (valid) {
+            const bool spec_dirty = !spec_sz || ((mis_s >> lane) & 1ull);
+            const bool stat_dirty = !stat_sz || ((mis_t >> lane) & 1ull);
+            const bool stat_join = stat_dirty && (v2.x + v2.y) != 0u;
+            myflag = (spec_dirty ? F_SPEC | F_JSPEC : 0u) | (stat_dirty ? F_STATUS : 0u) | (stat_join ? F_JSTAT : 0u) |
+                     (stat_dirty && !has_st_b ? F_SENT : 0u) | (((v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu) ? F_SEED : 0u);
+            mycap = (spec_dirty ? v1.x + v1.y : 0u) + (stat_dirty ? v2.x + v2.y + (has_st_b ? 0u : 1u) : 0u);
+        }
+        // ---- changed paths of the dirty pairs, in pair order, into this wave's arena
+        for (uint64_t dm = ballot((myflag & (F_SPEC | F_STATUS)) != 0u); dm; dm &= dm - 1) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(dm);
+            const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)myflag, (int)k);
+            const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
+            uint32_t src = 0, pc = 0;
+            bool defer = false;
+            if (used + ck <= arena_per_wave) {
+                src = wbase + used;
+                if (fk & (F_JSPEC | F_JSTAT)) {
+                    // the row again, as a scalar load (just read: an L2 hit), so the row registers are
+                    // dead during the join
+                    const gpudiff_pair_row r = rows[p0 + k];
+                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane);
+                } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
+                    if (lane == 0) {
+                        ah[src] = (fk & F_SEED) ? status_sentinel_hash((rows[p0 + k].flags_a >> GPUDIFF_OBJ_SEED_SHIFT) &
+                                                                       0xFFu, mask)
+                                                : sent0;
+                        ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                    }
+                    pc = 1;
+                }
+                used += pc;
+            } else {
+                defer = true;
+                deferred = true;
+            }
+            if (lane == k) {
+                if (defer) {
+                    myflag |= F_DEFER;
+                } else {
+                    mycap = 0;  // no K4 scratch slot needed
+                    mysrc = src;
+                    mycnt = pc;
+                }
+            }
+        }
+        const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
+        if (valid) {
+            flags[p0 + lane] = (uint8_t)myflag;
+            if (dirty) {
+                caps[p0 + lane] = mycap;
+                path_src[p0 + lane] = mysrc;
+                path_cnt[p0 + lane] = mycnt;
+            }
+        }
+        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
+        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
+        const uint32_t nd = popc64(ballot(dirty));
+        const uint32_t cs = wave_sum(dirty ? mycap : 0u);
+        if (lane == 0) {
+            if (!sub_shift) {
+                chunk_counts[c] = make_uint4(ns, nt, nd, cs);
+            } else if (ns | nt | nd | cs) {
+                uint32_t* cc = (uint32_t*)(chunk_counts + c);
+                atomicAdd(cc + 0, ns);
+                atomicAdd(cc + 1, nt);
+                atomicAdd(cc + 2, nd);
+                atomicAdd(cc + 3, cs);
+            }
+        }
+    }
+    if (deferred && lane == 0) summary[6] = 1u;
+}
+
 // ---------------------------------------------------------------- K6
 // Lane per dirty pair (most pairs have 1-3 paths); pairs with many paths
 // (list shifts in deep objects) are copied by the whole wave.
@@ -825,10 +1003,15 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
 }
 
 static uint32_t k2_cap_blocks(const DiffBuffers& b) {
-    // 5 resident 256-thread blocks per CU (20 waves/CU, the occupancy the fused
-    // kernel's 90 VGPRs allow): with joins inside K2 the extra waves keep HBM
-    // streaming while others join (tools/ab_k2.py: 11.18 vs 11.59 ms at 4)
-    return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : 5u);
+    // one resident 256-thread block per CU per wave slot of a SIMD: a grid
+    // larger than the occupancy would leave blocks waiting for a free slot
+    // (a tail).  k_compare: 90 VGPRs -> 5 waves/SIMD; with joins inside K2 the
+    // extra waves keep HBM streaming while others join (tools/ab_k2.py: 11.18
+    // vs 11.59 ms at 4).  k_compare_flat variants: their own occupancy.
+    static const uint8_t kFlatOcc[5] = {4, 4, 4, 5, 5};  // variants 8..12 (0 = 8)
+    const uint32_t v = b.k2_variant == 0 ? 8u : b.k2_variant;
+    const uint32_t occ = (v >= 8 && v <= 12) ? kFlatOcc[v - 8] : 5u;
+    return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : occ);
 }
 
 // 64-pair chunks split into 2^k items until there are >= 4 items per resident
@@ -866,7 +1049,13 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
         case 5: k_compare<true, 4, 6><<<grid, 256, 0, s>>>(K2ARGS); break;  // <= 80 VGPRs
         case 6: k_compare<true, 2, 8><<<grid, 256, 0, s>>>(K2ARGS); break;  // <= 64 VGPRs
         case 7: k_compare<true, 2, 6><<<grid, 256, 0, s>>>(K2ARGS); break;
-        default: k_compare<true, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 8: k_compare_flat<4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 9: k_compare_flat<2, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 10: k_compare_flat<4, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 11: k_compare_flat<2, 5><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 12: k_compare_flat<4, 5><<<grid, 256, 0, s>>>(K2ARGS); break;
+        case 13: k_compare<true, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;  // round 1's default
+        default: k_compare_flat<4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
     }
 #undef K2ARGS
     return hipGetLastError();

@@ -238,3 +238,17 @@ def test_submit_pipelining(eng):
     t2 = eng.submit(p2)
     assert_matches(eng.wait(t2), p2)
     assert_matches(eng.wait(t1), p1)
+
+
+@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13])
+def test_k2_variants_bit_exact(variant):
+    """Every decision-kernel variant (k_compare: wave per pair; k_compare_flat:
+    flattened chunk stream, several unrolls / occupancies) against the oracle on
+    mixed and deep populations, with joins in K2 and with deferred joins."""
+    pairs, _, _ = make_pairs(1200, seed=31, mutate_frac=0.3, pretty_frac=0)
+    deep, _, _ = make_pairs(120, seed=32, mix=(("crd", 1.0),), mutate_frac=0.5, crd_leaves=1500)
+    for shrink in (0, 12):
+        e = G.Engine(device=0, flags=(variant << 8) | (shrink << 21))
+        assert_matches(e.diff_pairs(pairs), pairs)
+        assert_matches(e.diff_pairs(deep), deep)
+        e.close()

@@ -53,12 +53,13 @@ def main():
         if "fetch_bytes_corrected" in k and "write_bytes" in k:
             k["hbm_bytes"] = k["fetch_bytes_corrected"] + k["write_bytes"]
         kernels[short(name)] = k
-    k2 = kernels.get("k_compare", {})
+    kname = "k_compare_flat" if "k_compare_flat" in kernels else "k_compare"
+    k2 = kernels.get(kname, {})
     rl = bench["roofline"]
     alg = rl["format"]["bytes_per_launch"] if "format" in rl else rl["bytes_per_launch"]
     summary = dict(
         workload=bench["config"]["workload"],
-        kernel="k_compare",
+        kernel=kname,
         k2_source_hash=rl.get("k2_source_hash"),
         algorithmic_bytes_per_launch=alg,
         survey_bytes_per_launch=rl.get("bytes_per_launch") if "format" in rl else None,
