@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=262144)
     ap.add_argument("--threads", type=int, default=0, help="host encode threads (default min(16, cpus))")
     ap.add_argument("--sample", type=int, default=600, help="pairs checked bit-exact vs the oracle (JSON path)")
-    ap.add_argument("--cpu-sample", type=int, default=20000, help="pairs in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=50000, help="pairs in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--json-in-pairs", type=int, default=131072,
@@ -415,17 +415,20 @@ def cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota):
     pairs = [pop.json_pair(int(i)) for i in idx]
     threads = aff
     dp = cpu_ref.DecodedPairs(pairs)
+    dp.decide(threads=threads)  # warm: first-touch page faults, thread start-up
     cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
     _, sweeps1, sec1 = dp.decide(threads=1, min_seconds=args.cpu_seconds / 3)
     hb = eng.encode(pairs)
     rows = hb.rows()
     csr = cpu_ref.CsrPairs(hb.pool(), rows)
+    csr.run(threads=threads)  # warm
     fcsr, csw, csec, _ = csr.run(threads=threads, min_seconds=args.cpu_seconds / 2)
     _, csw1, csec1, _ = csr.run(threads=1, min_seconds=args.cpu_seconds / 4)
     ref_rate, csr_rate = len(idx) * sweeps / sec, len(idx) * csw / csec
     cpu = dict(value=ref_rate, unit="pairs/s", cores=threads, kind="port",
-               sample="%d pairs (every %dth of this workload, JSON decoded untimed), %d sweeps in %.1f s; "
-                      "C++ tree-walk restatement of specsyncer.go:17-41 + statussyncer.go:15-27" % (
+               sample="%d pairs (every %dth of this workload, JSON decoded untimed), %.1f sweeps in %.1f s, "
+                      "threads rotating over slices; C++ tree-walk restatement of specsyncer.go:17-41 + "
+                      "statussyncer.go:15-27" % (
                           len(idx), max(1, n // len(idx)), sweeps, sec),
                one_core=len(idx) * sweeps1 / sec1, nproc=nproc, affinity_cpus=aff, cgroup_cpu_quota=quota,
                cpu_csr=dict(value=csr_rate, unit="pairs/s", cores=threads, one_core=len(idx) * csw1 / csec1,

@@ -1,8 +1,12 @@
 // Timed multi-thread sweeps for the oracle's CPU baselines (TEST
-// INFRASTRUCTURE / CPU BASELINE ONLY).  Threads are spawned once; thread t
-// repeats body(t, begin, end) over its slice [n t / T, n (t + 1) / T) until
-// min_seconds have passed (at least once).  Returns the items processed / n
-// (fractional sweeps); *seconds = wall time until the last thread finished.
+// INFRASTRUCTURE / CPU BASELINE ONLY).  The n items are cut into T slices
+// [n s / T, n (s + 1) / T); threads are spawned once and sweep until
+// min_seconds have passed (at least once), thread t taking slice (t + i) % T
+// in its i-th sweep -- so a thread never re-walks the slice its own caches
+// hold from the previous sweep (a small sample would otherwise be timed from
+// L1/L2).  body(s, begin, end) gets the slice index.  Returns the items
+// processed / n (fractional sweeps); *seconds = wall time until the last
+// thread finished.
 #pragma once
 #include <stddef.h>
 
@@ -23,9 +27,11 @@ double timed_sweeps(size_t n, int threads, double min_seconds, double* seconds, 
     std::vector<size_t> done(threads, 0);
     const auto t0 = std::chrono::steady_clock::now();
     auto run = [&](int t) {
-        const size_t b = n * t / threads, e = n * (t + 1) / threads;
+        size_t i = 0;
         do {
-            body(t, b, e);
+            const int sl = (int)((t + i++) % (size_t)threads);
+            const size_t b = n * sl / threads, e = n * (sl + 1) / threads;
+            body(sl, b, e);
             done[t] += e - b;
         } while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < min_seconds);
     };
