@@ -57,6 +57,15 @@ enum {
 #define GPUDIFF_SPEC_DIRTY 0x1u
 #define GPUDIFF_STATUS_DIRTY 0x2u
 #define GPUDIFF_DECODE_ERROR 0x4u
+/* write-path hints, set only on dirty pairs: the write the
+ * syncer issues for the decision would not change what the predicate compares, so the API call can
+ * be skipped.  GPUDIFF_SPEC_NOOP: every changed spec leaf is an int64 v on one side and a float64
+ * == v (|v| <= 2^53) on the other -- Go's json.Marshal writes both as the same digits and the API
+ * server decodes them back to int64 v, so A's body over B leaves B's compared content as it is.
+ * GPUDIFF_STATUS_NOOP: the same for the status leaves, and when B has no status key, A has none
+ * either (UpdateStatus would write nothing). */
+#define GPUDIFF_SPEC_NOOP 0x8u
+#define GPUDIFF_STATUS_NOOP 0x10u
 
 /* device encoder (K0) per-object status: 0 = encoded on the device; otherwise
  * the reason the object was handed to the host encoder (the Go-exact path) */
@@ -369,6 +378,30 @@ typedef struct gpudiff_bodies {
 int gpudiff_upsert_bodies(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, size_t n, uint32_t mode,
                           gpudiff_bodies* out);
 void gpudiff_bodies_release(gpudiff_ctx* ctx, gpudiff_bodies* b);
+
+/* Gate -> write on the device.  For a
+ * batch submitted with GPUDIFF_OPT_DEVICE_ENCODE and waited (gpudiff_wait), the
+ * writes the syncer issues for its decisions, rendered by K10 from the pairs'
+ * JSON still staged in HBM -- no re-upload:
+ *   every spec-dirty pair: upsertIntoDownstream's body of A (GPUDIFF_UPSERT_SPEC,
+ *     pkg/syncer/specsyncer.go:86-132), written over the downstream copy B;
+ *   every status-dirty pair: updateStatusInUpstream's body of B
+ *     (GPUDIFF_UPSERT_STATUS, statussyncer.go:41-63), written into A.
+ * A write whose pair carries GPUDIFF_SPEC_NOOP / GPUDIFF_STATUS_NOOP is listed
+ * with noop = 1 and no body: the call can be skipped.  Call after gpudiff_wait
+ * on the ticket and before the submit after the next one (the staging is
+ * reused then); GPUDIFF_E_STATE otherwise, or for a batch the context encoded
+ * on the host.  Release with gpudiff_write_plan_release. */
+typedef struct gpudiff_write_plan {
+    size_t n;                    /* writes: the spec-dirty pairs (ascending index), then the status-dirty ones */
+    const uint32_t* pair_index;  /* the pair's index in the submitted batch */
+    const uint8_t* kind;         /* GPUDIFF_UPSERT_SPEC / GPUDIFF_UPSERT_STATUS */
+    const uint8_t* noop;         /* 1 = skip the call (no body) */
+    gpudiff_bodies bodies;       /* n bodies (empty for no-op writes; status GPUDIFF_E_DECODE = undecodable) */
+    void* internal;
+} gpudiff_write_plan;
+int gpudiff_write_plan_get(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_write_plan* out);
+void gpudiff_write_plan_release(gpudiff_ctx* ctx, gpudiff_write_plan* p);
 
 /* The staged form: documents uploaded once into HBM (gpudiff_wbatch_create),
  * K10 launched on the context's stream (gpudiff_wbatch_run, asynchronous; with

@@ -85,6 +85,8 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.tile_sums = d->tile_sums;
     b.path_src = d->path_src;
     b.path_cnt = d->path_cnt;
+    b.nbits = d->nbits;
+    b.noop_d = d->noop_d;
     b.arena_h = d->arena_h;
     b.arena_k = d->arena_k;
     b.arena_per_wave = kArenaPerWave >> ((c->flags >> GPUDIFF_OPT_ARENA_SHIFT) & 0xFu);
@@ -382,7 +384,8 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
         (rc = dalloc(&d->summary, 8)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
         (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
-        (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) ||
+        (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) || (rc = dalloc(&d->nbits, np)) ||
+        (rc = dalloc(&d->noop_d, np)) ||
         (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments))) {
         d->chunk_counts = cc;
         dfree_all(d.get());
@@ -735,6 +738,18 @@ int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rsr) {
     }
     if (d->n_pairs) HIPCHK(hipMemcpy(rs->flags.data(), d->flags, d->n_pairs, hipMemcpyDeviceToHost));
     for (uint8_t& f : rs->flags) f &= (uint8_t)(GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY | GPUDIFF_DECODE_ERROR);
+    if (sum[2]) {  // the write-path no-op bits of the dirty pairs (K2 / K4 via K3), by pair index
+        std::vector<uint32_t> idx(sum[2]);
+        std::vector<uint8_t> nb(sum[2]);
+        HIPCHK(hipMemcpy(idx.data(), d->dirty_idx, sum[2] * 4ull, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(nb.data(), d->noop_d, sum[2], hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < sum[2]; k++) {
+            uint8_t& f = rs->flags[idx[k]];
+            if (f & GPUDIFF_DECODE_ERROR) continue;
+            if ((nb[k] & 1u) && (f & GPUDIFF_SPEC_DIRTY)) f |= GPUDIFF_SPEC_NOOP;
+            if ((nb[k] & 2u) && (f & GPUDIFF_STATUS_DIRTY)) f |= GPUDIFF_STATUS_NOOP;
+        }
+    }
     if (sum[0]) HIPCHK(hipMemcpy(rs->spec.data(), d->spec_ids, sum[0] * 4ull, hipMemcpyDeviceToHost));
     if (sum[1]) HIPCHK(hipMemcpy(rs->status.data(), d->status_ids, sum[1] * 4ull, hipMemcpyDeviceToHost));
     if (sum[2]) HIPCHK(hipMemcpy(rs->dirty.data(), d->dirty_ids, sum[2] * 4ull, hipMemcpyDeviceToHost));

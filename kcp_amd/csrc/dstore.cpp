@@ -62,6 +62,8 @@ struct Ring {
     bool k0_recorded = false;
     hipEvent_t t_ev[5] = {};      // GPUDIFF_OPT_TIMING: H2D begin/end (copy stream), K0 begin/end, K0c+K0x end
     std::vector<gpudiff_event> events;
+    std::vector<uint8_t> final_flags;  // the waited batch's result flags (deferred events resolved)
+    bool waited = false;
     uint32_t batch = 0, nev = 0;
     uint64_t bound = 0;
     gpudiff_ticket ticket = 0;
@@ -700,6 +702,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         return rc;
     }
     R.events.assign(ev, ev + n);
+    R.waited = false;
     R.batch = batch;
     R.nev = (uint32_t)n;
     R.bound = bound;
@@ -730,6 +733,10 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         }
         int r2 = ndef ? resolve(s, RR, rs) : GPUDIFF_OK;
         if (r2) s->broken = true;
+        if (!r2 && s->pair_mode) {  // kept for gpudiff_write_plan_get
+            RR.final_flags.assign(rs.flags.begin(), rs.flags.end());
+            RR.waited = true;
+        }
         // forgets older than every outstanding batch are settled
         for (auto it = s->forgotten.begin(); it != s->forgotten.end();)
             it = it->second < s->next_wait ? s->forgotten.erase(it) : std::next(it);
@@ -831,4 +838,35 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
                     (void*)s->res_err})
         if (p) (void)hipFree(p);
     delete s;
+}
+
+int dstore_staged_pairs(gpudiff_ctx* c, gpudiff_ticket t, StagedPairs* out) {
+    DStore* s = c->pair_store;
+    if (!s || !t) return GPUDIFF_E_STATE;
+    for (Ring& R : s->ring) {
+        if (R.ticket != t) continue;
+        if (!R.waited || R.outstanding) return GPUDIFF_E_STATE;  // gpudiff_wait first
+        const uint64_t max_docs = 2 * (uint64_t)R.nev;
+        (void)max_docs;
+        out->hdocs = (const TokDoc*)R.hmeta;
+        out->djson = R.djson;
+        out->hjson = R.hjson;
+        out->n = R.nev;
+        out->flags = &R.final_flags;
+        out->events = &R.events;
+        return GPUDIFF_OK;
+    }
+    return GPUDIFF_E_STATE;  // not a device-encoded batch, or its staging was reused
+}
+
+int dstore_staged_mark_read(gpudiff_ctx* c, gpudiff_ticket t) {
+    DStore* s = c->pair_store;
+    if (!s) return GPUDIFF_E_STATE;
+    for (Ring& R : s->ring)
+        if (R.ticket == t) {
+            HIPCHK(hipEventRecord(R.k0_done, c->stream));
+            R.k0_recorded = true;
+            return GPUDIFF_OK;
+        }
+    return GPUDIFF_E_STATE;
 }

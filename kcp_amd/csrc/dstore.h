@@ -1,6 +1,7 @@
 // Device-encode mode of the object store (dstore.cpp); internal.
 #pragma once
 #include "engine.h"
+#include "tokenize.h"
 
 struct DStore;
 
@@ -12,3 +13,19 @@ int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot);
 int dstore_submit_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpudiff_ticket* ticket);
 int dstore_stats(const DStore* s, gpudiff_store_stats* out);
 void dstore_free(gpudiff_ctx* c, DStore* s);
+
+// The staged JSON of a waited pair-mode batch (gpudiff_submit with GPUDIFF_OPT_DEVICE_ENCODE): pair i's
+// old object is document 2i, its new one 2i + 1; hdocs[] holds their offsets into djson (HBM) and hjson
+// (pinned host copy); flags = the batch's final result flags (host-deferred pairs resolved).  Valid until
+// the ring slot is reused by the submit after the next one.
+struct StagedPairs {
+    const gd::TokDoc* hdocs = nullptr;
+    const uint8_t* djson = nullptr;
+    const uint8_t* hjson = nullptr;
+    uint32_t n = 0;
+    const std::vector<uint8_t>* flags = nullptr;
+    const std::vector<gpudiff_event>* events = nullptr;
+};
+int dstore_staged_pairs(gpudiff_ctx* c, gpudiff_ticket t, StagedPairs* out);
+// work launched on the context stream now reads the batch's device JSON: the ring slot's next upload waits
+int dstore_staged_mark_read(gpudiff_ctx* c, gpudiff_ticket t);

@@ -79,6 +79,8 @@ struct gpudiff_dbatch {
     uint4* seg_tot = nullptr;  // running totals after each diff segment
     uint32_t* path_src = nullptr;
     uint32_t* path_cnt = nullptr;
+    uint8_t* nbits = nullptr;   // per pair: no-op bits of K2's joins
+    uint8_t* noop_d = nullptr;  // per dirty pair: no-op bits
     uint64_t arena_cap = 0;
     uint64_t* arena_h = nullptr;
     uint8_t* arena_k = nullptr;
@@ -155,7 +157,7 @@ inline void dfree_all(gpudiff_dbatch* d) {
     void* ps[] = {d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
                   d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
-                  d->scratch_h, d->scratch_k, d->out_h, d->out_k};
+                  d->scratch_h, d->scratch_k, d->out_h, d->out_k, d->nbits, d->noop_d};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);

@@ -18,6 +18,8 @@ struct DiffBuffers {
     uint32_t* caps;
     uint32_t* path_src;   // per pair: arena index of the paths K2 wrote
     uint32_t* path_cnt;   // per pair: number of those paths
+    uint8_t* nbits;       // per pair: write-path no-op bits K2 computed (NOOP_SPEC | NOOP_STATUS)
+    uint8_t* noop_d;      // per dirty pair (dirty order): the no-op bits (K3 copies K2's, K4 writes its own)
     void* chunk_counts;   // uint4 per 64 pairs
     uint32_t* summary;
     uint32_t* spec_ids;

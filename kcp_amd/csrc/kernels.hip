@@ -353,7 +353,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                                                  uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off,
                                                  uint32_t c_begin, uint32_t c_end, const uint32_t* __restrict__ path_src,
                                                  const uint32_t* __restrict__ path_cnt,
-                                                 uint32_t* __restrict__ path_count) {
+                                                 uint32_t* __restrict__ path_count, const uint8_t* __restrict__ nbits,
+                                                 uint8_t* __restrict__ noop_d) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -377,9 +378,10 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
             dirty_idx[d] = p;
             if (f & F_DEFER) {  // K4 joins it into its scratch slot and writes the count
                 scratch_off[d] = base.w + cincl - cap;
-            } else {            // K2 already wrote its paths into a wave arena
+            } else {            // K2 already wrote its paths into a wave arena (and the no-op bits)
                 scratch_off[d] = path_src[p] | ARENA_BIT;
                 path_count[d] = path_cnt[p];
+                noop_d[d] = nbits[p];
             }
         }
     }
@@ -468,13 +470,29 @@ __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a
     return (bad >> lane) & 1ull;
 }
 
+// A changed leaf whose two values Go's json.Marshal writes as the same text
+// and the API server decodes back to the same int64 (the write-path no-op rule,
+// DESIGN.md §4g): an int64 v on one side, a float64 f == v on the other,
+// |v| <= 2^53 (canonical values: int64 / float64 bits, -0.0 stored as +0.0).
+__device__ __forceinline__ bool wire_equal_number(uint32_t ma, uint64_t xa, uint32_t mb, uint64_t xb) {
+    const uint32_t ta = ma & 7u, tb = mb & 7u;
+    if (!((ta == GPUDIFF_TAG_INT && tb == GPUDIFF_TAG_FLOAT) || (ta == GPUDIFF_TAG_FLOAT && tb == GPUDIFF_TAG_INT)))
+        return false;
+    const int64_t v = (int64_t)(ta == GPUDIFF_TAG_INT ? xa : xb);
+    const double f = __longlong_as_double((long long)(ta == GPUDIFF_TAG_INT ? xb : xa));
+    const int64_t lim = 1ll << 53;
+    return v >= -lim && v <= lim && (double)v == f;
+}
+
 // Merge-join of one region; returns the number of paths emitted.  Emission
-// order = ascending key (the union of both sorted key lists).
+// order = ascending key (the union of both sorted key lists).  *weq_all: every
+// emitted path is a CHANGED leaf with wire_equal_number values (wave-uniform).
 template <bool EMIT>
 __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_t region_bit,
                                 uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
-                                uint32_t lane) {
+                                uint32_t lane, bool* weq_all) {
     uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
+    bool weq = true;
     const uint64_t lt = mask_lt(lane);
     while (ia < A.L || ib < B.L) {
         const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
@@ -515,6 +533,7 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         const bool emitA = inA && (!matchA || differ);
         const bool emitB = inB && !matchB;
         const uint64_t balA = ballot(emitA), balB = ballot(emitB);
+        if (ballot((emitA && !(matchA && wire_equal_number(ma, xa, mbj, xbj))) || emitB)) weq = false;
         if (EMIT) {
             if (emitA) {
                 const uint32_t pos = popc64(balA & lt) + popc64(balB & mask_lt(jA));
@@ -534,6 +553,7 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         ia += ca;
         ib += cb;
     }
+    *weq_all = weq;
     return outpos;
 }
 
@@ -548,20 +568,33 @@ __device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
     return xavalanche(h) & mask;
 }
 
+// The write-path no-op bits of a dirty pair: bit 0 = the spec
+// write (A's body over B) changes nothing deepEqualApartFromStatus compares
+// (every changed spec leaf is a wire_equal_number change); bit 1 = the status
+// write (B's status into A) changes nothing (every changed status leaf is one,
+// and when B has no status key, A has none either).
+constexpr uint32_t NOOP_SPEC = 1u, NOOP_STATUS = 2u;
+__device__ __forceinline__ uint32_t sentinel_noop_bits(uint32_t flags_a) {
+    return (flags_a & GPUDIFF_OBJ_HAS_STATUS) ? 0u : NOOP_STATUS;
+}
+
 template <bool EMIT>
 __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
-                              uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane) {
+                              uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane, uint32_t* noop) {
     uint32_t n = 0;
+    bool spec_weq = true, stat_weq = true;
     if (f & F_JSPEC) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
-        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane);
+        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
     }
     if (f & F_JSTAT) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
-        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane);
+        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
     }
+    const bool stat_ok = stat_weq && (!(f & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
+    *noop = (((f & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) | (((f & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u);
     if (f & F_SENT) {
         if (EMIT && lane == 0) {
             out_h[base + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
@@ -585,7 +618,8 @@ __global__ __launch_bounds__(256, 6) void k_join(const gpudiff_pair_row* __restr
                                               const uint32_t* __restrict__ scratch_off, uint32_t* __restrict__ summary,
                                               const uint4* __restrict__ tot_before, const uint4* __restrict__ tot_after,
                                               uint64_t scratch_cap, uint64_t mask, uint64_t* __restrict__ sh,
-                                              uint8_t* __restrict__ sk, uint32_t* __restrict__ path_count) {
+                                              uint8_t* __restrict__ sk, uint32_t* __restrict__ path_count,
+                                              uint8_t* __restrict__ noop_d) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -613,10 +647,13 @@ __global__ __launch_bounds__(256, 6) void k_join(const gpudiff_pair_row* __restr
             (void)pk;
             const gpudiff_pair_row r = rnext;
             if (m) rnext = rows[uni(shfl32(p, (uint32_t)__builtin_ctzll(m)))];  // prefetch the next join's row
-            uint32_t n;
-            if (fits) n = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane);
-            else n = join_pair<false>(r, fk, pool, mask, sh, sk, 0, lane);
-            if (lane == 0) path_count[d_begin + (c << 6) + k] = n;
+            uint32_t n, nb = 0;
+            if (fits) n = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
+            else n = join_pair<false>(r, fk, pool, mask, sh, sk, 0, lane, &nb);
+            if (lane == 0) {
+                path_count[d_begin + (c << 6) + k] = n;
+                noop_d[d_begin + (c << 6) + k] = (uint8_t)nb;
+            }
         }
     }
 }
@@ -637,8 +674,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                                                  uint32_t c_end, uint64_t* __restrict__ ah, uint8_t* __restrict__ ak,
                                                  uint32_t arena_off, uint32_t arena_per_wave, uint32_t arena_stride,
                                                  uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
-                                                 uint64_t mask, uint32_t* __restrict__ summary,
-                                                 uint32_t sub_shift) {
+                                                 uint8_t* __restrict__ nbits, uint64_t mask,
+                                                 uint32_t* __restrict__ summary, uint32_t sub_shift) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -655,17 +692,18 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
         const uint32_t p0 = (c << 6) + (it & ((1u << sub_shift) - 1u)) * per;
         if (p0 >= n) continue;
         const uint32_t cnt = min(per, n - p0);
-        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0;
+        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0, mynoop = 0;
         for (uint32_t k = 0; k < cnt; k++) {
             const gpudiff_pair_row r = rows[p0 + k];
             PairDecision d = compare_pair<NT, U>(r, pool, lane);
-            uint32_t src = 0, pc = 0;
+            uint32_t src = 0, pc = 0, nb = 0;
             if (d.flag & (F_SPEC | F_STATUS)) {
                 if (used + d.cap <= arena_per_wave) {
                     src = wbase + used;
                     if (d.flag & (F_JSPEC | F_JSTAT)) {
-                        pc = join_pair<true>(r, d.flag, pool, mask, ah, ak, src, lane);
+                        pc = join_pair<true>(r, d.flag, pool, mask, ah, ak, src, lane, &nb);
                     } else if (d.flag & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
+                        nb = sentinel_noop_bits(r.flags_a);
                         if (lane == 0) {
                             ah[src] = (d.flag & F_SEED)
                                           ? status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
@@ -686,6 +724,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                 mycap = d.cap;
                 mysrc = src;
                 mycnt = pc;
+                mynoop = nb;
             }
         }
         const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
@@ -695,6 +734,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                 caps[p0 + lane] = mycap;
                 path_src[p0 + lane] = mysrc;
                 path_cnt[p0 + lane] = mycnt;
+                nbits[p0 + lane] = (uint8_t)mynoop;
             }
         }
         const uint32_t ns = popc64(ballot(myflag & F_SPEC));
@@ -741,8 +781,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                                                       uint8_t* __restrict__ ak, uint32_t arena_off,
                                                       uint32_t arena_per_wave, uint32_t arena_stride,
                                                       uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
-                                                      uint64_t mask, uint32_t* __restrict__ summary,
-                                                      uint32_t sub_shift) {
+                                                      uint8_t* __restrict__ nbits, uint64_t mask,
+                                                      uint32_t* __restrict__ summary, uint32_t sub_shift) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -819,7 +859,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             }
         }
         // ---- decisions (compare_pair's rules)
-        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0;
+        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0, mynoop = 0;
         if (err) {
             myflag = F_SPEC | F_STATUS | F_ERR;
         } else if (valid) {
@@ -835,7 +875,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             const uint32_t k = (uint32_t)__builtin_ctzll(dm);
             const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)myflag, (int)k);
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
-            uint32_t src = 0, pc = 0;
+            uint32_t src = 0, pc = 0, nb = 0;
             bool defer = false;
             if (used + ck <= arena_per_wave) {
                 src = wbase + used;
@@ -843,11 +883,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
                     // dead during the join
                     const gpudiff_pair_row r = rows[p0 + k];
-                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane);
+                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
+                    const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
+                    nb = sentinel_noop_bits(fa);
                     if (lane == 0) {
-                        ah[src] = (fk & F_SEED) ? status_sentinel_hash((rows[p0 + k].flags_a >> GPUDIFF_OBJ_SEED_SHIFT) &
-                                                                       0xFFu, mask)
+                        ah[src] = (fk & F_SEED) ? status_sentinel_hash((fa >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
                                                 : sent0;
                         ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
                     }
@@ -865,6 +906,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     mycap = 0;  // no K4 scratch slot needed
                     mysrc = src;
                     mycnt = pc;
+                    mynoop = nb;
                 }
             }
         }
@@ -875,6 +917,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 caps[p0 + lane] = mycap;
                 path_src[p0 + lane] = mysrc;
                 path_cnt[p0 + lane] = mycnt;
+                nbits[p0 + lane] = (uint8_t)mynoop;
             }
         }
         const uint32_t ns = popc64(ballot(myflag & F_SPEC));
@@ -1040,7 +1083,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
-               b.arena_per_wave, b.path_src, b.path_cnt, b.hash_mask, b.summary, sub
+               b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, sub
     switch (b.k2_variant) {  // tuning variants (GPUDIFF_OPT_K2_VARIANT_SHIFT); 0 is the default
         case 1: k_compare<false, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
         case 2: k_compare<true, 8, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
@@ -1074,7 +1117,7 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     k_compact<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
                                                            (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
                                                            b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1,
-                                                           b.path_src, b.path_cnt, b.path_count);
+                                                           b.path_src, b.path_cnt, b.path_count, b.nbits, b.noop_d);
     return hipGetLastError();
 }
 
@@ -1082,7 +1125,7 @@ hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_
                        const uint4* after) {
     k_join<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off,
                                                               b.summary, before, after, b.scratch_cap, b.hash_mask,
-                                                              b.scratch_h, b.scratch_k, b.path_count);
+                                                              b.scratch_h, b.scratch_k, b.path_count, b.noop_d);
     return hipGetLastError();
 }
 

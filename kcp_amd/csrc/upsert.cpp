@@ -24,6 +24,7 @@
 #include <thread>
 #include <vector>
 
+#include "dstore.h"
 #include "engine.h"
 #include "json.h"
 #include "tokenize.h"
@@ -544,6 +545,152 @@ void gpudiff_bodies_release(gpudiff_ctx*, gpudiff_bodies* b) {
     if (!b) return;
     delete (BodiesStore*)b->internal;
     memset(b, 0, sizeof(*b));
+}
+
+// ------------------------------------------------------------------ gate -> write on the device
+struct PlanStore {
+    std::vector<uint32_t> pair_index;
+    std::vector<uint8_t> kind, noop;
+};
+
+int gpudiff_write_plan_get(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_write_plan* out) {
+    if (!c || !out) return GPUDIFF_E_INVAL;
+    memset(out, 0, sizeof(*out));
+    int rc = set_device(c);
+    if (rc) return rc;
+    StagedPairs sp;
+    if ((rc = dstore_staged_pairs(c, ticket, &sp))) return rc;
+    const std::vector<uint8_t>& fl = *sp.flags;
+    std::unique_ptr<PlanStore> ps(new (std::nothrow) PlanStore());
+    if (!ps) return GPUDIFF_E_NOMEM;
+    // the writes: spec-dirty pairs (A's body to downstream), then status-dirty pairs (B's body to upstream)
+    for (uint32_t kind = GPUDIFF_UPSERT_SPEC; kind <= GPUDIFF_UPSERT_STATUS; kind++) {
+        const uint8_t dirty = kind == GPUDIFF_UPSERT_SPEC ? GPUDIFF_SPEC_DIRTY : GPUDIFF_STATUS_DIRTY;
+        const uint8_t noop = kind == GPUDIFF_UPSERT_SPEC ? GPUDIFF_SPEC_NOOP : GPUDIFF_STATUS_NOOP;
+        for (uint32_t p = 0; p < sp.n; p++)
+            if (fl[p] & dirty) {
+                ps->pair_index.push_back(p);
+                ps->kind.push_back((uint8_t)kind);
+                ps->noop.push_back((fl[p] & noop) ? 1 : 0);
+            }
+    }
+    const size_t nw = ps->pair_index.size();
+    // K10 documents: the staged document of every write that is not a no-op, read where K0 read it (HBM)
+    std::vector<TokDoc> docs;
+    std::vector<uint32_t> wdoc(nw, UINT32_MAX);
+    uint32_t n_spec_docs = 0;
+    uint64_t sb = 0, ob = 0;
+    for (size_t w = 0; w < nw; w++) {
+        if (ps->noop[w]) continue;
+        const uint32_t di = 2 * ps->pair_index[w] + (ps->kind[w] == GPUDIFF_UPSERT_SPEC ? 0u : 1u);
+        TokDoc t = sp.hdocs[di];
+        t.seed = 0;
+        t.scratch_off = sb;
+        t.pad[0] = (uint32_t)ob;
+        t.pad[1] = (uint32_t)(ob >> 32);
+        sb += marshal_scratch_bytes(t.json_len);
+        ob += marshal_out_cap(t.json_len);
+        wdoc[w] = (uint32_t)docs.size();
+        docs.push_back(t);
+        if (ps->kind[w] == GPUDIFF_UPSERT_SPEC) n_spec_docs++;
+    }
+    const size_t nd = docs.size();
+    void *d_docs = nullptr, *d_scratch = nullptr, *d_out = nullptr, *d_res = nullptr;
+    auto cleanup = [&]() {
+        for (void* p : {d_docs, d_scratch, d_out, d_res})
+            if (p) (void)hipFree(p);
+    };
+    std::vector<TokOut> to(nd);
+    std::vector<uint8_t> raw(ob);
+    if (nd) {
+        hipError_t e;
+        if ((e = hipMalloc(&d_docs, nd * sizeof(TokDoc))) != hipSuccess ||
+            (e = hipMalloc(&d_scratch, std::max<uint64_t>(sb, 256))) != hipSuccess ||
+            (e = hipMalloc(&d_out, std::max<uint64_t>(ob, 256))) != hipSuccess ||
+            (e = hipMalloc(&d_res, nd * sizeof(TokOut))) != hipSuccess) {
+            cleanup();
+            return e == hipErrorOutOfMemory ? GPUDIFF_E_CAPACITY : GPUDIFF_E_DEVICE;
+        }
+        const uint32_t var = (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u;
+        hipError_t le = hipMemcpyAsync(d_docs, docs.data(), nd * sizeof(TokDoc), hipMemcpyHostToDevice, c->stream);
+        if (le == hipSuccess && n_spec_docs)
+            le = launch_marshal_docs(c->stream, (const TokDoc*)d_docs, n_spec_docs, sp.djson, (uint8_t*)d_scratch,
+                                     (uint8_t*)d_out, GPUDIFF_UPSERT_SPEC, (TokOut*)d_res, var);
+        if (le == hipSuccess && nd > n_spec_docs)
+            le = launch_marshal_docs(c->stream, (const TokDoc*)d_docs + n_spec_docs, (uint32_t)(nd - n_spec_docs),
+                                     sp.djson, (uint8_t*)d_scratch, (uint8_t*)d_out, GPUDIFF_UPSERT_STATUS,
+                                     (TokOut*)d_res + n_spec_docs, var);
+        if (le == hipSuccess && (rc = dstore_staged_mark_read(c, ticket))) le = hipErrorUnknown;
+        if (le == hipSuccess) le = hipMemcpyAsync(to.data(), d_res, nd * sizeof(TokOut), hipMemcpyDeviceToHost, c->stream);
+        if (le == hipSuccess) le = hipMemcpyAsync(raw.data(), d_out, ob, hipMemcpyDeviceToHost, c->stream);
+        if (le == hipSuccess) le = hipStreamSynchronize(c->stream);
+        cleanup();
+        if (le != hipSuccess) {
+            gd::g_last_hip_error = hipGetErrorString(le);
+            return GPUDIFF_E_DEVICE;
+        }
+    }
+    // K10's deferrals: the host path over the pinned host copy of the same staged JSON
+    std::vector<uint32_t> def;
+    for (size_t k = 0; k < nd; k++)
+        if (to[k].status != GPUDIFF_TOK_OK) def.push_back((uint32_t)k);
+    std::vector<std::string> hb(def.size());
+    std::vector<uint8_t> hok(def.size(), 0);
+    const uint32_t mode_split = n_spec_docs;
+    {
+        const uint32_t T = std::max<uint32_t>(1, std::min<uint32_t>(c->threads, (uint32_t)((def.size() + 63) / 64)));
+        auto work = [&](uint32_t t) {
+            for (size_t k = t; k < def.size(); k += T) {
+                const TokDoc& d = docs[def[k]];
+                hok[k] = host_body(sp.hjson + d.json_off, d.json_len,
+                                   def[k] < mode_split ? GPUDIFF_UPSERT_SPEC : GPUDIFF_UPSERT_STATUS, hb[k])
+                             ? 1
+                             : 0;
+            }
+        };
+        std::vector<std::thread> th;
+        for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+    }
+    std::vector<int32_t> hidx(nd, -1);
+    for (size_t k = 0; k < def.size(); k++) hidx[def[k]] = (int32_t)k;
+    BodiesStore* bs = new (std::nothrow) BodiesStore();
+    if (!bs) return GPUDIFF_E_NOMEM;
+    bs->offsets.resize(nw + 1);
+    bs->status.assign(nw, 0);
+    bs->k10.assign(nw, GPUDIFF_TOK_OK);
+    bs->source.assign(nw, GPUDIFF_BODY_DEVICE);
+    for (size_t w = 0; w < nw; w++) {
+        bs->offsets[w] = bs->bytes.size();
+        if (wdoc[w] == UINT32_MAX) continue;  // no-op write: no body
+        const uint32_t k = wdoc[w];
+        bs->k10[w] = (int32_t)to[k].status;
+        if (to[k].status == GPUDIFF_TOK_OK) {
+            const uint8_t* p = raw.data() + to[k].off;
+            bs->bytes.insert(bs->bytes.end(), p, p + to[k].bytes);
+        } else {
+            bs->source[w] = GPUDIFF_BODY_HOST;
+            const int32_t h = hidx[k];
+            if (hok[h]) bs->bytes.insert(bs->bytes.end(), hb[h].begin(), hb[h].end());
+            else bs->status[w] = GPUDIFF_E_DECODE;
+        }
+    }
+    bs->offsets[nw] = bs->bytes.size();
+    publish(bs, &out->bodies, nw, def.size());
+    out->n = nw;
+    out->pair_index = ps->pair_index.data();
+    out->kind = ps->kind.data();
+    out->noop = ps->noop.data();
+    out->internal = ps.release();
+    return GPUDIFF_OK;
+}
+
+void gpudiff_write_plan_release(gpudiff_ctx* c, gpudiff_write_plan* p) {
+    if (!p) return;
+    gpudiff_bodies_release(c, &p->bodies);
+    delete (PlanStore*)p->internal;
+    memset(p, 0, sizeof(*p));
 }
 
 }  // extern "C"

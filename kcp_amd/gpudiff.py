@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(_HERE, "libgpudiff.so")
 OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUND = range(-1, -9, -1)
 
-SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR = 0x1, 0x2, 0x4
+SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR, SPEC_NOOP, STATUS_NOOP = 0x1, 0x2, 0x4, 0x8, 0x10
 PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
 OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
@@ -124,6 +124,11 @@ class Bodies(C.Structure):
                 ("internal", C.c_void_p)]
 
 
+class WritePlanC(C.Structure):
+    _fields_ = [("n", C.c_size_t), ("pair_index", C.c_void_p), ("kind", C.c_void_p), ("noop", C.c_void_p),
+                ("bodies", Bodies), ("internal", C.c_void_p)]
+
+
 class WBatchStats(C.Structure):
     _fields_ = [("n_docs", C.c_uint64), ("json_bytes", C.c_uint64), ("body_bytes", C.c_uint64),
                 ("scratch_bytes", C.c_uint64), ("out_cap_bytes", C.c_uint64), ("k10_ms", C.c_double),
@@ -225,6 +230,8 @@ SIGNATURES = [
     ("gpudiff_upsert_bodies", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
                                         C.POINTER(Bodies)]),
     ("gpudiff_bodies_release", None, [_P, C.POINTER(Bodies)]),
+    ("gpudiff_write_plan_get", C.c_int, [_P, C.c_uint64, C.POINTER(WritePlanC)]),
+    ("gpudiff_write_plan_release", None, [_P, C.POINTER(WritePlanC)]),
     ("gpudiff_wbatch_create", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
                                         C.POINTER(_P)]),
     ("gpudiff_wbatch_run", C.c_int, [_P, _P]),
@@ -542,6 +549,7 @@ class Engine:
     def wait(self, ticket: int) -> DiffResult:
         r = Result()
         _chk(_lib.gpudiff_wait(self.ctx, ticket, C.byref(r)), "gpudiff_wait")
+        self.__dict__.get("_held", {}).pop(ticket, None)
         try:
             out = DiffResult(
                 pair_flags=_arr(r.pair_flags, r.n_pairs, np.uint8),
@@ -570,7 +578,17 @@ class Engine:
         arr, n, keep = self._pairs(pairs, ids, clusters)
         t = C.c_uint64()
         _chk(_lib.gpudiff_submit(self.ctx, arr, n, C.byref(t)), "gpudiff_submit")
+        self._hold(t.value, (arr, keep))
         return t.value
+
+    def _hold(self, ticket, bufs):
+        """The caller owns a submit's inputs until gpudiff_wait (the device-encode
+        path re-reads deferred pairs there): keep them alive per ticket; the
+        submit ring holds at most two batches, older tickets are dropped."""
+        held = self.__dict__.setdefault("_held", {})
+        held[ticket] = bufs
+        for t in sorted(held)[:-2]:
+            del held[t]
 
     def submit_array(self, arr: np.ndarray) -> int:
         """gpudiff_submit over a JSON_PAIR_DTYPE table (json_pair_array)."""
@@ -579,6 +597,25 @@ class Engine:
         _chk(_lib.gpudiff_submit(self.ctx, arr.ctypes.data_as(C.POINTER(JsonPair)), arr.size, C.byref(t)),
              "gpudiff_submit")
         return t.value
+
+    def write_plan(self, ticket: int) -> "WritePlan":
+        """gpudiff_write_plan_get: the writes for a waited device-encode batch (bodies from HBM)."""
+        wp = WritePlanC()
+        _chk(_lib.gpudiff_write_plan_get(self.ctx, ticket, C.byref(wp)), "gpudiff_write_plan_get")
+        try:
+            n = wp.n
+            b = wp.bodies
+            offs = np.ctypeslib.as_array(C.cast(b.offsets, C.POINTER(C.c_uint64)), (n + 1,)).copy()
+            st = _arr(b.status, n, np.int32)
+            src = _arr(b.source, n, np.uint8)
+            total = int(offs[-1]) if n else 0
+            raw = C.string_at(b.bytes, total) if total else b""
+            return WritePlan(pair_index=_arr(wp.pair_index, n, np.uint32), kind=_arr(wp.kind, n, np.uint8),
+                             noop=_arr(wp.noop, n, np.uint8),
+                             bodies=[None if st[i] != OK else raw[int(offs[i]):int(offs[i + 1])] for i in range(n)],
+                             source=src, n_host=int(b.n_host))
+        finally:
+            _lib.gpudiff_write_plan_release(self.ctx, C.byref(wp))
 
     def diff_pairs(self, pairs, ids=None, clusters=None) -> DiffResult:
         return self.wait(self.submit(pairs, ids, clusters))
@@ -678,6 +715,19 @@ def _doc_arrays(docs):
     ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p) for b in bufs])
     lens = (C.c_size_t * max(n, 1))(*[len(x) for x in docs])
     return docs, bufs, ptrs, lens
+
+
+@dataclass
+class WritePlan:
+    """The writes of one diffed batch (gpudiff_write_plan): spec writes (A's
+    body to downstream), then status writes (B's body to upstream); no-op
+    writes carry no body."""
+    pair_index: np.ndarray
+    kind: np.ndarray               # UPSERT_SPEC / UPSERT_STATUS
+    noop: np.ndarray
+    bodies: List[Optional[bytes]]  # b"" for no-op writes, None = undecodable
+    source: np.ndarray
+    n_host: int
 
 
 @dataclass

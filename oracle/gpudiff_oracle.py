@@ -642,23 +642,47 @@ def _diff_pair(a_json: bytes, b_json: bytes, hash_bits: int) -> Dict[str, Any]:
         a = informer_decode(a_json)
         b = informer_decode(b_json)
     except DecodeError:
-        return dict(spec_dirty=True, status_dirty=True, decode_error=True, seed=0, paths=[])
+        return dict(spec_dirty=True, status_dirty=True, decode_error=True, seed=0, paths=[], spec_noop=False,
+                    status_noop=False)
     sa, sb = spec_leaves(a), spec_leaves(b)
     ta, tb = status_leaves(a), status_leaves(b)
     seed = pair_seed(sa, sb, ta, tb, hash_bits)
     if seed < 0:
-        return dict(spec_dirty=True, status_dirty=True, decode_error=True, seed=0, paths=[])
+        return dict(spec_dirty=True, status_dirty=True, decode_error=True, seed=0, paths=[], spec_noop=False,
+                    status_noop=False)
     spec_dirty = not deep_equal_apart_from_status(a, b)
     status_dirty = not deep_equal_status(a, b)
     mask = (1 << hash_bits) - 1
     paths = _region_diff(sa, sb, seed, REGION_SPEC, mask)
+    spec_noop = spec_dirty and all(wire_equal_number(sa.get(p), sb.get(p)) for _h, _r, _k, p in paths)
+    status_noop = False
     if status_dirty:
-        paths += _region_diff(ta, tb, seed, REGION_STATUS, mask)
+        tpaths = _region_diff(ta, tb, seed, REGION_STATUS, mask)
+        status_noop = all(wire_equal_number(ta.get(p), tb.get(p)) for _h, _r, _k, p in tpaths)
+        paths += tpaths
         if "status" not in b:
             sp = (('K', 'status'),)
             paths.append((path_hash(sp, seed) & mask, REGION_STATUS, KIND_STATUS_ABSENT, sp))
+            status_noop = status_noop and "status" not in a
     return dict(spec_dirty=spec_dirty, status_dirty=status_dirty, decode_error=False,
-                seed=seed, paths=paths)
+                seed=seed, paths=paths, spec_noop=spec_noop, status_noop=status_noop)
+
+
+def wire_equal_number(la, lb) -> bool:
+    """The write-path no-op rule for one changed leaf (build-defined, DESIGN.md
+    §4g): an int64 v on one side and a float64 f == v on the other, |v| <=
+    2^53.  Go's json.Marshal writes float64(v) and int64(v) as the same digits
+    for such values, and the API server decodes those digits back to int64 v
+    (k8s util/json convertNumber), so writing one side over the other changes
+    nothing a predicate compares."""
+    if la is None or lb is None:
+        return False
+    (ta, ba), (tb, bb) = la, lb
+    if {ta, tb} != {TAG_INT, TAG_FLOAT}:
+        return False
+    v = struct.unpack('<q', ba if ta == TAG_INT else bb)[0]
+    f = struct.unpack('<d', bb if ta == TAG_INT else ba)[0]
+    return -(1 << 53) <= v <= (1 << 53) and float(v) == f
 
 
 def theorem_holds(a_json: bytes, b_json: bytes) -> bool:

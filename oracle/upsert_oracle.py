@@ -45,7 +45,7 @@ reference itself parity is UNPINNED.
 from __future__ import annotations
 
 import math
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -209,3 +209,23 @@ def _upsert_body(json_bytes: bytes, mode: int) -> Optional[bytes]:
     except DecodeError:
         return None
     return go_marshal(transform(obj, mode)) + b"\n"
+
+
+def write_plan(pairs) -> List[Tuple[int, int, bool, Optional[bytes]]]:
+    """The writes the syncer issues for a batch of (A=upstream, B=downstream)
+    pairs, as gpudiff_write_plan_get lists them: every spec-dirty pair
+    (upsertIntoDownstream, pkg/syncer/specsyncer.go:86-132: A's body,
+    MODE_SPEC), then every status-dirty pair (updateStatusInUpstream,
+    statussyncer.go:41-63: B's body, MODE_STATUS); a write the oracle marks
+    no-op (gpudiff_oracle.diff_pair spec_noop / status_noop) has no body.
+    Returns [(pair index, mode, noop, body or None if undecodable)]."""
+    from .gpudiff_oracle import diff_pair
+    rs = [diff_pair(a, b) for a, b in pairs]
+    out = []
+    for mode, dirty, noop, side in ((MODE_SPEC, "spec_dirty", "spec_noop", 0),
+                                    (MODE_STATUS, "status_dirty", "status_noop", 1)):
+        for i, r in enumerate(rs):
+            if r[dirty]:
+                skip = bool(r[noop])
+                out.append((i, mode, skip, b"" if skip else upsert_body(pairs[i][side], mode)))
+    return out

@@ -262,4 +262,29 @@ def cases():
     add("x28_depth_10000", deep(9998), deep(9998), True, True)
     add("x29_depth_10001", deep(9998), deep(9999), False, False)
     add("x30_depth_10000_changed", deep(9998), deep(9997) + b'', False, True)
+    # ---- the write-path no-op hints (GPUDIFF_SPEC_NOOP / GPUDIFF_STATUS_NOOP): dirty under
+    # DeepEqual (int64 != float64), identical on the wire
+    add("x31_noop_int_vs_integral_float", J(B), J(B).replace(b'"replicas":3,"selector"', b'"replicas":3.0,"selector"'),
+        False, True)
+    add("x32_not_noop_beyond_2p53", J(a25).replace(b'"x":1', b'"x":9007199254740993'),
+        J(a25).replace(b'"x":1', b'"x":9007199254740992.0'), False, True)
+    add("x33_noop_status_int_vs_float", J(B), J(B).replace(b'"readyReplicas":3', b'"readyReplicas":3e0'), True, False)
+    add("x34_not_noop_mixed", J(B), J(B).replace(b'"replicas":3,"selector"', b'"replicas":3.0,"selector"')
+        .replace(b'"revisionHistoryLimit":10', b'"revisionHistoryLimit":11'), False, True)
+    add("x35_noop_neg_zero", J(a25).replace(b'"x":1', b'"x":0'), J(a25).replace(b'"x":1', b'"x":-0.0'), False, True)
     return out
+
+
+# write-path no-op hints the oracle must produce for these rows: name -> (spec_noop, status_noop)
+NOOP_KAT = {
+    "x31_noop_int_vs_integral_float": (True, False),
+    "x32_not_noop_beyond_2p53": (False, False),
+    "x33_noop_status_int_vs_float": (False, True),
+    "x34_not_noop_mixed": (False, False),
+    "x35_noop_neg_zero": (True, False),
+    "x16_empty_objects": (False, True),           # neither side has a status key: UpdateStatus writes nothing
+    "20_new_has_no_status": (False, False),       # A has a status B would clear
+    "18_only_status_differs": (False, False),
+    "07_int_vs_float": (True, False),
+    "25_int64max_vs_overflow": (False, False),     # 2^63 - 1 vs 2^63 (float): beyond 2^53
+}

@@ -17,6 +17,10 @@ def expected_flags(r):
         f |= G.STATUS_DIRTY
     if r["decode_error"]:
         f |= G.DECODE_ERROR
+    if r.get("spec_noop"):
+        f |= G.SPEC_NOOP
+    if r.get("status_noop"):
+        f |= G.STATUS_NOOP
     return f
 
 

@@ -1,0 +1,114 @@
+"""Gate -> write on the device: for batches diffed
+through the device-encode submit path, gpudiff_write_plan_get lists the writes
+the syncer issues -- spec-dirty pairs: A's upsertIntoDownstream body; status-
+dirty pairs: B's updateStatusInUpstream body -- rendered by K10 from the JSON
+still staged in HBM, with the write-path no-op rule (no body, call skipped).
+Everything is compared with oracle/upsert_oracle.write_plan, i.e. the oracle's
+decisions, no-op rule and Go-exact bodies."""
+import json
+import random
+
+import pytest
+
+from kcp_amd import gpudiff as G
+from oracle import upsert_oracle as U
+from tests.golden.kat_cases import BASE, J, cases
+from tests.parity import assert_matches
+from tests.workload import make_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(eng, pairs):
+    t = eng.submit(pairs)
+    res = eng.wait(t)
+    assert_matches(res, pairs)
+    plan = eng.write_plan(t)
+    want = U.write_plan(pairs)
+    got = list(zip(plan.pair_index.tolist(), plan.kind.tolist(), [bool(x) for x in plan.noop], plan.bodies))
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert g == w, (g[:3], w[:3], (g[3] or b"")[:200], (w[3] or b"")[:200])
+    return plan
+
+
+def _noop_pairs(n, seed):
+    """int <-> integral-float retypes (no-op writes) mixed with real edits."""
+    rnd = random.Random(seed)
+    out = []
+    for i in range(n):
+        a = json.loads(J(BASE))
+        a["spec"]["replicas"] = rnd.randint(0, 50)
+        a["status"]["readyReplicas"] = rnd.randint(0, 50)
+        ja = J(a)
+        k = i % 5
+        if k == 0:    # spec no-op
+            jb = ja.replace(b'"replicas":%d,"selector"' % a["spec"]["replicas"],
+                            b'"replicas":%d.0,"selector"' % a["spec"]["replicas"])
+        elif k == 1:  # status no-op
+            jb = ja.replace(b'"readyReplicas":%d' % a["status"]["readyReplicas"],
+                            b'"readyReplicas":%de0' % a["status"]["readyReplicas"])
+        elif k == 2:  # a real spec edit beside a retype
+            jb = ja.replace(b'"replicas":%d,"selector"' % a["spec"]["replicas"],
+                            b'"replicas":%d.0,"selector"' % a["spec"]["replicas"]).replace(
+                b'"revisionHistoryLimit":10', b'"revisionHistoryLimit":12')
+        elif k == 3:  # no status on either side: the status write is a no-op
+            b = json.loads(ja)
+            del b["status"]
+            ja = jb = J(b)
+        else:         # identical
+            jb = ja
+        out.append((ja, jb))
+    return out
+
+
+def test_write_plan_kat_and_noops():
+    eng = G.Engine(device=0, device_encode=True)
+    pairs = [(a, b) for _, a, b, _, _ in cases()]
+    plan = _check(eng, pairs)
+    assert plan.noop.any()
+    np_ = _noop_pairs(200, 1)
+    plan = _check(eng, np_)
+    assert plan.noop.sum() >= 100 and (plan.noop == 0).any()
+    eng.close()
+
+
+@pytest.mark.parametrize("seed", [2, 3])
+def test_write_plan_populations(seed):
+    eng = G.Engine(device=0, device_encode=True, encode_threads=8)
+    pairs, _, _ = make_pairs(1500, seed=seed, mutate_frac=0.3)
+    _check(eng, pairs)
+    deep, _, _ = make_pairs(100, seed=seed + 10, mix=(("crd", 1.0),), mutate_frac=0.6, crd_leaves=1200)
+    _check(eng, deep)
+    eng.close()
+
+
+def test_write_plan_two_batches_in_flight_and_state_errors():
+    eng = G.Engine(device=0, device_encode=True)
+    p1, _, _ = make_pairs(300, seed=7, mutate_frac=0.3)
+    p2, _, _ = make_pairs(400, seed=8, mutate_frac=0.3)
+    t1 = eng.submit(p1)
+    t2 = eng.submit(p2)
+    with pytest.raises(G.GpuDiffError):  # not waited yet
+        eng.write_plan(t2)
+    eng.wait(t1)
+    eng.wait(t2)
+    want2 = U.write_plan(p2)
+    want1 = U.write_plan(p1)
+    plan2 = eng.write_plan(t2)
+    plan1 = eng.write_plan(t1)
+    assert [(int(i), int(k), bool(z), b) for i, k, z, b in zip(plan1.pair_index, plan1.kind, plan1.noop,
+                                                               plan1.bodies)] == want1
+    assert [(int(i), int(k), bool(z), b) for i, k, z, b in zip(plan2.pair_index, plan2.kind, plan2.noop,
+                                                               plan2.bodies)] == want2
+    t3 = eng.submit(p1)
+    eng.wait(t3)
+    with pytest.raises(G.GpuDiffError):  # t1's staging was reused by t3
+        eng.write_plan(t1)
+    host = G.Engine(device=0)  # host-encoded batches keep no JSON in HBM
+    th = host.submit(p1)
+    host.wait(th)
+    with pytest.raises(G.GpuDiffError):
+        host.write_plan(th)
+    host.close()
+    eng.close()

@@ -21,7 +21,7 @@ def _paths_of(offs, hs, ks, k):
 
 def _check(pairs, threads=1, paths=True):
     exp = oracle_batch(pairs)
-    want = np.array([expected_flags(r) for r in exp], dtype=np.uint8)
+    want = np.array([expected_flags(r) for r in exp], dtype=np.uint8) & 7  # the C++ baselines: decisions only
     d = cpu_ref.DecodedPairs(pairs)
     flags, sweeps, sec = d.decide(threads)
     assert (flags == want).all(), np.nonzero(flags != want)[0][:10]

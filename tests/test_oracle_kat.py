@@ -103,3 +103,14 @@ def test_self_equal(a):
     r = O.diff_pair(j, j)
     assert not r["spec_dirty"]
     assert r["status_dirty"] == ("status" not in a)
+
+
+def test_noop_rule_known_answers():
+    """The write-path no-op hints on the rows that pin them."""
+    from tests.golden.kat_cases import NOOP_KAT
+    by_name = {n: (a, b) for n, a, b, _, _ in CASES}
+    for name, (sn, tn) in NOOP_KAT.items():
+        r = O.diff_pair(*by_name[name])
+        assert (r["spec_noop"], r["status_noop"]) == (sn, tn), name
+        assert not r["spec_noop"] or r["spec_dirty"]
+        assert not r["status_noop"] or r["status_dirty"]
