@@ -422,7 +422,7 @@ __device__ __forceinline__ uint32_t tile_lower_bound(uint64_t x, uint64_t tile, 
 
 // Byte-exact confirmation of every lane's pending (hash-equal, same length)
 // long value at once.  The lanes' 16-byte chunks are flattened into one index
-// space (prefix sum of chunk counts); each pass the wave compares 256 chunks
+// space (prefix sum of chunk counts); each pass the wave compares 128 chunks
 // with 16-B loads (consecutive chunks of a value are consecutive addresses),
 // finding a chunk's owner lane by a cross-lane binary search over the prefix
 // sums.  Returns true in the lanes whose value differs (a hash collision).
@@ -432,12 +432,13 @@ __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a
     const uint32_t incl = wave_incl_scan(n16);
     const uint32_t total = shfl32(incl, 63);
     uint64_t bad = 0;  // lanes whose value differs (wave-uniform)
-    for (uint32_t base = 0; base < total; base += 256) {
-        u32x4 xa[4], xb[4];
-        uint32_t own[4];
-        bool act[4];
+    constexpr int CV_U = 2;  // chunk pairs in flight per lane: 4 costs the decision kernel a wave per SIMD
+    for (uint32_t base = 0; base < total; base += 64 * CV_U) {
+        u32x4 xa[CV_U], xb[CV_U];
+        uint32_t own[CV_U];
+        bool act[CV_U];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < CV_U; u++) {
             const uint32_t g = base + u * 64 + lane;
             act[u] = g < total;
             // owner = number of lanes whose inclusive chunk prefix is <= g
@@ -458,7 +459,7 @@ __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < CV_U; u++) {
             uint64_t m = ballot(act[u] && neq16(xa[u], xb[u]));
             while (m) {  // collisions only: practically never taken
                 const uint32_t j = (uint32_t)__builtin_ctzll(m);
@@ -1045,16 +1046,43 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
     return hipGetLastError();
 }
 
+// The decision kernel of each tuning variant (GPUDIFF_OPT_K2_VARIANT_SHIFT; 0 = the default).
+typedef void (*K2Fn)(const gpudiff_pair_row*, const uint8_t*, uint32_t, uint8_t*, uint32_t*, uint4*, uint32_t, uint32_t,
+                     uint64_t*, uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t*, uint32_t*, uint8_t*, uint64_t,
+                     uint32_t*, uint32_t);
+static K2Fn k2_kernel(uint32_t variant) {
+    switch (variant) {
+        case 1: return k_compare<false, 4, 1>;
+        case 2: return k_compare<true, 8, 1>;
+        case 3: return k_compare<false, 8, 1>;
+        case 4: return k_compare<true, 2, 1>;
+        case 5: return k_compare<true, 4, 6>;  // <= 80 VGPRs
+        case 6: return k_compare<true, 2, 8>;  // <= 64 VGPRs
+        case 7: return k_compare<true, 2, 6>;
+        case 8: return k_compare_flat<4, 1>;
+        case 9: return k_compare_flat<2, 1>;
+        case 11: return k_compare_flat<2, 5>;
+        case 12: return k_compare_flat<4, 5>;
+        case 13: return k_compare<true, 4, 1>;  // round 1's default (wave per pair)
+        case 10: return k_compare_flat<4, 4>;
+        default: return k_compare_flat<4, 1>;   // 0: 111 VGPRs, 4 waves/SIMD, no spills
+    }
+}
+
 static uint32_t k2_cap_blocks(const DiffBuffers& b) {
-    // one resident 256-thread block per CU per wave slot of a SIMD: a grid
-    // larger than the occupancy would leave blocks waiting for a free slot
-    // (a tail).  k_compare: 90 VGPRs -> 5 waves/SIMD; with joins inside K2 the
-    // extra waves keep HBM streaming while others join (tools/ab_k2.py: 11.18
-    // vs 11.59 ms at 4).  k_compare_flat variants: their own occupancy.
-    static const uint8_t kFlatOcc[5] = {4, 4, 4, 5, 5};  // variants 8..12 (0 = 8)
-    const uint32_t v = b.k2_variant == 0 ? 8u : b.k2_variant;
-    const uint32_t occ = (v >= 8 && v <= 12) ? kFlatOcc[v - 8] : 5u;
-    return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : occ);
+    // one resident 256-thread block per CU per wave slot a SIMD offers the
+    // kernel (its measured occupancy, hipOccupancyMaxActiveBlocksPerMultiprocessor):
+    // a larger grid would leave blocks waiting for a free slot, i.e. a tail
+    static int occ[16] = {0};
+    const uint32_t v = b.k2_variant & 15u;
+    if (!occ[v]) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k2_kernel(v)), 256, 0) !=
+                hipSuccess || n <= 0)
+            n = 4;
+        occ[v] = n;
+    }
+    return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : (uint32_t)occ[v]);
 }
 
 // 64-pair chunks split into 2^k items until there are >= 4 items per resident
@@ -1084,22 +1112,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, sub
-    switch (b.k2_variant) {  // tuning variants (GPUDIFF_OPT_K2_VARIANT_SHIFT); 0 is the default
-        case 1: k_compare<false, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 2: k_compare<true, 8, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 3: k_compare<false, 8, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 4: k_compare<true, 2, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 5: k_compare<true, 4, 6><<<grid, 256, 0, s>>>(K2ARGS); break;  // <= 80 VGPRs
-        case 6: k_compare<true, 2, 8><<<grid, 256, 0, s>>>(K2ARGS); break;  // <= 64 VGPRs
-        case 7: k_compare<true, 2, 6><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 8: k_compare_flat<4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 9: k_compare_flat<2, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 10: k_compare_flat<4, 4><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 11: k_compare_flat<2, 5><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 12: k_compare_flat<4, 5><<<grid, 256, 0, s>>>(K2ARGS); break;
-        case 13: k_compare<true, 4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;  // round 1's default
-        default: k_compare_flat<4, 1><<<grid, 256, 0, s>>>(K2ARGS); break;
-    }
+    k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
 }
