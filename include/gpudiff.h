@@ -494,17 +494,22 @@ int gpudiff_rollup_doc_host(const uint8_t* doc, size_t len, int32_t* v, uint8_t*
 
 /* ---- API-negotiation update classifier (second half) ----
  * Replaces the "Update" branch of Controller.enqueue,
- * pkg/reconciler/apiresource/controller.go:253-283, for APIResourceImport and
- * NegotiatedAPIResource objects (both have status {conditions: [{type, status,
- * lastTransitionTime, reason, message}]}).  Per (old, new) pair: no old object
+ * pkg/reconciler/apiresource/controller.go:253-283, for the three kinds its
+ * toQueueElementType (:185-236) types: APIResourceImport and
+ * NegotiatedAPIResource (GPUDIFF_NEG_KIND_API; both have status {conditions:
+ * [{type, status, lastTransitionTime, reason, message}]}) and
+ * CustomResourceDefinition (GPUDIFF_NEG_KIND_CRD, :186-199; apiextensions/v1
+ * status {conditions (same five fields), acceptedNames {plural, singular,
+ * shortNames[], kind, listKind, categories[]}, storedVersions[]}).  Per
+ * (old, new) pair: no old object
  * -> CREATED; equal resourceVersion -> IGNORE; different generation -> SPEC;
  * status not Semantic.DeepEqual (nil == empty, metav1.Time by instant) ->
  * STATUS; annotations differ OR labels EQUAL (the reference's missing `!` at
  * :278, reproduced) -> META; else IGNORE.  Objects are decoded with Go 1.16
  * encoding/json typed rules; DECODE when a side is not valid JSON, is not an
  * object, or a field the classifier reads (metadata.resourceVersion /
- * generation / labels / annotations, status.conditions and their elements)
- * fails Go's typed decode.  Type errors in fields the classifier does not read
+ * generation / labels / annotations, the typed status's fields and their
+ * elements) fails Go's typed decode.  Type errors in fields the classifier does not read
  * (spec, metadata.name, ...) are not checked: such an object cannot reach the
  * reference's informer at all, so no reference outcome exists for it.
  * Kernel K13 (negotiation mode of k_encode_docs) extracts each document's
@@ -516,6 +521,8 @@ int gpudiff_rollup_doc_host(const uint8_t* doc, size_t len, int32_t* v, uint8_t*
 #define GPUDIFF_NEG_META 3     /* AnnotationOrLabelsOnlyChanged */
 #define GPUDIFF_NEG_CREATED 4  /* no old object */
 #define GPUDIFF_NEG_DECODE (-1)
+#define GPUDIFF_NEG_KIND_API 0 /* APIResourceImport / NegotiatedAPIResource */
+#define GPUDIFF_NEG_KIND_CRD 1 /* CustomResourceDefinition */
 
 typedef struct gpudiff_nbatch gpudiff_nbatch;
 typedef struct gpudiff_nbatch_stats {
@@ -530,6 +537,11 @@ typedef struct gpudiff_nbatch_stats {
  * valid until gpudiff_nbatch_free. */
 int gpudiff_nbatch_create(gpudiff_ctx* ctx, const uint8_t* const* olds, const size_t* old_lens,
                           const uint8_t* const* news, const size_t* new_lens, size_t n, gpudiff_nbatch** out);
+/* kinds[i]: GPUDIFF_NEG_KIND_* of pair i (NULL: all GPUDIFF_NEG_KIND_API --
+ * what the *_kinds-less entry points use); other values: GPUDIFF_E_INVAL */
+int gpudiff_nbatch_create_kinds(gpudiff_ctx* ctx, const uint8_t* kinds, const uint8_t* const* olds,
+                                const size_t* old_lens, const uint8_t* const* news, const size_t* new_lens, size_t n,
+                                gpudiff_nbatch** out);
 int gpudiff_nbatch_run(gpudiff_ctx* ctx, gpudiff_nbatch* nb);
 int gpudiff_nbatch_fetch(gpudiff_ctx* ctx, gpudiff_nbatch* nb, int32_t* actions);
 int gpudiff_nbatch_stats_get(const gpudiff_nbatch* nb, gpudiff_nbatch_stats* st);
@@ -539,12 +551,20 @@ void gpudiff_nbatch_free(gpudiff_ctx* ctx, gpudiff_nbatch* nb);
  * K13's deferrals, exposed for CPU baselines and callers without a GPU. */
 int gpudiff_classify_updates_host(const uint8_t* const* olds, const size_t* old_lens, const uint8_t* const* news,
                                   const size_t* new_lens, size_t n, uint32_t threads, int32_t* actions);
+int gpudiff_classify_updates_host_kinds(const uint8_t* kinds, const uint8_t* const* olds, const size_t* old_lens,
+                                        const uint8_t* const* news, const size_t* new_lens, size_t n, uint32_t threads,
+                                        int32_t* actions);
 /* create + run + fetch + free */
 int gpudiff_classify_updates(gpudiff_ctx* ctx, const uint8_t* const* olds, const size_t* old_lens,
                              const uint8_t* const* news, const size_t* new_lens, size_t n, int32_t* actions);
+int gpudiff_classify_updates_kinds(gpudiff_ctx* ctx, const uint8_t* kinds, const uint8_t* const* olds,
+                                   const size_t* old_lens, const uint8_t* const* news, const size_t* new_lens, size_t n,
+                                   int32_t* actions);
 /* the host path for one pair (old == NULL: no old object) */
 int gpudiff_negotiate_pair_host(const uint8_t* old_json, size_t old_len, const uint8_t* new_json, size_t new_len,
                                 int32_t* action);
+int gpudiff_negotiate_pair_host_kind(uint32_t kind, const uint8_t* old_json, size_t old_len, const uint8_t* new_json,
+                                     size_t new_len, int32_t* action);
 
 /* ---- single-pair drop-ins (same semantics as the Go predicates) ---- */
 int gpudiff_spec_equal(gpudiff_ctx* ctx, const uint8_t* old_json, size_t old_len,

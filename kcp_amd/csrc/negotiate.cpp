@@ -34,6 +34,7 @@ struct gpudiff_nbatch {
     std::vector<TokDoc> docs;  // 2 per pair: old, new
     std::vector<const uint8_t*> olds, news;
     std::vector<size_t> old_lens, new_lens;
+    std::vector<uint8_t> kinds;  // GPUDIFF_NEG_KIND_* per pair
     uint64_t json_bytes = 0, scratch_bytes = 0, n_host = 0;
     bool ran = false;  // a run was issued (fetch before any run: GPUDIFF_E_STATE)
     void *d_json = nullptr, *d_scratch = nullptr, *d_docs = nullptr, *d_no = nullptr, *d_absent = nullptr,
@@ -57,12 +58,37 @@ struct Cond {
     }
 };
 
+// a Go slice over its backing array: backing.size() == cap, len elements in use
+template <class T>
+struct GoSlice {
+    std::vector<T> backing;
+    size_t len = 0;
+    bool operator==(const GoSlice& o) const {  // Semantic.DeepEqual: nil == empty
+        if (len != o.len) return false;
+        for (size_t i = 0; i < len; i++)
+            if (!(backing[i] == o.backing[i])) return false;
+        return true;
+    }
+};
+
+// apiextensions/v1 CustomResourceDefinitionNames
+struct CrdNames {
+    std::string s[4];  // plural, singular, kind, listKind
+    GoSlice<std::string> shortn, cat;
+    bool operator==(const CrdNames& o) const {
+        return s[0] == o.s[0] && s[1] == o.s[1] && s[2] == o.s[2] && s[3] == o.s[3] && shortn == o.shortn &&
+               cat == o.cat;
+    }
+};
+
 struct NegFields {
     std::string rv;
     int64_t gen = 0;
     std::map<std::string, std::string> lab, ann;  // nil and empty compare equal: no flag needed
-    std::vector<Cond> backing;                    // size() == cap
-    size_t clen = 0;
+    GoSlice<Cond> conds;
+    // kind GPUDIFF_NEG_KIND_CRD: the rest of CustomResourceDefinitionStatus
+    CrdNames names;
+    GoSlice<std::string> stored;
 };
 
 // ---------------------------------------------------------------- time.Parse(time.RFC3339, s), Go 1.16
@@ -155,6 +181,8 @@ bool parse_rfc3339(const std::string& s, int64_t* sec, int64_t* nsec) {
 
 const char* const kMetaNames[4] = {"resourceVersion", "generation", "labels", "annotations"};
 const char* const kCondNames[5] = {"type", "status", "lastTransitionTime", "reason", "message"};
+const char* const kCrdStatusNames[3] = {"conditions", "acceptedNames", "storedVersions"};
+const char* const kCrdNamesNames[6] = {"plural", "singular", "shortNames", "kind", "listKind", "categories"};
 
 // encoding/json object(): the first exact match among the struct's fields, else the first fold match
 int lookup(const char* const* names, int n, const std::string& k) {
@@ -167,7 +195,7 @@ int lookup(const char* const* names, int n, const std::string& k) {
 
 class NegScanner : public goscan::Scanner {
    public:
-    using goscan::Scanner::Scanner;
+    NegScanner(const uint8_t* p, size_t n, uint32_t kind) : goscan::Scanner(p, n), kind_(kind) {}
 
     bool run(NegFields& f) {
         ws();
@@ -183,6 +211,8 @@ class NegScanner : public goscan::Scanner {
     }
 
    private:
+    uint32_t kind_;
+
     bool string_into(std::string& out) {  // null: no-op; else a JSON string
         if (peek_null()) return lit("null");
         if (p_ >= e_ || *p_ != '"') return false;
@@ -202,6 +232,52 @@ class NegScanner : public goscan::Scanner {
             if (p_ >= e_ || *p_ != '"') return false;
             return str(&m[k]);
         });
+    }
+    // encoding/json array(): element i decoded INTO backing[i]; reflect growth
+    // (cap + cap/2, at least 4, the first len elements copied); the length
+    // becomes the array's; an empty array is an empty non-nil slice, null nil
+    template <class T, class F>
+    bool slice(GoSlice<T>& sl, F&& elem_into) {
+        if (peek_null()) {
+            sl.backing.clear();
+            sl.len = 0;
+            return lit("null");
+        }
+        if (p_ >= e_ || *p_ != '[') return false;
+        p_++;
+        ws();
+        size_t i = 0;
+        if (p_ < e_ && *p_ == ']') {
+            p_++;
+        } else {
+            while (true) {
+                if (i >= sl.backing.size()) {
+                    const size_t cap = std::max<size_t>(4, sl.backing.size() + sl.backing.size() / 2);
+                    std::vector<T> nb(cap);
+                    for (size_t q = 0; q < sl.len; q++) nb[q] = sl.backing[q];
+                    sl.backing.swap(nb);
+                }
+                if (i >= sl.len) sl.len = i + 1;
+                ws();
+                if (!elem_into(sl.backing[i])) return false;
+                i++;
+                ws();
+                if (p_ >= e_) return false;
+                const uint8_t x = *p_++;
+                if (x == ',') continue;
+                if (x == ']') break;
+                return false;
+            }
+        }
+        if (i < sl.len) sl.len = i;
+        if (i == 0) {
+            sl.backing.clear();
+            sl.len = 0;
+        }
+        return true;
+    }
+    bool strings(GoSlice<std::string>& sl) {
+        return slice(sl, [&](std::string& e) { return string_into(e); });
     }
     bool metadata(NegFields& f) {
         if (peek_null()) return lit("null");
@@ -261,67 +337,68 @@ class NegScanner : public goscan::Scanner {
             return string_into(c.f[fi == 0 ? 0 : fi == 1 ? 1 : fi == 3 ? 2 : 3]);
         });
     }
+    bool conditions(NegFields& f) {
+        return slice(f.conds, [&](Cond& c) { return cond_into(c); });
+    }
+    // CustomResourceDefinitionNames: a struct (null: no-op; a repeated key merges)
+    bool names_into(CrdNames& n) {
+        if (peek_null()) return lit("null");
+        if (p_ >= e_ || *p_ != '{') return false;
+        return members(3, [&](const std::string& k) -> bool {
+            switch (lookup(kCrdNamesNames, 6, k)) {
+                case 0:
+                    return string_into(n.s[0]);
+                case 1:
+                    return string_into(n.s[1]);
+                case 2:
+                    return strings(n.shortn);
+                case 3:
+                    return string_into(n.s[2]);
+                case 4:
+                    return string_into(n.s[3]);
+                case 5:
+                    return strings(n.cat);
+                default:
+                    return skip(3);
+            }
+        });
+    }
     bool status(NegFields& f) {
         if (peek_null()) return lit("null");
         if (p_ >= e_ || *p_ != '{') return false;
+        if (kind_ == GPUDIFF_NEG_KIND_CRD)
+            return members(2, [&](const std::string& k) -> bool {
+                switch (lookup(kCrdStatusNames, 3, k)) {
+                    case 0:
+                        return conditions(f);
+                    case 1:
+                        return names_into(f.names);
+                    case 2:
+                        return strings(f.stored);
+                    default:
+                        return skip(2);
+                }
+            });
         return members(2, [&](const std::string& k) -> bool {
             if (!field_match("conditions", k)) return skip(2);
-            if (peek_null()) {
-                f.backing.clear();  // nil slice
-                f.clen = 0;
-                return lit("null");
-            }
-            if (p_ >= e_ || *p_ != '[') return false;
-            p_++;
-            ws();
-            size_t i = 0;
-            if (p_ < e_ && *p_ == ']') {
-                p_++;
-            } else {
-                while (true) {
-                    if (i >= f.backing.size()) {  // reflect growth: cap + cap/2, at least 4; old elements copied
-                        const size_t cap = std::max<size_t>(4, f.backing.size() + f.backing.size() / 2);
-                        std::vector<Cond> nb(cap);
-                        for (size_t q = 0; q < f.clen; q++) nb[q] = f.backing[q];
-                        f.backing.swap(nb);
-                    }
-                    if (i >= f.clen) f.clen = i + 1;
-                    ws();
-                    if (!cond_into(f.backing[i])) return false;
-                    i++;
-                    ws();
-                    if (p_ >= e_) return false;
-                    const uint8_t x = *p_++;
-                    if (x == ',') continue;
-                    if (x == ']') break;
-                    return false;
-                }
-            }
-            if (i < f.clen) f.clen = i;
-            if (i == 0) {
-                f.backing.clear();  // an empty, non-nil slice
-                f.clen = 0;
-            }
-            return true;
+            return conditions(f);
         });
     }
 };
 
-bool host_fields(const uint8_t* doc, size_t len, NegFields& f) {
-    NegScanner sc(doc ? doc : (const uint8_t*)"", len);
+bool host_fields(const uint8_t* doc, size_t len, uint32_t kind, NegFields& f) {
+    NegScanner sc(doc ? doc : (const uint8_t*)"", len, kind);
     return sc.run(f);
 }
 
-int32_t classify_host(const uint8_t* a, size_t al, const uint8_t* b, size_t bl) {
+int32_t classify_host(const uint8_t* a, size_t al, const uint8_t* b, size_t bl, uint32_t kind) {
     NegFields B, A;
-    if (!host_fields(b, bl, B)) return GPUDIFF_NEG_DECODE;
+    if (!host_fields(b, bl, kind, B)) return GPUDIFF_NEG_DECODE;
     if (!a) return GPUDIFF_NEG_CREATED;
-    if (!host_fields(a, al, A)) return GPUDIFF_NEG_DECODE;
+    if (!host_fields(a, al, kind, A)) return GPUDIFF_NEG_DECODE;
     if (A.rv == B.rv) return GPUDIFF_NEG_IGNORE;
     if (A.gen != B.gen) return GPUDIFF_NEG_SPEC;
-    if (A.clen != B.clen) return GPUDIFF_NEG_STATUS;
-    for (size_t c = 0; c < A.clen; c++)
-        if (!(A.backing[c] == B.backing[c])) return GPUDIFF_NEG_STATUS;
+    if (!(A.conds == B.conds) || !(A.names == B.names) || !(A.stored == B.stored)) return GPUDIFF_NEG_STATUS;
     if (A.ann != B.ann || A.lab == B.lab) return GPUDIFF_NEG_META;
     return GPUDIFF_NEG_IGNORE;
 }
@@ -351,22 +428,28 @@ void fold_timing(gpudiff_nbatch* nb) {
 
 extern "C" {
 
-int gpudiff_negotiate_pair_host(const uint8_t* old_json, size_t old_len, const uint8_t* new_json, size_t new_len,
-                                int32_t* action) {
-    if (!action || (!new_json && new_len)) return GPUDIFF_E_INVAL;
-    *action = classify_host(old_json, old_len, new_json, new_len);
+int gpudiff_negotiate_pair_host_kind(uint32_t kind, const uint8_t* old_json, size_t old_len, const uint8_t* new_json,
+                                     size_t new_len, int32_t* action) {
+    if (!action || (!new_json && new_len) || kind > GPUDIFF_NEG_KIND_CRD) return GPUDIFF_E_INVAL;
+    *action = classify_host(old_json, old_len, new_json, new_len, kind);
     return GPUDIFF_OK;
 }
 
-int gpudiff_classify_updates_host(const uint8_t* const* olds, const size_t* old_lens, const uint8_t* const* news,
-                                  const size_t* new_lens, size_t n, uint32_t threads, int32_t* actions) {
+int gpudiff_negotiate_pair_host(const uint8_t* old_json, size_t old_len, const uint8_t* new_json, size_t new_len,
+                                int32_t* action) {
+    return gpudiff_negotiate_pair_host_kind(GPUDIFF_NEG_KIND_API, old_json, old_len, new_json, new_len, action);
+}
+
+int gpudiff_classify_updates_host_kinds(const uint8_t* kinds, const uint8_t* const* olds, const size_t* old_lens,
+                                        const uint8_t* const* news, const size_t* new_lens, size_t n, uint32_t threads,
+                                        int32_t* actions) {
     if (n && (!olds || !old_lens || !news || !new_lens || !actions)) return GPUDIFF_E_INVAL;
     for (size_t i = 0; i < n; i++)
-        if (!news[i] && new_lens[i]) return GPUDIFF_E_INVAL;
+        if ((!news[i] && new_lens[i]) || (kinds && kinds[i] > GPUDIFF_NEG_KIND_CRD)) return GPUDIFF_E_INVAL;
     const uint32_t T = (uint32_t)std::max<size_t>(1, std::min<size_t>(threads ? threads : 1, n ? n : 1));
     auto work = [&](uint32_t t) {
         for (size_t i = n * t / T, e = n * (t + 1) / T; i < e; i++)
-            actions[i] = classify_host(olds[i], olds[i] ? old_lens[i] : 0, news[i], new_lens[i]);
+            actions[i] = classify_host(olds[i], olds[i] ? old_lens[i] : 0, news[i], new_lens[i], kinds ? kinds[i] : 0);
     };
     std::vector<std::thread> th;
     for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
@@ -375,12 +458,18 @@ int gpudiff_classify_updates_host(const uint8_t* const* olds, const size_t* old_
     return GPUDIFF_OK;
 }
 
-int gpudiff_nbatch_create(gpudiff_ctx* c, const uint8_t* const* olds, const size_t* old_lens,
-                          const uint8_t* const* news, const size_t* new_lens, size_t n, gpudiff_nbatch** out) {
+int gpudiff_classify_updates_host(const uint8_t* const* olds, const size_t* old_lens, const uint8_t* const* news,
+                                  const size_t* new_lens, size_t n, uint32_t threads, int32_t* actions) {
+    return gpudiff_classify_updates_host_kinds(nullptr, olds, old_lens, news, new_lens, n, threads, actions);
+}
+
+int gpudiff_nbatch_create_kinds(gpudiff_ctx* c, const uint8_t* kinds, const uint8_t* const* olds,
+                                const size_t* old_lens, const uint8_t* const* news, const size_t* new_lens, size_t n,
+                                gpudiff_nbatch** out) {
     if (!c || !out || (n && (!olds || !old_lens || !news || !new_lens)) || n > 0x3FFFFFFFu) return GPUDIFF_E_INVAL;
     *out = nullptr;
     for (size_t i = 0; i < n; i++)
-        if (!news[i] && new_lens[i]) return GPUDIFF_E_INVAL;
+        if ((!news[i] && new_lens[i]) || (kinds && kinds[i] > GPUDIFF_NEG_KIND_CRD)) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
     gpudiff_nbatch* nb = new (std::nothrow) gpudiff_nbatch();
@@ -390,6 +479,8 @@ int gpudiff_nbatch_create(gpudiff_ctx* c, const uint8_t* const* olds, const size
     nb->news.assign(news, news + n);
     nb->old_lens.assign(old_lens, old_lens + n);
     nb->new_lens.assign(new_lens, new_lens + n);
+    if (kinds) nb->kinds.assign(kinds, kinds + n);
+    else nb->kinds.assign(n, (uint8_t)GPUDIFF_NEG_KIND_API);
     nb->docs.resize(2 * n);
     std::vector<uint8_t> absent(n, 0);
     uint64_t jb = 0, sb = 0;
@@ -404,6 +495,7 @@ int gpudiff_nbatch_create(gpudiff_ctx* c, const uint8_t* const* olds, const size
         t.json_off = jb;
         t.json_len = l;
         t.scratch_off = sb;
+        t.pad[0] = nb->kinds[p];  // K13: which typed status to read
         if (l <= kTokMaxLen) {
             jb = (jb + l + kTokSlack + 15) & ~15ull;
             sb += rollup_scratch_bytes(l);
@@ -488,7 +580,7 @@ int gpudiff_nbatch_fetch(gpudiff_ctx* c, gpudiff_nbatch* nb, int32_t* actions) {
     auto work = [&](uint32_t t) {
         for (size_t k = t; k < def.size(); k += T) {
             const uint32_t i = def[k];
-            actions[i] = classify_host(nb->olds[i], nb->old_lens[i], nb->news[i], nb->new_lens[i]);
+            actions[i] = classify_host(nb->olds[i], nb->old_lens[i], nb->news[i], nb->new_lens[i], nb->kinds[i]);
         }
     };
     std::vector<std::thread> th;
@@ -520,15 +612,26 @@ void gpudiff_nbatch_free(gpudiff_ctx* c, gpudiff_nbatch* nb) {
     free_nbatch(nb);
 }
 
-int gpudiff_classify_updates(gpudiff_ctx* c, const uint8_t* const* olds, const size_t* old_lens,
-                             const uint8_t* const* news, const size_t* new_lens, size_t n, int32_t* actions) {
+int gpudiff_nbatch_create(gpudiff_ctx* c, const uint8_t* const* olds, const size_t* old_lens,
+                          const uint8_t* const* news, const size_t* new_lens, size_t n, gpudiff_nbatch** out) {
+    return gpudiff_nbatch_create_kinds(c, nullptr, olds, old_lens, news, new_lens, n, out);
+}
+
+int gpudiff_classify_updates_kinds(gpudiff_ctx* c, const uint8_t* kinds, const uint8_t* const* olds,
+                                   const size_t* old_lens, const uint8_t* const* news, const size_t* new_lens, size_t n,
+                                   int32_t* actions) {
     gpudiff_nbatch* nb = nullptr;
-    int rc = gpudiff_nbatch_create(c, olds, old_lens, news, new_lens, n, &nb);
+    int rc = gpudiff_nbatch_create_kinds(c, kinds, olds, old_lens, news, new_lens, n, &nb);
     if (rc) return rc;
     rc = gpudiff_nbatch_run(c, nb);
     if (!rc) rc = gpudiff_nbatch_fetch(c, nb, actions);
     gpudiff_nbatch_free(c, nb);
     return rc;
+}
+
+int gpudiff_classify_updates(gpudiff_ctx* c, const uint8_t* const* olds, const size_t* old_lens,
+                             const uint8_t* const* news, const size_t* new_lens, size_t n, int32_t* actions) {
+    return gpudiff_classify_updates_kinds(c, nullptr, olds, old_lens, news, new_lens, n, actions);
 }
 
 }  // extern "C"

@@ -1,7 +1,7 @@
 // K14: the API-negotiation update classifier over K13's per-document fields
 // (pkg/reconciler/apiresource/controller.go:253-283).
 // One lane per (old, new) pair: documents 2i (old) and 2i+1 (new) of the batch.
-// The work per pair is a handful of short span compares on 2 x 944-byte NegOut
+// The work per pair is a handful of short span compares on 2 x 1184-byte NegOut
 // records; like K12 it is latency-bound and tiny next to K13.
 #include <hip/hip_runtime.h>
 
@@ -52,6 +52,24 @@ __device__ bool status_eq(const NegOut& A, const uint8_t* da, const NegOut& B, c
     return true;
 }
 
+// []string element-wise (nil == empty)
+__device__ bool list_eq(const NegSpan* a, uint32_t na, const uint8_t* da, const NegSpan* b, uint32_t nb,
+                        const uint8_t* db) {
+    if (na != nb) return false;
+    for (uint32_t i = 0; i < na; i++)
+        if (!span_eq(da + a[i].off, a[i].len, db + b[i].off, b[i].len)) return false;
+    return true;
+}
+
+// the rest of CustomResourceDefinitionStatus: acceptedNames (a struct: its four
+// strings and two lists), storedVersions
+__device__ bool crd_status_eq(const NegOut& A, const uint8_t* da, const NegOut& B, const uint8_t* db) {
+    for (uint32_t f = 0; f < 4; f++)
+        if (!span_eq(da + A.names[f].off, A.names[f].len, db + B.names[f].off, B.names[f].len)) return false;
+    return list_eq(A.shortn, A.n_short, da, B.shortn, B.n_short, db) && list_eq(A.cat, A.n_cat, da, B.cat, B.n_cat, db) &&
+           list_eq(A.stored, A.n_stored, da, B.stored, B.n_stored, db);
+}
+
 __global__ __launch_bounds__(256) void k_negotiate_pairs(const NegOut* __restrict__ outs, const uint8_t* __restrict__ absent,
                                                          const TokDoc* __restrict__ docs, const uint8_t* __restrict__ json,
                                                          uint32_t n, int32_t* __restrict__ actions) {
@@ -70,7 +88,9 @@ __global__ __launch_bounds__(256) void k_negotiate_pairs(const NegOut* __restric
         if (A.status != GPUDIFF_TOK_OK) act = kNegDefer;
         else if (span_eq(da + A.rv_off, A.rv_len, db + B.rv_off, B.rv_len)) act = GPUDIFF_NEG_IGNORE;  // :263-265
         else if (A.gen != B.gen) act = GPUDIFF_NEG_SPEC;                                                 // :267-270
-        else if (!status_eq(A, da, B, db)) act = GPUDIFF_NEG_STATUS;                                     // :272-275
+        else if (!status_eq(A, da, B, db) ||
+                 (docs[2u * i + 1u].pad[0] == GPUDIFF_NEG_KIND_CRD && !crd_status_eq(A, da, B, db)))
+            act = GPUDIFF_NEG_STATUS;  // :272-275
         else if (!map_eq(A.ann, A.n_ann, da, B.ann, B.n_ann, db) || map_eq(A.lab, A.n_lab, da, B.lab, B.n_lab, db))
             act = GPUDIFF_NEG_META;  // :277-281, the missing `!` before the labels term kept
         else

@@ -777,6 +777,14 @@ __device__ __forceinline__ const char* neg_cond_field(uint32_t k) {
 __device__ __forceinline__ uint32_t neg_cond_field_len(uint32_t k) {
     return k == 0 ? 4u : k == 1 ? 6u : k == 2 ? 6u : k == 3 ? 7u : 18u;
 }
+// apiextensions/v1 CustomResourceDefinitionNames json names, struct order
+__device__ __forceinline__ const char* neg_crd_names_field(uint32_t k) {
+    return k == 0 ? "plural" : k == 1 ? "singular" : k == 2 ? "shortNames" : k == 3 ? "kind" : k == 4 ? "listKind"
+                                                                                                       : "categories";
+}
+__device__ __forceinline__ uint32_t neg_crd_names_field_len(uint32_t k) {
+    return k == 0 ? 6u : k == 1 ? 8u : k == 2 ? 10u : k == 3 ? 4u : k == 4 ? 8u : 10u;
+}
 
 struct Scratch {
     uint32_t* tok;

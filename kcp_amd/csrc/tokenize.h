@@ -135,6 +135,10 @@ struct NegCond {
     int32_t nsec;
     uint32_t pad;
 };
+constexpr uint32_t kNegMaxList = 8;      // CRD []string elements on the device (each list)
+struct NegSpan {
+    uint32_t off, len;
+};
 struct NegOut {
     uint32_t status;          // GPUDIFF_TOK_*
     uint32_t n_lab, n_ann, n_cond;
@@ -143,8 +147,14 @@ struct NegOut {
     int64_t pad2;
     NegMember lab[kNegMaxMembers], ann[kNegMaxMembers];
     NegCond cond[kNegMaxConds];
+    // GPUDIFF_NEG_KIND_CRD only (TokDoc.pad[0]): status.acceptedNames {plural,
+    // singular, kind, listKind} (absent / null: empty spans), shortNames,
+    // categories, storedVersions (nil and empty: 0 elements)
+    NegSpan names[4];
+    uint32_t n_short, n_cat, n_stored, pad3;
+    NegSpan shortn[kNegMaxList], cat[kNegMaxList], stored[kNegMaxList];
 };
-static_assert(sizeof(NegCond) == 48 && sizeof(NegOut) == 944, "NegOut");
+static_assert(sizeof(NegCond) == 48 && sizeof(NegOut) == 1184, "NegOut");
 constexpr int64_t kZeroTimeSec = -62135596800ll;
 
 constexpr uint32_t kTokMaxLen = (1u << 24) - 64u;  // token words hold 24-bit positions

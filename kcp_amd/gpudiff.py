@@ -257,8 +257,18 @@ SIGNATURES = [
     ("gpudiff_nbatch_fetch", C.c_int, [_P, _P, C.POINTER(C.c_int32)]),
     ("gpudiff_nbatch_stats_get", C.c_int, [_P, C.POINTER(NBatchStats)]),
     ("gpudiff_nbatch_free", None, [_P, _P]),
+    ("gpudiff_nbatch_create_kinds", C.c_int, [_P, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                              C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(_P)]),
     ("gpudiff_classify_updates", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
                                            C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(C.c_int32)]),
+    ("gpudiff_classify_updates_kinds", C.c_int, [_P, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                                 C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                                 C.POINTER(C.c_int32)]),
+    ("gpudiff_classify_updates_host_kinds", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                                      C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                                      C.c_uint32, C.POINTER(C.c_int32)]),
+    ("gpudiff_negotiate_pair_host_kind", C.c_int, [C.c_uint32, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                                   C.POINTER(C.c_int32)]),
     ("gpudiff_classify_updates_host", C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
                                                 C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32, C.POINTER(C.c_int32)]),
     ("gpudiff_negotiate_pair_host", C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
@@ -484,6 +494,9 @@ class ObjectStore:
             pass
 
 
+NEG_KIND_API, NEG_KIND_CRD = 0, 1  # GPUDIFF_NEG_KIND_*: APIResourceImport/NegotiatedAPIResource, CRD
+
+
 class Engine:
     """One gpudiff context (one GPU, one stream, one submitting thread)."""
 
@@ -672,17 +685,18 @@ class Engine:
         return RBatch(self, docs)
 
     # ---- API-negotiation update classifier
-    def classify_updates(self, pairs) -> np.ndarray:
-        """Kernels K13 + K14 (host path for K13's deferrals): one NEG_* action per (old or None, new) pair."""
-        nb = self.nbatch(pairs)
+    def classify_updates(self, pairs, kinds=NEG_KIND_API) -> np.ndarray:
+        """Kernels K13 + K14 (host path for K13's deferrals): one NEG_* action per (old or None, new) pair.
+        kinds: one NEG_KIND_* for every pair, or a sequence with one per pair."""
+        nb = self.nbatch(pairs, kinds)
         try:
             nb.run()
             return nb.fetch()
         finally:
             nb.close()
 
-    def nbatch(self, pairs) -> "NBatch":
-        return NBatch(self, pairs)
+    def nbatch(self, pairs, kinds=NEG_KIND_API) -> "NBatch":
+        return NBatch(self, pairs, kinds)
 
     def k0_profile(self, enable: bool = True):
         """K0 per-phase wall-clock ticks (100 MHz) summed over waves since the last call."""
@@ -853,14 +867,26 @@ class RBatch:
             pass
 
 
-NEG_IGNORE, NEG_SPEC, NEG_STATUS, NEG_META, NEG_CREATED, NEG_DECODE = 0, 1, 2, 3, 4, -1
+def _kinds_array(kinds, n):
+    """NEG_KIND_* per pair as a uint8 array (kept alive by the caller), from one kind or a sequence"""
+    if isinstance(kinds, (int, np.integer)):
+        arr = np.full(max(n, 1), int(kinds), np.uint8)
+    else:
+        arr = np.ascontiguousarray(np.asarray(kinds, np.uint8))
+        if arr.size != n:
+            raise ValueError("kinds: %d entries for %d pairs" % (arr.size, n))
+        if n == 0:
+            arr = np.zeros(1, np.uint8)
+    return arr
 
 
 class NBatch:
-    """(old, new) pairs of APIResourceImport / NegotiatedAPIResource JSON resident in HBM for K13/K14
-    (gpudiff_nbatch_*); old None = no old object."""
+    """(old, new) pairs of APIResourceImport / NegotiatedAPIResource / CustomResourceDefinition JSON resident
+    in HBM for K13/K14 (gpudiff_nbatch_*); old None = no old object; kinds: NEG_KIND_* (one, or per pair)."""
 
-    def __init__(self, eng: "Engine", pairs):
+    def __init__(self, eng: "Engine", pairs, kinds=None):
+        if kinds is None:
+            kinds = NEG_KIND_API
         self.eng = eng
         pairs = list(pairs)
         self.n = len(pairs)
@@ -870,9 +896,10 @@ class NBatch:
         for i, a in enumerate(olds):
             if a is None:
                 optrs[i] = None
+        self._kinds = _kinds_array(kinds, self.n)
         h = C.c_void_p()
-        _chk(_lib.gpudiff_nbatch_create(eng.ctx, optrs, olens, nptrs, nlens, self.n, C.byref(h)),
-             "gpudiff_nbatch_create")
+        _chk(_lib.gpudiff_nbatch_create_kinds(eng.ctx, self._kinds.ctypes.data, optrs, olens, nptrs, nlens, self.n,
+                                              C.byref(h)), "gpudiff_nbatch_create_kinds")
         self.h = h
 
     def run(self):
@@ -901,13 +928,17 @@ class NBatch:
             pass
 
 
-def negotiate_pair_host(old, new) -> int:
-    """The classifier's host path (Go-exact) for one pair; old None = no old object."""
+def negotiate_pair_host(old, new, kind: int = None) -> int:
+    """The classifier's host path (Go-exact) for one pair; old None = no old object; kind NEG_KIND_*."""
     a = None if old is None else to_json_bytes(old)
     b = to_json_bytes(new)
     act = C.c_int32()
-    _chk(_lib.gpudiff_negotiate_pair_host(a, 0 if a is None else len(a), b, len(b), C.byref(act)),
-         "gpudiff_negotiate_pair_host")
+    if kind is None:
+        _chk(_lib.gpudiff_negotiate_pair_host(a, 0 if a is None else len(a), b, len(b), C.byref(act)),
+             "gpudiff_negotiate_pair_host")
+    else:
+        _chk(_lib.gpudiff_negotiate_pair_host_kind(kind, a, 0 if a is None else len(a), b, len(b), C.byref(act)),
+             "gpudiff_negotiate_pair_host_kind")
     return int(act.value)
 
 
@@ -915,9 +946,10 @@ class HostPairs:
     """(old, new) JSON pairs held in C memory for the classifier's host path
     (gpudiff_classify_updates_host); old None = no old object."""
 
-    def __init__(self, pairs):
+    def __init__(self, pairs, kinds=None):
         pairs = list(pairs)
         self.n = len(pairs)
+        self._kinds = None if kinds is None else _kinds_array(kinds, self.n)
         olds = [None if a is None else to_json_bytes(a) for a, _ in pairs]
         _, self._nb, self.nptrs, self.nlens = _doc_arrays([b for _, b in pairs])
         _, self._ob, self.optrs, self.olens = _doc_arrays([a if a is not None else b"" for a in olds])
@@ -927,9 +959,15 @@ class HostPairs:
 
     def classify(self, threads: int = 1) -> np.ndarray:
         out = np.zeros(max(self.n, 1), np.int32)
-        _chk(_lib.gpudiff_classify_updates_host(self.optrs, self.olens, self.nptrs, self.nlens, self.n, threads,
-                                                out.ctypes.data_as(C.POINTER(C.c_int32))),
-             "gpudiff_classify_updates_host")
+        if self._kinds is None:
+            _chk(_lib.gpudiff_classify_updates_host(self.optrs, self.olens, self.nptrs, self.nlens, self.n, threads,
+                                                    out.ctypes.data_as(C.POINTER(C.c_int32))),
+                 "gpudiff_classify_updates_host")
+        else:
+            _chk(_lib.gpudiff_classify_updates_host_kinds(self._kinds.ctypes.data, self.optrs, self.olens, self.nptrs,
+                                                          self.nlens, self.n, threads,
+                                                          out.ctypes.data_as(C.POINTER(C.c_int32))),
+                 "gpudiff_classify_updates_host_kinds")
         return out[:self.n]
 
 

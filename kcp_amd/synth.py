@@ -301,3 +301,92 @@ def negotiate_population(n_pairs: int, seed: int = 20211004 + 7, variants: bool 
         pairs.append((old, new))
         want.append(exp)
     return pairs, np.asarray(want, np.int32)
+
+
+def crd_population(n_pairs: int, seed: int = 20211004 + 8, n_props: int = 12):
+    """(old, new) Update pairs of CustomResourceDefinition JSON (kind
+    GPUDIFF_NEG_KIND_CRD; the third kind of controller.go:186-199), API-server
+    shaped: metadata with kcp labels, a spec with one served version whose
+    openAPIV3Schema has `n_props` properties (~3 KB at the default), status
+    {conditions: NamesAccepted + Established, acceptedNames {plural, singular,
+    kind, listKind, shortNames?, categories?}, storedVersions}.  Event mix: 15%
+    resync, 20% generation bump (a schema edit), 25% status change (a condition,
+    an accepted name, a short name / category added, a stored version
+    appended), 15% annotation change, 15% label change only, 10% nothing but
+    resourceVersion.  Returns (pairs, expected actions as designed)."""
+    rng = np.random.default_rng(seed)
+
+    def doc(name, rv, gen, labels, ann, conds, names, stored, nprops):
+        lab = ",".join('"%s":"%s"' % kv for kv in labels)
+        an = ",".join('"%s":"%s"' % kv for kv in ann)
+        cs = ",".join('{"type":"%s","status":"%s","lastTransitionTime":"%s","reason":"%s","message":"%s"}' % c
+                      for c in conds)
+        props = ",".join('"field%02d":{"type":"string","description":"field %d of %s","maxLength":%d}'
+                         % (k, k, name, 64 + k) for k in range(nprops))
+        nm = '"plural":"%s","singular":"%s","kind":"%s","listKind":"%sList"' % (
+            names["plural"], names["singular"], names["kind"], names["kind"])
+        if names.get("shortNames") is not None:
+            nm += ',"shortNames":[%s]' % ",".join('"%s"' % x for x in names["shortNames"])
+        if names.get("categories") is not None:
+            nm += ',"categories":[%s]' % ",".join('"%s"' % x for x in names["categories"])
+        sv = ",".join('"%s"' % v for v in stored)
+        return ('{"apiVersion":"apiextensions.k8s.io/v1","kind":"CustomResourceDefinition","metadata":{"name":'
+                '"%ss.example.dev","clusterName":"admin","uid":"7a1c%08x-8d1e-4c1b-9a61-0d1f2e3c4b5a",'
+                '"resourceVersion":"%d","generation":%d,"creationTimestamp":"2021-10-04T15:09:37Z","labels":{%s},'
+                '"annotations":{%s}},"spec":{"group":"example.dev","names":{%s},"scope":"Namespaced","versions":'
+                '[{"name":"v1","served":true,"storage":true,"schema":{"openAPIV3Schema":{"type":"object",'
+                '"properties":{"spec":{"type":"object","properties":{%s}},"status":{"type":"object",'
+                '"x-kubernetes-preserve-unknown-fields":true}}}},"subresources":{"status":{}}}],'
+                '"conversion":{"strategy":"None"}},"status":{"conditions":[%s],"acceptedNames":{%s},'
+                '"storedVersions":[%s]}}' % (name, rv & 0xFFFFFFFF, rv, gen, lab, an, nm, props, cs, nm, sv)).encode()
+
+    pairs, want = [], []
+    u = rng.random(n_pairs)
+    v = rng.random(n_pairs)
+    for i in range(n_pairs):
+        name = "widget%07d" % i
+        rv = 5000 + 11 * i
+        gen = 1 + (i % 4)
+        labels = [("kcp.dev/cluster", "lc-%05d" % (i % 10000)), ("app", "w%d" % (i % 97))]
+        ann = [("kcp.dev/schema", "v%d" % (i % 3))]
+        ts = "2021-10-%02dT%02d:%02d:%02dZ" % (1 + i % 28, i % 24, i % 60, (7 * i) % 60)
+        conds = [("NamesAccepted", "True", ts, "NoConflicts", "no conflicts found"),
+                 ("Established", "True", ts, "InitialNamesAccepted", "the initial names have been accepted")]
+        names = {"plural": name + "s", "singular": name, "kind": "W%07d" % i}
+        if i % 3 == 0:
+            names["shortNames"] = ["w%d" % i]
+        if i % 5 == 0:
+            names["categories"] = ["all"]
+        stored = ["v1"] if i % 4 else ["v1beta1", "v1"]
+        nprops = n_props
+        old = doc(name, rv, gen, labels, ann, conds, names, stored, nprops)
+        x = u[i]
+        nrv, ngen, nlab, nann, ncond, nnames, nstored = rv + 1, gen, labels, ann, list(conds), dict(names), stored
+        if x < 0.15:
+            nrv, exp = rv, 0
+        elif x < 0.35:
+            ngen, nprops, exp = gen + 1, n_props + 1, 1
+        elif x < 0.60:
+            y = v[i]
+            if y < 0.3:
+                c = ncond[1]
+                ncond[1] = (c[0], "False", "2021-11-01T00:00:00Z", "Terminating", "the object is being deleted")
+            elif y < 0.5:
+                nnames["kind"] = "X%07d" % i
+            elif y < 0.7:
+                nnames["shortNames"] = list(names.get("shortNames") or []) + ["x%d" % i]
+            elif y < 0.85:
+                nnames["categories"] = list(names.get("categories") or []) + ["kcp"]
+            else:
+                nstored = stored + ["v2"]
+            exp = 2
+        elif x < 0.75:
+            nann, exp = [("kcp.dev/schema", "v%d" % (i % 3 + 10))], 3
+        elif x < 0.90:
+            nlab, exp = labels[:1] + [("app", "moved")], 0   # the missing `!`: differing labels are ignored
+        else:
+            exp = 3                                           # equal labels: AnnotationOrLabelsOnlyChanged
+        new = doc(name, nrv, ngen, nlab, nann, ncond, nnames, nstored, nprops)
+        pairs.append((old, new))
+        want.append(exp)
+    return pairs, np.asarray(want, np.int32)

@@ -54,8 +54,20 @@ read (spec, metadata.name, creationTimestamp, ...) are not checked: Go's typed
 Unmarshal would reject those objects too, so no reference outcome exists for
 them, and the classification here follows the fields read (KAT
 "outside-domain-spec-type-error").  A root ``null`` (a zero object to Go's
-Unmarshal; never a watch event body) is reported as DECODE.  CustomResource-
-Definition events (the third kind, :186-199) are not covered.
+Unmarshal; never a watch event body) is reported as DECODE.
+
+* ``CustomResourceDefinition`` events (the third kind, :186-199; ``kind=
+  KIND_CRD``): the typed status is apiextensions/v1
+  ``CustomResourceDefinitionStatus`` (k8s.io/apiextensions-apiserver, pinned by
+  go.mod:32 to kcp-dev/kubernetes c954268bf177; not vendored in the reference,
+  restated from its published types): ``conditions`` (the same five fields),
+  ``acceptedNames`` -- a struct ``{plural, singular, shortNames []string, kind,
+  listKind, categories []string}`` (null leaves it as it is, a repeated key
+  merges into it) -- and ``storedVersions []string``.  ``[]string`` decodes
+  like ``conditions``: element i INTO the string already there (a null
+  element leaves it, so "" in a fresh backing array), Go's growth rule, a
+  later longer array exposing stale capacity.  Semantic.DeepEqual compares the
+  three fields with nil == empty slices.
 
 PARITY STATUS: no reference tests exist for the controller and Go is absent,
 so this restatement is pinned by the hand-written known-answer cases in
@@ -75,6 +87,10 @@ ACTION_NAMES = {IGNORE: "ignored", SPEC_CHANGED: "SpecChanged", STATUS_ONLY: "St
                 META_ONLY: "AnnotationOrLabelsOnlyChanged", CREATED: "Created", DECODE: "decode-error"}
 
 COND_FIELDS = ("type", "status", "lastTransitionTime", "reason", "message")
+# apiextensions/v1 CustomResourceDefinitionStatus / CustomResourceDefinitionNames field order (the fold lookup's order)
+CRD_STATUS_FIELDS = ("conditions", "acceptedNames", "storedVersions")
+CRD_NAMES_FIELDS = ("plural", "singular", "shortNames", "kind", "listKind", "categories")
+KIND_KCP, KIND_CRD = 0, 1
 META_FIELDS = ("resourceVersion", "generation", "labels", "annotations")
 INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
 ZERO_TIME = (-62135596800, 0)  # time.Time{}: 0001-01-01T00:00:00Z as (unix seconds, ns)
@@ -262,30 +278,35 @@ def _cond_into(c: _Cond, v: Any) -> None:
 
 class _Slice:
     """A Go slice header over a backing array (len, cap) -- enough of it to
-    reproduce decoding a repeated array key into the same field."""
+    reproduce decoding a repeated array key into the same field.  `zero` makes
+    an element's zero value, `into(cur, v)` decodes v into an element and
+    returns it (Go decodes element i INTO the value already there)."""
 
-    def __init__(self):
+    def __init__(self, zero=_Cond, into=None, what="conditions"):
         self.nil = True
-        self.backing: List[_Cond] = []  # len(backing) == cap
+        self.backing: List[Any] = []  # len(backing) == cap
         self.len = 0
+        self.zero = zero
+        self.into = into or _cond_elem
+        self.what = what
 
     def decode(self, v: Any) -> None:
         if v is None:
             self.nil, self.backing, self.len = True, [], 0
             return
         if isinstance(v, _Pairs) or not isinstance(v, list):
-            raise DecodeError("conditions is not an array")
+            raise DecodeError("%s is not an array" % self.what)
         i = 0
         for e in v:
-            if i >= len(self.backing):
+            if i >= len(self.backing):  # reflect growth: cap + cap/2, at least 4; the first len elements copied
                 newcap = max(4, len(self.backing) + len(self.backing) // 2)
-                nb = [_Cond() for _ in range(newcap)]
+                nb = [self.zero() for _ in range(newcap)]
                 for k in range(self.len):
                     nb[k] = self.backing[k]
                 self.backing = nb
             if i >= self.len:
                 self.len = i + 1
-            _cond_into(self.backing[i], e)
+            self.backing[i] = self.into(self.backing[i], e)
             i += 1
         if i < self.len:
             self.len = i
@@ -294,11 +315,56 @@ class _Slice:
         self.nil = False
 
     def value(self) -> Tuple:
-        return tuple(self.backing[k].key() for k in range(self.len))
+        return tuple(_key(self.backing[k]) for k in range(self.len))
 
 
-def extract(data: bytes) -> dict:
-    """The fields the classifier reads from one object, or DecodeError."""
+def _key(e: Any) -> Any:
+    return e.key() if isinstance(e, _Cond) else e
+
+
+def _cond_elem(c: _Cond, v: Any) -> _Cond:
+    _cond_into(c, v)
+    return c
+
+
+def _string_elem(cur: str, v: Any) -> str:
+    return _string(v, cur)  # null leaves the element as it is (the zero "" in a fresh backing array)
+
+
+def _strings() -> _Slice:
+    return _Slice(zero=str, into=_string_elem, what="[]string")
+
+
+class _Names:
+    """apiextensions/v1 CustomResourceDefinitionNames: plural, singular,
+    shortNames, kind, listKind, categories -- a struct, so a repeated
+    acceptedNames key merges into it and null leaves it as it is."""
+
+    def __init__(self):
+        self.s = {"plural": "", "singular": "", "kind": "", "listKind": ""}
+        self.shortNames = _strings()
+        self.categories = _strings()
+
+    def into(self, v: Any) -> None:
+        if v is None:
+            return
+        if not isinstance(v, _Pairs):
+            raise DecodeError("acceptedNames is not an object")
+        for f, x in _struct_members(v, CRD_NAMES_FIELDS):
+            if f in self.s:
+                self.s[f] = _string(x, self.s[f])
+            else:
+                getattr(self, f).decode(x)
+
+    def value(self) -> Tuple:
+        return (self.s["plural"], self.s["singular"], self.s["kind"], self.s["listKind"],
+                self.shortNames.value(), self.categories.value())
+
+
+def extract(data: bytes, kind: int = KIND_KCP) -> dict:
+    """The fields the classifier reads from one object, or DecodeError.
+    kind KIND_CRD reads a CustomResourceDefinition's status (conditions,
+    acceptedNames, storedVersions)."""
     if isinstance(data, str):
         data = data.encode("utf-8")
     root = _parse(data)
@@ -306,6 +372,8 @@ def extract(data: bytes) -> dict:
     labels: Optional[dict] = None
     ann: Optional[dict] = None
     conds = _Slice()
+    names = _Names()
+    stored = _strings()
     for name, v in _struct_members(root, ("metadata", "status")):
         if v is None:
             continue
@@ -321,32 +389,43 @@ def extract(data: bytes) -> dict:
                     labels = _string_map(x, labels)
                 else:
                     ann = _string_map(x, ann)
+        elif kind == KIND_CRD:
+            for f, x in _struct_members(v, CRD_STATUS_FIELDS):
+                if f == "conditions":
+                    conds.decode(x)
+                elif f == "acceptedNames":
+                    names.into(x)
+                else:
+                    stored.decode(x)
         else:
             for _, x in _struct_members(v, ("conditions",)):
                 conds.decode(x)
+    status: Tuple = (conds.value(),)
+    if kind == KIND_CRD:
+        status = (conds.value(), names.value(), stored.value())
     return {"resourceVersion": rv, "generation": gen, "labels": labels or {},
-            "annotations": ann or {}, "conditions": conds.value()}
+            "annotations": ann or {}, "conditions": conds.value(), "status": status}
 
 
-def classify(old: Optional[bytes], new: bytes) -> int:
-    """controller.go:238-295 for one Update event."""
+def classify(old: Optional[bytes], new: bytes, kind: int = KIND_KCP) -> int:
+    """controller.go:238-295 for one Update event of an object of `kind`."""
     try:
-        n = extract(new)
+        n = extract(new, kind)
         if old is None:
             return CREATED
-        o = extract(old)
+        o = extract(old, kind)
     except DecodeError:
         return DECODE
     if o["resourceVersion"] == n["resourceVersion"]:
         return IGNORE
     if o["generation"] != n["generation"]:
         return SPEC_CHANGED
-    if o["conditions"] != n["conditions"]:   # nil == empty (Semantic); times by instant
+    if o["status"] != n["status"]:   # Semantic.DeepEqual: nil == empty slices; times by instant
         return STATUS_ONLY
     if o["annotations"] != n["annotations"] or o["labels"] == n["labels"]:
         return META_ONLY
     return IGNORE
 
 
-def classify_batch(pairs: List[Tuple[Optional[bytes], bytes]]) -> List[int]:
-    return [classify(a, b) for a, b in pairs]
+def classify_batch(pairs: List[Tuple[Optional[bytes], bytes]], kind: int = KIND_KCP) -> List[int]:
+    return [classify(a, b, kind) for a, b in pairs]

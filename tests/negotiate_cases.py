@@ -133,3 +133,117 @@ def cases():
     out.append(("repeated-rv-last-wins", obj(rv="3"),
                 b'{"metadata": {"resourceVersion": "1", "resourceVersion": "3", "generation": 9}}', IGNORE))
     return out
+
+
+# ---------------------------------------------------------------- CustomResourceDefinition events (controller.go:186-199)
+NAMES = {"plural": "widgets", "singular": "widget", "kind": "Widget", "listKind": "WidgetList"}
+EST = [cond(t="NamesAccepted", reason="NoConflicts", msg="no conflicts found"),
+       cond(t="Established", reason="InitialNamesAccepted", msg="the initial names have been accepted")]
+_ABSENT = object()
+
+
+def crd(rv="1", gen=1, labels=None, ann=None, conds=EST, names=_ABSENT, stored=_ABSENT, status_extra=None):
+    """An apiextensions/v1 CustomResourceDefinition as the API server writes it
+    (names / stored default to NAMES / ["v1"]; pass None for a JSON null,
+    _ABSENT -- the default sentinel -- via absent=... below)."""
+    meta = {"name": "widgets.example.dev", "clusterName": "admin", "resourceVersion": rv, "generation": gen}
+    if labels is not None:
+        meta["labels"] = labels
+    if ann is not None:
+        meta["annotations"] = ann
+    st = {}
+    if conds is not None:
+        st["conditions"] = conds
+    st["acceptedNames"] = dict(NAMES) if names is _ABSENT else names
+    st["storedVersions"] = ["v1"] if stored is _ABSENT else stored
+    if status_extra:
+        st.update(status_extra)
+    return json.dumps({"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition", "metadata": meta,
+                       "spec": {"group": "example.dev", "names": dict(NAMES), "scope": "Namespaced",
+                                "versions": [{"name": "v1", "served": True, "storage": True,
+                                              "schema": {"openAPIV3Schema": {"type": "object"}}}]},
+                       "status": st}).encode()
+
+
+def _drop(doc, key):
+    """remove `"key": <value>, ` / `, "key": <value>` from a compact status (value: a JSON list/object/string)"""
+    d = json.loads(doc)
+    d["status"].pop(key)
+    return json.dumps(d).encode()
+
+
+def crd_cases():
+    """(name, old, new, expected) for kind CustomResourceDefinition; the typed
+    status is {conditions, acceptedNames {plural, singular, shortNames, kind,
+    listKind, categories}, storedVersions}."""
+    n2 = dict(NAMES, shortNames=["wd"], categories=["all"])
+    out = [
+        ("crd-created", None, crd(), CREATED),
+        ("crd-same-rv", crd(rv="4"), crd(rv="4", gen=2, names=dict(NAMES, plural="x")), IGNORE),
+        ("crd-gen-changed", crd(rv="1"), crd(rv="2", gen=2, stored=["v1", "v2"]), SPEC),
+        ("crd-established", crd(rv="1", conds=[]), crd(rv="2"), STATUS),
+        ("crd-plural-changed", crd(rv="1"), crd(rv="2", names=dict(NAMES, plural="widgetz")), STATUS),
+        ("crd-listkind-changed", crd(rv="1"), crd(rv="2", names=dict(NAMES, listKind="Widgets")), STATUS),
+        ("crd-names-absent-vs-null", _drop(crd(rv="1"), "acceptedNames"), crd(rv="2", names=None), META),
+        ("crd-names-absent-vs-empty", _drop(crd(rv="1"), "acceptedNames"), crd(rv="2", names={}), META),
+        ("crd-names-null-vs-set", crd(rv="1", names=None), crd(rv="2"), STATUS),
+        ("crd-shortnames-nil-vs-empty", crd(rv="1"), crd(rv="2", names=dict(NAMES, shortNames=[])), META),
+        ("crd-shortnames-null-vs-empty", crd(rv="1", names=dict(NAMES, shortNames=None)),
+         crd(rv="2", names=dict(NAMES, shortNames=[])), META),
+        ("crd-shortnames-added", crd(rv="1", names=dict(NAMES, shortNames=[])), crd(rv="2", names=n2), STATUS),
+        ("crd-shortnames-order", crd(rv="1", names=dict(NAMES, shortNames=["a", "b"])),
+         crd(rv="2", names=dict(NAMES, shortNames=["b", "a"])), STATUS),
+        ("crd-categories-changed", crd(rv="1", names=n2), crd(rv="2", names=dict(n2, categories=["all", "x"])), STATUS),
+        ("crd-categories-equal", crd(rv="1", names=n2), crd(rv="2", names=dict(n2)), META),
+        ("crd-stored-appended", crd(rv="1"), crd(rv="2", stored=["v1", "v2"]), STATUS),
+        ("crd-stored-null-vs-empty", crd(rv="1", stored=None), crd(rv="2", stored=[]), META),
+        ("crd-stored-absent-vs-null", _drop(crd(rv="1"), "storedVersions"), crd(rv="2", stored=None), META),
+        ("crd-stored-null-elem", crd(rv="1", stored=["", "v1"]), crd(rv="2", stored=[None, "v1"]), META),
+        ("crd-stored-empty-string-vs-none", crd(rv="1", stored=[]), crd(rv="2", stored=[""]), STATUS),
+        ("crd-stored-number", crd(rv="1"), crd(rv="2", stored=[1]), DECODE),
+        ("crd-stored-object", crd(rv="1"), crd(rv="2", stored={"v1": True}), DECODE),
+        ("crd-names-not-object", crd(rv="1"), crd(rv="2", names="widgets"), DECODE),
+        ("crd-names-array", crd(rv="1"), crd(rv="2", names=[]), DECODE),
+        ("crd-listkind-number", crd(rv="1"), crd(rv="2", names=dict(NAMES, listKind=3)), DECODE),
+        ("crd-shortname-object", crd(rv="1"), crd(rv="2", names=dict(NAMES, shortNames=[{}])), DECODE),
+        ("crd-plural-null-noop", crd(rv="1", names=dict(NAMES, plural="")), crd(rv="2", names=dict(NAMES, plural=None)),
+         META),
+        ("crd-names-fold-key", crd(rv="1"),
+         crd(rv="2").replace(b'"plural": "widgets", "singular": "widget", "kind": "Widget", "listKind": "WidgetList"}, '
+                             b'"storedVersions"',
+                             b'"PLURAL": "widgets", "singular": "widget", "kind": "Widget", "listKind": "WidgetList"}, '
+                             b'"storedVersions"'), META),
+        ("crd-status-fold-key", crd(rv="1"), crd(rv="2").replace(b'"storedVersions"', b'"StoredVersions"'), META),
+        ("crd-names-unknown-field", crd(rv="1"), crd(rv="2", names=dict(NAMES, extra="x")), META),
+        ("crd-status-unknown-field", crd(rv="1"), crd(rv="2", status_extra={"phase": "x"}), META),
+        ("crd-cond-time-same-instant", crd(rv="1", conds=[cond(t="Established", ltt="2021-10-04T15:09:37Z")]),
+         crd(rv="2", conds=[cond(t="Established", ltt="2021-10-04T16:09:37+01:00")]), META),
+        ("crd-meta-labels-changed-only", crd(rv="1", labels=L, ann=A), crd(rv="2", labels={"a": "b"}, ann=A), IGNORE),
+    ]
+    # repeated keys: Go decodes again into the same field
+    base = b'{"metadata": {"resourceVersion": "2", "generation": 1}, "status": {%s}}'
+    out.append(("crd-repeated-names-merge", crd(rv="1", conds=None, stored=None),
+                base % (b'"acceptedNames": {"plural": "widgets", "kind": "Nope"}, "acceptedNames": {"singular": '
+                        b'"widget", "kind": "Widget", "listKind": "WidgetList"}'), META))
+    out.append(("crd-repeated-names-null-keeps", crd(rv="1", conds=None, stored=None),
+                base % (b'"acceptedNames": {"plural": "widgets", "singular": "widget", "kind": "Widget", '
+                        b'"listKind": "WidgetList"}, "acceptedNames": null'), META))
+    out.append(("crd-repeated-stored-stale-capacity", crd(rv="1", conds=None, names=None, stored=["x", "b"]),
+                base % b'"storedVersions": ["a", "b"], "storedVersions": ["x"], "storedVersions": [null, null]', META))
+    out.append(("crd-repeated-shortnames-stale-capacity", crd(rv="1", conds=None, stored=None,
+                                                           names=dict(NAMES, shortNames=["p", "q", "r"])),
+                base % (b'"acceptedNames": {"plural": "widgets", "singular": "widget", "kind": "Widget", "listKind": '
+                        b'"WidgetList", "shortNames": ["a", "q", "r"]}, "acceptedNames": {"shortNames": ["p"]}, '
+                        b'"acceptedNames": {"shortNames": [null, null, null]}'), META))
+    return out
+
+
+def kcp_kind_ignores_crd_status():
+    """The same CRD documents classified as an APIResourceImport (kind 0): only
+    status.conditions is read, so acceptedNames / storedVersions changes are
+    invisible (metadata then decides)."""
+    return [
+        ("kcp-kind-plural-changed", crd(rv="1"), crd(rv="2", names=dict(NAMES, plural="widgetz")), META),
+        ("kcp-kind-stored-number", crd(rv="1"), crd(rv="2", stored=[1]), META),
+        ("kcp-kind-established", crd(rv="1", conds=[]), crd(rv="2"), STATUS),
+    ]

@@ -97,3 +97,65 @@ def test_condition_times_vs_oracle():
     st = _check(eng, pairs)
     assert st.n_host < len(pairs) // 3  # most shapes are parsed on the device, not deferred
     eng.close()
+
+
+# ---------------------------------------------------------------- CustomResourceDefinition events (controller.go:186-199)
+def _check_kinds(eng, pairs, kinds):
+    nb = eng.nbatch(pairs, kinds)
+    try:
+        nb.run()
+        got = nb.fetch().tolist()
+        st = nb.stats()
+    finally:
+        nb.close()
+    ks = [kinds] * len(pairs) if isinstance(kinds, int) else list(kinds)
+    want = [N.classify(a, b, k) for (a, b), k in zip(pairs, ks)]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, (len(bad), bad[:5], [(got[i], want[i], pairs[i]) for i in bad[:2]])
+    return st
+
+
+def test_crd_kat_batch():
+    eng = G.Engine(device=0)
+    _check_kinds(eng, [(a, b) for _, a, b, _ in C.crd_cases()], G.NEG_KIND_CRD)
+    _check_kinds(eng, [(a, b) for _, a, b, _ in C.kcp_kind_ignores_crd_status()], G.NEG_KIND_API)
+    eng.close()
+
+
+def test_crd_population_all_on_device():
+    eng = G.Engine(device=0)
+    pairs, want = S.crd_population(8000, seed=9)
+    st = _check_kinds(eng, pairs, G.NEG_KIND_CRD)
+    assert st.n_host == 0
+    assert eng.classify_updates(pairs, G.NEG_KIND_CRD).tolist() == want.tolist()
+    eng.close()
+
+
+def test_crd_fuzz():
+    from tests.test_negotiate import crd_fuzz_pairs
+    eng = G.Engine(device=0)
+    _check_kinds(eng, crd_fuzz_pairs(4000, 20211004 + 74), G.NEG_KIND_CRD)
+    eng.close()
+
+
+def test_mixed_kinds_batch():
+    eng = G.Engine(device=0)
+    api, _ = S.negotiate_population(3000, seed=10, variants=False)
+    crd, _ = S.crd_population(3000, seed=10, n_props=4)
+    pairs = [p for ab in zip(api, crd) for p in ab]
+    kinds = [k for _ in range(3000) for k in (G.NEG_KIND_API, G.NEG_KIND_CRD)]
+    st = _check_kinds(eng, pairs, kinds)
+    assert st.n_host == 0
+    eng.close()
+
+
+def test_crd_long_lists_defer():
+    """More than kNegMaxList (8) stored versions / short names: the host path decides."""
+    eng = G.Engine(device=0)
+    many = ["v%d" % i for i in range(10)]
+    pairs = [(C.crd(rv="1", stored=many), C.crd(rv="2", stored=many + ["v10"])),
+             (C.crd(rv="1", names=dict(C.NAMES, shortNames=many)), C.crd(rv="2", names=dict(C.NAMES, shortNames=many))),
+             (C.crd(rv="1", stored=many[:8]), C.crd(rv="2", stored=many[:8]))]
+    st = _check_kinds(eng, pairs, G.NEG_KIND_CRD)
+    assert st.n_host == 2
+    eng.close()

@@ -160,3 +160,87 @@ def test_host_batch_entry_point_matches_oracle():
     hp = G.HostPairs(pairs)
     got = hp.classify(threads=4).tolist()
     assert got == [N.classify(a, b) for a, b in pairs]
+
+
+# ---------------------------------------------------------------- CustomResourceDefinition events (controller.go:186-199)
+CRD_EDITS = [
+    (b'"acceptedNames":{', b'"AcceptedNames":{'), (b'"acceptedNames":{', b'"acceptedNames":null,"acceptedNames":{'),
+    (b'"acceptedNames":{', b'"acceptedNames":{"plural":"zz"},"acceptedNames":{'),
+    (b'"acceptedNames":{"plural"', b'"acceptedNames":{"PLURAL"'), (b'"storedVersions":[', b'"storedVersions":[null,'),
+    (b'"storedVersions":[', b'"storedVersions":["a","b","c"],"storedVersions":['),
+    (b'"storedVersions":[', b'"storedVersions":[1,'), (b'"storedVersions":[', b'"storedVersions":["\\u0076",'),
+    (b'"storedVersions":["v1"]', b'"storedVersions":null'), (b'"storedVersions":["v1"]', b'"storedVersions":[]'),
+    (b'"storedVersions":[', b'"storedversions":["x"],"storedVersions":['),
+    (b',"kind":"W', b',"kind":null,"x":"W'), (b',"kind":"W', b',"kind":5,"x":"W'),
+    (b'"listKind":"', b'"listKind":"\\n'), (b'"shortNames":[', b'"shortNames":[null,'),
+    (b'"shortNames":[', b'"shortNames":{},"x":['), (b'"categories":[', b'"categories":["a","b","c","d","e","f","g","h",'),
+    (b'"conditions":[', b'"conditions":[null,'), (b'"status":{"conditions"', b'"status":{"acceptedNames":"x","conditions"'),
+    (b'"status":{"conditions"', b'"status":{"acceptedNames":[],"conditions"'),
+    (b'"status":{"conditions"', b'"status":{"extra":{"a":[1,2]},"conditions"'),
+    (b'"singular":"', b'"singular":"x","singular":"'), (b'"metadata":{', b'"Metadata":{'),
+]
+
+
+def crd_fuzz_pairs(n, seed):
+    pairs, _ = S.crd_population(n, seed=seed, n_props=3)
+    rng = random.Random(seed)
+    out = []
+    for a, b in pairs:
+        r = rng.random()
+        if r < 0.3:
+            x, y = rng.choice(CRD_EDITS)
+            b = b.replace(x, y, 1)
+        elif r < 0.45:
+            x, y = rng.choice(CRD_EDITS)
+            a = a.replace(x, y, 1)
+        elif r < 0.5:
+            a = None
+        out.append((a, b))
+    return out
+
+
+@pytest.mark.parametrize("case", C.crd_cases(), ids=lambda c: c[0])
+def test_crd_oracle_kat(case):
+    name, a, b, want = case
+    assert N.classify(a, b, N.KIND_CRD) == want
+
+
+@pytest.mark.parametrize("case", C.crd_cases(), ids=lambda c: c[0])
+def test_crd_host_kat(case):
+    name, a, b, want = case
+    assert G.negotiate_pair_host(a, b, G.NEG_KIND_CRD) == want
+
+
+@pytest.mark.parametrize("case", C.kcp_kind_ignores_crd_status(), ids=lambda c: c[0])
+def test_kind_selects_typed_status(case):
+    """The same CRD documents typed as an APIResourceImport read only status.conditions."""
+    name, a, b, want = case
+    assert N.classify(a, b, N.KIND_KCP) == want
+    assert G.negotiate_pair_host(a, b) == want
+    assert G.negotiate_pair_host(a, b, G.NEG_KIND_API) == want
+
+
+def test_crd_population_matches_design():
+    pairs, want = S.crd_population(1500, seed=12)
+    assert [N.classify(a, b, N.KIND_CRD) for a, b in pairs] == want.tolist()
+
+
+def test_crd_host_matches_oracle_fuzz():
+    pairs = crd_fuzz_pairs(2500, 20211004 + 73)
+    got = G.HostPairs(pairs, G.NEG_KIND_CRD).classify(threads=4).tolist()
+    want = [N.classify(a, b, N.KIND_CRD) for a, b in pairs]
+    bad = [i for i in range(len(pairs)) if got[i] != want[i]]
+    assert not bad, (len(bad), pairs[bad[0]], got[bad[0]], want[bad[0]])
+    assert len(set(want)) >= 5  # the edits reach every outcome, DECODE included
+
+
+def test_mixed_kinds_host_batch():
+    """One batch holding both kinds: each pair decoded with its own kind's typed status."""
+    api = [(a, b) for _, a, b, _ in C.cases()]
+    crd = [(a, b) for _, a, b, _ in C.crd_cases()]
+    pairs = [p for ab in zip(api, crd) for p in ab]
+    kinds = [k for _ in zip(api, crd) for k in (G.NEG_KIND_API, G.NEG_KIND_CRD)]
+    got = G.HostPairs(pairs, kinds).classify(threads=2).tolist()
+    assert got == [N.classify(a, b, k) for (a, b), k in zip(pairs, kinds)]
+    with pytest.raises(G.GpuDiffError):
+        G.HostPairs(pairs[:2], [0, 7]).classify()
