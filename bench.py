@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--encode", default="device", choices=["device", "host"],
                     help="config5: encode events on the GPU (K0, raw JSON up) or on the host")
     ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")
+    ap.add_argument("--kind", default="api", choices=["api", "crd", "mixed"],
+                    help="negotiate: APIResourceImport/NegotiatedAPIResource events, CustomResourceDefinition events, "
+                         "or both interleaved in one batch")
     ap.add_argument("--clusters", type=int, default=0)
     ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
                     help="strong: the config's population split N ways (the metric's 10M/100k node-wide; "

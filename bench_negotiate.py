@@ -5,16 +5,20 @@ k_encode_docs: typed-decode fields of both sides from the raw JSON) + K14 (the
 controller.go:253-283 decision per pair).
 
 The population is `--pairs` (old, new) Update events of APIResourceImport /
-NegotiatedAPIResource objects, API-server JSON (~1.2 KB each; kcp.dev labels, a
-CommonAPIResourceSpec with column definitions, 1-3 status conditions), with the
-event mix of kcp_amd.synth.negotiate_population.  The documents are uploaded
+NegotiatedAPIResource objects (`--kind api`, the default), API-server JSON
+(~1.2 KB each; kcp.dev labels, a CommonAPIResourceSpec with column
+definitions, 1-3 status conditions), with the event mix of
+kcp_amd.synth.negotiate_population; `--kind crd`: CustomResourceDefinition
+events (~2.4 KB: an openAPIV3Schema, status conditions + acceptedNames +
+storedVersions; kcp_amd.synth.crd_population); `--kind mixed`: both,
+interleaved in one batch.  The documents are uploaded
 once (gpudiff_nbatch_create); a step is one K13 + K14 pass over all of them,
 resident in HBM.
 
 Reported: pairs/s (value: a step = K13 + K14 + the actions' copy-back + the
 host path for K13's deferrals, i.e. every pair classified inside the timed
-step), the device-only rate beside it, K13's HBM GB/s (JSON read + 944 B per
-document written) against the roofline, K14 time, checks (every action vs the
+step), the device-only rate beside it, K13's HBM GB/s (JSON read + 1184 B
+(NegOut) per document written) against the roofline, K14 time, checks (every action vs the
 generator's designed outcome, a sample vs the Python oracle), and the CPU
 baseline: the product's Go-exact C++ host path (gpudiff_classify_updates_host,
 typed decode of both sides + classification, decode timed) on every host CPU.
@@ -45,13 +49,26 @@ def run(args):
     from kcp_amd import synth as S
 
     t0 = time.time()
-    pairs, want = S.negotiate_population(args.pairs)
+    kind = getattr(args, "kind", "api")
+    if kind == "api":
+        pairs, want = S.negotiate_population(args.pairs)
+        kinds = [G.NEG_KIND_API] * len(pairs)
+    elif kind == "crd":
+        pairs, want = S.crd_population(args.pairs)
+        kinds = [G.NEG_KIND_CRD] * len(pairs)
+    else:
+        pa, wa = S.negotiate_population(args.pairs // 2)
+        pc, wc = S.crd_population(args.pairs - args.pairs // 2)
+        pairs = [p for ab in zip(pa, pc) for p in ab] + pc[len(pa):]
+        want = np.asarray([w for ab in zip(wa.tolist(), wc.tolist()) for w in ab] + wc.tolist()[len(pa):], np.int32)
+        kinds = [k for _ in range(len(pa)) for k in (G.NEG_KIND_API, G.NEG_KIND_CRD)] + \
+            [G.NEG_KIND_CRD] * (len(pc) - len(pa))
     N = len(pairs)
     json_bytes = sum(len(a) + len(b) for a, b in pairs)
     log("%d Update pairs, %.2f GB of JSON, generated in %.1f s" % (N, json_bytes / 1e9, time.time() - t0))
     torch.cuda.set_device(0)
     eng = G.Engine(device=0, timing=True)
-    nb = eng.nbatch(pairs)
+    nb = eng.nbatch(pairs, kinds)
     st0 = nb.stats()
     log("resident: scratch %.2f GB" % (st0.scratch_bytes / 1e9))
 
@@ -65,7 +82,7 @@ def run(args):
     from oracle import negotiate_oracle as NO
     n_s = min(args.cpu_sample, N)
     t1 = time.perf_counter()
-    sw = [NO.classify(a, b) for a, b in pairs[:n_s]]
+    sw = [NO.classify(a, b, k) for (a, b), k in zip(pairs[:n_s], kinds[:n_s])]
     t_or = time.perf_counter() - t1
     sample_ok = sw == got[:n_s].tolist()
     log("sample vs oracle:", sample_ok)
@@ -93,7 +110,7 @@ def run(args):
     runs = s_after.runs - s_before.runs
     k13_ms = (s_after.k13_ms * s_after.runs - s_before.k13_ms * s_before.runs) / max(1, runs)
     k14_ms = (s_after.k14_ms * s_after.runs - s_before.k14_ms * s_before.runs) / max(1, runs)
-    alg = json_bytes + 944 * 2 * N
+    alg = json_bytes + G.NEGOUT_BYTES * 2 * N
     achieved = alg / (k13_ms * 1e-3) / 1e9
     value = N * args.steps / dt
 
@@ -101,7 +118,7 @@ def run(args):
     if not args.no_cpu_baseline:
         T = len(os.sched_getaffinity(0))
         n_c = min(N, 20 * args.cpu_sample)
-        hp = G.HostPairs(pairs[:n_c])
+        hp = G.HostPairs(pairs[:n_c], kinds[:n_c])
         hp.classify(threads=T)  # warm
         reps, t_c = 0, time.perf_counter()
         while True:
@@ -131,9 +148,11 @@ def run(args):
                   "+ achieved HBM GB/s",
         "value": value, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic (APIResourceImport / NegotiatedAPIResource Update pairs, seeded event mix)",
-        "config": {"workload": "negotiate: %d Update pairs (%.2f GB JSON) resident in HBM, one K13+K14 pass per step"
-                               % (N, json_bytes / 1e9)},
+        "dtype": "u8", "data": "synthetic (%s Update pairs, seeded event mix)" % {
+            "api": "APIResourceImport / NegotiatedAPIResource", "crd": "CustomResourceDefinition",
+            "mixed": "APIResourceImport / NegotiatedAPIResource and CustomResourceDefinition"}[kind],
+        "config": {"workload": "negotiate (kind %s): %d Update pairs (%.2f GB JSON) resident in HBM, one K13+K14 "
+                               "pass per step" % (kind, N, json_bytes / 1e9)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_encode_docs<negotiate> (K13)",
                      "bytes_per_launch": alg, "avg_launch_ms": k13_ms, "launches_per_step": 1,

@@ -492,17 +492,35 @@ const (
 	NegDecode  = int32(C.GPUDIFF_NEG_DECODE)  // a side not valid JSON / not an object, or a field read that fails Go's typed decode
 )
 
+// The typed object of an event (toQueueElementType, controller.go:185-236).
+const (
+	KindAPIResource = uint8(C.GPUDIFF_NEG_KIND_API) // *APIResourceImport, *NegotiatedAPIResource
+	KindCRD         = uint8(C.GPUDIFF_NEG_KIND_CRD) // *apiextensionsv1.CustomResourceDefinition
+)
+
 // ClassifyUpdates is the batch form of the "Update" branch of
 // Controller.enqueue (controller.go:253-283) for APIResourceImport /
 // NegotiatedAPIResource JSON: one action per (olds[i], news[i]); olds[i] == nil
 // means no old object.  Kernels K13 + K14, host path for K13's deferrals.
 func (e *Engine) ClassifyUpdates(olds, news [][]byte) ([]int32, error) {
+	return e.ClassifyUpdatesKinds(nil, olds, news)
+}
+
+// ClassifyUpdatesKinds is ClassifyUpdates with each event's kind (KindAPIResource
+// or KindCRD; nil: all KindAPIResource), so one batch can carry the events of
+// all three informers the controller watches.
+func (e *Engine) ClassifyUpdatesKinds(kinds []uint8, olds, news [][]byte) ([]int32, error) {
 	n := len(news)
 	if n == 0 {
 		return nil, nil
 	}
-	if len(olds) != n {
+	if len(olds) != n || (kinds != nil && len(kinds) != n) {
 		return nil, errOf(C.GPUDIFF_E_INVAL)
+	}
+	var kp *C.uint8_t
+	if kinds != nil {
+		kp = (*C.uint8_t)(C.CBytes(kinds))
+		defer C.free(unsafe.Pointer(kp))
 	}
 	ptrSz := C.size_t(unsafe.Sizeof(uintptr(0)))
 	lenSz := C.size_t(unsafe.Sizeof(C.size_t(0)))
@@ -532,7 +550,7 @@ func (e *Engine) ClassifyUpdates(olds, news [][]byte) ([]int32, error) {
 	actions := make([]int32, n)
 	e.mu.Lock()
 	defer e.mu.Unlock()
-	rc := C.gpudiff_classify_updates(e.ctx, (**C.uint8_t)(optr), (*C.size_t)(olen), (**C.uint8_t)(nptr),
+	rc := C.gpudiff_classify_updates_kinds(e.ctx, kp, (**C.uint8_t)(optr), (*C.size_t)(olen), (**C.uint8_t)(nptr),
 		(*C.size_t)(nlen), C.size_t(n), (*C.int32_t)(unsafe.Pointer(&actions[0])))
 	if err := errOf(rc); err != nil {
 		return nil, err

@@ -495,6 +495,7 @@ class ObjectStore:
 
 
 NEG_KIND_API, NEG_KIND_CRD = 0, 1  # GPUDIFF_NEG_KIND_*: APIResourceImport/NegotiatedAPIResource, CRD
+NEGOUT_BYTES = 1184  # K13's per-document record (kcp_amd/csrc/tokenize.h NegOut)
 
 
 class Engine:
