@@ -76,6 +76,21 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 // the wave's own global writes become visible to its other lanes
 __device__ __forceinline__ void wave_sync() { __threadfence_block(); }
+// set bits of m in the lanes below this one
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// whole-wave lane shifts (DPP wave_shr:1 / wave_shl:1): lane i gets v of lane
+// i - 1 (i + 1); the lane without a source gets `fill`
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130, 0xF, 0xF, false);
+}
+// LDS written by this wave's lanes is read by its other lanes: LDS executes a
+// wave's operations in order, so only the compiler must not reorder
+__device__ __forceinline__ void lds_order() { __asm__ volatile("" ::: "memory"); }
 
 // unaligned 8-byte read; up to 15 bytes past p must be readable
 __device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {

@@ -121,34 +121,54 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         }
     };
     // ------------------------------------------------------------ phase 1: structural scan
-    // The document streams through a 2 x 1 KiB LDS ring (one 16-B load per
-    // lane per KiB, the next KiB staged before the current one is scanned, so
-    // an opening quote can look 12 bytes ahead for the region keywords).
+    // One byte per lane per 64-byte step.  Byte classes are VALU compares (their
+    // ballots are the step's masks), the in-string state is the parity of an
+    // mbcnt of unescaped quotes, token codes are chosen per lane without
+    // branches.  The document sits in a 4 x 1 KiB LDS ring: up to 4 KiB is
+    // staged in one go; past that, chunk ch + 1 (the lookahead of chunk ch) is
+    // written from registers loaded one chunk earlier, so no step waits on HBM.
     uint8_t* ring = lds;
     uint32_t ntok = 0;
-    uint64_t esc_carry = 0, str_carry = 0, atom_carry = 0;
+    uint64_t esc_carry = 0, atom_carry = 0;
+    uint32_t str_par = 0;
     uint32_t last_open_idx = NONE, last_open_pos = 0, last_marked = NONE;
     bool ctl_in_string = false;
     const uint32_t nchunks = (len + 1023u) >> 10;
-    auto stage = [&](uint32_t ch) {
+    auto ld_chunk = [&](uint32_t ch) -> u32x4 {
         const uint32_t o = (ch << 10) + lane * 16u;
         u32x4 v = {0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u};
         if (o < len) v = *(const u32x4*)(d + o);  // d is 16-B aligned, kTokSlack readable past len
-        *(u32x4*)(ring + ((ch & 1u) << 10) + lane * 16u) = v;
+        return v;
     };
-    auto rb = [&](uint32_t p) -> uint32_t { return p < len ? (uint32_t)ring[p & 2047u] : 0x20u; };
-    if (nchunks) stage(0);
+    auto put_chunk = [&](uint32_t ch, u32x4 v) { *(u32x4*)(ring + ((ch & 3u) << 10) + lane * 16u) = v; };
+    {
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            if (j < nchunks) v[j] = ld_chunk(j);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            if (j < nchunks) put_chunk(j, v[j]);
+    }
+    u32x4 pre = {0u, 0u, 0u, 0u};
+    if (nchunks > 4) pre = ld_chunk(4);
+    lds_order();
+    auto ring32 = [&](uint32_t p) -> uint32_t { return *(const uint32_t*)(ring + (p & 4095u)); };
     for (uint32_t ch = 0; ch < nchunks; ch++) {
-        if (ch + 1 < nchunks) stage(ch + 1);
-        wave_sync();
+        if (ch >= 3 && ch + 1 < nchunks) {  // the lookahead chunk, loaded during chunk ch - 1
+            put_chunk(ch + 1, pre);
+            if (ch + 2 < nchunks) pre = ld_chunk(ch + 2);
+            lds_order();
+        }
         const uint32_t bend = min(len, (ch + 1) << 10);
         for (uint32_t b = ch << 10; b < bend; b += 64) {
             const uint32_t pos = b + lane;
-            const uint32_t c = rb(pos);
+            const uint32_t c = pos < len ? (uint32_t)ring[pos & 4095u] : 0x20u;
             const uint64_t bs = ballot(c == '\\');
             const uint64_t qt = ballot(c == '"');
-            const uint64_t st = ballot(c == '{' || c == '}' || c == '[' || c == ']' || c == ':' || c == ',');
-            const uint64_t wsm = ballot(is_ws(c));
+            const uint32_t cb = c & 0xDFu;  // '[' ']' and '{' '}' fold together
+            const uint64_t st = ballot(cb == '[' || cb == ']' || c == ':' || c == ',');
+            const uint64_t wsm = ballot(c == ' ' || c == '\n' || c == '\r' || c == '\t');
             const uint64_t ctl = ballot(c < 0x20u);  // inside a string every control byte is an error
             const uint64_t hi = ballot(c >= 0x80u);
             // escaped characters: an unescaped backslash escapes the next byte
@@ -162,15 +182,11 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 else esc |= 1ull << (i + 1);
             }
             const uint64_t q = qt & ~esc;
-            uint64_t x = q;
-            x ^= x << 1;
-            x ^= x << 2;
-            x ^= x << 4;
-            x ^= x << 8;
-            x ^= x << 16;
-            x ^= x << 32;
-            const uint64_t instr = x ^ str_carry;  // opening quote + string body
-            str_carry = (instr >> 63) ? ~0ull : 0ull;
+            // inside a string (its opening quote included, its closing quote not):
+            // the parity of the unescaped quotes up to and including this byte
+            const uint32_t par = (mbcnt64(q) + (uint32_t)(c == '"' && !((esc >> lane) & 1ull)) + str_par) & 1u;
+            const uint64_t instr = ballot(par != 0u);
+            str_par = (uint32_t)(instr >> 63);
             const uint64_t valid = mask_lt(len - b);
             const uint64_t opens = q & instr, closes = q & ~instr;
             const uint64_t structural = st & ~instr & valid;
@@ -196,47 +212,25 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 marks = nx ? (marks & ~mask_lt((uint32_t)__builtin_ctzll(nx))) : 0ull;
             }
             if ((tokens >> lane) & 1ull) {
-                const uint32_t idx = ntok + popc64(tokens & mask_lt(lane));
-                uint32_t code = c;
-                if ((closes >> lane) & 1ull) {
-                    code = TK_CLOSEQ;
-                } else if ((slow_opens >> lane) & 1ull) {
-                    code = TK_OPENQ_SLOW;
-                } else if ((opens >> lane) & 1ull) {
-                    // region keywords (an exact string: its closing quote follows the word);
-                    // the 13 bytes after the quote come from three aligned LDS words
-                    const uint32_t a = (pos + 1u) & ~7u, sh = ((pos + 1u) & 7u) * 8u;
-                    const uint64_t w0 = *(const uint64_t*)(ring + (a & 2047u));
-                    const uint64_t w1 = *(const uint64_t*)(ring + ((a + 8u) & 2047u));
-                    const uint64_t w2 = *(const uint64_t*)(ring + ((a + 16u) & 2047u));
-                    const uint64_t k0 = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0;
-                    const uint64_t k1 = sh ? (w1 >> sh) | (w2 << (64u - sh)) : w1;
-                    if (pos + 13u < len) {  // all compared bytes inside the document
-                        if (k0 == 0x617461646174656dull && (k1 & 0xFF) == '"') code = TK_KEY_META;
-                        else if ((k0 & 0xFFFFFFFFFFFFFFull) == 0x22737574617473ull) code = TK_KEY_STATUS;
-                        else if ((k0 & 0xFFFFFFFFFFFFFFull) == 0x22736c6562616cull) code = TK_KEY_LABELS;
-                        else if (k0 == 0x697461746f6e6e61ull && (k1 & 0xFFFFFFFFull) == 0x22736e6full)
-                            code = TK_KEY_ANNOT;
-                    } else {
-                        const uint32_t c1 = rb(pos + 1);
-                        if (c1 == 's' && rb(pos + 2) == 't' && rb(pos + 3) == 'a' && rb(pos + 4) == 't' &&
-                            rb(pos + 5) == 'u' && rb(pos + 6) == 's' && rb(pos + 7) == '"')
-                            code = TK_KEY_STATUS;
-                        else if (c1 == 'm' && rb(pos + 2) == 'e' && rb(pos + 3) == 't' && rb(pos + 4) == 'a' &&
-                                 rb(pos + 5) == 'd' && rb(pos + 6) == 'a' && rb(pos + 7) == 't' &&
-                                 rb(pos + 8) == 'a' && rb(pos + 9) == '"')
-                            code = TK_KEY_META;
-                        else if (c1 == 'l' && rb(pos + 2) == 'a' && rb(pos + 3) == 'b' && rb(pos + 4) == 'e' &&
-                                 rb(pos + 5) == 'l' && rb(pos + 6) == 's' && rb(pos + 7) == '"')
-                            code = TK_KEY_LABELS;
-                        else if (c1 == 'a' && rb(pos + 2) == 'n' && rb(pos + 3) == 'n' && rb(pos + 4) == 'o' &&
-                                 rb(pos + 5) == 't' && rb(pos + 6) == 'a' && rb(pos + 7) == 't' &&
-                                 rb(pos + 8) == 'i' && rb(pos + 9) == 'o' && rb(pos + 10) == 'n' &&
-                                 rb(pos + 11) == 's' && rb(pos + 12) == '"')
-                            code = TK_KEY_ANNOT;
-                    }
-                }
-                S.tok[idx] = (code << 24) | pos;
+                // region keywords (an exact string: its closing quote follows the word):
+                // the 16 bytes after the byte, from five LDS words.  Bytes past the
+                // document cannot fake a match: a string that closes inside the
+                // document puts its quote inside the compared span.
+                const uint32_t a = (pos + 1u) & ~3u, sh = (pos + 1u) & 3u;
+                const uint32_t w0 = ring32(a), w1 = ring32(a + 4u), w2 = ring32(a + 8u), w3 = ring32(a + 12u);
+                const uint32_t w4 = ring32(a + 16u);
+                const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                const uint32_t x2 = __builtin_amdgcn_alignbyte(w3, w2, sh), x3 = __builtin_amdgcn_alignbyte(w4, w3, sh);
+                (void)x3;
+                uint32_t kw = c;
+                kw = (x0 == 0x6174656du && x1 == 0x61746164u && (x2 & 0xFFu) == 0x22u) ? TK_KEY_META : kw;  // metadata"
+                kw = (x0 == 0x74617473u && (x1 & 0xFFFFFFu) == 0x227375u) ? TK_KEY_STATUS : kw;          // status"
+                kw = (x0 == 0x6562616cu && (x1 & 0xFFFFFFu) == 0x22736cu) ? TK_KEY_LABELS : kw;          // labels"
+                kw = (x0 == 0x6f6e6e61u && x1 == 0x69746174u && x2 == 0x22736e6fu) ? TK_KEY_ANNOT : kw;  // annotations"
+                const bool is_close = (closes >> lane) & 1ull, is_slow = (slow_opens >> lane) & 1ull;
+                const bool is_open = (opens >> lane) & 1ull;
+                const uint32_t code = is_close ? TK_CLOSEQ : is_slow ? TK_OPENQ_SLOW : is_open ? kw : c;
+                S.tok[ntok + mbcnt64(tokens)] = (code << 24) | pos;
             }
             if (opens) {
                 const uint32_t ob = 63u - (uint32_t)__builtin_clzll(opens);
@@ -247,199 +241,182 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             ntok += popc64(tokens);
         }
     }
-    if (str_carry) status = GPUDIFF_TOK_SYNTAX;  // unterminated string
+    if (str_par) status = GPUDIFF_TOK_SYNTAX;  // unterminated string
     if (ctl_in_string && status == GPUDIFF_TOK_OK) status = GPUDIFF_TOK_STRING;
     wave_sync();
 
     mark(0);
     // ------------------------------------------------------------ phase 2: tree building
-    // Uniform state machine over the token list: everything lives in scalar
-    // registers (state, the innermost open container, region bookkeeping);
-    // outer containers go to an LDS stack on push and come back on pop.
-    uint32_t nn = 0, sp = 0, expect = E_ROOT;
-    bool skip = false;
-    uint32_t top_node = 0, top_meta = 0;  // innermost open container: is_arr | region << 1 | count << 4
-    uint32_t key_tok = 0, key_code = 0;
+    // Lane per token, 64 tokens per batch.  A token's level (containers open
+    // before it) is an mbcnt of opens minus closes; its enclosing container is
+    // the last open one level up before it: found with a ballot per level
+    // present in the batch, or carried from earlier batches in a per-level LDS
+    // table.  A quote is a key when the token two after it is ':' (lookahead),
+    // so node ids are a ballot prefix count and every lane checks its token
+    // against its predecessor on its own (the first failing token decides the
+    // status, as the sequential grammar would stop there).
+    struct LvlEnt {
+        uint32_t id, info, base, cnt1;  // last open at this level: node id, kind/region/flags, level+1 nodes
+                                        // before it; level+1 nodes so far
+    };
+    LvlEnt* const lvt = (LvlEnt*)lds;  // kMaxDepth entries (4080 B; the ring is free now)
+    constexpr uint32_t LF_ARR = 1u, LF_META = 16u, LF_LAB = 32u, LF_ANN = 64u;  // info: is_arr | reg << 1 | flags
+    uint32_t nn = 0;
     uint32_t meta_node = NONE, labels_node = NONE, annot_node = NONE;
     bool labels_ok = true, annot_ok = true, has_status = false;
     uint32_t max_depth = 0;
-    uint32_t rx = 0, ry = 0, rz = 0, rw = 0;  // pending node records, node k in lane k % 64
-    auto add_node = [&](uint32_t parent, uint32_t comp, uint32_t vtok, uint32_t info, uint32_t depth) -> uint32_t {
-        const uint32_t id = nn;
-        if (lane == (id & 63u)) {
-            rx = parent;
-            ry = comp;
-            rz = vtok;
-            rw = info | (depth << NI_DEPTH_SHIFT);
-        }
-        max_depth = max(max_depth, depth);
-        nn++;
-        if ((nn & 63u) == 0) S.rec[nn - 64 + lane] = make_uint4(rx, ry, rz, rw);
-        return id;
-    };
     if (status == GPUDIFF_TOK_OK) {
-        for (uint32_t tb = 0; tb < ntok && status == GPUDIFF_TOK_OK; tb += 64) {
-            const uint32_t tv = tb + lane < ntok ? S.tok[tb + lane] : 0u;
-            const uint32_t tnext = __builtin_amdgcn_readfirstlane(tb + 64 < ntok ? S.tok[tb + 64] : 0u);
-            const uint32_t kend = min(64u, ntok - tb);
-            for (uint32_t k = 0; k < kend; k++) {
-                if (skip) {  // the close of an empty container, consumed by its opener's peek
-                    skip = false;
-                    continue;
-                }
-                const uint32_t t = rdlane(tv, k);
-                const uint32_t code = t >> 24, ti = tb + k;
-                if (expect == E_KEY) {
-                    if (code == '"' || (code >= TK_KEY_META && code <= TK_KEY_ANNOT)) {
-                        key_tok = ti;
-                        key_code = code;
-                        expect = E_KEYCLOSE;
-                        // common case: close quote and ':' in this batch -> consume all three
-                        if (k + 2 < kend && (rdlane(tv, k + 2) >> 24) == ':') {
-                            k += 2;
-                            expect = E_VALUE;
-                        }
-                    } else {
-                        status = code == TK_OPENQ_SLOW ? GPUDIFF_TOK_KEY : GPUDIFF_TOK_SYNTAX;
-                        break;
-                    }
-                } else if (expect == E_KEYCLOSE) {
-                    expect = E_COLON;  // the token after an open quote is its close
-                } else if (expect == E_COLON) {
-                    if (code != ':') {
-                        status = GPUDIFF_TOK_SYNTAX;
-                        break;
-                    }
-                    expect = E_VALUE;
-                } else if (expect == E_STRCLOSE) {
-                    expect = E_NEXT;
-                } else if (expect == E_NEXT) {
-                    const bool is_arr = top_meta & 1u;
-                    if (code == ',') {
-                        expect = is_arr ? E_VALUE : E_KEY;
-                    } else if (code == (is_arr ? (uint32_t)']' : (uint32_t)'}')) {
-                        sp--;
-                        if (sp) {
-                            top_node = __builtin_amdgcn_readfirstlane(stk_node[sp - 1]);
-                            top_meta = __builtin_amdgcn_readfirstlane(stk_meta[sp - 1]);
-                            expect = E_NEXT;
-                        } else {
-                            expect = E_END;
-                        }
-                    } else {
-                        status = GPUDIFF_TOK_SYNTAX;
-                        break;
-                    }
-                } else if (expect == E_VALUE) {
-                    const uint32_t parent = top_node;
-                    const bool in_arr = top_meta & 1u;
-                    const uint32_t preg = (top_meta >> 1) & 7u;
-                    const uint32_t depth = sp;
-                    uint32_t comp;
-                    if (in_arr) {
-                        comp = top_meta >> 4;
-                        top_meta += 16u;
-                    } else {
-                        comp = key_tok | KEYBIT;
-                    }
-                    const bool is_str = code == '"' || (code >= TK_OPENQ_SLOW && code <= TK_KEY_ANNOT);
-                    uint32_t reg = preg;
-                    bool is_lab = false, is_ann = false, is_meta = false;
-                    if (depth == 1) {
-                        if (key_code == TK_KEY_META) {
+        for (uint32_t q = lane; q < kMaxDepth; q += 64) lvt[q] = LvlEnt{0u, 0u, 0u, 0u};
+        lds_order();
+        int32_t lvl_c = 0;                   // level at the batch start
+        uint32_t pc1 = 0, pc2 = 0, pc3 = 0;  // codes of the three tokens before the batch (0: none)
+        for (uint32_t tb = 0; tb < ntok; tb += 64) {
+            const bool live = tb + lane < ntok;
+            const uint32_t t = live ? S.tok[tb + lane] : 0u;
+            const uint32_t code = t >> 24;
+            const uint32_t tx = (lane < 2u && tb + 64u + lane < ntok) ? S.tok[tb + 64u + lane] : 0u;
+            const uint32_t nx0 = rdlane(tx, 0) >> 24, nx1 = rdlane(tx, 1) >> 24;
+            const uint32_t cp1 = wave_shr1(code, pc1), cp2 = wave_shr1(cp1, pc2), cp3 = wave_shr1(cp2, pc3);
+            const uint32_t cn1 = wave_shl1(code, nx0), cn2 = wave_shl1(cn1, nx1);
+            const bool is_o = live && (code == '{' || code == '[');
+            const bool is_c = live && (code == '}' || code == ']');
+            const bool is_qo = live && (code == '"' || (code >= TK_OPENQ_SLOW && code <= TK_KEY_ANNOT));
+            const bool is_key = is_qo && cn2 == ':';
+            const bool is_at = live && !is_o && !is_c && !is_qo && code != TK_CLOSEQ && code != ':' && code != ',';
+            const bool is_node = is_o || is_at || (is_qo && !is_key);
+            const uint64_t m_o = ballot(is_o), m_c = ballot(is_c), m_node = ballot(is_node);
+            const int32_t lvl = lvl_c + (int32_t)mbcnt64(m_o) - (int32_t)mbcnt64(m_c);
+            const uint32_t id = nn + mbcnt64(m_node);
+            const bool empty = is_o && cn1 == (code == '{' ? (uint32_t)'}' : (uint32_t)']');
+            // per-lane results of the level loop
+            uint32_t e_id = NONE, e_info = 0u, my_info = code == '[' ? LF_ARR : 0u, my_base = 0u, comp = 0u, reg = R_NONE;
+            bool bad_lab = false, bad_ann = false;
+            const int32_t lmin = (int32_t)wave_min_u32(live ? (uint32_t)(lvl + 0x40000000) : 0x7FFFFFFFu) - 0x40000000;
+            const int32_t lmax = (int32_t)wave_max(live ? (uint32_t)(lvl + 0x40000000) : 0u) - 0x40000000;
+            // levels of enclosing containers (lmin - 1 ..) and of this batch's opens (.. lmax)
+            const int32_t lo = max(lmin - 1, 0), hi = min(lmax, (int32_t)kMaxDepth - 1);
+            for (int32_t L = lo; L <= hi; L++) {
+                const bool at_l = is_o && lvl == L;
+                const bool at1 = live && lvl == L + 1;
+                const uint64_t m_ol = ballot(at_l), m_ch = ballot(at1 && is_node);
+                if (!m_ol && !ballot(at1)) continue;
+                LvlEnt st = lvt[L];
+                const uint32_t nb = st.cnt1 + mbcnt64(m_ch);  // level-(L+1) nodes before this token
+                if (at_l) my_base = nb;
+                const uint64_t below = m_ol & mask_lt(lane);
+                const uint32_t e = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+                const uint32_t x_id = shfl32(id, e), x_info = shfl32(my_info, e), x_base = shfl32(my_base, e);
+                if (at1) {
+                    e_id = below ? x_id : st.id;
+                    e_info = below ? x_info : st.info;
+                    if (is_node) {
+                        const uint32_t e_base = below ? x_base : st.base;
+                        const bool earr = e_info & LF_ARR;
+                        const uint32_t preg = (e_info >> 1) & 7u;
+                        const uint32_t depth = (uint32_t)L + 1u;
+                        comp = earr ? nb - e_base : ((tb + lane - 3u) | KEYBIT);
+                        reg = preg;
+                        uint32_t fl = 0;
+                        if (depth == 1u) {
+                            if (cp3 == TK_KEY_META) {
+                                reg = R_META;
+                                if (code == '{') fl = LF_META;
+                            } else {
+                                reg = code == 'n' ? R_NONE : cp3 == TK_KEY_STATUS ? R_STATUS : R_SPEC;
+                            }
+                        } else if (depth == 2u && !earr && (e_info & LF_META)) {
+                            if (code == '{') fl = cp3 == TK_KEY_LABELS ? LF_LAB : cp3 == TK_KEY_ANNOT ? LF_ANN : 0u;
+                        } else if (depth == 3u && (e_info & LF_LAB)) {
+                            reg = R_LABELS;
+                            bad_lab = !is_qo;
+                        } else if (depth == 3u && (e_info & LF_ANN)) {
+                            reg = R_ANNOT;
+                            bad_ann = !is_qo;
+                        } else if (preg == R_LABELS || preg == R_ANNOT) {
                             reg = R_META;
-                            is_meta = true;
-                        } else if (key_code == TK_KEY_STATUS) {
-                            has_status = true;
-                            reg = code == 'n' ? R_NONE : R_STATUS;
-                        } else {
-                            reg = code == 'n' ? R_NONE : R_SPEC;
                         }
-                    } else if (depth == 2 && !in_arr && parent == meta_node) {
-                        is_lab = key_code == TK_KEY_LABELS;
-                        is_ann = key_code == TK_KEY_ANNOT;
-                    } else if (depth == 3 && parent == labels_node) {
-                        reg = R_LABELS;
-                        if (!is_str) labels_ok = false;
-                    } else if (depth == 3 && parent == annot_node) {
-                        reg = R_ANNOT;
-                        if (!is_str) annot_ok = false;
-                    } else if (preg == R_LABELS || preg == R_ANNOT) {
-                        reg = R_META;
+                        my_info = (code == '[' ? LF_ARR : 0u) | (reg << 1) | fl;
                     }
-                    const uint32_t rinfo = reg << NI_REG_SHIFT;
-                    if (code == '{' || code == '[') {
-                        const uint32_t closer = code == '{' ? '}' : ']';
-                        const uint32_t pk = k + 1 < kend ? rdlane(tv, k + 1) : tnext;
-                        if (ti + 1 < ntok && (pk >> 24) == closer) {
-                            add_node(parent, comp, ti,
-                                     rinfo | NI_LEAF | (code == '{' ? GPUDIFF_TAG_EOBJ : GPUDIFF_TAG_EARR), depth);
-                            skip = true;
-                            expect = E_NEXT;
-                        } else {
-                            if (sp > kMaxDepth - 1) {
-                                status = GPUDIFF_TOK_DEPTH;
-                                break;
-                            }
-                            const uint32_t id = add_node(parent, comp, ti, rinfo, depth);
-                            if (code == '{') {
-                                if (is_meta) meta_node = id;
-                                if (is_lab) labels_node = id;
-                                if (is_ann) annot_node = id;
-                            }
-                            if (lane == 0) {  // push: the current innermost container goes to LDS
-                                stk_node[sp - 1] = top_node;
-                                stk_meta[sp - 1] = top_meta;
-                            }
-                            top_node = id;
-                            top_meta = (code == '[' ? 1u : 0u) | (reg << 1);
-                            sp++;
-                            expect = code == '{' ? E_KEY : E_VALUE;
-                        }
-                    } else if (is_str) {
-                        add_node(parent, comp, ti,
-                                 rinfo | NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u),
-                                 depth);
-                        expect = E_STRCLOSE;
-                        if (k + 1 < kend) {  // its close quote is the next token
-                            k++;
-                            expect = E_NEXT;
-                        }
-                    } else if (code == '}' || code == ']' || code == ',' || code == ':' || code == TK_CLOSEQ) {
-                        status = GPUDIFF_TOK_SYNTAX;
-                        break;
-                    } else {
-                        add_node(parent, comp, ti, rinfo | NI_LEAF | NI_ATOM, depth);
-                        expect = E_NEXT;
-                    }
-                    if (nn + 2 > ncap) {
-                        status = GPUDIFF_TOK_SIZE;
-                        break;
-                    }
-                } else if (expect == E_ROOT) {
-                    if (code != '{') {
-                        status = GPUDIFF_TOK_SYNTAX;
-                        break;
-                    }
-                    add_node(NONE, 0, ti, R_NONE << NI_REG_SHIFT, 0);
-                    const uint32_t pk = k + 1 < kend ? rdlane(tv, k + 1) : tnext;
-                    if (ti + 1 < ntok && (pk >> 24) == '}') {
-                        skip = true;  // {}: no leaves
-                        expect = E_END;
-                    } else {
-                        top_node = 0;
-                        top_meta = R_NONE << 1;
-                        sp = 1;
-                        expect = E_KEY;
-                    }
-                } else {  // E_END: trailing data
-                    status = GPUDIFF_TOK_SYNTAX;
-                    break;
+                }
+                // the table entry for level L
+                if (m_ol) {
+                    const uint32_t last = 63u - (uint32_t)__builtin_clzll(m_ol);
+                    st.id = rdlane(id, last);
+                    st.info = rdlane(my_info, last);
+                    st.base = rdlane(my_base, last);
+                }
+                st.cnt1 += popc64(m_ch);
+                if (m_ch) max_depth = max(max_depth, (uint32_t)L + 1u);
+                if (lane == 0) lvt[L] = st;
+                lds_order();
+            }
+            // grammar: each token against its predecessor (cp1; 0 before the first token)
+            const bool earr = e_info & LF_ARR;
+            const bool p_qo = cp1 == '"' || (cp1 >= TK_OPENQ_SLOW && cp1 <= TK_KEY_ANNOT);
+            const bool p_end = cp1 == TK_CLOSEQ || cp1 == '}' || cp1 == ']' ||
+                               (cp1 != 0u && !p_qo && cp1 != '{' && cp1 != '[' && cp1 != ':' && cp1 != ',');
+            uint32_t err = 0;
+            if (live) {
+                if (tb + lane == 0u) {
+                    if (code != '{') err = GPUDIFF_TOK_SYNTAX;
+                } else if (lvl <= 0) {
+                    err = GPUDIFF_TOK_SYNTAX;  // after the root closed
+                } else if (is_key) {
+                    if (!(cp1 == '{' || (cp1 == ',' && !earr))) err = GPUDIFF_TOK_SYNTAX;
+                    else if (code == TK_OPENQ_SLOW) err = GPUDIFF_TOK_KEY;
+                } else if (is_node) {
+                    if (!(cp1 == ':' || cp1 == '[' || (cp1 == ',' && earr))) err = GPUDIFF_TOK_SYNTAX;
+                    else if (is_o && !empty && lvl >= (int32_t)kMaxDepth) err = GPUDIFF_TOK_DEPTH;
+                    else if (id + 3u > ncap) err = GPUDIFF_TOK_SIZE;
+                } else if (code == ':') {
+                    if (cp1 != TK_CLOSEQ) err = GPUDIFF_TOK_SYNTAX;
+                } else if (code == ',') {
+                    if (!p_end) err = GPUDIFF_TOK_SYNTAX;
+                } else if (code == '}') {
+                    if (!(cp1 == '{' || (p_end && !earr))) err = GPUDIFF_TOK_SYNTAX;
+                } else if (code == ']') {
+                    if (!(cp1 == '[' || (p_end && earr))) err = GPUDIFF_TOK_SYNTAX;
                 }
             }
+            const uint64_t m_err = ballot(err != 0u);
+            const uint64_t upto = m_err ? mask_lt((uint32_t)__builtin_ctzll(m_err)) : ~0ull;
+            // node records (the root: no parent, no key, never a leaf)
+            if (is_node && ((upto >> lane) & 1ull) && id < ncap) {
+                uint32_t info;
+                if (tb + lane == 0u) {
+                    info = R_NONE << NI_REG_SHIFT;
+                } else {
+                    info = reg << NI_REG_SHIFT;
+                    if (is_o && empty) info |= NI_LEAF | (code == '{' ? GPUDIFF_TAG_EOBJ : GPUDIFF_TAG_EARR);
+                    else if (is_qo) info |= NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u);
+                    else if (is_at) info |= NI_LEAF | NI_ATOM;
+                    info |= (uint32_t)lvl << NI_DEPTH_SHIFT;
+                }
+                S.rec[id] = make_uint4(tb + lane == 0u ? NONE : e_id, comp, tb + lane, info);
+            }
+            const uint64_t ok_node = m_node & upto;
+            const uint64_t m_meta = ballot(is_node && lvl == 1 && cp3 == TK_KEY_META && code == '{') & upto;
+            const uint64_t m_lab = ballot(is_node && (my_info & LF_LAB)) & upto;
+            const uint64_t m_ann = ballot(is_node && (my_info & LF_ANN)) & upto;
+            if (m_meta) meta_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_meta));
+            if (m_lab) labels_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_lab));
+            if (m_ann) annot_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_ann));
+            if (ballot(is_node && lvl == 1 && cp3 == TK_KEY_STATUS) & upto) has_status = true;
+            if (ballot(bad_lab) & upto) labels_ok = false;
+            if (ballot(bad_ann) & upto) annot_ok = false;
+            nn += popc64(ok_node);
+            if (m_err) {
+                status = rdlane(err, (uint32_t)__builtin_ctzll(m_err));
+                break;
+            }
+            lvl_c += (int32_t)popc64(m_o) - (int32_t)popc64(m_c);
+            const uint32_t kend = min(64u, ntok - tb);
+            const uint32_t o1 = pc1, o2 = pc2;
+            pc1 = rdlane(code, kend - 1u);
+            pc2 = kend >= 2u ? rdlane(code, kend - 2u) : o1;
+            pc3 = kend >= 3u ? rdlane(code, kend - 3u) : kend == 2u ? o1 : o2;
         }
-        if (status == GPUDIFF_TOK_OK && expect != E_END) status = GPUDIFF_TOK_SYNTAX;
-        if ((nn & 63u) && lane < (nn & 63u)) S.rec[(nn & ~63u) + lane] = make_uint4(rx, ry, rz, rw);
+        if (status == GPUDIFF_TOK_OK && (ntok == 0u || lvl_c != 0)) status = GPUDIFF_TOK_SYNTAX;
     }
     wave_sync();
 

@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Host-to-device bandwidth probe (run on the GPU box): pinned H2D of one
+buffer, of the same bytes in 4/16 chunks, and the host memcpy rate into pinned
+staging -- the ceilings the watch-replay pipeline (config 5) works against."""
+import time
+
+import torch
+
+n = int(70e6)
+src = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+src.fill_(7)
+dst = torch.empty(n, dtype=torch.uint8, device="cuda")
+s = torch.cuda.Stream()
+for chunks in (1, 4, 16):
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(5):
+        t = time.perf_counter()
+        with torch.cuda.stream(s):
+            for c in range(chunks):
+                a, b = n * c // chunks, n * (c + 1) // chunks
+                dst[a:b].copy_(src[a:b], non_blocking=True)
+        s.synchronize()
+        best = min(best, time.perf_counter() - t)
+    print("H2D %d chunk(s): %.1f GB/s" % (chunks, n / best / 1e9))
+pageable = torch.empty(n, dtype=torch.uint8)
+pageable.fill_(3)
+best = 1e9
+for _ in range(5):
+    t = time.perf_counter()
+    src.copy_(pageable)
+    best = min(best, time.perf_counter() - t)
+print("host copy into pinned (torch, 1 call): %.1f GB/s" % (n / best / 1e9))
