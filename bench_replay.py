@@ -120,6 +120,10 @@ def run(args):
         on_b[sl] = new_is_b
         batches.append((sl, new_is_b, events(sl, new_is_b)))
     lat, gpu_ms, bytes_up = [], [], 0
+    results = []
+    up_bytes = [int(b[2]["new_len"].sum()) for b in batches]
+    t_sub, t_wait = [], []  # host time inside submit / wait per timed batch
+    ss0 = None
     mism = 0
     checked = 0
     sample_ok = None
@@ -134,35 +138,44 @@ def run(args):
                 tk, ts, kk = inflight.pop(0)
                 eng.wait(tk)
             eng.timing_reset()
+            ss0 = st.stats()
             t_start = time.time()
         ts = time.time()
         tk = submit(ev)
         if k >= args.warmup_batches:
-            # device encoding uploads the events' JSON; host encoding the encoded blobs
-            bytes_up += int(ev["new_len"].sum()) if dev_enc else st.stats().last_batch_bytes
+            t_sub.append(time.time() - ts)
+            # device encoding uploads the events' JSON (summed per batch before the clock); host
+            # encoding the encoded blobs
+            bytes_up += up_bytes[k] if dev_enc else st.stats().last_batch_bytes
         inflight.append((tk, ts, k))
         if len(inflight) == 2:
             tk0, ts0, k0 = inflight.pop(0)
+            tw = time.time()
             r = eng.wait(tk0)
             if k0 >= args.warmup_batches:
+                t_wait.append(time.time() - tw)
                 lat.append(time.time() - ts0)
-                f = r.pair_flags & 3
-                mism += int((f != (exp_ab[batches[k0][0]] & 3)).sum())
-                checked += f.size
-                if first_res is None:
-                    first_res = (r, batches[k0])
+                results.append((r, k0))  # checked against the ground truth after the clock stops
     while inflight:
         tk0, ts0, k0 = inflight.pop(0)
         r = eng.wait(tk0)
         lat.append(time.time() - ts0)
+        results.append((r, k0))
+    t_end = time.time()
+    el = t_end - t_start
+    for r, k0 in results:  # every timed decision against the generator's ground truth
         f = r.pair_flags & 3
         mism += int((f != (exp_ab[batches[k0][0]] & 3)).sum())
         checked += f.size
-    t_end = time.time()
-    el = t_end - t_start
+        if first_res is None:
+            first_res = (r, batches[k0])
     tm = eng.timings()
     ev_total = n_batches * B
     ss = st.stats()
+
+    def window(f):  # the mean of a per-batch store timing over the timed batches only
+        n1, n0 = ss.timing_batches, ss0.timing_batches
+        return (getattr(ss, f) * n1 - getattr(ss0, f) * n0) / max(1, n1 - n0)
     lat_ms = np.array(lat) * 1e3
 
     # ---- CPU baseline leg: the oracle's C++ port on a sample of the timed events
@@ -213,8 +226,13 @@ def run(args):
         "gpu_ms_per_batch": {"diff_pass": tm.total_ms, "k2": tm.compare_ms},
         "store": {"resident_gb": ss.live_bytes / 1e9, "compactions": ss.compactions, "reseeded": ss.reseeded,
                   "old_objects_encoded": ss.old_encoded, "deferred_to_host": ss.deferred},
-        "batch_ms": {"host_submit": ss.host_submit_ms, "h2d": ss.h2d_ms, "k0_encode": ss.encode_ms,
-                     "k0c_k0x_link": ss.link_ms, "diff_pass": tm.total_ms} if dev_enc else None,
+        "batch_ms": {"host_submit": window("host_submit_ms"), "h2d": window("h2d_ms"),
+                     "k0_encode": window("encode_ms"), "k0c_k0x_link": window("link_ms"), "diff_pass": tm.total_ms,
+                     "submit_split": {f: window(f) for f in ("submit_wait_ms", "submit_docs_ms", "submit_copy_ms",
+                                                             "submit_enqueue_ms")},
+                     "store_finish": window("finish_ms"),
+                     "submit_call": float(np.mean(t_sub) * 1e3), "wait_call": float(np.mean(t_wait) * 1e3)}
+        if dev_enc else None,
         "initial_list_objects_per_s": M / t_load,
         "checks": {"events_checked": checked, "decision_mismatches_vs_ground_truth": mism,
                    "sample_bit_exact_vs_oracle": sample_ok},

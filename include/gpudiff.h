@@ -297,6 +297,12 @@ typedef struct gpudiff_store_stats {
     /* device-encode with GPUDIFF_OPT_TIMING: per-batch means (ms) of the host side of submit,
      * the H2D copy, K0 and K0c+K0x */
     float host_submit_ms, h2d_ms, encode_ms, link_ms;
+    /* the host side of submit split: waiting for the ring slot's previous upload,
+     * the document / slot-chain tables, the JSON copy into pinned staging, the
+     * enqueue of copies and kernels; and the store's part of gpudiff_wait */
+    float submit_wait_ms, submit_docs_ms, submit_copy_ms, submit_enqueue_ms, finish_ms;
+    uint32_t timing_batches; /* batches the means are over */
+    uint32_t pad;
 } gpudiff_store_stats;
 
 int gpudiff_store_create(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,

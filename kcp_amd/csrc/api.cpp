@@ -164,6 +164,7 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
         for (auto& e : c->ev_k1) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&c->k2alt, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->rb, hipStreamNonBlocking));
         for (auto& e : c->seg_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->alt_start, hipEventDisableTiming));
@@ -190,7 +191,7 @@ void gpudiff_close(gpudiff_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         if (c->side_done) (void)hipEventDestroy(c->side_done);
         if (c->alt_start) (void)hipEventDestroy(c->alt_start);
-        for (hipStream_t s : {c->side, c->k2alt})
+        for (hipStream_t s : {c->side, c->k2alt, c->rb})
             if (s) {
                 (void)hipStreamSynchronize(s);
                 (void)hipStreamDestroy(s);
@@ -228,13 +229,7 @@ int gpudiff_encode_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t 
             part.errors = enc.decode_errors;
             part.reseeded = enc.reseeded;
         };
-        if (T == 1) {
-            work(0);
-        } else {
-            std::vector<std::thread> th;
-            for (uint32_t t = 0; t < T; t++) th.emplace_back(work, t);
-            for (auto& x : th) x.join();
-        }
+        workers(c).run(T, work);
     } catch (const std::bad_alloc&) {
         return GPUDIFF_E_NOMEM;
     }
@@ -714,17 +709,24 @@ int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rsr) {
     ResultStore* rs = &rsr;
     int rc;
     HIPCHK(hipEventSynchronize(d->done));
+    // read back on the context's readback stream: a synchronous hipMemcpy would also wait for the
+    // work queued behind this batch (the next batch's K0 / diff pass), serialising the pipeline
+    hipStream_t rb = c->rb;
     uint32_t sum[8];
-    HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost, rb));
+    HIPCHK(hipStreamSynchronize(rb));
     if (sum[4]) {  // path scratch overflow: grow to the exact need and redo the join
         if ((rc = ensure_paths(d, d->arena_cap, sum[3]))) return rc;
         uint32_t zero = 0;
         HIPCHK(hipMemcpyAsync(d->summary + 4, &zero, sizeof(zero), hipMemcpyHostToDevice, c->stream));
         if ((rc = enqueue_join_emit(c, d))) return rc;
         HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipMemcpy(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(sum, d->summary, sizeof(sum), hipMemcpyDeviceToHost, rb));
+        HIPCHK(hipStreamSynchronize(rb));
         if (sum[4]) return GPUDIFF_E_CAPACITY;
     }
+    std::vector<uint32_t> idx;
+    std::vector<uint8_t> nb;
     try {
         rs->flags.resize(d->n_pairs);
         rs->spec.resize(sum[0]);
@@ -733,30 +735,30 @@ int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rsr) {
         rs->off.resize((size_t)sum[2] + 1);
         rs->hashes.resize(sum[5]);
         rs->kinds.resize(sum[5]);
+        idx.resize(sum[2]);
+        nb.resize(sum[2]);
     } catch (const std::bad_alloc&) {
         return GPUDIFF_E_NOMEM;
     }
-    if (d->n_pairs) HIPCHK(hipMemcpy(rs->flags.data(), d->flags, d->n_pairs, hipMemcpyDeviceToHost));
+    auto d2h = [&](void* dst, const void* src, uint64_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, rb) : hipSuccess;
+    };
+    HIPCHK(d2h(rs->flags.data(), d->flags, d->n_pairs));
+    HIPCHK(d2h(idx.data(), d->dirty_idx, sum[2] * 4ull));
+    HIPCHK(d2h(nb.data(), d->noop_d, sum[2]));
+    HIPCHK(d2h(rs->spec.data(), d->spec_ids, sum[0] * 4ull));
+    HIPCHK(d2h(rs->status.data(), d->status_ids, sum[1] * 4ull));
+    HIPCHK(d2h(rs->dirty.data(), d->dirty_ids, sum[2] * 4ull));
+    HIPCHK(d2h(rs->off.data(), d->path_off, (sum[2] + 1ull) * 4ull));
+    HIPCHK(d2h(rs->hashes.data(), d->out_h, sum[5] * 8ull));
+    HIPCHK(d2h(rs->kinds.data(), d->out_k, sum[5]));
+    HIPCHK(hipStreamSynchronize(rb));
     for (uint8_t& f : rs->flags) f &= (uint8_t)(GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY | GPUDIFF_DECODE_ERROR);
-    if (sum[2]) {  // the write-path no-op bits of the dirty pairs (K2 / K4 via K3), by pair index
-        std::vector<uint32_t> idx(sum[2]);
-        std::vector<uint8_t> nb(sum[2]);
-        HIPCHK(hipMemcpy(idx.data(), d->dirty_idx, sum[2] * 4ull, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(nb.data(), d->noop_d, sum[2], hipMemcpyDeviceToHost));
-        for (uint32_t k = 0; k < sum[2]; k++) {
-            uint8_t& f = rs->flags[idx[k]];
-            if (f & GPUDIFF_DECODE_ERROR) continue;
-            if ((nb[k] & 1u) && (f & GPUDIFF_SPEC_DIRTY)) f |= GPUDIFF_SPEC_NOOP;
-            if ((nb[k] & 2u) && (f & GPUDIFF_STATUS_DIRTY)) f |= GPUDIFF_STATUS_NOOP;
-        }
-    }
-    if (sum[0]) HIPCHK(hipMemcpy(rs->spec.data(), d->spec_ids, sum[0] * 4ull, hipMemcpyDeviceToHost));
-    if (sum[1]) HIPCHK(hipMemcpy(rs->status.data(), d->status_ids, sum[1] * 4ull, hipMemcpyDeviceToHost));
-    if (sum[2]) HIPCHK(hipMemcpy(rs->dirty.data(), d->dirty_ids, sum[2] * 4ull, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(rs->off.data(), d->path_off, (sum[2] + 1ull) * 4ull, hipMemcpyDeviceToHost));
-    if (sum[5]) {
-        HIPCHK(hipMemcpy(rs->hashes.data(), d->out_h, sum[5] * 8ull, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(rs->kinds.data(), d->out_k, sum[5], hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < sum[2]; k++) {  // the write-path no-op bits of the dirty pairs (K2 / K4 via K3)
+        uint8_t& f = rs->flags[idx[k]];
+        if (f & GPUDIFF_DECODE_ERROR) continue;
+        if ((nb[k] & 1u) && (f & GPUDIFF_SPEC_DIRTY)) f |= GPUDIFF_SPEC_NOOP;
+        if ((nb[k] & 2u) && (f & GPUDIFF_STATUS_DIRTY)) f |= GPUDIFF_STATUS_NOOP;
     }
     return GPUDIFF_OK;
 }

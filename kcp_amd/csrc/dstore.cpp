@@ -25,9 +25,11 @@
 // submit order, at most two in flight.
 #include "dstore.h"
 
+#include <emmintrin.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <new>
 #include <thread>
@@ -61,6 +63,7 @@ struct Ring {
     hipEvent_t k0_done = nullptr;  // its K0..K0x finished reading the device JSON / document table
     bool k0_recorded = false;
     hipEvent_t t_ev[5] = {};      // GPUDIFF_OPT_TIMING: H2D begin/end (copy stream), K0 begin/end, K0c+K0x end
+    hipEvent_t chunk_ev[8] = {};  // each JSON chunk's H2D done: its K0 launches may start
     std::vector<gpudiff_event> events;
     std::vector<uint8_t> final_flags;  // the waited batch's result flags (deferred events resolved)
     bool waited = false;
@@ -109,9 +112,14 @@ struct DStore {
     uint32_t ring_next = 0;
     uint32_t batch_seq = 0;
     uint32_t next_wait = 1;  // batches are waited in submit order
-    std::vector<uint32_t> stamp;
-    std::vector<int32_t> last;
-    std::vector<uint8_t> seen;  // slot submitted before (its resident version may exist)
+    // per slot, one cache line fetch per event: the batch that last staged a document of the slot,
+    // that document, and whether the slot was submitted before (its resident version may exist)
+    struct SlotState {
+        uint32_t stamp;
+        int32_t last;
+    };
+    std::vector<SlotState> sstate;
+    std::vector<uint8_t> seen;
     std::unordered_map<uint32_t, uint32_t> forgotten;  // slot -> batch_seq at forget
     // resolution
     std::unique_ptr<PairEncoder> enc;
@@ -127,10 +135,28 @@ struct DStore {
     uint64_t deferred_total = 0;
     // GPUDIFF_OPT_TIMING: per-batch sums (ms) of host submit, H2D, K0, K0c+K0x
     double t_sum[4] = {0, 0, 0, 0};
+    double t_sub[5] = {0, 0, 0, 0, 0};  // submit: slot wait, tables, copy, enqueue; finisher
     uint64_t t_n = 0;
 };
 
 namespace {
+
+// one staged document: its bytes, then zeros up to `span` (a multiple of 16; dst 16-B aligned), with
+// non-temporal 16-B stores -- the pinned staging is only read by the DMA engine, so the stores skip
+// the read-for-ownership and do not evict the workers' caches
+void stream_doc(uint8_t* dst, const uint8_t* src, size_t len, size_t span) {
+    size_t i = 0;
+    for (; i + 16 <= len; i += 16)
+        _mm_stream_si128((__m128i*)(dst + i), _mm_loadu_si128((const __m128i*)(src + i)));
+    if (i < len) {
+        alignas(16) uint8_t t[16] = {0};
+        memcpy(t, src + i, len - i);
+        _mm_stream_si128((__m128i*)(dst + i), _mm_load_si128((const __m128i*)t));
+        i += 16;
+    }
+    const __m128i z = _mm_setzero_si128();
+    for (; i < span; i += 16) _mm_stream_si128((__m128i*)(dst + i), z);
+}
 
 int grow_pinned(uint8_t** p, uint64_t* cap, uint64_t need) {
     if (need <= *cap) return GPUDIFF_OK;
@@ -501,8 +527,7 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
         return (DStore*)nullptr;
     };
     try {
-        s->stamp.assign(max_slots, 0);
-        s->last.assign(max_slots, -1);
+        s->sstate.assign(max_slots, DStore::SlotState{0u, -1});
         s->seen.assign(max_slots, 0);
     } catch (const std::bad_alloc&) {
         return fail(GPUDIFF_E_NOMEM);
@@ -555,6 +580,13 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     }
     int rc;
     if (R.staged) HIPCHK(hipEventSynchronize(R.staged));
+    auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
+        if (!timing) return;
+        const auto now = std::chrono::steady_clock::now();
+        s->t_sub[k] += std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    };
+    lap(0);
     const uint32_t batch = ++s->batch_seq;
 
     // 1. documents and slot chains
@@ -582,20 +614,25 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         L.pair_id = e.pair_id;
         L.cluster_id = e.cluster_id;
         L.next = -1;
-        if (s->stamp[slot] == batch) {
-            L.prev = s->last[slot];
+        DStore::SlotState& ss = s->sstate[slot];
+        if (ss.stamp == batch) {
+            L.prev = ss.last;
             links[L.prev].next = (int32_t)nd;
         } else {
             L.prev = -1;
-            s->stamp[slot] = batch;
+            ss.stamp = batch;
             heads[nh++] = nd;
         }
-        s->last[slot] = (int32_t)nd;
+        ss.last = (int32_t)nd;
         src.push_back(p);
         nd++;
     };
     for (size_t i = 0; i < n; i++) {
         const gpudiff_event& e = ev[i];
+        if (i + 16 < n && ev[i + 16].slot < s->max_slots) {  // the slot state 16 events ahead
+            __builtin_prefetch(&s->sstate[ev[i + 16].slot], 1);
+            if (!s->pair_mode) __builtin_prefetch(&s->seen[ev[i + 16].slot], 1);
+        }
         if (e.slot >= s->max_slots || !e.new_json || e.new_len > kTokMaxLen || e.old_len > kTokMaxLen)
             return GPUDIFF_E_INVAL;
         if (s->pair_mode) {  // every pair: its old object, then its new one (an absent old object: decode error)
@@ -612,36 +649,34 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     }
     jbytes += kTokSlack;
     if ((rc = grow_pinned(&R.hjson, &R.hjson_cap, jbytes))) return rc;
-    {  // JSON into pinned staging, split over the host threads by bytes
-        const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(1u, c->threads), std::max<uint64_t>(1, jbytes >> 22));
-        auto copy = [&](uint32_t t) {
-            const uint64_t b0 = jbytes * t / T, b1 = jbytes * (t + 1) / T;
-            for (uint32_t k = 0; k < nd; k++) {
-                const uint64_t o = docs[k].json_off;
-                if (o < b0 || o >= b1) continue;
-                const uint64_t end = k + 1 < nd ? docs[k + 1].json_off : jbytes;
-                memcpy(R.hjson + o, src[k], docs[k].json_len);
-                memset(R.hjson + o + docs[k].json_len, 0, end - o - docs[k].json_len);
-            }
-        };
-        if (T == 1) {
-            copy(0);
-        } else {
-            std::vector<std::thread> th;
-            for (uint32_t t = 0; t < T; t++) th.emplace_back(copy, t);
-            for (auto& x : th) x.join();
+    lap(1);
+    // Chunks of the batch's JSON (by bytes, whole documents): the host copies chunk c into pinned
+    // staging while chunk c - 1 is uploading, and K0 starts on a chunk as soon as it has landed, so
+    // copy, upload and encode of one batch overlap instead of running back to back.
+    auto first_doc = [&](uint64_t b) -> uint32_t {  // first document starting at or after byte b
+        uint32_t lo = 0, hi = nd;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (docs[mid].json_off < b) lo = mid + 1;
+            else hi = mid;
         }
-        if (!nd) memset(R.hjson, 0, jbytes);
-    }
-    // K0 scratch: per-document areas within launches of at most kScratchCap
+        return lo;
+    };
+    const uint32_t C = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, jbytes >> 24));
+    uint32_t cdoc[9];
+    for (uint32_t q = 0; q <= C; q++) cdoc[q] = q == C ? nd : first_doc(jbytes * q / C);
+    auto cbyte = [&](uint32_t q) -> uint64_t { return q == C || cdoc[q] >= nd ? jbytes : docs[cdoc[q]].json_off; };
+    // K0 scratch: per-document areas within launches of at most kScratchCap, never across a chunk
     std::vector<std::pair<uint32_t, uint32_t>> launches;
-    {
+    std::vector<uint32_t> chunk_of_launch;
+    for (uint32_t q = 0; q < C; q++) {
         uint64_t sb = 0;
-        uint32_t first = 0;
-        for (uint32_t k = 0; k < nd; k++) {
+        uint32_t first = cdoc[q];
+        for (uint32_t k = cdoc[q]; k < cdoc[q + 1]; k++) {
             const uint64_t need = tok_scratch_bytes(docs[k].json_len);
             if (sb && sb + need > std::max(kScratchCap, need)) {
                 launches.emplace_back(first, k);
+                chunk_of_launch.push_back(q);
                 first = k;
                 sb = 0;
             }
@@ -649,7 +684,10 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
             sb += need;
             if ((rc = grow_dev(&s->scratch, &s->scratch_cap, sb))) return rc;
         }
-        if (nd) launches.emplace_back(first, nd);
+        if (cdoc[q + 1] > first) {
+            launches.emplace_back(first, cdoc[q + 1]);
+            chunk_of_launch.push_back(q);
+        }
     }
     // 2. capacity (compaction is stream-ordered after every earlier batch)
     if ((rc = ensure_space(s, bound))) return rc;
@@ -661,25 +699,81 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     hipStream_t st = c->stream, cs = s->cs;
     if (timing && !R.t_ev[0])
         for (auto& e : R.t_ev) HIPCHK(hipEventCreate(&e));
+    if (!R.chunk_ev[0])
+        for (auto& e : R.chunk_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // the upload runs on the copy stream, behind this ring slot's previous K0 (which read the
     // same device buffers), so it overlaps the other batch's K0 / diff pass
     if (R.k0_recorded) HIPCHK(hipStreamWaitEvent(cs, R.k0_done, 0));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[0], cs));
-    HIPCHK(hipMemcpyAsync(R.djson, R.hjson, jbytes, hipMemcpyHostToDevice, cs));
-    HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, meta_bytes, hipMemcpyHostToDevice, cs));
+    // the tables' used parts only (their device offsets are sized for 2n documents)
+    HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, (uint64_t)nd * sizeof(TokDoc), hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemcpyAsync(R.dmeta + max_docs * sizeof(TokDoc), R.hmeta + max_docs * sizeof(TokDoc),
+                          (uint64_t)nd * sizeof(DocLink), hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemcpyAsync(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)),
+                          R.hmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)), 4ull * nh + 4,
+                          hipMemcpyHostToDevice, cs));
+    // One run of the workers over all chunks: worker t copies its share of chunk 0, then of chunk
+    // 1, ... and counts each chunk done; the calling thread (worker 0) enqueues a chunk's upload as
+    // soon as every worker has counted it, then goes on with its own share of the next chunk.
+    const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(1u, c->threads), std::max<uint64_t>(1, jbytes >> 20));
+    std::atomic<uint32_t> chunk_done[8];
+    for (auto& x : chunk_done) x.store(0, std::memory_order_relaxed);
+    std::atomic<int> up_err{0};
+    uint32_t uploaded = 0;
+    auto upload = [&](uint32_t q) {
+        const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
+        if (q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
+        if (hipMemcpyAsync(R.djson + b0, R.hjson + b0, b1 - b0, hipMemcpyHostToDevice, cs) != hipSuccess ||
+            hipEventRecord(R.chunk_ev[q], cs) != hipSuccess)
+            up_err.store(1);
+    };
+    workers(c).run(T, [&](uint32_t t) {
+        for (uint32_t q = 0; q < C; q++) {
+            const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
+            const uint32_t k0 = std::max(cdoc[q], first_doc(b0 + (b1 - b0) * t / T));
+            const uint32_t k1 = std::min(cdoc[q + 1], first_doc(b0 + (b1 - b0) * (t + 1) / T));
+            for (uint32_t k = k0; k < k1; k++) {
+                const uint64_t o = docs[k].json_off;
+                const uint64_t end = k + 1 < nd ? docs[k + 1].json_off : jbytes;
+                stream_doc(R.hjson + o, src[k], docs[k].json_len, end - o);
+            }
+            _mm_sfence();  // the streaming stores are visible before the chunk counts as done
+            chunk_done[q].fetch_add(1, std::memory_order_release);
+            if (t == 0)  // upload every chunk all workers have finished, in order, without waiting
+                while (uploaded <= q && chunk_done[uploaded].load(std::memory_order_acquire) >= T) upload(uploaded++);
+        }
+        if (t == 0)
+            while (uploaded < C) {
+                if (chunk_done[uploaded].load(std::memory_order_acquire) < T) {
+                    std::this_thread::yield();
+                    continue;
+                }
+                upload(uploaded++);
+            }
+    });
+    if (up_err.load()) return GPUDIFF_E_DEVICE;
+    lap(2);
     HIPCHK(hipEventRecord(R.staged, cs));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[1], cs));
-    HIPCHK(hipStreamWaitEvent(st, R.staged, 0));
+    HIPCHK(hipStreamWaitEvent(st, R.chunk_ev[0], 0));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[2], st));
     if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
     const TokDoc* ddocs = (const TokDoc*)R.dmeta;
     const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
     const uint32_t* dheads = (const uint32_t*)(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
     uint8_t* space = s->space[s->cur];
-    for (auto& L : launches)
+    uint32_t waited_chunk = 0;
+    for (size_t li = 0; li < launches.size(); li++) {
+        const auto& L = launches[li];
+        if (chunk_of_launch[li] != waited_chunk) {
+            waited_chunk = chunk_of_launch[li];
+            HIPCHK(hipStreamWaitEvent(st, R.chunk_ev[waited_chunk], 0));
+        }
         HIPCHK(launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
                                   s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
                                   (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
+    }
+    HIPCHK(hipStreamWaitEvent(st, R.staged, 0));  // every chunk (and the tables) landed
     if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
     HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
     HIPCHK(hipMemsetAsync(R.dcnt, 0, 4, st));
@@ -710,6 +804,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     R.outstanding = true;
     Ring* Rp = &R;
     c->finishers[*ticket] = [s, Rp](ResultStore& rs) -> int {
+        const auto t_fin0 = std::chrono::steady_clock::now();
         Ring& RR = *Rp;
         RR.outstanding = false;
         if (!s->pair_mode) {
@@ -718,8 +813,9 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         }
         uint32_t ndef = 0;
         uint64_t used = 0;
-        HIPCHK(hipMemcpy(&ndef, RR.dcnt, 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(&used, s->used_dev, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(&ndef, RR.dcnt, 4, hipMemcpyDeviceToHost, s->c->rb));  // behind K0x: d->done waited
+        HIPCHK(hipMemcpyAsync(&used, s->used_dev, 8, hipMemcpyDeviceToHost, s->c->rb));
+        HIPCHK(hipStreamSynchronize(s->c->rb));
         // exact append point + what the other batch in flight may still add
         const Ring& other = s->ring[(Rp - s->ring) ^ 1];
         s->used_ub = std::max<uint64_t>(used, used + (other.outstanding ? other.bound : 0));
@@ -740,9 +836,11 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         // forgets older than every outstanding batch are settled
         for (auto it = s->forgotten.begin(); it != s->forgotten.end();)
             it = it->second < s->next_wait ? s->forgotten.erase(it) : std::next(it);
+        s->t_sub[4] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_fin0).count();
         return r2;
     };
     s->ring_next ^= 1u;
+    lap(3);
     if (timing)
         s->t_sum[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
     s->st.events += n;
@@ -805,6 +903,10 @@ int dstore_stats(const DStore* s, gpudiff_store_stats* out) {
         out->h2d_ms = (float)(s->t_sum[1] / s->t_n);
         out->encode_ms = (float)(s->t_sum[2] / s->t_n);
         out->link_ms = (float)(s->t_sum[3] / s->t_n);
+        float* sub[5] = {&out->submit_wait_ms, &out->submit_docs_ms, &out->submit_copy_ms, &out->submit_enqueue_ms,
+                         &out->finish_ms};
+        for (int k = 0; k < 5; k++) *sub[k] = (float)(s->t_sub[k] / s->t_n);
+        out->timing_batches = (uint32_t)s->t_n;
     }
     return GPUDIFF_OK;
 }
@@ -826,6 +928,8 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         if (R.staged) (void)hipEventDestroy(R.staged);
         if (R.k0_done) (void)hipEventDestroy(R.k0_done);
         for (auto& e : R.t_ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : R.chunk_ev)
             if (e) (void)hipEventDestroy(e);
     }
     if (s->res_d) gpudiff_dbatch_free(c, s->res_d);

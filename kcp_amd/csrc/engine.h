@@ -13,6 +13,7 @@
 
 #include "../../include/gpudiff.h"
 #include "encoder.h"
+#include "pool.h"
 #include "kernels.h"
 
 using gd::PairEncoder;
@@ -123,6 +124,7 @@ struct gpudiff_ctx {
     // segmented diff pass: side stream for K3/K4, one event per segment
     hipStream_t side = nullptr;
     hipStream_t k2alt = nullptr;  // second K2 stream (odd segments)
+    hipStream_t rb = nullptr;     // result readback (never behind work queued after the batch)
     hipEvent_t seg_ev[kMaxSegments] = {};
     hipEvent_t side_done = nullptr;
     hipEvent_t alt_start = nullptr;
@@ -135,9 +137,16 @@ struct gpudiff_ctx {
     gpudiff_dbatch* ring[2] = {nullptr, nullptr};
     gpudiff_hbatch* ring_hb[2] = {nullptr, nullptr};
     uint32_t ring_next = 0;
+    // persistent host workers (c->threads of them, the calling thread included), made on first use
+    std::unique_ptr<gd::WorkerPool> pool;
 };
 
 // ------------------------------------------------------------------ helpers
+inline gd::WorkerPool& workers(gpudiff_ctx* c) {
+    if (!c->pool) c->pool.reset(new gd::WorkerPool(c->threads));
+    return *c->pool;
+}
+
 inline int set_device(gpudiff_ctx* c) {
     if (!c->has_device) return GPUDIFF_E_NODEVICE;
     HIPCHK(hipSetDevice(c->device));

@@ -451,7 +451,7 @@ int gpudiff_classify_updates_host_kinds(const uint8_t* kinds, const uint8_t* con
         for (size_t i = n * t / T, e = n * (t + 1) / T; i < e; i++)
             actions[i] = classify_host(olds[i], olds[i] ? old_lens[i] : 0, news[i], new_lens[i], kinds ? kinds[i] : 0);
     };
-    std::vector<std::thread> th;
+    std::vector<std::thread> th;  // no context here: the caller's thread count, spawned per call
     for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
     work(0);
     for (auto& x : th) x.join();
@@ -583,10 +583,7 @@ int gpudiff_nbatch_fetch(gpudiff_ctx* c, gpudiff_nbatch* nb, int32_t* actions) {
             actions[i] = classify_host(nb->olds[i], nb->old_lens[i], nb->news[i], nb->new_lens[i], nb->kinds[i]);
         }
     };
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
+    workers(c).run(T, work);
     return GPUDIFF_OK;
 }
 

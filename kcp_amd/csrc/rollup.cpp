@@ -334,10 +334,7 @@ int gpudiff_rbatch_fetch(gpudiff_ctx* c, gpudiff_rbatch* rb, gpudiff_rollup* out
     auto work = [&](uint32_t t) {
         for (size_t k = t; k < def.size(); k += T) hok[k] = host_fields(rb->src[def[k]], rb->lens[def[k]], hf[k]);
     };
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
+    workers(c).run(T, work);
     // exact regrouping in document order (first appearance = ascending first_doc)
     std::unordered_map<std::string, int32_t> index;
     index.reserve(counts[0] + def.size());

@@ -374,13 +374,7 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
             w->touched.clear();
             w->pre.clear();
         }
-        if (T == 1) {
-            store_encode_part(c, s, ev, n, 0, 1, rows.data());
-        } else {
-            std::vector<std::thread> th;
-            for (uint32_t t = 0; t < T; t++) th.emplace_back(store_encode_part, c, s, ev, n, t, T, rows.data());
-            for (auto& x : th) x.join();
-        }
+        workers(c).run(T, [&](uint32_t t) { store_encode_part(c, s, ev, n, t, T, rows.data()); });
     } catch (const std::bad_alloc&) {
         s->broken = true;
         return GPUDIFF_E_NOMEM;

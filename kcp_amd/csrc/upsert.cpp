@@ -479,10 +479,7 @@ int gpudiff_wbatch_fetch(gpudiff_ctx* c, gpudiff_wbatch* wb, gpudiff_bodies* out
         for (size_t k = t; k < def.size(); k += T)
             hok[k] = host_body(wb->src[def[k]], wb->lens[def[k]], wb->mode, hb[k]) ? 1 : 0;
     };
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
+    workers(c).run(T, work);
     const size_t n_host = def.size();
     uint64_t dev_bytes = 0;
     size_t k = 0;
@@ -648,10 +645,7 @@ int gpudiff_write_plan_get(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_write_
                              : 0;
             }
         };
-        std::vector<std::thread> th;
-        for (uint32_t t = 1; t < T; t++) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
+        workers(c).run(T, work);
     }
     std::vector<int32_t> hidx(nd, -1);
     for (size_t k = 0; k < def.size(); k++) hidx[def[k]] = (int32_t)k;

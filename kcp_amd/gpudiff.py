@@ -99,7 +99,9 @@ class StoreStats(C.Structure):
                 ("events", C.c_uint64), ("old_encoded", C.c_uint64), ("reseeded", C.c_uint64),
                 ("collisions_unresolved", C.c_uint64), ("last_batch_bytes", C.c_uint64), ("deferred", C.c_uint64),
                 ("host_submit_ms", C.c_float), ("h2d_ms", C.c_float), ("encode_ms", C.c_float),
-                ("link_ms", C.c_float)]
+                ("link_ms", C.c_float), ("submit_wait_ms", C.c_float), ("submit_docs_ms", C.c_float),
+                ("submit_copy_ms", C.c_float), ("submit_enqueue_ms", C.c_float), ("finish_ms", C.c_float),
+                ("timing_batches", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class ObjInfo(C.Structure):

@@ -31,3 +31,21 @@ for _ in range(5):
     src.copy_(pageable)
     best = min(best, time.perf_counter() - t)
 print("host copy into pinned (torch, 1 call): %.1f GB/s" % (n / best / 1e9))
+
+# the same copy while another stream keeps every CU busy (what K0 does during a batch's upload)
+big = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+busy = torch.cuda.Stream()
+for chunks in (1, 16):
+    torch.cuda.synchronize()
+    with torch.cuda.stream(busy):
+        for _ in range(40):
+            big.mul_(1.0001)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        ev0.record(s)
+        for c in range(chunks):
+            a, b = n * c // chunks, n * (c + 1) // chunks
+            dst[a:b].copy_(src[a:b], non_blocking=True)
+        ev1.record(s)
+    torch.cuda.synchronize()
+    print("H2D %d chunk(s) beside a busy stream: %.1f GB/s" % (chunks, n / (ev0.elapsed_time(ev1) * 1e-3) / 1e9))
