@@ -71,7 +71,7 @@ def run(args):
     cluster = np.arange(M, dtype=np.uint32) % np.uint32(cfg.n_clusters)
 
     eng = G.Engine(device=0, encode_threads=threads, timing=True)
-    per_obj = float(lens.mean()) * 1.3 + 256
+    per_obj = float(lens.mean()) * 2.2 + 256  # blob + path table ~= 2x the JSON
     space = int(per_obj * M * 2.5) + (B * int(per_obj) * 4) + (256 << 20)
     dev_enc = args.encode == "device"
     st = eng.object_store(M, space, B, device_encode=dev_enc)

@@ -328,7 +328,10 @@ int gpudiff_store_stats_get(const gpudiff_store* st, gpudiff_store_stats* out);
 void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
 
 /* ---- object encoding in the device-store format (inspection / parity) ----
- * An object's blob followed by its fingerprint trailer.  gpudiff_encode_objects
+ * An object's blob followed by its path table (gpudiff_format.h: the node
+ * hashes, parent hashes and last components of the region leaves and their
+ * ancestors, which the store checks old-vs-new paths with exactly).
+ * gpudiff_encode_objects
  * runs kernel K0 (the device JSON tokenizer + encoder) over n documents;
  * gpudiff_encode_object_host runs the host encoder (the Go-exact path) over
  * one.  Where K0 reports GPUDIFF_TOK_OK the two are byte-identical. */
@@ -337,7 +340,9 @@ typedef struct gpudiff_obj_info {
     uint32_t oflags;         /* GPUDIFF_OBJ_HAS_STATUS */
     uint32_t spec_l, spec_ar, stat_l, stat_ar;
     uint64_t off;            /* blob offset in out */
-    uint64_t bytes;          /* blob + trailer bytes */
+    uint64_t bytes;          /* blob + path-table bytes */
+    uint32_t n_tab;          /* path-table entries */
+    uint32_t reserved;
 } gpudiff_obj_info;
 
 int gpudiff_encode_objects(gpudiff_ctx* ctx, const uint8_t* const* docs, const size_t* lens, const uint32_t* seeds,

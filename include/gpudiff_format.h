@@ -18,7 +18,9 @@
  * (pkg/syncer/specsyncer.go:17-41, statussyncer.go:15-27) iff their segments
  * are byte-identical, because the encoding is a deterministic function of the
  * leaf set and the path hash is verified injective over each pair's path
- * union by the encoder (it re-seeds the pair on a collision).
+ * union: by the encoder over both path sets (it re-seeds the pair on a
+ * collision), or, in the object store, against the resident version's path
+ * table (below).
  */
 #ifndef GPUDIFF_FORMAT_H
 #define GPUDIFF_FORMAT_H
@@ -41,9 +43,31 @@
 #define GPUDIFF_OBJ_DECODE_ERR 0x2u   /* JSON failed the Go decode rules */
 #define GPUDIFF_OBJ_FRESH 0x4u        /* object store: blob uploaded with this batch (K1 hashes
                                          its long values; resident blobs were hashed on arrival) */
-/* object store: root of the fingerprint chain, an independent second path hash
- * (fp(p + c) = XXH64(enc(c), fp(p))) kept after a resident blob's segments */
-#define GPUDIFF_FP_ROOT 0x9FB21C651E98DF25ull
+/* object store: the path table kept after a resident blob's segments (the
+ * "trailer"), which makes the store's old-vs-new path check exact.  Its n
+ * entries are the region leaves and all their ancestors except the root,
+ * ascending by (masked) path hash:
+ *
+ *   hs[n] u64 | phs[n] u64 | cs[n] u64 | key bytes | pad (the whole a multiple of 16)
+ *
+ *   hs    = the node's path hash; unique, and none equals the root's (the seed)
+ *   phs   = its parent's path hash (depth-1 nodes: the seed)
+ *   cs    = its last component: GPUDIFF_TAB_INDEX | index, or
+ *           (key length << 32) | offset of the key bytes in the key area
+ *
+ * Two tables agree when every hash both hold has the same parent hash and the
+ * same component in each.  By induction on depth (the root is the same in
+ * both; a node's parent hash names exactly one node of each table), agreeing
+ * tables give every shared hash the same path in both objects: an equal key in
+ * two segments is then an equal path, whatever the hash width. */
+#define GPUDIFF_TAB_INDEX 0x8000000000000000ull
+/* entry count of a blob stored without a valid table (its node hashes are not
+ * unique under the pair's seed): nothing agrees with it, so the next event on
+ * its slot is re-encoded from old_json */
+#define GPUDIFF_TAB_NONE 0xFFFFFFFFu
+static inline uint64_t gpudiff_tab_bytes(uint32_t n, uint64_t key_bytes) {
+    return (24ull * n + key_bytes + 15u) & ~(uint64_t)15u;
+}
 
 /* bits 8..15 of flags_a: per-pair path-hash seed */
 #define GPUDIFF_OBJ_SEED_SHIFT 8u

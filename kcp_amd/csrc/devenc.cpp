@@ -45,7 +45,8 @@ int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, ui
     std::vector<uint8_t> pool;
     uint64_t off;
     uint32_t bytes;
-    enc.write_object_fp(o, pool, &off, &info->spec_l, &info->spec_ar, &info->stat_l, &info->stat_ar, &bytes);
+    enc.write_object_tab(o, pool, &off, &info->spec_l, &info->spec_ar, &info->stat_l, &info->stat_ar, &bytes);
+    info->n_tab = o.tab.n;
     info->off = 0;
     info->bytes = bytes;
     if (out) {
@@ -108,6 +109,7 @@ int gpudiff_encode_objects(gpudiff_ctx* c, const uint8_t* const* docs, const siz
         f.stat_ar = to[i].stat_ar;
         f.off = to[i].off;
         f.bytes = to[i].bytes;
+        f.n_tab = to[i].n_tab;
     }
     return GPUDIFF_OK;
 }

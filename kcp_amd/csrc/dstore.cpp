@@ -73,24 +73,6 @@ struct Ring {
     bool outstanding = false;
 };
 
-struct HF {
-    uint64_t h, fp;
-};
-
-bool no_collision(const std::vector<HF>& old, const std::vector<LeafRec>& nw) {
-    size_t i = 0, j = 0;
-    while (i < old.size() && j < nw.size()) {
-        if (old[i].h < nw[j].h) i++;
-        else if (old[i].h > nw[j].h) j++;
-        else {
-            if (old[i].fp != nw[j].fp) return false;
-            i++;
-            j++;
-        }
-    }
-    return true;
-}
-
 }  // namespace
 
 struct DStore {
@@ -210,9 +192,9 @@ struct HostSlot {
     bool live = false, has_status = false;
     uint32_t seed = 0;
     uint64_t off = 0;  // absolute, or kRelTag | offset in the resolution pool
-    uint32_t sl = 0, sar = 0, tl = 0, tar = 0, bytes = 0;
-    bool hf_loaded = false;
-    std::vector<HF> spec, stat;
+    uint32_t sl = 0, sar = 0, tl = 0, tar = 0, bytes = 0, n_tab = 0;
+    bool tab_loaded = false;
+    PathTable tab;
 };
 
 int fetch_slot(DStore* s, uint32_t slot, HostSlot& H) {
@@ -228,33 +210,27 @@ int fetch_slot(DStore* s, uint32_t slot, HostSlot& H) {
     H.tl = d.stat_l;
     H.tar = d.stat_ar;
     H.bytes = d.bytes;
-    H.hf_loaded = false;
+    H.n_tab = d.n_tab;
+    H.tab_loaded = false;
     return GPUDIFF_OK;
 }
 
-// (pathHash, fingerprint) lists of a device-resident blob: its keys + trailer
-int load_hf(DStore* s, HostSlot& H) {
-    if (H.hf_loaded) return GPUDIFF_OK;
-    const uint64_t seg_s = gpudiff_seg_bytes(H.sl, H.sar), seg_t = gpudiff_seg_bytes(H.tl, H.tar);
-    std::vector<uint64_t> ks(H.sl), kt(H.tl), fp(H.sl + H.tl);
-    const uint8_t* b = s->space[s->cur] + H.off;
-    if (H.sl) HIPCHK(hipMemcpy(ks.data(), b, 8ull * H.sl, hipMemcpyDeviceToHost));
-    if (H.tl) HIPCHK(hipMemcpy(kt.data(), b + seg_s, 8ull * H.tl, hipMemcpyDeviceToHost));
-    if (H.sl + H.tl) HIPCHK(hipMemcpy(fp.data(), b + seg_s + seg_t, 8ull * (H.sl + H.tl), hipMemcpyDeviceToHost));
-    H.spec.resize(H.sl);
-    H.stat.resize(H.tl);
-    for (uint32_t i = 0; i < H.sl; i++) H.spec[i] = HF{ks[i], fp[i]};
-    for (uint32_t i = 0; i < H.tl; i++) H.stat[i] = HF{kt[i], fp[H.sl + i]};
-    H.hf_loaded = true;
+// the path table of a device-resident blob: its trailer
+int load_tab(DStore* s, HostSlot& H) {
+    if (H.tab_loaded) return GPUDIFF_OK;
+    const uint64_t segs = gpudiff_seg_bytes(H.sl, H.sar) + gpudiff_seg_bytes(H.tl, H.tar);
+    H.tab.n = H.n_tab;
+    H.tab.data.resize(H.bytes - segs);
+    if (!H.tab.data.empty())
+        HIPCHK(hipMemcpy(H.tab.data.data(), s->space[s->cur] + H.off + segs, H.tab.data.size(), hipMemcpyDeviceToHost));
+    H.tab_loaded = true;
     return GPUDIFF_OK;
 }
 
-void set_hf(HostSlot& H, const FlatObject& o) {
-    H.spec.resize(o.spec.size());
-    for (size_t k = 0; k < o.spec.size(); k++) H.spec[k] = HF{o.spec[k].h, o.spec[k].fp};
-    H.stat.resize(o.stat.size());
-    for (size_t k = 0; k < o.stat.size(); k++) H.stat[k] = HF{o.stat[k].h, o.stat[k].fp};
-    H.hf_loaded = true;
+void set_tab(HostSlot& H, const FlatObject& o) {
+    H.tab = o.tab;
+    H.n_tab = o.tab.n;
+    H.tab_loaded = true;
 }
 
 // Re-does the batch's deferred events on the host (store.cpp's decisions),
@@ -312,7 +288,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
         if (!enc.flatten_json(e.new_json, e.new_len, arena_new, fn)) {
             conservative();
             S.live = false;
-            S.hf_loaded = false;
+            S.tab_loaded = false;
             continue;
         }
         bool ok = false, pair_error = false, a_live = false;
@@ -330,8 +306,8 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
             a_of = S.has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
         };
         if (S.live && S.seed == 0) {
-            if ((rc = load_hf(s, S))) return rc;
-            if (enc.hash_single(fn, 0) && no_collision(S.spec, fn.spec) && no_collision(S.stat, fn.stat)) {
+            if ((rc = load_tab(s, S))) return rc;
+            if (enc.hash_single(fn, 0) && tab_agree(tab_view(S.tab), tab_view(fn.tab))) {
                 ok = true;
                 a_is_slot();
             }
@@ -350,8 +326,8 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
                 pair_error = true;
             }
         } else if (!ok && S.live && S.seed) {
-            if ((rc = load_hf(s, S))) return rc;
-            if (enc.hash_single(fn, S.seed) && no_collision(S.spec, fn.spec) && no_collision(S.stat, fn.stat)) {
+            if ((rc = load_tab(s, S))) return rc;
+            if (enc.hash_single(fn, S.seed) && tab_agree(tab_view(S.tab), tab_view(fn.tab))) {
                 ok = true;
                 seed = S.seed;
                 a_is_slot();
@@ -360,8 +336,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
                 s->st.collisions_unresolved++;
             }
         } else if (!ok && !S.live) {
-            for (seed = 0; seed <= 255 && !ok; seed++) ok = enc.hash_single(fn, seed);
-            seed--;
+            ok = enc.first_seed(fn, &seed);
             pair_error = !ok;
         } else if (!ok) {
             pair_error = true;
@@ -369,18 +344,15 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
         }
         if (pair_error) {
             conservative();
-            bool self = false;
-            for (seed = 0; seed <= 255 && !self; seed++) self = enc.hash_single(fn, seed);
-            seed--;
-            if (!self) {
+            if (!enc.store_seed(fn, &seed)) {
                 S.live = false;
-                S.hf_loaded = false;
+                S.tab_loaded = false;
                 continue;
             }
         }
         uint64_t off;
         uint32_t sl, sar, tl, tar, bytes;
-        enc.write_object_fp(fn, pool, &off, &sl, &sar, &tl, &tar, &bytes);
+        enc.write_object_tab(fn, pool, &off, &sl, &sar, &tl, &tar, &bytes);
         if (!pair_error) {
             r.off_a = a_live ? a_off : 0;
             r.spec_l_a = a_sl;
@@ -404,7 +376,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
         S.tl = tl;
         S.tar = tar;
         S.bytes = bytes;
-        set_hf(S, fn);
+        set_tab(S, fn);
     }
     // slot states (forgotten-since slots keep their forget)
     std::vector<SlotUpdate> ups;
@@ -422,6 +394,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
             u.entry.stat_l = S.tl;
             u.entry.stat_ar = S.tar;
             u.entry.bytes = S.bytes;
+            u.entry.n_tab = S.n_tab;
             u.entry.flags = DS_LIVE | (S.has_status ? DS_HAS_STATUS : 0u) | (S.seed << 8);
         } else {
             s->seen[slot] = 0;  // the next event stages its old object again
@@ -606,7 +579,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         D.json_off = jbytes;
         D.json_len = (uint32_t)len;
         jbytes = (jbytes + len + kTokSlack + 15) & ~15ull;
-        bound += len + len / 2 + 64;  // typical blob <= JSON; K0 defers what does not fit (SPACE)
+        bound += 3 * len + 128;  // typical blob + path table < 3x JSON; K0 defers what does not fit (SPACE)
         DocLink& L = links[nd];
         memset(&L, 0, sizeof(L));
         L.slot = slot;

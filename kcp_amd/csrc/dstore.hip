@@ -3,11 +3,12 @@
 // else -- encoding (K0, tokenize.hip), collision checks, slot chains,
 // compaction -- stays in HBM.
 //
-//   K0c k_collide        wave per event: every key of the new blob is looked up
-//                        in its old side (the previous document of the slot in
-//                        this batch, else the slot's resident blob) by a lane-
-//                        parallel binary search; an equal key whose fingerprint
-//                        differs is a path-hash collision (host re-seeds)
+//   K0c k_collide        wave per event: every path-table node of the new blob
+//                        is looked up in its old side's table (the previous
+//                        document of the slot in this batch, else the slot's
+//                        resident blob) by a lane-parallel binary search; an
+//                        equal hash whose parent hash or component (key bytes,
+//                        index) differs is a path-hash collision (host re-seeds)
 //   K0x k_link           lane per slot chain: walks the slot's documents in
 //                        batch order, writes each event's (old, new) row for the
 //                        diff pass or defers the rest of the chain to the host,
@@ -36,14 +37,15 @@ struct BlobRef {
     uint64_t off;
     uint32_t sl, sar, tl, tar;
     uint32_t oflags;  // GPUDIFF_OBJ_HAS_STATUS
+    uint32_t ntab;    // path-table entries
 };
 
 __device__ __forceinline__ BlobRef ref_of(const TokOut& o) {
-    return BlobRef{o.off, o.spec_l, o.spec_ar, o.stat_l, o.stat_ar, o.oflags};
+    return BlobRef{o.off, o.spec_l, o.spec_ar, o.stat_l, o.stat_ar, o.oflags, o.n_tab};
 }
 __device__ __forceinline__ BlobRef ref_of(const DSlot& s) {
     return BlobRef{s.off, s.spec_l, s.spec_ar, s.stat_l, s.stat_ar,
-                   (s.flags & DS_HAS_STATUS) ? GPUDIFF_OBJ_HAS_STATUS : 0u};
+                   (s.flags & DS_HAS_STATUS) ? GPUDIFF_OBJ_HAS_STATUS : 0u, s.n_tab};
 }
 
 }  // namespace
@@ -74,26 +76,40 @@ __global__ __launch_bounds__(256) void k_collide(const DocLink* __restrict__ lin
             }
         }
     }
-    bool bad = false;
-    if (have_a) {
-        const uint64_t a_st = seg_bytes(A.sl, A.sar), b_st = seg_bytes(B.spec_l, B.spec_ar);
-        const uint64_t a_tr = a_st + seg_bytes(A.tl, A.tar), b_tr = b_st + seg_bytes(B.stat_l, B.stat_ar);
-        for (uint32_t g = 0; g < 2; g++) {
-            const uint32_t na = g ? A.tl : A.sl, nb = g ? B.stat_l : B.spec_l;
-            if (!na || !nb) continue;
-            const uint64_t* ka = (const uint64_t*)(space + A.off + (g ? a_st : 0));
-            const uint64_t* kb = (const uint64_t*)(space + B.off + (g ? b_st : 0));
-            const uint64_t* fa = (const uint64_t*)(space + A.off + a_tr) + (g ? A.sl : 0);
-            const uint64_t* fb = (const uint64_t*)(space + B.off + b_tr) + (g ? B.spec_l : 0);
-            for (uint32_t i = lane; i < nb; i += 64) {
-                const uint64_t k = kb[i];
-                uint32_t lo = 0, hi = na;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (ka[mid] < k) lo = mid + 1;
-                    else hi = mid;
+    bool bad = have_a && A.ntab == GPUDIFF_TAB_NONE;  // stored without a valid table: old_json decides
+    if (have_a && !bad && B.n_tab && A.ntab) {
+        // the path tables (include/gpudiff_format.h): a hash both hold must have the same parent
+        // hash and the same last component in each
+        const uint32_t na = A.ntab, nb = B.n_tab;
+        const uint64_t* ha = (const uint64_t*)(space + A.off + seg_bytes(A.sl, A.sar) + seg_bytes(A.tl, A.tar));
+        const uint64_t* hb = (const uint64_t*)(space + B.off + seg_bytes(B.spec_l, B.spec_ar) +
+                                               seg_bytes(B.stat_l, B.stat_ar));
+        const uint8_t* ka = (const uint8_t*)(ha + 3ull * na);
+        const uint8_t* kb = (const uint8_t*)(hb + 3ull * nb);
+        for (uint32_t i = lane; i < nb; i += 64) {
+            const uint64_t k = hb[i];
+            uint32_t lo = 0, hi = na;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (ha[mid] < k) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < na && ha[lo] == k) {
+                const uint64_t ca = ha[2ull * na + lo], cb = hb[2ull * nb + i];
+                const bool ia = (ca & GPUDIFF_TAB_INDEX) != 0, ib = (cb & GPUDIFF_TAB_INDEX) != 0;
+                if (ha[na + lo] != hb[nb + i] || ia != ib || (ia && ca != cb)) {
+                    bad = true;
+                } else if (!ia) {
+                    const uint32_t l = (uint32_t)(ca >> 32);
+                    if (l != (uint32_t)(cb >> 32)) {
+                        bad = true;
+                    } else {
+                        const uint8_t* x = ka + (uint32_t)ca;
+                        const uint8_t* y = kb + (uint32_t)cb;
+                        for (uint32_t q = 0; q < l; q++)
+                            if (x[q] != y[q]) bad = true;
+                    }
                 }
-                if (lo < na && ka[lo] == k && fa[lo] != fb[i]) bad = true;
             }
         }
     }
@@ -117,7 +133,7 @@ __global__ __launch_bounds__(256) void k_link(const uint32_t* __restrict__ heads
     bool defer = (S0.flags & DS_PENDING) != 0;
     const uint32_t seed = (S0.flags >> 8) & 0xFFu;
     bool have_a = was_live && !defer;
-    BlobRef A = have_a ? ref_of(S0) : BlobRef{0, 0, 0, 0, 0, 0};
+    BlobRef A = have_a ? ref_of(S0) : BlobRef{0, 0, 0, 0, 0, 0, 0};
     uint32_t a_bytes = S0.bytes;
     bool changed = false;
     uint32_t n_def = 0;
@@ -173,6 +189,7 @@ __global__ __launch_bounds__(256) void k_link(const uint32_t* __restrict__ heads
         N.stat_l = A.tl;
         N.stat_ar = A.tar;
         N.bytes = a_bytes;
+        N.n_tab = A.ntab;
         N.flags = DS_LIVE | ((A.oflags & GPUDIFF_OBJ_HAS_STATUS) ? DS_HAS_STATUS : 0u) | (seed << 8) |
                   (defer ? DS_PENDING : 0u);
         N.pend = defer ? batch : S0.pend;

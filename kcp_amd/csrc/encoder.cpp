@@ -199,31 +199,30 @@ static bool sentinel_check(const FlatObject& o, const std::vector<LeafRec>& v, u
     return it->path_len == sp.size() && memcmp(o.paths.data() + it->path_off, sp.data(), sp.size()) == 0;
 }
 
-bool PairEncoder::assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed_out) {
+bool PairEncoder::pair_valid(FlatObject& a, FlatObject& b, uint32_t seed) {
     const uint64_t mask = cfg_.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg_.hash_bits) - 1);
     auto by_h = [](const LeafRec& x, const LeafRec& y) { return x.h < y.h; };
-    for (uint32_t seed = 0; seed <= 255; seed++) {
-        for (FlatObject* o : {&a, &b})
-            for (std::vector<LeafRec>* v : {&o->spec, &o->stat}) {
-                for (LeafRec& r : *v) r.h = chain_hash(o->paths.data() + r.path_off, r.path_len, seed) & mask;
-                std::sort(v->begin(), v->end(), by_h);
-            }
-        bool ok = true;
-        for (FlatObject* o : {&a, &b})
-            for (std::vector<LeafRec>* v : {&o->spec, &o->stat})
-                for (size_t i = 1; ok && i < v->size(); i++)
-                    if ((*v)[i].h == (*v)[i - 1].h) ok = false;  // paths are unique within an object
-        ok = ok && merge_check(a, a.spec, b, b.spec) && merge_check(a, a.stat, b, b.stat);
-        if (ok) {
-            const std::string& sp = status_path_bytes();
-            uint64_t hs = chain_hash(sp.data(), sp.size(), seed) & mask;
-            ok = sentinel_check(a, a.stat, hs) && sentinel_check(b, b.stat, hs);
+    for (FlatObject* o : {&a, &b})
+        for (std::vector<LeafRec>* v : {&o->spec, &o->stat}) {
+            for (LeafRec& r : *v) r.h = chain_hash(o->paths.data() + r.path_off, r.path_len, seed) & mask;
+            std::sort(v->begin(), v->end(), by_h);
         }
-        if (ok) {
+    for (FlatObject* o : {&a, &b})
+        for (std::vector<LeafRec>* v : {&o->spec, &o->stat})
+            for (size_t i = 1; i < v->size(); i++)
+                if ((*v)[i].h == (*v)[i - 1].h) return false;  // paths are unique within an object
+    if (!merge_check(a, a.spec, b, b.spec) || !merge_check(a, a.stat, b, b.stat)) return false;
+    const std::string& sp = status_path_bytes();
+    const uint64_t hs = chain_hash(sp.data(), sp.size(), seed) & mask;
+    return sentinel_check(a, a.stat, hs) && sentinel_check(b, b.stat, hs);
+}
+
+bool PairEncoder::assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed_out) {
+    for (uint32_t seed = 0; seed <= 255; seed++)
+        if (pair_valid(a, b, seed)) {
             *seed_out = seed;
             return true;
         }
-    }
     return false;
 }
 
@@ -323,12 +322,134 @@ bool PairEncoder::flatten_json(const uint8_t* json, size_t len, Arena& arena, Fl
     return true;
 }
 
-static void fingerprints(FlatObject& o) {
-    for (std::vector<LeafRec>* v : {&o.spec, &o.stat})
-        for (LeafRec& r : *v) r.fp = chain_hash(o.paths.data() + r.path_off, r.path_len, kFingerprintSeed);
+bool PairEncoder::path_table(FlatObject& o, uint32_t seed) {
+    // every non-root prefix of every region leaf's path: (hash, parent hash,
+    // component, the prefix itself to tell a shared node from a collision)
+    // (prefix = paths[poff, pend); key bytes at paths[koff, koff + klen))
+    using PN = TabNode;
+    const uint64_t mask = cfg_.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg_.hash_bits) - 1);
+    const uint64_t root = (uint64_t)seed & mask;
+    std::vector<PN>& v = tab_scratch_;
+    v.clear();
+    const char* P = o.paths.data();
+    for (const std::vector<LeafRec>* lv : {&o.spec, &o.stat})
+        for (const LeafRec& r : *lv) {
+            uint64_t hp = seed;
+            uint32_t i = 0;
+            while (i + 5 <= r.path_len) {
+                const char* c = P + r.path_off + i;
+                uint32_t x;
+                memcpy(&x, c + 1, 4);
+                const bool key = c[0] == 0x01;
+                const uint32_t len = key ? 5u + x : 5u;
+                const uint64_t h = xxh64_host(c, len, hp);
+                PN n;
+                n.h = h & mask;
+                n.ph = hp & mask;
+                n.c = key ? ((uint64_t)x << 32) : (GPUDIFF_TAB_INDEX | x);
+                n.poff = r.path_off;
+                n.pend = r.path_off + i + len;
+                n.koff = r.path_off + i + 5;
+                if (n.h == root) {
+                    o.tab.n = GPUDIFF_TAB_NONE;
+                    o.tab.data.clear();
+                    return false;
+                }
+                v.push_back(n);
+                hp = h;
+                i += len;
+            }
+        }
+    std::sort(v.begin(), v.end(), [](const PN& a, const PN& b) { return a.h < b.h; });
+    size_t u = 0, kb = 0;
+    for (size_t i = 0; i < v.size(); i++) {
+        if (u && v[u - 1].h == v[i].h) {
+            const PN& a = v[u - 1];
+            const PN& b = v[i];
+            if (a.pend - a.poff != b.pend - b.poff || memcmp(P + a.poff, P + b.poff, a.pend - a.poff) != 0) {
+                o.tab.n = GPUDIFF_TAB_NONE;  // two nodes, one hash
+                o.tab.data.clear();
+                return false;
+            }
+            continue;
+        }
+        v[u++] = v[i];
+        if (!(v[i].c & GPUDIFF_TAB_INDEX)) kb += v[i].c >> 32;
+    }
+    v.resize(u);
+    const uint32_t n = (uint32_t)u;
+    PathTable& t = o.tab;
+    t.n = n;
+    t.data.assign(gpudiff_tab_bytes(n, kb), 0);
+    uint64_t* hs = (uint64_t*)t.data.data();
+    uint64_t* phs = hs + n;
+    uint64_t* cs = phs + n;
+    uint8_t* keys = t.data.data() + 24ull * n;
+    uint32_t ko = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        hs[i] = v[i].h;
+        phs[i] = v[i].ph;
+        if (v[i].c & GPUDIFF_TAB_INDEX) {
+            cs[i] = v[i].c;
+        } else {
+            const uint32_t kl = (uint32_t)(v[i].c >> 32);
+            cs[i] = ((uint64_t)kl << 32) | ko;
+            memcpy(keys + ko, P + v[i].koff, kl);
+            ko += kl;
+        }
+    }
+    return true;
+}
+
+bool tab_agree(const TabView& a, const TabView& b) {
+    if (a.n == GPUDIFF_TAB_NONE || b.n == GPUDIFF_TAB_NONE) return false;
+    uint32_t i = 0, j = 0;
+    while (i < a.n && j < b.n) {
+        if (a.hs[i] < b.hs[j]) {
+            i++;
+        } else if (a.hs[i] > b.hs[j]) {
+            j++;
+        } else {
+            if (a.phs[i] != b.phs[j]) return false;
+            const uint64_t ca = a.cs[i], cb = b.cs[j];
+            if ((ca & GPUDIFF_TAB_INDEX) || (cb & GPUDIFF_TAB_INDEX)) {
+                if (ca != cb) return false;
+            } else {
+                const uint32_t l = (uint32_t)(ca >> 32);
+                if (l != (uint32_t)(cb >> 32) || memcmp(a.keys + (uint32_t)ca, b.keys + (uint32_t)cb, l) != 0)
+                    return false;
+            }
+            i++;
+            j++;
+        }
+    }
+    return true;
 }
 
 bool PairEncoder::hash_single(FlatObject& o, uint32_t seed) {
+    return hash_leaves(o, seed) && path_table(o, seed);
+}
+
+bool PairEncoder::first_seed(FlatObject& o, uint32_t* seed) {
+    for (uint32_t s = 0; s <= 255; s++)
+        if (hash_leaves(o, s)) {
+            *seed = s;
+            (void)path_table(o, s);
+            return true;
+        }
+    return false;
+}
+
+bool PairEncoder::store_seed(FlatObject& o, uint32_t* seed) {
+    for (uint32_t s = 0; s <= 255; s++)
+        if (hash_single(o, s)) {
+            *seed = s;
+            return true;
+        }
+    return first_seed(o, seed);
+}
+
+bool PairEncoder::hash_leaves(FlatObject& o, uint32_t seed) {
     const uint64_t mask = cfg_.hash_bits >= 64 ? ~0ULL : ((1ULL << cfg_.hash_bits) - 1);
     auto by_h = [](const LeafRec& x, const LeafRec& y) { return x.h < y.h; };
     for (std::vector<LeafRec>* v : {&o.spec, &o.stat}) {
@@ -338,14 +459,12 @@ bool PairEncoder::hash_single(FlatObject& o, uint32_t seed) {
             if ((*v)[i].h == (*v)[i - 1].h) return false;
     }
     const std::string& sp = status_path_bytes();
-    if (!sentinel_check(o, o.stat, chain_hash(sp.data(), sp.size(), seed) & mask)) return false;
-    fingerprints(o);
-    return true;
+    return sentinel_check(o, o.stat, chain_hash(sp.data(), sp.size(), seed) & mask);
 }
 
 bool PairEncoder::pair_seed(FlatObject& a, FlatObject& b, uint32_t* seed) {
     if (!assign_seed(a, b, seed)) return false;
-    fingerprints(b);
+    (void)path_table(b, *seed);  // b.tab: valid, or GPUDIFF_TAB_NONE (its slot then goes through old_json)
     return true;
 }
 
@@ -354,18 +473,10 @@ void PairEncoder::write_object(const FlatObject& o, std::vector<uint8_t>& pool, 
     write_blob(o, pool, off, sl, sar, tl, tar);
 }
 
-void PairEncoder::write_object_fp(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
-                                  uint32_t* sar, uint32_t* tl, uint32_t* tar, uint32_t* bytes) {
+void PairEncoder::write_object_tab(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
+                                   uint32_t* sar, uint32_t* tl, uint32_t* tar, uint32_t* bytes) {
     write_blob(o, pool, off, sl, sar, tl, tar);
-    const size_t n = o.spec.size() + o.stat.size();
-    const size_t base = pool.size();
-    pool.resize(base + ((8 * n + 15) & ~(size_t)15), 0);
-    uint8_t* f = pool.data() + base;
-    for (const std::vector<LeafRec>* v : {&o.spec, &o.stat})
-        for (const LeafRec& r : *v) {
-            memcpy(f, &r.fp, 8);
-            f += 8;
-        }
+    pool.insert(pool.end(), o.tab.data.begin(), o.tab.data.end());
     *bytes = (uint32_t)(pool.size() - *off);
 }
 

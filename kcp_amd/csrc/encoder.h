@@ -25,7 +25,6 @@ namespace gd {
 
 struct LeafRec {
     uint64_t h;
-    uint64_t fp;  // object store: second, independent 64-bit path hash (collision detection)
     uint64_t val;
     uint32_t meta;
     uint32_t path_off;
@@ -34,14 +33,54 @@ struct LeafRec {
     const char* vptr;
 };
 
+// Object store: a blob's path table (include/gpudiff_format.h), serialized as
+// the device trailer: hs[n] | phs[n] | cs[n] | key bytes | pad to a multiple of 16.
+struct PathTable {
+    std::vector<uint8_t> data;
+    uint32_t n = 0;  // GPUDIFF_TAB_NONE: no valid table (data empty)
+    void clear() {
+        data.clear();
+        n = 0;
+    }
+};
+
+// read-only view of a table (host memory: a PathTable or a trailer copied back)
+struct TabView {
+    const uint64_t* hs = nullptr;
+    const uint64_t* phs = nullptr;
+    const uint64_t* cs = nullptr;
+    const uint8_t* keys = nullptr;
+    uint32_t n = 0;
+};
+inline TabView tab_view(const uint8_t* trailer, uint32_t n) {
+    TabView v;
+    if (n == GPUDIFF_TAB_NONE) {
+        v.n = n;
+        return v;
+    }
+    v.hs = (const uint64_t*)trailer;
+    v.phs = v.hs + n;
+    v.cs = v.phs + n;
+    v.keys = trailer + 24ull * n;
+    v.n = n;
+    return v;
+}
+inline TabView tab_view(const PathTable& t) { return tab_view(t.data.data(), t.n); }
+// true iff both tables are valid and every path hash both hold has the same
+// parent hash and the same last component in each (then the shared hashes
+// name the same paths)
+bool tab_agree(const TabView& old, const TabView& nw);
+
 struct FlatObject {
     std::vector<LeafRec> spec, stat;
     std::string paths;   // concatenated path bytes
     uint32_t flags = 0;  // GPUDIFF_OBJ_*
+    PathTable tab;       // object store: built by hash_single / pair_seed
     void clear() {
         spec.clear();
         stat.clear();
         paths.clear();
+        tab.clear();
         flags = 0;
     }
 };
@@ -69,20 +108,33 @@ class PairEncoder {
     // ---- object store (single objects against a resident version)
     // Parses and flattens one object into `o` (false on a decode error).
     bool flatten_json(const uint8_t* json, size_t len, Arena& arena, FlatObject& o);
-    // Path hashes under `seed` (sorted) plus fingerprints; true iff the hashes
-    // are unique within the object and the status sentinel is unambiguous.
+    // Path hashes under `seed` (sorted) plus the path table; true iff the
+    // hashes are unique within the object, the status sentinel is unambiguous
+    // and the table is valid (its node hashes unique and none the root's).
     bool hash_single(FlatObject& o, uint32_t seed);
+    // The leaf part of hash_single (the seed the pair ({}, o) takes); o.tab
+    // is left alone.
+    bool hash_leaves(FlatObject& o, uint32_t seed);
+    // Smallest seed for o diffed against the empty object (as encode_json
+    // picks it), with o.tab built (GPUDIFF_TAB_NONE if not valid there).
+    bool first_seed(FlatObject& o, uint32_t* seed);
+    // Seed o is stored with when its event is reported conservatively: the
+    // smallest with a valid table, else the smallest leaf-valid one.
+    bool store_seed(FlatObject& o, uint32_t* seed);
     // Smallest seed valid for the pair (a, b) as encode_json would pick it;
-    // fills b's fingerprints too.  False if no seed <= 255 works.
+    // fills b.tab (GPUDIFF_TAB_NONE if b's table is not valid under that
+    // seed).  False if no seed <= 255 works.
     bool pair_seed(FlatObject& a, FlatObject& b, uint32_t* seed);
+    // o.tab for the region leaves' paths under `seed` (false, and n =
+    // GPUDIFF_TAB_NONE: not valid)
+    bool path_table(FlatObject& o, uint32_t seed);
     // Appends o's blob (16-B aligned) and reports its layout.
     void write_object(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl, uint32_t* sar,
                       uint32_t* tl, uint32_t* tar);
-    // Device object store format: the blob followed by the fingerprint trailer
-    // (fp of the spec leaves, then of the status leaves, in key order; padded
-    // to 16 B) -- the bytes kernel K0 writes for the same object.
-    void write_object_fp(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl, uint32_t* sar,
-                         uint32_t* tl, uint32_t* tar, uint32_t* bytes);
+    // Device object store format: the blob followed by its path table (o.tab)
+    // -- the bytes kernel K0 writes for the same object.
+    void write_object_tab(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
+                          uint32_t* sar, uint32_t* tl, uint32_t* tar, uint32_t* bytes);
 
     uint64_t leaves_written = 0;
     uint64_t reseeded = 0;
@@ -94,9 +146,15 @@ class PairEncoder {
 
    private:
     bool assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed);
+    bool pair_valid(FlatObject& a, FlatObject& b, uint32_t seed);
     void write_blob(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
                     uint32_t* sar, uint32_t* tl, uint32_t* tar);
     EncodeConfig cfg_;
+    struct TabNode {  // path_table's working set: one per path prefix
+        uint64_t h, ph, c;
+        uint32_t pend, koff, poff;
+    };
+    std::vector<TabNode> tab_scratch_;
 };
 
 // Chained path hash over encoded path bytes: h(empty) = seed,
@@ -104,8 +162,6 @@ class PairEncoder {
 // parent's hash and its own component, so the device tokenizer hashes a tree
 // level by level (kernels K0*).  Masking to hash_bits happens on the result.
 uint64_t chain_hash(const char* p, size_t n, uint64_t seed);
-// Root of the object store's fingerprint chain (an independent second path hash)
-constexpr uint64_t kFingerprintSeed = GPUDIFF_FP_ROOT;
 
 // Status-region sentinel path bytes: [Key "status"]
 const std::string& status_path_bytes();

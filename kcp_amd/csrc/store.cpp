@@ -7,11 +7,11 @@
 //   1. events are split by slot over the encode threads (slot % T), so the
 //      events of one slot are encoded in order by one thread and chain;
 //   2. each new object is parsed, flattened, hashed with the slot's seed and
-//      checked against the resident version's (pathHash, fingerprint) lists
-//      (a second independent 64-bit hash of every path): equal hashes with
-//      different fingerprints are a collision and the pair is re-encoded from
-//      old_json with a fresh seed (PairEncoder::pair_seed, the same seed the
-//      batch path would pick);
+//      its path table checked against the resident version's (exact: a hash
+//      both hold must have the same parent hash and last component in each,
+//      include/gpudiff_format.h); a disagreement is a collision and the pair is
+//      re-encoded from old_json with a fresh seed (PairEncoder::pair_seed, the
+//      same seed the batch path would pick when b's table allows it);
 //   3. blobs go to per-thread parts with batch-local offsets; after the
 //      threads join, the current space is compacted into the other one if
 //      the batch does not fit (K7 k_move_blobs packs every live blob and every
@@ -39,10 +39,6 @@ namespace {
 constexpr uint64_t kLocal = 1ull << 63;  // offset tag: batch-local (part << 48 | offset in part)
 constexpr int kLocalPartShift = 48;
 
-struct HF {
-    uint64_t h, fp;
-};
-
 struct Slot {
     bool live = false;
     uint32_t seed = 0;
@@ -50,7 +46,7 @@ struct Slot {
     uint32_t bytes = 0, spec_l = 0, spec_ar = 0, stat_l = 0, stat_ar = 0;
     uint32_t oflags = 0;   // GPUDIFF_OBJ_HAS_STATUS
     uint64_t epoch = 0;    // last batch that touched the slot
-    std::vector<HF> spec, stat;
+    PathTable tab;         // the resident version's path table (host RAM)
 };
 
 struct Blob {
@@ -71,20 +67,6 @@ struct Worker {
 };
 
 inline uint64_t local_tag(uint32_t part, uint64_t off) { return kLocal | ((uint64_t)part << kLocalPartShift) | off; }
-
-bool no_collision(const std::vector<HF>& old, const std::vector<LeafRec>& nw) {
-    size_t i = 0, j = 0;
-    while (i < old.size() && j < nw.size()) {
-        if (old[i].h < nw[j].h) i++;
-        else if (old[i].h > nw[j].h) j++;
-        else {
-            if (old[i].fp != nw[j].fp) return false;
-            i++;
-            j++;
-        }
-    }
-    return true;
-}
 
 uint32_t blob_bytes(uint32_t sl, uint32_t sar, uint32_t tl, uint32_t tar) {
     return (uint32_t)(gpudiff_seg_bytes(sl, sar) + gpudiff_seg_bytes(tl, tar));
@@ -190,15 +172,13 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
         if (!enc.flatten_json(e.new_json, e.new_len, w.arena_new, w.fn)) {
             conservative();
             S.live = false;
-            S.spec.clear();
-            S.stat.clear();
+            S.tab.clear();
             continue;
         }
         Blob A{0, 0, 0, 0, 0, 0, 0, false};
         uint32_t seed = 0;
         bool ok = false, pair_error = false;
-        if (S.live && S.seed == 0 && enc.hash_single(w.fn, 0) && no_collision(S.spec, w.fn.spec) &&
-            no_collision(S.stat, w.fn.stat)) {
+        if (S.live && S.seed == 0 && enc.hash_single(w.fn, 0) && tab_agree(tab_view(S.tab), tab_view(w.fn.tab))) {
             ok = true;  // the common case: the resident version is the old side as it stands
             A = Blob{S.off, S.bytes, S.spec_l, S.spec_ar, S.stat_l, S.stat_ar, S.oflags, false};
         } else if (e.old_json) {
@@ -217,15 +197,14 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
             } else {
                 pair_error = true;  // undecodable old object or no valid seed: as gpudiff_encode_pairs
             }
-        } else if (S.live && S.seed && enc.hash_single(w.fn, S.seed) && no_collision(S.spec, w.fn.spec) &&
-                   no_collision(S.stat, w.fn.stat)) {
+        } else if (S.live && S.seed && enc.hash_single(w.fn, S.seed) &&
+                   tab_agree(tab_view(S.tab), tab_view(w.fn.tab))) {
             ok = true;  // slot re-seeded earlier and no old object to re-encode: keep its seed
             seed = S.seed;
             A = Blob{S.off, S.bytes, S.spec_l, S.spec_ar, S.stat_l, S.stat_ar, S.oflags, false};
         } else if (!S.live) {
             // first sighting without an old object: diff against the empty object {}
-            for (seed = 0; seed <= 255 && !ok; seed++) ok = enc.hash_single(w.fn, seed);
-            seed--;
+            ok = enc.first_seed(w.fn, &seed);
             pair_error = !ok;
         } else {
             pair_error = true;
@@ -234,13 +213,9 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
         // store the new version (self-consistent seed if the pair failed)
         if (pair_error) {
             conservative();
-            bool self = false;
-            for (seed = 0; seed <= 255 && !self; seed++) self = enc.hash_single(w.fn, seed);
-            seed--;
-            if (!self) {
+            if (!enc.store_seed(w.fn, &seed)) {
                 S.live = false;
-                S.spec.clear();
-                S.stat.clear();
+                S.tab.clear();
                 continue;
             }
         }
@@ -282,10 +257,7 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
         S.oflags = w.fn.flags & GPUDIFF_OBJ_HAS_STATUS;
         w.live_delta++;
         w.bytes_delta += S.bytes;
-        S.spec.resize(w.fn.spec.size());
-        for (size_t k = 0; k < w.fn.spec.size(); k++) S.spec[k] = HF{w.fn.spec[k].h, w.fn.spec[k].fp};
-        S.stat.resize(w.fn.stat.size());
-        for (size_t k = 0; k < w.fn.stat.size(); k++) S.stat[k] = HF{w.fn.stat[k].h, w.fn.stat[k].fp};
+        std::swap(S.tab, w.fn.tab);
         w.touched.push_back(e.slot);
     }
     size_t pad = (w.pool.size() + 15) & ~(size_t)15;
@@ -480,10 +452,7 @@ int gpudiff_store_forget(gpudiff_ctx* c, gpudiff_store* s, uint32_t slot) {
     }
     S.live = false;
     S.seed = 0;
-    S.spec.clear();
-    S.spec.shrink_to_fit();
-    S.stat.clear();
-    S.stat.shrink_to_fit();
+    S.tab = PathTable();
     return GPUDIFF_OK;
 }
 

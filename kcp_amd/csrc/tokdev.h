@@ -804,7 +804,7 @@ __device__ __forceinline__ uint32_t neg_crd_names_field_len(uint32_t k) {
 struct Scratch {
     uint32_t* tok;
     uint4* rec;
-    uint64_t *h, *fp, *val, *skey;
+    uint64_t *h, *val, *skey;
     uint32_t *meta, *order, *sidx;
     uint8_t* str;
 };

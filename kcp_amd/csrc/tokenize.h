@@ -3,9 +3,9 @@
 //
 // One wave turns one raw JSON object (an informer event body) into the same
 // blob the host encoder writes (include/gpudiff_format.h), followed by the
-// fingerprint trailer the object store checks collisions with:
+// path table the object store checks old-vs-new paths with:
 //
-//   blob = [spec segment][status segment][fp(spec leaves) u64][fp(status leaves) u64]
+//   blob = [spec segment][status segment][hs u64[n] | phs u64[n] | cs u64[n] | key bytes | pad]
 //
 // Anything outside the device's exact subset -- a Go decode error of any kind,
 // a float literal beyond the exact fast path, a key that needs unescaping, a
@@ -30,12 +30,12 @@ struct TokDoc {
 
 struct TokOut {
     uint64_t off;          // blob offset in the output space
-    uint32_t bytes;        // blob bytes incl. fingerprint trailer (multiple of 16)
+    uint32_t bytes;        // blob bytes incl. the path table (multiple of 16)
     uint32_t spec_l, spec_ar, stat_l, stat_ar;
     uint32_t oflags;       // GPUDIFF_OBJ_HAS_STATUS
     uint32_t status;       // GPUDIFF_TOK_*
     uint32_t n_nodes;
-    uint32_t pad;
+    uint32_t n_tab;        // path-table entries
 };
 static_assert(sizeof(TokDoc) == 32, "TokDoc");
 static_assert(sizeof(TokOut) == 48, "TokOut");
@@ -47,7 +47,7 @@ __host__ __device__ inline uint32_t node_cap(uint32_t len) { return len / 2u + 2
 // Per-document working area: tokens, node records, hashes, values, sort keys,
 // decoded strings.  Bounded by the JSON length (a node needs >= 2 bytes).
 struct TokLayout {
-    uint64_t tok, rec, h, fp, val, skey, meta, order, sidx, str, total;
+    uint64_t tok, rec, h, val, skey, meta, order, sidx, str, total;
 };
 __host__ __device__ inline TokLayout tok_layout(uint32_t len) {
     TokLayout L;
@@ -55,8 +55,7 @@ __host__ __device__ inline TokLayout tok_layout(uint32_t len) {
     L.tok = 0;
     L.rec = tok_align(4ull * tok_cap(len));
     L.h = L.rec + tok_align(16ull * nc);
-    L.fp = L.h + tok_align(8ull * nc);
-    L.val = L.fp + tok_align(8ull * nc);
+    L.val = L.h + tok_align(8ull * nc);
     L.skey = L.val + tok_align(8ull * nc);
     L.meta = L.skey + tok_align(8ull * nc);
     L.order = L.meta + tok_align(4ull * nc);
@@ -66,8 +65,9 @@ __host__ __device__ inline TokLayout tok_layout(uint32_t len) {
     return L;
 }
 __host__ __device__ inline uint64_t tok_scratch_bytes(uint32_t len) { return tok_layout(len).total; }
-// upper bound of a document's blob (leaf >= 2 JSON bytes -> 28 B; segment pads)
-__host__ __device__ inline uint64_t tok_blob_bound(uint32_t len) { return 14ull * len + 64u; }
+// upper bound of a document's blob: a node takes >= 2 JSON bytes and <= 20 B
+// of segment + 16 B of long-value pad + 24 B of path table; key bytes <= len
+__host__ __device__ inline uint64_t tok_blob_bound(uint32_t len) { return 31ull * len + 96u; }
 
 // K10 (k_encode_docs in marshal mode, the write path): per-document working
 // area.  tok/rec/str are laid out as phases 1-2 of K0 expect; the rest holds
@@ -162,14 +162,14 @@ constexpr uint32_t kTokSlack = 32u;                 // readable bytes K0 needs a
 
 // ------------------------------------------------------------ device object store
 // One slot per informer-cache object: its resident blob (K0 format, with the
-// fingerprint trailer) in the current space.
+// path table) in the current space.
 struct DSlot {
     uint64_t off;
     uint32_t spec_l, spec_ar, stat_l, stat_ar;
-    uint32_t bytes;   // blob + trailer
+    uint32_t bytes;   // blob + path table
     uint32_t flags;   // DS_* | seed << 8
     uint32_t pend;    // last batch that deferred an event of this slot to the host
-    uint32_t pad;
+    uint32_t n_tab;   // path-table entries
 };
 static_assert(sizeof(DSlot) == 40, "DSlot");
 constexpr uint32_t DS_LIVE = 1u, DS_HAS_STATUS = 2u, DS_PENDING = 4u;
@@ -226,7 +226,7 @@ hipError_t launch_negotiate_pairs(hipStream_t s, const NegOut* outs, const uint8
                                   const uint8_t* json, uint32_t n_pairs, int32_t* actions);
 // K12: group the documents by owned-by label (xxh64 radix sort + byte check),
 // int32 sums per group; see rollup.hip
-// K0c: per event, a path-hash collision with its old side (equal key, other fingerprint)
+// K0c: per event, a path-hash collision with its old side (the two path tables disagree)
 hipError_t launch_collide(hipStream_t s, const DocLink* links, const TokOut* outs, const DSlot* slots, uint32_t n,
                           const uint8_t* space, uint8_t* coll);
 // K0x: walk each slot's chain: rows for K2, deferrals, the slot's new resident blob

@@ -18,13 +18,16 @@
 //     metadata/status, top-level null dropped), L/N (metadata.labels /
 //     metadata.annotations children, kept only if every value is a string),
 //     T (status subtree) -- specsyncer.go:17-41, statussyncer.go:15-27
-//   3 per node, lane-parallel: chained path hash and fingerprint level by
-//     level (h(child) = XXH64(component, h(parent))), value decoding (Go
-//     escapes / UTF-8 repair, int64 or exact-fast-path float64, literals)
+//   3 per node, lane-parallel: chained path hash level by level
+//     (h(child) = XXH64(component, h(parent))), value decoding (Go escapes /
+//     UTF-8 repair, int64 or exact-fast-path float64, literals)
 //   4 bitonic sort of the node keys; equal neighbours (a duplicate key or a
-//     collision) hand the document to the host
+//     collision) or a node hash equal to the root's hand the document to the
+//     host
 //   5 ballot/prefix compaction of the spec / status leaves in key order into
-//     the blob, allocated with one atomic on the space's append point
+//     the blob, and of the path-table nodes (region leaves and their
+//     ancestors) behind it, allocated with one atomic on the space's append
+//     point
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -100,7 +103,6 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         S.tok = (uint32_t*)(base + LY.tok);
         S.rec = (uint4*)(base + LY.rec);
         S.h = (uint64_t*)(base + LY.h);
-        S.fp = (uint64_t*)(base + LY.fp);
         S.val = (uint64_t*)(base + LY.val);
         S.skey = (uint64_t*)(base + LY.skey);
         S.meta = (uint32_t*)(base + LY.meta);
@@ -522,19 +524,15 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t i = S.order[beg + j0 + lane];
                     const uint4 r = S.rec[i];
                     const uint64_t ph = r.x == 0 ? seed : S.h[r.x];
-                    const uint64_t pf = r.x == 0 ? GPUDIFF_FP_ROOT : S.fp[r.x];
-                    uint64_t hh, ff;
+                    uint64_t hh;
                     if (r.y & KEYBIT) {
                         const uint32_t kt = r.y & ~KEYBIT;
                         const uint32_t op = S.tok[kt] & POS_MASK, cp = S.tok[kt + 1] & POS_MASK;
                         hh = hash_key(ph, d + op + 1, cp - op - 1);
-                        ff = hash_key(pf, d + op + 1, cp - op - 1);
                     } else {
                         hh = hash_index(ph, r.y);
-                        ff = hash_index(pf, r.y);
                     }
                     S.h[i] = hh;
-                    S.fp[i] = ff;
                 }
             }
             beg += cnt;
@@ -574,14 +572,17 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 wave_sync();
             }
         }
+        // unique node hashes, none the root's: a parent hash in the path table
+        // then names exactly one node (include/gpudiff_format.h)
+        const uint64_t root = seed & mask;
         bool dup = false;
-        for (uint32_t j = lane + 1; j < ns; j += 64)
-            if (skey[j] == skey[j - 1]) dup = true;
+        for (uint32_t j = lane; j < ns; j += 64)
+            if ((j && skey[j] == skey[j - 1]) || skey[j] == root) dup = true;
         if (ballot(dup)) status = GPUDIFF_TOK_HASH;
     }
 
     mark(4);
-    // ------------------------------------------------------------ phase 5: blob
+    // ------------------------------------------------------------ phase 5: blob + path table
     o.n_nodes = nn;
     o.oflags = has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
     if (status == GPUDIFF_TOK_OK) {
@@ -591,22 +592,48 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             if (reg == R_SPEC || (reg == R_LABELS && labels_ok) || (reg == R_ANNOT && annot_ok)) return 1u;
             return reg == R_STATUS ? 2u : 0u;
         };
-        uint32_t Ls = 0, Lt = 0, ARs = 0, ARt = 0;
+        // path-table nodes: the region leaves and their ancestors but the root -- every
+        // container of the spec / status subtrees, and metadata, metadata.labels and
+        // metadata.annotations when label / annotation leaves are encoded
+        const bool lab_in = labels_node != NONE && labels_ok && !(S.rec[labels_node].w & NI_LEAF);
+        const bool ann_in = annot_node != NONE && annot_ok && !(S.rec[annot_node].w & NI_LEAF);
+        const bool meta_in = lab_in || ann_in;
+        auto in_tab = [&](uint32_t i, uint32_t w) -> bool {
+            if (region_of(w)) return true;
+            const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
+            if (!(w & NI_LEAF) && (reg == R_SPEC || reg == R_STATUS)) return true;
+            return (i == meta_node && meta_in) || (i == labels_node && lab_in) || (i == annot_node && ann_in);
+        };
+        auto key_span = [&](const uint4& r, uint32_t* op) -> uint32_t {  // key bytes of a member node
+            if (!(r.y & KEYBIT)) return 0u;
+            const uint32_t kt = r.y & ~KEYBIT;
+            *op = (S.tok[kt] & POS_MASK) + 1u;
+            return (S.tok[kt + 1] & POS_MASK) - *op;
+        };
+        uint32_t Ls = 0, Lt = 0, ARs = 0, ARt = 0, Nt = 0, KB = 0;
         for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
             const uint32_t j = j0 + lane;
-            uint32_t rg = 0, ar = 0;
+            uint32_t rg = 0, ar = 0, kl = 0;
+            bool t = false;
             if (j < ns) {
                 const uint32_t i = sidx[j];
-                rg = region_of(S.rec[i].w);
+                const uint4 r = S.rec[i];
+                rg = region_of(r.w);
                 if (rg) ar = meta_arena(S.meta[i]);
+                t = in_tab(i, r.w);
+                uint32_t op;
+                if (t) kl = key_span(r, &op);
             }
             Ls += popc64(ballot(rg == 1));
             Lt += popc64(ballot(rg == 2));
+            Nt += popc64(ballot(t));
             ARs += wave_sum(rg == 1 ? ar : 0u);
             ARt += wave_sum(rg == 2 ? ar : 0u);
+            KB += wave_sum(kl);
         }
         const uint64_t seg_s = seg_bytes(Ls, ARs), seg_t = seg_bytes(Lt, ARt);
-        const uint64_t bytes = (seg_s + seg_t + 8ull * (Ls + Lt) + 15ull) & ~15ull;
+        const uint64_t tab = (24ull * Nt + KB + 15u) & ~15ull;  // gpudiff_tab_bytes: blobs stay 16-B multiples
+        const uint64_t bytes = seg_s + seg_t + tab;
         uint64_t off = 0;
         if (lane == 0) off = atomicAdd(used, (unsigned long long)bytes);
         off = rdlane64(off, 0);
@@ -616,26 +643,34 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             uint8_t* blob = space + off;
             uint8_t* segp[2] = {blob, blob + seg_s};
             const uint32_t Lr[2] = {Ls, Lt};
-            uint64_t* fpt[2] = {(uint64_t*)(blob + seg_s + seg_t), (uint64_t*)(blob + seg_s + seg_t) + Ls};
-            // zero the pad between metas and arena, and the trailer pad
+            uint64_t* hs = (uint64_t*)(blob + seg_s + seg_t);
+            uint64_t* phs = hs + Nt;
+            uint64_t* cs = phs + Nt;
+            uint8_t* keys = (uint8_t*)(cs + Nt);
+            // zero the pad between metas and arena, and the key area's pad
             for (uint32_t g = 0; g < 2; g++) {
                 const uint32_t L = Lr[g];
                 const uint32_t pad_beg = 20u * L, pad_end = (20u * L + 15u) & ~15u;
                 if (lane < (pad_end - pad_beg) / 4u) ((uint32_t*)(segp[g] + pad_beg))[lane] = 0u;
             }
-            if (lane == 0 && ((Ls + Lt) & 1u)) *(uint64_t*)(blob + seg_s + seg_t + 8ull * (Ls + Lt)) = 0ull;
-            uint32_t rank[2] = {0, 0}, aoff[2] = {0, 0};
+            if (lane < tab - 24ull * Nt - KB) keys[KB + lane] = 0;
+            const uint64_t root = seed & mask;
+            uint32_t rank[2] = {0, 0}, aoff[2] = {0, 0}, trank = 0, tko = 0;
             for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
                 const uint32_t j = j0 + lane;
-                uint32_t rg = 0, i = 0, m = 0, ar = 0;
+                uint32_t rg = 0, i = 0, m = 0, ar = 0, kl = 0, kop = 0;
+                uint4 r = make_uint4(0u, 0u, 0u, 0u);
+                bool t = false;
                 if (j < ns) {
                     i = sidx[j];
-                    const uint32_t w = S.rec[i].w;
-                    rg = region_of(w);
+                    r = S.rec[i];
+                    rg = region_of(r.w);
                     if (rg) {
                         m = S.meta[i];
                         ar = meta_arena(m);
                     }
+                    t = in_tab(i, r.w);
+                    if (t) kl = key_span(r, &kop);
                 }
                 uint32_t my_rank = 0, my_aoff = 0;
                 for (uint32_t g = 0; g < 2; g++) {
@@ -655,8 +690,20 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     ((uint64_t*)sp8)[my_rank] = skey[j];
                     ((uint64_t*)(sp8 + 8ull * L))[my_rank] = S.val[i];
                     ((uint32_t*)(sp8 + 16ull * L))[my_rank] = m;
-                    fpt[g][my_rank] = S.fp[i];
                 }
+                // the path-table entry: hash, parent hash, component (+ key bytes)
+                const uint64_t tbal = ballot(t);
+                const uint32_t kinc = wave_incl_scan(kl);
+                if (t) {
+                    const uint32_t tr = trank + popc64(tbal & mask_lt(lane));
+                    const uint32_t ko = tko + kinc - kl;
+                    hs[tr] = skey[j];
+                    phs[tr] = r.x == 0 ? root : (S.h[r.x] & mask);
+                    cs[tr] = (r.y & KEYBIT) ? (((uint64_t)kl << 32) | ko) : (GPUDIFF_TAB_INDEX | r.y);
+                    for (uint32_t q = 0; q < kl; q++) keys[ko + q] = d[kop + q];
+                }
+                trank += popc64(tbal);
+                tko += rdlane(kinc, 63);
                 // long strings: wave-cooperative 16-B copies into the arena
                 for (uint64_t bl = ballot(ar != 0); bl; bl &= bl - 1) {
                     const uint32_t src_lane = (uint32_t)__builtin_ctzll(bl);
@@ -664,9 +711,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t sm = rdlane(m, src_lane);
                     const uint32_t sg = rdlane(rg, src_lane) - 1u;
                     const uint32_t sa = rdlane(my_aoff, src_lane);
-                    const uint4 r = S.rec[si];
-                    const uint32_t op = S.tok[r.z] & POS_MASK;
-                    const uint8_t* src = (r.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1);
+                    const uint4 rr = S.rec[si];
+                    const uint32_t op = S.tok[rr.z] & POS_MASK;
+                    const uint8_t* src = (rr.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1);
                     const uint32_t slen = sm >> 3;
                     uint8_t* dst = segp[sg] + ((20ull * Lr[sg] + 15ull) & ~15ull) + sa;
                     for (uint32_t c16 = lane; c16 * 16u < slen; c16 += 64) {
@@ -692,6 +739,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             o.spec_ar = ARs;
             o.stat_l = Lt;
             o.stat_ar = ARt;
+            o.n_tab = Nt;
         }
     }
     o.status = status;

@@ -106,7 +106,8 @@ class StoreStats(C.Structure):
 
 class ObjInfo(C.Structure):
     _fields_ = [("status", C.c_int32), ("oflags", C.c_uint32), ("spec_l", C.c_uint32), ("spec_ar", C.c_uint32),
-                ("stat_l", C.c_uint32), ("stat_ar", C.c_uint32), ("off", C.c_uint64), ("bytes", C.c_uint64)]
+                ("stat_l", C.c_uint32), ("stat_ar", C.c_uint32), ("off", C.c_uint64), ("bytes", C.c_uint64),
+                ("n_tab", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -640,7 +641,7 @@ class Engine:
                      device_encode: bool = False) -> ObjectStore:
         return ObjectStore(self, max_slots, space_bytes, max_events, device_encode)
 
-    # ---- object encoding (device-store format: blob + fingerprint trailer)
+    # ---- object encoding (device-store format: blob + path table)
     def encode_objects(self, docs, seeds=None, out_cap: int = 0):
         """Kernel K0 over the documents: [(ObjInfo dict, blob bytes or None)]."""
         docs = [to_json_bytes(x) for x in docs]
@@ -649,7 +650,7 @@ class Engine:
         ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p) for b in bufs])
         lens = (C.c_size_t * max(n, 1))(*[len(x) for x in docs])
         sd = (C.c_uint32 * max(n, 1))(*(list(seeds) if seeds is not None else [0] * n))
-        cap = out_cap or sum(14 * len(x) + 64 for x in docs) + 16
+        cap = out_cap or sum(31 * len(x) + 96 for x in docs) + 16
         out = C.create_string_buffer(cap)
         info = (ObjInfo * max(n, 1))()
         _chk(_lib.gpudiff_encode_objects(self.ctx, ptrs, lens, sd, n, C.cast(out, C.c_void_p), cap, info),
@@ -1035,6 +1036,36 @@ def encode_object_host(doc, seed: int = 0, path_hash_bits: int = 64):
 
 
 # ------------------------------------------------------------------ decoding helpers (tests / tooling)
+
+TAB_INDEX = 1 << 63
+TAB_NONE = 0xFFFFFFFF
+
+
+def decode_path_table(blob: bytes, info: dict):
+    """Path table of a device-store blob (include/gpudiff_format.h) -> [(hash,
+    parent hash, component)], component ('K', key bytes) or ('I', index), in
+    table order; None for a blob stored without a valid table."""
+    n = info["n_tab"]
+    if n == TAB_NONE:
+        return None
+    seg = lambda L, ar: (((20 * L) + 15) & ~15) + ar
+    base = seg(info["spec_l"], info["spec_ar"]) + seg(info["stat_l"], info["stat_ar"])
+    if not n:
+        return []
+    hs = np.frombuffer(blob, "<u8", n, base)
+    phs = np.frombuffer(blob, "<u8", n, base + 8 * n)
+    cs = np.frombuffer(blob, "<u8", n, base + 16 * n)
+    keys = base + 24 * n
+    out = []
+    for h, ph, c in zip(hs.tolist(), phs.tolist(), cs.tolist()):
+        if c & TAB_INDEX:
+            comp = ("I", c & 0xFFFFFFFF)
+        else:
+            ko, kl = c & 0xFFFFFFFF, c >> 32
+            comp = ("K", blob[keys + ko:keys + ko + kl])
+        out.append((h, ph, comp))
+    return out
+
 
 def decode_segment(pool: bytes, off: int, L: int, arena: int):
     """Canonical segment -> list of (key, val, meta, value_bytes)."""

@@ -89,6 +89,7 @@ def test_replay_matches_oracle(drop_old, dev):
     _run(e, st, _stream(1, 60, 6, 150), drop_old)
     s = st.stats()
     assert s.events == 900 and s.live_slots == 60 and s.collisions_unresolved == 0
+    assert s.deferred == 0 or drop_old  # regular objects: K0 encodes and K0c confirms every event
     st.free()
     e.close()
 
@@ -103,6 +104,7 @@ def test_compaction_keeps_results_exact(dev):
     s = st.stats()
     assert s.compactions >= 3, s.compactions
     assert s.used_bytes <= 512 << 10
+    assert s.deferred == 0  # compacted blobs keep their path tables whole (no false collisions)
     st.free()
     e.close()
 
@@ -114,6 +116,51 @@ def test_forced_collisions_reseed_through_old_json(dev):
     _run(e, st, _stream(3, 30, 5, 80))
     s = st.stats()
     assert s.reseeded > 0 and s.collisions_unresolved == 0
+    st.free()
+    e.close()
+
+
+@MODES
+def test_path_tables_exact_at_16_bits(dev):
+    """16-bit path hashes: paths of an object's old and new versions share hashes
+    by chance in a good fraction of the events; the path tables (K0c on the
+    device, tab_agree on the host) catch every such collision exactly and the
+    pair is re-encoded from old_json, so every result equals the oracle's."""
+    e = G.Engine(device=0, encode_threads=4, path_hash_bits=16)
+    st = e.object_store(max_slots=40, space_bytes=64 << 20, max_events=256, device_encode=dev)
+    _run(e, st, _stream(9, 40, 6, 120))
+    s = st.stats()
+    assert s.reseeded > 0 and s.collisions_unresolved == 0
+    st.free()
+    e.close()
+
+
+@MODES
+def test_adversarial_collisions_never_equal(dev):
+    """Objects built so that the old and new versions' segments are identical
+    key for key and value for value under 16-bit path hashes although the paths
+    differ (same parent, other key; other parent): with old_json the result is
+    the oracle's, without it the event is reported dirty (conservative), never
+    equal."""
+    from tests.test_path_table import adversarial_pairs
+    pairs = adversarial_pairs(16)
+    e = G.Engine(device=0, encode_threads=2, path_hash_bits=16)
+    st = e.object_store(max_slots=8, space_bytes=8 << 20, max_events=16, device_encode=dev)
+    olds = [json.dumps(a, separators=(",", ":")).encode() for a, _b in pairs]
+    news = [json.dumps(b, separators=(",", ":")).encode() for _a, b in pairs]
+    k = len(pairs)
+    # first sightings (slots 0..k-1 and k..2k-1 hold the old versions), diffed against {}
+    r = e.wait(st.submit([(i, olds[i % k], None, i) for i in range(2 * k)]))
+    assert_matches(r, [(b"{}", olds[i % k]) for i in range(2 * k)], hash_bits=16)
+    # the new versions with old_json (slots 0..k-1): the oracle's results
+    r = e.wait(st.submit([(i, news[i], olds[i], i) for i in range(k)]))
+    exp = assert_matches(r, [(olds[i], news[i]) for i in range(k)], hash_bits=16)
+    assert all(x["spec_dirty"] and x["seed"] != 0 for x in exp)
+    # without old_json (slots k..2k-1): conservative, never equal
+    r = e.wait(st.submit([(k + i, news[i], None, i) for i in range(k)]))
+    assert r.pair_flags.tolist() == [G.SPEC_DIRTY | G.STATUS_DIRTY | G.DECODE_ERROR] * k
+    s = st.stats()
+    assert s.collisions_unresolved == k
     st.free()
     e.close()
 
