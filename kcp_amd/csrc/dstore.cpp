@@ -179,11 +179,12 @@ int compact(DStore* s) {
     return GPUDIFF_OK;
 }
 
-int ensure_space(DStore* s, uint64_t bytes) {
-    if (s->used_ub + bytes <= s->space_bytes) return GPUDIFF_OK;
+// compacts when `want` bytes may not fit; fails only when not even `need` bytes fit after it
+int ensure_space(DStore* s, uint64_t want, uint64_t need) {
+    if (s->used_ub + want <= s->space_bytes) return GPUDIFF_OK;
     int rc = compact(s);
     if (rc) return rc;
-    return s->used_ub + bytes <= s->space_bytes ? GPUDIFF_OK : GPUDIFF_E_CAPACITY;
+    return s->used_ub + need <= s->space_bytes ? GPUDIFF_OK : GPUDIFF_E_CAPACITY;
 }
 
 // ------------------------------------------------------------------ host resolution
@@ -404,7 +405,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
     // place: blobs behind the append point, rows, slot states
     const uint64_t pbytes = (pool.size() + 15) & ~15ull;
     pool.resize(pbytes, 0);
-    if ((rc = ensure_space(s, pbytes))) return rc;
+    if ((rc = ensure_space(s, pbytes, pbytes))) return rc;
     if ((rc = grow_dev(&s->res_stage, &s->res_stage_cap, std::max<uint64_t>(pbytes, 16)))) return rc;
     if ((rc = grow_dev(&s->res_ups, &s->res_ups_cap, std::max<size_t>(ups.size(), 1)))) return rc;
     gpudiff_dbatch* d = s->res_d;
@@ -572,14 +573,17 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     std::vector<const uint8_t*> src;
     src.reserve(max_docs);
     uint32_t nd = 0, nh = 0;
-    uint64_t jbytes = 0, bound = 0;
+    uint64_t jbytes = 0, bound = 0, floor = 0;
     auto add_doc = [&](const uint8_t* p, size_t len, uint32_t slot, uint32_t row, const gpudiff_event& e) {
         TokDoc& D = docs[nd];
         memset(&D, 0, sizeof(D));
         D.json_off = jbytes;
         D.json_len = (uint32_t)len;
         jbytes = (jbytes + len + kTokSlack + 15) & ~15ull;
-        bound += 3 * len + 128;  // typical blob + path table < 3x JSON; K0 defers what does not fit (SPACE)
+        // blob + path table: typically < 2.5x the JSON (the append estimate that triggers compaction);
+        // K0 defers a document that does not fit (SPACE) to the host
+        bound += (5 * (uint64_t)len) / 2 + 128;
+        floor += len;
         DocLink& L = links[nd];
         memset(&L, 0, sizeof(L));
         L.slot = slot;
@@ -663,7 +667,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         }
     }
     // 2. capacity (compaction is stream-ordered after every earlier batch)
-    if ((rc = ensure_space(s, bound))) return rc;
+    if ((rc = ensure_space(s, bound, floor))) return rc;
     // 3. upload + kernels
     if ((rc = grow_dev(&R.djson, &R.djson_cap, jbytes)) ||
         (rc = grow_dev(&R.dmeta, &R.dmeta_cap, meta_bytes)) || (rc = grow_dev(&R.douts, &R.docs_cap, nd + 1)))

@@ -104,7 +104,21 @@ def test_compaction_keeps_results_exact(dev):
     s = st.stats()
     assert s.compactions >= 3, s.compactions
     assert s.used_bytes <= 512 << 10
-    assert s.deferred == 0  # compacted blobs keep their path tables whole (no false collisions)
+    st.free()
+    e.close()
+
+
+@MODES
+def test_compaction_keeps_path_tables(dev):
+    """Blobs moved by compactions keep their path tables whole: with room for
+    every batch, K0c confirms every event after the moves (no false collision
+    defers one to the host)."""
+    e = G.Engine(device=0, encode_threads=4)
+    st = e.object_store(max_slots=40, space_bytes=2 << 20, max_events=128, device_encode=dev)
+    _run(e, st, _stream(6, 40, 40, 60))
+    s = st.stats()
+    assert s.compactions >= 2, s.compactions
+    assert s.deferred == 0 and s.reseeded == 0
     st.free()
     e.close()
 
