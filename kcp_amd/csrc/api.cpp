@@ -376,7 +376,7 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
     uint4* cc = nullptr;
     if ((rc = dalloc(&d->pool, d->pool_cap)) || (rc = dalloc(&d->rows, np)) || (rc = dalloc(&d->pair_ids, np)) ||
         (rc = dalloc(&d->flags, np)) || (rc = dalloc(&d->caps, np)) || (rc = dalloc(&cc, nchunks)) ||
-        (rc = dalloc(&d->summary, 8)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
+        (rc = dalloc(&d->summary, 8 + kMaxSegments)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
         (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
         (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) || (rc = dalloc(&d->nbits, np)) ||
@@ -560,7 +560,7 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         if (!ev) return GPUDIFF_E_DEVICE;
     }
     hipStream_t ms = c->stream;
-    HIPCHK(hipMemsetAsync(d->summary, 0, 8 * sizeof(uint32_t), ms));
+    HIPCHK(hipMemsetAsync(d->summary, 0, (8 + kMaxSegments) * sizeof(uint32_t), ms));  // + K2 item counters
     if (ev) HIPCHK(hipEventRecord(ev[0], ms));
     DiffBuffers b = buffers_of(c, d);
     const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);

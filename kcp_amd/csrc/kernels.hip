@@ -760,6 +760,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 }
 
 // ---------------------------------------------------------------- K2, flattened stream
+// DYN variants: chunks at the end of a launch handed out as 8-pair items (about
+// four per wave), unless the whole launch is split already
+__host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift) {
+    return sub_shift ? 0u : min(nch, nwaves / 2u);
+}
+
 // One wave per work item of P = 64 >> sub_shift consecutive pairs.  Lane k
 // loads pair k's 64-B row with four coalesced 16-B loads (one 4 KiB read per
 // item instead of a scalar row load per pair).  The item's compared segments
@@ -773,7 +779,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // its pair (spec or status region); then the wave merge-joins its dirty pairs
 // one at a time into its arena, exactly as k_compare does (same flags, caps,
 // arena order and F_DEFER rule).
-template <int U, int MINB>
+// DYN: after its first item a wave takes the next one from a per-launch counter
+// (summary[8 + segment], zeroed with the pass), fetched while it streams the
+// current item, so the launch ends when the work does, not when the wave with
+// the heaviest static share of items does; the last k2_tail_chunks() chunks are
+// handed out as 8-pair items, so the final round of items is short too.
+template <int U, int MINB, bool DYN = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -791,11 +802,21 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
-    const uint32_t per = 64u >> sub_shift;
-    const uint32_t nitems = (c_end - c_begin) << sub_shift;
-    for (uint32_t it = wave; it < nitems; it += nwaves) {
-        const uint32_t c = c_begin + (it >> sub_shift);
-        const uint32_t p0 = (c << 6) + (it & ((1u << sub_shift) - 1u)) * per;
+    const uint32_t nch = c_end - c_begin;
+    const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift) : 0u;
+    const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
+    const uint32_t nitems = n_full + (tail_c << 3);
+    uint32_t* const ctr = summary + 8u + (arena_per_wave ? arena_off / arena_per_wave : 0u);
+    for (uint32_t it = wave, tk = 0; it < nitems; it = DYN ? uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves : it + nwaves) {
+        if constexpr (DYN) {
+            if (lane == 0) tk = atomicAdd(ctr, 1u);  // the next item; waited for only at the loop's end
+        }
+        const bool tail = it >= n_full;
+        const uint32_t ish = tail ? 3u : sub_shift;
+        const uint32_t j = tail ? it - n_full : it;
+        const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
+        const uint32_t per = 64u >> ish;
+        const uint32_t p0 = (c << 6) + (j & ((1u << ish) - 1u)) * per;
         if (p0 >= n) continue;
         const uint32_t cnt = min(per, n - p0);
         const bool valid = lane < cnt;
@@ -926,7 +947,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t nd = popc64(ballot(dirty));
         const uint32_t cs = wave_sum(dirty ? mycap : 0u);
         if (lane == 0) {
-            if (!sub_shift) {
+            if (!ish) {
                 chunk_counts[c] = make_uint4(ns, nt, nd, cs);
             } else if (ns | nt | nd | cs) {
                 uint32_t* cc = (uint32_t*)(chunk_counts + c);
@@ -1065,7 +1086,18 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 12: return k_compare_flat<4, 5>;
         case 13: return k_compare<true, 4, 1>;  // round 1's default (wave per pair)
         case 10: return k_compare_flat<4, 4>;
-        default: return k_compare_flat<4, 1>;   // 0: 111 VGPRs, 4 waves/SIMD, no spills
+        case 14: return k_compare_flat<4, 1, true>;
+        case 15: return k_compare_flat<2, 1, true>;
+        // 0: 111 VGPRs, 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than
+        // static striding = variant 8 on config3, tools/ab_k2.py on MI355X)
+        default: return k_compare_flat<4, 1, true>;
+    }
+}
+
+static bool k2_is_dyn(uint32_t variant) {
+    switch (variant) {
+        case 0: case 14: case 15: return true;
+        default: return false;
     }
 }
 
@@ -1104,8 +1136,11 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
     uint4* cc = (uint4*)b.chunk_counts;
     const uint32_t sub = k2_sub_shift(b, c1 - c0);
-    if (sub) {
-        hipError_t e = hipMemsetAsync(cc + c0, 0, (size_t)(c1 - c0) * sizeof(uint4), s);
+    const uint32_t v = b.k2_variant & 15u;
+    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub) : 0u;
+    if (sub || tail) {  // split chunks accumulate their counts with atomics
+        const uint32_t z0 = sub ? c0 : c1 - tail;
+        hipError_t e = hipMemsetAsync(cc + z0, 0, (size_t)(c1 - z0) * sizeof(uint4), s);
         if (e != hipSuccess) return e;
     }
     // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment

@@ -5,10 +5,10 @@ opened with different tuning flags (include/gpudiff.h GPUDIFF_OPT_*); all
 variants must produce identical results.
 
 usage: python tools/ab_k2.py [--pairs N] [--rounds R] [--variants name=flags,...]
-  flags bits: 8-11 K2 variant (0 NT x4, 1 plain x4, 2 NT x8, 3 plain x8, 4 NT x2,
-              5 NT x4 <=80 VGPRs, 6 NT x2 <=64 VGPRs, 7 NT x2 <=80 VGPRs; flattened stream:
-              8 x4 = the default 0, 9 x2, 10 x4 <= 128 VGPRs, 11 x2 5 waves/SIMD, 12 x4 5 waves/SIMD;
-              13 = round 1's wave-per-pair k_compare),
+  flags bits: 8-11 K2 variant (wave per pair: 1 plain x4, 2 NT x8, 3 plain x8, 4 NT x2,
+              5 NT x4 <=80 VGPRs, 6 NT x2 <=64 VGPRs, 7 NT x2 <=80 VGPRs, 13 = round 1's default;
+              flattened stream, static items: 8 x4, 9 x2, 10 x4 <= 128 VGPRs, 11 x2 5 waves/SIMD,
+              12 x4 5 waves/SIMD; dynamic items + 8-pair tail: 0 = 14 x4 (the default), 15 x2),
               12-15 K2 blocks/CU (0 = default 5), 16-19 forced segments,
               0x100000 no alternate K2 stream
 """
