@@ -100,6 +100,9 @@ def main():
                     help="strong: the config's population split N ways (the metric's 10M/100k node-wide; "
                          "default for N > 1); weak: per-GPU work fixed (node population = N x the config)")
     ap.add_argument("--chunk", type=int, default=262144)
+    ap.add_argument("--engine-flags", type=lambda x: int(x, 0), default=0,
+                    help="extra GPUDIFF_OPT_* tuning bits for the diff engine (diagnostics, e.g. 0xF << 21 defers "
+                         "every join to K4)")
     ap.add_argument("--threads", type=int, default=0, help="host encode threads (default min(16, cpus))")
     ap.add_argument("--sample", type=int, default=600, help="pairs checked bit-exact vs the oracle (JSON path)")
     ap.add_argument("--cpu-sample", type=int, default=50000, help="pairs in the CPU-baseline sample")
@@ -154,7 +157,8 @@ def main():
     aff, nproc, quota = host_cores()
     threads = args.threads or max(1, min(16, aff))
 
-    eng = G.Engine(device=local_rank, encode_threads=threads, stream=stream.cuda_stream, timing=True)
+    eng = G.Engine(device=local_rank, encode_threads=threads, stream=stream.cuda_stream, timing=True,
+                   flags=args.engine_flags)
     base = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=args.clusters)
     mult = world if scaling == "weak" else 1
     cfg = S.make_cfg(args.config, n_pairs=base.n_pairs * mult, n_clusters=base.n_clusters * mult)
@@ -363,7 +367,7 @@ def main():
                          "format": {"bytes_per_launch": fmt_bytes / launches, "achieved": achieved_fmt,
                                     "frac": achieved_fmt / HBM_PEAK_GBPS,
                                     "def": "bytes K2 reads in this build's CSR format: 64-B row + flag + both "
-                                           "size-matched segments (20 B/leaf + 16-B padded arena)"},
+                                           "size-matched segments (20 B/leaf + the arena: long strings 4-B aligned, padded to 16)"},
                          "diff_pass": {"ms": pass_ms, "achieved": achieved_pass, "frac": achieved_pass / HBM_PEAK_GBPS,
                                        "def": "SURVEY bytes over the whole diff pass (K2..K6)"},
                          "k2_source_hash": src_hash},

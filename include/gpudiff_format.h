@@ -7,7 +7,9 @@
  *   [ spec segment ][ status segment ]
  *
  *   segment(L, arena) = keys[L] u64 | vals[L] u64 | metas[L] u32 | pad to 16
- *                       | arena (each long string value padded to 16 bytes)
+ *                       | arena: the long string values in key order, each at a
+ *                         4-byte aligned offset (zero padded to 4), the whole
+ *                         zero padded to a multiple of 16
  *
  *   keys   = pathHash = XXH64(path bytes, pair seed), ascending, unique
  *   vals   = inline value bytes (<= 8, zero padded) or, for strings longer
@@ -99,9 +101,13 @@ static inline uint32_t gpudiff_meta_len(uint32_t m) { return m >> 3; }
 static inline int gpudiff_meta_is_long(uint32_t m) {
     return gpudiff_meta_tag(m) == GPUDIFF_TAG_STR && gpudiff_meta_len(m) > GPUDIFF_INLINE_MAX;
 }
+/* arena bytes of one leaf's value (long strings: the length rounded up to 4) */
 static inline uint32_t gpudiff_meta_arena(uint32_t m) {
-    return gpudiff_meta_is_long(m) ? ((gpudiff_meta_len(m) + 15u) & ~15u) : 0u;
+    return gpudiff_meta_is_long(m) ? ((gpudiff_meta_len(m) + 3u) & ~3u) : 0u;
 }
+/* a segment's arena size (the row's *_ar fields): the sum of its leaves'
+ * gpudiff_meta_arena, rounded up to 16 */
+static inline uint32_t gpudiff_arena_bytes(uint32_t sum) { return (sum + 15u) & ~15u; }
 
 #ifdef __cplusplus
 }

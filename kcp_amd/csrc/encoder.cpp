@@ -239,7 +239,8 @@ void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, ui
         const size_t n = v.size();
         uint32_t arena = 0;
         for (const LeafRec& r : v)
-            if (gpudiff_meta_is_long(r.meta)) arena += (r.vlen + 15u) & ~15u;
+            arena += gpudiff_meta_arena(r.meta);
+        arena = gpudiff_arena_bytes(arena);
         const size_t head = ((n * 20) + 15) & ~(size_t)15;
         const size_t base = pool.size();
         pool.resize(base + head + arena, 0);
@@ -254,7 +255,7 @@ void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, ui
             uint64_t val = r.val;
             if (gpudiff_meta_is_long(r.meta)) {
                 memcpy(ar + aoff, r.vptr, r.vlen);
-                aoff += (r.vlen + 15u) & ~15u;
+                aoff += gpudiff_meta_arena(r.meta);
                 val = cfg_.host_value_hash ? xxh64_host(r.vptr, r.vlen, 0) : 0;
             }
             memcpy(&keys[i], &r.h, 8);

@@ -79,7 +79,8 @@ __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
     return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
 }
 __device__ __forceinline__ bool meta_long(uint32_t m) { return (m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > 8u; }
-__device__ __forceinline__ uint32_t meta_arena(uint32_t m) { return meta_long(m) ? (((m >> 3) + 15u) & ~15u) : 0u; }
+// arena bytes of a leaf's value: long strings at 4-byte aligned offsets (include/gpudiff_format.h)
+__device__ __forceinline__ uint32_t meta_arena(uint32_t m) { return meta_long(m) ? (((m >> 3) + 3u) & ~3u) : 0u; }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -89,18 +90,22 @@ __device__ __forceinline__ bool neq16(const u32x4& a, const u32x4& b) {
 }
 
 // ---------------------------------------------------------------- K1
-// XXH64 over a value stored 16-byte aligned (zero padded) in the arena.
-__device__ uint64_t xxh64_a16(const uint4* p, uint32_t len, uint64_t seed) {
+// XXH64 over a value stored 4-byte aligned in the arena: dword loads, none
+// past the value's 4-byte padded end (the next value, or the segment's end,
+// follows it directly).
+__device__ __forceinline__ uint64_t ld64_a4(const uint32_t* p, uint32_t i) {
+    return ((uint64_t)p[2 * i + 1] << 32) | p[2 * i];
+}
+__device__ uint64_t xxh64_a4(const uint32_t* p, uint32_t len, uint64_t seed) {
     uint64_t h;
     uint32_t stripes = len >> 5;
     if (stripes) {
         uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
         for (uint32_t s = 0; s < stripes; s++) {
-            uint4 a = p[2 * s], b = p[2 * s + 1];
-            v1 = xround(v1, ((uint64_t)a.y << 32) | a.x);
-            v2 = xround(v2, ((uint64_t)a.w << 32) | a.z);
-            v3 = xround(v3, ((uint64_t)b.y << 32) | b.x);
-            v4 = xround(v4, ((uint64_t)b.w << 32) | b.z);
+            v1 = xround(v1, ld64_a4(p, 4 * s));
+            v2 = xround(v2, ld64_a4(p, 4 * s + 1));
+            v3 = xround(v3, ld64_a4(p, 4 * s + 2));
+            v4 = xround(v4, ld64_a4(p, 4 * s + 3));
         }
         h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
         h = xmerge(h, v1);
@@ -111,18 +116,15 @@ __device__ uint64_t xxh64_a16(const uint4* p, uint32_t len, uint64_t seed) {
         h = seed + XP5;
     }
     h += len;
-    uint32_t rem = len & 31u;
-    uint64_t w[4] = {0, 0, 0, 0};
-    if (rem) {
-        uint4 a = p[2 * stripes];
-        w[0] = ((uint64_t)a.y << 32) | a.x;
-        w[1] = ((uint64_t)a.w << 32) | a.z;
-        if (rem > 16) {
-            uint4 b = p[2 * stripes + 1];
-            w[2] = ((uint64_t)b.y << 32) | b.x;
-            w[3] = ((uint64_t)b.w << 32) | b.z;
-        }
-    }
+    const uint32_t rem = len & 31u;
+    uint32_t w32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t* t = p + 8 * stripes;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++)
+        if (4 * k < rem) w32[k] = t[k];
+    uint64_t w[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) w[k] = ((uint64_t)w32[2 * k + 1] << 32) | w32[2 * k];
     h = xxh64_tail(h, w, rem);
     return xavalanche(h);
 }
@@ -148,14 +150,14 @@ __global__ __launch_bounds__(256) void k_value_hash(const gpudiff_pair_row* __re
         uint8_t* seg = pool + off + (st ? seg_bytes(sl, sar) : 0);
         uint64_t* vals = (uint64_t*)(seg + 8ull * L);
         const uint32_t* metas = (const uint32_t*)(seg + 16ull * L);
-        const uint4* arena = (const uint4*)(seg + ((20ull * L + 15ull) & ~15ull));
+        const uint32_t* arena = (const uint32_t*)(seg + ((20ull * L + 15ull) & ~15ull));
         uint32_t run = 0;  // running arena byte offset
         for (uint32_t w = 0; w < L; w += 64) {
             const uint32_t i = w + lane;
             const uint32_t m = i < L ? metas[i] : 0u;
             const uint32_t asz = meta_arena(m);
             const uint32_t incl = wave_incl_scan(asz);
-            if (asz) vals[i] = xxh64_a16(arena + ((run + incl - asz) >> 4), m >> 3, 0);
+            if (asz) vals[i] = xxh64_a4(arena + ((run + incl - asz) >> 2), m >> 3, 0);
             run += shfl32(incl, 63);
         }
     }
@@ -421,27 +423,30 @@ __device__ __forceinline__ uint32_t tile_lower_bound(uint64_t x, uint64_t tile, 
 }
 
 // Byte-exact confirmation of every lane's pending (hash-equal, same length)
-// long value at once.  The lanes' 16-byte chunks are flattened into one index
-// space (prefix sum of chunk counts); each pass the wave compares 128 chunks
-// with 16-B loads (consecutive chunks of a value are consecutive addresses),
-// finding a chunk's owner lane by a cross-lane binary search over the prefix
-// sums.  Returns true in the lanes whose value differs (a hash collision).
+// long value at once.  The lanes' values are flattened into one index space of
+// dwords (prefix sum of dword counts: values sit at 4-byte aligned arena
+// offsets, zero padded to 4, so two equal-length values are equal iff their
+// padded dwords are); each pass the wave compares 64 x CV_U dwords (consecutive
+// dwords of a value are consecutive addresses), finding a dword's owner lane by
+// a cross-lane binary search over the prefix sums.  No load reaches past a
+// value's padded end.  Returns true in the lanes whose value differs (a hash
+// collision).
 __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a, const uint8_t* arena_b,
                                uint32_t off_b, uint32_t len, uint32_t lane) {
-    const uint32_t n16 = need ? (len + 15u) >> 4 : 0u;
-    const uint32_t incl = wave_incl_scan(n16);
+    const uint32_t n4 = need ? (len + 3u) >> 2 : 0u;
+    const uint32_t incl = wave_incl_scan(n4);
     const uint32_t total = shfl32(incl, 63);
     uint64_t bad = 0;  // lanes whose value differs (wave-uniform)
-    constexpr int CV_U = 2;  // chunk pairs in flight per lane: 4 costs the decision kernel a wave per SIMD
+    constexpr int CV_U = 4;  // dword pairs in flight per lane
     for (uint32_t base = 0; base < total; base += 64 * CV_U) {
-        u32x4 xa[CV_U], xb[CV_U];
+        uint32_t xa[CV_U], xb[CV_U];
         uint32_t own[CV_U];
         bool act[CV_U];
 #pragma unroll
         for (int u = 0; u < CV_U; u++) {
             const uint32_t g = base + u * 64 + lane;
             act[u] = g < total;
-            // owner = number of lanes whose inclusive chunk prefix is <= g
+            // owner = number of lanes whose inclusive dword prefix is <= g
             uint32_t o = 0;
 #pragma unroll
             for (uint32_t s = 64; s >= 1; s >>= 1) {
@@ -451,16 +456,16 @@ __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a
             }
             own[u] = min(o, 63u);
             const uint32_t oa = shfl32(off_a, own[u]), ob = shfl32(off_b, own[u]);
-            const uint32_t first = shfl32(incl - n16, own[u]);
+            const uint32_t first = shfl32(incl - n4, own[u]);
             if (act[u]) {
                 const uint32_t k = g - first;
-                xa[u] = *(const u32x4*)(arena_a + oa + 16u * k);
-                xb[u] = *(const u32x4*)(arena_b + ob + 16u * k);
+                xa[u] = *(const uint32_t*)(arena_a + oa + 4u * k);
+                xb[u] = *(const uint32_t*)(arena_b + ob + 4u * k);
             }
         }
 #pragma unroll
         for (int u = 0; u < CV_U; u++) {
-            uint64_t m = ballot(act[u] && neq16(xa[u], xb[u]));
+            uint64_t m = ballot(act[u] && xa[u] != xb[u]);
             while (m) {  // collisions only: practically never taken
                 const uint32_t j = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1;

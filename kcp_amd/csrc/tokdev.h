@@ -152,7 +152,8 @@ __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
     return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
 }
 __device__ __forceinline__ uint32_t meta_arena(uint32_t m) {
-    return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) + 15u) & ~15u) : 0u;
+    // long strings at 4-byte aligned arena offsets (include/gpudiff_format.h)
+    return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) + 3u) & ~3u) : 0u;
 }
 
 __device__ __forceinline__ bool is_ws(uint32_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }

@@ -631,6 +631,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             ARt += wave_sum(rg == 2 ? ar : 0u);
             KB += wave_sum(kl);
         }
+        ARs = (ARs + 15u) & ~15u;  // gpudiff_arena_bytes: each arena a multiple of 16
+        ARt = (ARt + 15u) & ~15u;
         const uint64_t seg_s = seg_bytes(Ls, ARs), seg_t = seg_bytes(Lt, ARt);
         const uint64_t tab = (24ull * Nt + KB + 15u) & ~15ull;  // gpudiff_tab_bytes: blobs stay 16-B multiples
         const uint64_t bytes = seg_s + seg_t + tab;
@@ -704,7 +706,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 }
                 trank += popc64(tbal);
                 tko += rdlane(kinc, 63);
-                // long strings: wave-cooperative 16-B copies into the arena
+                // long strings: wave-cooperative dword copies into the arena (values at
+                // 4-byte aligned offsets; the last dword's bytes past the value are zero)
                 for (uint64_t bl = ballot(ar != 0); bl; bl &= bl - 1) {
                     const uint32_t src_lane = (uint32_t)__builtin_ctzll(bl);
                     const uint32_t si = rdlane(i, src_lane);
@@ -715,23 +718,20 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t op = S.tok[rr.z] & POS_MASK;
                     const uint8_t* src = (rr.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1);
                     const uint32_t slen = sm >> 3;
-                    uint8_t* dst = segp[sg] + ((20ull * Lr[sg] + 15ull) & ~15ull) + sa;
-                    for (uint32_t c16 = lane; c16 * 16u < slen; c16 += 64) {
-                        const uint32_t b0 = c16 * 16u;
-                        uint64_t w0 = ld8u(src + b0), w1 = ld8u(src + b0 + 8);
-                        const uint32_t rem = slen - b0;
-                        if (rem < 16) {
-                            if (rem <= 8) {
-                                w0 &= rem == 8 ? ~0ull : ((1ull << (8 * rem)) - 1ull);
-                                w1 = 0;
-                            } else {
-                                w1 &= (1ull << (8 * (rem - 8))) - 1ull;
-                            }
-                        }
-                        ((uint64_t*)(dst + b0))[0] = w0;
-                        ((uint64_t*)(dst + b0))[1] = w1;
+                    uint32_t* dst = (uint32_t*)(segp[sg] + ((20ull * Lr[sg] + 15ull) & ~15ull) + sa);
+                    for (uint32_t c4 = lane; c4 * 4u < slen; c4 += 64) {
+                        uint32_t w = (uint32_t)ld8u(src + 4u * c4);
+                        const uint32_t rem = slen - 4u * c4;
+                        if (rem < 4) w &= (1u << (8 * rem)) - 1u;
+                        dst[c4] = w;
                     }
                 }
+            }
+            // zero each arena's tail pad (its values end 4-byte aligned; the arena is a multiple of 16)
+            for (uint32_t g = 0; g < 2; g++) {
+                const uint32_t ARg = g ? ARt : ARs;
+                uint32_t* tail = (uint32_t*)(segp[g] + ((20ull * Lr[g] + 15ull) & ~15ull) + aoff[g]);
+                if (lane < (ARg - aoff[g]) / 4u) tail[lane] = 0u;
             }
             o.off = off;
             o.bytes = (uint32_t)bytes;

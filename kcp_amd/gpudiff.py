@@ -1068,7 +1068,8 @@ def decode_path_table(blob: bytes, info: dict):
 
 
 def decode_segment(pool: bytes, off: int, L: int, arena: int):
-    """Canonical segment -> list of (key, val, meta, value_bytes)."""
+    """Canonical segment -> list of (key, val, meta, value_bytes).  Long
+    strings sit in the arena at 4-byte aligned offsets (include/gpudiff_format.h)."""
     keys = np.frombuffer(pool, dtype="<u8", count=L, offset=off) if L else np.zeros(0, "<u8")
     vals = np.frombuffer(pool, dtype="<u8", count=L, offset=off + 8 * L) if L else np.zeros(0, "<u8")
     metas = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 16 * L) if L else np.zeros(0, "<u4")
@@ -1079,7 +1080,7 @@ def decode_segment(pool: bytes, off: int, L: int, arena: int):
         tag, ln = m & 7, m >> 3
         if tag == 5 and ln > 8:
             vb = pool[ar:ar + ln]
-            ar += (ln + 15) & ~15
+            ar += (ln + 3) & ~3
         elif tag == 5:
             vb = int(v).to_bytes(8, "little")[:ln]
         elif tag in (3, 4):
@@ -1087,7 +1088,7 @@ def decode_segment(pool: bytes, off: int, L: int, arena: int):
         else:
             vb = b""
         out.append((k, v, m, vb))
-    assert ar == off + head + arena, (ar, off, head, arena)
+    assert ((ar - off - head + 15) & ~15) == arena, (ar, off, head, arena)
     return out
 
 
