@@ -367,7 +367,7 @@ def main():
                          "format": {"bytes_per_launch": fmt_bytes / launches, "achieved": achieved_fmt,
                                     "frac": achieved_fmt / HBM_PEAK_GBPS,
                                     "def": "bytes K2 reads in this build's CSR format: 64-B row + flag + both "
-                                           "size-matched segments (20 B/leaf + the arena: long strings 4-B aligned, padded to 16)"},
+                                           "size-matched segments (16 B per leaf record: value u64 + 32-bit path hash + meta; + the arena: long strings 4-B aligned, padded to 16)"},
                          "diff_pass": {"ms": pass_ms, "achieved": achieved_pass, "frac": achieved_pass / HBM_PEAK_GBPS,
                                        "def": "SURVEY bytes over the whole diff pass (K2..K6)"},
                          "k2_source_hash": src_hash},

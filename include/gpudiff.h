@@ -119,7 +119,7 @@ typedef struct gpudiff_opts {
     uint32_t encode_threads; /* 0 = all host cores */
     void* stream;            /* hipStream_t to launch on; NULL = context-owned stream */
     uint32_t flags;          /* GPUDIFF_OPT_* */
-    uint32_t path_hash_bits; /* 0 or 64 normally; 8..63 only to force collisions in tests */
+    uint32_t path_hash_bits; /* 0 (or >= 32): GPUDIFF_PATH_HASH_BITS = 32; 8..31 only to force collisions in tests */
 } gpudiff_opts;
 
 typedef struct gpudiff_json_pair {

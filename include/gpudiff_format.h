@@ -6,12 +6,13 @@
  *
  *   [ spec segment ][ status segment ]
  *
- *   segment(L, arena) = keys[L] u64 | vals[L] u64 | metas[L] u32 | pad to 16
+ *   segment(L, arena) = vals[L] u64 | keys[L] u32 | metas[L] u32
  *                       | arena: the long string values in key order, each at a
  *                         4-byte aligned offset (zero padded to 4), the whole
  *                         zero padded to a multiple of 16
  *
- *   keys   = pathHash = XXH64(path bytes, pair seed), ascending, unique
+ *   keys   = pathHash: the chained XXH64 path hash under the pair seed, cut
+ *            to GPUDIFF_PATH_HASH_BITS (32) bits, ascending, unique
  *   vals   = inline value bytes (<= 8, zero padded) or, for strings longer
  *            than 8 bytes, XXH64(value bytes, 0) filled by kernel K1
  *   metas  = (len << 3) | tag
@@ -39,6 +40,11 @@
 #define GPUDIFF_TAG_EARR 7u
 
 #define GPUDIFF_INLINE_MAX 8u
+/* width of the path hashes kept in segments and reported in changed-path
+ * lists: 32 bits (16 B per leaf record).  Exactness never rests on the width:
+ * the hash is verified injective over each pair's path union (re-seeded on a
+ * collision) and the object store's path tables agree at any width. */
+#define GPUDIFF_PATH_HASH_BITS 32u
 
 /* object flags (PairRow.flags_a / flags_b) */
 #define GPUDIFF_OBJ_HAS_STATUS 0x1u   /* top-level "status" key present (even null) */
@@ -91,9 +97,8 @@ typedef struct gpudiff_pair_row {
     uint32_t pair_id, cluster_id;
 } gpudiff_pair_row;
 
-static inline uint64_t gpudiff_seg_bytes(uint32_t l, uint32_t arena) {
-    return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
-}
+/* segment bytes: 16 B per leaf record (a multiple of 16) + the arena */
+static inline uint64_t gpudiff_seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + (uint64_t)arena; }
 
 static inline uint32_t gpudiff_meta(uint32_t tag, uint32_t len) { return (len << 3) | tag; }
 static inline uint32_t gpudiff_meta_tag(uint32_t m) { return m & 7u; }

@@ -142,7 +142,8 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
     uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
     c->threads = o.encode_threads ? o.encode_threads : std::min(hw, 16u);
     c->flags = o.flags;
-    c->ecfg.hash_bits = (o.path_hash_bits == 0 || o.path_hash_bits >= 64) ? 64 : o.path_hash_bits;
+    c->ecfg.hash_bits = (o.path_hash_bits == 0 || o.path_hash_bits >= GPUDIFF_PATH_HASH_BITS) ? GPUDIFF_PATH_HASH_BITS
+                                                                                            : o.path_hash_bits;
     if (c->ecfg.hash_bits < 8) return GPUDIFF_E_INVAL;
     c->ecfg.host_value_hash = (o.flags & GPUDIFF_OPT_HOST_VALUE_HASH) != 0;
     c->hash_mask = c->ecfg.hash_bits >= 64 ? ~0ULL : ((1ULL << c->ecfg.hash_bits) - 1);
@@ -838,7 +839,7 @@ int gpudiff_resolve_path(const uint8_t* a, size_t al, const uint8_t* b, size_t b
                          uint32_t bits, char* buf, size_t cap, size_t* out_len) {
     if (!a || !b) return GPUDIFF_E_INVAL;
     EncodeConfig cfg;
-    cfg.hash_bits = (bits == 0 || bits >= 64) ? 64 : bits;
+    cfg.hash_bits = (bits == 0 || bits >= GPUDIFF_PATH_HASH_BITS) ? GPUDIFF_PATH_HASH_BITS : bits;
     PairEncoder enc(cfg);
     std::vector<uint8_t> pool;
     gpudiff_pair_row row;

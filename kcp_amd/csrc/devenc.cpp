@@ -28,7 +28,7 @@ int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, ui
     if (!doc || !info || seed > 255) return GPUDIFF_E_INVAL;
     memset(info, 0, sizeof(*info));
     EncodeConfig cfg;
-    cfg.hash_bits = (bits == 0 || bits >= 64) ? 64 : bits;
+    cfg.hash_bits = (bits == 0 || bits >= GPUDIFF_PATH_HASH_BITS) ? GPUDIFF_PATH_HASH_BITS : bits;
     cfg.host_value_hash = true;  // K0 fills the long-value digests itself
     PairEncoder enc(cfg);
     Arena arena;

@@ -241,13 +241,13 @@ void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, ui
         for (const LeafRec& r : v)
             arena += gpudiff_meta_arena(r.meta);
         arena = gpudiff_arena_bytes(arena);
-        const size_t head = ((n * 20) + 15) & ~(size_t)15;
+        const size_t head = n * 16;  // vals u64 | keys u32 | metas u32
         const size_t base = pool.size();
         pool.resize(base + head + arena, 0);
         uint8_t* p = pool.data() + base;
-        uint64_t* keys = (uint64_t*)p;
-        uint8_t* vals = p + 8 * n;
-        uint8_t* metas = p + 16 * n;
+        uint8_t* vals = p;
+        uint8_t* keys = p + 8 * n;
+        uint8_t* metas = p + 12 * n;
         uint8_t* ar = p + head;
         uint32_t aoff = 0;
         for (size_t i = 0; i < n; i++) {
@@ -258,7 +258,8 @@ void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, ui
                 aoff += gpudiff_meta_arena(r.meta);
                 val = cfg_.host_value_hash ? xxh64_host(r.vptr, r.vlen, 0) : 0;
             }
-            memcpy(&keys[i], &r.h, 8);
+            const uint32_t k32 = (uint32_t)r.h;  // hashes are masked to <= 32 bits
+            memcpy(keys + 4 * i, &k32, 4);
             memcpy(vals + 8 * i, &val, 8);
             memcpy(metas + 4 * i, &r.meta, 4);
         }

@@ -86,7 +86,7 @@ struct FlatObject {
 };
 
 struct EncodeConfig {
-    uint32_t hash_bits = 64;
+    uint32_t hash_bits = GPUDIFF_PATH_HASH_BITS;  // <= 32: segments keep 32-bit keys
     bool host_value_hash = false;
 };
 

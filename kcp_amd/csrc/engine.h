@@ -178,10 +178,10 @@ int collect_results(gpudiff_ctx* c, gpudiff_dbatch* d, ResultStore& rs);
 // canonical bytes of one object's long string values (V of SURVEY §8(d)); blob at pool + off
 inline uint64_t blob_value_bytes(const uint8_t* blob, uint32_t spec_l, uint32_t spec_ar, uint32_t stat_l) {
     uint64_t v = 0;
-    const uint32_t* m = (const uint32_t*)(blob + 16ull * spec_l);
+    const uint32_t* m = (const uint32_t*)(blob + 12ull * spec_l);
     for (uint32_t i = 0; i < spec_l; i++)
         if (gpudiff_meta_is_long(m[i])) v += gpudiff_meta_len(m[i]);
-    m = (const uint32_t*)(blob + gpudiff_seg_bytes(spec_l, spec_ar) + 16ull * stat_l);
+    m = (const uint32_t*)(blob + gpudiff_seg_bytes(spec_l, spec_ar) + 12ull * stat_l);
     for (uint32_t i = 0; i < stat_l; i++)
         if (gpudiff_meta_is_long(m[i])) v += gpudiff_meta_len(m[i]);
     return v;

@@ -75,9 +75,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
-    return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
-}
+__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + arena; }
 __device__ __forceinline__ bool meta_long(uint32_t m) { return (m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > 8u; }
 // arena bytes of a leaf's value: long strings at 4-byte aligned offsets (include/gpudiff_format.h)
 __device__ __forceinline__ uint32_t meta_arena(uint32_t m) { return meta_long(m) ? (((m >> 3) + 3u) & ~3u) : 0u; }
@@ -148,9 +146,9 @@ __global__ __launch_bounds__(256) void k_value_hash(const gpudiff_pair_row* __re
         const uint32_t AR = st ? (b ? r.stat_ar_b : r.stat_ar_a) : sar;
         if (AR == 0 || L == 0) continue;
         uint8_t* seg = pool + off + (st ? seg_bytes(sl, sar) : 0);
-        uint64_t* vals = (uint64_t*)(seg + 8ull * L);
-        const uint32_t* metas = (const uint32_t*)(seg + 16ull * L);
-        const uint32_t* arena = (const uint32_t*)(seg + ((20ull * L + 15ull) & ~15ull));
+        uint64_t* vals = (uint64_t*)seg;
+        const uint32_t* metas = (const uint32_t*)(seg + 12ull * L);
+        const uint32_t* arena = (const uint32_t*)(seg + 16ull * L);
         uint32_t run = 0;  // running arena byte offset
         for (uint32_t w = 0; w < L; w += 64) {
             const uint32_t i = w + lane;
@@ -391,7 +389,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
 
 // ---------------------------------------------------------------- K4
 struct RegionView {
-    const uint64_t* keys;
+    const uint32_t* keys;
     const uint64_t* vals;
     const uint32_t* metas;
     const uint8_t* arena;
@@ -402,21 +400,21 @@ __device__ __forceinline__ RegionView region_view(const uint8_t* pool, uint64_t 
                                                   bool status, uint32_t L) {
     const uint8_t* seg = pool + off + (status ? seg_bytes(sl, sar) : 0);
     RegionView v;
-    v.keys = (const uint64_t*)seg;
-    v.vals = (const uint64_t*)(seg + 8ull * L);
-    v.metas = (const uint32_t*)(seg + 16ull * L);
-    v.arena = seg + ((20ull * L + 15ull) & ~15ull);
+    v.vals = (const uint64_t*)seg;  // vals u64 | keys u32 | metas u32 | arena (include/gpudiff_format.h)
+    v.keys = (const uint32_t*)(seg + 8ull * L);
+    v.metas = (const uint32_t*)(seg + 12ull * L);
+    v.arena = seg + 16ull * L;
     v.L = L;
     return v;
 }
 
 // number of tile keys (lanes < nt, ascending) strictly less than x
-__device__ __forceinline__ uint32_t tile_lower_bound(uint64_t x, uint64_t tile, uint32_t nt) {
+__device__ __forceinline__ uint32_t tile_lower_bound(uint32_t x, uint32_t tile, uint32_t nt) {
     uint32_t j = 0;
 #pragma unroll
     for (uint32_t s = 64; s >= 1; s >>= 1) {
         const uint32_t cand = j + s;
-        const uint64_t t = shfl64(tile, min(cand, 64u) - 1u);
+        const uint32_t t = shfl32(tile, min(cand, 64u) - 1u);
         if (cand <= nt && t < x) j = cand;
     }
     return j;
@@ -503,18 +501,18 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
     while (ia < A.L || ib < B.L) {
         const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
         const bool va = lane < na, vb = lane < nb;
-        const uint64_t ka = va ? A.keys[ia + lane] : 0ull;
-        const uint64_t kb = vb ? B.keys[ib + lane] : 0ull;
+        const uint32_t ka = va ? A.keys[ia + lane] : 0u;
+        const uint32_t kb = vb ? B.keys[ib + lane] : 0u;
         const uint32_t ma = va ? A.metas[ia + lane] : 0u;
         const uint32_t mb = vb ? B.metas[ib + lane] : 0u;
         const uint64_t xa = va ? A.vals[ia + lane] : 0ull;
         const uint64_t xb = vb ? B.vals[ib + lane] : 0ull;
         const bool endA = ia + na == A.L, endB = ib + nb == B.L;
-        const uint64_t lastA = na ? shfl64(ka, na - 1) : 0ull;
-        const uint64_t lastB = nb ? shfl64(kb, nb - 1) : 0ull;
+        const uint32_t lastA = na ? shfl32(ka, na - 1) : 0u;
+        const uint32_t lastB = nb ? shfl32(kb, nb - 1) : 0u;
         // everything <= bound is resolvable in this window
         bool inf = true;
-        uint64_t bound = 0;
+        uint32_t bound = 0;
         if (!endA) { bound = lastA; inf = false; }
         if (!endB) { bound = inf ? lastB : min(bound, lastB); inf = false; }
         const bool inA = va && (inf || ka <= bound);
@@ -525,7 +523,7 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         const uint32_t offA = arA + incA - asA, offB = arB + incB - asB;
         // resolve A keys against the B window
         const uint32_t jA = tile_lower_bound(ka, kb, nb);
-        const uint64_t kbj = shfl64(kb, min(jA, 63u));
+        const uint32_t kbj = shfl32(kb, min(jA, 63u));
         const uint32_t mbj = shfl32(mb, min(jA, 63u));
         const uint64_t xbj = shfl64(xb, min(jA, 63u));
         const uint32_t obj = shfl32(offB, min(jA, 63u));
@@ -534,7 +532,7 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, ma >> 3, lane);
         // resolve B keys against the A window
         const uint32_t iB = tile_lower_bound(kb, ka, na);
-        const uint64_t kai = shfl64(ka, min(iB, 63u));
+        const uint32_t kai = shfl32(ka, min(iB, 63u));
         const bool matchB = inB && iB < na && kai == kb;
         const bool emitA = inA && (!matchA || differ);
         const bool emitB = inB && !matchB;

@@ -148,9 +148,7 @@ __device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, uint32_t len) {
     return xxh64_words(0, len, [&](uint32_t i) -> uint64_t { return ld8u(p + 8u * i); });
 }
 
-__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) {
-    return ((((uint64_t)l * 20u) + 15u) & ~(uint64_t)15u) + (uint64_t)arena;
-}
+__device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + arena; }
 __device__ __forceinline__ uint32_t meta_arena(uint32_t m) {
     // long strings at 4-byte aligned arena offsets (include/gpudiff_format.h)
     return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) + 3u) & ~3u) : 0u;

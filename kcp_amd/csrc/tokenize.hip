@@ -649,12 +649,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             uint64_t* phs = hs + Nt;
             uint64_t* cs = phs + Nt;
             uint8_t* keys = (uint8_t*)(cs + Nt);
-            // zero the pad between metas and arena, and the key area's pad
-            for (uint32_t g = 0; g < 2; g++) {
-                const uint32_t L = Lr[g];
-                const uint32_t pad_beg = 20u * L, pad_end = (20u * L + 15u) & ~15u;
-                if (lane < (pad_end - pad_beg) / 4u) ((uint32_t*)(segp[g] + pad_beg))[lane] = 0u;
-            }
+            // zero the key area's pad (a segment's leaf records are 16 B each: no pad before the arena)
             if (lane < tab - 24ull * Nt - KB) keys[KB + lane] = 0;
             const uint64_t root = seed & mask;
             uint32_t rank[2] = {0, 0}, aoff[2] = {0, 0}, trank = 0, tko = 0;
@@ -689,9 +684,10 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t g = rg - 1;
                     const uint32_t L = Lr[g];
                     uint8_t* sp8 = segp[g];
-                    ((uint64_t*)sp8)[my_rank] = skey[j];
-                    ((uint64_t*)(sp8 + 8ull * L))[my_rank] = S.val[i];
-                    ((uint32_t*)(sp8 + 16ull * L))[my_rank] = m;
+                    // vals u64 | keys u32 | metas u32 (include/gpudiff_format.h); keys masked to <= 32 bits
+                    ((uint64_t*)sp8)[my_rank] = S.val[i];
+                    ((uint32_t*)(sp8 + 8ull * L))[my_rank] = (uint32_t)skey[j];
+                    ((uint32_t*)(sp8 + 12ull * L))[my_rank] = m;
                 }
                 // the path-table entry: hash, parent hash, component (+ key bytes)
                 const uint64_t tbal = ballot(t);
@@ -718,7 +714,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t op = S.tok[rr.z] & POS_MASK;
                     const uint8_t* src = (rr.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1);
                     const uint32_t slen = sm >> 3;
-                    uint32_t* dst = (uint32_t*)(segp[sg] + ((20ull * Lr[sg] + 15ull) & ~15ull) + sa);
+                    uint32_t* dst = (uint32_t*)(segp[sg] + 16ull * Lr[sg] + sa);
                     for (uint32_t c4 = lane; c4 * 4u < slen; c4 += 64) {
                         uint32_t w = (uint32_t)ld8u(src + 4u * c4);
                         const uint32_t rem = slen - 4u * c4;
@@ -730,7 +726,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             // zero each arena's tail pad (its values end 4-byte aligned; the arena is a multiple of 16)
             for (uint32_t g = 0; g < 2; g++) {
                 const uint32_t ARg = g ? ARt : ARs;
-                uint32_t* tail = (uint32_t*)(segp[g] + ((20ull * Lr[g] + 15ull) & ~15ull) + aoff[g]);
+                uint32_t* tail = (uint32_t*)(segp[g] + 16ull * Lr[g] + aoff[g]);
                 if (lane < (ARg - aoff[g]) / 4u) tail[lane] = 0u;
             }
             o.off = off;

@@ -27,6 +27,7 @@ OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
 OPT_DEVICE_ENCODE = 0x2000000
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
+PATH_HASH_BITS = 32  # GPUDIFF_PATH_HASH_BITS: segment keys and reported path hashes
 OBJ_HAS_STATUS, OBJ_DECODE_ERR, OBJ_FRESH, OBJ_SEED_SHIFT = 0x1, 0x2, 0x4, 8
 STORE_DEVICE_ENCODE = 0x1
 EXPORT_COUNTS, EXPORT_SPEC_IDS, EXPORT_STATUS_IDS, EXPORT_DIRTY_IDS, EXPORT_FLAGS = range(5)
@@ -505,7 +506,7 @@ class Engine:
     """One gpudiff context (one GPU, one stream, one submitting thread)."""
 
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
-                 timing: bool = False, path_hash_bits: int = 64, host_value_hash: bool = False,
+                 timing: bool = False, path_hash_bits: int = PATH_HASH_BITS, host_value_hash: bool = False,
                  no_value_hash: bool = False, flags: int = 0, device_encode: bool = False):
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
                  flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0) |
@@ -515,7 +516,7 @@ class Engine:
         h = C.c_void_p()
         _chk(_lib.gpudiff_open(C.byref(o), C.byref(h)), "gpudiff_open")
         self.ctx = h
-        self.path_hash_bits = path_hash_bits
+        self.path_hash_bits = min(path_hash_bits or PATH_HASH_BITS, PATH_HASH_BITS)  # the library clamps the same way
 
     def close(self):
         if self.ctx:
@@ -1008,7 +1009,7 @@ def upsert_body_host(doc, mode: int = UPSERT_SPEC) -> Optional[bytes]:
     return out.raw[:n.value]
 
 
-def resolve_path(old, new, path_hash: int, path_kind: int, path_hash_bits: int = 64) -> str:
+def resolve_path(old, new, path_hash: int, path_kind: int, path_hash_bits: int = PATH_HASH_BITS) -> str:
     a, b = to_json_bytes(old), to_json_bytes(new)
     buf = C.create_string_buffer(4096)
     n = C.c_size_t()
@@ -1021,7 +1022,7 @@ def resolve_path(old, new, path_hash: int, path_kind: int, path_hash_bits: int =
     return buf.value.decode("utf-8", "replace")
 
 
-def encode_object_host(doc, seed: int = 0, path_hash_bits: int = 64):
+def encode_object_host(doc, seed: int = 0, path_hash_bits: int = PATH_HASH_BITS):
     """Host encoder (the Go-exact path) in the device-store format: (ObjInfo dict, blob bytes or None)."""
     b = to_json_bytes(doc)
     info = ObjInfo()
@@ -1048,7 +1049,7 @@ def decode_path_table(blob: bytes, info: dict):
     n = info["n_tab"]
     if n == TAB_NONE:
         return None
-    seg = lambda L, ar: (((20 * L) + 15) & ~15) + ar
+    seg = segment_bytes
     base = seg(info["spec_l"], info["spec_ar"]) + seg(info["stat_l"], info["stat_ar"])
     if not n:
         return []
@@ -1070,10 +1071,10 @@ def decode_path_table(blob: bytes, info: dict):
 def decode_segment(pool: bytes, off: int, L: int, arena: int):
     """Canonical segment -> list of (key, val, meta, value_bytes).  Long
     strings sit in the arena at 4-byte aligned offsets (include/gpudiff_format.h)."""
-    keys = np.frombuffer(pool, dtype="<u8", count=L, offset=off) if L else np.zeros(0, "<u8")
-    vals = np.frombuffer(pool, dtype="<u8", count=L, offset=off + 8 * L) if L else np.zeros(0, "<u8")
-    metas = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 16 * L) if L else np.zeros(0, "<u4")
-    head = ((20 * L) + 15) & ~15
+    vals = np.frombuffer(pool, dtype="<u8", count=L, offset=off) if L else np.zeros(0, "<u8")
+    keys = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 8 * L) if L else np.zeros(0, "<u4")
+    metas = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 12 * L) if L else np.zeros(0, "<u4")
+    head = 16 * L
     ar = off + head
     out = []
     for k, v, m in zip(keys.tolist(), vals.tolist(), metas.tolist()):
@@ -1093,4 +1094,5 @@ def decode_segment(pool: bytes, off: int, L: int, arena: int):
 
 
 def segment_bytes(L: int, arena: int) -> int:
-    return (((20 * L) + 15) & ~15) + arena
+    """vals u64 | keys u32 | metas u32 per leaf, then the arena (include/gpudiff_format.h)."""
+    return 16 * L + arena

@@ -31,10 +31,10 @@ namespace {
 struct Seg {
     const uint8_t* p;
     uint32_t l, ar;
-    const uint64_t* keys() const { return (const uint64_t*)p; }
-    const uint64_t* vals() const { return (const uint64_t*)(p + 8ull * l); }
-    const uint32_t* metas() const { return (const uint32_t*)(p + 16ull * l); }
-    const uint8_t* arena() const { return p + ((20ull * l + 15ull) & ~15ull); }
+    const uint64_t* vals() const { return (const uint64_t*)p; }
+    const uint32_t* keys() const { return (const uint32_t*)(p + 8ull * l); }
+    const uint32_t* metas() const { return (const uint32_t*)(p + 12ull * l); }
+    const uint8_t* arena() const { return p + 16ull * l; }
     uint64_t bytes() const { return gpudiff_seg_bytes(l, ar); }
 };
 
@@ -47,7 +47,8 @@ template <class Emit>
 void join(const Seg& a, const Seg& b, uint8_t region, Emit&& emit) {
     uint32_t i = 0, j = 0;
     uint64_t oa = 0, ob = 0;  // arena offsets of the next long value
-    const uint64_t *ka = a.keys(), *kb = b.keys(), *va = a.vals(), *vb = b.vals();
+    const uint32_t *ka = a.keys(), *kb = b.keys();
+    const uint64_t *va = a.vals(), *vb = b.vals();
     const uint32_t *ma = a.metas(), *mb = b.metas();
     while (i < a.l || j < b.l) {
         if (j >= b.l || (i < a.l && ka[i] < kb[j])) {
@@ -77,7 +78,7 @@ void join(const Seg& a, const Seg& b, uint8_t region, Emit&& emit) {
 
 uint64_t status_sentinel(uint32_t seed) {
     uint8_t comp[11] = {0x01, 6, 0, 0, 0, 's', 't', 'a', 't', 'u', 's'};
-    return oracle::xxh64_ref(comp, sizeof comp, seed);
+    return oracle::xxh64_ref(comp, sizeof comp, seed) & ((1ull << GPUDIFF_PATH_HASH_BITS) - 1);  // the build's width
 }
 
 // one pair: flags (bit0 spec, bit1 status, bit2 decode error); paths via emit

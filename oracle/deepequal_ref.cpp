@@ -34,6 +34,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "../include/gpudiff_format.h"
 #include "timed_threads.h"
 #include "xxh64_ref.h"
 
@@ -387,6 +388,9 @@ static void put_comp(std::string& p, uint8_t kind, const void* data, uint32_t n)
     }
 }
 
+// reported path hashes are cut to the build's width (include/gpudiff_format.h)
+static const uint64_t kPathMask = (1ull << GPUDIFF_PATH_HASH_BITS) - 1;
+
 static void flatten(const Value& v, std::string& path, uint64_t h, LeafMap& out) {
     if (v.k == Value::MAP && !v.m->empty()) {
         for (const auto& kv : *v.m) {
@@ -471,6 +475,7 @@ static void region_diff(const LeafMap& a, const LeafMap& b, uint8_t region_bit,
     }
     for (const auto& kv : b)
         if (!a.count(kv.first)) out.push_back({kv.second.first, (uint8_t)(1 | region_bit)});  // added
+    for (size_t i = base; i < out.size(); i++) out[i].first &= kPathMask;  // the build's width
     std::sort(out.begin() + base, out.end());
 }
 
@@ -530,7 +535,7 @@ long oracle_tree_paths(void* h, const uint8_t* seeds, uint32_t* offsets, uint64_
             region_diff(ta, tb, 0x80, ent);
             if (!p->b[i].m->count("status")) {
                 std::string path;
-                ent.push_back({key_hash(seeds[i], "status", path), (uint8_t)(3 | 0x80)});
+                ent.push_back({key_hash(seeds[i], "status", path) & kPathMask, (uint8_t)(3 | 0x80)});
             }
         }
         if (total + ent.size() > cap) return -1;

@@ -487,6 +487,9 @@ def deep_equal_status(old: Dict[str, Any], new: Dict[str, Any]) -> bool:
 TAG_NULL, TAG_FALSE, TAG_TRUE, TAG_INT, TAG_FLOAT, TAG_STR, TAG_EOBJ, TAG_EARR = range(8)
 KIND_CHANGED, KIND_ADDED, KIND_REMOVED, KIND_STATUS_ABSENT = 0, 1, 2, 3
 REGION_SPEC, REGION_STATUS = 0, 1
+# the build's path-hash width (include/gpudiff_format.h GPUDIFF_PATH_HASH_BITS):
+# segments keep, and results report, the chained hash cut to 32 bits
+PATH_HASH_BITS = 32
 
 Path = Tuple[Tuple[str, Any], ...]
 
@@ -594,7 +597,7 @@ def _region_diff(la, lb, seed: int, region: int, mask: int):
 MAX_SEED = 255
 
 
-def pair_seed(sa, sb, ta, tb, hash_bits: int = 64) -> int:
+def pair_seed(sa, sb, ta, tb, hash_bits: int = PATH_HASH_BITS) -> int:
     """Smallest seed s in [0, 255] for which the path hash is injective over
     the pair's spec-path union and, separately, over its status-path union
     plus the sentinel path ``status`` (the build re-seeds per pair on a
@@ -621,7 +624,7 @@ def pair_seed(sa, sb, ta, tb, hash_bits: int = 64) -> int:
     return -1
 
 
-def diff_pair(a_json: bytes, b_json: bytes, hash_bits: int = 64) -> Dict[str, Any]:
+def diff_pair(a_json: bytes, b_json: bytes, hash_bits: int = PATH_HASH_BITS) -> Dict[str, Any]:
     """Oracle result for one (A=old/upstream, B=new/downstream) pair.
 
     Returns spec_dirty, status_dirty, decode_error, seed and the changed-path
@@ -693,7 +696,7 @@ def theorem_holds(a_json: bytes, b_json: bytes) -> bool:
 
 
 def _theorem_holds(a_json: bytes, b_json: bytes) -> bool:
-    r = _diff_pair(a_json, b_json, 64)
+    r = _diff_pair(a_json, b_json, PATH_HASH_BITS)
     if r["decode_error"]:
         return True
     ps = [e for e in r["paths"] if e[1] == REGION_SPEC]

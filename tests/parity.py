@@ -5,7 +5,7 @@ from kcp_amd import gpudiff as G
 from oracle import gpudiff_oracle as O
 
 
-def oracle_batch(pairs, hash_bits=64):
+def oracle_batch(pairs, hash_bits=O.PATH_HASH_BITS):
     return [O.diff_pair(G.to_json_bytes(a), G.to_json_bytes(b), hash_bits) for a, b in pairs]
 
 
@@ -28,7 +28,7 @@ def expected_paths(r):
     return [(h, k | (G.PATH_REGION_STATUS if region else 0)) for (h, region, k, _p) in r["paths"]]
 
 
-def assert_matches(res: G.DiffResult, pairs, ids=None, hash_bits=64, exp=None):
+def assert_matches(res: G.DiffResult, pairs, ids=None, hash_bits=O.PATH_HASH_BITS, exp=None):
     n = len(pairs)
     ids = list(range(n)) if ids is None else list(ids)
     exp = oracle_batch(pairs, hash_bits) if exp is None else exp

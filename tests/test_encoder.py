@@ -25,7 +25,7 @@ def host_engine():
     e.close()
 
 
-def expected_segments(a_json: bytes, b_json: bytes, bits: int = 64):
+def expected_segments(a_json: bytes, b_json: bytes, bits: int = O.PATH_HASH_BITS):
     """Oracle view: (seed, [(key, tag, bytes)] for spec/status of A and B, flags)."""
     if O._nesting_bound(a_json) + O._nesting_bound(b_json) > 1000:  # 10000-deep KATs: a thread with a big stack
         return O._on_big_stack(_expected_segments, a_json, b_json, bits)
@@ -74,7 +74,7 @@ def actual_segments(hb: G.HostBatch):
     return out
 
 
-def check_pairs(engine, pairs, bits=64):
+def check_pairs(engine, pairs, bits=O.PATH_HASH_BITS):
     hb = engine.encode(pairs)
     got = actual_segments(hb)
     for (a, b), g in zip(pairs, got):

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 HOST_OK_DEFERRALS = {G.TOK_NUMBER, G.TOK_KEY, G.TOK_STRING, G.TOK_HASH, G.TOK_DEPTH}
 
 
-def _check(eng, docs, seeds=None, must_encode=True, bits=64, allowed=None):
+def _check(eng, docs, seeds=None, must_encode=True, bits=G.PATH_HASH_BITS, allowed=None):
     seeds = seeds if seeds is not None else [0] * len(docs)
     dev = eng.encode_objects(docs, seeds)
     codes = []

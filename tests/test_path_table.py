@@ -18,7 +18,7 @@ from oracle import gpudiff_oracle as O
 from tests.golden.kat_cases import cases as kat_cases
 from tests.workload import configmap, crd, deployment
 
-SEEDS_BITS = [(0, 64), (5, 64), (0, 16), (3, 16)]
+SEEDS_BITS = [(0, 32), (5, 32), (0, 16), (3, 16)]
 
 
 def _objects():

@@ -44,7 +44,7 @@ def main():
     for k, (doc, (di, db)) in enumerate(zip(samp, dev)):
         if di["status"] != G.TOK_OK:
             continue
-        hi, hb = G.encode_object_host(doc, 0, 64)
+        hi, hb = G.encode_object_host(doc, 0, G.PATH_HASH_BITS)
         if hb == db:
             ident += 1
         else:
