@@ -98,6 +98,10 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.hash_mask = c->hash_mask;
     b.k2_variant = (c->flags >> GPUDIFF_OPT_K2_VARIANT_SHIFT) & 0xFu;
     b.k2_blocks_per_cu = (c->flags >> GPUDIFF_OPT_K2_BLOCKS_SHIFT) & 0xFu;
+    {
+        const uint32_t it = (c->flags >> GPUDIFF_OPT_K2_ITEMS_SHIFT) & 3u;
+        b.k2_items_per_wave = it ? 2u << it : 0u;
+    }
     return b;
 }
 
@@ -224,7 +228,7 @@ int gpudiff_encode_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t 
                 enc.encode_json(p.old_json, p.old_len, p.new_json, p.new_len, p.pair_id, p.cluster_id, part.pool,
                                 part.rows[i - b]);
             }
-            size_t pad = (part.pool.size() + 15) & ~(size_t)15;
+            size_t pad = (part.pool.size() + GPUDIFF_BLOB_ALIGN - 1) & ~(size_t)(GPUDIFF_BLOB_ALIGN - 1);
             part.pool.resize(pad, 0);
             part.leaves = enc.leaves_written;
             part.errors = enc.decode_errors;

@@ -219,7 +219,7 @@ int fetch_slot(DStore* s, uint32_t slot, HostSlot& H) {
 // the path table of a device-resident blob: its trailer
 int load_tab(DStore* s, HostSlot& H) {
     if (H.tab_loaded) return GPUDIFF_OK;
-    const uint64_t segs = gpudiff_seg_bytes(H.sl, H.sar) + gpudiff_seg_bytes(H.tl, H.tar);
+    const uint64_t segs = gpudiff_blob_body(H.sl, H.sar, H.tl, H.tar);  // the table follows the body
     H.tab.n = H.n_tab;
     H.tab.data.resize(H.bytes - segs);
     if (!H.tab.data.empty())
@@ -403,7 +403,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
         ups.push_back(u);
     }
     // place: blobs behind the append point, rows, slot states
-    const uint64_t pbytes = (pool.size() + 15) & ~15ull;
+    const uint64_t pbytes = (pool.size() + GPUDIFF_BLOB_ALIGN - 1) & ~(uint64_t)(GPUDIFF_BLOB_ALIGN - 1);
     pool.resize(pbytes, 0);
     if ((rc = ensure_space(s, pbytes, pbytes))) return rc;
     if ((rc = grow_dev(&s->res_stage, &s->res_stage_cap, std::max<uint64_t>(pbytes, 16)))) return rc;
@@ -582,7 +582,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         jbytes = (jbytes + len + kTokSlack + 15) & ~15ull;
         // blob + path table: typically < 2.5x the JSON (the append estimate that triggers compaction);
         // K0 defers a document that does not fit (SPACE) to the host
-        bound += (5 * (uint64_t)len) / 2 + 128;
+        bound += (5 * (uint64_t)len) / 2 + 384;  // + the body's and the table's pads to 128 B
         floor += len;
         DocLink& L = links[nd];
         memset(&L, 0, sizeof(L));

@@ -79,9 +79,10 @@ __global__ __launch_bounds__(256) void k_collide(const DocLink* __restrict__ lin
         // the path tables (include/gpudiff_format.h): a hash both hold must have the same parent
         // hash and the same last component in each
         const uint32_t na = A.ntab, nb = B.n_tab;
-        const uint64_t* ha = (const uint64_t*)(space + A.off + seg_bytes(A.sl, A.sar) + seg_bytes(A.tl, A.tar));
-        const uint64_t* hb = (const uint64_t*)(space + B.off + seg_bytes(B.spec_l, B.spec_ar) +
-                                               seg_bytes(B.stat_l, B.stat_ar));
+        // each table at its blob's body end (gpudiff_blob_body: the segments rounded up to 128 B)
+        const uint64_t* ha = (const uint64_t*)(space + A.off + ((seg_bytes(A.sl, A.sar) + seg_bytes(A.tl, A.tar) + 127u) & ~127ull));
+        const uint64_t* hb = (const uint64_t*)(space + B.off + ((seg_bytes(B.spec_l, B.spec_ar) +
+                                                                 seg_bytes(B.stat_l, B.stat_ar) + 127u) & ~127ull));
         const uint8_t* ka = (const uint8_t*)(ha + 3ull * na);
         const uint8_t* kb = (const uint8_t*)(hb + 3ull * nb);
         for (uint32_t i = lane; i < nb; i += 64) {

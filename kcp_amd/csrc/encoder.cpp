@@ -226,14 +226,14 @@ bool PairEncoder::assign_seed(FlatObject& a, FlatObject& b, uint32_t* seed_out) 
     return false;
 }
 
-static inline void pool_align16(std::vector<uint8_t>& pool) {
-    size_t n = (pool.size() + 15) & ~(size_t)15;
+static inline void pool_align(std::vector<uint8_t>& pool) {
+    size_t n = (pool.size() + GPUDIFF_BLOB_ALIGN - 1) & ~(size_t)(GPUDIFF_BLOB_ALIGN - 1);
     pool.resize(n, 0);
 }
 
 void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, uint64_t* off, uint32_t* sl,
                              uint32_t* sar, uint32_t* tl, uint32_t* tar) {
-    pool_align16(pool);
+    pool_align(pool);
     *off = pool.size();
     auto seg = [&](const std::vector<LeafRec>& v, uint32_t* L, uint32_t* AR) {
         const size_t n = v.size();
@@ -269,6 +269,7 @@ void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, ui
     };
     seg(o.spec, sl, sar);
     seg(o.stat, tl, tar);
+    pool_align(pool);  // the body's zero pad (gpudiff_blob_body)
 }
 
 void PairEncoder::encode_flat(FlatObject* fa, FlatObject* fb, uint32_t pair_id, uint32_t cluster_id,
@@ -279,7 +280,7 @@ void PairEncoder::encode_flat(FlatObject* fa, FlatObject* fb, uint32_t pair_id, 
     uint32_t seed = 0;
     if (!fa || !fb || !assign_seed(*fa, *fb, &seed)) {
         decode_errors++;
-        pool_align16(pool);
+        pool_align(pool);
         row.off_a = row.off_b = pool.size();
         row.flags_a = row.flags_b = GPUDIFF_OBJ_DECODE_ERR;
         return;

@@ -187,12 +187,20 @@ inline uint64_t blob_value_bytes(const uint8_t* blob, uint32_t spec_l, uint32_t 
     return v;
 }
 
-// bytes the decision kernel must read for this pair (DESIGN.md "Roofline")
+// bytes the decision kernel must read for this pair (DESIGN.md "Roofline"): the row, the flag, and
+// per object the compared 16-B chunks -- the same rule as k_compare_flat: with both regions compared
+// the stream covers the whole body (segments + zero pad to 128 B); with spec only, the spec segment,
+// padded too when neither side has status leaves; with status only, the status segment
 inline uint64_t pair_compare_bytes(const gpudiff_pair_row& r) {
     uint64_t b = sizeof(gpudiff_pair_row) + 1;
     if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) return b;
-    if (r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b) b += 2 * gpudiff_seg_bytes(r.spec_l_a, r.spec_ar_a);
-    if ((r.flags_b & GPUDIFF_OBJ_HAS_STATUS) && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b)
-        b += 2 * gpudiff_seg_bytes(r.stat_l_a, r.stat_ar_a);
-    return b;
+    const bool spec_sz = r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b;
+    const bool stat_sz = (r.flags_b & GPUDIFF_OBJ_HAS_STATUS) && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b;
+    const uint64_t seg_s = gpudiff_seg_bytes(r.spec_l_a, r.spec_ar_a), seg_t = gpudiff_seg_bytes(r.stat_l_a, r.stat_ar_a);
+    const uint64_t al = GPUDIFF_BLOB_ALIGN - 1;
+    uint64_t per = 0;
+    if (spec_sz && stat_sz) per = (seg_s + seg_t + al) & ~al;
+    else if (spec_sz) per = (r.stat_l_a | r.stat_l_b | r.stat_ar_a | r.stat_ar_b) ? seg_s : (seg_s + al) & ~al;
+    else if (stat_sz) per = seg_t;
+    return b + 2 * per;
 }

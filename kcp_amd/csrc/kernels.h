@@ -40,6 +40,7 @@ struct DiffBuffers {
     uint8_t* out_k;
     uint64_t hash_mask;
     uint32_t k2_variant;        // tuning: 0 default = k_compare_flat, 4 x 16-B chunks in flight per lane per object
+    uint32_t k2_items_per_wave; // tuning: 0 = default; 64-pair chunks split until each resident wave has this many items
     uint32_t k2_blocks_per_cu;  // tuning: 0 = the variant's occupancy (4 resident 256-thread blocks per CU)
 };
 

@@ -766,7 +766,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // DYN variants: chunks at the end of a launch handed out as 8-pair items (about
 // four per wave), unless the whole launch is split already
 __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift) {
-    return sub_shift ? 0u : min(nch, nwaves / 2u);
+    return sub_shift >= 3u ? 0u : min(nch, nwaves / 2u);
 }
 
 // One wave per work item of P = 64 >> sub_shift consecutive pairs.  Lane k
@@ -839,8 +839,15 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const bool has_st_b = (v3.y & GPUDIFF_OBJ_HAS_STATUS) != 0u;
         const bool stat_sz = has_st_b && v2.x == v2.y && v2.z == v2.w;
         const uint32_t seg_a = (uint32_t)seg_bytes(v1.x, v1.z), seg_b = (uint32_t)seg_bytes(v1.y, v1.w);
-        const uint32_t n1 = (ok && spec_sz) ? seg_a >> 4 : 0u;
-        const uint32_t n2 = (ok && stat_sz) ? (uint32_t)(seg_bytes(v2.x, v2.z) >> 4) : 0u;
+        const uint32_t seg_t = (uint32_t)seg_bytes(v2.x, v2.z);
+        // whole 128-B lines wherever both sides' spans are equal: with both regions compared the stream
+        // runs to the body's end (segments + zero pad, gpudiff_blob_body), with spec only and no status
+        // leaves on either side the spec span is padded the same way; a stream that ends inside a line
+        // costs a partial-line request per object (engine.h pair_compare_bytes counts the same chunks)
+        const uint32_t r128 = ((seg_a + seg_t + 127u) & ~127u);
+        const bool no_stat = (v2.x | v2.y | v2.z | v2.w) == 0u;
+        const uint32_t n1 = (ok && spec_sz) ? ((!stat_sz && no_stat) ? ((seg_a + 127u) & ~127u) : seg_a) >> 4 : 0u;
+        const uint32_t n2 = (ok && stat_sz) ? (spec_sz ? r128 - seg_a : seg_t) >> 4 : 0u;
         const uint32_t tot = n1 + n2;
         const uint32_t incl = wave_incl_scan(tot);
         const uint32_t total = uni(shfl32(incl, 63));
@@ -1104,6 +1111,9 @@ static bool k2_is_dyn(uint32_t variant) {
     }
 }
 
+// 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
+constexpr uint32_t kK2ItemsPerWave = 8;  // A/B at the N = 8 shard size (1.25M pairs): 8 beats 4 by 1.5%, 16 loses 8%
+
 static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     // one resident 256-thread block per CU per wave slot a SIMD offers the
     // kernel (its measured occupancy, hipOccupancyMaxActiveBlocksPerMultiprocessor):
@@ -1123,7 +1133,7 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
 // 64-pair chunks split into 2^k items until there are >= 4 items per resident
 // wave (config3's 156k chunks: k = 0; config4's 1.6k chunks of deep pairs: k = 4)
 static uint32_t k2_sub_shift(const DiffBuffers& b, uint32_t nchunks) {
-    const uint64_t want = 4ull * 4u * k2_cap_blocks(b);
+    const uint64_t want = (uint64_t)(b.k2_items_per_wave ? b.k2_items_per_wave : kK2ItemsPerWave) * 4u * k2_cap_blocks(b);
     uint32_t k = 0;
     while (k < 6 && (uint64_t)nchunks << k < want) k++;
     return k;

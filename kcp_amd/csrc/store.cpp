@@ -69,7 +69,7 @@ struct Worker {
 inline uint64_t local_tag(uint32_t part, uint64_t off) { return kLocal | ((uint64_t)part << kLocalPartShift) | off; }
 
 uint32_t blob_bytes(uint32_t sl, uint32_t sar, uint32_t tl, uint32_t tar) {
-    return (uint32_t)(gpudiff_seg_bytes(sl, sar) + gpudiff_seg_bytes(tl, tar));
+    return (uint32_t)gpudiff_blob_body(sl, sar, tl, tar);
 }
 
 }  // namespace
@@ -260,7 +260,7 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
         std::swap(S.tab, w.fn.tab);
         w.touched.push_back(e.slot);
     }
-    size_t pad = (w.pool.size() + 15) & ~(size_t)15;
+    size_t pad = (w.pool.size() + GPUDIFF_BLOB_ALIGN - 1) & ~(size_t)(GPUDIFF_BLOB_ALIGN - 1);
     w.pool.resize(pad, 0);
 }
 

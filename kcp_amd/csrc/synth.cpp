@@ -761,7 +761,7 @@ int gpudiff_synth_encode(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t 
             }
             w.truth[i - b] = (uint8_t)truth;
         }
-        w.pool.resize((w.pool.size() + 15) & ~(size_t)15, 0);
+        w.pool.resize((w.pool.size() + GPUDIFF_BLOB_ALIGN - 1) & ~(size_t)(GPUDIFF_BLOB_ALIGN - 1), 0);
         w.leaves = w.enc.leaves_written;
     };
     std::vector<std::thread> th;

@@ -634,8 +634,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         ARs = (ARs + 15u) & ~15u;  // gpudiff_arena_bytes: each arena a multiple of 16
         ARt = (ARt + 15u) & ~15u;
         const uint64_t seg_s = seg_bytes(Ls, ARs), seg_t = seg_bytes(Lt, ARt);
-        const uint64_t tab = (24ull * Nt + KB + 15u) & ~15ull;  // gpudiff_tab_bytes: blobs stay 16-B multiples
-        const uint64_t bytes = seg_s + seg_t + tab;
+        const uint64_t body = (seg_s + seg_t + 127u) & ~127ull;  // gpudiff_blob_body: 128-B line multiples
+        const uint64_t tab = (24ull * Nt + KB + 127u) & ~127ull; // gpudiff_tab_bytes
+        const uint64_t bytes = body + tab;
         uint64_t off = 0;
         if (lane == 0) off = atomicAdd(used, (unsigned long long)bytes);
         off = rdlane64(off, 0);
@@ -645,12 +646,13 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             uint8_t* blob = space + off;
             uint8_t* segp[2] = {blob, blob + seg_s};
             const uint32_t Lr[2] = {Ls, Lt};
-            uint64_t* hs = (uint64_t*)(blob + seg_s + seg_t);
+            uint64_t* hs = (uint64_t*)(blob + body);
             uint64_t* phs = hs + Nt;
             uint64_t* cs = phs + Nt;
             uint8_t* keys = (uint8_t*)(cs + Nt);
             // zero the key area's pad (a segment's leaf records are 16 B each: no pad before the arena)
-            if (lane < tab - 24ull * Nt - KB) keys[KB + lane] = 0;
+            for (uint32_t q = lane; q < tab - 24ull * Nt - KB; q += 64) keys[KB + q] = 0;
+            if (lane < (body - seg_s - seg_t) / 16u) ((u32x4*)(blob + seg_s + seg_t))[lane] = u32x4{0u, 0u, 0u, 0u};
             const uint64_t root = seed & mask;
             uint32_t rank[2] = {0, 0}, aoff[2] = {0, 0}, trank = 0, tko = 0;
             for (uint32_t j0 = 0; j0 < ns; j0 += 64) {

@@ -651,7 +651,7 @@ class Engine:
         ptrs = (C.c_void_p * max(n, 1))(*[C.cast(b, C.c_void_p) for b in bufs])
         lens = (C.c_size_t * max(n, 1))(*[len(x) for x in docs])
         sd = (C.c_uint32 * max(n, 1))(*(list(seeds) if seeds is not None else [0] * n))
-        cap = out_cap or sum(31 * len(x) + 96 for x in docs) + 16
+        cap = out_cap or sum(31 * len(x) + 352 for x in docs) + 16  # + a body and a table pad to 128 B each
         out = C.create_string_buffer(cap)
         info = (ObjInfo * max(n, 1))()
         _chk(_lib.gpudiff_encode_objects(self.ctx, ptrs, lens, sd, n, C.cast(out, C.c_void_p), cap, info),
@@ -1049,8 +1049,7 @@ def decode_path_table(blob: bytes, info: dict):
     n = info["n_tab"]
     if n == TAB_NONE:
         return None
-    seg = segment_bytes
-    base = seg(info["spec_l"], info["spec_ar"]) + seg(info["stat_l"], info["stat_ar"])
+    base = blob_body(info["spec_l"], info["spec_ar"], info["stat_l"], info["stat_ar"])
     if not n:
         return []
     hs = np.frombuffer(blob, "<u8", n, base)
@@ -1091,6 +1090,14 @@ def decode_segment(pool: bytes, off: int, L: int, arena: int):
         out.append((k, v, m, vb))
     assert ((ar - off - head + 15) & ~15) == arena, (ar, off, head, arena)
     return out
+
+
+BLOB_ALIGN = 128  # GPUDIFF_BLOB_ALIGN
+
+
+def blob_body(sl: int, sar: int, tl: int, tar: int) -> int:
+    """Both segments zero padded to 128 B (gpudiff_blob_body): a store blob's path table starts here."""
+    return (segment_bytes(sl, sar) + segment_bytes(tl, tar) + BLOB_ALIGN - 1) & ~(BLOB_ALIGN - 1)
 
 
 def segment_bytes(L: int, arena: int) -> int:

@@ -77,10 +77,13 @@ def tensor_fill(spec_ids, status_ids):
 
 
 class DirtyGather:
-    """The per-step collective with no host synchronisation: preallocated
-    buffers of a fixed capacity per list, one all-gather of the per-rank
-    counts (int32 [8]: n_spec, n_status, ...) and one of each ID list, padded
-    to the capacity.  The capacities are agreed once, before the timed steps
+    """The per-step collective with no host synchronisation and ONE all-gather
+    per step: each rank packs [counts int32[8] (n_spec, n_status, ...) |
+    spec-dirty IDs (capacity cap_spec) | status-dirty IDs (capacity
+    cap_status)] into one preallocated int32 buffer and the buffers are
+    all-gathered in a single RCCL call (one collective latency instead of
+    three: at N = 8 the step's diff pass is ~1 ms, so per-call latency
+    matters).  The capacities are agreed once, before the timed steps
     (`agree_capacity`: the all-gathered maximum of a first pass's counts); the
     gathered counts say how many IDs of each rank's slot are real, and
     `check()` -- called after the timed region -- reports a rank whose count
@@ -91,10 +94,11 @@ class DirtyGather:
         import torch
         self.world, self.dist = world, dist
         self.cap = (max(1, int(cap_spec)), max(1, int(cap_status)))
-        self.counts = torch.zeros(8, dtype=torch.int32, device=device)
-        self.all_counts = torch.zeros(world * 8, dtype=torch.int32, device=device)
-        self.buf = [torch.zeros(c, dtype=torch.int32, device=device) for c in self.cap]
-        self.all_ids = [torch.zeros(world * c, dtype=torch.int32, device=device) for c in self.cap]
+        self.width = 8 + self.cap[0] + self.cap[1]
+        self.send = torch.zeros(self.width, dtype=torch.int32, device=device)
+        self.all = torch.zeros(world * self.width, dtype=torch.int32, device=device)
+        self.counts = self.send[:8]
+        self.buf = [self.send[8:8 + self.cap[0]], self.send[8 + self.cap[0]:]]
 
     @staticmethod
     def agree_capacity(counts, world: int, dist, slack: float = 1.0):
@@ -107,17 +111,20 @@ class DirtyGather:
 
     def step(self, fill_counts, fill_ids):
         """fill_counts(tensor[8]) and fill_ids(col, tensor[cap]) write this
-        rank's values on the device (the GPU path: gpudiff_dbatch_export
-        straight from HBM, ordered on the stream before the collectives)."""
+        rank's values into its slots of the send buffer on the device (the GPU
+        path: gpudiff_dbatch_export straight from HBM, ordered on the stream
+        before the collective)."""
         fill_counts(self.counts)
-        self.dist.all_gather_into_tensor(self.all_counts, self.counts)
         for col in (0, 1):
             fill_ids(col, self.buf[col])
-            self.dist.all_gather_into_tensor(self.all_ids[col], self.buf[col])
+        self.dist.all_gather_into_tensor(self.all, self.send)
+
+    def _rows(self):
+        return self.all.view(self.world, self.width)
 
     def check(self):
         """-> (ok, host count matrix [world, 8])"""
-        cc = self.all_counts.view(self.world, -1).cpu()
+        cc = self._rows()[:, :8].cpu()
         ok = bool((cc[:, 0] <= self.cap[0]).all() and (cc[:, 1] <= self.cap[1]).all())
         return ok, cc
 
@@ -127,8 +134,7 @@ class DirtyGather:
         ok, cc = self.check()
         if not ok:
             raise RuntimeError("dirty-ID capacity exceeded: %s > %s" % (cc[:, :2].tolist(), self.cap))
-        out = []
-        for col in (0, 1):
-            v = self.all_ids[col].view(self.world, self.cap[col])
-            out.append(torch.cat([v[r, :int(cc[r, col])] for r in range(self.world)]))
-        return out[0], out[1]
+        rows = self._rows()
+        spec = torch.cat([rows[r, 8:8 + int(cc[r, 0])] for r in range(self.world)])
+        stat = torch.cat([rows[r, 8 + self.cap[0]:8 + self.cap[0] + int(cc[r, 1])] for r in range(self.world)])
+        return spec, stat
