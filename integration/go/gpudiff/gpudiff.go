@@ -409,6 +409,82 @@ func (e *Engine) UpsertBodies(objs []interface{}, mode Mode) ([][]byte, error) {
 	return res, nil
 }
 
+// OptDeviceEncode opens an engine whose submits send raw JSON to the GPU (kernel K0); DiffAndPlan needs it.
+const OptDeviceEncode = uint32(C.GPUDIFF_OPT_DEVICE_ENCODE)
+
+// Write is one API call the syncer's decisions imply (gpudiff_write_plan_get): for a spec-dirty pair
+// upsertIntoDownstream's body of the upstream object A, written over the downstream copy B
+// (specsyncer.go:86-132); for a status-dirty pair updateStatusInUpstream's body of B, written into A
+// (statussyncer.go:41-63).
+type Write struct {
+	Pair int    // index into the olds / news given to DiffAndPlan
+	Kind Mode   // UpsertSpec or UpsertStatus
+	Noop bool   // the write changes nothing the predicates compare (GPUDIFF_SPEC_NOOP / _STATUS_NOOP): skip the call
+	Body []byte // the request body; nil for a no-op, or when Go cannot decode the object (reference path)
+}
+
+// DiffAndPlan decides n (old, new) pairs on the device and renders the writes those decisions imply from
+// the JSON still staged in HBM (kernel K10, no second upload): flags[i] are the pair's GPUDIFF_* result
+// bits, writes list the spec writes (ascending pair) then the status writes.  The engine must have been
+// opened with OptDeviceEncode.  The caller issues each non-no-op write as today (Create, then Update with
+// the live resourceVersion on AlreadyExists, specsyncer.go:110-129).
+func (e *Engine) DiffAndPlan(olds, news [][]byte) ([]uint8, []Write, error) {
+	n := len(olds)
+	if n == 0 || len(news) != n {
+		return nil, nil, nil
+	}
+	pairs := (*[1 << 28]C.gpudiff_json_pair)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_json_pair{}))))[:n:n]
+	defer C.free(unsafe.Pointer(&pairs[0]))
+	for i := range olds {
+		pa, la := cmem(olds[i])
+		pb, lb := cmem(news[i])
+		pairs[i] = C.gpudiff_json_pair{old_json: pa, old_len: la, new_json: pb, new_len: lb, pair_id: C.uint32_t(i)}
+	}
+	defer func() {
+		for i := range pairs {
+			C.free(unsafe.Pointer(pairs[i].old_json))
+			C.free(unsafe.Pointer(pairs[i].new_json))
+		}
+	}()
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	var ticket C.gpudiff_ticket
+	if err := errOf(C.gpudiff_submit(e.ctx, &pairs[0], C.size_t(n), &ticket)); err != nil {
+		return nil, nil, err
+	}
+	var res C.gpudiff_result
+	if err := errOf(C.gpudiff_wait(e.ctx, ticket, &res)); err != nil {
+		return nil, nil, err
+	}
+	flags := make([]uint8, n)
+	copy(flags, (*[1 << 30]uint8)(unsafe.Pointer(res.pair_flags))[:n:n])
+	C.gpudiff_result_release(e.ctx, &res)
+	var plan C.gpudiff_write_plan
+	if err := errOf(C.gpudiff_write_plan_get(e.ctx, ticket, &plan)); err != nil {
+		return flags, nil, err
+	}
+	defer C.gpudiff_write_plan_release(e.ctx, &plan)
+	m := int(plan.n)
+	writes := make([]Write, m)
+	if m == 0 {
+		return flags, writes, nil
+	}
+	idx := (*[1 << 30]C.uint32_t)(unsafe.Pointer(plan.pair_index))[:m:m]
+	kind := (*[1 << 30]C.uint8_t)(unsafe.Pointer(plan.kind))[:m:m]
+	noop := (*[1 << 30]C.uint8_t)(unsafe.Pointer(plan.noop))[:m:m]
+	offs := (*[1 << 30]C.uint64_t)(unsafe.Pointer(plan.bodies.offsets))[: m+1 : m+1]
+	st := (*[1 << 30]C.int32_t)(unsafe.Pointer(plan.bodies.status))[:m:m]
+	for k := 0; k < m; k++ {
+		w := Write{Pair: int(idx[k]), Kind: Mode(kind[k]), Noop: noop[k] != 0}
+		if !w.Noop && st[k] == 0 {
+			w.Body = C.GoBytes(unsafe.Pointer(uintptr(unsafe.Pointer(plan.bodies.bytes))+uintptr(offs[k])),
+				C.int(offs[k+1]-offs[k]))
+		}
+		writes[k] = w
+	}
+	return flags, writes, nil
+}
+
 // RollupGroup is the status roll-up of one root Deployment
 // (pkg/reconciler/deployment/deployment.go:71-91): the int32 sums of its
 // leaves' status counters and the index of others[0] (whose
