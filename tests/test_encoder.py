@@ -94,13 +94,35 @@ def test_rows_layout(host_engine):
     hb = host_engine.encode([(J(BASE), J(BASE))], ids=[77], clusters=[5])
     r = hb.rows()[0]
     assert r["pair_id"] == 77 and r["cluster_id"] == 5
-    assert r["off_a"] % 16 == 0 and r["off_b"] % 16 == 0
+    assert r["off_a"] % 128 == 0 and r["off_b"] % 128 == 0  # GPUDIFF_BLOB_ALIGN: blobs start on HBM lines
     assert r["spec_ar_a"] % 16 == 0
     # identical objects -> byte-identical segments
     pool = hb.pool()
     la = G.segment_bytes(int(r["spec_l_a"]), int(r["spec_ar_a"])) + G.segment_bytes(int(r["stat_l_a"]),
                                                                                         int(r["stat_ar_a"]))
     assert pool[r["off_a"]:r["off_a"] + la] == pool[r["off_b"]:r["off_b"] + la]
+    # the body: segments zero padded to 128 B (the decision kernel streams the pad)
+    body = G.blob_body(int(r["spec_l_a"]), int(r["spec_ar_a"]), int(r["stat_l_a"]), int(r["stat_ar_a"]))
+    assert body % 128 == 0 and body - la < 128 and pool[r["off_a"] + la:r["off_a"] + body] == bytes(body - la)
+
+
+def test_bodies_line_aligned_and_zero_padded(host_engine):
+    """Every blob of a mixed batch starts on a 128-B line and its body's pad is zero (K2 compares the pad
+    of both sides whenever their sizes match, so a nonzero pad would be a false 'dirty')."""
+    pairs = [(a, b) for _, a, b, _, _ in CASES]
+    hb = host_engine.encode(pairs)
+    pool = hb.pool()
+    for r in hb.rows():
+        if r["flags_a"] & G.OBJ_DECODE_ERR:
+            continue
+        for s in ("a", "b"):
+            off = int(r["off_" + s])
+            la = G.segment_bytes(int(r["spec_l_" + s]), int(r["spec_ar_" + s])) + \
+                G.segment_bytes(int(r["stat_l_" + s]), int(r["stat_ar_" + s]))
+            body = G.blob_body(int(r["spec_l_" + s]), int(r["spec_ar_" + s]), int(r["stat_l_" + s]),
+                               int(r["stat_ar_" + s]))
+            assert off % 128 == 0 and off + body <= len(pool)
+            assert pool[off + la:off + body] == bytes(body - la)
 
 
 def test_value_hash_host_matches_xxhash():

@@ -34,6 +34,7 @@ def _check(eng, docs, seeds=None, must_encode=True, bits=G.PATH_HASH_BITS, allow
             for f in ("oflags", "spec_l", "spec_ar", "stat_l", "stat_ar", "bytes", "n_tab"):
                 assert di[f] == hi[f], (k, f, di, hi, doc[:300])
             assert db == hb, "blob differs for doc %d: %r" % (k, doc[:300])
+            assert di["off"] % 128 == 0 and di["bytes"] % 128 == 0, di  # line-aligned store blobs
         else:
             if hi["status"] == G.TOK_OK:  # a document Go accepts is deferred only for a documented reason
                 assert di["status"] in HOST_OK_DEFERRALS, (k, di["status"], doc[:300])
