@@ -486,6 +486,88 @@ __device__ __forceinline__ void wave_esc_put(uint8_t* o, const uint8_t* s, uint3
 }
 constexpr uint32_t kLongString = 16;
 
+// ---- flattened string passes (K10): every lane's string (at most one per lane) is cut into 4-byte
+// units laid end to end; each pass the wave takes 64 consecutive units, a unit's owner lane found by a
+// binary search over the inclusive unit prefix (as K2 does over 16-B chunks), so a window's strings of
+// any length cost sum(len) / 256 passes instead of one pass per long string plus the longest short one.
+// Unit loads read up to 15 bytes past a string (ld8u): the JSON and decoded-string buffers keep that slack.
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    return ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32) | shfl32((uint32_t)v, src);
+}
+struct FlatUnits {
+    uint32_t incl, total;
+};
+__device__ __forceinline__ FlatUnits flat_units(bool has, uint32_t n) {
+    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const uint32_t incl = wave_incl_scan(units);
+    return FlatUnits{incl, rdlane(incl, 63)};
+}
+// owner lane of unit g (the first lane whose inclusive prefix exceeds g; 63 past the end)
+__device__ __forceinline__ uint32_t flat_owner(const FlatUnits& f, uint32_t g) {
+    uint32_t o = 0;
+#pragma unroll
+    for (uint32_t st = 32; st >= 1; st >>= 1)
+        if (shfl32(f.incl, o + st - 1u) <= g) o += st;
+    return min(o, 63u);
+}
+// extra output bytes of this lane's string s[0, n) under Go's HTML-safe escaping (escaped length - n);
+// 0 iff every byte is written as it is
+__device__ uint32_t wave_esc_extra(bool has, const uint8_t* s, uint32_t n) {
+    const uint32_t lane = __lane_id();
+    const FlatUnits f = flat_units(has, n);
+    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const uint64_t sp = (uint64_t)(uintptr_t)s;
+    int32_t acc = 0;
+    for (uint32_t b = 0; b < f.total; b += 64) {
+        const uint32_t g = b + lane;
+        const uint32_t o = flat_owner(f, g);
+        const uint32_t first = shfl32(f.incl - units, o), on = shfl32(n, o);
+        const uint64_t op = shfl64(sp, o);
+        int32_t extra = 0;
+        if (g < f.total) {
+            const uint32_t k = 4u * (g - first);
+            const uint8_t* p = (const uint8_t*)(uintptr_t)op;
+            const uint32_t w = (uint32_t)ld8u(p + k);
+            const uint32_t nb = min(4u, on - k);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint32_t c = (w >> (8u * j)) & 0xFFu;
+                const bool plain = c >= 0x20u && c < 0x80u && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&';
+                if (j < nb && !plain) extra += (int32_t)esc_unit(p, on, k + j) - 1;
+            }
+        }
+        for (uint64_t m = __ballot(extra != 0); m; m &= m - 1) {  // escapes are rare
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            const int32_t e = (int32_t)rdlane((uint32_t)extra, j);
+            if (lane == rdlane(o, j)) acc += e;
+        }
+    }
+    return (uint32_t)acc;
+}
+// copies this lane's string s[0, n) to o[0, n) (strings that need no escaping)
+__device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* o) {
+    const uint32_t lane = __lane_id();
+    const FlatUnits f = flat_units(has, n);
+    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const uint64_t sp = (uint64_t)(uintptr_t)s, dp = (uint64_t)(uintptr_t)o;
+    for (uint32_t b = 0; b < f.total; b += 64) {
+        const uint32_t g = b + lane;
+        const uint32_t ow = flat_owner(f, g);
+        const uint32_t first = shfl32(f.incl - units, ow), on = shfl32(n, ow);
+        const uint64_t op = shfl64(sp, ow), od = shfl64(dp, ow);
+        if (g < f.total) {
+            const uint32_t k = 4u * (g - first);
+            const uint32_t w = (uint32_t)ld8u((const uint8_t*)(uintptr_t)op + k);
+            uint8_t* q = (uint8_t*)(uintptr_t)od + k;
+            const uint32_t nb = min(4u, on - k);
+            q[0] = (uint8_t)w;
+            if (nb > 1) q[1] = (uint8_t)(w >> 8);
+            if (nb > 2) q[2] = (uint8_t)(w >> 16);
+            if (nb > 3) q[3] = (uint8_t)(w >> 24);
+        }
+    }
+}
+
 // ---- float64 -> Go text (floatEncoder(64): strconv.AppendFloat(f, 'f'|'e', -1, 64)
 // with the 1e-6 / 1e21 switch and the e-09 -> e-9 clean-up).  The shortest,
 // closest (ties to even) digit string is Ryu's (Adams, PLDI 2018): this is
@@ -700,6 +782,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return v;
 }
 constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u, MF_FLOAT = 16u;
+constexpr uint32_t MF_VCLEAN = 32u, MF_KCLEAN = 64u;  // string value / key written as its own bytes
 constexpr uint32_t kMarshalMaxMembers = 2048;
 constexpr int kModeEncode = 0, kModeMarshal = 1, kModeRollup = 2, kModeNegotiate = 3;
 
