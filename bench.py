@@ -59,6 +59,15 @@ def k2_source_hash():
     return h.hexdigest()[:16]
 
 
+def free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    p = sk.getsockname()[1]
+    sk.close()
+    return p
+
+
 def host_cores():
     """(threads for the CPU baseline = every CPU this process may run on, nproc, cgroup CPU quota or None)."""
     aff = len(os.sched_getaffinity(0))
@@ -100,6 +109,10 @@ def main():
                     help="strong: the config's population split N ways (the metric's 10M/100k node-wide; "
                          "default for N > 1); weak: per-GPU work fixed (node population = N x the config)")
     ap.add_argument("--chunk", type=int, default=262144)
+    ap.add_argument("--gather-depth", type=int, default=2,
+                    help="N > 1: pipelined all-gathers in flight (step s's collective overlaps step s+1's diff); 1 = serial")
+    ap.add_argument("--gather-world1", action="store_true",
+                    help="run the per-step RCCL collective even at world size 1 (exercises/measures it on one GPU)")
     ap.add_argument("--engine-flags", type=lambda x: int(x, 0), default=0,
                     help="extra GPUDIFF_OPT_* tuning bits for the diff engine (diagnostics, e.g. 0xF << 21 defers "
                          "every join to K4)")
@@ -151,8 +164,11 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    collective = world > 1 or args.gather_world1
+    if collective:
+        dist.init_process_group("nccl", device_id=dev, world_size=world, rank=rank,
+                                init_method=None if world > 1 or "MASTER_ADDR" in os.environ else
+                                "tcp://127.0.0.1:%d" % free_port())
     stream = torch.cuda.current_stream(dev)
     aff, nproc, quota = host_cores()
     threads = args.threads or max(1, min(16, aff))
@@ -224,12 +240,12 @@ def main():
 
     # ---------------- the collective (N > 1): capacities agreed once, untimed
     gather = None
-    if world > 1:
+    if collective:
         counts = torch.zeros(8, dtype=torch.int32, device=dev)
         db.export(G.EXPORT_COUNTS, counts.data_ptr(), 8)
         torch.cuda.synchronize()
         cap_s, cap_t = shard.DirtyGather.agree_capacity(counts, world, dist)
-        gather = shard.DirtyGather(world, cap_s, cap_t, dev, dist)
+        gather = shard.DirtyGather(world, cap_s, cap_t, dev, dist, depth=args.gather_depth)
 
         def fill_counts(t):
             db.export(G.EXPORT_COUNTS, t.data_ptr(), 8)
@@ -238,6 +254,7 @@ def main():
             db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
                       buf.numel())
         gather.step(fill_counts, fill_ids)  # warm the communicator
+        gather.finish()
         torch.cuda.synchronize()
 
     # ---------------- timed region
@@ -250,18 +267,21 @@ def main():
         eng.diff(db)
         if gather is not None:
             gather.step(fill_counts, fill_ids)
+    if gather is not None:
+        gather.finish()  # every step's collective completes inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     tm = eng.timings()
     gather_check = None
-    if world > 1:
+    if gather is not None:
         ok, cc = gather.check()
         sa, ta = gather.result() if ok else (None, None)
         gather_check = dict(capacity_ok=ok, node_spec_dirty=int(cc[:, 0].sum()), node_status_dirty=int(cc[:, 1].sum()),
                             gathered_spec=None if sa is None else int(sa.numel()),
-                            gathered_status=None if ta is None else int(ta.numel()))
+                            gathered_status=None if ta is None else int(ta.numel()),
+                            depth=gather.depth, bytes_per_rank=4 * gather.width)
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -357,7 +377,8 @@ def main():
                     "40% ConfigMap/Secret, 40% Deployment, 20% CRD" if args.config == "config3" else args.config),
                 "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9,
                 "parallelism": "shard-by-logical-cluster x%d (LPT)%s" % (
-                    world, ", RCCL all-gather of dirty counts+IDs per step" if world > 1 else ""),
+                    world, (", RCCL all-gather of dirty counts+IDs per step (%d in flight)" % args.gather_depth)
+                    if collective else ""),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
@@ -381,7 +402,7 @@ def main():
             "ingest_s": t_gen,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if collective:
         dist.destroy_process_group()
 
 

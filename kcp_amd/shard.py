@@ -88,15 +88,33 @@ class DirtyGather:
     gathered counts say how many IDs of each rank's slot are real, and
     `check()` -- called after the timed region -- reports a rank whose count
     exceeded the capacity (its IDs were truncated: the step must be redone
-    with larger buffers, never silently accepted)."""
+    with larger buffers, never silently accepted).
 
-    def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist):
+    Pipelining (`depth` > 1): the all-gather is issued asynchronously
+    (async_op=True) on the backend's own stream, so step s's collective runs
+    while step s+1's diff pass streams on the compute stream -- the same
+    overlap of communication with compute a training step gets from bucketed
+    all-reduce.  Step s writes send buffer s % depth; before a buffer is
+    refilled the compute stream waits (device-side, `work.wait()`) for the
+    collective that last read it, so no host synchronisation is added and
+    every step's gather completes.  `finish()` joins the outstanding
+    collectives; it belongs inside the timed region."""
+
+    def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist, depth: int = 1):
         import torch
         self.world, self.dist = world, dist
         self.cap = (max(1, int(cap_spec)), max(1, int(cap_status)))
         self.width = 8 + self.cap[0] + self.cap[1]
-        self.send = torch.zeros(self.width, dtype=torch.int32, device=device)
-        self.all = torch.zeros(world * self.width, dtype=torch.int32, device=device)
+        self.depth = max(1, int(depth))
+        self.sends = [torch.zeros(self.width, dtype=torch.int32, device=device) for _ in range(self.depth)]
+        self.alls = [torch.zeros(world * self.width, dtype=torch.int32, device=device) for _ in range(self.depth)]
+        self.works = [None] * self.depth
+        self.used = [False] * self.depth
+        self.n_steps = 0
+        self._select(0)
+
+    def _select(self, b: int):
+        self.send, self.all = self.sends[b], self.alls[b]
         self.counts = self.send[:8]
         self.buf = [self.send[8:8 + self.cap[0]], self.send[8 + self.cap[0]:]]
 
@@ -114,22 +132,46 @@ class DirtyGather:
         rank's values into its slots of the send buffer on the device (the GPU
         path: gpudiff_dbatch_export straight from HBM, ordered on the stream
         before the collective)."""
+        b = self.n_steps % self.depth
+        if self.works[b] is not None:  # the collective that last read this buffer
+            self.works[b].wait()
+            self.works[b] = None
+        self._select(b)
         fill_counts(self.counts)
         for col in (0, 1):
             fill_ids(col, self.buf[col])
-        self.dist.all_gather_into_tensor(self.all, self.send)
+        if self.depth > 1:
+            self.works[b] = self.dist.all_gather_into_tensor(self.all, self.send, async_op=True)
+        else:
+            self.dist.all_gather_into_tensor(self.all, self.send)
+        self.used[b] = True
+        self.n_steps += 1
+
+    def finish(self):
+        """Join every outstanding collective (the compute stream waits for them)."""
+        for b in range(self.depth):
+            if self.works[b] is not None:
+                self.works[b].wait()
+                self.works[b] = None
 
     def _rows(self):
         return self.all.view(self.world, self.width)
 
     def check(self):
-        """-> (ok, host count matrix [world, 8])"""
+        """-> (ok, host count matrix [world, 8] of the last step); ok only if no
+        rank exceeded its capacity in ANY pipelined buffer's last step."""
+        self.finish()
+        ok = True
+        for b in range(self.depth):
+            if self.used[b]:
+                c = self.alls[b].view(self.world, self.width)[:, :8].cpu()
+                ok = ok and bool((c[:, 0] <= self.cap[0]).all() and (c[:, 1] <= self.cap[1]).all())
         cc = self._rows()[:, :8].cpu()
-        ok = bool((cc[:, 0] <= self.cap[0]).all() and (cc[:, 1] <= self.cap[1]).all())
         return ok, cc
 
     def result(self):
-        """Node-wide (spec IDs, status IDs) in rank order (host sync; after the timed steps)."""
+        """Node-wide (spec IDs, status IDs) of the last step, in rank order
+        (host sync; after the timed steps)."""
         import torch
         ok, cc = self.check()
         if not ok:

@@ -44,7 +44,6 @@ def test_dirty_gather_over_rccl_world1():
         torch.cuda.synchronize()
         cap_s, cap_t = shard.DirtyGather.agree_capacity(counts, 1, dist)
         assert (cap_s, cap_t) == (want.spec_dirty_ids.size + 1, want.status_dirty_ids.size + 1)
-        g = shard.DirtyGather(1, cap_s, cap_t, dev, dist)
 
         def fill_counts(t):
             db.export(G.EXPORT_COUNTS, t.data_ptr(), 8)
@@ -52,13 +51,19 @@ def test_dirty_gather_over_rccl_world1():
         def fill_ids(col, buf):
             db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
                       buf.numel())
-        for _ in range(3):  # diff + collective, no host sync in between
-            eng.diff(db)
-            g.step(fill_counts, fill_ids)
-        torch.cuda.synchronize()
-        sa, ta = g.result()
-        assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
-        assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        for depth in (1, 2, 3):  # serial, and pipelined (step s's collective overlaps step s+1's diff)
+            g = shard.DirtyGather(1, cap_s, cap_t, dev, dist, depth=depth)
+            for _ in range(5):  # diff + collective, no host sync in between
+                eng.diff(db)
+                g.step(fill_counts, fill_ids)
+            g.finish()
+            torch.cuda.synchronize()
+            for b in range(depth):  # every buffer of the ring holds a full step's gather
+                rows = g.alls[b].view(1, g.width)
+                assert int(rows[0, 0]) == want.spec_dirty_ids.size and int(rows[0, 1]) == want.status_dirty_ids.size
+            sa, ta = g.result()
+            assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+            assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
         # the general (trimmed) form
         s2, t2 = shard.gather_dirty(counts, lambda col, buf, k: db.export(
             G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(), k), 0, 1, dist, dev)

@@ -120,7 +120,7 @@ def test_strong_scaling_shards_split_one_config(world):
     assert max(sizes) - min(sizes) <= cfg.n_pairs // world * 0.002
 
 
-def _worker_fixed(rank, world, port, flags_all, owners, shrink, q):
+def _worker_fixed(rank, world, port, flags_all, owners, shrink, q, depth=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -131,7 +131,7 @@ def _worker_fixed(rank, world, port, flags_all, owners, shrink, q):
     counts = torch.zeros(8, dtype=torch.int32)
     counts[0], counts[1] = spec.numel(), stat.numel()
     cs, ct = shard.DirtyGather.agree_capacity(counts, world, dist)
-    g = shard.DirtyGather(world, cs - shrink, ct, "cpu", dist)
+    g = shard.DirtyGather(world, cs - shrink, ct, "cpu", dist, depth=depth)
 
     def fill_counts(t):
         t.copy_(counts)
@@ -140,8 +140,9 @@ def _worker_fixed(rank, world, port, flags_all, owners, shrink, q):
         src = spec if col == 0 else stat
         k = min(buf.numel(), src.numel())
         buf[:k] = src[:k]
-    for _ in range(3):  # repeated steps reuse the buffers
+    for _ in range(3):  # repeated steps reuse the buffers (pipelined: round-robin over depth buffers)
         g.step(fill_counts, fill_ids)
+    g.finish()
     ok, _ = g.check()
     if ok:
         sa, ta = g.result()
@@ -151,8 +152,8 @@ def _worker_fixed(rank, world, port, flags_all, owners, shrink, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("shrink", [0, 5])
-def test_dirty_gather_fixed_capacity_gloo_world2(shrink):
+@pytest.mark.parametrize("shrink,depth", [(0, 1), (5, 1), (0, 2), (5, 2), (0, 3)])
+def test_dirty_gather_fixed_capacity_gloo_world2(shrink, depth):
     """The bench's per-step collective (shard.DirtyGather: no host sync, fixed
     capacity): node-wide dirty sets equal the single-rank view; a capacity
     below a rank's count is reported, never truncated silently."""
@@ -166,7 +167,7 @@ def test_dirty_gather_fixed_capacity_gloo_world2(shrink):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_fixed, args=(r, 2, port, flags, owners, shrink, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_fixed, args=(r, 2, port, flags, owners, shrink, q, depth)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
