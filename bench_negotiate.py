@@ -156,8 +156,7 @@ def run(args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_encode_docs<negotiate> (K13)",
                      "bytes_per_launch": alg, "avg_launch_ms": k13_ms, "launches_per_step": 1,
-                     "limiter": "issue (a wave's scalar scan/tree state machine per document, DESIGN.md 6e); "
-                                "the HBM fraction is informational"},
+                     "limiter": "issue/latency: a wave per document walks ~15 dependent lane-per-node phases (DESIGN.md 6e); the HBM fraction is informational, not the bound"},
         "kernels_ms": {"k13": k13_ms, "k14_classify": k14_ms},
         "device_only": {"pairs_per_s": N * args.steps / dt_dev, "ms_per_step": dt_dev / args.steps * 1e3,
                         "what": "K13 + K14 only; the deferred pairs' host path is outside this rate"},

@@ -124,7 +124,8 @@ def run(args):
                    "groups": len(got["groups"])},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_encode_docs<rollup> (K11)",
-                     "bytes_per_launch": alg, "avg_launch_ms": k11_ms, "launches_per_step": 1},
+                     "bytes_per_launch": alg, "avg_launch_ms": k11_ms, "launches_per_step": 1,
+                     "limiter": "issue/latency: a wave per document walks ~15 dependent lane-per-node phases (DESIGN.md 6d); the HBM fraction is informational, not the bound"},
         "kernels_ms": {"k11": k11_ms, "k12_group": k12_ms},
         "cpu_baseline": cpu,
         "checks": {"full_size": full, "sample": dict(docs=len(sdocs), bit_exact_vs_oracle=sample_ok)},

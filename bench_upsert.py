@@ -147,7 +147,8 @@ def run(args):
                    "device_docs": n_dev, "host_docs": int(res.n_host)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_encode_docs<marshal> (K10)",
-                     "bytes_per_launch": alg, "avg_launch_ms": k10_ms, "launches_per_step": 1},
+                     "bytes_per_launch": alg, "avg_launch_ms": k10_ms, "launches_per_step": 1,
+                     "limiter": "issue/latency: a wave per document walks ~15 dependent lane-per-node phases (DESIGN.md 6c); the HBM fraction is informational, not the bound"},
         "host_completion": {"docs": int(res.n_host), "fetch_s": t_host_docs,
                             "note": "deferred documents marshalled by the host path inside gpudiff_wbatch_fetch "
                                     "(the context's encode threads); fetch_s includes the D2H copy of all bodies"},
