@@ -114,6 +114,15 @@ int gpudiff_encode_objects(gpudiff_ctx* c, const uint8_t* const* docs, const siz
     return GPUDIFF_OK;
 }
 
+int gpudiff_k2_profile(gpudiff_ctx* c, uint64_t* dev_buf, uint32_t cap_waves) {
+    if (!c) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(k2_profile(dev_buf, cap_waves));
+    return GPUDIFF_OK;
+}
+
 int gpudiff_k0_profile(gpudiff_ctx* c, int enable, uint64_t* ticks8) {
     if (!c) return GPUDIFF_E_INVAL;
     int rc = set_device(c);

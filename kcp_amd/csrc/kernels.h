@@ -66,5 +66,8 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after);
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
+// tuning: K2 variant 14 writes 8 u64 per wave (start, first item end, items, last item start, end,
+// streaming ticks, join ticks, hw id) into dev_buf (cap_waves waves); nullptr disables
+hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves);
 
 }  // namespace gd

@@ -787,7 +787,13 @@ __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves
 // current item, so the launch ends when the work does, not when the wave with
 // the heaviest static share of items does; the last k2_tail_chunks() chunks are
 // handed out as 8-pair items, so the final round of items is short too.
-template <int U, int MINB, bool DYN = false>
+// K2 per-wave timeline (tuning variant 14 only, tools/k2_wave_profile.py): 8 u64 per wave --
+// start, end of the first item, items, start of the last item, end, streaming ticks, join ticks,
+// hardware id (wall clock: 100 MHz)
+__device__ uint64_t* g_k2_prof;
+__device__ uint32_t g_k2_prof_cap;
+
+template <int U, int MINB, bool DYN = false, bool PROF = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -805,6 +811,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
+    [[maybe_unused]] uint64_t tp_start = 0, tp_first = 0, tp_last = 0, tp_stream = 0, tp_join = 0, tp_items = 0;
+    if constexpr (PROF) tp_start = wall_clock64();
     const uint32_t nch = c_end - c_begin;
     const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift) : 0u;
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
@@ -813,6 +821,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     for (uint32_t it = wave, tk = 0; it < nitems; it = DYN ? uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves : it + nwaves) {
         if constexpr (DYN) {
             if (lane == 0) tk = atomicAdd(ctr, 1u);  // the next item; waited for only at the loop's end
+        }
+        [[maybe_unused]] uint64_t tp_i = 0;
+        if constexpr (PROF) {
+            tp_i = wall_clock64();
+            tp_last = tp_i;
+            tp_items++;
         }
         const bool tail = it >= n_full;
         const uint32_t ish = tail ? 3u : sub_shift;
@@ -855,6 +869,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         // chunk k of a pair: spec chunk at off + 16k (k < n1), status chunk at off + seg + 16 (k - n1)
         const uint32_t adj_a = seg_a - 16u * n1, adj_b = seg_b - 16u * n1;
         uint64_t mis_s = 0, mis_t = 0;  // pairs with a differing spec / status chunk (wave-uniform)
+        [[maybe_unused]] uint64_t tp_s0 = 0;
+        if constexpr (PROF) tp_s0 = wall_clock64();
         for (uint32_t base = 0; base < total; base += 64u * U) {
             u32x4 va[U], vb[U];
             uint32_t own[U];
@@ -889,6 +905,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     else mis_s |= bit;
                 }
             }
+        }
+        [[maybe_unused]] uint64_t tp_s1 = 0;
+        if constexpr (PROF) {
+            tp_s1 = wall_clock64();
+            tp_stream += tp_s1 - tp_s0;
         }
         // ---- decisions (compare_pair's rules)
         uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0, mynoop = 0;
@@ -942,6 +963,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 }
             }
         }
+        if constexpr (PROF) {
+            const uint64_t t = wall_clock64();
+            tp_join += t - tp_s1;
+            if (tp_items == 1) tp_first = t;
+        }
         const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
         if (valid) {
             flags[p0 + lane] = (uint8_t)myflag;
@@ -969,6 +995,26 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         }
     }
     if (deferred && lane == 0) summary[6] = 1u;
+    if constexpr (PROF) {
+        const uint64_t t_end = wall_clock64();
+        if (lane == 0 && g_k2_prof && wave < g_k2_prof_cap) {
+            uint64_t* r = g_k2_prof + 8ull * wave;
+            r[0] = tp_start;
+            r[1] = tp_first;
+            r[2] = tp_items;
+            r[3] = tp_last;
+            r[4] = t_end;
+            r[5] = tp_stream;
+            r[6] = tp_join;
+            r[7] = (uint64_t)__smid();
+        }
+    }
+}
+
+hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_k2_prof), &dev_buf, sizeof(dev_buf));
+    if (e != hipSuccess) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_k2_prof_cap), &cap_waves, sizeof(cap_waves));
 }
 
 // ---------------------------------------------------------------- K6
@@ -1096,7 +1142,7 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 12: return k_compare_flat<4, 5>;
         case 13: return k_compare<true, 4, 1>;  // round 1's default (wave per pair)
         case 10: return k_compare_flat<4, 4>;
-        case 14: return k_compare_flat<4, 1, true>;
+        case 14: return k_compare_flat<4, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
         case 15: return k_compare_flat<2, 1, true>;
         // 0: 111 VGPRs, 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than
         // static striding = variant 8 on config3, tools/ab_k2.py on MI355X)
