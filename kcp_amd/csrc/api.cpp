@@ -102,6 +102,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
         const uint32_t it = (c->flags >> GPUDIFF_OPT_K2_ITEMS_SHIFT) & 3u;
         b.k2_items_per_wave = it ? 2u << it : 0u;
     }
+    b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
     return b;
 }
 
@@ -381,7 +382,7 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
     uint4* cc = nullptr;
     if ((rc = dalloc(&d->pool, d->pool_cap)) || (rc = dalloc(&d->rows, np)) || (rc = dalloc(&d->pair_ids, np)) ||
         (rc = dalloc(&d->flags, np)) || (rc = dalloc(&d->caps, np)) || (rc = dalloc(&cc, nchunks)) ||
-        (rc = dalloc(&d->summary, 8 + kMaxSegments)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
+        (rc = dalloc(&d->summary, kSummaryWords)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
         (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
         (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) || (rc = dalloc(&d->nbits, np)) ||
@@ -565,7 +566,8 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         if (!ev) return GPUDIFF_E_DEVICE;
     }
     hipStream_t ms = c->stream;
-    HIPCHK(hipMemsetAsync(d->summary, 0, (8 + kMaxSegments) * sizeof(uint32_t), ms));  // + K2 item counters
+    static_assert(kMaxSegments <= kK2TailCounters, "K2 item counters per segment");
+    HIPCHK(hipMemsetAsync(d->summary, 0, kSummaryWords * sizeof(uint32_t), ms));  // + K2 item counters
     if (ev) HIPCHK(hipEventRecord(ev[0], ms));
     DiffBuffers b = buffers_of(c, d);
     const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);

@@ -765,8 +765,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // ---------------------------------------------------------------- K2, flattened stream
 // DYN variants: chunks at the end of a launch handed out as 8-pair items (about
 // four per wave), unless the whole launch is split already
-__host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift) {
-    return sub_shift >= 3u ? 0u : min(nch, nwaves / 2u);
+// tq: tail size in quarters of the launch's wave count (0 = the default, 2: half a chunk per wave)
+__host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t tq) {
+    return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * (tq ? tq : kK2TailQuarters));
 }
 
 // One wave per work item of P = 64 >> sub_shift consecutive pairs.  Lane k
@@ -803,10 +804,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                                                       uint32_t arena_per_wave, uint32_t arena_stride,
                                                       uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
                                                       uint8_t* __restrict__ nbits, uint64_t mask,
-                                                      uint32_t* __restrict__ summary, uint32_t sub_shift) {
+                                                      uint32_t* __restrict__ summary, uint32_t sub_arg) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t sub_shift = sub_arg & 0xFFu, tail_q = sub_arg >> 8;  // (launch_compare packs both)
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
@@ -814,13 +816,34 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     [[maybe_unused]] uint64_t tp_start = 0, tp_first = 0, tp_last = 0, tp_stream = 0, tp_join = 0, tp_items = 0;
     if constexpr (PROF) tp_start = wall_clock64();
     const uint32_t nch = c_end - c_begin;
-    const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift) : 0u;
+    const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
     const uint32_t nitems = n_full + (tail_c << 3);
+    // Two ticket counters per segment: main items are taken with a prefetch (the next main ticket as an
+    // item starts, waited for only at its end); tail items from their own counter only when a wave is
+    // free. With one counter a prefetch made as a long main item started could reserve a tail item,
+    // which then waited behind that item (and its joins) while every other wave had run out of work
+    // (the last ~0.13 ms of a 10M-pair pass, tools/k2_wave_profile.py).
     uint32_t* const ctr = summary + 8u + (arena_per_wave ? arena_off / arena_per_wave : 0u);
-    for (uint32_t it = wave, tk = 0; it < nitems; it = DYN ? uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves : it + nwaves) {
+    uint32_t* const ctr_tail = ctr + kK2TailCounters;
+    const uint32_t tail0 = max(n_full, nwaves);  // the first item the tail counter hands out
+    auto advance = [&](uint32_t cur, uint32_t tk) -> uint32_t {
+        if constexpr (!DYN) {
+            return cur + nwaves;
+        } else {
+            if (cur < n_full) {
+                const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
+                if (nx < n_full) return nx;
+            }
+            uint32_t tt = 0;
+            if (lane == 0) tt = atomicAdd(ctr_tail, 1u);
+            return tail0 + uni(__builtin_amdgcn_readlane(tt, 0));
+        }
+    };
+    for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
+        const bool tail = it >= n_full;
         if constexpr (DYN) {
-            if (lane == 0) tk = atomicAdd(ctr, 1u);  // the next item; waited for only at the loop's end
+            if (!tail && lane == 0) tk = atomicAdd(ctr, 1u);
         }
         [[maybe_unused]] uint64_t tp_i = 0;
         if constexpr (PROF) {
@@ -828,7 +851,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_last = tp_i;
             tp_items++;
         }
-        const bool tail = it >= n_full;
         const uint32_t ish = tail ? 3u : sub_shift;
         const uint32_t j = tail ? it - n_full : it;
         const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
@@ -1196,7 +1218,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     uint4* cc = (uint4*)b.chunk_counts;
     const uint32_t sub = k2_sub_shift(b, c1 - c0);
     const uint32_t v = b.k2_variant & 15u;
-    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub) : 0u;
+    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, b.k2_tail_quarters) : 0u;
     if (sub || tail) {  // split chunks accumulate their counts with atomics
         const uint32_t z0 = sub ? c0 : c1 - tail;
         hipError_t e = hipMemsetAsync(cc + z0, 0, (size_t)(c1 - z0) * sizeof(uint4), s);
@@ -1205,7 +1227,8 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
-               b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, sub
+               b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
+               sub | (k2_is_dyn(v) ? b.k2_tail_quarters << 8 : 0u)
     k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
