@@ -110,8 +110,10 @@ enum {
                                                 encodes (as GPUDIFF_STORE_DEVICE_ENCODE does for the store) */
 #define GPUDIFF_OPT_K0_VARIANT_SHIFT 26u /* 2 bits: K0 / K10 occupancy variant (0: 8 waves/SIMD, 1: unconstrained;
                                            K10 also 2: 5 waves, 3: 6 waves) */
-#define GPUDIFF_OPT_K2_TAIL_SHIFT 4u    /* 3 bits: decision-kernel tail of 8-pair items, in quarters of its
-                                           wave count (0: default 2) */
+#define GPUDIFF_OPT_K2_TAIL_SHIFT 4u    /* 3 bits t: decision-kernel tail of t - 1 quarters of its wave count
+                                           in 64-pair chunks (0: the default, 2 quarters; t = 1: no tail,
+                                           the last two rounds of tickets fetched late) */
+#define GPUDIFF_OPT_K2_TAIL8 0x80u      /* tuning: tail items of 8 pairs instead of half a main item */
 #define GPUDIFF_OPT_K2_ITEMS_SHIFT 28u   /* 2 bits: decision-kernel items per resident wave before 64-pair
                                             chunks are split (0: default 8, 1: 4, 2: 8, 3: 16) */
 

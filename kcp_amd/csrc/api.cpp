@@ -103,6 +103,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
         b.k2_items_per_wave = it ? 2u << it : 0u;
     }
     b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
+    b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
     return b;
 }
 

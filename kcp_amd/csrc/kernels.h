@@ -42,13 +42,17 @@ struct DiffBuffers {
     uint32_t k2_variant;        // tuning: 0 default = k_compare_flat, 4 x 16-B chunks in flight per lane per object
     uint32_t k2_items_per_wave; // tuning: 0 = default; 64-pair chunks split until each resident wave has this many items
     uint32_t k2_blocks_per_cu;  // tuning: 0 = the variant's occupancy (4 resident 256-thread blocks per CU)
-    uint32_t k2_tail_quarters;  // tuning: 8-pair tail of (this many / 4) x the launch's waves chunks; 0 = default
+    uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default
+    uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
 };
 
 // summary[8 + seg]: K2's main item counter of segment seg; summary[8 + kK2TailCounters + seg]: its tail
 // item counter (zeroed with the pass)
 constexpr uint32_t kK2TailCounters = 8, kSummaryWords = 8 + 2 * kK2TailCounters;
-constexpr uint32_t kK2TailQuarters = 2;  // default tail: half a 64-pair chunk per resident wave
+// default tail: half a chunk per resident wave, in items of half a main item (in-process A/B on MI355X,
+// profiles/r02zj-r02zm: 8-pair tail items cost more than the imbalance they remove; with no tail at all
+// the main items' tickets are fetched late in the last two rounds instead)
+constexpr uint32_t kK2TailQuarters = 2;
 
 // waves of a K2 launch over nchunks 64-pair chunks (sizes the wave arenas)
 uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks);

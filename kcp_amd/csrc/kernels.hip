@@ -765,9 +765,13 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // ---------------------------------------------------------------- K2, flattened stream
 // DYN variants: chunks at the end of a launch handed out as 8-pair items (about
 // four per wave), unless the whole launch is split already
-// tq: tail size in quarters of the launch's wave count (0 = the default, 2: half a chunk per wave)
-__host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t tq) {
-    return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * (tq ? tq : kK2TailQuarters));
+// a tail of q quarters of the launch's wave count, in 64-pair chunks
+__host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t q) {
+    return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * q);
+}
+// the tail quarters a launch uses (GPUDIFF_OPT_K2_TAIL_SHIFT: 0 = default, else t - 1)
+static inline uint32_t k2_tail_q(const DiffBuffers& b) {
+    return b.k2_tail_quarters ? b.k2_tail_quarters - 1u : kK2TailQuarters;
 }
 
 // One wave per work item of P = 64 >> sub_shift consecutive pairs.  Lane k
@@ -808,7 +812,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t sub_shift = sub_arg & 0xFFu, tail_q = sub_arg >> 8;  // (launch_compare packs both)
+    // (launch_compare packs: sub_shift | tail quarters << 8 | late fetch << 16)
+    const uint32_t sub_shift = sub_arg & 0xFFu, tail_q = (sub_arg >> 8) & 0xFFu;
+    const bool late = (sub_arg >> 16) & 1u;
+    const uint32_t tail_ish = ((sub_arg >> 17) & 1u) ? 3u : min(sub_shift + 1u, 3u);  // tail items: half or 8 pairs
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
@@ -818,7 +825,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     const uint32_t nch = c_end - c_begin;
     const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
-    const uint32_t nitems = n_full + (tail_c << 3);
+    const uint32_t nitems = n_full + (tail_c << tail_ish);
     // Two ticket counters per segment: main items are taken with a prefetch (the next main ticket as an
     // item starts, waited for only at its end); tail items from their own counter only when a wave is
     // free. With one counter a prefetch made as a long main item started could reserve a tail item,
@@ -827,11 +834,15 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     uint32_t* const ctr = summary + 8u + (arena_per_wave ? arena_off / arena_per_wave : 0u);
     uint32_t* const ctr_tail = ctr + kK2TailCounters;
     const uint32_t tail0 = max(n_full, nwaves);  // the first item the tail counter hands out
+    // late fetch: the last two rounds of main items take their next ticket when they are done, so
+    // no ticket waits behind a long item at the end of the pass (the others prefetch as they start)
+    const uint32_t pf_end = late ? (n_full > 2u * nwaves ? n_full - 2u * nwaves : 0u) : n_full;
     auto advance = [&](uint32_t cur, uint32_t tk) -> uint32_t {
         if constexpr (!DYN) {
             return cur + nwaves;
         } else {
             if (cur < n_full) {
+                if (cur >= pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
                 const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
                 if (nx < n_full) return nx;
             }
@@ -843,7 +854,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
         const bool tail = it >= n_full;
         if constexpr (DYN) {
-            if (!tail && lane == 0) tk = atomicAdd(ctr, 1u);
+            if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
         }
         [[maybe_unused]] uint64_t tp_i = 0;
         if constexpr (PROF) {
@@ -851,7 +862,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_last = tp_i;
             tp_items++;
         }
-        const uint32_t ish = tail ? 3u : sub_shift;
+        const uint32_t ish = tail ? tail_ish : sub_shift;
         const uint32_t j = tail ? it - n_full : it;
         const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
         const uint32_t per = 64u >> ish;
@@ -1218,7 +1229,8 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     uint4* cc = (uint4*)b.chunk_counts;
     const uint32_t sub = k2_sub_shift(b, c1 - c0);
     const uint32_t v = b.k2_variant & 15u;
-    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, b.k2_tail_quarters) : 0u;
+    const uint32_t tq = k2_tail_q(b);
+    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq) : 0u;
     if (sub || tail) {  // split chunks accumulate their counts with atomics
         const uint32_t z0 = sub ? c0 : c1 - tail;
         hipError_t e = hipMemsetAsync(cc + z0, 0, (size_t)(c1 - z0) * sizeof(uint4), s);
@@ -1228,7 +1240,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
-               sub | (k2_is_dyn(v) ? b.k2_tail_quarters << 8 : 0u)
+               sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u)
     k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
