@@ -36,8 +36,8 @@ for on in (False, True):
     dt = time.time() - t
     prof = eng.k0_profile(False)
     print("profile=%s: %.2f ms per launch, %d host-completed" % (on, dt * 1e3, r.n_host))
-names = ["scan", "tree", "M1 sizes", "M2-M5", "M6-M8", "M9 emit"]
-tot = sum(prof[:6])
+names = ["scan", "tree", "M1 sizes", "M5 ranks+depth sort", "M6-M8", "M9 emit", "M1 floats", "M2-M4"]
+tot = sum(prof[:8])
 for k, nm in enumerate(names):
     print("  %-9s %6.1f%%  %.2f us/doc-wave" % (nm, 100.0 * prof[k] / max(1, tot), prof[k] / 100.0 / n))
 # per-kind launch times
