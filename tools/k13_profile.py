@@ -26,8 +26,9 @@ for on in (False, True):
     dt = time.time() - t
     prof = eng.k0_profile(False)
     print("profile=%s: K13+K14 %.2f ms for %d docs" % (on, dt * 1e3, n))
-tot = sum(prof[:3])
-for k, nm in enumerate(["scan", "tree", "N0-N4"]):
-    print("  %-6s %6.1f%%  %.2f us/doc-wave" % (nm, 100.0 * prof[k] / max(1, tot), prof[k] / 100.0 / n))
+tot = sum(prof[:7])
+for k, nm in [(0, "scan"), (1, "tree"), (3, "N0 atoms/escapes"), (4, "N1 root members"), (5, "N2 metadata/conds"),
+              (6, "N3 maps/elements"), (2, "N4 cond fields+out")]:
+    print("  %-18s %6.1f%%  %.2f us/doc-wave" % (nm, 100.0 * prof[k] / max(1, tot), prof[k] / 100.0 / n))
 nb.close()
 eng.close()
