@@ -159,3 +159,30 @@ def test_crd_long_lists_defer():
     st = _check_kinds(eng, pairs, G.NEG_KIND_CRD)
     assert st.n_host == 2
     eng.close()
+
+
+def _reorder_root(doc: bytes, rng) -> bytes:
+    """The same object with its root members in another order, plus decoy "metadata" / "status"
+    members nested in spec (only the root's count): the passes after N1 / R1 look inside the
+    metadata and status subtrees by their pre-order ranges, which this moves around."""
+    import json
+    o = json.loads(doc)
+    if isinstance(o.get("spec"), dict):
+        o["spec"]["metadata"] = {"labels": {"kcp.dev/owned-by": "decoy"}, "resourceVersion": "9"}
+        o["spec"]["status"] = {"conditions": [{"type": "Decoy", "status": "True"}], "replicas": 99}
+    keys = list(o)
+    rng.shuffle(keys)
+    if rng.random() < 0.5 and "status" in keys:  # status first / metadata last at times
+        keys.remove("status")
+        keys.insert(0, "status")
+    return json.dumps({k: o[k] for k in keys}, separators=(",", ":")).encode()
+
+
+def test_root_member_order_and_decoys():
+    import random
+    rng = random.Random(77)
+    eng = G.Engine(device=0)
+    pairs, _ = S.negotiate_population(600, seed=78)
+    moved = [(_reorder_root(a, rng), _reorder_root(b, rng)) for a, b in pairs]
+    _check(eng, moved)
+    eng.close()

@@ -252,3 +252,14 @@ def test_k2_variants_bit_exact(variant):
         assert_matches(e.diff_pairs(pairs), pairs)
         assert_matches(e.diff_pairs(deep), deep)
         e.close()
+
+
+@pytest.mark.parametrize("tail_flags", [0x10, 0x50, 0x80, 0x10 | (1 << 28)], ids=["no_tail_late", "tail4q", "tail8", "no_tail_ipw4"])
+def test_k2_tail_tunings_bit_exact(tail_flags):
+    """K2's work hand-out variants (GPUDIFF_OPT_K2_TAIL_SHIFT / _K2_TAIL8 / items per wave): main and
+    tail tickets, late fetch, 8-pair or half-size tail items -- identical results, against the oracle."""
+    pairs, _, _ = make_pairs(6000, seed=33, mutate_frac=0.2, pretty_frac=0)
+    e = G.Engine(device=0, flags=tail_flags)
+    res = e.diff_pairs(pairs)
+    assert_matches(res, pairs)
+    e.close()

@@ -104,3 +104,17 @@ def test_empty_and_single():
     _check(eng, [C.dep({C.O: "r"}, {"replicas": 3})])
     _check(eng, [b"{}"])
     eng.close()
+
+
+def test_root_member_order_and_decoys():
+    """Root members reordered (status first, metadata last at times) and decoy metadata / status
+    objects nested in spec: R2/R3 look only inside the root's metadata and status subtrees."""
+    import random
+
+    from tests.test_gpu_negotiate import _reorder_root
+    rng = random.Random(79)
+    docs, _ = S.rollup_population(200, 4, seed=80)
+    eng = G.Engine(device=0)
+    res = _check(eng, [_reorder_root(d, rng) for d in docs])
+    assert res.n_host < len(docs) // 10  # clean API-server JSON: decided on the device
+    eng.close()
