@@ -70,7 +70,7 @@ def run(args):
     exp_ab = pop.expected_flags(truth)  # decisions of A -> B (and, by symmetry, of B -> A)
     cluster = np.arange(M, dtype=np.uint32) % np.uint32(cfg.n_clusters)
 
-    eng = G.Engine(device=0, encode_threads=threads, timing=True)
+    eng = G.Engine(device=0, encode_threads=threads, timing=True, flags=args.engine_flags)
     per_obj = float(lens.mean()) * 2.2 + 256  # blob + path table ~= 2x the JSON
     space = int(per_obj * M * 2.5) + (B * int(per_obj) * 4) + (256 << 20)
     dev_enc = args.encode == "device"

@@ -1190,8 +1190,9 @@ static bool k2_is_dyn(uint32_t variant) {
     }
 }
 
+constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
-constexpr uint32_t kK2ItemsPerWave = 8;  // A/B at the N = 8 shard size (1.25M pairs): 8 beats 4 by 1.5%, 16 loses 8%
+constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
 
 static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     // one resident 256-thread block per CU per wave slot a SIMD offers the
@@ -1213,8 +1214,11 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
 // wave (config3's 156k chunks: k = 0; config4's 1.6k chunks of deep pairs: k = 4)
 static uint32_t k2_sub_shift(const DiffBuffers& b, uint32_t nchunks) {
     const uint64_t want = (uint64_t)(b.k2_items_per_wave ? b.k2_items_per_wave : kK2ItemsPerWave) * 4u * k2_cap_blocks(b);
+    // items of at least 8 pairs: a small batch (a watch-replay batch of 64k events: 1k chunks) split
+    // further than that pays a row load, a prefix sum and a ticket per 2-4 pairs (config5: K2 0.42 ms
+    // at 2-pair items vs 0.26 at 4 -- profiles/r02zy)
     uint32_t k = 0;
-    while (k < 6 && (uint64_t)nchunks << k < want) k++;
+    while (k < kK2MaxSubShift && (uint64_t)nchunks << k < want) k++;
     return k;
 }
 
