@@ -9,8 +9,10 @@ usage: python tools/ab_k2.py [--pairs N] [--rounds R] [--variants name=flags,...
               5 NT x4 <=80 VGPRs, 6 NT x2 <=64 VGPRs, 7 NT x2 <=80 VGPRs, 13 = round 1's default;
               flattened stream, static items: 8 x4, 9 x2, 10 x4 <= 128 VGPRs, 11 x2 5 waves/SIMD,
               12 x4 5 waves/SIMD; dynamic items + 8-pair tail: 0 = 14 x4 (the default), 15 x2),
-              12-15 K2 blocks/CU (0 = default 5), 16-19 forced segments,
-              0x100000 no alternate K2 stream
+              12-15 K2 blocks/CU (0 = the measured occupancy), 16-19 forced segments,
+              0x100000 no alternate K2 stream, 4-6 tail t (t - 1 quarters of the waves in chunks; 0 = default 2,
+              1 = no tail + late tickets), 0x80 8-pair tail items, 28-29 items per wave (0 = 6, 1: 4, 2: 8, 3: 16);
+              variant 14 = the default kernel + per-wave timeline (tools/k2_wave_profile.py)
 """
 import argparse
 import json
