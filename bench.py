@@ -16,7 +16,9 @@ in HBM before timing.
 A step = one diff pass of the hot path (K2 compare + fused merge-join, K3
 compaction, K4 deferred joins, K5/K6 path emit) over the rank's resident
 pairs, plus (N > 1) the RCCL all-gather of per-rank dirty counts and dirty
-pair IDs (shard.DirtyGather: preallocated, no host sync in the step).
+pair IDs (shard.DirtyGather: one all-gather into preallocated buffers; the
+gathered counts are read back after it and a capacity overflow is regrown and
+re-gathered inside the step).
 
 Beside the timed line (rank 0, N = 1): the roofline on both byte definitions
 (this build's format bytes, and SURVEY.md §8(d)'s B_pair = sum(24 L + V + 8) +
@@ -25,8 +27,10 @@ baselines on all host cores (the C++ tree-walk restatement of the predicates
 and the CPU merge over the CSR encoding) and a three-way parity check of
 decisions and changed paths (GPU, tree-walk, CSR merge) on the CPU sample.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU).  Rank 0 prints one JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 either
+under torch.distributed.run (one process per GPU; WORLD_SIZE must equal N) or
+bare, in which case bench.py starts that launch itself as a child process and
+relays rank 0's line.  Rank 0 prints one JSON line.
 """
 import argparse
 import hashlib
@@ -57,6 +61,12 @@ def k2_source_hash():
         with open(os.path.join(ROOT, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+def cpu_threads(aff, quota):
+    """CPU-baseline threads: min(affinity, ceil(cgroup quota)) -- the cores the process can run at once."""
+    import math
+    return max(1, min(aff, math.ceil(quota))) if quota else aff
 
 
 def free_port():
@@ -92,8 +102,38 @@ def claim_stdout():
     sys.stdout = os.fdopen(fd, "w", buffering=1)
 
 
+def launch_cmd(gpus, argv):
+    """The one-process-per-GPU launch of this same command line (torch.distributed.run, rendezvous on
+    127.0.0.1): what `bench.py --gpus N` runs as a child when no launcher started it."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % gpus,
+            "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + list(argv)
+
+
+def self_launch(args, argv):
+    """--gpus N > 1 without a launcher (no WORLD_SIZE): start the N ranks as a CHILD process before
+    anything touches the GPU, relay rank 0's JSON line (inherited stdout) and exit with the child's
+    code.  A launcher whose world size differs from --gpus is an error, never a silent 1-GPU run."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            log("error: --gpus %d but WORLD_SIZE %s" % (args.gpus, world))
+            sys.exit(2)
+        return
+    if args.gpus <= 1 and not args.print_launch:
+        return
+    cmd = launch_cmd(args.gpus, [a for a in argv if a != "--print-launch"])
+    if args.print_launch:
+        print(json.dumps({"launch": cmd, "world_size": args.gpus}), flush=True)
+        sys.exit(0)
+    import subprocess
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main():
-    claim_stdout()
+    argv = sys.argv[1:]
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -139,7 +179,14 @@ def main():
                     help="PMC traffic summary to attach as roofline.traffic (default: the newest committed "
                          "profiles/**/pmc_summary.json, used only if it was measured on this workload with the "
                          "same K2 sources; 'none' to skip)")
-    args = ap.parse_args()
+    ap.add_argument("--print-launch", action="store_true",
+                    help="print the launch command --gpus N resolves to (one process per GPU) and exit")
+    args = ap.parse_args(argv)
+    self_launch(args, argv)
+    claim_stdout()
+    if args.gpus > 1 and args.config not in ("config1", "config2", "config3", "config4"):
+        log("error: --config %s is a one-GPU side bench" % args.config)
+        sys.exit(2)
 
     if args.config == "upsert":
         import bench_upsert
@@ -163,8 +210,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     scaling = args.scaling if args.scaling != "auto" else ("strong" if world > 1 else "weak")
 
     import torch
@@ -295,7 +340,7 @@ def main():
         gather_check = dict(capacity_ok=ok, node_spec_dirty=int(cc[:, 0].sum()), node_status_dirty=int(cc[:, 1].sum()),
                             gathered_spec=None if sa is None else int(sa.numel()),
                             gathered_status=None if ta is None else int(ta.numel()),
-                            depth=gather.depth, bytes_per_rank=4 * gather.width)
+                            depth=gather.depth, bytes_per_rank=4 * gather.width, regrows=gather.n_regrows)
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -455,11 +500,17 @@ def cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota):
     from oracle import cpu_ref
     idx = np.unique(np.linspace(0, n - 1, min(args.cpu_sample, n)).astype(np.int64))
     pairs = [pop.json_pair(int(i)) for i in idx]
-    threads = aff
+    # the cores this process may actually use: affinity, capped by the cgroup CPU quota (more threads than
+    # the quota only time-slice and understate the baseline); the all-affinity figure is printed beside it
+    threads = cpu_threads(aff, quota)
     dp = cpu_ref.DecodedPairs(pairs)
     dp.decide(threads=threads)  # warm: first-touch page faults, thread start-up
     cflags, sweeps, sec = dp.decide(threads=threads, min_seconds=args.cpu_seconds)
     _, sweeps1, sec1 = dp.decide(threads=1, min_seconds=args.cpu_seconds / 3)
+    aff_rate = None
+    if aff > threads:
+        _, swa, seca = dp.decide(threads=aff, min_seconds=args.cpu_seconds / 3)
+        aff_rate = len(idx) * swa / seca
     hb = eng.encode(pairs)
     rows = hb.rows()
     csr = cpu_ref.CsrPairs(hb.pool(), rows)
@@ -473,6 +524,7 @@ def cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota):
                       "statussyncer.go:15-27" % (
                           len(idx), max(1, n // len(idx)), sweeps, sec),
                one_core=len(idx) * sweeps1 / sec1, nproc=nproc, affinity_cpus=aff, cgroup_cpu_quota=quota,
+               all_affinity_threads=None if aff_rate is None else dict(value=aff_rate, threads=aff),
                cpu_csr=dict(value=csr_rate, unit="pairs/s", cores=threads, one_core=len(idx) * csw1 / csec1,
                             what="the build's CPU merge over the canonical CSR encoding (oracle/csr_ref.cpp), "
                                  "decisions + changed paths"))

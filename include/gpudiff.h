@@ -61,7 +61,8 @@ enum {
  * syncer issues for the decision would not change what the predicate compares, so the API call can
  * be skipped.  GPUDIFF_SPEC_NOOP: every changed spec leaf is an int64 v on one side and a float64
  * == v (|v| <= 2^53) on the other -- Go's json.Marshal writes both as the same digits and the API
- * server decodes them back to int64 v, so A's body over B leaves B's compared content as it is.
+ * server decodes them back to int64 v, so the two documents' bodies agree on the wire in that
+ * region (gpudiff_write_plan_get_ex says what that means for informer and for (A, B) pairs).
  * GPUDIFF_STATUS_NOOP: the same for the status leaves, and when B has no status key, A has none
  * either (UpdateStatus would write nothing). */
 #define GPUDIFF_SPEC_NOOP 0x8u
@@ -268,9 +269,13 @@ int gpudiff_submit(gpudiff_ctx* ctx, const gpudiff_json_pair* pairs, size_t n,
  * resident version -- UpdateFunc(old, new), specsyncer.go:47-51 and
  * statussyncer.go:32-36 -- and the new version becomes the resident one.
  * Events of one batch apply in order, so two events on one slot chain.
- * Exactness: the host keeps a second, independent 64-bit hash of every
- * resident path; a path-hash collision between versions (or within the new
- * one) re-encodes the pair with a fresh seed from old_json.  Blobs are
+ * Exactness: every resident blob carries a path table (one entry per region
+ * leaf and ancestor: its hash, its parent's hash, its last component;
+ * include/gpudiff_format.h); a new version's table must agree
+ * with the resident one, which makes every shared path hash name the same path
+ * in both.  A disagreement (a path-hash collision between versions, or within
+ * the new one) re-encodes the pair with the smallest valid seed from old_json
+ * (dirty with GPUDIFF_DECODE_ERROR when old_json is absent).  Blobs are
  * appended to the current space and the live ones are packed into the other
  * space (K7 k_move_blobs) when it fills. */
 typedef struct gpudiff_store gpudiff_store;
@@ -404,16 +409,35 @@ void gpudiff_bodies_release(gpudiff_ctx* ctx, gpudiff_bodies* b);
 /* Gate -> write on the device.  For a
  * batch submitted with GPUDIFF_OPT_DEVICE_ENCODE and waited (gpudiff_wait), the
  * writes the syncer issues for its decisions, rendered by K10 from the pairs'
- * JSON still staged in HBM -- no re-upload:
- *   every spec-dirty pair: upsertIntoDownstream's body of A (GPUDIFF_UPSERT_SPEC,
- *     pkg/syncer/specsyncer.go:86-132), written over the downstream copy B;
- *   every status-dirty pair: updateStatusInUpstream's body of B
- *     (GPUDIFF_UPSERT_STATUS, statussyncer.go:41-63), written into A.
+ * JSON still staged in HBM -- no re-upload.  Which document a write renders
+ * depends on what the submitted pairs are (`mode` of gpudiff_write_plan_get_ex):
+ *   GPUDIFF_PLAN_INFORMER (default): each pair is an informer Update event
+ *     (old, new).  UpdateFunc enqueues newObj (specsyncer.go:47-50,
+ *     statussyncer.go:32-35) and the worker writes that object, so both kinds
+ *     render the NEW document: a spec-dirty pair gets upsertIntoDownstream's
+ *     body of new (GPUDIFF_UPSERT_SPEC, specsyncer.go:86-132), a status-dirty
+ *     pair updateStatusInUpstream's body of new (GPUDIFF_UPSERT_STATUS,
+ *     statussyncer.go:41-63).
+ *   GPUDIFF_PLAN_UPSTREAM_DOWNSTREAM: each pair is (A = upstream/kcp copy,
+ *     B = downstream copy): a spec-dirty pair gets the spec body
+ *     of A (written over B), a status-dirty pair the status body of B (written
+ *     into A).
+ * GPUDIFF_PLAN_SPEC / GPUDIFF_PLAN_STATUS select which kinds are listed (an
+ * upstream informer's batch wants spec writes only, a downstream informer's
+ * status writes only); neither bit = both.
  * A write whose pair carries GPUDIFF_SPEC_NOOP / GPUDIFF_STATUS_NOOP is listed
- * with noop = 1 and no body: the call can be skipped.  Call after gpudiff_wait
- * on the ticket and before the submit after the next one (the staging is
- * reused then); GPUDIFF_E_STATE otherwise, or for a batch the context encoded
- * on the host.  Release with gpudiff_write_plan_release. */
+ * with noop = 1 and no body: what the write carries in that region is, on the
+ * wire, exactly what the write of the other document of the pair carries (Go
+ * marshals int64 v and float64 v the same way).  For informer pairs that means
+ * the call repeats the write already issued for `old`; for (A, B) pairs it
+ * leaves B's compared content as it is.  Call after gpudiff_wait on the ticket
+ * and before the submit after the next one (the staging is reused then);
+ * GPUDIFF_E_STATE otherwise, or for a batch the context encoded on the host.
+ * Release with gpudiff_write_plan_release. */
+#define GPUDIFF_PLAN_INFORMER 0x0u
+#define GPUDIFF_PLAN_SPEC 0x1u
+#define GPUDIFF_PLAN_STATUS 0x2u
+#define GPUDIFF_PLAN_UPSTREAM_DOWNSTREAM 0x4u
 typedef struct gpudiff_write_plan {
     size_t n;                    /* writes: the spec-dirty pairs (ascending index), then the status-dirty ones */
     const uint32_t* pair_index;  /* the pair's index in the submitted batch */
@@ -422,7 +446,8 @@ typedef struct gpudiff_write_plan {
     gpudiff_bodies bodies;       /* n bodies (empty for no-op writes; status GPUDIFF_E_DECODE = undecodable) */
     void* internal;
 } gpudiff_write_plan;
-int gpudiff_write_plan_get(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_write_plan* out);
+int gpudiff_write_plan_get(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_write_plan* out); /* = _ex(..., 0, ...) */
+int gpudiff_write_plan_get_ex(gpudiff_ctx* ctx, gpudiff_ticket ticket, uint32_t mode, gpudiff_write_plan* out);
 void gpudiff_write_plan_release(gpudiff_ctx* ctx, gpudiff_write_plan* p);
 
 /* The staged form: documents uploaded once into HBM (gpudiff_wbatch_create),

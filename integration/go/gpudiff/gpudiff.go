@@ -15,10 +15,14 @@ package gpudiff
 import "C"
 
 import (
+	"bytes"
 	"errors"
 	"fmt"
+	"math"
+	"strconv"
 	"sync"
 	"time"
+	"unicode/utf8"
 	"unsafe"
 
 	"k8s.io/apimachinery/pkg/apis/meta/v1/unstructured"
@@ -66,16 +70,143 @@ func (e *Engine) Close() {
 	}
 }
 
+// jsonOf renders an informer object as the JSON text the engine decodes.
+//
+// Marker contract.  The engine reads numbers with k8s util/json's rule (an integer literal ->
+// int64, a literal with a fraction or an exponent -> float64), and the predicates compare Go
+// dynamic types (equality.Semantic.DeepEqual: int64(3) != float64(3), specsyncer.go:36;
+// SURVEY.md A.4 rows 7/8/25/26).  u.MarshalJSON cannot be used: encoding/json writes
+// float64(3) as "3" and float64(-0) as "-0", which the engine reads back as int64 -- an
+// int64-vs-float64 difference would come out "equal".  appendValue writes instead:
+//
+//	int64                  decimal digits, never a '.', 'e' or 'E'
+//	float64                shortest round-trip digits (strconv 'g', -1) that always carry a '.'
+//	                       or an exponent: 3 -> "3.0", -0 -> "-0.0", 1e21 -> "1e+21";
+//	                       NaN / Inf -> not transferable
+//	string, map key        a JSON string whose decoded bytes are the Go string's bytes
+//	                       (only '"', '\\' and bytes < 0x20 escaped); a string that is not
+//	                       valid UTF-8 -> not transferable (the decoder would fold it to U+FFFD)
+//	bool, nil              true / false / null
+//	map[string]interface{} an object (Go's iteration order: the engine's encoding is canonical)
+//	[]interface{}          an array
+//	anything else          not transferable: int, int32, float32, json.Number, structs ... never
+//	                       come out of the informer's JSON decode, DeepEqual tells them apart from
+//	                       int64/float64 by type, so no JSON text can stand for them
+//	nesting deeper than 10000 containers: not transferable (encoding/json's limit)
+//
+// A not-transferable object gives ok = false, which every caller treats as "differs" -- the
+// reference's rule for a failed type assertion (specsyncer.go:20-22) -- so the transfer can
+// cost an unnecessary enqueue, never a false "equal".  tests/goshim.py restates this function
+// and tests/test_gpu_goshim.py runs every known-answer and golden pair through that restatement
+// and the C-ABI against the oracle.  It is also cheaper than MarshalJSON on the informer path: no
+// reflection, no key sort and no HTML escaping.
 func jsonOf(obj interface{}) ([]byte, bool) {
 	u, ok := obj.(*unstructured.Unstructured)
 	if !ok || u == nil {
 		return nil, false
 	}
-	b, err := u.MarshalJSON()
-	if err != nil {
-		return nil, false
+	var m interface{} = u.Object
+	if u.Object == nil {
+		m = map[string]interface{}{}
 	}
-	return b, true
+	return appendValue(make([]byte, 0, 2048), m, 0)
+}
+
+const maxNesting = 10000 // encoding/json scanner maxNestingDepth
+
+func appendValue(buf []byte, v interface{}, depth int) ([]byte, bool) {
+	switch x := v.(type) {
+	case nil:
+		return append(buf, "null"...), true
+	case bool:
+		if x {
+			return append(buf, "true"...), true
+		}
+		return append(buf, "false"...), true
+	case int64:
+		return strconv.AppendInt(buf, x, 10), true
+	case float64:
+		if math.IsNaN(x) || math.IsInf(x, 0) {
+			return buf, false
+		}
+		start := len(buf)
+		buf = strconv.AppendFloat(buf, x, 'g', -1, 64)
+		if bytes.IndexAny(buf[start:], ".eE") < 0 {
+			buf = append(buf, '.', '0')
+		}
+		return buf, true
+	case string:
+		return appendString(buf, x)
+	case map[string]interface{}:
+		if depth+1 > maxNesting {
+			return buf, false
+		}
+		buf = append(buf, '{')
+		first := true
+		for k, e := range x {
+			if !first {
+				buf = append(buf, ',')
+			}
+			first = false
+			var ok bool
+			if buf, ok = appendString(buf, k); !ok {
+				return buf, false
+			}
+			buf = append(buf, ':')
+			if buf, ok = appendValue(buf, e, depth+1); !ok {
+				return buf, false
+			}
+		}
+		return append(buf, '}'), true
+	case []interface{}:
+		if depth+1 > maxNesting {
+			return buf, false
+		}
+		buf = append(buf, '[')
+		for i, e := range x {
+			if i > 0 {
+				buf = append(buf, ',')
+			}
+			var ok bool
+			if buf, ok = appendValue(buf, e, depth+1); !ok {
+				return buf, false
+			}
+		}
+		return append(buf, ']'), true
+	}
+	return buf, false
+}
+
+const hexDigits = "0123456789abcdef"
+
+func appendString(buf []byte, s string) ([]byte, bool) {
+	if !utf8.ValidString(s) {
+		return buf, false
+	}
+	buf = append(buf, '"')
+	start := 0
+	for i := 0; i < len(s); i++ {
+		c := s[i]
+		if c >= 0x20 && c != '"' && c != '\\' {
+			continue
+		}
+		buf = append(buf, s[start:i]...)
+		switch c {
+		case '"', '\\':
+			buf = append(buf, '\\', c)
+		case '\n':
+			buf = append(buf, '\\', 'n')
+		case '\r':
+			buf = append(buf, '\\', 'r')
+		case '\t':
+			buf = append(buf, '\\', 't')
+		default:
+			buf = append(buf, '\\', 'u', '0', '0', hexDigits[c>>4], hexDigits[c&15])
+		}
+		start = i + 1
+	}
+	buf = append(buf, s[start:]...)
+	return append(buf, '"'), true
 }
 
 func cbytes(b []byte) (*C.uint8_t, C.size_t) {
@@ -412,25 +543,43 @@ func (e *Engine) UpsertBodies(objs []interface{}, mode Mode) ([][]byte, error) {
 // OptDeviceEncode opens an engine whose submits send raw JSON to the GPU (kernel K0); DiffAndPlan needs it.
 const OptDeviceEncode = uint32(C.GPUDIFF_OPT_DEVICE_ENCODE)
 
-// Write is one API call the syncer's decisions imply (gpudiff_write_plan_get): for a spec-dirty pair
-// upsertIntoDownstream's body of the upstream object A, written over the downstream copy B
-// (specsyncer.go:86-132); for a status-dirty pair updateStatusInUpstream's body of B, written into A
-// (statussyncer.go:41-63).
+// Write is one API call the syncer's decisions imply (gpudiff_write_plan_get_ex).  For informer
+// pairs (PlanInformer) both kinds render the NEW object -- UpdateFunc enqueues newObj
+// (specsyncer.go:47-50, statussyncer.go:32-35) and the worker writes it: a spec write is
+// upsertIntoDownstream's body (specsyncer.go:86-132), a status write updateStatusInUpstream's
+// (statussyncer.go:41-63).  For (upstream A, downstream B) pairs (PlanUpstreamDownstream) the spec
+// write renders A and the status write B.
 type Write struct {
 	Pair int    // index into the olds / news given to DiffAndPlan
 	Kind Mode   // UpsertSpec or UpsertStatus
-	Noop bool   // the write changes nothing the predicates compare (GPUDIFF_SPEC_NOOP / _STATUS_NOOP): skip the call
+	Noop bool   // the body equals the other document's on the wire in that region (GPUDIFF_SPEC_NOOP / _STATUS_NOOP)
 	Body []byte // the request body; nil for a no-op, or when Go cannot decode the object (reference path)
 }
 
-// DiffAndPlan decides n (old, new) pairs on the device and renders the writes those decisions imply from
-// the JSON still staged in HBM (kernel K10, no second upload): flags[i] are the pair's GPUDIFF_* result
-// bits, writes list the spec writes (ascending pair) then the status writes.  The engine must have been
-// opened with OptDeviceEncode.  The caller issues each non-no-op write as today (Create, then Update with
-// the live resourceVersion on AlreadyExists, specsyncer.go:110-129).
+// Plan modes (GPUDIFF_PLAN_*): which writes DiffAndPlanMode lists and which document they render.
+const (
+	PlanInformer           = uint32(C.GPUDIFF_PLAN_INFORMER)            // pairs are (old, new) events; both kinds
+	PlanSpec               = uint32(C.GPUDIFF_PLAN_SPEC)                // only spec writes (an upstream informer's batch)
+	PlanStatus             = uint32(C.GPUDIFF_PLAN_STATUS)              // only status writes (a downstream informer's batch)
+	PlanUpstreamDownstream = uint32(C.GPUDIFF_PLAN_UPSTREAM_DOWNSTREAM) // pairs are (A upstream, B downstream)
+)
+
+// DiffAndPlan is DiffAndPlanMode(olds, news, PlanInformer).
 func (e *Engine) DiffAndPlan(olds, news [][]byte) ([]uint8, []Write, error) {
+	return e.DiffAndPlanMode(olds, news, PlanInformer)
+}
+
+// DiffAndPlanMode decides n pairs on the device and renders the writes those decisions imply from
+// the JSON still staged in HBM (kernel K10, no second upload): flags[i] are the pair's GPUDIFF_*
+// result bits, writes list the spec writes (ascending pair) then the status writes.  The engine must
+// have been opened with OptDeviceEncode.  The caller issues each non-no-op write as today (Create,
+// then Update with the live resourceVersion on AlreadyExists, specsyncer.go:110-129).
+func (e *Engine) DiffAndPlanMode(olds, news [][]byte, mode uint32) ([]uint8, []Write, error) {
 	n := len(olds)
-	if n == 0 || len(news) != n {
+	if len(news) != n {
+		return nil, nil, errOf(C.GPUDIFF_E_INVAL)
+	}
+	if n == 0 {
 		return nil, nil, nil
 	}
 	pairs := (*[1 << 28]C.gpudiff_json_pair)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_json_pair{}))))[:n:n]
@@ -460,7 +609,7 @@ func (e *Engine) DiffAndPlan(olds, news [][]byte) ([]uint8, []Write, error) {
 	copy(flags, (*[1 << 30]uint8)(unsafe.Pointer(res.pair_flags))[:n:n])
 	C.gpudiff_result_release(e.ctx, &res)
 	var plan C.gpudiff_write_plan
-	if err := errOf(C.gpudiff_write_plan_get(e.ctx, ticket, &plan)); err != nil {
+	if err := errOf(C.gpudiff_write_plan_get_ex(e.ctx, ticket, C.uint32_t(mode), &plan)); err != nil {
 		return flags, nil, err
 	}
 	defer C.gpudiff_write_plan_release(e.ctx, &plan)

@@ -551,7 +551,17 @@ struct PlanStore {
 };
 
 int gpudiff_write_plan_get(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_write_plan* out) {
+    return gpudiff_write_plan_get_ex(c, ticket, GPUDIFF_PLAN_INFORMER, out);
+}
+
+int gpudiff_write_plan_get_ex(gpudiff_ctx* c, gpudiff_ticket ticket, uint32_t mode, gpudiff_write_plan* out) {
     if (!c || !out) return GPUDIFF_E_INVAL;
+    if (mode & ~(GPUDIFF_PLAN_SPEC | GPUDIFF_PLAN_STATUS | GPUDIFF_PLAN_UPSTREAM_DOWNSTREAM)) return GPUDIFF_E_INVAL;
+    const uint32_t kinds = (mode & (GPUDIFF_PLAN_SPEC | GPUDIFF_PLAN_STATUS)) ? mode : (GPUDIFF_PLAN_SPEC | GPUDIFF_PLAN_STATUS);
+    // informer pairs (old, new): UpdateFunc enqueues newObj and the worker writes it (specsyncer.go:47-50 ->
+    // :86-132, statussyncer.go:32-35 -> :41-63), so both kinds render document 2i+1; (A, B) pairs: the spec
+    // write is A's (2i), the status write B's (2i+1)
+    const uint32_t spec_side = (mode & GPUDIFF_PLAN_UPSTREAM_DOWNSTREAM) ? 0u : 1u;
     memset(out, 0, sizeof(*out));
     int rc = set_device(c);
     if (rc) return rc;
@@ -560,8 +570,9 @@ int gpudiff_write_plan_get(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_write_
     const std::vector<uint8_t>& fl = *sp.flags;
     std::unique_ptr<PlanStore> ps(new (std::nothrow) PlanStore());
     if (!ps) return GPUDIFF_E_NOMEM;
-    // the writes: spec-dirty pairs (A's body to downstream), then status-dirty pairs (B's body to upstream)
+    // the writes: spec-dirty pairs, then status-dirty pairs
     for (uint32_t kind = GPUDIFF_UPSERT_SPEC; kind <= GPUDIFF_UPSERT_STATUS; kind++) {
+        if (!(kinds & (kind == GPUDIFF_UPSERT_SPEC ? GPUDIFF_PLAN_SPEC : GPUDIFF_PLAN_STATUS))) continue;
         const uint8_t dirty = kind == GPUDIFF_UPSERT_SPEC ? GPUDIFF_SPEC_DIRTY : GPUDIFF_STATUS_DIRTY;
         const uint8_t noop = kind == GPUDIFF_UPSERT_SPEC ? GPUDIFF_SPEC_NOOP : GPUDIFF_STATUS_NOOP;
         for (uint32_t p = 0; p < sp.n; p++)
@@ -579,7 +590,7 @@ int gpudiff_write_plan_get(gpudiff_ctx* c, gpudiff_ticket ticket, gpudiff_write_
     uint64_t sb = 0, ob = 0;
     for (size_t w = 0; w < nw; w++) {
         if (ps->noop[w]) continue;
-        const uint32_t di = 2 * ps->pair_index[w] + (ps->kind[w] == GPUDIFF_UPSERT_SPEC ? 0u : 1u);
+        const uint32_t di = 2 * ps->pair_index[w] + (ps->kind[w] == GPUDIFF_UPSERT_SPEC ? spec_side : 1u);
         TokDoc t = sp.hdocs[di];
         t.seed = 0;
         t.scratch_off = sb;

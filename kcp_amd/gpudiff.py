@@ -119,6 +119,8 @@ TOK_OK, TOK_SYNTAX, TOK_NUMBER, TOK_KEY, TOK_STRING, TOK_HASH, TOK_DEPTH, TOK_SI
 ROLLUP_NONE, ROLLUP_DECODE = -1, -2
 
 UPSERT_SPEC, UPSERT_STATUS = 0, 1
+# gpudiff_write_plan_get_ex modes: which writes, rendered from which document of a pair
+PLAN_INFORMER, PLAN_SPEC, PLAN_STATUS, PLAN_UPSTREAM_DOWNSTREAM = 0x0, 0x1, 0x2, 0x4
 BODY_DEVICE, BODY_HOST = 0, 1
 
 
@@ -236,6 +238,7 @@ SIGNATURES = [
                                         C.POINTER(Bodies)]),
     ("gpudiff_bodies_release", None, [_P, C.POINTER(Bodies)]),
     ("gpudiff_write_plan_get", C.c_int, [_P, C.c_uint64, C.POINTER(WritePlanC)]),
+    ("gpudiff_write_plan_get_ex", C.c_int, [_P, C.c_uint64, C.c_uint32, C.POINTER(WritePlanC)]),
     ("gpudiff_write_plan_release", None, [_P, C.POINTER(WritePlanC)]),
     ("gpudiff_wbatch_create", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
                                         C.POINTER(_P)]),
@@ -617,10 +620,13 @@ class Engine:
              "gpudiff_submit")
         return t.value
 
-    def write_plan(self, ticket: int) -> "WritePlan":
-        """gpudiff_write_plan_get: the writes for a waited device-encode batch (bodies from HBM)."""
+    def write_plan(self, ticket: int, mode: int = PLAN_INFORMER) -> "WritePlan":
+        """gpudiff_write_plan_get_ex: the writes for a waited device-encode batch (bodies from HBM).
+        mode PLAN_INFORMER (default): pairs are informer (old, new) events, every write renders new;
+        | PLAN_UPSTREAM_DOWNSTREAM: pairs are (A upstream, B downstream), spec writes render A;
+        | PLAN_SPEC / PLAN_STATUS: only those writes (neither: both)."""
         wp = WritePlanC()
-        _chk(_lib.gpudiff_write_plan_get(self.ctx, ticket, C.byref(wp)), "gpudiff_write_plan_get")
+        _chk(_lib.gpudiff_write_plan_get_ex(self.ctx, ticket, mode, C.byref(wp)), "gpudiff_write_plan_get_ex")
         try:
             n = wp.n
             b = wp.bodies
@@ -743,9 +749,9 @@ def _doc_arrays(docs):
 
 @dataclass
 class WritePlan:
-    """The writes of one diffed batch (gpudiff_write_plan): spec writes (A's
-    body to downstream), then status writes (B's body to upstream); no-op
-    writes carry no body."""
+    """The writes of one diffed batch (gpudiff_write_plan): spec writes, then
+    status writes, each rendered from the document the plan mode names (informer
+    pairs: new); no-op writes carry no body."""
     pair_index: np.ndarray
     kind: np.ndarray               # UPSERT_SPEC / UPSERT_STATUS
     noop: np.ndarray

@@ -77,40 +77,58 @@ def tensor_fill(spec_ids, status_ids):
 
 
 class DirtyGather:
-    """The per-step collective with no host synchronisation and ONE all-gather
-    per step: each rank packs [counts int32[8] (n_spec, n_status, ...) |
-    spec-dirty IDs (capacity cap_spec) | status-dirty IDs (capacity
-    cap_status)] into one preallocated int32 buffer and the buffers are
-    all-gathered in a single RCCL call (one collective latency instead of
-    three: at N = 8 the step's diff pass is ~1 ms, so per-call latency
-    matters).  The capacities are agreed once, before the timed steps
-    (`agree_capacity`: the all-gathered maximum of a first pass's counts); the
-    gathered counts say how many IDs of each rank's slot are real, and
-    `check()` -- called after the timed region -- reports a rank whose count
-    exceeded the capacity (its IDs were truncated: the step must be redone
-    with larger buffers, never silently accepted).
+    """The per-step collective with ONE all-gather per step: each rank packs
+    [counts int32[8] (n_spec, n_status, ...) | spec-dirty IDs (capacity
+    cap_spec) | status-dirty IDs (capacity cap_status)] into one preallocated
+    int32 buffer and the buffers are all-gathered in a single RCCL call (one
+    collective latency instead of three: at N = 8 the step's diff pass is
+    ~1 ms, so per-call latency matters).  The capacities start at a value agreed
+    before the timed steps (`agree_capacity`: the all-gathered maximum of a
+    first pass's counts).
+
+    A changing dirty count (a real watch stream) is handled inside the step
+    (`depth` = 1, the default): after the gather, the gathered counts -- 32 B
+    per rank, identical on every rank -- are read back (one small D2H copy on
+    the stream, waited by an event, not a device synchronisation), and if any
+    rank's count exceeded its capacity every rank grows its buffers to the
+    gathered maximum (x `grow`) and redoes that step's gather from the same
+    results, so the node-wide sets are always exact.  `n_regrows` counts the
+    redone steps.
 
     Pipelining (`depth` > 1): the all-gather is issued asynchronously
     (async_op=True) on the backend's own stream, so step s's collective runs
-    while step s+1's diff pass streams on the compute stream -- the same
-    overlap of communication with compute a training step gets from bucketed
-    all-reduce.  Step s writes send buffer s % depth; before a buffer is
-    refilled the compute stream waits (device-side, `work.wait()`) for the
-    collective that last read it, so no host synchronisation is added and
-    every step's gather completes.  `finish()` joins the outstanding
-    collectives; it belongs inside the timed region."""
+    while step s+1's diff pass streams on the compute stream.  Step s writes
+    send buffer s % depth; before a buffer is refilled the compute stream
+    waits (device-side, `work.wait()`) for the collective that last read it.
+    There the counts are not read back per step (that would serialise the
+    pipeline); instead a running maximum of every step's gathered counts is
+    kept on the device and `check()` reports a capacity overflow in ANY step
+    -- the IDs of such a step were truncated and `result()` refuses them.
+    `finish()` joins the outstanding collectives; it belongs inside the timed
+    region."""
 
-    def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist, depth: int = 1):
+    def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist, depth: int = 1,
+                 grow: float = 1.25):
         import torch
-        self.world, self.dist = world, dist
+        self.world, self.dist, self.device = world, dist, device
+        self.depth = max(1, int(depth))
+        self.grow = max(1.0, float(grow))
+        self.n_steps = 0
+        self.n_regrows = 0
+        self.maxc = torch.zeros((world, 2), dtype=torch.int32, device=device)
+        self._alloc(cap_spec, cap_status)
+
+    def _alloc(self, cap_spec: int, cap_status: int):
+        import torch
         self.cap = (max(1, int(cap_spec)), max(1, int(cap_status)))
         self.width = 8 + self.cap[0] + self.cap[1]
-        self.depth = max(1, int(depth))
-        self.sends = [torch.zeros(self.width, dtype=torch.int32, device=device) for _ in range(self.depth)]
-        self.alls = [torch.zeros(world * self.width, dtype=torch.int32, device=device) for _ in range(self.depth)]
+        self.sends = [torch.zeros(self.width, dtype=torch.int32, device=self.device) for _ in range(self.depth)]
+        self.alls = [torch.zeros(self.world * self.width, dtype=torch.int32, device=self.device)
+                     for _ in range(self.depth)]
         self.works = [None] * self.depth
         self.used = [False] * self.depth
-        self.n_steps = 0
+        pinned = torch.device(self.device).type == "cuda"
+        self.host_counts = torch.zeros((self.world, 2), dtype=torch.int32, pin_memory=pinned)
         self._select(0)
 
     def _select(self, b: int):
@@ -127,15 +145,29 @@ class DirtyGather:
         cc = allc.view(world, -1).cpu()
         return int(cc[:, 0].max() * slack) + 1, int(cc[:, 1].max() * slack) + 1
 
+    def _gathered_counts(self, b: int):
+        return self.alls[b].view(self.world, self.width)[:, :2]
+
+    def _read_counts(self):
+        """The gathered (n_spec, n_status) of the current buffer on the host: a 8 B x world copy on the
+        current stream, waited by an event (the host waits for this step's gather only)."""
+        import torch
+        self.host_counts.copy_(self._gathered_counts(0), non_blocking=True)
+        if self.host_counts.is_pinned():
+            ev = torch.cuda.Event()
+            ev.record()
+            ev.synchronize()
+        return self.host_counts
+
     def step(self, fill_counts, fill_ids):
         """fill_counts(tensor[8]) and fill_ids(col, tensor[cap]) write this
         rank's values into its slots of the send buffer on the device (the GPU
         path: gpudiff_dbatch_export straight from HBM, ordered on the stream
-        before the collective)."""
+        before the collective).  Both may be called again within one step (a
+        capacity regrow re-exports the same results)."""
+        import torch
         b = self.n_steps % self.depth
-        if self.works[b] is not None:  # the collective that last read this buffer
-            self.works[b].wait()
-            self.works[b] = None
+        self._join(b)  # the collective that last read this buffer
         self._select(b)
         fill_counts(self.counts)
         for col in (0, 1):
@@ -144,28 +176,44 @@ class DirtyGather:
             self.works[b] = self.dist.all_gather_into_tensor(self.all, self.send, async_op=True)
         else:
             self.dist.all_gather_into_tensor(self.all, self.send)
+            hc = self._read_counts()
+            if bool((hc[:, 0] > self.cap[0]).any() or (hc[:, 1] > self.cap[1]).any()):
+                # every rank sees the same gathered counts, so all take this branch together
+                ms, mt = int(hc[:, 0].max()), int(hc[:, 1].max())
+                self._alloc(max(self.cap[0], int(ms * self.grow) + 1), max(self.cap[1], int(mt * self.grow) + 1))
+                fill_counts(self.counts)
+                for col in (0, 1):
+                    fill_ids(col, self.buf[col])
+                self.dist.all_gather_into_tensor(self.all, self.send)
+                self.n_regrows += 1
+            torch.maximum(self.maxc, self._gathered_counts(0), out=self.maxc)
         self.used[b] = True
         self.n_steps += 1
+
+    def _join(self, b: int):
+        """Device-side wait for buffer b's outstanding collective, then fold its gathered counts into the
+        running maximum (ordered after the wait on the current stream)."""
+        import torch
+        if self.works[b] is not None:
+            self.works[b].wait()
+            self.works[b] = None
+            torch.maximum(self.maxc, self._gathered_counts(b), out=self.maxc)
 
     def finish(self):
         """Join every outstanding collective (the compute stream waits for them)."""
         for b in range(self.depth):
-            if self.works[b] is not None:
-                self.works[b].wait()
-                self.works[b] = None
+            self._join(b)
 
     def _rows(self):
         return self.all.view(self.world, self.width)
 
     def check(self):
         """-> (ok, host count matrix [world, 8] of the last step); ok only if no
-        rank exceeded its capacity in ANY pipelined buffer's last step."""
+        rank exceeded its capacity in ANY step since the buffers were last sized
+        (the device-side running maximum of the gathered counts)."""
         self.finish()
-        ok = True
-        for b in range(self.depth):
-            if self.used[b]:
-                c = self.alls[b].view(self.world, self.width)[:, :8].cpu()
-                ok = ok and bool((c[:, 0] <= self.cap[0]).all() and (c[:, 1] <= self.cap[1]).all())
+        mx = self.maxc.cpu()
+        ok = bool((mx[:, 0] <= self.cap[0]).all() and (mx[:, 1] <= self.cap[1]).all())
         cc = self._rows()[:, :8].cpu()
         return ok, cc
 
@@ -175,7 +223,7 @@ class DirtyGather:
         import torch
         ok, cc = self.check()
         if not ok:
-            raise RuntimeError("dirty-ID capacity exceeded: %s > %s" % (cc[:, :2].tolist(), self.cap))
+            raise RuntimeError("dirty-ID capacity exceeded: %s > %s" % (self.maxc.cpu().tolist(), self.cap))
         rows = self._rows()
         spec = torch.cat([rows[r, 8:8 + int(cc[r, 0])] for r in range(self.world)])
         stat = torch.cat([rows[r, 8 + self.cap[0]:8 + self.cap[0] + int(cc[r, 1])] for r in range(self.world)])

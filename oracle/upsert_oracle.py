@@ -211,21 +211,34 @@ def _upsert_body(json_bytes: bytes, mode: int) -> Optional[bytes]:
     return go_marshal(transform(obj, mode)) + b"\n"
 
 
-def write_plan(pairs) -> List[Tuple[int, int, bool, Optional[bytes]]]:
-    """The writes the syncer issues for a batch of (A=upstream, B=downstream)
-    pairs, as gpudiff_write_plan_get lists them: every spec-dirty pair
-    (upsertIntoDownstream, pkg/syncer/specsyncer.go:86-132: A's body,
-    MODE_SPEC), then every status-dirty pair (updateStatusInUpstream,
-    statussyncer.go:41-63: B's body, MODE_STATUS); a write the oracle marks
+PLAN_SPEC, PLAN_STATUS, PLAN_UPSTREAM_DOWNSTREAM = 0x1, 0x2, 0x4  # gpudiff_write_plan_get_ex modes
+
+
+def write_plan(pairs, mode: int = 0) -> List[Tuple[int, int, bool, Optional[bytes]]]:
+    """The writes the syncer issues for a batch of pairs, as
+    gpudiff_write_plan_get_ex lists them: every spec-dirty pair
+    (upsertIntoDownstream, pkg/syncer/specsyncer.go:86-132, MODE_SPEC), then
+    every status-dirty pair (updateStatusInUpstream, statussyncer.go:41-63,
+    MODE_STATUS); PLAN_SPEC / PLAN_STATUS restrict the kinds (neither = both).
+
+    Which document a write renders: for informer pairs (old, new) -- the
+    default -- UpdateFunc enqueues newObj (specsyncer.go:47-50,
+    statussyncer.go:32-35) and the worker writes it, so both kinds render new;
+    with PLAN_UPSTREAM_DOWNSTREAM the pairs are (A upstream, B downstream) and
+    the spec write renders A, the status write B.  A write the oracle marks
     no-op (gpudiff_oracle.diff_pair spec_noop / status_noop) has no body.
     Returns [(pair index, mode, noop, body or None if undecodable)]."""
     from .gpudiff_oracle import diff_pair
+    kinds = mode & (PLAN_SPEC | PLAN_STATUS) or (PLAN_SPEC | PLAN_STATUS)
+    spec_side = 0 if mode & PLAN_UPSTREAM_DOWNSTREAM else 1
     rs = [diff_pair(a, b) for a, b in pairs]
     out = []
-    for mode, dirty, noop, side in ((MODE_SPEC, "spec_dirty", "spec_noop", 0),
-                                    (MODE_STATUS, "status_dirty", "status_noop", 1)):
+    for bit, kind, dirty, noop, side in ((PLAN_SPEC, MODE_SPEC, "spec_dirty", "spec_noop", spec_side),
+                                         (PLAN_STATUS, MODE_STATUS, "status_dirty", "status_noop", 1)):
+        if not kinds & bit:
+            continue
         for i, r in enumerate(rs):
             if r[dirty]:
                 skip = bool(r[noop])
-                out.append((i, mode, skip, b"" if skip else upsert_body(pairs[i][side], mode)))
+                out.append((i, kind, skip, b"" if skip else upsert_body(pairs[i][side], kind)))
     return out

@@ -1,0 +1,146 @@
+"""The Go drop-in's object transfer (integration/go/gpudiff/gpudiff.go:jsonOf),
+restated in tests/goshim.py, on CPU: the type-marked text must carry every
+value the predicates compare (Go int64 vs float64 included, specsyncer.go:36;
+SURVEY.md A.4 rows 7/8/9/25/26), so the oracle and the product's host encoder
+see the same thing through it as through the original JSON.  The GPU half is
+tests/test_gpu_goshim.py."""
+import math
+import random
+import struct
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from kcp_amd import gpudiff as G
+from oracle import gpudiff_oracle as O
+from tests import goshim as S
+from tests.golden import fixtures as F
+from tests.golden.kat_cases import cases
+
+
+def all_pairs():
+    out = [(name, a, b) for name, a, b, _, _ in cases()]
+    for fx in F.NAMES:
+        out += [(fx + "/" + name, a, b) for name, a, b, _ in F.load(fx)]
+    return out
+
+
+PAIRS = all_pairs()
+
+# strconv.FormatFloat(f, 'g', -1, 64) answers
+GO_G = {3.0: "3", -0.0: "-0", 1e21: "1e+21", 1.5e-7: "1.5e-07", 100.0: "100", 1234567.0: "1.234567e+06",
+        123456.0: "123456", 0.0001: "0.0001", 0.00001: "1e-05", 2.5e-5: "2.5e-05", 5e-324: "5e-324",
+        1.7976931348623157e308: "1.7976931348623157e+308", 0.1: "0.1", -12.25: "-12.25",
+        9.223372036854775808e18: "9.223372036854776e+18"}
+
+
+def test_go_format_g_known_answers_and_round_trip():
+    for f, want in GO_G.items():
+        assert S.go_format_g(f) == want, f
+    rnd = random.Random(7)
+    for _ in range(50000):
+        f = struct.unpack("<d", struct.pack("<Q", rnd.getrandbits(64)))[0]
+        if not (math.isnan(f) or math.isinf(f)):
+            assert float(S.go_format_g(f)) == f
+
+
+def test_marker_contract():
+    txt = S.shim_json({"i": 3, "f": 3.0, "z": -0.0, "e": 1e21, "s": 'a"\\\n\x01é', "n": None,
+                       "l": [True, False, {}, []]})
+    obj = O.go_json_decode(txt)
+    assert type(obj["i"]) is int and type(obj["f"]) is float and type(obj["e"]) is float
+    assert math.copysign(1.0, obj["z"]) < 0 and obj["s"] == 'a"\\\n\x01é'
+    assert b'"f":3.0' in txt and b'"z":-0.0' in txt and b'"e":1e+21' in txt
+    # not transferable -> None (the batcher reports the pair dirty)
+    assert S.shim_json({"x": float("nan")}) is None
+    assert S.shim_json({"x": "\ud800"}) is None           # not valid UTF-8 as a Go string
+    assert S.shim_json({"x": 1 << 63}) is None            # no int64 holds it
+    assert S.shim_json({"x": (1,)}) is None               # a dynamic type JSON never yields
+
+
+def test_old_marshal_json_transfer_loses_types():
+    """The defect VERDICT r2 found: MarshalJSON writes float64(3) as 3, so KAT 7 read back equal."""
+    a, b = b'{"spec":{"replicas":3}}', b'{"spec":{"replicas":3.0}}'
+    assert O.diff_pair(a, b)["spec_dirty"]
+    old = [S.go_marshal_json(O.go_json_decode(x)) for x in (a, b)]
+    assert not O.diff_pair(*old)["spec_dirty"]            # false "equal" through the old transfer
+    new = S.shim_pair(a, b)
+    assert O.diff_pair(*new)["spec_dirty"]
+    for x, y in ((b'{"spec":{"x":0}}', b'{"spec":{"x":-0.0}}'),
+                 (b'{"spec":{"x":9223372036854775807}}', b'{"spec":{"x":9223372036854775808}}')):
+        assert O.diff_pair(x, y)["spec_dirty"] and O.diff_pair(*S.shim_pair(x, y))["spec_dirty"]
+
+
+def _strip(r):
+    return {k: v for k, v in r.items()}
+
+
+def test_every_kat_and_golden_pair_through_the_shim_oracle():
+    """Through the transfer the oracle reaches the same decision, seed and path list as on the
+    original JSON; a pair the shim cannot transfer is one the informer could not have delivered."""
+    n_bad = 0
+    for name, a, b in PAIRS:
+        want = O.diff_pair(a, b)
+        sp = S.shim_pair(a, b)
+        if sp is None:
+            n_bad += 1
+            assert want["decode_error"] and want["spec_dirty"] and want["status_dirty"], name
+            continue
+        got = O.diff_pair(*sp)
+        assert got == want, name
+    assert n_bad < len(PAIRS) // 4
+
+
+@pytest.fixture(scope="module")
+def host_engine():
+    e = G.Engine(device=G.DEVICE_NONE, encode_threads=4)
+    yield e
+    e.close()
+
+
+def test_host_encoder_sees_identical_blobs(host_engine):
+    """The product's host encoder turns the shim's text into the same canonical blobs and rows as the
+    original JSON (so every downstream kernel sees identical input)."""
+    orig, shim = [], []
+    for name, a, b in PAIRS:
+        sp = S.shim_pair(a, b)
+        if sp is not None:
+            orig.append((a, b))
+            shim.append(sp)
+    h1, h2 = host_engine.encode(orig), host_engine.encode(shim)
+    r1, r2 = h1.rows(), h2.rows()
+    assert np.array_equal(r1, r2)
+    assert h1.pool() == h2.pool()
+    h1.free()
+    h2.free()
+
+
+def _trees():
+    scalars = st.one_of(st.none(), st.booleans(), st.integers(O.INT64_MIN, O.INT64_MAX),
+                        st.floats(allow_nan=False, allow_infinity=False), st.text(max_size=12))
+    return st.recursive(scalars, lambda ch: st.one_of(st.lists(ch, max_size=4),
+                                                       st.dictionaries(st.text(max_size=6), ch, max_size=4)),
+                        max_leaves=24)
+
+
+def _same_typed(x, y):
+    if type(x) is not type(y):
+        return False
+    if isinstance(x, float):
+        return x == y and math.copysign(1.0, x) == math.copysign(1.0, y)
+    if isinstance(x, dict):
+        return x.keys() == y.keys() and all(_same_typed(x[k], y[k]) for k in x)
+    if isinstance(x, list):
+        return len(x) == len(y) and all(_same_typed(p, q) for p, q in zip(x, y))
+    return x == y
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.dictionaries(st.text(max_size=6), _trees(), max_size=5))
+def test_round_trip_keeps_go_types(obj):
+    txt = S.shim_json(obj)
+    if any(0xD800 <= ord(c) < 0xE000 for c in repr(obj)):
+        return  # lone surrogates: not a Go string (covered above)
+    assert txt is not None
+    assert _same_typed(O.go_json_decode(txt), obj)

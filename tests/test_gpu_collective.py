@@ -1,7 +1,7 @@
 """The multi-GPU step's collective over RCCL ("nccl" backend = RCCL on ROCm) on
-real hardware at world_size 1: shard.DirtyGather (the bench's host-sync-free
-per-step all-gather, IDs exported straight from HBM with
-gpudiff_dbatch_export) and shard.gather_dirty return the node-wide dirty sets
+real hardware at world_size 1: shard.DirtyGather (the bench's per-step
+all-gather, IDs exported straight from HBM with gpudiff_dbatch_export, a
+capacity overflow regrown inside the step) and shard.gather_dirty return the node-wide dirty sets
 of a diffed device batch.  World size 2 of the same code runs on CPU (gloo) in
 tests/test_multirank.py."""
 import socket
@@ -64,6 +64,16 @@ def test_dirty_gather_over_rccl_world1():
             sa, ta = g.result()
             assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
             assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        # a capacity below the dirty count: regrown inside the first step, exact from then on
+        g = shard.DirtyGather(1, max(1, cap_s // 2), max(1, cap_t // 3), dev, dist)
+        for _ in range(3):
+            eng.diff(db)
+            g.step(fill_counts, fill_ids)
+        g.finish()
+        assert g.n_regrows == 1 and g.cap[0] >= want.spec_dirty_ids.size
+        sa, ta = g.result()
+        assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+        assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
         # the general (trimmed) form
         s2, t2 = shard.gather_dirty(counts, lambda col, buf, k: db.export(
             G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(), k), 0, 1, dist, dev)

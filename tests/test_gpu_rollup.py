@@ -118,3 +118,20 @@ def test_root_member_order_and_decoys():
     res = _check(eng, [_reorder_root(d, rng) for d in docs])
     assert res.n_host < len(docs) // 10  # clean API-server JSON: decided on the device
     eng.close()
+
+
+@pytest.mark.parametrize("phase", ["created", "available"])
+def test_kubecon_transcript(phase):
+    """K11 + K12 against the reference's own transcript (contrib/demo/kubecon.result:196-208): the two
+    leaves createLeafs makes from contrib/demo/deployment.yaml roll up into the root's 0/10 10 0 while
+    the pods start and 10/10 10 10 once Available -- decided on the device, equal to the oracle."""
+    from tests import kubecon_demo as K
+    docs, root, _leaves = K.cache(phase)
+    eng = G.Engine(device=0)
+    res = _check(eng, docs)
+    assert res.n_host == 0
+    assert res.doc_group.tolist() == [G.ROLLUP_NONE, 0, 0]
+    st = K.root_status_from_sums(res.sums[0])
+    assert K.kubectl_row(root["spec"]["replicas"], st) == K.TRANSCRIPT[phase][K.ROOT_NAME]
+    assert int(res.first_doc[0]) == 1  # others[0]: the us-east1 leaf's conditions go to the root
+    eng.close()

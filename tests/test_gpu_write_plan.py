@@ -1,10 +1,13 @@
 """Gate -> write on the device: for batches diffed
-through the device-encode submit path, gpudiff_write_plan_get lists the writes
-the syncer issues -- spec-dirty pairs: A's upsertIntoDownstream body; status-
-dirty pairs: B's updateStatusInUpstream body -- rendered by K10 from the JSON
-still staged in HBM, with the write-path no-op rule (no body, call skipped).
-Everything is compared with oracle/upsert_oracle.write_plan, i.e. the oracle's
-decisions, no-op rule and Go-exact bodies."""
+through the device-encode submit path, gpudiff_write_plan_get[_ex] lists the
+writes the syncer issues -- spec-dirty pairs: an upsertIntoDownstream body;
+status-dirty pairs: an updateStatusInUpstream body -- rendered by K10 from the
+JSON still staged in HBM, with the write-path no-op rule (no body, call
+skipped).  For informer (old, new) pairs (the default) both render the NEW
+object, the one UpdateFunc enqueues (specsyncer.go:47-50); for (upstream,
+downstream) pairs the spec write renders A.  Everything is compared with
+oracle/upsert_oracle.write_plan, i.e. the oracle's decisions, no-op rule and
+Go-exact bodies."""
 import json
 import random
 
@@ -19,12 +22,12 @@ from tests.workload import make_pairs
 pytestmark = pytest.mark.gpu
 
 
-def _check(eng, pairs):
+def _check(eng, pairs, mode=G.PLAN_INFORMER):
     t = eng.submit(pairs)
     res = eng.wait(t)
     assert_matches(res, pairs)
-    plan = eng.write_plan(t)
-    want = U.write_plan(pairs)
+    plan = eng.write_plan(t, mode)
+    want = U.write_plan(pairs, mode)
     got = list(zip(plan.pair_index.tolist(), plan.kind.tolist(), [bool(x) for x in plan.noop], plan.bodies))
     assert len(got) == len(want)
     for g, w in zip(got, want):
@@ -111,4 +114,37 @@ def test_write_plan_two_batches_in_flight_and_state_errors():
     with pytest.raises(G.GpuDiffError):
         host.write_plan(th)
     host.close()
+    eng.close()
+
+
+def test_write_plan_informer_renders_new_object():
+    """an informer Update (old, new) that changes the spec must write NEW downstream
+    (UpdateFunc -> AddToQueue(gvr, newObj), specsyncer.go:47-50 -> upsertIntoDownstream); rendering old
+    would push the stale version and undo the change."""
+    eng = G.Engine(device=0, device_encode=True)
+    pairs = []
+    for i in range(40):
+        a = json.loads(J(BASE))
+        a["spec"]["replicas"] = i
+        b = json.loads(J(a))
+        b["spec"]["replicas"] = i + 100
+        b["status"]["readyReplicas"] = i + 7
+        b["metadata"]["resourceVersion"] = "rv-%d" % i
+        pairs.append((J(a), J(b)))
+    t = eng.submit(pairs)
+    eng.wait(t)
+    for mode in (G.PLAN_INFORMER, G.PLAN_SPEC, G.PLAN_STATUS, G.PLAN_UPSTREAM_DOWNSTREAM,
+                 G.PLAN_UPSTREAM_DOWNSTREAM | G.PLAN_SPEC):
+        plan = eng.write_plan(t, mode)
+        want = U.write_plan(pairs, mode)
+        got = list(zip(plan.pair_index.tolist(), plan.kind.tolist(), [bool(x) for x in plan.noop], plan.bodies))
+        assert got == want, mode
+        kinds = set(plan.kind.tolist())
+        assert kinds == ({G.UPSERT_SPEC} if mode & 3 == G.PLAN_SPEC else {G.UPSERT_STATUS} if mode & 3 == G.PLAN_STATUS
+                         else {G.UPSERT_SPEC, G.UPSERT_STATUS})
+        for i, k, body in zip(plan.pair_index.tolist(), plan.kind.tolist(), plan.bodies):
+            side = 0 if (k == G.UPSERT_SPEC and mode & G.PLAN_UPSTREAM_DOWNSTREAM) else 1
+            assert body == U.upsert_body(pairs[i][side], k)
+            if side == 1:
+                assert b'"replicas":%d' % (i + 100) in body
     eng.close()

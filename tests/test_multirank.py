@@ -146,17 +146,81 @@ def _worker_fixed(rank, world, port, flags_all, owners, shrink, q, depth=1):
     ok, _ = g.check()
     if ok:
         sa, ta = g.result()
-        q.put((rank, True, sorted(sa.tolist()), sorted(ta.tolist())))
+        q.put((rank, True, sorted(sa.tolist()), sorted(ta.tolist()), g.n_regrows))
     else:
-        q.put((rank, False, None, None))
+        q.put((rank, False, None, None, g.n_regrows))
     dist.destroy_process_group()
+
+
+def _worker_growing(rank, world, port, flags_all, owners, q):
+    """A stream whose dirty count grows step by step past the agreed capacity (depth 1): every step's
+    node-wide sets must be exact, the buffers regrown inside the step."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = np.nonzero(owners == rank)[0]
+    f = flags_all[mine]
+    g = None
+    out = []
+    for step in range(4):
+        keep = (len(mine) * (step + 1)) // 4  # this step's results: a growing prefix of the rank's pairs
+        spec = torch.tensor(mine[:keep][(f[:keep] & 1) != 0], dtype=torch.int32)
+        stat = torch.tensor(mine[:keep][(f[:keep] & 2) != 0], dtype=torch.int32)
+        counts = torch.zeros(8, dtype=torch.int32)
+        counts[0], counts[1] = spec.numel(), stat.numel()
+        if g is None:
+            cs, ct = shard.DirtyGather.agree_capacity(counts, world, dist)
+            g = shard.DirtyGather(world, cs, ct, "cpu", dist)
+
+        def fill_counts(t):
+            t.copy_(counts)
+
+        def fill_ids(col, buf):
+            src = spec if col == 0 else stat
+            k = min(buf.numel(), src.numel())
+            buf[:k] = src[:k]
+        g.step(fill_counts, fill_ids)
+        sa, ta = g.result()
+        out.append((sorted(sa.tolist()), sorted(ta.tolist())))
+    q.put((rank, out, g.n_regrows))
+    dist.destroy_process_group()
+
+
+def test_dirty_gather_regrows_inside_the_step_gloo_world2():
+    rnd = np.random.default_rng(5)
+    n = 4000
+    clusters = rnd.integers(0, 61, n)
+    flags = rnd.integers(0, 4, n).astype(np.uint8)
+    owners = np.zeros(n, dtype=np.int32)
+    for r, idx in enumerate(shard.shard_pairs(clusters, 2)):
+        owners[idx] = r
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_growing, args=(r, 2, port, flags, owners, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out, regrows in res:
+        assert regrows >= 1
+        for step, (s, t) in enumerate(out):
+            sel = np.zeros(n, dtype=bool)
+            for r in range(2):
+                mine = np.nonzero(owners == r)[0]
+                sel[mine[:(len(mine) * (step + 1)) // 4]] = True
+            assert s == sorted(np.nonzero(sel & ((flags & 1) != 0))[0].tolist())
+            assert t == sorted(np.nonzero(sel & ((flags & 2) != 0))[0].tolist())
 
 
 @pytest.mark.parametrize("shrink,depth", [(0, 1), (5, 1), (0, 2), (5, 2), (0, 3)])
 def test_dirty_gather_fixed_capacity_gloo_world2(shrink, depth):
-    """The bench's per-step collective (shard.DirtyGather: no host sync, fixed
-    capacity): node-wide dirty sets equal the single-rank view; a capacity
-    below a rank's count is reported, never truncated silently."""
+    """The bench's per-step collective (shard.DirtyGather, one all-gather per
+    step): node-wide dirty sets equal the single-rank view; a capacity below a
+    rank's count is regrown inside the step (depth 1) or reported (pipelined),
+    never truncated silently."""
     rnd = np.random.default_rng(4)
     n = 4000
     clusters = rnd.integers(0, 61, n)
@@ -176,8 +240,10 @@ def test_dirty_gather_fixed_capacity_gloo_world2(shrink, depth):
         assert p.exitcode == 0
     want_s = sorted(np.nonzero(flags & 1)[0].tolist())
     want_t = sorted(np.nonzero(flags & 2)[0].tolist())
-    for rank, ok, s, t in res:
-        if shrink:
-            assert not ok
+    for rank, ok, s, t, regrows in res:
+        if shrink and depth > 1:
+            assert not ok  # pipelined: an overflow in any step is reported, never accepted
         else:
+            # depth 1: a capacity below a rank's count is regrown inside the step, the sets stay exact
             assert ok and s == want_s and t == want_t
+            assert regrows == (1 if shrink else 0)

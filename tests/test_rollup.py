@@ -105,3 +105,29 @@ def test_cpp_restatement_matches_oracle():
         _, _, got = rd.run(threads=4)
         rd.close()
         assert got == _strip(R.rollup(docs))
+
+
+# ---------------------------------------------------------------- the reference's own transcript
+@pytest.mark.parametrize("phase", ["created", "available"])
+def test_kubecon_transcript_oracle_and_host_path(phase):
+    """contrib/demo/kubecon.result:196-208 (the one reference-held outcome of the roll-up): the root's
+    READY / UP-TO-DATE / AVAILABLE from the sums of createLeafs' two leaves equal the transcript's row,
+    by the oracle and by the product's host path (summed per owned-by label)."""
+    from tests import kubecon_demo as K
+    docs, root, leaves = K.cache(phase)
+    want = K.TRANSCRIPT[phase]
+    for lf in leaves:  # the leaves' own rows
+        assert K.kubectl_row(lf["spec"]["replicas"], lf["status"]) == want[lf["metadata"]["name"]]
+    res = R.rollup(docs)
+    assert res["doc_group"] == [R.GROUP_NONE, 0, 0]  # the root is no leaf; both leaves roll up into one group
+    (g,) = res["groups"]
+    assert g["first_doc"] == 1 and g["n_members"] == 2
+    st = K.root_status_from_sums(g["sums"])
+    assert K.kubectl_row(root["spec"]["replicas"], st) == want[K.ROOT_NAME]
+    sums = [0] * 5
+    for d in docs:
+        h = G.rollup_doc_host(d)
+        assert h is not None
+        if h[1] == K.ROOT_NAME.encode():
+            sums = [a + b for a, b in zip(sums, h[0])]
+    assert sums == g["sums"]
