@@ -173,6 +173,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=50000, help="pairs in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full-paths", action="store_true",
+                    help="skip the CPU merge's full-size decision + changed-path check during ingest")
+    ap.add_argument("--no-k1", action="store_true", help="skip the K1 (value digest) pass and the hash + diff rate")
     ap.add_argument("--json-in-pairs", type=int, default=131072,
                     help="pairs of the end-to-end JSON-in measurement (0 = skip)")
     ap.add_argument("--traffic-json", default="latest",
@@ -243,6 +246,23 @@ def main():
     # ---------------- ingest: synthesize + encode on the host, stage, H2D, K1
     t_gen = time.time()
     first = pop.chunk(eng, 0, min(args.chunk, n), threads)
+    # full-size changed-path parity (north_star: bit-exact changed-path lists for all 10M pairs): the CPU
+    # merge over the same CSR encoding (oracle/csr_ref.cpp, pinned to the oracle by tests/test_oracle_cpp.py)
+    # decides and lists the paths of every chunk on the host while it is staged; checked against the
+    # GPU's first pass below.  Untimed.
+    cpu_parts = [] if not args.no_full_paths else None
+    t_cpu_paths = 0.0
+
+    def cpu_paths(hb):
+        nonlocal t_cpu_paths
+        if cpu_parts is None:
+            return
+        from oracle import cpu_ref
+        t_c = time.time()
+        inf = hb.info()
+        cpu_parts.append(cpu_ref.csr_paths_ptr(inf.pool, hb.rows(), threads))
+        t_cpu_paths += time.time() - t_c
+    cpu_paths(first.hb)
     per_pair = first.pool_bytes / max(1, min(args.chunk, n))
     margin = 1.15 if args.config != "config4" else 1.4
     pool_cap = int(per_pair * n * margin) + (64 << 20)
@@ -257,6 +277,7 @@ def main():
     while pos < n:
         m = min(args.chunk, n - pos)
         ch = pop.chunk(eng, pos, m, threads, reuse=stage[k & 1])
+        cpu_paths(ch.hb)
         stage[k & 1] = ch.hb
         db.append(ch.hb)
         truth[pos:pos + m] = ch.truth
@@ -285,8 +306,26 @@ def main():
     n_spec, n_status, n_paths = int(res.spec_dirty_ids.size), int(res.status_dirty_ids.size), int(res.path_hashes.size)
     full_check = dict(pairs=n, flag_mismatches=n_bad, every_dirty_pair_has_paths=every_dirty_has_path,
                       id_lists_consistent=ids_ok, spec_dirty=n_spec, status_dirty=n_status, paths=n_paths)
+    if cpu_parts is not None:
+        c_flags = np.concatenate([q[0] for q in cpu_parts])
+        c_offs, base = [np.zeros(1, np.int64)], 0
+        for q in cpu_parts:
+            c_offs.append(q[1][1:].astype(np.int64) + base)
+            base += int(q[1][-1])
+        c_offs = np.concatenate(c_offs)
+        c_h = np.concatenate([q[2] for q in cpu_parts])
+        c_k = np.concatenate([q[3] for q in cpu_parts])
+        full_check.update(
+            flags_eq_cpu_csr=bool(np.array_equal(res.pair_flags & 7, c_flags)),
+            paths_eq_cpu_csr=bool(np.array_equal(offs, c_offs) and np.array_equal(res.path_hashes, c_h) and
+                                  np.array_equal(res.path_kinds, c_k)),
+            cpu_csr_paths=int(c_h.size), cpu_csr_seconds=round(t_cpu_paths, 2),
+            cpu_csr="oracle/csr_ref.cpp over every chunk's host CSR (decisions + changed-path lists, all pairs)")
+        if not (full_check["flags_eq_cpu_csr"] and full_check["paths_eq_cpu_csr"]):
+            log("FULL-SIZE PATH PARITY FAILED")
+        del cpu_parts, c_flags, c_offs, c_h, c_k
     log("full-size check:", json.dumps(full_check))
-    if n_bad or not every_dirty_has_path or not ids_ok:
+    if n_bad or not every_dirty_has_path or not ids_ok or full_check.get("paths_eq_cpu_csr") is False:
         log("FULL-SIZE CHECK FAILED")
     pop_flags = res.pair_flags.copy()
     del res
@@ -386,6 +425,43 @@ def main():
         if pmc.get("k2_source_hash") == src_hash and pmc.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
 
+    # ---------------- K1 (value digests) as a stand-alone pass and "hash + diff" per step (SURVEY 8(d)'s
+    # K1+K2+K3): every step re-hashes the whole resident population, as if it were new in every step
+    k1 = None
+    if not args.no_k1:
+        k1_list = []
+        for _ in range(3):
+            db.hash_values()
+            eng.sync()
+            k1_list.append(eng.timings().value_hash_ms)
+        k1_avg = sum(k1_list) / len(k1_list)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            db.hash_values()
+            eng.diff(db)
+            if gather is not None:
+                gather.step(fill_counts, fill_ids)
+        if gather is not None:
+            gather.finish()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt1 = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([dt1], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt1 = float(t.item())
+        k1_gbs = st.hash_bytes / (k1_avg * 1e-3) / 1e9 if k1_avg > 0 else 0.0
+        k1 = dict(value_incl_k1=total_pairs * args.steps / dt1, ms_per_step_incl_k1=dt1 / args.steps * 1e3,
+                  k1_ms=k1_avg, k1_launch_ms=k1_list, bytes_per_launch=st.hash_bytes, achieved=k1_gbs,
+                  frac=k1_gbs / HBM_PEAK_GBPS, unit="GB/s",
+                  bytes_def="K1: per pair its 64-B row; per segment holding long values its metas (4 B/leaf), "
+                            "arena, and 8 B per digest written")
+        log("K1:", json.dumps(k1))
+
     db.free()  # the JSON-in and CPU legs below need no resident population
 
     # ---------------- rank 0, N = 1: end-to-end JSON-in, CPU baselines, three-way parity
@@ -453,7 +529,10 @@ def main():
                          "k2_source_hash": src_hash},
             "kernels_ms": {"compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,
                            "join_exposed": tm.join_ms, "emit": tm.emit_ms, "diff_pass": tm.total_ms,
-                           "passes": tm.n_passes, "value_hash_last_chunk": k1_ms},
+                           "passes": tm.n_passes, "value_hash_last_chunk": k1_ms,
+                           "value_hash_population": None if k1 is None else k1["k1_ms"]},
+            "value_incl_k1": None if k1 is None else k1["value_incl_k1"],
+            "k1": k1,
             "cpu_baseline": cpu,
             "json_in": json_in,
             "checks": {"full_size": full_check, "sample": sample_check, "three_way": three_way,

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GPUDIFF_ABI_VERSION 2
+#define GPUDIFF_ABI_VERSION 3
 
 enum {
     GPUDIFF_OK = 0,
@@ -185,10 +185,12 @@ typedef struct gpudiff_batch_stats {
     uint64_t compare_bytes;    /* format bytes one diff pass reads */
     uint64_t value_bytes;      /* canonical bytes of the long (non-inline) string values of every object:
                                   V of SURVEY.md §8(d)'s B_pair = sum over A, B of (24 L + V + 8) + O */
+    uint64_t hash_bytes;       /* bytes one K1 pass (value digests) moves: per pair its 64-B row, per segment
+                                  holding long values its metas (4 B per leaf) and arena, 8 B per digest written */
 } gpudiff_batch_stats;
 
 typedef struct gpudiff_timings {
-    float value_hash_ms;  /* K1 over the last appended chunk */
+    float value_hash_ms;  /* K1 over the last appended chunk, or the last gpudiff_dbatch_hash_values */
     float compare_ms;     /* K2: all k2_launches launches of a pass (back to back on the stream) */
     float compact_ms;     /* K3 (scan + compaction); 0 when overlapped with K2 (segmented pass) */
     float join_ms;        /* K4 merge-join; segmented pass: the part not hidden behind K2 */
@@ -227,6 +229,13 @@ int gpudiff_dbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, uint64_t max_pa
                           gpudiff_dbatch** out);
 /* async H2D of hb into the batch + K1 value hashing of the new objects */
 int gpudiff_dbatch_append(gpudiff_ctx* ctx, gpudiff_dbatch* db, const gpudiff_hbatch* hb);
+/* K1 over every pair already resident (the value digests gpudiff_dbatch_append computes per
+ * chunk at ingest), on the context's stream, asynchronous; with GPUDIFF_OPT_TIMING its duration is
+ * value_hash_ms.  The digests it writes equal those already there: this is the ingest hashing step
+ * as a stand-alone pass, so a caller can time "hash then diff" over a population that is new in
+ * every step.  No-op for a context that hashes on the host (GPUDIFF_OPT_HOST_VALUE_HASH /
+ * GPUDIFF_OPT_NO_VALUE_HASH). */
+int gpudiff_dbatch_hash_values(gpudiff_ctx* ctx, gpudiff_dbatch* d);
 int gpudiff_dbatch_reset(gpudiff_ctx* ctx, gpudiff_dbatch* db);
 int gpudiff_dbatch_stats_get(const gpudiff_dbatch* db, gpudiff_batch_stats* st);
 int gpudiff_dbatch_device_view(const gpudiff_dbatch* db, gpudiff_device_view* v);

@@ -424,16 +424,19 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
             c->k1_recorded = true;
         }
     }
-    uint64_t cb = 0, vb = 0;
+    uint64_t cb = 0, vb = 0, kb = 0;
     for (size_t i = 0; i < hb->n; i++) {
         const gpudiff_pair_row& r = hb->rows[i];
         cb += pair_compare_bytes(r);
+        kb += sizeof(gpudiff_pair_row) + blob_hash_bytes(hb->pool + r.off_a, r.spec_l_a, r.spec_ar_a, r.stat_l_a, r.stat_ar_a) +
+              blob_hash_bytes(hb->pool + r.off_b, r.spec_l_b, r.spec_ar_b, r.stat_l_b, r.stat_ar_b);
         if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) continue;
         vb += blob_value_bytes(hb->pool + r.off_a, r.spec_l_a, r.spec_ar_a, r.stat_l_a) +
               blob_value_bytes(hb->pool + r.off_b, r.spec_l_b, r.spec_ar_b, r.stat_l_b);
     }
     d->compare_bytes += cb;
     d->value_bytes += vb;
+    d->hash_bytes += kb;
     d->pool_used += hb->pool_bytes;
     d->n_pairs = end;
     d->leaves += hb->leaves;
@@ -445,7 +448,7 @@ int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
     int rc = set_device(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
-    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = 0;
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->hash_bytes = 0;
     d->ticket = 0;
     return GPUDIFF_OK;
 }
@@ -457,6 +460,21 @@ int gpudiff_dbatch_stats_get(const gpudiff_dbatch* d, gpudiff_batch_stats* st) {
     st->total_leaves = d->leaves;
     st->compare_bytes = d->compare_bytes;
     st->value_bytes = d->value_bytes;
+    st->hash_bytes = d->hash_bytes;
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_hash_values(gpudiff_ctx* c, gpudiff_dbatch* d) {
+    if (!c || !d) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (c->ecfg.host_value_hash || (c->flags & GPUDIFF_OPT_NO_VALUE_HASH) || !d->n_pairs) return GPUDIFF_OK;
+    if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
+    HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)d->n_pairs, d->pool));
+    if (c->flags & GPUDIFF_OPT_TIMING) {
+        HIPCHK(hipEventRecord(c->ev_k1[1], c->stream));
+        c->k1_recorded = true;
+    }
     return GPUDIFF_OK;
 }
 
@@ -810,7 +828,7 @@ int gpudiff_submit(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpu
             return rc;
         }
     }
-    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = 0;
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->hash_bytes = 0;
     if ((rc = gpudiff_dbatch_append(c, d, hb)) || (rc = gpudiff_diff(c, d, ticket))) {
         gpudiff_hbatch_free(c, hb);
         return rc;

@@ -88,22 +88,47 @@ __device__ __forceinline__ bool neq16(const u32x4& a, const u32x4& b) {
 }
 
 // ---------------------------------------------------------------- K1
-// XXH64 over a value stored 4-byte aligned in the arena: dword loads, none
-// past the value's 4-byte padded end (the next value, or the segment's end,
-// follows it directly).
-__device__ __forceinline__ uint64_t ld64_a4(const uint32_t* p, uint32_t i) {
-    return ((uint64_t)p[2 * i + 1] << 32) | p[2 * i];
-}
-__device__ uint64_t xxh64_a4(const uint32_t* p, uint32_t len, uint64_t seed) {
+// XXH64 of every long string value (> 8 bytes; the shorter ones are inline and need no digest).
+//
+// Round 2's K1 ran one wave per (pair, object, region) with a lane per value: a ConfigMap's spec
+// has 8 long values, so 8 of 64 lanes worked, each with 4-B loads (0.7-1.2 TB/s).  This K1 keeps
+// every lane busy on its own value and loads 16 B per lane:
+//   walk   each wave owns a contiguous range of pairs; a lane takes one pair at a time (idle lanes
+//          pull the next pairs of the range by ballot) and walks its segments' metas 4 at a time
+//          with one 16-B load, appending each long leaf's (value offset, length, digest slot) to
+//          the wave's LDS list (wave prefix sum of the per-lane counts: no atomics);
+//   hash   when the list is nearly full (and at the end), lanes take entries round-robin -- values
+//          of many pairs, so the lengths even out -- and hash each value in 128-B bursts (eight
+//          16-B loads in flight, then four 32-B stripes), the < 32-byte tail from dword loads
+//          within the value's 4-byte padding; the digest goes to the leaf's 8-B value slot.
+// Values sit 4-byte aligned in the arena (include/gpudiff_format.h), so the 16-B loads are
+// dword-aligned (gfx950 global loads need only dword alignment); no load passes the value's
+// padded end (bursts cover whole stripes only) or the segment (metas end where a >= 16-B arena
+// starts).
+typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ uint64_t lo64(const u32x4u& v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint64_t hi64(const u32x4u& v) { return ((uint64_t)v.w << 32) | v.z; }
+
+__device__ __forceinline__ uint64_t xxh64_lane(const uint8_t* __restrict__ p, uint32_t len) {
     uint64_t h;
-    uint32_t stripes = len >> 5;
-    if (stripes) {
-        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
-        for (uint32_t s = 0; s < stripes; s++) {
-            v1 = xround(v1, ld64_a4(p, 4 * s));
-            v2 = xround(v2, ld64_a4(p, 4 * s + 1));
-            v3 = xround(v3, ld64_a4(p, 4 * s + 2));
-            v4 = xround(v4, ld64_a4(p, 4 * s + 3));
+    const uint32_t nstr = len >> 5;
+    if (nstr) {
+        uint64_t v1 = XP1 + XP2, v2 = XP2, v3 = 0, v4 = 0ull - XP1;
+        for (uint32_t s = 0; s < nstr; s += 4) {
+            const uint32_t nb = min(4u, nstr - s);
+            u32x4u q[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++)
+                if (k < 2 * nb) q[k] = *(const u32x4u*)(p + 32u * s + 16u * k);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++)
+                if (j < nb) {
+                    v1 = xround(v1, lo64(q[2 * j]));
+                    v2 = xround(v2, hi64(q[2 * j]));
+                    v3 = xround(v3, lo64(q[2 * j + 1]));
+                    v4 = xround(v4, hi64(q[2 * j + 1]));
+                }
         }
         h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
         h = xmerge(h, v1);
@@ -111,54 +136,154 @@ __device__ uint64_t xxh64_a4(const uint32_t* p, uint32_t len, uint64_t seed) {
         h = xmerge(h, v3);
         h = xmerge(h, v4);
     } else {
-        h = seed + XP5;
+        h = XP5;
     }
     h += len;
+    // tail: rem < 32 bytes as up to 8 dwords (inside the value's 4-byte padding), then 8-, 4- and
+    // 1-byte steps with static register indices only
     const uint32_t rem = len & 31u;
-    uint32_t w32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint32_t* t = p + 8 * stripes;
+    const uint32_t* t = (const uint32_t*)(p + 32u * nstr);
+    uint32_t d[8];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; k++)
-        if (4 * k < rem) w32[k] = t[k];
-    uint64_t w[4];
+    for (uint32_t k = 0; k < 8; k++) d[k] = 4u * k < rem ? t[k] : 0u;
+    const uint64_t w0 = ((uint64_t)d[1] << 32) | d[0], w1 = ((uint64_t)d[3] << 32) | d[2];
+    const uint64_t w2 = ((uint64_t)d[5] << 32) | d[4], w3 = ((uint64_t)d[7] << 32) | d[6];
+    if (rem >= 8) h = xrotl(h ^ xround(0, w0), 27) * XP1 + XP4;
+    if (rem >= 16) h = xrotl(h ^ xround(0, w1), 27) * XP1 + XP4;
+    if (rem >= 24) h = xrotl(h ^ xround(0, w2), 27) * XP1 + XP4;
+    const uint32_t q8 = rem >> 3;
+    uint64_t wq = q8 == 0 ? w0 : q8 == 1 ? w1 : q8 == 2 ? w2 : w3;
+    if (rem & 4u) {
+        h ^= (uint64_t)(uint32_t)wq * XP1;
+        h = xrotl(h, 23) * XP2 + XP3;
+        wq >>= 32;
+    }
+    const uint32_t nb = rem & 3u;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) w[k] = ((uint64_t)w32[2 * k + 1] << 32) | w32[2 * k];
-    h = xxh64_tail(h, w, rem);
+    for (uint32_t b = 0; b < 3; b++)
+        if (b < nb) {
+            h ^= ((wq >> (8 * b)) & 0xFFu) * XP5;
+            h = xrotl(h, 11) * XP1;
+        }
     return xavalanche(h);
 }
 
-// One wave per (row, object, region) item.  fresh_only: only the objects
-// flagged GPUDIFF_OBJ_FRESH (the object store's newly uploaded blobs; the
-// resident ones were hashed when they arrived).
+constexpr uint32_t K1_VCAP = 512;  // list entries per wave (8 KiB of LDS)
+struct K1Ent {
+    uint64_t aoff;   // value at pool + aoff
+    uint32_t len;
+    uint32_t vback;  // its digest slot at pool + aoff - vback
+};
+
+__device__ __forceinline__ void k1_flush(const K1Ent* E, uint32_t nv, uint8_t* __restrict__ pool, uint32_t lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t k = lane; k < nv; k += 64) {
+        const K1Ent e = E[k];
+        const uint64_t h = xxh64_lane(pool + e.aoff, e.len);
+        *(uint64_t*)(pool + e.aoff - e.vback) = h;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// fresh_only: only the objects flagged GPUDIFF_OBJ_FRESH (the object store's newly uploaded
+// blobs; the resident ones were hashed when they arrived).
 __global__ __launch_bounds__(256) void k_value_hash(const gpudiff_pair_row* __restrict__ rows, uint32_t row_begin,
                                                     uint32_t row_end, uint8_t* __restrict__ pool, bool fresh_only) {
+    __shared__ K1Ent ents[4][K1_VCAP];
     const uint32_t lane = lane_id();
-    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t nitems = (row_end - row_begin) * 4u;
-    for (uint32_t it = wave; it < nitems; it += nwaves) {
-        const gpudiff_pair_row& r = rows[row_begin + (it >> 2)];
-        const bool b = it & 1u, st = it & 2u;
-        if (fresh_only && !((b ? r.flags_b : r.flags_a) & GPUDIFF_OBJ_FRESH)) continue;
-        const uint64_t off = b ? r.off_b : r.off_a;
-        const uint32_t sl = b ? r.spec_l_b : r.spec_l_a, sar = b ? r.spec_ar_b : r.spec_ar_a;
-        const uint32_t L = st ? (b ? r.stat_l_b : r.stat_l_a) : sl;
-        const uint32_t AR = st ? (b ? r.stat_ar_b : r.stat_ar_a) : sar;
-        if (AR == 0 || L == 0) continue;
-        uint8_t* seg = pool + off + (st ? seg_bytes(sl, sar) : 0);
-        uint64_t* vals = (uint64_t*)seg;
-        const uint32_t* metas = (const uint32_t*)(seg + 12ull * L);
-        const uint32_t* arena = (const uint32_t*)(seg + 16ull * L);
-        uint32_t run = 0;  // running arena byte offset
-        for (uint32_t w = 0; w < L; w += 64) {
-            const uint32_t i = w + lane;
-            const uint32_t m = i < L ? metas[i] : 0u;
-            const uint32_t asz = meta_arena(m);
-            const uint32_t incl = wave_incl_scan(asz);
-            if (asz) vals[i] = xxh64_a4(arena + ((run + incl - asz) >> 2), m >> 3, 0);
-            run += shfl32(incl, 63);
+    K1Ent* E = ents[threadIdx.x >> 6];
+    const uint32_t gw = uni(blockIdx.x * 4u + (threadIdx.x >> 6)), nw = gridDim.x * 4u;
+    const uint64_t n = row_end - row_begin;
+    const uint32_t p1 = row_begin + (uint32_t)(n * (gw + 1) / nw);
+    uint32_t next = row_begin + (uint32_t)(n * gw / nw);  // wave-uniform: the range's next unassigned pair
+    uint32_t nv = 0;                                       // wave-uniform: list entries
+    // lane state: the pair (its row fields), the segment being walked (0..3 = A spec, A status,
+    // B spec, B status), the next leaf and the arena bytes before it
+    bool has = false;
+    uint32_t sidx = 4, i = 0, L = 0, run = 0;
+    uint64_t seg = 0;
+    uint64_t off_a = 0, off_b = 0;
+    uint32_t sla = 0, sara = 0, tla = 0, tara = 0, slb = 0, sarb = 0, tlb = 0, tarb = 0, fla = 0, flb = 0;
+    auto next_segment = [&]() {
+        for (;;) {
+            if (++sidx >= 4u) {
+                has = false;
+                return;
+            }
+            const bool b = sidx & 2u, st = sidx & 1u;
+            if (fresh_only && !((b ? flb : fla) & GPUDIFF_OBJ_FRESH)) continue;
+            const uint32_t sl = b ? slb : sla, sar = b ? sarb : sara;
+            const uint32_t l = st ? (b ? tlb : tla) : sl, ar = st ? (b ? tarb : tara) : sar;
+            if (!l || !ar) continue;
+            seg = (b ? off_b : off_a) + (st ? seg_bytes(sl, sar) : 0ull);
+            L = l;
+            i = 0;
+            run = 0;
+            return;
+        }
+    };
+    for (;;) {
+        // lanes without a pair pull the range's next pairs
+        const uint64_t idle = ballot(!has);
+        if (idle && next < p1) {
+            const uint32_t pos = next + popc64(idle & mask_lt(lane));
+            if (!has && pos < p1) {
+                const gpudiff_pair_row& r = rows[pos];
+                off_a = r.off_a;
+                off_b = r.off_b;
+                sla = r.spec_l_a; sara = r.spec_ar_a; tla = r.stat_l_a; tara = r.stat_ar_a;
+                slb = r.spec_l_b; sarb = r.spec_ar_b; tlb = r.stat_l_b; tarb = r.stat_ar_b;
+                fla = r.flags_a; flb = r.flags_b;
+                has = true;
+                sidx = ~0u;  // next_segment() starts at 0
+                next_segment();
+            }
+            next = min(p1, next + popc64(idle));
+        }
+        if (!ballot(has)) {
+            if (next >= p1) break;
+            continue;  // every pulled pair had nothing to hash
+        }
+        // four metas per lane, one 16-B load; each long leaf -> one list entry
+        uint32_t cnt = 0, m[4] = {0, 0, 0, 0};
+        if (has) {
+            const u32x4u mv = *(const u32x4u*)(pool + seg + 12ull * L + 4ull * i);
+            m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                if (i + j >= L) m[j] = 0;
+                cnt += meta_long(m[j]) ? 1u : 0u;
+            }
+        }
+        const uint32_t incl = wave_incl_scan(cnt);
+        uint32_t pos = nv + incl - cnt;
+        if (has) {
+            const uint64_t arena = seg + 16ull * L;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                if (meta_long(m[j])) {
+                    K1Ent e;
+                    e.aoff = arena + run;
+                    e.len = m[j] >> 3;
+                    e.vback = (uint32_t)(16ull * L + run - 8ull * (i + j));
+                    E[pos++] = e;
+                }
+                run += meta_arena(m[j]);
+            }
+            i += 4;
+            if (i >= L) next_segment();
+        }
+        nv += shfl32(incl, 63);
+        if (nv > K1_VCAP - 256u) {
+            k1_flush(E, nv, pool, lane);
+            nv = 0;
         }
     }
+    if (nv) k1_flush(E, nv, pool, lane);
 }
 
 // ---------------------------------------------------------------- K2
@@ -1145,8 +1270,17 @@ hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, 
 hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool,
                              bool fresh_only) {
     if (end <= begin) return hipSuccess;
-    k_value_hash<<<grid_for((uint64_t)(end - begin) * 4, kPersistBlocks), 256, 0, s>>>(rows, begin, end, pool,
-                                                                                        fresh_only);
+    // one resident block per CU per slot the kernel's occupancy allows, and >= 16 pairs per wave
+    static int occ = 0;
+    if (!occ) {
+        int o = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(k_value_hash), 256, 0) !=
+                hipSuccess || o <= 0)
+            o = 4;
+        occ = o;
+    }
+    k_value_hash<<<grid_for(((uint64_t)(end - begin) + 15) / 16, 256u * (uint32_t)occ), 256, 0, s>>>(rows, begin, end,
+                                                                                                   pool, fresh_only);
     return hipGetLastError();
 }
 

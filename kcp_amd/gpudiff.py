@@ -183,7 +183,7 @@ class DeviceView(C.Structure):
 
 class BatchStats(C.Structure):
     _fields_ = [("n_pairs", C.c_uint64), ("pool_bytes", C.c_uint64), ("total_leaves", C.c_uint64),
-                ("compare_bytes", C.c_uint64), ("value_bytes", C.c_uint64)]
+                ("compare_bytes", C.c_uint64), ("value_bytes", C.c_uint64), ("hash_bytes", C.c_uint64)]
 
 
 class Timings(C.Structure):
@@ -205,6 +205,7 @@ SIGNATURES = [
     ("gpudiff_hbatch_free", None, [_P, _P]),
     ("gpudiff_dbatch_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     ("gpudiff_dbatch_append", C.c_int, [_P, _P, _P]),
+    ("gpudiff_dbatch_hash_values", C.c_int, [_P, _P]),
     ("gpudiff_dbatch_reset", C.c_int, [_P, _P]),
     ("gpudiff_dbatch_stats_get", C.c_int, [_P, C.POINTER(BatchStats)]),
     ("gpudiff_dbatch_device_view", C.c_int, [_P, C.POINTER(DeviceView)]),
@@ -394,6 +395,10 @@ class DeviceBatch:
 
     def append(self, hb: HostBatch):
         _chk(_lib.gpudiff_dbatch_append(self.engine.ctx, self.h, hb.h), "gpudiff_dbatch_append")
+
+    def hash_values(self):
+        """K1 over every resident pair (asynchronous; value_hash_ms with timing)."""
+        _chk(_lib.gpudiff_dbatch_hash_values(self.engine.ctx, self.h), "gpudiff_dbatch_hash_values")
 
     def reset(self):
         _chk(_lib.gpudiff_dbatch_reset(self.engine.ctx, self.h), "gpudiff_dbatch_reset")

@@ -210,3 +210,40 @@ class CsrPairs:
                 nd = int(np.count_nonzero(flags[:self.n] & 3))
                 return flags[:self.n], offs[:nd + 1], hs[:m], ks[:m]
             cap *= 4
+
+
+def csr_paths_ptr(pool_ptr: int, rows: np.ndarray, threads: int = 8):
+    """The CPU merge's changed-path CSR of a host batch read in place (pool_ptr = the batch's host pool,
+    rows = its pair rows), split over threads (ctypes drops the GIL): (flags u8[n], offsets
+    u32[n_dirty + 1], hashes u64, kinds u8) in gpudiff_result layout.  Checker only (bench.py's
+    full-size path parity, untimed)."""
+    from concurrent.futures import ThreadPoolExecutor
+    rows = np.ascontiguousarray(rows)
+    n = len(rows)
+    T = max(1, min(threads, n // 4096 + 1))
+    cuts = [n * t // T for t in range(T + 1)]
+
+    def one(t):
+        sub = rows[cuts[t]:cuts[t + 1]]
+        m = len(sub)
+        cap = max(1024, 16 * m)
+        while True:
+            flags = np.zeros(max(m, 1), np.uint8)
+            offs = np.zeros(m + 1, np.uint32)
+            hs = np.zeros(cap, np.uint64)
+            ks = np.zeros(cap, np.uint8)
+            k = lib().oracle_csr_paths(pool_ptr, sub.ctypes.data, m, flags.ctypes.data, offs.ctypes.data,
+                                       hs.ctypes.data, ks.ctypes.data, cap)
+            if k >= 0:
+                nd = int(np.count_nonzero(flags[:m] & 3))
+                return flags[:m], offs[:nd + 1], hs[:k], ks[:k]
+            cap *= 4
+    with ThreadPoolExecutor(T) as ex:
+        parts = list(ex.map(one, range(T)))
+    flags = np.concatenate([p[0] for p in parts]) if n else np.zeros(0, np.uint8)
+    offs, base = [np.zeros(1, np.uint64)], 0
+    for p in parts:
+        offs.append(p[1][1:].astype(np.uint64) + base)
+        base += int(p[1][-1])
+    return (flags, np.concatenate(offs), np.concatenate([p[2] for p in parts]),
+            np.concatenate([p[3] for p in parts]))

@@ -204,6 +204,55 @@ def test_k1_value_hashes_on_device(eng):
     hb.free()
 
 
+def _k1_corpus():
+    """Long values of every length class K1 handles differently: tail-only (9-31 B), whole 128-B bursts
+    and partial ones, values past a burst, a 5 KB value, and one object with 700 long values (its lane
+    fills the wave's list several times); in spec and status segments of both objects."""
+    import random
+    rnd = random.Random(11)
+    out = []
+    for n in list(range(9, 70)) + [95, 96, 97, 127, 128, 129, 130, 159, 160, 161, 255, 256, 257, 511, 512, 513, 5000]:
+        a = {"kind": "ConfigMap", "metadata": {"name": "k1-%d" % n},
+             "data": {"v%d" % j: "".join(rnd.choice("abcdefgh\u00e9") for _ in range(n + j)) for j in range(3)},
+             "status": {"s": "x" * (n + 5), "short": "y" * 7}}
+        b = json.loads(json.dumps(a))
+        b["data"]["v1"] = b["data"]["v1"][::-1]
+        out.append((json.dumps(a).encode(), json.dumps(b).encode()))
+    many = {"kind": "Big", "metadata": {"name": "many"}, "spec": {"k%04d" % j: "v" * (9 + j % 200) for j in range(700)}}
+    out.append((json.dumps(many).encode(), json.dumps(many).encode()))
+    return out
+
+
+@pytest.mark.parametrize("n_pairs", [1, 37, 3000])
+def test_k1_digests_equal_host_encoder(eng, n_pairs):
+    """K1's pool after ingest is byte-identical to the host encoder's with host-side XXH64 digests (every
+    segment of both objects: digests in place, nothing else touched), and a stand-alone K1 pass over the
+    resident batch (gpudiff_dbatch_hash_values) rewrites the same bytes."""
+    pairs, _, _ = make_pairs(n_pairs, seed=70 + n_pairs, mutate_frac=0.2)
+    if n_pairs > 1:
+        pairs = _k1_corpus() + pairs
+    host = G.Engine(device=G.DEVICE_NONE, host_value_hash=True)
+    ref = host.encode(pairs)
+    hb = eng.encode(pairs)
+    info = hb.info()
+    assert info.pool_bytes == ref.info().pool_bytes
+    db = eng.device_batch(info.pool_bytes + 1024, len(pairs))
+    db.append(hb)
+    eng.sync()
+    want = ref.pool()
+    assert db.read_pool(0, info.pool_bytes) == want
+    assert db.stats().hash_bytes > 0
+    db.hash_values()
+    eng.sync()
+    assert db.read_pool(0, info.pool_bytes) == want
+    res = eng.wait(eng.diff(db))
+    assert_matches(res, pairs)
+    db.free()
+    hb.free()
+    ref.free()
+    host.close()
+
+
 def test_append_chunks_and_rediff(eng):
     pairs, cl, _ = make_pairs(1500, seed=8, mutate_frac=0.1)
     chunks = [pairs[0:100], pairs[100:900], pairs[900:]]

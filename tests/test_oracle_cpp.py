@@ -78,3 +78,27 @@ def test_xxh64_ref_matches_xxhash():
         comp = b"\x01" + len(key.encode()).to_bytes(4, "little") + key.encode()
         assert hs.tolist() == [xxhash.xxh64_intdigest(comp, seed=seed) & 0xFFFFFFFF], key  # reported at 32 bits
         d.close()
+
+
+def test_csr_paths_ptr_threads_equal_single_pass():
+    """bench.py's full-size path check (cpu_ref.csr_paths_ptr: the CPU merge over a host batch in place,
+    split over threads) equals the single-threaded CSR checker and the oracle's paths."""
+    from kcp_amd import gpudiff as G
+    from oracle import cpu_ref
+    from tests.parity import expected_paths, oracle_batch
+    from tests.workload import make_pairs
+    pairs, _, _ = make_pairs(9000, seed=31, mutate_frac=0.2)
+    e = G.Engine(device=G.DEVICE_NONE, encode_threads=4, host_value_hash=True)
+    hb = e.encode(pairs)
+    rows = hb.rows()
+    f1, o1, h1, k1 = cpu_ref.CsrPairs(hb.pool(), rows).paths()
+    f2, o2, h2, k2 = cpu_ref.csr_paths_ptr(hb.info().pool, rows, threads=5)
+    assert np.array_equal(f1, f2) and np.array_equal(o1.astype(np.int64), o2.astype(np.int64))
+    assert np.array_equal(h1, h2) and np.array_equal(k1, k2)
+    exp = oracle_batch(pairs[:800])
+    dirty = [i for i in range(800) if f2[i] & 3]
+    for j, i in enumerate(dirty):
+        got = list(zip(h2[o2[j]:o2[j + 1]].tolist(), k2[o2[j]:o2[j + 1]].tolist()))
+        assert got == expected_paths(exp[i])
+    hb.free()
+    e.close()
