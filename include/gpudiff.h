@@ -115,6 +115,8 @@ enum {
                                            in 64-pair chunks (0: the default, 2 quarters; t = 1: no tail,
                                            the last two rounds of tickets fetched late) */
 #define GPUDIFF_OPT_K2_TAIL8 0x80u      /* tuning: tail items of 8 pairs instead of half a main item */
+#define GPUDIFF_OPT_K1_VARIANT_SHIFT 30u /* 2 bits: value-hash kernel (0: LDS windows of 4 KiB, 1: 8 KiB windows,
+                                            2: values read by their lanes straight from HBM, 3: 2 KiB windows) */
 #define GPUDIFF_OPT_K2_ITEMS_SHIFT 28u   /* 2 bits: decision-kernel items per resident wave before 64-pair
                                             chunks are split (0: default 8, 1: 4, 2: 8, 3: 16) */
 
@@ -323,6 +325,8 @@ typedef struct gpudiff_store_stats {
     float submit_wait_ms, submit_docs_ms, submit_copy_ms, submit_enqueue_ms, finish_ms;
     uint32_t timing_batches; /* batches the means are over */
     uint32_t pad;
+    uint64_t space_conservative; /* device-encode: deferred events reported dirty (GPUDIFF_DECODE_ERROR, slot
+                                    emptied) because the space could not take their re-encoded blobs */
 } gpudiff_store_stats;
 
 int gpudiff_store_create(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,

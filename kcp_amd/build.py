@@ -17,7 +17,7 @@ SOURCES = ["kernels.hip", "tokenize.hip", "rollup.hip", "negotiate.hip", "dstore
            "encoder.cpp", "json.cpp"]
 SYNTH_SOURCES = ["synth.cpp", "encoder.cpp", "json.cpp"]
 SYNTH_LIB = os.path.join(HERE, "libgpudiff_synth.so")
-HEADERS = ["kernels.h", "tokenize.h", "tokdev.h", "marshal_phases.inc", "rollup_phases.inc", "negotiate_phases.inc", "goscan.h", "rollup.h", "ryu_tables.h", "dstore.h", "decfloat.h", "pow10_128.h", "encoder.h", "engine.h", "json.h", "xxh64.h"]
+HEADERS = ["kernels.h", "pool.h", "tokenize.h", "tokdev.h", "marshal_phases.inc", "rollup_phases.inc", "negotiate_phases.inc", "goscan.h", "rollup.h", "ryu_tables.h", "dstore.h", "decfloat.h", "pow10_128.h", "encoder.h", "engine.h", "json.h", "xxh64.h"]
 INCLUDES = [os.path.join(ROOT, "include", h) for h in ("gpudiff.h", "gpudiff_format.h", "gpudiff_synth.h")]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}",
           "-I" + os.path.join(ROOT, "include")]

@@ -418,7 +418,7 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
     HIPCHK(launch_rebase(c->stream, d->rows, begin, end, base, d->pair_ids));
     if (!c->ecfg.host_value_hash && !(c->flags & GPUDIFF_OPT_NO_VALUE_HASH)) {
         if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
-        HIPCHK(launch_value_hash(c->stream, d->rows, begin, end, d->pool));
+        HIPCHK(launch_value_hash(c->stream, d->rows, begin, end, d->pool, false, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
         if (c->flags & GPUDIFF_OPT_TIMING) {
             HIPCHK(hipEventRecord(c->ev_k1[1], c->stream));
             c->k1_recorded = true;
@@ -470,7 +470,7 @@ int gpudiff_dbatch_hash_values(gpudiff_ctx* c, gpudiff_dbatch* d) {
     if (rc) return rc;
     if (c->ecfg.host_value_hash || (c->flags & GPUDIFF_OPT_NO_VALUE_HASH) || !d->n_pairs) return GPUDIFF_OK;
     if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
-    HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)d->n_pairs, d->pool));
+    HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)d->n_pairs, d->pool, false, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
     if (c->flags & GPUDIFF_OPT_TIMING) {
         HIPCHK(hipEventRecord(c->ev_k1[1], c->stream));
         c->k1_recorded = true;

@@ -405,7 +405,56 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
     // place: blobs behind the append point, rows, slot states
     const uint64_t pbytes = (pool.size() + GPUDIFF_BLOB_ALIGN - 1) & ~(uint64_t)(GPUDIFF_BLOB_ALIGN - 1);
     pool.resize(pbytes, 0);
-    if ((rc = ensure_space(s, pbytes, pbytes))) return rc;
+    if ((rc = ensure_space(s, pbytes, pbytes))) {
+        if (rc != GPUDIFF_E_CAPACITY) return rc;
+        // The space cannot take the re-encoded blobs even after a compaction (K0 deferred these
+        // events for lack of space, and the host's blobs do not fit either).  The store stays
+        // usable: the events are reported dirty with GPUDIFF_DECODE_ERROR (the reference's
+        // conservative rule, specsyncer.go:20-22: never "equal") and their slots are emptied, so
+        // each slot's next event stages its old object again.
+        for (SlotUpdate& u : ups) {
+            memset(&u.entry, 0, sizeof(u.entry));
+            s->seen[u.slot] = 0;
+        }
+        if ((rc = grow_dev(&s->res_ups, &s->res_ups_cap, std::max<size_t>(ups.size(), 1)))) return rc;
+        if (!ups.empty()) HIPCHK(hipMemcpy(s->res_ups, ups.data(), ups.size() * sizeof(SlotUpdate), hipMemcpyHostToDevice));
+        HIPCHK(hipMemsetAsync(s->res_err, 0, 4, c->stream));
+        HIPCHK(launch_place(c->stream, nullptr, 0, s->space[s->cur], s->used_dev, s->space_bytes, nullptr, nullptr, 0,
+                            s->res_ups, (uint32_t)ups.size(), s->slots, s->ctr, s->res_err));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        s->st.space_conservative += drows.size();
+        ResultStore out;
+        out.flags.resize(R.nev);
+        out.off.push_back(0);
+        size_t jr = 0;
+        for (uint32_t i = 0; i < R.nev; i++) {
+            uint8_t f = rs.flags[i];
+            uint32_t lo = 0, hi = 0;
+            if (f & (GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY)) {
+                lo = rs.off[jr];
+                hi = rs.off[jr + 1];
+                jr++;
+            }
+            if (def[i]) {
+                f = GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY | GPUDIFF_DECODE_ERROR;
+                lo = hi = 0;
+            }
+            out.flags[i] = f;
+            const uint32_t pid = R.events[i].pair_id;
+            if (f & GPUDIFF_SPEC_DIRTY) out.spec.push_back(pid);
+            if (f & GPUDIFF_STATUS_DIRTY) out.status.push_back(pid);
+            if (f & (GPUDIFF_SPEC_DIRTY | GPUDIFF_STATUS_DIRTY)) {
+                out.dirty.push_back(pid);
+                for (uint32_t q = lo; q < hi; q++) {
+                    out.hashes.push_back(rs.hashes[q]);
+                    out.kinds.push_back(rs.kinds[q]);
+                }
+                out.off.push_back((uint32_t)out.hashes.size());
+            }
+        }
+        rs = std::move(out);
+        return GPUDIFF_OK;
+    }
     if ((rc = grow_dev(&s->res_stage, &s->res_stage_cap, std::max<uint64_t>(pbytes, 16)))) return rc;
     if ((rc = grow_dev(&s->res_ups, &s->res_ups_cap, std::max<size_t>(ups.size(), 1)))) return rc;
     gpudiff_dbatch* d = s->res_d;

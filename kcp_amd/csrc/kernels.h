@@ -60,7 +60,7 @@ uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks);
 hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
                          uint32_t* pair_ids);
 hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool,
-                             bool fresh_only = false);
+                             bool fresh_only = false, uint32_t variant = 0);
 // object-store compaction: blob copies between the two spaces
 struct BlobMove {
     uint64_t src, dst, bytes;

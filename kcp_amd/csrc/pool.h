@@ -41,6 +41,7 @@ class WorkerPool {
             T_ = T;
             left_ = T - 1;
             gen_++;
+            worker_ex_ = nullptr;
         }
         cv_.notify_all();
         std::exception_ptr ex;
@@ -53,6 +54,8 @@ class WorkerPool {
             std::unique_lock<std::mutex> g(m_);
             done_.wait(g, [&] { return left_ == 0; });
             job_ = nullptr;
+            if (!ex) ex = worker_ex_;  // a worker's exception (e.g. std::bad_alloc) reaches the caller too
+            worker_ex_ = nullptr;
         }
         if (ex) std::rethrow_exception(ex);
     }
@@ -70,8 +73,14 @@ class WorkerPool {
                 if (t >= T_) continue;  // not part of this run
                 job = job_;
             }
-            (*job)(t);
+            std::exception_ptr ex;
+            try {
+                (*job)(t);
+            } catch (...) {
+                ex = std::current_exception();  // never leaves the thread (std::terminate): run() rethrows it
+            }
             std::lock_guard<std::mutex> g(m_);
+            if (ex && !worker_ex_) worker_ex_ = ex;
             if (--left_ == 0) done_.notify_one();
         }
     }
@@ -82,6 +91,7 @@ class WorkerPool {
     uint32_t T_ = 0, left_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+    std::exception_ptr worker_ex_;  // the first exception a worker thread threw in the current run
 };
 
 }  // namespace gd

@@ -418,7 +418,7 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
     if (n) {
         HIPCHK(launch_rebase(c->stream, d->rows, 0, (uint32_t)n, 0, d->pair_ids));  // pair_ids SoA copy
         if (!c->ecfg.host_value_hash && !(c->flags & GPUDIFF_OPT_NO_VALUE_HASH))
-            HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)n, space, true));
+            HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)n, space, true, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
     }
     s->used += total;
     d->pool = space;

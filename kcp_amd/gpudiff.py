@@ -102,7 +102,7 @@ class StoreStats(C.Structure):
                 ("host_submit_ms", C.c_float), ("h2d_ms", C.c_float), ("encode_ms", C.c_float),
                 ("link_ms", C.c_float), ("submit_wait_ms", C.c_float), ("submit_docs_ms", C.c_float),
                 ("submit_copy_ms", C.c_float), ("submit_enqueue_ms", C.c_float), ("finish_ms", C.c_float),
-                ("timing_batches", C.c_uint32), ("pad", C.c_uint32)]
+                ("timing_batches", C.c_uint32), ("pad", C.c_uint32), ("space_conservative", C.c_uint64)]
 
 
 class ObjInfo(C.Structure):

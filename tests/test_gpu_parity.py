@@ -223,11 +223,13 @@ def _k1_corpus():
     return out
 
 
+@pytest.mark.parametrize("k1_variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("n_pairs", [1, 37, 3000])
-def test_k1_digests_equal_host_encoder(eng, n_pairs):
+def test_k1_digests_equal_host_encoder(n_pairs, k1_variant):
     """K1's pool after ingest is byte-identical to the host encoder's with host-side XXH64 digests (every
     segment of both objects: digests in place, nothing else touched), and a stand-alone K1 pass over the
-    resident batch (gpudiff_dbatch_hash_values) rewrites the same bytes."""
+    resident batch (gpudiff_dbatch_hash_values) rewrites the same bytes.  Every K1 tuning variant."""
+    eng = G.Engine(device=0, encode_threads=8, flags=k1_variant << 30)
     pairs, _, _ = make_pairs(n_pairs, seed=70 + n_pairs, mutate_frac=0.2)
     if n_pairs > 1:
         pairs = _k1_corpus() + pairs
@@ -251,6 +253,7 @@ def test_k1_digests_equal_host_encoder(eng, n_pairs):
     hb.free()
     ref.free()
     host.close()
+    eng.close()
 
 
 def test_append_chunks_and_rediff(eng):

@@ -279,3 +279,54 @@ def test_device_encode_deferrals_exact(drop_old):
             assert s.deferred > 0
         st.free()
         e.close()
+
+
+def test_device_store_space_pressure_stays_usable():
+    """under space pressure K0 defers documents that do not fit (SPACE) and the
+    host's re-encoded blobs may not fit either; those events must come back dirty (DECODE_ERROR, never
+    "equal", slot emptied) and the store must stay usable -- every other event exact, later batches
+    exact."""
+    e = G.Engine(device=0, encode_threads=4)
+    st = e.object_store(max_slots=64, space_bytes=192 << 10, max_events=64, device_encode=True)
+    rnd = random.Random(17)
+    objs = [crd(rnd, i, i % 3, 60) for i in range(60)]
+    docs = [json.dumps(o, separators=(",", ":")).encode() for o in objs]
+    assert 100 << 10 < sum(len(d) for d in docs) < 192 << 10  # the JSON fits, its blobs + tables do not
+    res = e.wait(st.submit([(i, d, None) for i, d in enumerate(docs)]))
+    pairs = [(b"{}", d) for d in docs]
+    from tests.parity import oracle_batch, expected_flags, expected_paths
+    exp = oracle_batch(pairs)
+    cons = 0
+    dirty = 0
+    for i, r in enumerate(exp):
+        f = int(res.pair_flags[i])
+        if f == G.SPEC_DIRTY | G.STATUS_DIRTY | G.DECODE_ERROR:
+            cons += 1
+            assert res.paths_of(dirty) == []
+        else:
+            assert f == expected_flags(r), i
+            assert res.paths_of(dirty) == expected_paths(r), i
+        if f & (G.SPEC_DIRTY | G.STATUS_DIRTY):
+            dirty += 1
+    s = st.stats()
+    assert cons > 0 and s.space_conservative == cons
+    # the store goes on: forget most slots, then small batches are exact again
+    for i in range(8, 64):
+        st.forget(i)
+    rnd2 = random.Random(18)
+    for b in range(3):
+        items, pairs = [], []
+        for i in range(8):
+            o = _next_version(rnd2, objs[i])
+            nj = json.dumps(o, separators=(",", ":")).encode()
+            items.append((i, nj, docs[i]))
+            pairs.append((docs[i] if b == 0 else prev[i], nj))
+        prev = {i: it[1] for i, it in enumerate(items)}
+        r = e.wait(st.submit(items))
+        # a slot emptied by the conservative path stages the event's old object again: same as the oracle's
+        assert_matches(r, pairs)
+        for i in range(8):
+            objs[i] = json.loads(prev[i])
+        docs = [prev[i] for i in range(8)]
+    st.free()
+    e.close()

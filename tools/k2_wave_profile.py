@@ -4,7 +4,7 @@ Ingests config3 (optionally resized) like bench.py, times the default K2 (varian
 variant 14 -- the same kernel plus wall-clock stamps (100 MHz) -- recording per wave: start, end of
 its first item, items taken, start of its last item, end, ticks spent streaming and in the join.
 
-    python tools/k2_wave_profile.py --pairs 1250000 [--passes 5] > out.json
+    python tools/k2_wave_profile.py --pairs 1250000 [--passes 5] [--config config4 --flags 0xF00000] > out.json
 """
 import argparse
 import json
@@ -25,6 +25,8 @@ def pct(a, qs=(0, 1, 5, 25, 50, 75, 95, 99, 100)):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=1250000)
+    ap.add_argument("--config", default="config3")
+    ap.add_argument("--flags", type=lambda x: int(x, 0), default=0, help="extra engine flags (e.g. 0xF << 21: every join in K4)")
     ap.add_argument("--passes", type=int, default=5)
     ap.add_argument("--threads", type=int, default=16)
     args = ap.parse_args()
@@ -35,16 +37,16 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
-    cfg = S.make_cfg("config3", n_pairs=args.pairs, n_clusters=max(1, args.pairs // 100))
+    cfg = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=max(1, args.pairs // 100))
     pop = S.Population(cfg, 1, 0)
     n = pop.n
     out = {"pairs": n}
     for variant in (0, 14):
         eng = G.Engine(device=0, encode_threads=args.threads, stream=stream.cuda_stream, timing=True,
-                       flags=variant << 8)
+                       flags=(variant << 8) | args.flags)
         first = pop.chunk(eng, 0, min(262144, n), args.threads)
         per_pair = first.pool_bytes / max(1, min(262144, n))
-        db = eng.device_batch(int(per_pair * n * 1.15) + (64 << 20), n)
+        db = eng.device_batch(int(per_pair * n * (1.4 if args.config == "config4" else 1.15)) + (64 << 20), n)
         db.append(first.hb)
         pos, k, stage = first.truth.size, 1, [first.hb, None]
         while pos < n:
@@ -61,7 +63,8 @@ def main():
             eng.diff(db)
         eng.sync()
         tm = eng.timings()
-        rec = {"k2_ms": tm.compare_ms, "pass_ms": tm.total_ms}
+        rec = {"k2_ms": tm.compare_ms, "pass_ms": tm.total_ms, "join_ms": tm.join_ms, "emit_ms": tm.emit_ms,
+               "compact_ms": tm.compact_ms, "format_bytes": db.stats().compare_bytes}
         if variant == 14:
             cap = 1 << 16
             buf = torch.zeros(cap * 8, dtype=torch.int64, device=dev)
