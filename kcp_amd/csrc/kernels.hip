@@ -371,7 +371,7 @@ __device__ __forceinline__ uint32_t lane_upper(uint32_t v, uint32_t x) {
 constexpr uint32_t K1_WLEAVES = 256;  // leaves per window (4 metas per lane)
 
 template <uint32_t W>
-struct K1Lds {
+struct alignas(16) K1Lds {
     uint32_t img[W / 4];        // the window's staged arena ranges
     uint32_t vpos[K1_WLEAVES];  // long value: LDS byte offset | len << 16
     uint64_t vdig[K1_WLEAVES];  // its digest slot (pool byte offset)
@@ -525,11 +525,13 @@ __global__ __launch_bounds__(256) void k_value_hash_win(const gpudiff_pair_row* 
 #pragma unroll
             for (uint32_t r = 0; r < R; r++) {
                 const uint32_t c = r * 64u + lane;
+                // cross-lane reads with every lane active (ds_bpermute returns nothing useful from an
+                // inactive source lane), the load only where there is a chunk
+                const uint32_t o = min(lane_upper(chincl, c), 63u);
+                const uint32_t k = c - (shfl32(chincl, o) - shfl32(nch, o));
+                const uint64_t src = shfl64(seg_off, o) + 16ull * shfl32(L, o) + shfl32(c0, o) + 16ull * k;
                 dst[r] = ~0u;
                 if (c < nchunks) {
-                    const uint32_t o = min(lane_upper(chincl, c), 63u);
-                    const uint32_t k = c - (shfl32(chincl, o) - shfl32(nch, o));
-                    const uint64_t src = shfl64(seg_off, o) + 16ull * shfl32(L, o) + shfl32(c0, o) + 16ull * k;
                     v[r] = __builtin_nontemporal_load((const u32x4*)(pool + src));
                     dst[r] = c * 4u;
                 }
