@@ -382,6 +382,9 @@ int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
  * item, items, start of the last item, end, streaming ticks, join ticks, hardware CU id; 100 MHz)
  * into device memory dev_buf of cap_waves records; dev_buf NULL stops recording */
 int gpudiff_k2_profile(gpudiff_ctx* ctx, uint64_t* dev_buf, uint32_t cap_waves);
+/* diagnostics: the windowed K1's first wave records 12 u32 per window (batch, cursor, window size,
+ * cut, last segment, chunks, values, next cursor) into dev_buf (cap records); NULL stops */
+int gpudiff_k1_trace(gpudiff_ctx* ctx, uint32_t* dev_buf, uint32_t cap);
 
 /* ---- write path: the request body for a dirty object ----
  * GPUDIFF_UPSERT_SPEC: what upsertIntoDownstream hands to client.Create

@@ -114,6 +114,15 @@ int gpudiff_encode_objects(gpudiff_ctx* c, const uint8_t* const* docs, const siz
     return GPUDIFF_OK;
 }
 
+int gpudiff_k1_trace(gpudiff_ctx* c, uint32_t* dev_buf, uint32_t cap) {
+    if (!c) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(k1_trace(dev_buf, cap));
+    return GPUDIFF_OK;
+}
+
 int gpudiff_k2_profile(gpudiff_ctx* c, uint64_t* dev_buf, uint32_t cap_waves) {
     if (!c) return GPUDIFF_E_INVAL;
     int rc = set_device(c);

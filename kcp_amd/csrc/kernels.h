@@ -79,5 +79,6 @@ hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
 // tuning: K2 variant 14 writes 8 u64 per wave (start, first item end, items, last item start, end,
 // streaming ticks, join ticks, hw id) into dev_buf (cap_waves waves); nullptr disables
 hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves);
+hipError_t k1_trace(uint32_t* dev_buf, uint32_t cap);
 
 }  // namespace gd

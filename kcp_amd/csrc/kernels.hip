@@ -370,6 +370,10 @@ __device__ __forceinline__ uint32_t lane_upper(uint32_t v, uint32_t x) {
 
 constexpr uint32_t K1_WLEAVES = 256;  // leaves per window (4 metas per lane)
 
+// diagnostics (gpudiff_k1_trace): wave 0 of the windowed K1 records 12 u32 per window
+__device__ uint32_t* g_k1_trace;
+__device__ uint32_t g_k1_trace_cap;
+
 template <uint32_t W>
 struct alignas(16) K1Lds {
     uint32_t img[W / 4];        // the window's staged arena ranges
@@ -388,6 +392,7 @@ __global__ __launch_bounds__(256) void k_value_hash_win(const gpudiff_pair_row* 
     const uint32_t gw = uni(blockIdx.x * 4u + (threadIdx.x >> 6)), nw = gridDim.x * 4u;
     const uint64_t n = row_end - row_begin;
     const uint32_t P0 = row_begin + (uint32_t)(n * gw / nw), P1 = row_begin + (uint32_t)(n * (gw + 1) / nw);
+    uint32_t ntrace = 0;
     for (uint32_t pb0 = P0; pb0 < P1; pb0 += 16) {
         // ---- this batch's segments with long values: lane j holds segment j
         uint32_t cnt = 0;
@@ -506,7 +511,8 @@ __global__ __launch_bounds__(256) void k_value_hash_win(const gpudiff_pair_row* 
 #pragma unroll
             for (uint32_t u = 0; u < 4; u++) {  // the end of each segment's last window leaf
                 const uint32_t g = u * 64u + lane;
-                const bool last = g < gcut && (g == glast || g + 1u == shfl32(lincl, own[u]));
+                const uint32_t oend_g = shfl32(lincl, own[u]);  // (not inside the && below: every lane must read)
+                const bool last = g < gcut && (g == glast || g + 1u == oend_g);
                 if (last) S.pb[own[u]] = off[u] + asz[u];  // (pb no longer needed: reuse it for hi)
             }
             wave_sync_lds();
@@ -564,6 +570,15 @@ __global__ __launch_bounds__(256) void k_value_hash_win(const gpudiff_pair_row* 
             // advance the cursor past leaf glast
             const uint32_t llast = uni(shfl32(leaf[glast >> 6], glast & 63u));
             const uint32_t oend = uni(shfl32(off[glast >> 6] + asz[glast >> 6], glast & 63u));
+            if (g_k1_trace && gw == 0) {
+                const uint32_t v0 = S.vpos[0];
+                if (lane == 0 && ntrace < g_k1_trace_cap) {
+                    uint32_t* t = g_k1_trace + 12u * ntrace;
+                    t[0] = pb0; t[1] = cs; t[2] = cl; t[3] = ca; t[4] = G; t[5] = gcut; t[6] = jl; t[7] = nchunks;
+                    t[8] = nv; t[9] = llast; t[10] = oend; t[11] = v0;
+                }
+                ntrace++;
+            }
             if (llast + 1u >= uni(shfl32(L, jl))) {
                 cs = jl + 1u;
                 cl = 0;
@@ -1459,6 +1474,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             r[7] = (uint64_t)__smid();
         }
     }
+}
+
+hipError_t k1_trace(uint32_t* dev_buf, uint32_t cap) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_k1_trace), &dev_buf, sizeof(dev_buf));
+    if (e != hipSuccess) return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_k1_trace_cap), &cap, sizeof(cap));
 }
 
 hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves) {

@@ -235,6 +235,7 @@ SIGNATURES = [
                                              C.POINTER(ObjInfo)]),
     ("gpudiff_k0_profile", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
     ("gpudiff_k2_profile", C.c_int, [_P, C.c_void_p, C.c_uint32]),
+    ("gpudiff_k1_trace", C.c_int, [_P, C.c_void_p, C.c_uint32]),
     ("gpudiff_upsert_bodies", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
                                         C.POINTER(Bodies)]),
     ("gpudiff_bodies_release", None, [_P, C.POINTER(Bodies)]),
@@ -720,6 +721,10 @@ class Engine:
         out = (C.c_uint64 * 8)()
         _chk(_lib.gpudiff_k0_profile(self.ctx, 1 if enable else 0, out), "gpudiff_k0_profile")
         return list(out)
+
+    def k1_trace(self, dev_ptr: int, cap: int):
+        """Record the windowed K1's first-wave window trace (12 u32 per window) into device memory."""
+        _chk(_lib.gpudiff_k1_trace(self.ctx, dev_ptr or None, cap), "gpudiff_k1_trace")
 
     def k2_profile(self, dev_ptr: int, cap_waves: int):
         """Record K2 variant 14's per-wave timeline into device memory (8 u64 per wave); 0 stops."""
