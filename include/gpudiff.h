@@ -96,7 +96,12 @@ enum {
 
 /* context option flags */
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
-#define GPUDIFF_OPT_HOST_VALUE_HASH 0x2u /* hash long values on the host instead of K1 */
+#define GPUDIFF_OPT_HOST_VALUE_HASH 0x2u /* hash long values in the host encoder (the default since ABI 3; kept
+                                            for callers that set it) */
+#define GPUDIFF_OPT_DEVICE_VALUE_HASH 0x8u /* hash long values with kernel K1 after each H2D instead of in the
+                                              host encoder (XXH64 is multiply-bound on CDNA --
+                                              no 64-bit integer multiplier -- so the host encoder, which reads
+                                              every byte anyway, is the cheaper place) */
 #define GPUDIFF_OPT_NO_VALUE_HASH 0x4u   /* tests: leave value digests 0 so every equal-length
                                             long value goes through byte confirmation (the
                                             path a digest collision would take) */
@@ -231,12 +236,11 @@ int gpudiff_dbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, uint64_t max_pa
                           gpudiff_dbatch** out);
 /* async H2D of hb into the batch + K1 value hashing of the new objects */
 int gpudiff_dbatch_append(gpudiff_ctx* ctx, gpudiff_dbatch* db, const gpudiff_hbatch* hb);
-/* K1 over every pair already resident (the value digests gpudiff_dbatch_append computes per
- * chunk at ingest), on the context's stream, asynchronous; with GPUDIFF_OPT_TIMING its duration is
- * value_hash_ms.  The digests it writes equal those already there: this is the ingest hashing step
- * as a stand-alone pass, so a caller can time "hash then diff" over a population that is new in
- * every step.  No-op for a context that hashes on the host (GPUDIFF_OPT_HOST_VALUE_HASH /
- * GPUDIFF_OPT_NO_VALUE_HASH). */
+/* K1 over every pair already resident, on the context's stream, asynchronous; with
+ * GPUDIFF_OPT_TIMING its duration is value_hash_ms.  The digests it writes equal those the encoder
+ * (or K1 at ingest, GPUDIFF_OPT_DEVICE_VALUE_HASH) already wrote: this is the GPU hashing step as a
+ * stand-alone pass, so a caller can time "hash then diff" over a population that is new in every
+ * step.  No-op with GPUDIFF_OPT_NO_VALUE_HASH. */
 int gpudiff_dbatch_hash_values(gpudiff_ctx* ctx, gpudiff_dbatch* d);
 int gpudiff_dbatch_reset(gpudiff_ctx* ctx, gpudiff_dbatch* db);
 int gpudiff_dbatch_stats_get(const gpudiff_dbatch* db, gpudiff_batch_stats* st);

@@ -104,6 +104,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     }
     b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
     b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
+    b.avg_pair_bytes = d->n_pairs ? d->compare_bytes / d->n_pairs : 0;
     return b;
 }
 
@@ -151,7 +152,9 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
     c->ecfg.hash_bits = (o.path_hash_bits == 0 || o.path_hash_bits >= GPUDIFF_PATH_HASH_BITS) ? GPUDIFF_PATH_HASH_BITS
                                                                                             : o.path_hash_bits;
     if (c->ecfg.hash_bits < 8) return GPUDIFF_E_INVAL;
-    c->ecfg.host_value_hash = (o.flags & GPUDIFF_OPT_HOST_VALUE_HASH) != 0;
+    // value digests: in the host encoder unless K1 is asked for (GPUDIFF_OPT_DEVICE_VALUE_HASH)
+    c->ecfg.host_value_hash = !(o.flags & GPUDIFF_OPT_NO_VALUE_HASH) &&
+                              (!(o.flags & GPUDIFF_OPT_DEVICE_VALUE_HASH) || (o.flags & GPUDIFF_OPT_HOST_VALUE_HASH));
     c->hash_mask = c->ecfg.hash_bits >= 64 ? ~0ULL : ((1ULL << c->ecfg.hash_bits) - 1);
     if (o.device != GPUDIFF_DEVICE_NONE) {
         int n = 0;
@@ -468,7 +471,7 @@ int gpudiff_dbatch_hash_values(gpudiff_ctx* c, gpudiff_dbatch* d) {
     if (!c || !d) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
-    if (c->ecfg.host_value_hash || (c->flags & GPUDIFF_OPT_NO_VALUE_HASH) || !d->n_pairs) return GPUDIFF_OK;
+    if ((c->flags & GPUDIFF_OPT_NO_VALUE_HASH) || !d->n_pairs) return GPUDIFF_OK;
     if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
     HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)d->n_pairs, d->pool, false, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
     if (c->flags & GPUDIFF_OPT_TIMING) {

@@ -1669,15 +1669,26 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : (uint32_t)occ[v]);
 }
 
-// 64-pair chunks split into 2^k items until there are >= 4 items per resident
-// wave (config3's 156k chunks: k = 0; config4's 1.6k chunks of deep pairs: k = 4)
+// Deep pairs (>= 16 KiB of compared bytes on average: config4's 8-64 KiB objects) are split down to
+// single-pair items, >= 24 per resident wave: with 8-pair items a config4 wave had 2-5 items of
+// ~0.5 MB each and the pass ended ~0.5 ms after the median wave (tools/k2_wave_profile.py,
+// profiles/r03e/wave_c4.json: 68% of the span busy)
+constexpr uint64_t kK2BigPairBytes = 16384;
+constexpr uint32_t kK2ItemsPerWaveBig = 24, kK2MaxSubShiftBig = 6;
+
+// 64-pair chunks split into 2^k items until there are >= kK2ItemsPerWave items per resident wave
+// (config3's 156k chunks: k = 0; deep pairs: see above)
 static uint32_t k2_sub_shift(const DiffBuffers& b, uint32_t nchunks) {
-    const uint64_t want = (uint64_t)(b.k2_items_per_wave ? b.k2_items_per_wave : kK2ItemsPerWave) * 4u * k2_cap_blocks(b);
+    const bool big = b.avg_pair_bytes >= kK2BigPairBytes;
+    const uint64_t want = (uint64_t)(b.k2_items_per_wave ? b.k2_items_per_wave
+                                                         : (big ? kK2ItemsPerWaveBig : kK2ItemsPerWave)) *
+                          4u * k2_cap_blocks(b);
+    const uint32_t max_shift = big ? kK2MaxSubShiftBig : kK2MaxSubShift;
     // items of at least 8 pairs: a small batch (a watch-replay batch of 64k events: 1k chunks) split
     // further than that pays a row load, a prefix sum and a ticket per 2-4 pairs (config5: K2 0.42 ms
     // at 2-pair items vs 0.26 at 4 -- profiles/r02zy)
     uint32_t k = 0;
-    while (k < kK2MaxSubShift && (uint64_t)nchunks << k < want) k++;
+    while (k < max_shift && (uint64_t)nchunks << k < want) k++;
     return k;
 }
 

@@ -23,7 +23,7 @@ E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUN
 SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR, SPEC_NOOP, STATUS_NOOP = 0x1, 0x2, 0x4, 0x8, 0x10
 PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
-OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH = 0x1, 0x2, 0x4
+OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH, OPT_DEVICE_VALUE_HASH = 0x1, 0x2, 0x4, 0x8
 OPT_DEVICE_ENCODE = 0x2000000
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
@@ -517,9 +517,13 @@ class Engine:
 
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
                  timing: bool = False, path_hash_bits: int = PATH_HASH_BITS, host_value_hash: bool = False,
-                 no_value_hash: bool = False, flags: int = 0, device_encode: bool = False):
+                 no_value_hash: bool = False, flags: int = 0, device_encode: bool = False,
+                 device_value_hash: bool = False):
+        """Value digests of long strings come from the host encoder by default; device_value_hash=True
+        hashes them with kernel K1 after each upload instead."""
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
                  flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0) |
+                       (OPT_DEVICE_VALUE_HASH if device_value_hash else 0) |
                        (OPT_NO_VALUE_HASH if no_value_hash else 0) | (OPT_DEVICE_ENCODE if device_encode else 0) |
                        flags,
                  path_hash_bits=path_hash_bits)

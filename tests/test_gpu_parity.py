@@ -149,8 +149,9 @@ def test_forced_collisions(dev):
 
 
 def test_host_vs_device_value_hash(eng):
+    """Digests from the host encoder (the default) and from K1 at ingest give identical results."""
     pairs, _, _ = make_pairs(400, seed=6, mutate_frac=0.3)
-    e2 = G.Engine(device=0, host_value_hash=True)
+    e2 = G.Engine(device=0, device_value_hash=True)
     r1 = eng.diff_pairs(pairs)
     r2 = e2.diff_pairs(pairs)
     for f in ("pair_flags", "spec_dirty_ids", "status_dirty_ids", "dirty_ids", "path_offsets", "path_hashes",
@@ -229,7 +230,7 @@ def test_k1_digests_equal_host_encoder(n_pairs, k1_variant):
     """K1's pool after ingest is byte-identical to the host encoder's with host-side XXH64 digests (every
     segment of both objects: digests in place, nothing else touched), and a stand-alone K1 pass over the
     resident batch (gpudiff_dbatch_hash_values) rewrites the same bytes.  Every K1 tuning variant."""
-    eng = G.Engine(device=0, encode_threads=8, flags=k1_variant << 30)
+    eng = G.Engine(device=0, encode_threads=8, flags=k1_variant << 30, device_value_hash=True)
     pairs, _, _ = make_pairs(n_pairs, seed=70 + n_pairs, mutate_frac=0.2)
     if n_pairs > 1:
         pairs = _k1_corpus() + pairs

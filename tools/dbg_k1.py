@@ -11,7 +11,7 @@ from tests.workload import make_pairs
 variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 sets = {"kat": [(a, b) for _, a, b, _, _ in cases()], "mix": make_pairs(500, seed=5, mutate_frac=0.2)[0]}
 host = G.Engine(device=G.DEVICE_NONE, host_value_hash=True)
-eng = G.Engine(device=0, flags=variant << 30)
+eng = G.Engine(device=0, flags=variant << 30, device_value_hash=True)
 for name, pairs in sets.items():
     ref = host.encode(pairs)
     hb = eng.encode(pairs)

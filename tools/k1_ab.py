@@ -28,7 +28,7 @@ def main():
     n = pop.n
     out = {"pairs": n, "config": args.config}
     for v in [int(x) for x in args.variants.split(",")]:
-        eng = G.Engine(device=0, encode_threads=16, timing=True, flags=v << 30)
+        eng = G.Engine(device=0, encode_threads=16, timing=True, flags=v << 30, device_value_hash=True)
         first = pop.chunk(eng, 0, min(262144, n), 16)
         per_pair = first.pool_bytes / max(1, min(262144, n))
         db = eng.device_batch(int(per_pair * n * (1.4 if args.config == "config4" else 1.15)) + (64 << 20), n)
