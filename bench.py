@@ -592,7 +592,7 @@ def cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota):
         aff_rate = len(idx) * swa / seca
     hb = eng.encode(pairs)
     rows = hb.rows()
-    csr = cpu_ref.CsrPairs(hb.pool(), rows)
+    csr = cpu_ref.CsrPairs(hb.pool_view(), rows)
     csr.run(threads=threads)  # warm
     fcsr, csw, csec, _ = csr.run(threads=threads, min_seconds=args.cpu_seconds / 2)
     _, csw1, csec1, _ = csr.run(threads=1, min_seconds=args.cpu_seconds / 4)

@@ -375,6 +375,15 @@ class HostBatch:
         inf = self.info()
         return C.string_at(inf.pool, inf.pool_bytes) if inf.pool_bytes else b""
 
+    def pool_view(self) -> np.ndarray:
+        """The pool as a u8 array over the batch's own host memory (no copy; C.string_at takes a C int
+        size, so pools over 2 GiB -- config4's 7 GB -- cannot go through pool()).  Valid while the batch
+        lives."""
+        inf = self.info()
+        if not inf.pool_bytes:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array((C.c_uint8 * inf.pool_bytes).from_address(inf.pool))
+
     def free(self):
         if self.h:
             _lib.gpudiff_hbatch_free(self.engine.ctx, self.h)

@@ -183,7 +183,9 @@ class CsrPairs:
     rows) for the CPU merge over CSR ("cpu-csr", oracle/csr_ref.cpp)."""
 
     def __init__(self, pool: bytes, rows: np.ndarray):
-        self.pool = np.frombuffer(pool, dtype=np.uint8) if pool else np.zeros(16, np.uint8)
+        # bytes, or a u8 array (HostBatch.pool_view: pools over 2 GiB)
+        pool = pool if isinstance(pool, np.ndarray) else np.frombuffer(pool, dtype=np.uint8)
+        self.pool = pool if pool.size else np.zeros(16, np.uint8)
         self.rows = np.ascontiguousarray(rows)
         self.n = len(rows)
 
