@@ -175,7 +175,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full-paths", action="store_true",
                     help="skip the CPU merge's full-size decision + changed-path check during ingest")
-    ap.add_argument("--no-k1", action="store_true", help="skip the K1 (value digest) pass and the hash + diff rate")
     ap.add_argument("--json-in-pairs", type=int, default=131072,
                     help="pairs of the end-to-end JSON-in measurement (0 = skip)")
     ap.add_argument("--traffic-json", default="latest",
@@ -243,7 +242,7 @@ def main():
     log("config %s (%s scaling): %d pairs / %d clusters node-wide; this rank %d pairs / %d clusters; %d host threads"
         % (args.config, scaling, cfg.n_pairs, cfg.n_clusters, n, pop.n_clusters, threads))
 
-    # ---------------- ingest: synthesize + encode on the host, stage, H2D, K1
+    # ---------------- ingest: synthesize + encode on the host, stage, H2D
     t_gen = time.time()
     first = pop.chunk(eng, 0, min(args.chunk, n), threads)
     # full-size changed-path parity (north_star: bit-exact changed-path lists for all 10M pairs): the CPU
@@ -289,7 +288,6 @@ def main():
     eng.sync()
     t_gen = time.time() - t_gen
     st = db.stats()
-    k1_ms = eng.timings().value_hash_ms or None  # None: digests came from the host encoder (the default)
     log("ingest done in %.1f s: %.2f GB resident, %.1f leaves/pair, %.2f GB compared per pass" % (
         t_gen, st.pool_bytes / 1e9, st.total_leaves / max(1, n), st.compare_bytes / 1e9))
 
@@ -425,43 +423,6 @@ def main():
         if pmc.get("k2_source_hash") == src_hash and pmc.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
 
-    # ---------------- K1 (value digests) as a stand-alone pass and "hash + diff" per step (SURVEY 8(d)'s
-    # K1+K2+K3): every step re-hashes the whole resident population, as if it were new in every step
-    k1 = None
-    if not args.no_k1:
-        k1_list = []
-        for _ in range(3):
-            db.hash_values()
-            eng.sync()
-            k1_list.append(eng.timings().value_hash_ms)
-        k1_avg = sum(k1_list) / len(k1_list)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            db.hash_values()
-            eng.diff(db)
-            if gather is not None:
-                gather.step(fill_counts, fill_ids)
-        if gather is not None:
-            gather.finish()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        dt1 = time.perf_counter() - t1
-        if world > 1:
-            t = torch.tensor([dt1], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt1 = float(t.item())
-        k1_gbs = st.hash_bytes / (k1_avg * 1e-3) / 1e9 if k1_avg > 0 else 0.0
-        k1 = dict(value_incl_k1=total_pairs * args.steps / dt1, ms_per_step_incl_k1=dt1 / args.steps * 1e3,
-                  k1_ms=k1_avg, k1_launch_ms=k1_list, bytes_per_launch=st.hash_bytes, achieved=k1_gbs,
-                  frac=k1_gbs / HBM_PEAK_GBPS, unit="GB/s",
-                  bytes_def="K1: per pair its 64-B row; per segment holding long values its metas (4 B/leaf), "
-                            "arena, and 8 B per digest written")
-        log("K1:", json.dumps(k1))
-
     db.free()  # the JSON-in and CPU legs below need no resident population
 
     # ---------------- rank 0, N = 1: end-to-end JSON-in, CPU baselines, three-way parity
@@ -523,16 +484,13 @@ def main():
                          "format": {"bytes_per_launch": fmt_bytes / launches, "achieved": achieved_fmt,
                                     "frac": achieved_fmt / HBM_PEAK_GBPS,
                                     "def": "bytes K2 reads in this build's CSR format: 64-B row + flag + both "
-                                           "size-matched segments (16 B per leaf record: value u64 + 32-bit path hash + meta; + the arena: long strings 4-B aligned, padded to 16)"},
+                                           "size-matched segments (16 B per leaf record: value u64 = the value's first 8 bytes, 32-bit path hash, meta; + the arena: long strings' tails past 8 bytes, 4-B aligned, padded to 16)"},
                          "diff_pass": {"ms": pass_ms, "achieved": achieved_pass, "frac": achieved_pass / HBM_PEAK_GBPS,
                                        "def": "SURVEY bytes over the whole diff pass (K2..K6)"},
                          "k2_source_hash": src_hash},
             "kernels_ms": {"compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,
                            "join_exposed": tm.join_ms, "emit": tm.emit_ms, "diff_pass": tm.total_ms,
-                           "passes": tm.n_passes, "value_hash_last_chunk": k1_ms,
-                           "value_hash_population": None if k1 is None else k1["k1_ms"]},
-            "value_incl_k1": None if k1 is None else k1["value_incl_k1"],
-            "k1": k1,
+                           "passes": tm.n_passes},
             "cpu_baseline": cpu,
             "json_in": json_in,
             "checks": {"full_size": full_check, "sample": sample_check, "three_way": three_way,
@@ -547,7 +505,7 @@ def main():
 def json_in_rates(G, pop, m, threads, device):
     """End-to-end JSON-in pairs/s on the first m pairs of this workload: JSON in
     host memory -> gpudiff_submit -> gpudiff_wait (results on the host),
-    once with host encoding (16 encode threads, pinned H2D, K1, diff pass) and
+    once with host encoding (16 encode threads, pinned H2D, diff pass) and
     once with device encoding (pinned staging, H2D, K0, diff pass).  Includes
     PCIe; the timed headline (`value`) does not."""
     buf, offs, _truth = pop.json_range(0, m, threads)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GPUDIFF_ABI_VERSION 3
+#define GPUDIFF_ABI_VERSION 4
 
 enum {
     GPUDIFF_OK = 0,
@@ -96,15 +96,9 @@ enum {
 
 /* context option flags */
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
-#define GPUDIFF_OPT_HOST_VALUE_HASH 0x2u /* hash long values in the host encoder (the default since ABI 3; kept
-                                            for callers that set it) */
-#define GPUDIFF_OPT_DEVICE_VALUE_HASH 0x8u /* hash long values with kernel K1 after each H2D instead of in the
-                                              host encoder (XXH64 is multiply-bound on CDNA --
-                                              no 64-bit integer multiplier -- so the host encoder, which reads
-                                              every byte anyway, is the cheaper place) */
-#define GPUDIFF_OPT_NO_VALUE_HASH 0x4u   /* tests: leave value digests 0 so every equal-length
-                                            long value goes through byte confirmation (the
-                                            path a digest collision would take) */
+/* bits 0x2, 0x4, 0x8 and 30-31 are reserved: until ABI 3 they chose where long-value digests were
+   computed (host encoder or kernel K1); since ABI 4 the format has no digests (include/gpudiff_format.h:
+   a long string's first 8 bytes sit in its leaf record, the rest in the arena) and they are ignored */
 /* tuning knobs (A/B measurements; 0 = defaults) */
 #define GPUDIFF_OPT_K2_VARIANT_SHIFT 8u  /* 4 bits: decision-kernel load policy / unroll */
 #define GPUDIFF_OPT_K2_BLOCKS_SHIFT 12u  /* 4 bits: resident blocks per CU for the decision kernel */
@@ -120,8 +114,6 @@ enum {
                                            in 64-pair chunks (0: the default, 2 quarters; t = 1: no tail,
                                            the last two rounds of tickets fetched late) */
 #define GPUDIFF_OPT_K2_TAIL8 0x80u      /* tuning: tail items of 8 pairs instead of half a main item */
-#define GPUDIFF_OPT_K1_VARIANT_SHIFT 30u /* 2 bits: value-hash kernel (0: LDS windows of 4 KiB, 1: 8 KiB windows,
-                                            2: values read by their lanes straight from HBM, 3: 2 KiB windows) */
 #define GPUDIFF_OPT_K2_ITEMS_SHIFT 28u   /* 2 bits: decision-kernel items per resident wave before 64-pair
                                             chunks are split (0: default 8, 1: 4, 2: 8, 3: 16) */
 
@@ -192,12 +184,9 @@ typedef struct gpudiff_batch_stats {
     uint64_t compare_bytes;    /* format bytes one diff pass reads */
     uint64_t value_bytes;      /* canonical bytes of the long (non-inline) string values of every object:
                                   V of SURVEY.md §8(d)'s B_pair = sum over A, B of (24 L + V + 8) + O */
-    uint64_t hash_bytes;       /* bytes one K1 pass (value digests) moves: per pair its 64-B row, per segment
-                                  holding long values its metas (4 B per leaf) and arena, 8 B per digest written */
 } gpudiff_batch_stats;
 
 typedef struct gpudiff_timings {
-    float value_hash_ms;  /* K1 over the last appended chunk, or the last gpudiff_dbatch_hash_values */
     float compare_ms;     /* K2: all k2_launches launches of a pass (back to back on the stream) */
     float compact_ms;     /* K3 (scan + compaction); 0 when overlapped with K2 (segmented pass) */
     float join_ms;        /* K4 merge-join; segmented pass: the part not hidden behind K2 */
@@ -234,14 +223,8 @@ void gpudiff_hbatch_free(gpudiff_ctx* ctx, gpudiff_hbatch* hb);
 /* ---- device batches ---- */
 int gpudiff_dbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, uint64_t max_pairs,
                           gpudiff_dbatch** out);
-/* async H2D of hb into the batch + K1 value hashing of the new objects */
+/* async H2D of hb into the batch (rows rebased onto the batch's pool) */
 int gpudiff_dbatch_append(gpudiff_ctx* ctx, gpudiff_dbatch* db, const gpudiff_hbatch* hb);
-/* K1 over every pair already resident, on the context's stream, asynchronous; with
- * GPUDIFF_OPT_TIMING its duration is value_hash_ms.  The digests it writes equal those the encoder
- * (or K1 at ingest, GPUDIFF_OPT_DEVICE_VALUE_HASH) already wrote: this is the GPU hashing step as a
- * stand-alone pass, so a caller can time "hash then diff" over a population that is new in every
- * step.  No-op with GPUDIFF_OPT_NO_VALUE_HASH. */
-int gpudiff_dbatch_hash_values(gpudiff_ctx* ctx, gpudiff_dbatch* d);
 int gpudiff_dbatch_reset(gpudiff_ctx* ctx, gpudiff_dbatch* db);
 int gpudiff_dbatch_stats_get(const gpudiff_dbatch* db, gpudiff_batch_stats* st);
 int gpudiff_dbatch_device_view(const gpudiff_dbatch* db, gpudiff_device_view* v);
@@ -344,7 +327,7 @@ int gpudiff_store_create(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_by
 #define GPUDIFF_STORE_DEVICE_ENCODE 0x1u
 int gpudiff_store_create_ex(gpudiff_ctx* ctx, uint32_t max_slots, uint64_t space_bytes, uint32_t max_events,
                             uint32_t flags, gpudiff_store** out);
-/* encode (host threads), H2D into the current space, K1 on the new blobs,
+/* encode (host threads), H2D into the current space,
  * K2..K6 over the batch's (resident, new) pairs; results via gpudiff_wait.
  * Two submits may be in flight (the next batch encodes while the GPU diffs
  * the previous one); wait on a ticket before its slot in the ring is reused. */
@@ -386,9 +369,6 @@ int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
  * item, items, start of the last item, end, streaming ticks, join ticks, hardware CU id; 100 MHz)
  * into device memory dev_buf of cap_waves records; dev_buf NULL stops recording */
 int gpudiff_k2_profile(gpudiff_ctx* ctx, uint64_t* dev_buf, uint32_t cap_waves);
-/* diagnostics: the windowed K1's first wave records 12 u32 per window (batch, cursor, window size,
- * cut, last segment, chunks, values, next cursor) into dev_buf (cap records); NULL stops */
-int gpudiff_k1_trace(gpudiff_ctx* ctx, uint32_t* dev_buf, uint32_t cap);
 
 /* ---- write path: the request body for a dirty object ----
  * GPUDIFF_UPSERT_SPEC: what upsertIntoDownstream hands to client.Create

@@ -12,15 +12,22 @@
  * aligned blobs of ~3.2 KB read at 6.1 TB/s, line-aligned ones at 6.8 TB/s).
  *
  *   segment(L, arena) = vals[L] u64 | keys[L] u32 | metas[L] u32
- *                       | arena: the long string values in key order, each at a
- *                         4-byte aligned offset (zero padded to 4), the whole
- *                         zero padded to a multiple of 16
+ *                       | arena: the tails of the long string values in key
+ *                         order, each at a 4-byte aligned offset (zero padded
+ *                         to 4), the whole zero padded to a multiple of 16
  *
  *   keys   = pathHash: the chained XXH64 path hash under the pair seed, cut
  *            to GPUDIFF_PATH_HASH_BITS (32) bits, ascending, unique
- *   vals   = inline value bytes (<= 8, zero padded) or, for strings longer
- *            than 8 bytes, XXH64(value bytes, 0) filled by kernel K1
+ *   vals   = the value's first 8 bytes: the whole value when it fits (inline:
+ *            <= 8 bytes, zero padded), else the head of a long string, whose
+ *            remaining len - 8 bytes (its tail) sit in the arena
  *   metas  = (len << 3) | tag
+ *
+ * Every byte of a value is stored exactly once: the leaf record carries the
+ * first 8, the arena the rest.  (Until ABI 4 a long string's vals slot held an
+ * XXH64 digest and the arena the whole value: the decision kernel compares
+ * arena bytes anyway, so the digest was 8 redundant bytes per long value in
+ * every pass -- 9.6% of config3's compared bytes.)
  *
  * Two objects' compared regions are equal under the reference predicates
  * (pkg/syncer/specsyncer.go:17-41, statussyncer.go:15-27) iff their segments
@@ -54,8 +61,7 @@
 /* object flags (PairRow.flags_a / flags_b) */
 #define GPUDIFF_OBJ_HAS_STATUS 0x1u   /* top-level "status" key present (even null) */
 #define GPUDIFF_OBJ_DECODE_ERR 0x2u   /* JSON failed the Go decode rules */
-#define GPUDIFF_OBJ_FRESH 0x4u        /* object store: blob uploaded with this batch (K1 hashes
-                                         its long values; resident blobs were hashed on arrival) */
+#define GPUDIFF_OBJ_FRESH 0x4u        /* object store: blob uploaded with this batch (informational) */
 /* object store: the path table kept after a resident blob's segments (the
  * "trailer"), which makes the store's old-vs-new path check exact.  Its n
  * entries are the region leaves and all their ancestors except the root,
@@ -120,9 +126,10 @@ static inline uint32_t gpudiff_meta_len(uint32_t m) { return m >> 3; }
 static inline int gpudiff_meta_is_long(uint32_t m) {
     return gpudiff_meta_tag(m) == GPUDIFF_TAG_STR && gpudiff_meta_len(m) > GPUDIFF_INLINE_MAX;
 }
-/* arena bytes of one leaf's value (long strings: the length rounded up to 4) */
+/* arena bytes of one leaf's value (long strings: the tail past the 8 bytes in
+ * vals, its length rounded up to 4) */
 static inline uint32_t gpudiff_meta_arena(uint32_t m) {
-    return gpudiff_meta_is_long(m) ? ((gpudiff_meta_len(m) + 3u) & ~3u) : 0u;
+    return gpudiff_meta_is_long(m) ? ((gpudiff_meta_len(m) - GPUDIFF_INLINE_MAX + 3u) & ~3u) : 0u;
 }
 /* a segment's arena size (the row's *_ar fields): the sum of its leaves'
  * gpudiff_meta_arena, rounded up to 16 */

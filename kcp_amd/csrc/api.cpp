@@ -152,9 +152,6 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
     c->ecfg.hash_bits = (o.path_hash_bits == 0 || o.path_hash_bits >= GPUDIFF_PATH_HASH_BITS) ? GPUDIFF_PATH_HASH_BITS
                                                                                             : o.path_hash_bits;
     if (c->ecfg.hash_bits < 8) return GPUDIFF_E_INVAL;
-    // value digests: in the host encoder unless K1 is asked for (GPUDIFF_OPT_DEVICE_VALUE_HASH)
-    c->ecfg.host_value_hash = !(o.flags & GPUDIFF_OPT_NO_VALUE_HASH) &&
-                              (!(o.flags & GPUDIFF_OPT_DEVICE_VALUE_HASH) || (o.flags & GPUDIFF_OPT_HOST_VALUE_HASH));
     c->hash_mask = c->ecfg.hash_bits >= 64 ? ~0ULL : ((1ULL << c->ecfg.hash_bits) - 1);
     if (o.device != GPUDIFF_DEVICE_NONE) {
         int n = 0;
@@ -171,7 +168,6 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             c->own_stream = true;
         }
-        for (auto& e : c->ev_k1) HIPCHK(hipEventCreate(&e));
         HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&c->k2alt, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&c->rb, hipStreamNonBlocking));
@@ -193,8 +189,6 @@ void gpudiff_close(gpudiff_ctx* c) {
             if (c->ring[i]) gpudiff_dbatch_free(c, c->ring[i]);
             if (c->ring_hb[i]) gpudiff_hbatch_free(c, c->ring_hb[i]);
         }
-        for (auto& e : c->ev_k1)
-            if (e) (void)hipEventDestroy(e);
         for (auto& a : c->pass_ev)
             for (auto& e : a) (void)hipEventDestroy(e);
         for (auto& e : c->seg_ev)
@@ -419,27 +413,16 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
                           c->stream));
     if (hb->used) HIPCHK(hipEventRecord(hb->used, c->stream));
     HIPCHK(launch_rebase(c->stream, d->rows, begin, end, base, d->pair_ids));
-    if (!c->ecfg.host_value_hash && !(c->flags & GPUDIFF_OPT_NO_VALUE_HASH)) {
-        if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
-        HIPCHK(launch_value_hash(c->stream, d->rows, begin, end, d->pool, false, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
-        if (c->flags & GPUDIFF_OPT_TIMING) {
-            HIPCHK(hipEventRecord(c->ev_k1[1], c->stream));
-            c->k1_recorded = true;
-        }
-    }
-    uint64_t cb = 0, vb = 0, kb = 0;
+    uint64_t cb = 0, vb = 0;
     for (size_t i = 0; i < hb->n; i++) {
         const gpudiff_pair_row& r = hb->rows[i];
         cb += pair_compare_bytes(r);
-        kb += sizeof(gpudiff_pair_row) + blob_hash_bytes(hb->pool + r.off_a, r.spec_l_a, r.spec_ar_a, r.stat_l_a, r.stat_ar_a) +
-              blob_hash_bytes(hb->pool + r.off_b, r.spec_l_b, r.spec_ar_b, r.stat_l_b, r.stat_ar_b);
         if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) continue;
         vb += blob_value_bytes(hb->pool + r.off_a, r.spec_l_a, r.spec_ar_a, r.stat_l_a) +
               blob_value_bytes(hb->pool + r.off_b, r.spec_l_b, r.spec_ar_b, r.stat_l_b);
     }
     d->compare_bytes += cb;
     d->value_bytes += vb;
-    d->hash_bytes += kb;
     d->pool_used += hb->pool_bytes;
     d->n_pairs = end;
     d->leaves += hb->leaves;
@@ -451,7 +434,7 @@ int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
     int rc = set_device(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
-    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->hash_bytes = 0;
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = 0;
     d->ticket = 0;
     return GPUDIFF_OK;
 }
@@ -463,21 +446,6 @@ int gpudiff_dbatch_stats_get(const gpudiff_dbatch* d, gpudiff_batch_stats* st) {
     st->total_leaves = d->leaves;
     st->compare_bytes = d->compare_bytes;
     st->value_bytes = d->value_bytes;
-    st->hash_bytes = d->hash_bytes;
-    return GPUDIFF_OK;
-}
-
-int gpudiff_dbatch_hash_values(gpudiff_ctx* c, gpudiff_dbatch* d) {
-    if (!c || !d) return GPUDIFF_E_INVAL;
-    int rc = set_device(c);
-    if (rc) return rc;
-    if ((c->flags & GPUDIFF_OPT_NO_VALUE_HASH) || !d->n_pairs) return GPUDIFF_OK;
-    if (c->flags & GPUDIFF_OPT_TIMING) HIPCHK(hipEventRecord(c->ev_k1[0], c->stream));
-    HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)d->n_pairs, d->pool, false, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
-    if (c->flags & GPUDIFF_OPT_TIMING) {
-        HIPCHK(hipEventRecord(c->ev_k1[1], c->stream));
-        c->k1_recorded = true;
-    }
     return GPUDIFF_OK;
 }
 
@@ -675,8 +643,6 @@ int gpudiff_last_timings(gpudiff_ctx* c, gpudiff_timings* t) {
     if (!c->has_device) return GPUDIFF_E_NODEVICE;
     if (!(c->flags & GPUDIFF_OPT_TIMING)) return GPUDIFF_E_STATE;
     HIPCHK(hipStreamSynchronize(c->stream));
-    float ms = 0;
-    if (c->k1_recorded && hipEventElapsedTime(&ms, c->ev_k1[0], c->ev_k1[1]) == hipSuccess) t->value_hash_ms = ms;
     t->n_passes = (uint32_t)c->n_pass;
     t->k2_launches = c->pass_k2_launches;
     if (!c->n_pass) return GPUDIFF_OK;
@@ -831,7 +797,7 @@ int gpudiff_submit(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpu
             return rc;
         }
     }
-    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->hash_bytes = 0;
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = 0;
     if ((rc = gpudiff_dbatch_append(c, d, hb)) || (rc = gpudiff_diff(c, d, ticket))) {
         gpudiff_hbatch_free(c, hb);
         return rc;

@@ -29,7 +29,6 @@ int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, ui
     memset(info, 0, sizeof(*info));
     EncodeConfig cfg;
     cfg.hash_bits = (bits == 0 || bits >= GPUDIFF_PATH_HASH_BITS) ? GPUDIFF_PATH_HASH_BITS : bits;
-    cfg.host_value_hash = true;  // K0 fills the long-value digests itself
     PairEncoder enc(cfg);
     Arena arena;
     FlatObject o;
@@ -111,15 +110,6 @@ int gpudiff_encode_objects(gpudiff_ctx* c, const uint8_t* const* docs, const siz
         f.bytes = to[i].bytes;
         f.n_tab = to[i].n_tab;
     }
-    return GPUDIFF_OK;
-}
-
-int gpudiff_k1_trace(gpudiff_ctx* c, uint32_t* dev_buf, uint32_t cap) {
-    if (!c) return GPUDIFF_E_INVAL;
-    int rc = set_device(c);
-    if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(k1_trace(dev_buf, cap));
     return GPUDIFF_OK;
 }
 

@@ -556,7 +556,6 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
         return fail(GPUDIFF_E_NOMEM);
     }
     EncodeConfig cfg = c->ecfg;
-    cfg.host_value_hash = true;  // resolved blobs carry their digests like K0's
     s->enc.reset(new (std::nothrow) PairEncoder(cfg));
     if (!s->enc) return fail(GPUDIFF_E_NOMEM);
     for (auto& sp : s->space)

@@ -253,10 +253,10 @@ void PairEncoder::write_blob(const FlatObject& o, std::vector<uint8_t>& pool, ui
         for (size_t i = 0; i < n; i++) {
             const LeafRec& r = v[i];
             uint64_t val = r.val;
-            if (gpudiff_meta_is_long(r.meta)) {
-                memcpy(ar + aoff, r.vptr, r.vlen);
+            if (gpudiff_meta_is_long(r.meta)) {  // head in the record, tail in the arena
+                memcpy(&val, r.vptr, GPUDIFF_INLINE_MAX);
+                memcpy(ar + aoff, r.vptr + GPUDIFF_INLINE_MAX, r.vlen - GPUDIFF_INLINE_MAX);
                 aoff += gpudiff_meta_arena(r.meta);
-                val = cfg_.host_value_hash ? xxh64_host(r.vptr, r.vlen, 0) : 0;
             }
             const uint32_t k32 = (uint32_t)r.h;  // hashes are masked to <= 32 bits
             memcpy(keys + 4 * i, &k32, 4);

@@ -87,7 +87,6 @@ struct FlatObject {
 
 struct EncodeConfig {
     uint32_t hash_bits = GPUDIFF_PATH_HASH_BITS;  // <= 32: segments keep 32-bit keys
-    bool host_value_hash = false;
 };
 
 // Flattens a decoded top-level object into its spec/status leaves.

@@ -60,7 +60,7 @@ struct gpudiff_hbatch {
 struct gpudiff_dbatch {
     uint64_t pool_cap = 0, pool_used = 0;
     uint64_t max_pairs = 0, n_pairs = 0;
-    uint64_t leaves = 0, compare_bytes = 0, value_bytes = 0, hash_bytes = 0;
+    uint64_t leaves = 0, compare_bytes = 0, value_bytes = 0;
     uint8_t* pool = nullptr;
     bool pool_borrowed = false;  // pool owned by a gpudiff_store (its current space)
     gpudiff_pair_row* rows = nullptr;
@@ -116,8 +116,6 @@ struct gpudiff_ctx {
     std::vector<gd::Part> parts;
     gpudiff_ticket next_ticket = 1;
     std::unordered_map<gpudiff_ticket, gpudiff_dbatch*> tickets;
-    hipEvent_t ev_k1[2] = {};
-    bool k1_recorded = false;
     std::vector<std::array<hipEvent_t, 5>> pass_ev;
     size_t n_pass = 0;
     uint32_t pass_k2_launches = 1;
@@ -184,23 +182,6 @@ inline uint64_t blob_value_bytes(const uint8_t* blob, uint32_t spec_l, uint32_t 
     m = (const uint32_t*)(blob + gpudiff_seg_bytes(spec_l, spec_ar) + 12ull * stat_l);
     for (uint32_t i = 0; i < stat_l; i++)
         if (gpudiff_meta_is_long(m[i])) v += gpudiff_meta_len(m[i]);
-    return v;
-}
-
-// bytes K1 moves for one object: per segment holding long values, its metas (4 B per
-// leaf), its arena (padded) and one 8-B digest per long value written
-inline uint64_t blob_hash_bytes(const uint8_t* blob, uint32_t spec_l, uint32_t spec_ar, uint32_t stat_l,
-                                uint32_t stat_ar) {
-    uint64_t v = 0;
-    const uint64_t seg[2] = {0, gpudiff_seg_bytes(spec_l, spec_ar)};
-    const uint32_t l[2] = {spec_l, stat_l}, ar[2] = {spec_ar, stat_ar};
-    for (int s = 0; s < 2; s++) {
-        if (!l[s] || !ar[s]) continue;
-        const uint32_t* m = (const uint32_t*)(blob + seg[s] + 12ull * l[s]);
-        uint64_t nl = 0;
-        for (uint32_t i = 0; i < l[s]; i++) nl += gpudiff_meta_is_long(m[i]) ? 1 : 0;
-        v += 4ull * l[s] + ar[s] + 8 * nl;
-    }
     return v;
 }
 

@@ -60,8 +60,6 @@ uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks);
 
 hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint64_t base,
                          uint32_t* pair_ids);
-hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool,
-                             bool fresh_only = false, uint32_t variant = 0);
 // object-store compaction: blob copies between the two spaces
 struct BlobMove {
     uint64_t src, dst, bytes;
@@ -80,6 +78,5 @@ hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
 // tuning: K2 variant 14 writes 8 u64 per wave (start, first item end, items, last item start, end,
 // streaming ticks, join ticks, hw id) into dev_buf (cap_waves waves); nullptr disables
 hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves);
-hipError_t k1_trace(uint32_t* dev_buf, uint32_t cap);
 
 }  // namespace gd

@@ -1,18 +1,20 @@
 // HIP kernels of the gpudiff engine, written for gfx950 (CDNA4, wave64).
 //
-//   K1 k_value_hash   XXH64 of every long string leaf value (ingest)
-//   K2 k_compare      spec/status decision per pair: 16-B-per-lane streaming
-//                     compare of the two canonical segments (one wave per
-//                     pair, 64 pairs per wave-chunk, ballot counts per chunk)
+//   K2 k_compare_flat spec/status decision per pair: the item's compared
+//                     segments flattened into one stream of 16-B chunks,
+//                     streamed by the whole wave (non-temporal 16-B loads),
+//                     mismatches marked by ballot; a dirty pair's changed
+//                     paths merge-joined on the spot (join_pair) into the
+//                     wave's path arena
 //   K3 k_scan_*<V4>   reduce-then-scan of the per-chunk counts
 //      k_compact      ballot/prefix compaction of dirty pair IDs + scratch
-//                     slots for the changed-path join
-//   K4 k_join         merge-join of the sorted leaf keys, one wave per dirty
-//                     pair, in 64-key windows held in registers (cross-lane
-//                     binary search with ds_bpermute), byte-exact confirmation
-//                     of hash-equal long values; trivial pairs lane-parallel
+//                     slots for the deferred joins
+//   K4 k_join         merge-join of the pairs K2 deferred: sorted leaf keys in
+//                     64-key windows held in registers (cross-lane binary
+//                     search with ds_bpermute), byte-exact confirmation of
+//                     long values whose first 8 bytes agree
 //   K5 k_scan_*<u32>  exclusive scan of per-pair path counts
-//   K6 k_copy_paths   compaction of the path scratch into the output CSR
+//   K6 k_copy_paths   compaction of the path arenas / scratch into the CSR
 //
 // Semantics: DESIGN.md "Kernels"; reference predicates
 // pkg/syncer/specsyncer.go:17-41 and pkg/syncer/statussyncer.go:15-27.
@@ -77,520 +79,15 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 
 __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + arena; }
 __device__ __forceinline__ bool meta_long(uint32_t m) { return (m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > 8u; }
-// arena bytes of a leaf's value: long strings at 4-byte aligned offsets (include/gpudiff_format.h)
-__device__ __forceinline__ uint32_t meta_arena(uint32_t m) { return meta_long(m) ? (((m >> 3) + 3u) & ~3u) : 0u; }
+// arena bytes of a leaf's value: a long string's tail past its first 8 bytes (which sit in vals), at a
+// 4-byte aligned offset (include/gpudiff_format.h)
+__device__ __forceinline__ uint32_t meta_arena(uint32_t m) { return meta_long(m) ? (((m >> 3) - 8u + 3u) & ~3u) : 0u; }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bool neq16(const u32x4& a, const u32x4& b) {
     const u32x4 x = a ^ b;
     return (x.x | x.y | x.z | x.w) != 0u;
-}
-
-// ---------------------------------------------------------------- K1
-// XXH64 of every long string value (> 8 bytes; the shorter ones are inline and need no digest).
-//
-// Round 2's K1 ran one wave per (pair, object, region) with a lane per value: a ConfigMap's spec
-// has 8 long values, so 8 of 64 lanes worked, each with 4-B loads (0.7-1.2 TB/s).  This K1 keeps
-// every lane busy on its own value and loads 16 B per lane:
-//   walk   each wave owns a contiguous range of pairs; a lane takes one pair at a time (idle lanes
-//          pull the next pairs of the range by ballot) and walks its segments' metas 4 at a time
-//          with one 16-B load, appending each long leaf's (value offset, length, digest slot) to
-//          the wave's LDS list (wave prefix sum of the per-lane counts: no atomics);
-//   hash   when the list is nearly full (and at the end), lanes take entries round-robin -- values
-//          of many pairs, so the lengths even out -- and hash each value in 128-B bursts (eight
-//          16-B loads in flight, then four 32-B stripes), the < 32-byte tail from dword loads
-//          within the value's 4-byte padding; the digest goes to the leaf's 8-B value slot.
-// Values sit 4-byte aligned in the arena (include/gpudiff_format.h), so the 16-B loads are
-// dword-aligned (gfx950 global loads need only dword alignment); no load passes the value's
-// padded end (bursts cover whole stripes only) or the segment (metas end where a >= 16-B arena
-// starts).
-typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(4)));
-
-__device__ __forceinline__ uint64_t lo64(const u32x4u& v) { return ((uint64_t)v.y << 32) | v.x; }
-__device__ __forceinline__ uint64_t hi64(const u32x4u& v) { return ((uint64_t)v.w << 32) | v.z; }
-
-__device__ __forceinline__ uint64_t xxh64_lane(const uint8_t* __restrict__ p, uint32_t len) {
-    uint64_t h;
-    const uint32_t nstr = len >> 5;
-    if (nstr) {
-        uint64_t v1 = XP1 + XP2, v2 = XP2, v3 = 0, v4 = 0ull - XP1;
-        for (uint32_t s = 0; s < nstr; s += 4) {
-            const uint32_t nb = min(4u, nstr - s);
-            u32x4u q[8];
-#pragma unroll
-            for (uint32_t k = 0; k < 8; k++)
-                if (k < 2 * nb) q[k] = *(const u32x4u*)(p + 32u * s + 16u * k);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++)
-                if (j < nb) {
-                    v1 = xround(v1, lo64(q[2 * j]));
-                    v2 = xround(v2, hi64(q[2 * j]));
-                    v3 = xround(v3, lo64(q[2 * j + 1]));
-                    v4 = xround(v4, hi64(q[2 * j + 1]));
-                }
-        }
-        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
-        h = xmerge(h, v1);
-        h = xmerge(h, v2);
-        h = xmerge(h, v3);
-        h = xmerge(h, v4);
-    } else {
-        h = XP5;
-    }
-    h += len;
-    // tail: rem < 32 bytes as up to 8 dwords (inside the value's 4-byte padding), then 8-, 4- and
-    // 1-byte steps with static register indices only
-    const uint32_t rem = len & 31u;
-    const uint32_t* t = (const uint32_t*)(p + 32u * nstr);
-    uint32_t d[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) d[k] = 4u * k < rem ? t[k] : 0u;
-    const uint64_t w0 = ((uint64_t)d[1] << 32) | d[0], w1 = ((uint64_t)d[3] << 32) | d[2];
-    const uint64_t w2 = ((uint64_t)d[5] << 32) | d[4], w3 = ((uint64_t)d[7] << 32) | d[6];
-    if (rem >= 8) h = xrotl(h ^ xround(0, w0), 27) * XP1 + XP4;
-    if (rem >= 16) h = xrotl(h ^ xround(0, w1), 27) * XP1 + XP4;
-    if (rem >= 24) h = xrotl(h ^ xround(0, w2), 27) * XP1 + XP4;
-    const uint32_t q8 = rem >> 3;
-    uint64_t wq = q8 == 0 ? w0 : q8 == 1 ? w1 : q8 == 2 ? w2 : w3;
-    if (rem & 4u) {
-        h ^= (uint64_t)(uint32_t)wq * XP1;
-        h = xrotl(h, 23) * XP2 + XP3;
-        wq >>= 32;
-    }
-    const uint32_t nb = rem & 3u;
-#pragma unroll
-    for (uint32_t b = 0; b < 3; b++)
-        if (b < nb) {
-            h ^= ((wq >> (8 * b)) & 0xFFu) * XP5;
-            h = xrotl(h, 11) * XP1;
-        }
-    return xavalanche(h);
-}
-
-constexpr uint32_t K1_VCAP = 512;  // list entries per wave (8 KiB of LDS)
-struct K1Ent {
-    uint64_t aoff;   // value at pool + aoff
-    uint32_t len;
-    uint32_t vback;  // its digest slot at pool + aoff - vback
-};
-
-__device__ __forceinline__ void k1_flush(const K1Ent* E, uint32_t nv, uint8_t* __restrict__ pool, uint32_t lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t k = lane; k < nv; k += 64) {
-        const K1Ent e = E[k];
-        const uint64_t h = xxh64_lane(pool + e.aoff, e.len);
-        *(uint64_t*)(pool + e.aoff - e.vback) = h;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// fresh_only: only the objects flagged GPUDIFF_OBJ_FRESH (the object store's newly uploaded
-// blobs; the resident ones were hashed when they arrived).  (Tuning variant 2: values read
-// straight from HBM by their lanes; the default is k_value_hash_win below.)
-__global__ __launch_bounds__(256) void k_value_hash_list(const gpudiff_pair_row* __restrict__ rows, uint32_t row_begin,
-                                                         uint32_t row_end, uint8_t* __restrict__ pool, bool fresh_only) {
-    __shared__ K1Ent ents[4][K1_VCAP];
-    const uint32_t lane = lane_id();
-    K1Ent* E = ents[threadIdx.x >> 6];
-    const uint32_t gw = uni(blockIdx.x * 4u + (threadIdx.x >> 6)), nw = gridDim.x * 4u;
-    const uint64_t n = row_end - row_begin;
-    const uint32_t p1 = row_begin + (uint32_t)(n * (gw + 1) / nw);
-    uint32_t next = row_begin + (uint32_t)(n * gw / nw);  // wave-uniform: the range's next unassigned pair
-    uint32_t nv = 0;                                       // wave-uniform: list entries
-    // lane state: the pair (its row fields), the segment being walked (0..3 = A spec, A status,
-    // B spec, B status), the next leaf and the arena bytes before it
-    bool has = false;
-    uint32_t sidx = 4, i = 0, L = 0, run = 0;
-    uint64_t seg = 0;
-    uint64_t off_a = 0, off_b = 0;
-    uint32_t sla = 0, sara = 0, tla = 0, tara = 0, slb = 0, sarb = 0, tlb = 0, tarb = 0, fla = 0, flb = 0;
-    auto next_segment = [&]() {
-        for (;;) {
-            if (++sidx >= 4u) {
-                has = false;
-                return;
-            }
-            const bool b = sidx & 2u, st = sidx & 1u;
-            if (fresh_only && !((b ? flb : fla) & GPUDIFF_OBJ_FRESH)) continue;
-            const uint32_t sl = b ? slb : sla, sar = b ? sarb : sara;
-            const uint32_t l = st ? (b ? tlb : tla) : sl, ar = st ? (b ? tarb : tara) : sar;
-            if (!l || !ar) continue;
-            seg = (b ? off_b : off_a) + (st ? seg_bytes(sl, sar) : 0ull);
-            L = l;
-            i = 0;
-            run = 0;
-            return;
-        }
-    };
-    for (;;) {
-        // lanes without a pair pull the range's next pairs
-        const uint64_t idle = ballot(!has);
-        if (idle && next < p1) {
-            const uint32_t pos = next + popc64(idle & mask_lt(lane));
-            if (!has && pos < p1) {
-                const gpudiff_pair_row& r = rows[pos];
-                off_a = r.off_a;
-                off_b = r.off_b;
-                sla = r.spec_l_a; sara = r.spec_ar_a; tla = r.stat_l_a; tara = r.stat_ar_a;
-                slb = r.spec_l_b; sarb = r.spec_ar_b; tlb = r.stat_l_b; tarb = r.stat_ar_b;
-                fla = r.flags_a; flb = r.flags_b;
-                has = true;
-                sidx = ~0u;  // next_segment() starts at 0
-                next_segment();
-            }
-            next = min(p1, next + popc64(idle));
-        }
-        if (!ballot(has)) {
-            if (next >= p1) break;
-            continue;  // every pulled pair had nothing to hash
-        }
-        // four metas per lane, one 16-B load; each long leaf -> one list entry
-        uint32_t cnt = 0, m[4] = {0, 0, 0, 0};
-        if (has) {
-            const u32x4u mv = *(const u32x4u*)(pool + seg + 12ull * L + 4ull * i);
-            m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++) {
-                if (i + j >= L) m[j] = 0;
-                cnt += meta_long(m[j]) ? 1u : 0u;
-            }
-        }
-        const uint32_t incl = wave_incl_scan(cnt);
-        uint32_t pos = nv + incl - cnt;
-        if (has) {
-            const uint64_t arena = seg + 16ull * L;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++) {
-                if (meta_long(m[j])) {
-                    K1Ent e;
-                    e.aoff = arena + run;
-                    e.len = m[j] >> 3;
-                    e.vback = (uint32_t)(16ull * L + run - 8ull * (i + j));
-                    E[pos++] = e;
-                }
-                run += meta_arena(m[j]);
-            }
-            i += 4;
-            if (i >= L) next_segment();
-        }
-        nv += shfl32(incl, 63);
-        if (nv > K1_VCAP - 256u) {
-            k1_flush(E, nv, pool, lane);
-            nv = 0;
-        }
-    }
-    if (nv) k1_flush(E, nv, pool, lane);
-}
-
-// The default K1: values staged through LDS in windows.  A wave owns a contiguous range of pairs
-// and walks it 16 pairs at a time: lane j holds the j-th segment (of the 64 the 16 pairs have) that
-// carries long values.  A window is the next <= 256 leaves from the cursor (segment, leaf, arena
-// offset), cut where the arena bytes they span -- 16-B aligned per segment -- would pass W:
-//   metas    each lane loads the metas of 4 of the window's leaves (owner segment by a cross-lane
-//            binary search over the segments' leaf prefix), a wave scan of their arena sizes gives
-//            every long value its offset in its segment's arena;
-//   stage    the window's arena ranges (one contiguous range per segment) come in as 16-B chunks,
-//            W/1 KiB coalesced wave loads in flight per lane, written to the wave's LDS image;
-//   hash     the window's long values (~64 at config3's median 25 B) are listed in LDS and hashed
-//            round-robin, one lane per value, from LDS; each digest goes to its leaf's 8-B slot.
-// A value too long for any window (> W - 32 bytes) is hashed by one lane straight from HBM.
-__device__ __forceinline__ uint32_t lds_dw(const uint32_t* __restrict__ img, uint32_t byte_off) {
-    return img[byte_off >> 2];
-}
-
-__device__ __forceinline__ uint64_t xxh64_lds(const uint32_t* __restrict__ img, uint32_t off, uint32_t len) {
-    uint64_t h;
-    const uint32_t nstr = len >> 5;
-    uint32_t p = off;
-    if (nstr) {
-        uint64_t v1 = XP1 + XP2, v2 = XP2, v3 = 0, v4 = 0ull - XP1;
-        for (uint32_t s = 0; s < nstr; s++, p += 32) {
-            uint32_t d[8];
-#pragma unroll
-            for (uint32_t k = 0; k < 8; k++) d[k] = lds_dw(img, p + 4u * k);
-            v1 = xround(v1, ((uint64_t)d[1] << 32) | d[0]);
-            v2 = xround(v2, ((uint64_t)d[3] << 32) | d[2]);
-            v3 = xround(v3, ((uint64_t)d[5] << 32) | d[4]);
-            v4 = xround(v4, ((uint64_t)d[7] << 32) | d[6]);
-        }
-        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
-        h = xmerge(h, v1);
-        h = xmerge(h, v2);
-        h = xmerge(h, v3);
-        h = xmerge(h, v4);
-    } else {
-        h = XP5;
-    }
-    h += len;
-    const uint32_t rem = len & 31u;
-    uint32_t d[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) d[k] = 4u * k < rem ? lds_dw(img, p + 4u * k) : 0u;
-    const uint64_t w0 = ((uint64_t)d[1] << 32) | d[0], w1 = ((uint64_t)d[3] << 32) | d[2];
-    const uint64_t w2 = ((uint64_t)d[5] << 32) | d[4], w3 = ((uint64_t)d[7] << 32) | d[6];
-    if (rem >= 8) h = xrotl(h ^ xround(0, w0), 27) * XP1 + XP4;
-    if (rem >= 16) h = xrotl(h ^ xround(0, w1), 27) * XP1 + XP4;
-    if (rem >= 24) h = xrotl(h ^ xround(0, w2), 27) * XP1 + XP4;
-    const uint32_t q8 = rem >> 3;
-    uint64_t wq = q8 == 0 ? w0 : q8 == 1 ? w1 : q8 == 2 ? w2 : w3;
-    if (rem & 4u) {
-        h ^= (uint64_t)(uint32_t)wq * XP1;
-        h = xrotl(h, 23) * XP2 + XP3;
-        wq >>= 32;
-    }
-    const uint32_t nb = rem & 3u;
-#pragma unroll
-    for (uint32_t b = 0; b < 3; b++)
-        if (b < nb) {
-            h ^= ((wq >> (8 * b)) & 0xFFu) * XP5;
-            h = xrotl(h, 11) * XP1;
-        }
-    return xavalanche(h);
-}
-
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// first lane j (0..63) with v_j > x, for v non-decreasing across lanes (64 if none)
-__device__ __forceinline__ uint32_t lane_upper(uint32_t v, uint32_t x) {
-    uint32_t o = 0;
-#pragma unroll
-    for (uint32_t s = 32; s >= 1; s >>= 1)
-        if (shfl32(v, o + s - 1u) <= x) o += s;
-    return o;
-}
-
-constexpr uint32_t K1_WLEAVES = 256;  // leaves per window (4 metas per lane)
-
-// diagnostics (gpudiff_k1_trace): wave 0 of the windowed K1 records 12 u32 per window
-__device__ uint32_t* g_k1_trace;
-__device__ uint32_t g_k1_trace_cap;
-
-template <uint32_t W>
-struct alignas(16) K1Lds {
-    uint32_t img[W / 4];        // the window's staged arena ranges
-    uint32_t vpos[K1_WLEAVES];  // long value: LDS byte offset | len << 16
-    uint64_t vdig[K1_WLEAVES];  // its digest slot (pool byte offset)
-    uint32_t pb[64];            // per segment: arena prefix at its first leaf in the window
-};
-
-template <uint32_t W>
-__global__ __launch_bounds__(256) void k_value_hash_win(const gpudiff_pair_row* __restrict__ rows, uint32_t row_begin,
-                                                        uint32_t row_end, uint8_t* __restrict__ pool, bool fresh_only) {
-    static_assert(W % 1024 == 0 && W <= 65536, "window");
-    __shared__ K1Lds<W> lds_all[4];
-    K1Lds<W>& S = lds_all[threadIdx.x >> 6];
-    const uint32_t lane = lane_id();
-    const uint32_t gw = uni(blockIdx.x * 4u + (threadIdx.x >> 6)), nw = gridDim.x * 4u;
-    const uint64_t n = row_end - row_begin;
-    const uint32_t P0 = row_begin + (uint32_t)(n * gw / nw), P1 = row_begin + (uint32_t)(n * (gw + 1) / nw);
-    uint32_t ntrace = 0;
-    for (uint32_t pb0 = P0; pb0 < P1; pb0 += 16) {
-        // ---- this batch's segments with long values: lane j holds segment j
-        uint32_t cnt = 0;
-        uint64_t so[4] = {0, 0, 0, 0};
-        uint32_t sL[4] = {0, 0, 0, 0}, sA[4] = {0, 0, 0, 0};
-        if (lane < 16 && pb0 + lane < P1) {
-            const gpudiff_pair_row r = rows[pb0 + lane];
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
-                const bool b = q & 2u, st = q & 1u;
-                const uint32_t fl = b ? r.flags_b : r.flags_a;
-                const uint32_t sl = b ? r.spec_l_b : r.spec_l_a, sar = b ? r.spec_ar_b : r.spec_ar_a;
-                const uint32_t l = st ? (b ? r.stat_l_b : r.stat_l_a) : sl;
-                const uint32_t ar = st ? (b ? r.stat_ar_b : r.stat_ar_a) : sar;
-                if (!l || !ar || (fresh_only && !(fl & GPUDIFF_OBJ_FRESH))) continue;
-                so[cnt] = (b ? r.off_b : r.off_a) + (st ? seg_bytes(sl, sar) : 0ull);
-                sL[cnt] = l;
-                sA[cnt] = ar;
-                cnt++;
-            }
-        }
-        const uint32_t cincl = wave_incl_scan(cnt);
-        const uint32_t nseg = uni(shfl32(cincl, 63));
-        if (!nseg) continue;
-        // lane j <- segment j: a gather by the segment's owner lane and slot
-        uint64_t seg_off = 0;
-        uint32_t L = 0, AR = 0;
-        {
-            const uint32_t src = lane_upper(cincl, lane);  // owner lane of segment `lane`
-            const uint32_t slot = lane - (shfl32(cincl, min(src, 63u)) - shfl32(cnt, min(src, 63u)));
-            uint64_t o[4];
-            uint32_t l[4], a[4];
-#pragma unroll
-            for (uint32_t q = 0; q < 4; q++) {
-                o[q] = shfl64(so[q], min(src, 63u));
-                l[q] = shfl32(sL[q], min(src, 63u));
-                a[q] = shfl32(sA[q], min(src, 63u));
-            }
-            if (lane < nseg) {
-                seg_off = slot == 0 ? o[0] : slot == 1 ? o[1] : slot == 2 ? o[2] : o[3];
-                L = slot == 0 ? l[0] : slot == 1 ? l[1] : slot == 2 ? l[2] : l[3];
-                AR = slot == 0 ? a[0] : slot == 1 ? a[1] : slot == 2 ? a[2] : a[3];
-            }
-        }
-        // ---- windows from the cursor (cs, cl, ca)
-        uint32_t cs = 0, cl = 0, ca = 0;
-        while (cs < nseg) {
-            const uint32_t lv = lane < cs ? 0u : lane == cs ? L - cl : L;  // leaves of each segment from the cursor
-            const uint32_t lincl = wave_incl_scan(lv);
-            const uint32_t G = min(K1_WLEAVES, uni(shfl32(lincl, 63)));
-            // metas of the window's leaves: flattened index g = u * 64 + lane
-            uint32_t m[4], own[4], leaf[4], asz[4];
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t g = u * 64u + lane;
-                const uint32_t o = min(lane_upper(lincl, g), 63u);
-                own[u] = o;
-                const uint32_t first = shfl32(lincl - lv, o);
-                leaf[u] = g - first + (o == cs ? cl : 0u);
-                const uint64_t sof = shfl64(seg_off, o);
-                const uint32_t sl = shfl32(L, o);
-                m[u] = g < G ? *(const uint32_t*)(pool + sof + 12ull * sl + 4ull * leaf[u]) : 0u;
-            }
-            // arena prefix over the window (in leaf order), then per-segment offsets
-            uint32_t pin[4], run = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                asz[u] = meta_arena(m[u]);
-                const uint32_t inc = wave_incl_scan(asz[u]);
-                pin[u] = run + inc;
-                run += shfl32(inc, 63);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {  // a segment's first leaf in the window records the prefix there
-                const uint32_t g = u * 64u + lane;
-                const uint32_t first = shfl32(lincl - lv, own[u]);
-                if (g < G && g == first) S.pb[own[u]] = pin[u] - asz[u];
-            }
-            wave_sync_lds();
-            // cut: the leaves whose staged bytes (raw span + <= 32 of alignment per segment) fit W
-            uint32_t off[4], gcut = 0;
-            bool open = true;
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t g = u * 64u + lane;
-                off[u] = (own[u] == cs ? ca : 0u) + (pin[u] - asz[u]) - S.pb[own[u]];
-                const bool fits = g < G && pin[u] + 32u * (own[u] - cs + 1u) <= W;
-                const uint64_t bm = ballot(fits);
-                if (open) {
-                    const uint32_t k = bm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~bm);
-                    gcut += k;
-                    open = k == 64u;
-                }
-            }
-            gcut = uni(gcut);
-            if (gcut == 0) {
-                // the cursor's leaf is a value longer than any window: lane 0 hashes it from HBM
-                const uint64_t sof = shfl64(seg_off, cs);
-                const uint32_t sl = shfl32(L, cs);
-                const uint32_t mm = shfl32(m[0], 0);
-                if (lane == 0)
-                    *(uint64_t*)(pool + sof + 8ull * cl) = xxh64_lane(pool + sof + 16ull * sl + ca, mm >> 3);
-                ca += meta_arena(mm);
-                if (++cl >= shfl32(L, cs)) {
-                    cs++;
-                    cl = 0;
-                    ca = 0;
-                }
-                wave_sync_lds();
-                continue;
-            }
-            // pieces: segment j's staged range [lo & ~15, align16(hi)) of its arena
-            const uint32_t glast = gcut - 1u;
-            const uint32_t jl = uni(shfl32(own[glast >> 6], glast & 63u));  // last segment in the window
-            uint32_t hi = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {  // the end of each segment's last window leaf
-                const uint32_t g = u * 64u + lane;
-                const uint32_t oend_g = shfl32(lincl, own[u]);  // (not inside the && below: every lane must read)
-                const bool last = g < gcut && (g == glast || g + 1u == oend_g);
-                if (last) S.pb[own[u]] = off[u] + asz[u];  // (pb no longer needed: reuse it for hi)
-            }
-            wave_sync_lds();
-            const bool piece = lane >= cs && lane <= jl;
-            const uint32_t lo = piece ? (lane == cs ? ca : 0u) : 0u;
-            hi = piece ? S.pb[lane] : 0u;
-            const uint32_t c0 = lo & ~15u;
-            const uint32_t nch = piece && hi > lo ? ((hi + 15u) & ~15u) / 16u - c0 / 16u : 0u;
-            const uint32_t chincl = wave_incl_scan(nch);
-            const uint32_t nchunks = uni(shfl32(chincl, 63));
-            const uint32_t lbase = (chincl - nch) * 16u;  // this piece's LDS image offset
-            // stage: all loads in flight, then the LDS writes
-            constexpr uint32_t R = W / 1024u;
-            u32x4 v[R];
-            uint32_t dst[R];
-#pragma unroll
-            for (uint32_t r = 0; r < R; r++) {
-                const uint32_t c = r * 64u + lane;
-                // cross-lane reads with every lane active (ds_bpermute returns nothing useful from an
-                // inactive source lane), the load only where there is a chunk
-                const uint32_t o = min(lane_upper(chincl, c), 63u);
-                const uint32_t k = c - (shfl32(chincl, o) - shfl32(nch, o));
-                const uint64_t src = shfl64(seg_off, o) + 16ull * shfl32(L, o) + shfl32(c0, o) + 16ull * k;
-                dst[r] = ~0u;
-                if (c < nchunks) {
-                    v[r] = __builtin_nontemporal_load((const u32x4*)(pool + src));
-                    dst[r] = c * 4u;
-                }
-            }
-#pragma unroll
-            for (uint32_t r = 0; r < R; r++)
-                if (dst[r] != ~0u) *(u32x4*)(S.img + dst[r]) = v[r];
-            // the window's long values -> list
-            uint32_t nv = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t g = u * 64u + lane;
-                const bool lg = g < gcut && asz[u] != 0u;
-                const uint64_t bm = ballot(lg);
-                const uint32_t lbo = shfl32(lbase, own[u]), c0o = shfl32(c0, own[u]);
-                const uint64_t sof = shfl64(seg_off, own[u]);
-                if (lg) {
-                    const uint32_t pos = nv + popc64(bm & mask_lt(lane));
-                    S.vpos[pos] = (lbo + off[u] - c0o) | ((m[u] >> 3) << 16);
-                    S.vdig[pos] = sof + 8ull * leaf[u];
-                }
-                nv += popc64(bm);
-            }
-            wave_sync_lds();
-            for (uint32_t k = lane; k < nv; k += 64) {
-                const uint32_t vp = S.vpos[k];
-                const uint64_t h = xxh64_lds(S.img, vp & 0xFFFFu, vp >> 16);
-                *(uint64_t*)(pool + S.vdig[k]) = h;
-            }
-            // advance the cursor past leaf glast
-            const uint32_t llast = uni(shfl32(leaf[glast >> 6], glast & 63u));
-            const uint32_t oend = uni(shfl32(off[glast >> 6] + asz[glast >> 6], glast & 63u));
-            if (g_k1_trace && gw == 0) {
-                const uint32_t v0 = S.vpos[0];
-                if (lane == 0 && ntrace < g_k1_trace_cap) {
-                    uint32_t* t = g_k1_trace + 12u * ntrace;
-                    t[0] = pb0; t[1] = cs; t[2] = cl; t[3] = ca; t[4] = G; t[5] = gcut; t[6] = jl; t[7] = nchunks;
-                    t[8] = nv; t[9] = llast; t[10] = oend; t[11] = v0;
-                }
-                ntrace++;
-            }
-            if (llast + 1u >= uni(shfl32(L, jl))) {
-                cs = jl + 1u;
-                cl = 0;
-                ca = 0;
-            } else {
-                cs = jl;
-                cl = llast + 1u;
-                ca = oend;
-            }
-            wave_sync_lds();  // the next window rewrites the image and lists
-        }
-    }
 }
 
 // ---------------------------------------------------------------- K2
@@ -852,15 +349,15 @@ __device__ __forceinline__ uint32_t tile_lower_bound(uint32_t x, uint32_t tile, 
     return j;
 }
 
-// Byte-exact confirmation of every lane's pending (hash-equal, same length)
-// long value at once.  The lanes' values are flattened into one index space of
-// dwords (prefix sum of dword counts: values sit at 4-byte aligned arena
-// offsets, zero padded to 4, so two equal-length values are equal iff their
-// padded dwords are); each pass the wave compares 64 x CV_U dwords (consecutive
-// dwords of a value are consecutive addresses), finding a dword's owner lane by
-// a cross-lane binary search over the prefix sums.  No load reaches past a
-// value's padded end.  Returns true in the lanes whose value differs (a hash
-// collision).
+// Byte-exact confirmation of every lane's pending long value at once (same
+// length, same first 8 bytes): the tails of len bytes in the two arenas.  The
+// lanes' tails are flattened into one index space of dwords (prefix sum of
+// dword counts: tails sit at 4-byte aligned arena offsets, zero padded to 4, so
+// two equal-length tails are equal iff their padded dwords are); each pass the
+// wave compares 64 x CV_U dwords (consecutive dwords of a tail are consecutive
+// addresses), finding a dword's owner lane by a cross-lane binary search over
+// the prefix sums.  No load reaches past a tail's padded end.  Returns true in
+// the lanes whose tail differs.
 __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a, const uint8_t* arena_b,
                                uint32_t off_b, uint32_t len, uint32_t lane) {
     const uint32_t n4 = need ? (len + 3u) >> 2 : 0u;
@@ -896,7 +393,7 @@ __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a
 #pragma unroll
         for (int u = 0; u < CV_U; u++) {
             uint64_t m = ballot(act[u] && xa[u] != xb[u]);
-            while (m) {  // collisions only: practically never taken
+            while (m) {  // values that differ only past their first 8 bytes
                 const uint32_t j = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1;
                 bad |= 1ull << shfl32(own[u], j);
@@ -961,7 +458,8 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         const uint32_t obj = shfl32(offB, min(jA, 63u));
         const bool matchA = inA && jA < nb && kbj == ka;
         bool differ = matchA && (ma != mbj || xa != xbj);
-        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, ma >> 3, lane);
+        // equal head (the first 8 bytes, in vals) and length: confirm the tails in the arenas
+        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
         // resolve B keys against the A window
         const uint32_t iB = tile_lower_bound(kb, ka, na);
         const uint32_t kai = shfl32(ka, min(iB, 63u));
@@ -1476,11 +974,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     }
 }
 
-hipError_t k1_trace(uint32_t* dev_buf, uint32_t cap) {
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_k1_trace), &dev_buf, sizeof(dev_buf));
-    if (e != hipSuccess) return e;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_k1_trace_cap), &cap, sizeof(cap));
-}
 
 hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves) {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_k2_prof), &dev_buf, sizeof(dev_buf));
@@ -1580,34 +1073,7 @@ hipError_t launch_rebase(hipStream_t s, gpudiff_pair_row* rows, uint32_t begin, 
     return hipGetLastError();
 }
 
-typedef void (*K1Fn)(const gpudiff_pair_row*, uint32_t, uint32_t, uint8_t*, bool);
-static K1Fn k1_kernel(uint32_t variant) {
-    switch (variant) {
-        case 1: return k_value_hash_win<8192>;
-        case 2: return k_value_hash_list;
-        case 3: return k_value_hash_win<2048>;
-        default: return k_value_hash_win<4096>;
-    }
-}
 
-hipError_t launch_value_hash(hipStream_t s, const gpudiff_pair_row* rows, uint32_t begin, uint32_t end, uint8_t* pool,
-                             bool fresh_only, uint32_t variant) {
-    if (end <= begin) return hipSuccess;
-    // one resident block per CU per slot the kernel's occupancy allows, and >= 16 pairs per wave
-    static int occ[4] = {0, 0, 0, 0};
-    variant &= 3u;
-    const K1Fn fn = k1_kernel(variant);
-    if (!occ[variant]) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, reinterpret_cast<const void*>(fn), 256, 0) != hipSuccess ||
-            o <= 0)
-            o = 4;
-        occ[variant] = o;
-    }
-    fn<<<grid_for(((uint64_t)(end - begin) + 15) / 16, 256u * (uint32_t)occ[variant]), 256, 0, s>>>(rows, begin, end,
-                                                                                                   pool, fresh_only);
-    return hipGetLastError();
-}
 
 hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, const BlobMove* moves, uint32_t n) {
     if (!n) return hipSuccess;

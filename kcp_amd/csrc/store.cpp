@@ -17,8 +17,8 @@
 //      the batch does not fit (K7 k_move_blobs packs every live blob and every
 //      blob this batch still reads), offsets are finalised, and one H2D copies
 //      the batch's blobs behind the space's append point;
-//   4. K1 hashes the long values of the fresh blobs only, and the ordinary diff
-//      pass (K2..K6, gpudiff_diff) runs over the batch's (resident, new) rows.
+//   4. the ordinary diff pass (K2..K6, gpudiff_diff) runs over the batch's
+//      (resident, new) rows.
 #include <string.h>
 
 #include <algorithm>
@@ -237,8 +237,8 @@ static void store_encode_part(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_ev
             r.stat_ar_b = tar;
             r.flags_b = w.fn.flags | (seed << GPUDIFF_OBJ_SEED_SHIFT) | GPUDIFF_OBJ_FRESH;
         } else {
-            // the conservative row reads nothing; K1 must still hash the stored blob: give it a
-            // row of its own side only (flags_b FRESH with zero-length A)
+            // the conservative row reads nothing (decode error): it still names the stored blob,
+            // on its own side only (flags_b FRESH with zero-length A)
             r.off_b = local_tag(t, off);
             r.spec_l_b = sl;
             r.spec_ar_b = sar;
@@ -397,7 +397,7 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
         s->st.collisions_unresolved += w.unresolved;
         w.old_encoded = w.reseeded = w.unresolved = 0;
     }
-    // 4: stage (pinned), H2D, K1 on the fresh blobs, diff
+    // 4: stage (pinned), H2D, diff
     gpudiff_hbatch*& hb = s->staging[slot_ring];
     uint8_t* hp = nullptr;
     gpudiff_pair_row* hr = nullptr;
@@ -417,8 +417,6 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
     if (hb->used) HIPCHK(hipEventRecord(hb->used, c->stream));
     if (n) {
         HIPCHK(launch_rebase(c->stream, d->rows, 0, (uint32_t)n, 0, d->pair_ids));  // pair_ids SoA copy
-        if (!c->ecfg.host_value_hash && !(c->flags & GPUDIFF_OPT_NO_VALUE_HASH))
-            HIPCHK(launch_value_hash(c->stream, d->rows, 0, (uint32_t)n, space, true, c->flags >> GPUDIFF_OPT_K1_VARIANT_SHIFT));
     }
     s->used += total;
     d->pool = space;

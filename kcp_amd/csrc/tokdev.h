@@ -150,8 +150,9 @@ __device__ __forceinline__ uint64_t hash_bytes(const uint8_t* p, uint32_t len) {
 
 __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + arena; }
 __device__ __forceinline__ uint32_t meta_arena(uint32_t m) {
-    // long strings at 4-byte aligned arena offsets (include/gpudiff_format.h)
-    return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) + 3u) & ~3u) : 0u;
+    // long strings: the tail past the first 8 bytes, at a 4-byte aligned arena offset (include/gpudiff_format.h)
+    return ((m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > GPUDIFF_INLINE_MAX) ? (((m >> 3) - GPUDIFF_INLINE_MAX + 3u) & ~3u)
+                                                                         : 0u;
 }
 
 __device__ __forceinline__ bool is_ws(uint32_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }

@@ -1,8 +1,8 @@
 // K0 k_encode_docs: device JSON tokenizer + canonical encoder (gfx950, wave64).
 //
 // One wave per document (a raw informer event body).  The output is the blob
-// the host encoder writes for the same object (encoder.cpp write_blob with
-// value digests filled) plus the fingerprint trailer of the object store:
+// the host encoder writes for the same object (encoder.cpp write_blob) plus
+// the path-table trailer of the object store:
 // byte-identical, so the diff kernels cannot tell the two producers apart.
 //
 // Phases (all inside one wave, working set in a per-document scratch area):
@@ -469,8 +469,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     sl = (uint32_t)dl;
                 }
                 mlen = sl;
+                // the value's first 8 bytes (a long string's tail goes to the arena in phase 5)
                 if (sl <= GPUDIFF_INLINE_MAX) v = sl ? (ld8u(src) & (~0ull >> (64u - 8u * sl))) : 0ull;
-                else v = hash_bytes(src, sl);
+                else v = ld8u(src);
             } else if (r.w & NI_ATOM) {
                 const uint32_t ap = S.tok[r.z] & POS_MASK;
                 const uint32_t e = parse_atom(d + ap, d + len, &tag, &v);
@@ -704,8 +705,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 }
                 trank += popc64(tbal);
                 tko += rdlane(kinc, 63);
-                // long strings: wave-cooperative dword copies into the arena (values at
-                // 4-byte aligned offsets; the last dword's bytes past the value are zero)
+                // long strings: wave-cooperative dword copies of the tail (the bytes after the
+                // first 8, which sit in the leaf record) into the arena (tails at 4-byte aligned
+                // offsets; the last dword's bytes past the value are zero)
                 for (uint64_t bl = ballot(ar != 0); bl; bl &= bl - 1) {
                     const uint32_t src_lane = (uint32_t)__builtin_ctzll(bl);
                     const uint32_t si = rdlane(i, src_lane);
@@ -714,8 +716,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t sa = rdlane(my_aoff, src_lane);
                     const uint4 rr = S.rec[si];
                     const uint32_t op = S.tok[rr.z] & POS_MASK;
-                    const uint8_t* src = (rr.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1);
-                    const uint32_t slen = sm >> 3;
+                    const uint8_t* src = ((rr.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1)) + GPUDIFF_INLINE_MAX;
+                    const uint32_t slen = (sm >> 3) - GPUDIFF_INLINE_MAX;
                     uint32_t* dst = (uint32_t*)(segp[sg] + 16ull * Lr[sg] + sa);
                     for (uint32_t c4 = lane; c4 * 4u < slen; c4 += 64) {
                         uint32_t w = (uint32_t)ld8u(src + 4u * c4);

@@ -23,7 +23,7 @@ E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUN
 SPEC_DIRTY, STATUS_DIRTY, DECODE_ERROR, SPEC_NOOP, STATUS_NOOP = 0x1, 0x2, 0x4, 0x8, 0x10
 PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
-OPT_TIMING, OPT_HOST_VALUE_HASH, OPT_NO_VALUE_HASH, OPT_DEVICE_VALUE_HASH = 0x1, 0x2, 0x4, 0x8
+OPT_TIMING = 0x1
 OPT_DEVICE_ENCODE = 0x2000000
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
@@ -183,11 +183,11 @@ class DeviceView(C.Structure):
 
 class BatchStats(C.Structure):
     _fields_ = [("n_pairs", C.c_uint64), ("pool_bytes", C.c_uint64), ("total_leaves", C.c_uint64),
-                ("compare_bytes", C.c_uint64), ("value_bytes", C.c_uint64), ("hash_bytes", C.c_uint64)]
+                ("compare_bytes", C.c_uint64), ("value_bytes", C.c_uint64)]
 
 
 class Timings(C.Structure):
-    _fields_ = [("value_hash_ms", C.c_float), ("compare_ms", C.c_float), ("compact_ms", C.c_float),
+    _fields_ = [("compare_ms", C.c_float), ("compact_ms", C.c_float),
                 ("join_ms", C.c_float), ("emit_ms", C.c_float), ("total_ms", C.c_float),
                 ("n_passes", C.c_uint32), ("k2_launches", C.c_uint32)]
 
@@ -205,7 +205,6 @@ SIGNATURES = [
     ("gpudiff_hbatch_free", None, [_P, _P]),
     ("gpudiff_dbatch_create", C.c_int, [_P, C.c_uint64, C.c_uint64, C.POINTER(_P)]),
     ("gpudiff_dbatch_append", C.c_int, [_P, _P, _P]),
-    ("gpudiff_dbatch_hash_values", C.c_int, [_P, _P]),
     ("gpudiff_dbatch_reset", C.c_int, [_P, _P]),
     ("gpudiff_dbatch_stats_get", C.c_int, [_P, C.POINTER(BatchStats)]),
     ("gpudiff_dbatch_device_view", C.c_int, [_P, C.POINTER(DeviceView)]),
@@ -235,7 +234,6 @@ SIGNATURES = [
                                              C.POINTER(ObjInfo)]),
     ("gpudiff_k0_profile", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
     ("gpudiff_k2_profile", C.c_int, [_P, C.c_void_p, C.c_uint32]),
-    ("gpudiff_k1_trace", C.c_int, [_P, C.c_void_p, C.c_uint32]),
     ("gpudiff_upsert_bodies", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.c_size_t, C.c_uint32,
                                         C.POINTER(Bodies)]),
     ("gpudiff_bodies_release", None, [_P, C.POINTER(Bodies)]),
@@ -406,10 +404,6 @@ class DeviceBatch:
     def append(self, hb: HostBatch):
         _chk(_lib.gpudiff_dbatch_append(self.engine.ctx, self.h, hb.h), "gpudiff_dbatch_append")
 
-    def hash_values(self):
-        """K1 over every resident pair (asynchronous; value_hash_ms with timing)."""
-        _chk(_lib.gpudiff_dbatch_hash_values(self.engine.ctx, self.h), "gpudiff_dbatch_hash_values")
-
     def reset(self):
         _chk(_lib.gpudiff_dbatch_reset(self.engine.ctx, self.h), "gpudiff_dbatch_reset")
 
@@ -525,16 +519,10 @@ class Engine:
     """One gpudiff context (one GPU, one stream, one submitting thread)."""
 
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
-                 timing: bool = False, path_hash_bits: int = PATH_HASH_BITS, host_value_hash: bool = False,
-                 no_value_hash: bool = False, flags: int = 0, device_encode: bool = False,
-                 device_value_hash: bool = False):
-        """Value digests of long strings come from the host encoder by default; device_value_hash=True
-        hashes them with kernel K1 after each upload instead."""
+                 timing: bool = False, path_hash_bits: int = PATH_HASH_BITS, flags: int = 0,
+                 device_encode: bool = False):
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
-                 flags=(OPT_TIMING if timing else 0) | (OPT_HOST_VALUE_HASH if host_value_hash else 0) |
-                       (OPT_DEVICE_VALUE_HASH if device_value_hash else 0) |
-                       (OPT_NO_VALUE_HASH if no_value_hash else 0) | (OPT_DEVICE_ENCODE if device_encode else 0) |
-                       flags,
+                 flags=(OPT_TIMING if timing else 0) | (OPT_DEVICE_ENCODE if device_encode else 0) | flags,
                  path_hash_bits=path_hash_bits)
         h = C.c_void_p()
         _chk(_lib.gpudiff_open(C.byref(o), C.byref(h)), "gpudiff_open")
@@ -734,10 +722,6 @@ class Engine:
         out = (C.c_uint64 * 8)()
         _chk(_lib.gpudiff_k0_profile(self.ctx, 1 if enable else 0, out), "gpudiff_k0_profile")
         return list(out)
-
-    def k1_trace(self, dev_ptr: int, cap: int):
-        """Record the windowed K1's first-wave window trace (12 u32 per window) into device memory."""
-        _chk(_lib.gpudiff_k1_trace(self.ctx, dev_ptr or None, cap), "gpudiff_k1_trace")
 
     def k2_profile(self, dev_ptr: int, cap_waves: int):
         """Record K2 variant 14's per-wave timeline into device memory (8 u64 per wave); 0 stops."""
@@ -1102,8 +1086,9 @@ def decode_path_table(blob: bytes, info: dict):
 
 
 def decode_segment(pool: bytes, off: int, L: int, arena: int):
-    """Canonical segment -> list of (key, val, meta, value_bytes).  Long
-    strings sit in the arena at 4-byte aligned offsets (include/gpudiff_format.h)."""
+    """Canonical segment -> list of (key, val, meta, value_bytes).  A long
+    string's first 8 bytes sit in its value slot, its tail in the arena at a
+    4-byte aligned offset (include/gpudiff_format.h)."""
     vals = np.frombuffer(pool, dtype="<u8", count=L, offset=off) if L else np.zeros(0, "<u8")
     keys = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 8 * L) if L else np.zeros(0, "<u4")
     metas = np.frombuffer(pool, dtype="<u4", count=L, offset=off + 12 * L) if L else np.zeros(0, "<u4")
@@ -1113,8 +1098,8 @@ def decode_segment(pool: bytes, off: int, L: int, arena: int):
     for k, v, m in zip(keys.tolist(), vals.tolist(), metas.tolist()):
         tag, ln = m & 7, m >> 3
         if tag == 5 and ln > 8:
-            vb = pool[ar:ar + ln]
-            ar += (ln + 3) & ~3
+            vb = int(v).to_bytes(8, "little") + bytes(pool[ar:ar + ln - 8])
+            ar += (ln - 8 + 3) & ~3
         elif tag == 5:
             vb = int(v).to_bytes(8, "little")[:ln]
         elif tag in (3, 4):

@@ -10,8 +10,8 @@
 // segments are byte-identical", and for a dirty pair the build-defined
 // field-path diff as a merge-join of the two sorted
 // key arrays: equal keys whose (meta, value) differ are CHANGED, keys only in
-// A REMOVED, only in B ADDED; long strings compared by their arena bytes (the
-// host pool holds no value digests).  Written from the format definition, not
+// A REMOVED, only in B ADDED; a long string is its first 8 bytes in the value
+// slot plus its tail in the arena, and both are compared.  Written from the format definition, not
 // from the kernels' code; parity with the device is checked by the bench's
 // three-way sample check and tests/test_oracle_cpp.py.
 #include <stdint.h>
@@ -60,13 +60,9 @@ void join(const Seg& a, const Seg& b, uint8_t region, Emit&& emit) {
             ob += gpudiff_meta_arena(mb[j]);
             j++;
         } else {
-            bool same = ma[i] == mb[j];
-            if (same) {
-                if (gpudiff_meta_is_long(ma[i]))
-                    same = memcmp(a.arena() + oa, b.arena() + ob, gpudiff_meta_len(ma[i])) == 0;
-                else
-                    same = va[i] == vb[j];
-            }
+            bool same = ma[i] == mb[j] && va[i] == vb[j];
+            if (same && gpudiff_meta_is_long(ma[i]))
+                same = memcmp(a.arena() + oa, b.arena() + ob, gpudiff_meta_len(ma[i]) - GPUDIFF_INLINE_MAX) == 0;
             if (!same) emit(ka[i], (uint8_t)(GPUDIFF_PATH_CHANGED | region));
             oa += gpudiff_meta_arena(ma[i]);
             ob += gpudiff_meta_arena(mb[j]);

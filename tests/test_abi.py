@@ -39,7 +39,7 @@ def test_host_only_context_refuses_device_work():
     with pytest.raises(G.GpuDiffError) as ei:
         e.submit([(b"{}", b"{}")])
     assert ei.value.code == G.E_NODEVICE
-    assert G.lib().gpudiff_abi_version() == 3
+    assert G.lib().gpudiff_abi_version() == 4
     e.close()
 
 

@@ -8,7 +8,6 @@ import random
 
 import numpy as np
 import pytest
-import xxhash
 from hypothesis import given, settings, strategies as st
 
 from kcp_amd import gpudiff as G
@@ -125,17 +124,41 @@ def test_bodies_line_aligned_and_zero_padded(host_engine):
             assert pool[off + la:off + body] == bytes(body - la)
 
 
-def test_value_hash_host_matches_xxhash():
-    e = G.Engine(device=G.DEVICE_NONE, host_value_hash=True)
+def test_long_values_head_in_record_tail_in_arena():
+    """A long string (> 8 bytes) keeps its first 8 bytes in the leaf's value slot and the rest in the
+    arena at a 4-byte aligned offset, zero padded (include/gpudiff_format.h): decode_segment reads every
+    value of the KAT base object back whole, and the arena holds exactly the tails."""
+    e = G.Engine(device=G.DEVICE_NONE)
     hb = e.encode([(J(BASE), J(BASE))])
     pool = hb.pool()
     r = hb.rows()[0]
-    n_long = 0
-    for (k, v, m, vb) in G.decode_segment(pool, int(r["off_a"]), int(r["spec_l_a"]), int(r["spec_ar_a"])):
-        if (m & 7) == 5 and (m >> 3) > 8:
-            assert v == xxhash.xxh64_intdigest(vb)
-            n_long += 1
-    assert n_long > 5
+    off, sl, sar = int(r["off_a"]), int(r["spec_l_a"]), int(r["spec_ar_a"])
+    seg = G.decode_segment(pool, off, sl, sar)
+    longs = [(v, m, vb) for (k, v, m, vb) in seg if (m & 7) == 5 and (m >> 3) > 8]
+    assert len(longs) > 5
+    arena = pool[off + 16 * sl:off + 16 * sl + sar]
+    pos = 0
+    for v, m, vb in longs:
+        assert len(vb) == m >> 3 and int(v).to_bytes(8, "little") == vb[:8]
+        tail = vb[8:]
+        assert arena[pos:pos + len(tail)] == tail
+        pad = (len(tail) + 3) & ~3
+        assert arena[pos + len(tail):pos + pad] == bytes(pad - len(tail))
+        pos += pad
+    assert sar == (pos + 15) & ~15 and arena[pos:] == bytes(sar - pos)
+    strings = set()
+
+    def walk(x):
+        if isinstance(x, str):
+            strings.add(x.encode())
+        elif isinstance(x, dict):
+            for y in x.values():
+                walk(y)
+        elif isinstance(x, list):
+            for y in x:
+                walk(y)
+    walk(json.loads(J(BASE)))
+    assert all(vb in strings for (v, m, vb) in longs)
     e.close()
 
 

@@ -2,15 +2,14 @@
 
 Covers the Appendix A.4 KAT table, mixed synthetic populations (configs 1-4
 shapes, 5% mutated), deep objects (>64 leaves per region -> multi-window
-merge-join, values >32 B -> XXH64 stripes), forced path-hash collisions,
-multi-chunk batches (scan tiles), appends, single-pair drop-ins, and K1's
-device value hashes against the xxhash package."""
+merge-join, long values split into an 8-B head and an arena tail), forced
+path-hash collisions, multi-chunk batches (scan tiles), appends and
+single-pair drop-ins."""
 import json
 import random
 
 import numpy as np
 import pytest
-import xxhash
 
 from kcp_amd import gpudiff as G
 from oracle import gpudiff_oracle as O
@@ -148,23 +147,12 @@ def test_forced_collisions(dev):
     e.close()
 
 
-def test_host_vs_device_value_hash(eng):
-    """Digests from the host encoder (the default) and from K1 at ingest give identical results."""
-    pairs, _, _ = make_pairs(400, seed=6, mutate_frac=0.3)
-    e2 = G.Engine(device=0, device_value_hash=True)
-    r1 = eng.diff_pairs(pairs)
-    r2 = e2.diff_pairs(pairs)
-    for f in ("pair_flags", "spec_dirty_ids", "status_dirty_ids", "dirty_ids", "path_offsets", "path_hashes",
-              "path_kinds"):
-        assert np.array_equal(getattr(r1, f), getattr(r2, f)), f
-    e2.close()
-
-
 @pytest.mark.parametrize("shrink", [0, 14])
-def test_byte_confirmation_without_digests(shrink):
-    """With value digests left at 0, every equal-length long value is decided
-    by the byte confirmation alone -- the path a digest collision takes -- both
-    for joins inside K2 (shrink 0) and in K4 (shrink 14: every pair deferred)."""
+def test_tail_confirmation(shrink):
+    """Long values of equal length whose first 8 bytes (the head, in the leaf record) agree are decided by
+    the byte confirmation of their tails in the arenas: one flipped byte anywhere in a 9-400 byte value,
+    at least half of them past the head, both for joins inside K2 (shrink 0) and in K4 (shrink 14: every
+    pair deferred)."""
     rnd = random.Random(12)
     pairs = []
     for i in range(300):
@@ -174,46 +162,23 @@ def test_byte_confirmation_without_digests(shrink):
         if i % 2:
             k = rnd.randrange(12)
             s = b["spec"]["vals"][k]
-            j = rnd.randrange(len(s))
+            j = rnd.randrange(8, len(s)) if i % 4 == 1 else rnd.randrange(len(s))
             b["spec"]["vals"][k] = s[:j] + ("x" if s[j] == "y" else "y") + s[j + 1:]  # same length, one byte
         pairs.append((J(a), J(b)))
-    e = G.Engine(device=0, no_value_hash=True, flags=shrink << 21)
+    e = G.Engine(device=0, flags=shrink << 21)
     res = e.diff_pairs(pairs)
     assert_matches(res, pairs)
     e.close()
 
 
-def test_k1_value_hashes_on_device(eng):
-    pairs, _, _ = make_pairs(100, seed=7)
-    hb = eng.encode(pairs)
-    info = hb.info()
-    db = eng.device_batch(info.pool_bytes + 1024, len(pairs))
-    db.append(hb)
-    eng.sync()
-    pool = db.read_pool(0, info.pool_bytes)
-    rows = hb.rows()
-    checked = 0
-    for r in rows:
-        for off, sl, sar in ((int(r["off_a"]), int(r["spec_l_a"]), int(r["spec_ar_a"])),
-                             (int(r["off_b"]), int(r["spec_l_b"]), int(r["spec_ar_b"]))):
-            for (k, v, m, vb) in G.decode_segment(pool, off, sl, sar):
-                if (m & 7) == 5 and (m >> 3) > 8:
-                    assert v == xxhash.xxh64_intdigest(vb)
-                    checked += 1
-    assert checked > 1000
-    db.free()
-    hb.free()
-
-
-def _k1_corpus():
-    """Long values of every length class K1 handles differently: tail-only (9-31 B), whole 128-B bursts
-    and partial ones, values past a burst, a 5 KB value, and one object with 700 long values (its lane
-    fills the wave's list several times); in spec and status segments of both objects."""
-    import random
+def _long_value_corpus():
+    """Long values of every length class the format splits differently: 9-70 B (tails of 1-62 B), values
+    around 128-B lines, a 5 KB value, non-ASCII bytes, and one object with 700 long values; in spec and
+    status segments of both objects."""
     rnd = random.Random(11)
     out = []
     for n in list(range(9, 70)) + [95, 96, 97, 127, 128, 129, 130, 159, 160, 161, 255, 256, 257, 511, 512, 513, 5000]:
-        a = {"kind": "ConfigMap", "metadata": {"name": "k1-%d" % n},
+        a = {"kind": "ConfigMap", "metadata": {"name": "lv-%d" % n},
              "data": {"v%d" % j: "".join(rnd.choice("abcdefgh\u00e9") for _ in range(n + j)) for j in range(3)},
              "status": {"s": "x" * (n + 5), "short": "y" * 7}}
         b = json.loads(json.dumps(a))
@@ -224,37 +189,60 @@ def _k1_corpus():
     return out
 
 
-@pytest.mark.parametrize("k1_variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("n_pairs", [1, 37, 3000])
-def test_k1_digests_equal_host_encoder(n_pairs, k1_variant):
-    """K1's pool after ingest is byte-identical to the host encoder's with host-side XXH64 digests (every
-    segment of both objects: digests in place, nothing else touched), and a stand-alone K1 pass over the
-    resident batch (gpudiff_dbatch_hash_values) rewrites the same bytes.  Every K1 tuning variant."""
-    eng = G.Engine(device=0, encode_threads=8, flags=k1_variant << 30, device_value_hash=True)
-    pairs, _, _ = make_pairs(n_pairs, seed=70 + n_pairs, mutate_frac=0.2)
-    if n_pairs > 1:
-        pairs = _k1_corpus() + pairs
-    host = G.Engine(device=G.DEVICE_NONE, host_value_hash=True)
-    ref = host.encode(pairs)
+def _json_strings(x, out):
+    if isinstance(x, str):
+        out.append(x.encode())
+    elif isinstance(x, dict):
+        for v in x.values():
+            _json_strings(v, out)
+    elif isinstance(x, list):
+        for v in x:
+            _json_strings(v, out)
+    return out
+
+
+def test_value_heads_and_tails_resident(eng):
+    """After the upload the resident pool is the host encoder's byte for byte, and every long string reads
+    back whole from its head (the leaf's 8-B value slot) and its tail (the arena): the multiset of long
+    values per object equals the JSON's strings longer than 8 bytes in the compared regions."""
+    pairs = _long_value_corpus()
     hb = eng.encode(pairs)
     info = hb.info()
-    assert info.pool_bytes == ref.info().pool_bytes
     db = eng.device_batch(info.pool_bytes + 1024, len(pairs))
     db.append(hb)
     eng.sync()
-    want = ref.pool()
-    assert db.read_pool(0, info.pool_bytes) == want
-    assert db.stats().hash_bytes > 0
-    db.hash_values()
-    eng.sync()
-    assert db.read_pool(0, info.pool_bytes) == want
+    pool = db.read_pool(0, info.pool_bytes)
+    assert pool == hb.pool()
+    checked = 0
+    for r, (ja, jb) in zip(hb.rows(), pairs):
+        for side, js in (("a", ja), ("b", jb)):
+            off, sl, sar = int(r["off_" + side]), int(r["spec_l_" + side]), int(r["spec_ar_" + side])
+            tl, tar = int(r["stat_l_" + side]), int(r["stat_ar_" + side])
+            got = [vb for (k, v, m, vb) in G.decode_segment(pool, off, sl, sar) +
+                   G.decode_segment(pool, off + G.segment_bytes(sl, sar), tl, tar) if (m & 7) == 5 and (m >> 3) > 8]
+            obj = json.loads(js)
+            want = [x for x in _json_strings({k: v for k, v in obj.items() if k != "metadata"}, []) if len(x) > 8]
+            assert sorted(got) == sorted(want)
+            checked += len(got)
+    assert checked > 1000
     res = eng.wait(eng.diff(db))
     assert_matches(res, pairs)
     db.free()
     hb.free()
-    ref.free()
-    host.close()
-    eng.close()
+
+
+@pytest.mark.parametrize("dev", [False, True], ids=["host_encode", "device_encode"])
+@pytest.mark.parametrize("n_pairs", [1, 37, 3000])
+def test_long_value_corpus_vs_oracle(n_pairs, dev):
+    """The long-value corpus plus mixed populations through both encoders (host CSR / K0): flags, ID lists
+    and changed paths equal the oracle's."""
+    e = G.Engine(device=0, encode_threads=8, device_encode=dev)
+    pairs, _, _ = make_pairs(n_pairs, seed=70 + n_pairs, mutate_frac=0.2)
+    if n_pairs > 1:
+        pairs = _long_value_corpus() + pairs
+    res = e.diff_pairs(pairs)
+    assert_matches(res, pairs)
+    e.close()
 
 
 def test_append_chunks_and_rediff(eng):

@@ -88,7 +88,7 @@ def test_csr_paths_ptr_threads_equal_single_pass():
     from tests.parity import expected_paths, oracle_batch
     from tests.workload import make_pairs
     pairs, _, _ = make_pairs(9000, seed=31, mutate_frac=0.2)
-    e = G.Engine(device=G.DEVICE_NONE, encode_threads=4, host_value_hash=True)
+    e = G.Engine(device=G.DEVICE_NONE, encode_threads=4)
     hb = e.encode(pairs)
     rows = hb.rows()
     f1, o1, h1, k1 = cpu_ref.CsrPairs(hb.pool(), rows).paths()
