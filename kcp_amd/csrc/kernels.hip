@@ -728,7 +728,15 @@ static inline uint32_t k2_tail_q(const DiffBuffers& b) {
 __device__ uint64_t* g_k2_prof;
 __device__ uint32_t g_k2_prof_cap;
 
-template <int U, int MINB, bool DYN = false, bool PROF = false>
+// RPF (with DYN): the next main item's 64 rows are fetched into LDS by direct-to-LDS loads
+// (global_load_lds_dwordx4: no VGPRs held) as soon as its ticket is known -- after the current
+// item's first streaming pass -- so an item no longer starts with a dependent HBM round trip for
+// its rows (under a saturated memory system that round trip costs several microseconds: a
+// config4 pair's single-pair item spent ~14% of its time outside streaming and joining,
+// profiles/r03g/wave_c4.json). One 4 KiB buffer per wave suffices: an item's rows are read from it
+// before its first loads issue (their addresses depend on them), and the next prefetch into it is
+// issued only after that first pass.
+template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -750,6 +758,47 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    __shared__ u32x4 rowbuf[RPF ? 4 * 4 * 64 : 1];  // [wave in block][16-B piece][lane]
+    const uint32_t wv = threadIdx.x >> 6;
+    uint32_t pf_item = ~0u;     // the item whose rows are in this wave's rowbuf (wave-uniform)
+    // RPF: an item's result stores are issued after the next item's rows are read, so no item waits for
+    // the previous item's stores to complete (gfx9 counts stores in vmcnt, and both the ticket read and
+    // the LDS read of prefetched rows wait on vmcnt): per lane its flag, cap, path source / count,
+    // no-op bits and seed; per wave the item's first pair, size, 64-pair chunk, split shift and counts
+    uint32_t q_flag = 0, q_cap = 0, q_src = 0, q_cnt = 0, q_noop = 0, q_seed = 0;
+    uint32_t q_p0 = 0, q_n = 0, q_c = 0, q_ish = 0, q_ns = 0, q_nt = 0, q_nd = 0, q_cs = 0;
+    bool q_pending = false;
+    auto flush = [&]() {
+        if (!q_pending) return;
+        q_pending = false;
+        const bool dirty = (q_flag & (F_SPEC | F_STATUS)) != 0u;
+        if (lane < q_n) {
+            flags[q_p0 + lane] = (uint8_t)q_flag;
+            if (dirty) {
+                caps[q_p0 + lane] = q_cap;
+                path_src[q_p0 + lane] = q_src;
+                path_cnt[q_p0 + lane] = q_cnt;
+                nbits[q_p0 + lane] = (uint8_t)q_noop;
+                // a status-absent-only pair's one path (the sentinel), written lane-parallel here
+                if ((q_flag & F_SENT) && !(q_flag & (F_JSPEC | F_JSTAT | F_DEFER))) {
+                    ah[q_src] = (q_flag & F_SEED) ? status_sentinel_hash(q_seed, mask) : sent0;
+                    ak[q_src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                }
+            }
+        }
+        if (lane == 0) {
+            if (!q_ish) {
+                chunk_counts[q_c] = make_uint4(q_ns, q_nt, q_nd, q_cs);
+            } else if (q_ns | q_nt | q_nd | q_cs) {
+                uint32_t* cc = (uint32_t*)(chunk_counts + q_c);
+                atomicAdd(cc + 0, q_ns);
+                atomicAdd(cc + 1, q_nt);
+                atomicAdd(cc + 2, q_nd);
+                atomicAdd(cc + 3, q_cs);
+            }
+        }
+    };
     [[maybe_unused]] uint64_t tp_start = 0, tp_first = 0, tp_last = 0, tp_stream = 0, tp_join = 0, tp_items = 0;
     if constexpr (PROF) tp_start = wall_clock64();
     const uint32_t nch = c_end - c_begin;
@@ -802,13 +851,23 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const bool valid = lane < cnt;
         // ---- rows: lane k holds pair p0 + k
         u32x4 v0 = {0, 0, 0, 0}, v1 = v0, v2 = v0, v3 = v0;
-        if (valid) {
+        if (RPF && it == pf_item) {  // prefetched into LDS during the previous item
+            if (valid) {
+                const u32x4* rb = rowbuf + wv * 256u + lane;
+                v0 = rb[0];
+                v1 = rb[64];
+                v2 = rb[128];
+                v3 = rb[192];
+            }
+        } else if (valid) {
             const u32x4* rp = (const u32x4*)(rows + p0 + lane);
             v0 = rp[0];  // off_a, off_b
             v1 = rp[1];  // spec_l_a, spec_l_b, spec_ar_a, spec_ar_b
             v2 = rp[2];  // stat_l_a, stat_l_b, stat_ar_a, stat_ar_b
             v3 = rp[3];  // flags_a, flags_b, pair_id, cluster_id
         }
+        pf_item = ~0u;
+        if constexpr (RPF) flush();  // the previous item's results
         const uint64_t off_a = ((uint64_t)v0.y << 32) | v0.x, off_b = ((uint64_t)v0.w << 32) | v0.z;
         const bool err = valid && ((v3.x | v3.y) & GPUDIFF_OBJ_DECODE_ERR) != 0u;
         const bool ok = valid && !err;
@@ -868,6 +927,26 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     else mis_s |= bit;
                 }
             }
+            if constexpr (RPF && DYN) {
+                // after the first pass the next main ticket (fetched as this item started, before its
+                // rows and first loads) is back: start its rows' trip into LDS
+                if (base == 0u && it < pf_end) {
+                    const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
+                    const uint32_t q0 = ((c_begin + (nx >> sub_shift)) << 6) +
+                                        (nx & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
+                    if (nx < n_full && q0 < n) {
+                        if (lane < min(64u >> sub_shift, n - q0)) {
+                            const u32x4* rp = (const u32x4*)(rows + q0 + lane);
+                            u32x4* rb = rowbuf + wv * 256u;
+                            __builtin_amdgcn_global_load_lds(rp + 0, (lds_ptr)(rb + 0), 16, 0, 0);
+                            __builtin_amdgcn_global_load_lds(rp + 1, (lds_ptr)(rb + 64), 16, 0, 0);
+                            __builtin_amdgcn_global_load_lds(rp + 2, (lds_ptr)(rb + 128), 16, 0, 0);
+                            __builtin_amdgcn_global_load_lds(rp + 3, (lds_ptr)(rb + 192), 16, 0, 0);
+                        }
+                        pf_item = nx;
+                    }
+                }
+            }
         }
         [[maybe_unused]] uint64_t tp_s1 = 0;
         if constexpr (PROF) {
@@ -903,7 +982,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
                     const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
                     nb = sentinel_noop_bits(fa);
-                    if (lane == 0) {
+                    if (!RPF && lane == 0) {  // RPF: written lane-parallel by flush()
                         ah[src] = (fk & F_SEED) ? status_sentinel_hash((fa >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
                                                 : sent0;
                         ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
@@ -932,6 +1011,28 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             if (tp_items == 1) tp_first = t;
         }
         const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
+        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
+        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
+        const uint32_t nd = popc64(ballot(dirty));
+        const uint32_t cs = wave_sum(dirty ? mycap : 0u);
+        if constexpr (RPF) {
+            q_flag = myflag;
+            q_cap = mycap;
+            q_src = mysrc;
+            q_cnt = mycnt;
+            q_noop = mynoop;
+            q_seed = (v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu;
+            q_p0 = p0;
+            q_n = cnt;
+            q_c = c;
+            q_ish = ish;
+            q_ns = ns;
+            q_nt = nt;
+            q_nd = nd;
+            q_cs = cs;
+            q_pending = true;
+            continue;
+        }
         if (valid) {
             flags[p0 + lane] = (uint8_t)myflag;
             if (dirty) {
@@ -941,10 +1042,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 nbits[p0 + lane] = (uint8_t)mynoop;
             }
         }
-        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
-        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
-        const uint32_t nd = popc64(ballot(dirty));
-        const uint32_t cs = wave_sum(dirty ? mycap : 0u);
         if (lane == 0) {
             if (!ish) {
                 chunk_counts[c] = make_uint4(ns, nt, nd, cs);
@@ -957,6 +1054,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             }
         }
     }
+    if constexpr (RPF) flush();  // the last item's results
     if (deferred && lane == 0) summary[6] = 1u;
     if constexpr (PROF) {
         const uint64_t t_end = wall_clock64();
@@ -1099,18 +1197,18 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 11: return k_compare_flat<2, 5>;
         case 12: return k_compare_flat<4, 5>;
         case 13: return k_compare<true, 4, 1>;  // round 1's default (wave per pair)
-        case 10: return k_compare_flat<4, 4>;
-        case 14: return k_compare_flat<4, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
+        case 10: return k_compare_flat<4, 1, true>;  // round 2's default: rows loaded as each item starts
+        case 14: return k_compare_flat<4, 1, true, true, true>;  // the default + per-wave timeline (g_k2_prof)
         case 15: return k_compare_flat<2, 1, true>;
-        // 0: 111 VGPRs, 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than
-        // static striding = variant 8 on config3, tools/ab_k2.py on MI355X)
-        default: return k_compare_flat<4, 1, true>;
+        // 0: 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than static striding =
+        // variant 8 on config3, tools/ab_k2.py on MI355X); next item's rows prefetched into LDS
+        default: return k_compare_flat<4, 1, true, false, true>;
     }
 }
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 14: case 15: return true;
+        case 0: case 10: case 14: case 15: return true;
         default: return false;
     }
 }
