@@ -21,6 +21,11 @@ HEADERS = ["kernels.h", "pool.h", "tokenize.h", "tokdev.h", "marshal_phases.inc"
 INCLUDES = [os.path.join(ROOT, "include", h) for h in ("gpudiff.h", "gpudiff_format.h", "gpudiff_synth.h")]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}",
           "-I" + os.path.join(ROOT, "include")]
+# kernels.hip: no wave-level atomic aggregation.  K2 takes its next item's ticket with one lane's
+# atomicAdd as an item starts and reads it only at the item's end; the optimizer's broadcast of the
+# returned value (readfirstlane + per-lane prefix) waited for the atomic's round trip right where it
+# was issued -- a full, queue-loaded HBM latency at the start of every item.
+FILE_FLAGS = {"kernels.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 
 def _newer(target, deps):
@@ -33,10 +38,10 @@ def _newer(target, deps):
 def _compile(src, verbose):
     s = os.path.join(CSRC, src)
     o = os.path.join(OUT, src + ".o")
-    deps = [s] + [os.path.join(CSRC, h) for h in HEADERS] + INCLUDES
+    deps = [s, os.path.abspath(__file__)] + [os.path.join(CSRC, h) for h in HEADERS] + INCLUDES
     if not _newer(o, deps):
         return o
-    cmd = [HIPCC] + CFLAGS + ["-c", s, "-o", o]
+    cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(src, []) + ["-c", s, "-o", o]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

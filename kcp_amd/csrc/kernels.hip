@@ -832,7 +832,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     };
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
         const bool tail = it >= n_full;
-        if constexpr (DYN) {
+        // the next main ticket: fetched while this item streams (with RPF only after this item's rows are
+        // read from LDS -- the LDS read waits on vmcnt, which would otherwise wait for the atomic's return)
+        if constexpr (DYN && !RPF) {
             if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
         }
         [[maybe_unused]] uint64_t tp_i = 0;
@@ -846,7 +848,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
         const uint32_t per = 64u >> ish;
         const uint32_t p0 = (c << 6) + (j & ((1u << ish) - 1u)) * per;
-        if (p0 >= n) continue;
+        if (p0 >= n) {
+            if constexpr (DYN && RPF) {
+                if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
+            }
+            continue;
+        }
         const uint32_t cnt = min(per, n - p0);
         const bool valid = lane < cnt;
         // ---- rows: lane k holds pair p0 + k
@@ -867,6 +874,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             v3 = rp[3];  // flags_a, flags_b, pair_id, cluster_id
         }
         pf_item = ~0u;
+        if constexpr (DYN && RPF) {
+            if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
+        }
         if constexpr (RPF) flush();  // the previous item's results
         const uint64_t off_a = ((uint64_t)v0.y << 32) | v0.x, off_b = ((uint64_t)v0.w << 32) | v0.z;
         const bool err = valid && ((v3.x | v3.y) & GPUDIFF_OBJ_DECODE_ERR) != 0u;
