@@ -365,9 +365,11 @@ int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, ui
  * keeps recording */
 int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
 /* tuning: the decision kernel's per-wave timeline, recorded by K2 tuning variant 14 (the default
- * kernel plus timestamps; GPUDIFF_OPT_K2_VARIANT_SHIFT): 8 u64 per wave (start, end of the first
- * item, items, start of the last item, end, streaming ticks, join ticks, hardware CU id; 100 MHz)
- * into device memory dev_buf of cap_waves records; dev_buf NULL stops recording */
+ * kernel plus timestamps; GPUDIFF_OPT_K2_VARIANT_SHIFT): 12 u64 per wave (start, end of the first
+ * item, items, start of the last item, end, streaming ticks, join ticks, hardware CU id, then ticks
+ * spent per item on its rows, between its rows and its first pass, after its joins, and from one
+ * item's end to the next one's start; 100 MHz) into device memory dev_buf of cap_waves records;
+ * dev_buf NULL stops recording */
 int gpudiff_k2_profile(gpudiff_ctx* ctx, uint64_t* dev_buf, uint32_t cap_waves);
 
 /* ---- write path: the request body for a dirty object ----

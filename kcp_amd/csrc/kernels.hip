@@ -491,6 +491,110 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
     return outpos;
 }
 
+// One side's 64-key window of the pipelined merge-join: lane l holds entry start + l's key and meta
+// (zeros past the region).
+struct JWin {
+    uint32_t k, m;
+};
+__device__ __forceinline__ JWin jwin_load(const RegionView& R, uint32_t start, uint32_t lane) {
+    JWin w = {0u, 0u};
+    if (start + lane < R.L) {
+        w.k = R.keys[start + lane];
+        w.m = R.metas[start + lane];
+    }
+    return w;
+}
+// the window c entries later, from the current window and the prefetched next one: lane l < 64 - c
+// takes cur[l + c], the others pre[l + c - 64] -- a source lane s offers cur[s] when s >= c and pre[s]
+// otherwise, and everything rotates left by c (one bpermute per value)
+__device__ __forceinline__ JWin jwin_shift(const JWin& cur, const JWin& pre, uint32_t c, uint32_t lane) {
+    const bool own = lane >= c;
+    const uint32_t src = (lane + c) & 63u;
+    JWin w;
+    w.k = shfl32(own ? cur.k : pre.k, src);
+    w.m = shfl32(own ? cur.m : pre.m, src);
+    return w;
+}
+
+// join_region, software-pipelined: each side keeps its current 64-entry window of keys and metas and
+// the next 64 in registers; once a window is resolved the current one moves forward by the entries
+// consumed (a register rotate) and the following 64 are loaded, so those loads fly while the next
+// window is resolved (and its tails confirmed) instead of opening every window with a dependent HBM
+// round trip.  The values (first 8 bytes) are loaded per window as it opens: they are needed only
+// after the binary searches.  Same results as join_region.
+template <bool EMIT>
+__device__ uint32_t join_region_pl(const RegionView& A, const RegionView& B, uint8_t region_bit,
+                                   uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
+                                   uint32_t lane, bool* weq_all) {
+    uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
+    bool weq = true;
+    const uint64_t lt = mask_lt(lane);
+    JWin curA = jwin_load(A, 0u, lane), curB = jwin_load(B, 0u, lane);
+    JWin preA = jwin_load(A, 64u, lane), preB = jwin_load(B, 64u, lane);
+    while (ia < A.L || ib < B.L) {
+        const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
+        const bool va = lane < na, vb = lane < nb;
+        const uint64_t xa = va ? A.vals[ia + lane] : 0ull;
+        const uint64_t xb = vb ? B.vals[ib + lane] : 0ull;
+        const uint32_t ka = curA.k, kb = curB.k, ma = curA.m, mb = curB.m;  // zeros past the regions
+        const bool endA = ia + na == A.L, endB = ib + nb == B.L;
+        const uint32_t lastA = na ? shfl32(ka, na - 1) : 0u;
+        const uint32_t lastB = nb ? shfl32(kb, nb - 1) : 0u;
+        bool inf = true;
+        uint32_t bound = 0;
+        if (!endA) { bound = lastA; inf = false; }
+        if (!endB) { bound = inf ? lastB : min(bound, lastB); inf = false; }
+        const bool inA = va && (inf || ka <= bound);
+        const bool inB = vb && (inf || kb <= bound);
+        const uint32_t asA = va ? meta_arena(ma) : 0u, asB = vb ? meta_arena(mb) : 0u;
+        const uint32_t incA = wave_incl_scan(asA), incB = wave_incl_scan(asB);
+        const uint32_t offA = arA + incA - asA, offB = arB + incB - asB;
+        const uint32_t jA = tile_lower_bound(ka, kb, nb);
+        const uint32_t kbj = shfl32(kb, min(jA, 63u));
+        const uint32_t mbj = shfl32(mb, min(jA, 63u));
+        const uint32_t obj = shfl32(offB, min(jA, 63u));
+        const uint32_t iB = tile_lower_bound(kb, ka, na);
+        const uint32_t kai = shfl32(ka, min(iB, 63u));
+        const uint64_t xbj = shfl64(xb, min(jA, 63u));
+        const bool matchA = inA && jA < nb && kbj == ka;
+        bool differ = matchA && (ma != mbj || xa != xbj);
+        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
+        const bool matchB = inB && iB < na && kai == kb;
+        const bool emitA = inA && (!matchA || differ);
+        const bool emitB = inB && !matchB;
+        const uint64_t balA = ballot(emitA), balB = ballot(emitB);
+        if (ballot((emitA && !(matchA && wire_equal_number(ma, xa, mbj, xbj))) || emitB)) weq = false;
+        if (EMIT) {
+            if (emitA) {
+                const uint32_t pos = popc64(balA & lt) + popc64(balB & mask_lt(jA));
+                out_h[out_base + outpos + pos] = ka;
+                out_k[out_base + outpos + pos] = region_bit | (matchA ? GPUDIFF_PATH_CHANGED : GPUDIFF_PATH_REMOVED);
+            }
+            if (emitB) {
+                const uint32_t pos = popc64(balB & lt) + popc64(balA & mask_lt(iB));
+                out_h[out_base + outpos + pos] = kb;
+                out_k[out_base + outpos + pos] = region_bit | GPUDIFF_PATH_ADDED;
+            }
+        }
+        outpos += popc64(balA) + popc64(balB);
+        const uint32_t ca = popc64(ballot(inA)), cb = popc64(ballot(inB));
+        arA += ca ? shfl32(incA, ca - 1) : 0u;
+        arB += cb ? shfl32(incB, cb - 1) : 0u;
+        ia += ca;
+        ib += cb;
+        if (ca) {
+            curA = jwin_shift(curA, preA, ca, lane);
+            preA = jwin_load(A, ia + 64u, lane);
+        }
+        if (cb) {
+            curB = jwin_shift(curB, preB, cb, lane);
+            preB = jwin_load(B, ib + 64u, lane);
+        }
+    }
+    *weq_all = weq;
+    return outpos;
+}
+
 __device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
     // XXH64 of the 11 path bytes 01 06 00 00 00 's' 't' 'a' 't' 'u' 's'
     // bytes: [0]=01 [1]=06 [2..4]=00 [5]='s' [6]='t' [7]='a' | [8]='t' [9]='u' [10]='s'
@@ -512,7 +616,7 @@ __device__ __forceinline__ uint32_t sentinel_noop_bits(uint32_t flags_a) {
     return (flags_a & GPUDIFF_OBJ_HAS_STATUS) ? 0u : NOOP_STATUS;
 }
 
-template <bool EMIT>
+template <bool EMIT, bool PL = true>
 __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
                               uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane, uint32_t* noop) {
     uint32_t n = 0;
@@ -520,12 +624,14 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
     if (f & F_JSPEC) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
-        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
+        n += PL ? join_region_pl<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq)
+                : join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
     }
     if (f & F_JSTAT) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
-        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
+        n += PL ? join_region_pl<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq)
+                : join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
     }
     const bool stat_ok = stat_weq && (!(f & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
     *noop = (((f & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) | (((f & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u);
@@ -736,7 +842,7 @@ __device__ uint32_t g_k2_prof_cap;
 // profiles/r03g/wave_c4.json). One 4 KiB buffer per wave suffices: an item's rows are read from it
 // before its first loads issue (their addresses depend on them), and the next prefetch into it is
 // issued only after that first pass.
-template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false>
+template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false, bool JPL = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -800,6 +906,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         }
     };
     [[maybe_unused]] uint64_t tp_start = 0, tp_first = 0, tp_last = 0, tp_stream = 0, tp_join = 0, tp_items = 0;
+    [[maybe_unused]] uint64_t tp_rows = 0, tp_pre = 0, tp_post = 0, tp_adv = 0, tp_e = 0, tp_r = 0, tp_je = 0;
     if constexpr (PROF) tp_start = wall_clock64();
     const uint32_t nch = c_end - c_begin;
     const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
@@ -840,6 +947,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         [[maybe_unused]] uint64_t tp_i = 0;
         if constexpr (PROF) {
             tp_i = wall_clock64();
+            if (tp_e) tp_adv += tp_i - tp_e;  // the previous item's end to this one's start (ticket)
             tp_last = tp_i;
             tp_items++;
         }
@@ -878,6 +986,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
         }
         if constexpr (RPF) flush();  // the previous item's results
+        if constexpr (PROF) {
+            tp_r = wall_clock64();
+            tp_rows += tp_r - tp_i;
+        }
         const uint64_t off_a = ((uint64_t)v0.y << 32) | v0.x, off_b = ((uint64_t)v0.w << 32) | v0.z;
         const bool err = valid && ((v3.x | v3.y) & GPUDIFF_OBJ_DECODE_ERR) != 0u;
         const bool ok = valid && !err;
@@ -902,7 +1014,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t adj_a = seg_a - 16u * n1, adj_b = seg_b - 16u * n1;
         uint64_t mis_s = 0, mis_t = 0;  // pairs with a differing spec / status chunk (wave-uniform)
         [[maybe_unused]] uint64_t tp_s0 = 0;
-        if constexpr (PROF) tp_s0 = wall_clock64();
+        if constexpr (PROF) {
+            tp_s0 = wall_clock64();
+            tp_pre += tp_s0 - tp_r;
+        }
         for (uint32_t base = 0; base < total; base += 64u * U) {
             u32x4 va[U], vb[U];
             uint32_t own[U];
@@ -988,7 +1103,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
                     // dead during the join
                     const gpudiff_pair_row r = rows[p0 + k];
-                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
+                    pc = join_pair<true, JPL>(r, fk, pool, mask, ah, ak, src, lane, &nb);
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
                     const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
                     nb = sentinel_noop_bits(fa);
@@ -1019,6 +1134,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             const uint64_t t = wall_clock64();
             tp_join += t - tp_s1;
             if (tp_items == 1) tp_first = t;
+            tp_je = t;  // the item's end section starts here
         }
         const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
         const uint32_t ns = popc64(ballot(myflag & F_SPEC));
@@ -1041,6 +1157,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             q_nd = nd;
             q_cs = cs;
             q_pending = true;
+            if constexpr (PROF) {
+                tp_e = wall_clock64();
+                tp_post += tp_e - tp_je;
+            }
             continue;
         }
         if (valid) {
@@ -1069,7 +1189,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     if constexpr (PROF) {
         const uint64_t t_end = wall_clock64();
         if (lane == 0 && g_k2_prof && wave < g_k2_prof_cap) {
-            uint64_t* r = g_k2_prof + 8ull * wave;
+            uint64_t* r = g_k2_prof + 12ull * wave;
             r[0] = tp_start;
             r[1] = tp_first;
             r[2] = tp_items;
@@ -1078,6 +1198,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             r[5] = tp_stream;
             r[6] = tp_join;
             r[7] = (uint64_t)__smid();
+            r[8] = tp_rows;
+            r[9] = tp_pre;
+            r[10] = tp_post;
+            r[11] = tp_adv;
         }
     }
 }
@@ -1206,19 +1330,20 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 9: return k_compare_flat<2, 1>;
         case 11: return k_compare_flat<2, 5>;
         case 12: return k_compare_flat<4, 5>;
-        case 13: return k_compare<true, 4, 1>;  // round 1's default (wave per pair)
+        case 13: return k_compare_flat<4, 1, true, false, true, false>;  // the default with round 2's join
         case 10: return k_compare_flat<4, 1, true>;  // round 2's default: rows loaded as each item starts
-        case 14: return k_compare_flat<4, 1, true, true, true>;  // the default + per-wave timeline (g_k2_prof)
+        case 14: return k_compare_flat<4, 4, true, true, true, true>;  // the default + per-wave timeline (g_k2_prof)
         case 15: return k_compare_flat<2, 1, true>;
         // 0: 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than static striding =
         // variant 8 on config3, tools/ab_k2.py on MI355X); next item's rows prefetched into LDS
-        default: return k_compare_flat<4, 1, true, false, true>;
+        // (MINB 4: <= 128 VGPRs, 4 waves per SIMD, with the pipelined join's window registers)
+        default: return k_compare_flat<4, 4, true, false, true, true>;
     }
 }
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 10: case 14: case 15: return true;
+        case 0: case 10: case 13: case 14: case 15: return true;
         default: return false;
     }
 }

@@ -67,12 +67,12 @@ def main():
                "compact_ms": tm.compact_ms, "format_bytes": db.stats().compare_bytes}
         if variant == 14:
             cap = 1 << 16
-            buf = torch.zeros(cap * 8, dtype=torch.int64, device=dev)
+            buf = torch.zeros(cap * 12, dtype=torch.int64, device=dev)
             eng.k2_profile(buf.data_ptr(), cap)
             eng.diff(db)
             eng.sync()
             eng.k2_profile(0, 0)
-            r = buf.view(cap, 8).cpu().numpy().astype(np.int64)
+            r = buf.view(cap, 12).cpu().numpy().astype(np.int64)
             r = r[r[:, 4] != 0]
             t0 = r[:, 0].min()
             us = lambda x: (x.astype(np.float64)) / 100.0  # 100 MHz ticks -> us
@@ -91,6 +91,11 @@ def main():
                 "stream_frac_of_busy": float(us(r[:, 5]).sum() / busy.sum()),
                 "join_frac_of_busy": float(us(r[:, 6]).sum() / busy.sum()),
                 "other_frac_of_busy": float(1 - (us(r[:, 5]).sum() + us(r[:, 6]).sum()) / busy.sum()),
+                # the "other" time, split: rows (+ result stores, ticket), rows -> first pass, after the
+                # joins (counts, stores), item end -> next item start (ticket); per item, us
+                "per_item_us": {k: float(us(r[:, c]).sum() / max(1, r[:, 2].sum()))
+                                for k, c in (("rows", 8), ("pre_stream", 9), ("post_join", 10), ("advance", 11),
+                                             ("stream", 5), ("join", 6))},
                 "idle_before_us_mean": float(start.mean()),
                 "idle_after_us_mean": float((span - end).mean()),
             })
