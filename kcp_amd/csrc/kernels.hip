@@ -76,6 +76,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// lane j's value (j wave-uniform), as a scalar
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
+    return ((uint64_t)rdl((uint32_t)(v >> 32), j) << 32) | rdl((uint32_t)v, j);
+}
 
 __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + arena; }
 __device__ __forceinline__ bool meta_long(uint32_t m) { return (m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > 8u; }
@@ -842,7 +847,13 @@ __device__ uint32_t g_k2_prof_cap;
 // profiles/r03g/wave_c4.json). One 4 KiB buffer per wave suffices: an item's rows are read from it
 // before its first loads issue (their addresses depend on them), and the next prefetch into it is
 // issued only after that first pass.
-template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false, bool JPL = false>
+// OC: a chunk's owner pair found by a wave-uniform cursor instead of a cross-lane binary search.  The
+// owners of consecutive chunks never decrease, so each 64-chunk window starts at the pair holding the
+// previous window's last chunk and walks only the pairs that begin inside the window (one for a deep
+// pair, one or two for config3's): their first chunk, sizes and offsets come by v_readlane into scalar
+// registers and each lane keeps the last one it reaches -- instead of a 6-step chain of dependent
+// ds_bpermute plus six more per 64 chunks, computed while none of the wave's loads are in flight.
+template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false, bool JPL = false, bool OC = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -1018,6 +1029,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_s0 = wall_clock64();
             tp_pre += tp_s0 - tp_r;
         }
+        uint32_t oc = 0;  // OC: the pair holding the next window's first chunk (wave-uniform)
         for (uint32_t base = 0; base < total; base += 64u * U) {
             u32x4 va[U], vb[U];
             uint32_t own[U];
@@ -1026,15 +1038,46 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             for (int u = 0; u < U; u++) {
                 const uint32_t g = base + (uint32_t)u * 64u + lane;
                 act[u] = g < total;
-                uint32_t o = 0;  // owner = number of lanes whose inclusive prefix is <= g
+                uint32_t o, k, xa, xb;
+                uint64_t oa, ob;
+                if constexpr (OC) {
+                    const uint32_t wend = base + (uint32_t)u * 64u + 64u;
+                    o = oc;
+                    uint32_t fo = rdl(first, oc), n1o = rdl(n1, oc);
+                    xa = rdl(adj_a, oc);
+                    xb = rdl(adj_b, oc);
+                    oa = rdl64(off_a, oc);
+                    ob = rdl64(off_b, oc);
+                    for (uint32_t jj = oc + 1u; jj < 64u; jj++) {
+                        const uint32_t fj = rdl(first, jj);
+                        if (fj >= wend || fj >= total) break;  // starts past this window / owns nothing
+                        const bool take = g >= fj;
+                        const uint32_t n1j = rdl(n1, jj), xaj = rdl(adj_a, jj), xbj = rdl(adj_b, jj);
+                        const uint64_t oaj = rdl64(off_a, jj), obj = rdl64(off_b, jj);
+                        o = take ? jj : o;
+                        fo = take ? fj : fo;
+                        n1o = take ? n1j : n1o;
+                        xa = take ? xaj : xa;
+                        xb = take ? xbj : xb;
+                        oa = take ? oaj : oa;
+                        ob = take ? obj : ob;
+                    }
+                    oc = rdl(o, 63u);
+                    k = g - fo;
+                    st[u] = k >= n1o;
+                } else {
+                    o = 0;  // owner = number of lanes whose inclusive prefix is <= g
 #pragma unroll
-                for (uint32_t s = 32; s >= 1; s >>= 1)
-                    if (shfl32(incl, o + s - 1u) <= g) o += s;
+                    for (uint32_t s = 32; s >= 1; s >>= 1)
+                        if (shfl32(incl, o + s - 1u) <= g) o += s;
+                    k = g - shfl32(first, o);
+                    st[u] = k >= shfl32(n1, o);
+                    xa = shfl32(adj_a, o);
+                    xb = shfl32(adj_b, o);
+                    oa = shfl64(off_a, o);
+                    ob = shfl64(off_b, o);
+                }
                 own[u] = o;
-                const uint32_t k = g - shfl32(first, o);
-                st[u] = k >= shfl32(n1, o);
-                const uint32_t xa = shfl32(adj_a, o), xb = shfl32(adj_b, o);
-                const uint64_t oa = shfl64(off_a, o), ob = shfl64(off_b, o);
                 const uint64_t rel = 16ull * k;
                 if (act[u]) {
                     va[u] = __builtin_nontemporal_load((const u32x4*)(pool + oa + rel + (st[u] ? xa : 0u)));
@@ -1329,21 +1372,21 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 8: return k_compare_flat<4, 1>;
         case 9: return k_compare_flat<2, 1>;
         case 11: return k_compare_flat<2, 5>;
-        case 12: return k_compare_flat<4, 5>;
+        case 12: return k_compare_flat<4, 4, true, false, true, true>;  // the default with binary-search owners
         case 13: return k_compare_flat<4, 1, true, false, true, false>;  // the default with round 2's join
         case 10: return k_compare_flat<4, 1, true>;  // round 2's default: rows loaded as each item starts
-        case 14: return k_compare_flat<4, 4, true, true, true, true>;  // the default + per-wave timeline (g_k2_prof)
+        case 14: return k_compare_flat<4, 4, true, true, true, true, true>;  // the default + per-wave timeline (g_k2_prof)
         case 15: return k_compare_flat<2, 1, true>;
         // 0: 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than static striding =
         // variant 8 on config3, tools/ab_k2.py on MI355X); next item's rows prefetched into LDS
         // (MINB 4: <= 128 VGPRs, 4 waves per SIMD, with the pipelined join's window registers)
-        default: return k_compare_flat<4, 4, true, false, true, true>;
+        default: return k_compare_flat<4, 4, true, false, true, true, true>;
     }
 }
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 10: case 13: case 14: case 15: return true;
+        case 0: case 10: case 12: case 13: case 14: case 15: return true;
         default: return false;
     }
 }
@@ -1368,12 +1411,13 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : (uint32_t)occ[v]);
 }
 
-// Deep pairs (>= 16 KiB of compared bytes on average: config4's 8-64 KiB objects) are split down to
-// single-pair items, >= 24 per resident wave: with 8-pair items a config4 wave had 2-5 items of
+// Deep pairs (>= 16 KiB of compared bytes on average: config4's 8-64 KiB objects) are split below
+// 8-pair items, until >= 8 items per resident wave: with 8-pair items a config4 wave had 2-5 items of
 // ~0.5 MB each and the pass ended ~0.5 ms after the median wave (tools/k2_wave_profile.py,
-// profiles/r03e/wave_c4.json: 68% of the span busy)
+// profiles/r03e/wave_c4.json: 68% of the span busy); in-process A/B on config4 (profiles/r03h,
+// r03i ab_c4.json): 1-pair items 1.56 ms, 2-pair 1.21, 4-pair 1.26-1.28 -- 8 per wave gives 2-pair
 constexpr uint64_t kK2BigPairBytes = 16384;
-constexpr uint32_t kK2ItemsPerWaveBig = 24, kK2MaxSubShiftBig = 6;
+constexpr uint32_t kK2ItemsPerWaveBig = 8, kK2MaxSubShiftBig = 6;
 
 // 64-pair chunks split into 2^k items until there are >= kK2ItemsPerWave items per resident wave
 // (config3's 156k chunks: k = 0; deep pairs: see above)

@@ -17,9 +17,9 @@ timeout -k 10 300 python bench.py --config config2 --steps 20 --cpu-seconds 2 --
 python -c "import json;d=json.load(open('$O/bench_c2.json'));print('c2', d['value'], d['ms_per_step'], d['roofline']['format']['frac'], d['kernels_ms'])"
 timeout -k 10 300 python bench.py --pairs 1250000 --clusters 12500 --steps 50 --no-cpu-baseline --sample 0 --json-in-pairs 0 > $O/bench_share.json 2> $O/bench_share.log || { tail -20 $O/bench_share.log; exit 1; }
 python -c "import json;d=json.load(open('$O/bench_share.json'));print('share', d['value'], d['ms_per_step'], d['kernels_ms'])"
-timeout -k 10 400 python tools/ab_k2.py --config config4 --pairs 100000 --clusters 1000 --rounds 4 --passes 3 --variants "def=0,v13=0xD00,v10=0xA00,it8=0x20000000,it8v13=0x20000D00" > $O/ab_c4.json 2> $O/ab_c4.log || { tail -20 $O/ab_c4.log; exit 1; }
+timeout -k 10 400 python tools/ab_k2.py --config config4 --pairs 100000 --clusters 1000 --rounds 4 --passes 3 --variants "def=0,v12=0xC00,v13=0xD00,v10=0xA00,ipw24=0x30000000" > $O/ab_c4.json 2> $O/ab_c4.log || { tail -20 $O/ab_c4.log; exit 1; }
 tail -c 1500 $O/ab_c4.json
-timeout -k 10 400 python tools/ab_k2.py --config config3 --rounds 3 --passes 3 --variants "def=0,v13=0xD00,v10=0xA00" > $O/ab_c3.json 2> $O/ab_c3.log || { tail -20 $O/ab_c3.log; exit 1; }
+timeout -k 10 400 python tools/ab_k2.py --config config3 --rounds 3 --passes 3 --variants "def=0,v12=0xC00,v13=0xD00,v10=0xA00" > $O/ab_c3.json 2> $O/ab_c3.log || { tail -20 $O/ab_c3.log; exit 1; }
 tail -c 800 $O/ab_c3.json
-timeout -k 10 400 python tools/ab_k2.py --config config3 --pairs 1250000 --clusters 12500 --rounds 4 --passes 5 --variants "def=0,v10=0xA00" > $O/ab_share.json 2> $O/ab_share.log || { tail -20 $O/ab_share.log; exit 1; }
+timeout -k 10 400 python tools/ab_k2.py --config config3 --pairs 1250000 --clusters 12500 --rounds 4 --passes 5 --variants "def=0,v12=0xC00,v10=0xA00" > $O/ab_share.json 2> $O/ab_share.log || { tail -20 $O/ab_share.log; exit 1; }
 tail -c 800 $O/ab_share.json
