@@ -76,11 +76,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-// lane j's value (j wave-uniform), as a scalar
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j); }
-__device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t j) {
-    return ((uint64_t)rdl((uint32_t)(v >> 32), j) << 32) | rdl((uint32_t)v, j);
-}
 
 __device__ __forceinline__ uint64_t seg_bytes(uint32_t l, uint32_t arena) { return (uint64_t)l * 16u + arena; }
 __device__ __forceinline__ bool meta_long(uint32_t m) { return (m & 7u) == GPUDIFF_TAG_STR && (m >> 3) > 8u; }
@@ -496,110 +491,6 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
     return outpos;
 }
 
-// One side's 64-key window of the pipelined merge-join: lane l holds entry start + l's key and meta
-// (zeros past the region).
-struct JWin {
-    uint32_t k, m;
-};
-__device__ __forceinline__ JWin jwin_load(const RegionView& R, uint32_t start, uint32_t lane) {
-    JWin w = {0u, 0u};
-    if (start + lane < R.L) {
-        w.k = R.keys[start + lane];
-        w.m = R.metas[start + lane];
-    }
-    return w;
-}
-// the window c entries later, from the current window and the prefetched next one: lane l < 64 - c
-// takes cur[l + c], the others pre[l + c - 64] -- a source lane s offers cur[s] when s >= c and pre[s]
-// otherwise, and everything rotates left by c (one bpermute per value)
-__device__ __forceinline__ JWin jwin_shift(const JWin& cur, const JWin& pre, uint32_t c, uint32_t lane) {
-    const bool own = lane >= c;
-    const uint32_t src = (lane + c) & 63u;
-    JWin w;
-    w.k = shfl32(own ? cur.k : pre.k, src);
-    w.m = shfl32(own ? cur.m : pre.m, src);
-    return w;
-}
-
-// join_region, software-pipelined: each side keeps its current 64-entry window of keys and metas and
-// the next 64 in registers; once a window is resolved the current one moves forward by the entries
-// consumed (a register rotate) and the following 64 are loaded, so those loads fly while the next
-// window is resolved (and its tails confirmed) instead of opening every window with a dependent HBM
-// round trip.  The values (first 8 bytes) are loaded per window as it opens: they are needed only
-// after the binary searches.  Same results as join_region.
-template <bool EMIT>
-__device__ uint32_t join_region_pl(const RegionView& A, const RegionView& B, uint8_t region_bit,
-                                   uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
-                                   uint32_t lane, bool* weq_all) {
-    uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
-    bool weq = true;
-    const uint64_t lt = mask_lt(lane);
-    JWin curA = jwin_load(A, 0u, lane), curB = jwin_load(B, 0u, lane);
-    JWin preA = jwin_load(A, 64u, lane), preB = jwin_load(B, 64u, lane);
-    while (ia < A.L || ib < B.L) {
-        const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
-        const bool va = lane < na, vb = lane < nb;
-        const uint64_t xa = va ? A.vals[ia + lane] : 0ull;
-        const uint64_t xb = vb ? B.vals[ib + lane] : 0ull;
-        const uint32_t ka = curA.k, kb = curB.k, ma = curA.m, mb = curB.m;  // zeros past the regions
-        const bool endA = ia + na == A.L, endB = ib + nb == B.L;
-        const uint32_t lastA = na ? shfl32(ka, na - 1) : 0u;
-        const uint32_t lastB = nb ? shfl32(kb, nb - 1) : 0u;
-        bool inf = true;
-        uint32_t bound = 0;
-        if (!endA) { bound = lastA; inf = false; }
-        if (!endB) { bound = inf ? lastB : min(bound, lastB); inf = false; }
-        const bool inA = va && (inf || ka <= bound);
-        const bool inB = vb && (inf || kb <= bound);
-        const uint32_t asA = va ? meta_arena(ma) : 0u, asB = vb ? meta_arena(mb) : 0u;
-        const uint32_t incA = wave_incl_scan(asA), incB = wave_incl_scan(asB);
-        const uint32_t offA = arA + incA - asA, offB = arB + incB - asB;
-        const uint32_t jA = tile_lower_bound(ka, kb, nb);
-        const uint32_t kbj = shfl32(kb, min(jA, 63u));
-        const uint32_t mbj = shfl32(mb, min(jA, 63u));
-        const uint32_t obj = shfl32(offB, min(jA, 63u));
-        const uint32_t iB = tile_lower_bound(kb, ka, na);
-        const uint32_t kai = shfl32(ka, min(iB, 63u));
-        const uint64_t xbj = shfl64(xb, min(jA, 63u));
-        const bool matchA = inA && jA < nb && kbj == ka;
-        bool differ = matchA && (ma != mbj || xa != xbj);
-        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
-        const bool matchB = inB && iB < na && kai == kb;
-        const bool emitA = inA && (!matchA || differ);
-        const bool emitB = inB && !matchB;
-        const uint64_t balA = ballot(emitA), balB = ballot(emitB);
-        if (ballot((emitA && !(matchA && wire_equal_number(ma, xa, mbj, xbj))) || emitB)) weq = false;
-        if (EMIT) {
-            if (emitA) {
-                const uint32_t pos = popc64(balA & lt) + popc64(balB & mask_lt(jA));
-                out_h[out_base + outpos + pos] = ka;
-                out_k[out_base + outpos + pos] = region_bit | (matchA ? GPUDIFF_PATH_CHANGED : GPUDIFF_PATH_REMOVED);
-            }
-            if (emitB) {
-                const uint32_t pos = popc64(balB & lt) + popc64(balA & mask_lt(iB));
-                out_h[out_base + outpos + pos] = kb;
-                out_k[out_base + outpos + pos] = region_bit | GPUDIFF_PATH_ADDED;
-            }
-        }
-        outpos += popc64(balA) + popc64(balB);
-        const uint32_t ca = popc64(ballot(inA)), cb = popc64(ballot(inB));
-        arA += ca ? shfl32(incA, ca - 1) : 0u;
-        arB += cb ? shfl32(incB, cb - 1) : 0u;
-        ia += ca;
-        ib += cb;
-        if (ca) {
-            curA = jwin_shift(curA, preA, ca, lane);
-            preA = jwin_load(A, ia + 64u, lane);
-        }
-        if (cb) {
-            curB = jwin_shift(curB, preB, cb, lane);
-            preB = jwin_load(B, ib + 64u, lane);
-        }
-    }
-    *weq_all = weq;
-    return outpos;
-}
-
 __device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
     // XXH64 of the 11 path bytes 01 06 00 00 00 's' 't' 'a' 't' 'u' 's'
     // bytes: [0]=01 [1]=06 [2..4]=00 [5]='s' [6]='t' [7]='a' | [8]='t' [9]='u' [10]='s'
@@ -621,7 +512,7 @@ __device__ __forceinline__ uint32_t sentinel_noop_bits(uint32_t flags_a) {
     return (flags_a & GPUDIFF_OBJ_HAS_STATUS) ? 0u : NOOP_STATUS;
 }
 
-template <bool EMIT, bool PL = true>
+template <bool EMIT>
 __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
                               uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane, uint32_t* noop) {
     uint32_t n = 0;
@@ -629,14 +520,12 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
     if (f & F_JSPEC) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
-        n += PL ? join_region_pl<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq)
-                : join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
+        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
     }
     if (f & F_JSTAT) {
         RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
         RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
-        n += PL ? join_region_pl<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq)
-                : join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
+        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
     }
     const bool stat_ok = stat_weq && (!(f & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
     *noop = (((f & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) | (((f & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u);
@@ -847,13 +736,7 @@ __device__ uint32_t g_k2_prof_cap;
 // profiles/r03g/wave_c4.json). One 4 KiB buffer per wave suffices: an item's rows are read from it
 // before its first loads issue (their addresses depend on them), and the next prefetch into it is
 // issued only after that first pass.
-// OC: a chunk's owner pair found by a wave-uniform cursor instead of a cross-lane binary search.  The
-// owners of consecutive chunks never decrease, so each 64-chunk window starts at the pair holding the
-// previous window's last chunk and walks only the pairs that begin inside the window (one for a deep
-// pair, one or two for config3's): their first chunk, sizes and offsets come by v_readlane into scalar
-// registers and each lane keeps the last one it reaches -- instead of a 6-step chain of dependent
-// ds_bpermute plus six more per 64 chunks, computed while none of the wave's loads are in flight.
-template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false, bool JPL = false, bool OC = false>
+template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -1029,7 +912,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_s0 = wall_clock64();
             tp_pre += tp_s0 - tp_r;
         }
-        uint32_t oc = 0;  // OC: the pair holding the next window's first chunk (wave-uniform)
         for (uint32_t base = 0; base < total; base += 64u * U) {
             u32x4 va[U], vb[U];
             uint32_t own[U];
@@ -1038,45 +920,14 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             for (int u = 0; u < U; u++) {
                 const uint32_t g = base + (uint32_t)u * 64u + lane;
                 act[u] = g < total;
-                uint32_t o, k, xa, xb;
-                uint64_t oa, ob;
-                if constexpr (OC) {
-                    const uint32_t wend = base + (uint32_t)u * 64u + 64u;
-                    o = oc;
-                    uint32_t fo = rdl(first, oc), n1o = rdl(n1, oc);
-                    xa = rdl(adj_a, oc);
-                    xb = rdl(adj_b, oc);
-                    oa = rdl64(off_a, oc);
-                    ob = rdl64(off_b, oc);
-                    for (uint32_t jj = oc + 1u; jj < 64u; jj++) {
-                        const uint32_t fj = rdl(first, jj);
-                        if (fj >= wend || fj >= total) break;  // starts past this window / owns nothing
-                        const bool take = g >= fj;
-                        const uint32_t n1j = rdl(n1, jj), xaj = rdl(adj_a, jj), xbj = rdl(adj_b, jj);
-                        const uint64_t oaj = rdl64(off_a, jj), obj = rdl64(off_b, jj);
-                        o = take ? jj : o;
-                        fo = take ? fj : fo;
-                        n1o = take ? n1j : n1o;
-                        xa = take ? xaj : xa;
-                        xb = take ? xbj : xb;
-                        oa = take ? oaj : oa;
-                        ob = take ? obj : ob;
-                    }
-                    oc = rdl(o, 63u);
-                    k = g - fo;
-                    st[u] = k >= n1o;
-                } else {
-                    o = 0;  // owner = number of lanes whose inclusive prefix is <= g
+                uint32_t o = 0;  // owner = number of lanes whose inclusive prefix is <= g
 #pragma unroll
-                    for (uint32_t s = 32; s >= 1; s >>= 1)
-                        if (shfl32(incl, o + s - 1u) <= g) o += s;
-                    k = g - shfl32(first, o);
-                    st[u] = k >= shfl32(n1, o);
-                    xa = shfl32(adj_a, o);
-                    xb = shfl32(adj_b, o);
-                    oa = shfl64(off_a, o);
-                    ob = shfl64(off_b, o);
-                }
+                for (uint32_t s = 32; s >= 1; s >>= 1)
+                    if (shfl32(incl, o + s - 1u) <= g) o += s;
+                const uint32_t k = g - shfl32(first, o);
+                st[u] = k >= shfl32(n1, o);
+                const uint32_t xa = shfl32(adj_a, o), xb = shfl32(adj_b, o);
+                const uint64_t oa = shfl64(off_a, o), ob = shfl64(off_b, o);
                 own[u] = o;
                 const uint64_t rel = 16ull * k;
                 if (act[u]) {
@@ -1146,7 +997,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
                     // dead during the join
                     const gpudiff_pair_row r = rows[p0 + k];
-                    pc = join_pair<true, JPL>(r, fk, pool, mask, ah, ak, src, lane, &nb);
+                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
                     const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
                     nb = sentinel_noop_bits(fa);
@@ -1225,6 +1076,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 atomicAdd(cc + 2, nd);
                 atomicAdd(cc + 3, cs);
             }
+        }
+        if constexpr (PROF) {
+            tp_e = wall_clock64();
+            tp_post += tp_e - tp_je;
         }
     }
     if constexpr (RPF) flush();  // the last item's results
@@ -1372,21 +1227,20 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 8: return k_compare_flat<4, 1>;
         case 9: return k_compare_flat<2, 1>;
         case 11: return k_compare_flat<2, 5>;
-        case 12: return k_compare_flat<4, 4, true, false, true, true>;  // the default with binary-search owners
-        case 13: return k_compare_flat<4, 1, true, false, true, false>;  // the default with round 2's join
-        case 10: return k_compare_flat<4, 1, true>;  // round 2's default: rows loaded as each item starts
-        case 14: return k_compare_flat<4, 4, true, true, true, true, true>;  // the default + per-wave timeline (g_k2_prof)
+        case 12: return k_compare_flat<4, 5>;
+        case 13: return k_compare_flat<4, 1, true, false, true>;  // + next rows prefetched into LDS (RPF)
+        case 10: return k_compare_flat<4, 4>;
+        case 14: return k_compare_flat<4, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
         case 15: return k_compare_flat<2, 1, true>;
-        // 0: 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than static striding =
-        // variant 8 on config3, tools/ab_k2.py on MI355X); next item's rows prefetched into LDS
-        // (MINB 4: <= 128 VGPRs, 4 waves per SIMD, with the pipelined join's window registers)
-        default: return k_compare_flat<4, 4, true, false, true, true, true>;
+        // 0: 105 VGPRs, 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than static
+        // striding = variant 8 on config3, tools/ab_k2.py on MI355X)
+        default: return k_compare_flat<4, 1, true>;
     }
 }
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 10: case 12: case 13: case 14: case 15: return true;
+        case 0: case 13: case 14: case 15: return true;
         default: return false;
     }
 }

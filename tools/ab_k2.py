@@ -6,12 +6,13 @@ variants must produce identical results.
 
 usage: python tools/ab_k2.py [--pairs N] [--rounds R] [--variants name=flags,...]
   flags bits: 8-11 K2 variant (wave per pair: 1 plain x4, 2 NT x8, 3 plain x8, 4 NT x2,
-              5 NT x4 <=80 VGPRs, 6 NT x2 <=64 VGPRs, 7 NT x2 <=80 VGPRs, 13 = round 1's default;
+              5 NT x4 <=80 VGPRs, 6 NT x2 <=64 VGPRs, 7 NT x2 <=80 VGPRs;
               flattened stream, static items: 8 x4, 9 x2, 10 x4 <= 128 VGPRs, 11 x2 5 waves/SIMD,
-              12 x4 5 waves/SIMD; dynamic items + 8-pair tail: 0 = 14 x4 (the default), 15 x2),
-              12-15 K2 blocks/CU (0 = the measured occupancy), 16-19 forced segments,
-              0x100000 no alternate K2 stream, 4-6 tail t (t - 1 quarters of the waves in chunks; 0 = default 2,
-              1 = no tail + late tickets), 0x80 8-pair tail items, 28-29 items per wave (0 = 6, 1: 4, 2: 8, 3: 16);
+              12 x4 5 waves/SIMD; dynamic items + tail: 0 = x4 (the default), 13 = the default with the
+              next item's rows prefetched into LDS, 15 x2), 12-15 K2 blocks/CU (0 = the measured
+              occupancy), 16-19 forced segments, 0x100000 no alternate K2 stream, 4-6 tail t (t - 1
+              quarters of the waves in chunks; 0 = default 2, 1 = no tail + late tickets), 0x80 8-pair
+              tail items, 28-29 items per wave (0 = 6 / 8 for deep pairs, 1: 4, 2: 8, 3: 16);
               variant 14 = the default kernel + per-wave timeline (tools/k2_wave_profile.py)
 """
 import argparse
