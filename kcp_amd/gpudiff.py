@@ -25,6 +25,7 @@ PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
 OPT_TIMING = 0x1
 OPT_DEVICE_ENCODE = 0x2000000
+OPT_K2_FUSE_DEEP = 0x40000000  # tuning: deep joins stay in K2 (no K4 merge-path slices)
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
 PATH_HASH_BITS = 32  # GPUDIFF_PATH_HASH_BITS: segment keys and reported path hashes

@@ -15,7 +15,7 @@ from kcp_amd import gpudiff as G
 from oracle import gpudiff_oracle as O
 from tests.golden.kat_cases import BASE, J, cases
 from tests.parity import assert_matches, oracle_batch
-from tests.workload import make_pairs
+from tests.workload import deep_pairs, make_pairs
 
 pytestmark = pytest.mark.gpu
 
@@ -303,4 +303,17 @@ def test_k2_tail_tunings_bit_exact(tail_flags):
     e = G.Engine(device=0, flags=tail_flags)
     res = e.diff_pairs(pairs)
     assert_matches(res, pairs)
+    e.close()
+
+
+@pytest.mark.parametrize("mode", ["slices", "fused", "slices_all"])
+def test_deep_joins_merge_path(mode):
+    """Joins over 2048 keys go to K4's merge-path slices (1024 merged keys each: several slices per
+    region, equal keys straddling slice boundaries, list shifts with thousands of changed paths);
+    "fused": GPUDIFF_OPT_K2_FUSE_DEEP keeps them in K2; "slices_all": a shrunken K2 arena sends every
+    dirty pair, small ones included, through the slices.  Flags, IDs and paths equal the oracle's."""
+    pairs = deep_pairs() + make_pairs(300, seed=43, mutate_frac=0.4)[0]
+    flags = {"slices": 0, "fused": G.OPT_K2_FUSE_DEEP, "slices_all": 14 << 21}[mode]
+    e = G.Engine(device=0, flags=flags)
+    assert_matches(e.diff_pairs(pairs), pairs)
     e.close()

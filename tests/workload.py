@@ -7,7 +7,7 @@ import copy
 import json
 import random
 
-from tests.golden.kat_cases import BASE
+from tests.golden.kat_cases import BASE, J
 
 SEED = 20211004
 
@@ -213,3 +213,32 @@ def make_pairs(n, seed=SEED, mix=(("cm", 0.25), ("secret", 0.25), ("deploy", 0.3
         cl.append(c)
         muts.append(m)
     return pairs, cl, muts
+
+
+def deep_pairs(seed=41, n_pairs=24, sizes=(1500, 3000, 6000)):
+    """Pairs whose joins cover thousands of keys: list inserts / deletes (every later index path
+    changes), single value changes, key renames, status list inserts and equal pairs."""
+    rnd = random.Random(seed)
+    pairs = []
+    for i in range(n_pairs):
+        n = rnd.choice(sizes)
+        a = {"apiVersion": "v1", "kind": "Deep", "metadata": {"name": "d%d" % i},
+             "spec": {"items": ["v%05d-%s" % (j, "x" * (j % 13)) for j in range(n)],
+                      "map": {"k%05d" % j: j for j in range(n // 2)}},
+             "status": {"conds": [{"type": "C%d" % j, "ok": j % 2 == 0} for j in range(n // 4)]}}
+        b = json.loads(json.dumps(a))
+        op = i % 6
+        if op == 0:
+            b["spec"]["items"].insert(rnd.randrange(n), "inserted")
+        elif op == 1:
+            del b["spec"]["items"][rnd.randrange(n)]
+        elif op == 2:
+            b["spec"]["map"]["k%05d" % rnd.randrange(n // 2)] = -1
+        elif op == 3:
+            b["spec"]["map"]["znew"] = 1
+            del b["spec"]["map"]["k00000"]
+        elif op == 4:
+            b["status"]["conds"].insert(3, {"type": "X"})
+        pairs.append((J(a), J(b)))
+    return pairs
+
