@@ -54,10 +54,18 @@ static int ensure_paths(gpudiff_dbatch* d, uint64_t arena, uint64_t scratch) {
     }
     if (!ok_s) {
         scratch = std::max<uint64_t>({scratch + scratch / 8, d->scratch_cap, 1u << 16});
+        scratch = (scratch + kJoinSliceHost - 1) / kJoinSliceHost * kJoinSliceHost;  // whole K4 slice slots
         drop(d->scratch_h);
         drop(d->scratch_k);
+        drop(d->slot_owner);
+        drop(d->slice_cnt);
+        drop(d->slice_weq);
         d->scratch_cap = 0;
-        if ((rc = dalloc(&d->scratch_h, scratch)) || (rc = dalloc(&d->scratch_k, scratch))) return rc;
+        const uint64_t slots = scratch / kJoinSliceHost;
+        if ((rc = dalloc(&d->scratch_h, scratch)) || (rc = dalloc(&d->scratch_k, scratch)) ||
+            (rc = dalloc(&d->slot_owner, slots)) || (rc = dalloc(&d->slice_cnt, slots)) ||
+            (rc = dalloc(&d->slice_weq, slots)))
+            return rc;
         d->scratch_cap = scratch;
     }
     const uint64_t out = d->arena_cap + d->scratch_cap;
@@ -95,6 +103,10 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.scratch_cap = d->scratch_cap;
     b.out_h = d->out_h;
     b.out_k = d->out_k;
+    b.slot_owner = d->slot_owner;
+    b.slice_cnt = d->slice_cnt;
+    b.slice_weq = d->slice_weq;
+    b.k2_fuse_deep = (c->flags & GPUDIFF_OPT_K2_FUSE_DEEP) ? 1u : 0u;
     b.hash_mask = c->hash_mask;
     b.k2_variant = (c->flags >> GPUDIFF_OPT_K2_VARIANT_SHIFT) & 0xFu;
     b.k2_blocks_per_cu = (c->flags >> GPUDIFF_OPT_K2_BLOCKS_SHIFT) & 0xFu;
@@ -519,6 +531,7 @@ static hipEvent_t* pass_events(gpudiff_ctx* c) {
 static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d) {
     DiffBuffers b = buffers_of(c, d);
     const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);
+    HIPCHK(launch_slot_owners(c->stream, b));
     HIPCHK(launch_join(c->stream, b, 0, nchunks, nullptr, (const uint4*)d->summary));
     HIPCHK(launch_emit(c->stream, b));
     return GPUDIFF_OK;

@@ -88,6 +88,9 @@ struct gpudiff_dbatch {
     uint64_t scratch_cap = 0;
     uint64_t* scratch_h = nullptr;
     uint8_t* scratch_k = nullptr;
+    uint32_t* slot_owner = nullptr;  // K4 slices (kernels.h DiffBuffers)
+    uint32_t* slice_cnt = nullptr;
+    uint8_t* slice_weq = nullptr;
     uint64_t* out_h = nullptr;
     uint8_t* out_k = nullptr;
     hipEvent_t done = nullptr;
@@ -164,7 +167,8 @@ inline void dfree_all(gpudiff_dbatch* d) {
     void* ps[] = {d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
                   d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
-                  d->scratch_h, d->scratch_k, d->out_h, d->out_k, d->nbits, d->noop_d};
+                  d->scratch_h, d->scratch_k, d->out_h, d->out_k, d->nbits, d->noop_d, d->slot_owner,
+                  d->slice_cnt, d->slice_weq};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);

@@ -7,6 +7,9 @@
 
 namespace gd {
 
+// K4 slices: a deferred pair's scratch is a whole number of kJoinSlice-entry slots
+constexpr uint32_t kJoinSliceHost = 1024;  // = kJoinSlice in kernels.hip
+
 // Device buffers of one diff pass.  summary[]: 0 n_spec, 1 n_status,
 // 2 n_dirty, 3 K4 scratch cap, 4 overflow, 5 n_paths, 6 any pair deferred to K4, 7 -.
 struct DiffBuffers {
@@ -36,6 +39,9 @@ struct DiffBuffers {
     uint64_t* scratch_h;    // K4 scratch for deferred pairs
     uint8_t* scratch_k;
     uint64_t scratch_cap;
+    uint32_t* slot_owner;   // per K4 slice slot of the scratch (kJoinSlice entries): its dirty pair (K3)
+    uint32_t* slice_cnt;    // per slot: paths its slice wrote (K4a)
+    uint8_t* slice_weq;     // per slot: every path a wire-equal number change (K4a)
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
@@ -45,6 +51,7 @@ struct DiffBuffers {
     uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default
     uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
     uint64_t avg_pair_bytes;    // format bytes K2 reads per pair, averaged over the batch (0: unknown)
+    uint32_t k2_fuse_deep;      // tuning: K2 joins deep pairs itself instead of deferring them to K4's slices
 };
 
 // summary[8 + seg]: K2's main item counter of segment seg; summary[8 + kK2TailCounters + seg]: its tail
@@ -72,6 +79,8 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                           uint4* after);
 // K4 over the deferred dirty pairs the segment added (before.z .. after.z)
+// K4's slot owners again (the scratch-overflow re-run of K4-K6)
+hipError_t launch_slot_owners(hipStream_t s, const DiffBuffers& b);
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after);
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);

@@ -37,6 +37,20 @@ constexpr uint32_t F_SEED = 64u;   // pair path-hash seed != 0
 constexpr uint32_t F_DEFER = 128u; // paths not produced by K2 (wave arena full): K4 joins it
 constexpr uint32_t ARENA_BIT = 0x80000000u;  // scratch_off[d]: paths live in the K2 wave arenas
 
+// K4 merge-path slices (k_join_slices below)
+constexpr uint32_t kJoinSlice = 1024;  // merged keys per slice (<= 16 windows of 64 + 64)
+constexpr uint32_t kDeepJoin = 2048;   // K2 defers a dirty pair whose join covers more keys
+
+// scratch entries of a deferred pair: each region's merged keys rounded up to whole slices, the status
+// region with one more entry for the sentinel
+__device__ __forceinline__ uint32_t defer_cap(uint32_t spec_l_a, uint32_t spec_l_b, uint32_t stat_l_a,
+                                              uint32_t stat_l_b, uint32_t f) {
+    const uint32_t Ls = (f & F_JSPEC) ? spec_l_a + spec_l_b : 0u;
+    const uint32_t Lt = (f & F_JSTAT) ? stat_l_a + stat_l_b : 0u;
+    return ((Ls + kJoinSlice - 1u) / kJoinSlice + (Lt + kJoinSlice) / kJoinSlice) * kJoinSlice;
+}
+
+
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
@@ -283,7 +297,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                                                  uint32_t c_begin, uint32_t c_end, const uint32_t* __restrict__ path_src,
                                                  const uint32_t* __restrict__ path_cnt,
                                                  uint32_t* __restrict__ path_count, const uint8_t* __restrict__ nbits,
-                                                 uint8_t* __restrict__ noop_d) {
+                                                 uint8_t* __restrict__ noop_d, uint32_t* __restrict__ slot_owner,
+                                                 uint64_t scratch_cap) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -306,7 +321,10 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
             dirty_ids[d] = id;
             dirty_idx[d] = p;
             if (f & F_DEFER) {  // K4 joins it into its scratch slot and writes the count
-                scratch_off[d] = base.w + cincl - cap;
+                const uint32_t so = base.w + cincl - cap;  // whole K4 slices (defer_cap)
+                scratch_off[d] = so;
+                if ((uint64_t)so + cap <= scratch_cap)  // else K4 reports the overflow, the host re-runs
+                    for (uint32_t q = 0; q < cap / kJoinSlice; q++) slot_owner[so / kJoinSlice + q] = d;
             } else {            // K2 already wrote its paths into a wave arena (and the no-op bits)
                 scratch_off[d] = path_src[p] | ARENA_BIT;
                 path_count[d] = path_cnt[p];
@@ -539,54 +557,226 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
     return n;
 }
 
-// One wave per 64 consecutive dirty pairs.  Pairs that need no merge-join
-// (status dirty only because the new object has no status key, and no
-// status leaves on either side: every ConfigMap/Secret update) are finished
-// lane-parallel; the others are joined one at a time by the whole wave.
-// Paths go to the pair's scratch slot (sized by K2's cap), counts to
-// path_count.  Works on the dirty pairs of one batch segment: indices
-// [before.z, after.z) of the running (n_spec, n_status, n_dirty, cap) totals.
-__global__ __launch_bounds__(256, 6) void k_join(const gpudiff_pair_row* __restrict__ rows,
-                                              const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
-                                              const uint32_t* __restrict__ dirty_idx,
-                                              const uint32_t* __restrict__ scratch_off, uint32_t* __restrict__ summary,
-                                              const uint4* __restrict__ tot_before, const uint4* __restrict__ tot_after,
-                                              uint64_t scratch_cap, uint64_t mask, uint64_t* __restrict__ sh,
-                                              uint8_t* __restrict__ sk, uint32_t* __restrict__ path_count,
-                                              uint8_t* __restrict__ noop_d) {
+// ---------------------------------------------------------------- K4: merge-path slices
+// A deferred pair's join -- one K2 could not hold in its wave arena, or one over kDeepJoin keys that
+// would keep a single K2 wave busy long after the others finish (config4's list shifts: thousands of
+// changed paths) -- is cut along its merge path: each region's two sorted key
+// lists, merged (A before B on equal keys), are split into slices of kJoinSlice merged keys, and every
+// slice is joined by its own wave, all slices of all deferred pairs spread over the whole grid.  The
+// scratch a deferred pair gets (its K2 cap, rounded by defer_cap) holds one kJoinSlice-entry slot per
+// slice, so a slice writes its paths at its slot with no coordination; K4b (k_join_gather) then packs
+// each pair's slices in order and adds the status-absent sentinel.  K3 maps every slot to its pair.
+// merge-path split of two sorted unique key lists (A before B on equal keys): the number of A keys
+// among the first dg merged keys.  64-ary search: each step the lanes probe 64 evenly spaced
+// candidates of the remaining range at once.
+__device__ uint32_t merge_split(const uint32_t* __restrict__ ka, uint32_t La, const uint32_t* __restrict__ kb,
+                                uint32_t Lb, uint32_t dg, uint32_t lane) {
+    uint32_t lo = dg > Lb ? dg - Lb : 0u, hi = min(dg, La);  // the answer is in [lo, hi]
+    while (lo < hi) {
+        // candidate ia = lo + step * (lane + 1) - 1 ... : "A[ia] belongs to the first dg" <=> A[ia] <= B[dg-ia-1]
+        const uint32_t span = hi - lo;
+        const uint32_t step = (span + 63u) / 64u;
+        const uint32_t ia = lo + lane * step;
+        bool inc = false;  // A[ia] is among the first dg merged keys
+        if (ia < hi) inc = ka[ia] <= kb[dg - ia - 1u];
+        const uint64_t b = ballot(ia < hi && !inc);
+        // the predicate is monotone (true then false): the first false lane bounds the answer
+        if (!b) {
+            const uint32_t last = min(63u, (span - 1u) / step);  // last probing lane
+            lo = lo + last * step + 1u;
+            if (step == 1u) break;
+            hi = min(hi, lo + step - 1u);
+        } else {
+            const uint32_t f = (uint32_t)__builtin_ctzll(b);
+            const uint32_t nhi = lo + f * step;            // A[nhi] is not included: answer <= nhi
+            lo = f ? lo + (f - 1u) * step + 1u : lo;       // A[lo + (f-1) step] is included
+            hi = nhi;
+        }
+    }
+    return lo;
+}
+
+// arena bytes of entries [0, n) of a region (long values' tails before entry n)
+__device__ uint32_t arena_prefix(const uint32_t* __restrict__ metas, uint32_t n, uint32_t lane) {
+    uint32_t acc = 0;
+    for (uint32_t i = 0; i < n; i += 256u) {
+        uint32_t a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t j = i + (uint32_t)u * 64u + lane;
+            a[u] = j < n ? meta_arena(metas[j]) : 0u;
+        }
+        acc += a[0] + a[1] + a[2] + a[3];
+    }
+    return wave_sum(acc);
+}
+
+// one slice [dg0, dg1) of a region's merge path, joined into out[base ...]; returns the paths written
+__device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_t dg0, uint32_t dg1,
+                               uint8_t region_bit, uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k,
+                               uint32_t base, uint32_t lane, bool* weq) {
+    uint32_t ia0 = merge_split(A.keys, A.L, B.keys, B.L, dg0, lane), ib0 = dg0 - ia0;
+    uint32_t ia1 = merge_split(A.keys, A.L, B.keys, B.L, dg1, lane), ib1 = dg1 - ia1;
+    // an equal key straddling a split (A[ia - 1] last before it, B[ib] first after it) belongs to the
+    // slice holding its A side
+    if (ia0 > 0u && ib0 < B.L && A.keys[ia0 - 1u] == B.keys[ib0]) ib0++;
+    if (ia1 > 0u && ib1 < B.L && A.keys[ia1 - 1u] == B.keys[ib1]) ib1++;
+    RegionView As = A, Bs = B;
+    As.keys += ia0;
+    As.vals += ia0;
+    As.metas += ia0;
+    As.arena += arena_prefix(A.metas, ia0, lane);
+    As.L = ia1 - ia0;
+    Bs.keys += ib0;
+    Bs.vals += ib0;
+    Bs.metas += ib0;
+    Bs.arena += arena_prefix(B.metas, ib0, lane);
+    Bs.L = ib1 > ib0 ? ib1 - ib0 : 0u;
+    return join_region<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq);
+}
+
+// K4a: wave per slice of the scratch slots [before.w, after.w) / kJoinSlice (this segment's deferred
+// pairs); writes each slice's path count and whether all its paths are wire-equal number changes
+__global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __restrict__ rows,
+                                                     const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
+                                                     const uint32_t* __restrict__ dirty_idx,
+                                                     const uint32_t* __restrict__ scratch_off,
+                                                     const uint32_t* __restrict__ slot_owner,
+                                                     uint32_t* __restrict__ summary, const uint4* __restrict__ tot_before,
+                                                     const uint4* __restrict__ tot_after, uint64_t scratch_cap,
+                                                     uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
+                                                     uint32_t* __restrict__ slice_cnt, uint8_t* __restrict__ slice_weq) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t d_begin = tot_before ? tot_before->z : 0u;
-    const uint4 after = *tot_after;
-    const uint32_t ndirty = after.z;
-    const bool fits = (uint64_t)after.w <= scratch_cap;
-    if (!fits && blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
     if (summary[6] == 0u) return;  // K2 produced every pair's paths (no F_DEFER)
+    const uint4 after = *tot_after;
+    if ((uint64_t)after.w > scratch_cap) {  // the host grows the scratch and re-runs K4-K6
+        if (blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
+        return;
+    }
+    const uint32_t s0 = (tot_before ? tot_before->w : 0u) / kJoinSlice, s1 = after.w / kJoinSlice;
+    for (uint32_t s = s0 + wave; s < s1; s += nwaves) {
+        const uint32_t d = uni(slot_owner[s]);
+        const uint32_t so = uni(scratch_off[d]);
+        const uint32_t i = s - so / kJoinSlice;  // slice of this pair
+        const uint32_t p = uni(dirty_idx[d]);
+        const uint32_t f = uni((uint32_t)flags[p]);
+        const gpudiff_pair_row r = rows[p];
+        const uint32_t Ls = (f & F_JSPEC) ? r.spec_l_a + r.spec_l_b : 0u;
+        const uint32_t Lt = (f & F_JSTAT) ? r.stat_l_a + r.stat_l_b : 0u;
+        const uint32_t nsl = (Ls + kJoinSlice - 1u) / kJoinSlice, ntl = (Lt + kJoinSlice - 1u) / kJoinSlice;
+        uint32_t cnt = 0;
+        bool weq = true;
+        if (i < nsl) {
+            const RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
+            const RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
+            const uint32_t dg0 = i * kJoinSlice;
+            cnt = join_slice(A, B, dg0, min(dg0 + kJoinSlice, Ls), 0, sh, sk, so + i * kJoinSlice, lane, &weq);
+        } else if (i - nsl < ntl) {
+            const RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
+            const RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
+            const uint32_t dg0 = (i - nsl) * kJoinSlice;
+            cnt = join_slice(A, B, dg0, min(dg0 + kJoinSlice, Lt), GPUDIFF_PATH_REGION_STATUS, sh, sk,
+                             so + i * kJoinSlice, lane, &weq);
+        }
+        if (lane == 0) {
+            slice_cnt[s] = cnt;
+            slice_weq[s] = weq ? 1u : 0u;
+        }
+    }
+}
+
+// The slot owners of every deferred pair (the overflow re-run: K3 wrote none past the old scratch)
+__global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__ flags, const uint32_t* __restrict__ caps,
+                                                     const uint32_t* __restrict__ dirty_idx,
+                                                     const uint32_t* __restrict__ scratch_off,
+                                                     const uint32_t* __restrict__ summary, uint64_t scratch_cap,
+                                                     uint32_t* __restrict__ slot_owner) {
+    const uint32_t ndirty = summary[2];
+    if (summary[6] == 0u) return;
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ndirty; d += gridDim.x * blockDim.x) {
+        const uint32_t p = dirty_idx[d];
+        if (!(flags[p] & F_DEFER)) continue;
+        const uint32_t so = scratch_off[d], cap = caps[p];
+        if ((uint64_t)so + cap <= scratch_cap)
+            for (uint32_t q = 0; q < cap / kJoinSlice; q++) slot_owner[so / kJoinSlice + q] = d;
+    }
+}
+
+// K4b: wave per 64 dirty pairs of this segment; each deferred one's slices are packed in order at the
+// start of its scratch slot (moving left, 64 entries at a time: every entry is read before any write
+// can reach it), the sentinel appended, its path count and no-op bits written
+__global__ __launch_bounds__(256) void k_join_gather(const gpudiff_pair_row* __restrict__ rows,
+                                                     const uint8_t* __restrict__ flags,
+                                                     const uint32_t* __restrict__ dirty_idx,
+                                                     const uint32_t* __restrict__ scratch_off,
+                                                     const uint32_t* __restrict__ summary,
+                                                     const uint4* __restrict__ tot_before,
+                                                     const uint4* __restrict__ tot_after, uint64_t mask,
+                                                     uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
+                                                     const uint32_t* __restrict__ slice_cnt,
+                                                     const uint8_t* __restrict__ slice_weq,
+                                                     uint32_t* __restrict__ path_count, uint8_t* __restrict__ noop_d) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    if (summary[6] == 0u || summary[4] != 0u) return;
+    const uint32_t d_begin = tot_before ? tot_before->z : 0u;
+    const uint32_t ndirty = tot_after->z;
     const uint32_t nchunks = (ndirty - d_begin + 63u) >> 6;
     for (uint32_t c = wave; c < nchunks; c += nwaves) {
         const uint32_t d = d_begin + (c << 6) + lane;
         const bool valid = d < ndirty;
         const uint32_t p = valid ? dirty_idx[d] : 0u;
         const uint32_t f = valid ? flags[p] : 0u;
-        const uint32_t so = valid ? scratch_off[d] : 0u;
-        const bool needj = (f & F_DEFER) != 0u;
-        uint64_t m = ballot(valid && needj);
-        gpudiff_pair_row rnext;
-        if (m) rnext = rows[uni(shfl32(p, (uint32_t)__builtin_ctzll(m)))];
-        while (m) {
+        for (uint64_t m = ballot(valid && (f & F_DEFER)); m; m &= m - 1) {
             const uint32_t k = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            const uint32_t pk = uni(shfl32(p, k)), fk = uni(shfl32(f, k)), sok = uni(shfl32(so, k));
-            (void)pk;
-            const gpudiff_pair_row r = rnext;
-            if (m) rnext = rows[uni(shfl32(p, (uint32_t)__builtin_ctzll(m)))];  // prefetch the next join's row
-            uint32_t n, nb = 0;
-            if (fits) n = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
-            else n = join_pair<false>(r, fk, pool, mask, sh, sk, 0, lane, &nb);
+            const uint32_t dk = d_begin + (c << 6) + k;
+            const uint32_t fk = uni(shfl32(f, k)), pk = uni(shfl32(p, k));
+            const uint32_t so = uni(scratch_off[dk]);
+            const gpudiff_pair_row r = rows[pk];
+            const uint32_t Ls = (fk & F_JSPEC) ? r.spec_l_a + r.spec_l_b : 0u;
+            const uint32_t Lt = (fk & F_JSTAT) ? r.stat_l_a + r.stat_l_b : 0u;
+            const uint32_t nsl = (Ls + kJoinSlice - 1u) / kJoinSlice, ntl = (Lt + kJoinSlice - 1u) / kJoinSlice;
+            const uint32_t s_first = so / kJoinSlice;
+            uint32_t n = 0;
+            bool spec_weq = true, stat_weq = true;
+            for (uint32_t i = 0; i < nsl + ntl; i++) {
+                const uint32_t cnt = uni(slice_cnt[s_first + i]);
+                const bool w = uni((uint32_t)slice_weq[s_first + i]) != 0u;
+                if (i < nsl) spec_weq &= w;
+                else stat_weq &= w;
+                const uint32_t src = so + i * kJoinSlice, dst = so + n;
+                if (src != dst)
+                    for (uint32_t q = 0; q < cnt; q += 64u) {
+                        const bool act = q + lane < cnt;
+                        uint64_t h = 0;
+                        uint8_t kk = 0;
+                        if (act) {
+                            h = sh[src + q + lane];
+                            kk = sk[src + q + lane];
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        if (act) {
+                            sh[dst + q + lane] = h;
+                            sk[dst + q + lane] = kk;
+                        }
+                    }
+                n += cnt;
+            }
+            if (fk & F_SENT) {
+                if (lane == 0) {
+                    sh[so + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
+                    sk[so + n] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                }
+                n += 1;
+            }
+            const bool stat_ok = stat_weq && (!(fk & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
             if (lane == 0) {
-                path_count[d_begin + (c << 6) + k] = n;
-                noop_d[d_begin + (c << 6) + k] = (uint8_t)nb;
+                path_count[dk] = n;
+                noop_d[dk] = (uint8_t)((((fk & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) |
+                                       (((fk & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u));
             }
         }
     }
@@ -609,10 +799,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                                                  uint32_t arena_off, uint32_t arena_per_wave, uint32_t arena_stride,
                                                  uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
                                                  uint8_t* __restrict__ nbits, uint64_t mask,
-                                                 uint32_t* __restrict__ summary, uint32_t sub_shift) {
+                                                 uint32_t* __restrict__ summary, uint32_t sub_arg) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t sub_shift = sub_arg & 0xFFu;
+    const bool fuse_deep = (sub_arg >> 18) & 1u;  // GPUDIFF_OPT_K2_FUSE_DEEP: deep joins stay in K2
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
@@ -632,7 +824,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
             PairDecision d = compare_pair<NT, U>(r, pool, lane);
             uint32_t src = 0, pc = 0, nb = 0;
             if (d.flag & (F_SPEC | F_STATUS)) {
-                if (used + d.cap <= arena_per_wave) {
+                if (used + d.cap <= arena_per_wave && (d.cap <= kDeepJoin || fuse_deep)) {
                     src = wbase + used;
                     if (d.flag & (F_JSPEC | F_JSTAT)) {
                         pc = join_pair<true>(r, d.flag, pool, mask, ah, ak, src, lane, &nb);
@@ -650,6 +842,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                     d.cap = 0;  // no K4 scratch slot needed
                 } else {
                     d.flag |= F_DEFER;
+                    d.cap = defer_cap(r.spec_l_a, r.spec_l_b, r.stat_l_a, r.stat_l_b, d.flag);
                     deferred = true;
                 }
             }
@@ -753,6 +946,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     // (launch_compare packs: sub_shift | tail quarters << 8 | late fetch << 16)
     const uint32_t sub_shift = sub_arg & 0xFFu, tail_q = (sub_arg >> 8) & 0xFFu;
     const bool late = (sub_arg >> 16) & 1u;
+    const bool fuse_deep = (sub_arg >> 18) & 1u;  // GPUDIFF_OPT_K2_FUSE_DEEP: deep joins stay in K2
     const uint32_t tail_ish = ((sub_arg >> 17) & 1u) ? 3u : min(sub_shift + 1u, 3u);  // tail items: half or 8 pairs
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
@@ -991,7 +1185,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
             uint32_t src = 0, pc = 0, nb = 0;
             bool defer = false;
-            if (used + ck <= arena_per_wave) {
+            if (used + ck <= arena_per_wave && (ck <= kDeepJoin || fuse_deep)) {
                 src = wbase + used;
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
@@ -1016,6 +1210,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             if (lane == k) {
                 if (defer) {
                     myflag |= F_DEFER;
+                    mycap = defer_cap(v1.x, v1.y, v2.x, v2.y, myflag);  // whole K4 slices
                 } else {
                     mycap = 0;  // no K4 scratch slot needed
                     mysrc = src;
@@ -1311,7 +1506,8 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
-               sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u)
+               sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
+                   (b.k2_fuse_deep ? 1u << 18 : 0u)
     k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
@@ -1330,15 +1526,30 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     k_compact<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
                                                            (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
                                                            b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1,
-                                                           b.path_src, b.path_cnt, b.path_count, b.nbits, b.noop_d);
+                                                           b.path_src, b.path_cnt, b.path_count, b.nbits, b.noop_d,
+                                                           b.slot_owner, b.scratch_cap);
     return hipGetLastError();
 }
 
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after) {
-    k_join<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off,
-                                                              b.summary, before, after, b.scratch_cap, b.hash_mask,
-                                                              b.scratch_h, b.scratch_k, b.path_count, b.noop_d);
+    // K4a: a resident grid walks the segment's slices (their number is on the device); exits at once
+    // when K2 deferred nothing
+    (void)c0;
+    (void)c1;
+    k_join_slices<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
+                                                 b.summary, before, after, b.scratch_cap, b.scratch_h, b.scratch_k,
+                                                 b.slice_cnt, b.slice_weq);
+    k_join_gather<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off,
+                                                                     b.summary, before, after, b.hash_mask,
+                                                                     b.scratch_h, b.scratch_k, b.slice_cnt,
+                                                                     b.slice_weq, b.path_count, b.noop_d);
+    return hipGetLastError();
+}
+
+hipError_t launch_slot_owners(hipStream_t s, const DiffBuffers& b) {
+    k_slot_owners<<<kPersistBlocks, 256, 0, s>>>(b.flags, b.caps, b.dirty_idx, b.scratch_off, b.summary, b.scratch_cap,
+                                                 b.slot_owner);
     return hipGetLastError();
 }
 
