@@ -96,7 +96,7 @@ enum {
 
 /* context option flags */
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
-/* bits 0x2, 0x4, 0x8 and 31 are reserved: until ABI 3 they (and bit 30) chose where long-value digests were
+/* bits 0x2, 0x4 and 0x8 are reserved: until ABI 3 they (and bits 30-31) chose where long-value digests were
    computed (host encoder or kernel K1); since ABI 4 the format has no digests (include/gpudiff_format.h:
    a long string's first 8 bytes sit in its leaf record, the rest in the arena) and they are ignored */
 /* tuning knobs (A/B measurements; 0 = defaults) */
@@ -114,9 +114,10 @@ enum {
                                            in 64-pair chunks (0: the default, 2 quarters; t = 1: no tail,
                                            the last two rounds of tickets fetched late) */
 #define GPUDIFF_OPT_K2_TAIL8 0x80u      /* tuning: tail items of 8 pairs instead of half a main item */
-#define GPUDIFF_OPT_K2_FUSE_DEEP 0x40000000u /* tuning: K2 joins every dirty pair its wave arena holds, deep ones
-                                               included, instead of deferring joins over 2048 keys to K4's
-                                               merge-path slices */
+#define GPUDIFF_OPT_K2_DEEP_SHIFT 30u     /* 2 bits, tuning: 0 = K2 defers joins over 2048 keys to K4's merge-path
+                                            slices (the default), 1 = K2 joins every dirty pair its wave arena
+                                            holds, 2 / 3 = defer joins over 4096 / 8192 keys */
+#define GPUDIFF_OPT_K2_FUSE_DEEP (1u << GPUDIFF_OPT_K2_DEEP_SHIFT)
 #define GPUDIFF_OPT_K2_ITEMS_SHIFT 28u   /* 2 bits: decision-kernel items per resident wave before 64-pair
                                             chunks are split (0: default 8, 1: 4, 2: 8, 3: 16) */
 

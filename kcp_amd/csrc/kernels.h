@@ -51,7 +51,8 @@ struct DiffBuffers {
     uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default
     uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
     uint64_t avg_pair_bytes;    // format bytes K2 reads per pair, averaged over the batch (0: unknown)
-    uint32_t k2_fuse_deep;      // tuning: K2 joins deep pairs itself instead of deferring them to K4's slices
+    uint32_t k2_deep_mode;      // tuning (GPUDIFF_OPT_K2_DEEP_SHIFT): 0 defer joins over 2048 keys to K4's
+                                // slices, 1 keep every join in K2, 2 / 3 defer over 4096 / 8192
 };
 
 // summary[8 + seg]: K2's main item counter of segment seg; summary[8 + kK2TailCounters + seg]: its tail

@@ -40,6 +40,12 @@ constexpr uint32_t ARENA_BIT = 0x80000000u;  // scratch_off[d]: paths live in th
 // K4 merge-path slices (k_join_slices below)
 constexpr uint32_t kJoinSlice = 1024;  // merged keys per slice (<= 16 windows of 64 + 64)
 constexpr uint32_t kDeepJoin = 2048;   // K2 defers a dirty pair whose join covers more keys
+// the deep-join bound of a K2 launch (sub_arg bits 18-19 = GPUDIFF_OPT_K2_DEEP_SHIFT's field: 0 the
+// default, 1 none -- every join the wave arena holds stays in K2 --, 2 and 3: 2x and 4x the default)
+__device__ __forceinline__ uint32_t deep_join_max(uint32_t sub_arg) {
+    const uint32_t m = (sub_arg >> 18) & 3u;
+    return m == 1u ? ~0u : kDeepJoin << (m ? m - 1u : 0u);
+}
 
 // scratch entries of a deferred pair: each region's merged keys rounded up to whole slices, the status
 // region with one more entry for the sentinel
@@ -804,7 +810,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t sub_shift = sub_arg & 0xFFu;
-    const bool fuse_deep = (sub_arg >> 18) & 1u;  // GPUDIFF_OPT_K2_FUSE_DEEP: deep joins stay in K2
+    const uint32_t deep_max = deep_join_max(sub_arg);  // joins over this many keys go to K4's slices
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
@@ -824,7 +830,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
             PairDecision d = compare_pair<NT, U>(r, pool, lane);
             uint32_t src = 0, pc = 0, nb = 0;
             if (d.flag & (F_SPEC | F_STATUS)) {
-                if (used + d.cap <= arena_per_wave && (d.cap <= kDeepJoin || fuse_deep)) {
+                if (used + d.cap <= arena_per_wave && d.cap <= deep_max) {
                     src = wbase + used;
                     if (d.flag & (F_JSPEC | F_JSTAT)) {
                         pc = join_pair<true>(r, d.flag, pool, mask, ah, ak, src, lane, &nb);
@@ -946,7 +952,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     // (launch_compare packs: sub_shift | tail quarters << 8 | late fetch << 16)
     const uint32_t sub_shift = sub_arg & 0xFFu, tail_q = (sub_arg >> 8) & 0xFFu;
     const bool late = (sub_arg >> 16) & 1u;
-    const bool fuse_deep = (sub_arg >> 18) & 1u;  // GPUDIFF_OPT_K2_FUSE_DEEP: deep joins stay in K2
+    const uint32_t deep_max = deep_join_max(sub_arg);  // joins over this many keys go to K4's slices
     const uint32_t tail_ish = ((sub_arg >> 17) & 1u) ? 3u : min(sub_shift + 1u, 3u);  // tail items: half or 8 pairs
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
@@ -1185,7 +1191,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
             uint32_t src = 0, pc = 0, nb = 0;
             bool defer = false;
-            if (used + ck <= arena_per_wave && (ck <= kDeepJoin || fuse_deep)) {
+            if (used + ck <= arena_per_wave && ck <= deep_max) {
                 src = wbase + used;
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
@@ -1507,7 +1513,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
-                   (b.k2_fuse_deep ? 1u << 18 : 0u)
+                   ((b.k2_deep_mode & 3u) << 18)
     k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
