@@ -515,6 +515,113 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
     return outpos;
 }
 
+// One side's 64-key window of the pipelined merge-join: lane l holds entry start + l's key and meta
+// (zeros past the region).
+struct JWin {
+    uint32_t k, m;
+};
+__device__ __forceinline__ JWin jwin_load(const RegionView& R, uint32_t start, uint32_t lane) {
+    JWin w = {0u, 0u};
+    if (start + lane < R.L) {
+        w.k = R.keys[start + lane];
+        w.m = R.metas[start + lane];
+    }
+    return w;
+}
+// the window c entries later, from the current window and the prefetched next one: lane l < 64 - c
+// takes cur[l + c], the others pre[l + c - 64] -- a source lane s offers cur[s] when s >= c and pre[s]
+// otherwise, and everything rotates left by c (one bpermute per value)
+__device__ __forceinline__ JWin jwin_shift(const JWin& cur, const JWin& pre, uint32_t c, uint32_t lane) {
+    const bool own = lane >= c;
+    const uint32_t src = (lane + c) & 63u;
+    JWin w;
+    w.k = shfl32(own ? cur.k : pre.k, src);
+    w.m = shfl32(own ? cur.m : pre.m, src);
+    return w;
+}
+
+// join_region, software-pipelined: each side keeps its current 64-entry window of keys and metas and
+// the next 64 in registers; once a window is resolved the current one moves forward by the entries
+// consumed (a register rotate) and the following 64 are loaded, so those loads fly while the next
+// window is resolved (and its tails confirmed) instead of opening every window with a dependent HBM
+// round trip.  The values (first 8 bytes) are loaded per window as it opens: they are needed only
+// after the binary searches.  Same results as join_region.  Used by K4's slices, which run on an
+// otherwise idle memory system where a window's round trips are the whole cost; inside K2 (a
+// saturated memory pipeline, other waves streaming) it measured no faster than join_region
+// (profiles/r03j) and cost VGPRs the streaming loop needs.
+template <bool EMIT>
+__device__ uint32_t join_region_pl(const RegionView& A, const RegionView& B, uint8_t region_bit,
+                                   uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
+                                   uint32_t lane, bool* weq_all) {
+    uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
+    bool weq = true;
+    const uint64_t lt = mask_lt(lane);
+    JWin curA = jwin_load(A, 0u, lane), curB = jwin_load(B, 0u, lane);
+    JWin preA = jwin_load(A, 64u, lane), preB = jwin_load(B, 64u, lane);
+    while (ia < A.L || ib < B.L) {
+        const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
+        const bool va = lane < na, vb = lane < nb;
+        const uint64_t xa = va ? A.vals[ia + lane] : 0ull;
+        const uint64_t xb = vb ? B.vals[ib + lane] : 0ull;
+        const uint32_t ka = curA.k, kb = curB.k, ma = curA.m, mb = curB.m;  // zeros past the regions
+        const bool endA = ia + na == A.L, endB = ib + nb == B.L;
+        const uint32_t lastA = na ? shfl32(ka, na - 1) : 0u;
+        const uint32_t lastB = nb ? shfl32(kb, nb - 1) : 0u;
+        bool inf = true;
+        uint32_t bound = 0;
+        if (!endA) { bound = lastA; inf = false; }
+        if (!endB) { bound = inf ? lastB : min(bound, lastB); inf = false; }
+        const bool inA = va && (inf || ka <= bound);
+        const bool inB = vb && (inf || kb <= bound);
+        const uint32_t asA = va ? meta_arena(ma) : 0u, asB = vb ? meta_arena(mb) : 0u;
+        const uint32_t incA = wave_incl_scan(asA), incB = wave_incl_scan(asB);
+        const uint32_t offA = arA + incA - asA, offB = arB + incB - asB;
+        const uint32_t jA = tile_lower_bound(ka, kb, nb);
+        const uint32_t kbj = shfl32(kb, min(jA, 63u));
+        const uint32_t mbj = shfl32(mb, min(jA, 63u));
+        const uint32_t obj = shfl32(offB, min(jA, 63u));
+        const uint32_t iB = tile_lower_bound(kb, ka, na);
+        const uint32_t kai = shfl32(ka, min(iB, 63u));
+        const uint64_t xbj = shfl64(xb, min(jA, 63u));
+        const bool matchA = inA && jA < nb && kbj == ka;
+        bool differ = matchA && (ma != mbj || xa != xbj);
+        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
+        const bool matchB = inB && iB < na && kai == kb;
+        const bool emitA = inA && (!matchA || differ);
+        const bool emitB = inB && !matchB;
+        const uint64_t balA = ballot(emitA), balB = ballot(emitB);
+        if (ballot((emitA && !(matchA && wire_equal_number(ma, xa, mbj, xbj))) || emitB)) weq = false;
+        if (EMIT) {
+            if (emitA) {
+                const uint32_t pos = popc64(balA & lt) + popc64(balB & mask_lt(jA));
+                out_h[out_base + outpos + pos] = ka;
+                out_k[out_base + outpos + pos] = region_bit | (matchA ? GPUDIFF_PATH_CHANGED : GPUDIFF_PATH_REMOVED);
+            }
+            if (emitB) {
+                const uint32_t pos = popc64(balB & lt) + popc64(balA & mask_lt(iB));
+                out_h[out_base + outpos + pos] = kb;
+                out_k[out_base + outpos + pos] = region_bit | GPUDIFF_PATH_ADDED;
+            }
+        }
+        outpos += popc64(balA) + popc64(balB);
+        const uint32_t ca = popc64(ballot(inA)), cb = popc64(ballot(inB));
+        arA += ca ? shfl32(incA, ca - 1) : 0u;
+        arB += cb ? shfl32(incB, cb - 1) : 0u;
+        ia += ca;
+        ib += cb;
+        if (ca) {
+            curA = jwin_shift(curA, preA, ca, lane);
+            preA = jwin_load(A, ia + 64u, lane);
+        }
+        if (cb) {
+            curB = jwin_shift(curB, preB, cb, lane);
+            preB = jwin_load(B, ib + 64u, lane);
+        }
+    }
+    *weq_all = weq;
+    return outpos;
+}
+
 __device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
     // XXH64 of the 11 path bytes 01 06 00 00 00 's' 't' 'a' 't' 'u' 's'
     // bytes: [0]=01 [1]=06 [2..4]=00 [5]='s' [6]='t' [7]='a' | [8]='t' [9]='u' [10]='s'
@@ -618,6 +725,7 @@ __device__ uint32_t arena_prefix(const uint32_t* __restrict__ metas, uint32_t n,
 }
 
 // one slice [dg0, dg1) of a region's merge path, joined into out[base ...]; returns the paths written
+template <bool PL>
 __device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_t dg0, uint32_t dg1,
                                uint8_t region_bit, uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k,
                                uint32_t base, uint32_t lane, bool* weq) {
@@ -638,11 +746,14 @@ __device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_
     Bs.metas += ib0;
     Bs.arena += arena_prefix(B.metas, ib0, lane);
     Bs.L = ib1 > ib0 ? ib1 - ib0 : 0u;
-    return join_region<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq);
+    return PL ? join_region_pl<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq)
+              : join_region<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq);
 }
 
-// K4a: wave per slice of the scratch slots [before.w, after.w) / kJoinSlice (this segment's deferred
+// K4a (PL: the software-pipelined join_region_pl, the default; GPUDIFF_OPT_K4_PLAIN_JOIN: join_region)
+// wave per slice of the scratch slots [before.w, after.w) / kJoinSlice (this segment's deferred
 // pairs); writes each slice's path count and whether all its paths are wire-equal number changes
+template <bool PL>
 __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __restrict__ rows,
                                                      const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
                                                      const uint32_t* __restrict__ dirty_idx,
@@ -678,12 +789,12 @@ __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __r
             const RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
             const RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
             const uint32_t dg0 = i * kJoinSlice;
-            cnt = join_slice(A, B, dg0, min(dg0 + kJoinSlice, Ls), 0, sh, sk, so + i * kJoinSlice, lane, &weq);
+            cnt = join_slice<PL>(A, B, dg0, min(dg0 + kJoinSlice, Ls), 0, sh, sk, so + i * kJoinSlice, lane, &weq);
         } else if (i - nsl < ntl) {
             const RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
             const RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
             const uint32_t dg0 = (i - nsl) * kJoinSlice;
-            cnt = join_slice(A, B, dg0, min(dg0 + kJoinSlice, Lt), GPUDIFF_PATH_REGION_STATUS, sh, sk,
+            cnt = join_slice<PL>(A, B, dg0, min(dg0 + kJoinSlice, Lt), GPUDIFF_PATH_REGION_STATUS, sh, sk,
                              so + i * kJoinSlice, lane, &weq);
         }
         if (lane == 0) {
@@ -1543,7 +1654,7 @@ hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_
     // when K2 deferred nothing
     (void)c0;
     (void)c1;
-    k_join_slices<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
+    (b.k4_plain ? k_join_slices<false> : k_join_slices<true>)<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                  b.summary, before, after, b.scratch_cap, b.scratch_h, b.scratch_k,
                                                  b.slice_cnt, b.slice_weq);
     k_join_gather<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off,

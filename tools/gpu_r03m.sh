@@ -2,9 +2,9 @@
 # K4 merge-path slices: deep-join threshold A/B on config4, parity subset.
 set -o pipefail
 O=${O:-gpurun_out/r03m}; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "deep or variants or tail" -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -k "deep or variants or tail or golden or collision or tail_confirmation" -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-timeout -k 10 400 python tools/ab_k2.py --config config4 --pairs 100000 --clusters 1000 --rounds 5 --passes 3 --variants "d2048=0,d4096=0x80000000,d8192=0xC0000000,fused=0x40000000" > $O/ab_c4.json 2> $O/ab_c4.log || { tail -20 $O/ab_c4.log; exit 1; }
+timeout -k 10 400 python tools/ab_k2.py --config config4 --pairs 100000 --clusters 1000 --rounds 5 --passes 3 --variants "d2048=0,plain=0x8,d4096=0x80000000,d8192=0xC0000000,fused=0x40000000" > $O/ab_c4.json 2> $O/ab_c4.log || { tail -20 $O/ab_c4.log; exit 1; }
 python -c "
 import json; d=json.load(open('$O/ab_c4.json'))
 for k,v in d['variants'].items(): print(k, round(v['pass_ms_median'],4), round(v['k2_span_ms'],4), round(v['join_exposed_ms'],4))"
