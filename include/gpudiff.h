@@ -96,8 +96,8 @@ enum {
 
 /* context option flags */
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
-#define GPUDIFF_OPT_K4_PLAIN_JOIN 0x8u   /* tuning: K4's merge-path slices join window by window without the
-                                            pipelined key/meta prefetch */
+#define GPUDIFF_OPT_K4_PIPELINED_JOIN 0x8u /* tuning: K4's merge-path slices prefetch the next window's keys and
+                                              metas (software-pipelined join) */
 /* bits 0x2 and 0x4 are reserved: until ABI 3 they (and 0x8, bits 30-31) chose where long-value digests were
    computed (host encoder or kernel K1); since ABI 4 the format has no digests (include/gpudiff_format.h:
    a long string's first 8 bytes sit in its leaf record, the rest in the arena) and they are ignored */

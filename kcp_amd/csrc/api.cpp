@@ -107,7 +107,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.slice_cnt = d->slice_cnt;
     b.slice_weq = d->slice_weq;
     b.k2_deep_mode = (c->flags >> GPUDIFF_OPT_K2_DEEP_SHIFT) & 3u;
-    b.k4_plain = (c->flags & GPUDIFF_OPT_K4_PLAIN_JOIN) ? 1u : 0u;
+    b.k4_pipelined = (c->flags & GPUDIFF_OPT_K4_PIPELINED_JOIN) ? 1u : 0u;
     b.hash_mask = c->hash_mask;
     b.k2_variant = (c->flags >> GPUDIFF_OPT_K2_VARIANT_SHIFT) & 0xFu;
     b.k2_blocks_per_cu = (c->flags >> GPUDIFF_OPT_K2_BLOCKS_SHIFT) & 0xFu;

@@ -51,7 +51,7 @@ struct DiffBuffers {
     uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default
     uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
     uint64_t avg_pair_bytes;    // format bytes K2 reads per pair, averaged over the batch (0: unknown)
-    uint32_t k4_plain;          // tuning (GPUDIFF_OPT_K4_PLAIN_JOIN): K4's slices with the unpipelined join
+    uint32_t k4_pipelined;      // tuning (GPUDIFF_OPT_K4_PIPELINED_JOIN): K4's slices with join_region_pl
     uint32_t k2_deep_mode;      // tuning (GPUDIFF_OPT_K2_DEEP_SHIFT): 0 defer joins over 2048 keys to K4's
                                 // slices, 1 keep every join in K2, 2 / 3 defer over 4096 / 8192
 };

@@ -545,10 +545,10 @@ __device__ __forceinline__ JWin jwin_shift(const JWin& cur, const JWin& pre, uin
 // consumed (a register rotate) and the following 64 are loaded, so those loads fly while the next
 // window is resolved (and its tails confirmed) instead of opening every window with a dependent HBM
 // round trip.  The values (first 8 bytes) are loaded per window as it opens: they are needed only
-// after the binary searches.  Same results as join_region.  Used by K4's slices, which run on an
-// otherwise idle memory system where a window's round trips are the whole cost; inside K2 (a
-// saturated memory pipeline, other waves streaming) it measured no faster than join_region
-// (profiles/r03j) and cost VGPRs the streaming loop needs.
+// after the binary searches.  Same results as join_region.  A tuning variant of K4's slices
+// (GPUDIFF_OPT_K4_PIPELINED_JOIN): it measured slower than join_region there (profiles/r03m) and no
+// faster inside K2 (profiles/r03j) -- a window is bound by its instructions (cross-lane searches,
+// scans, the tail confirmation), not by the key loads it would hide.
 template <bool EMIT>
 __device__ uint32_t join_region_pl(const RegionView& A, const RegionView& B, uint8_t region_bit,
                                    uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
@@ -750,7 +750,8 @@ __device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_
               : join_region<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq);
 }
 
-// K4a (PL: the software-pipelined join_region_pl, the default; GPUDIFF_OPT_K4_PLAIN_JOIN: join_region)
+// K4a (join_region by default; PL, GPUDIFF_OPT_K4_PIPELINED_JOIN: the software-pipelined join_region_pl,
+// measured 15% slower on config4's slices, profiles/r03m)
 // wave per slice of the scratch slots [before.w, after.w) / kJoinSlice (this segment's deferred
 // pairs); writes each slice's path count and whether all its paths are wire-equal number changes
 template <bool PL>
@@ -1654,7 +1655,7 @@ hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_
     // when K2 deferred nothing
     (void)c0;
     (void)c1;
-    (b.k4_plain ? k_join_slices<false> : k_join_slices<true>)<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
+    (b.k4_pipelined ? k_join_slices<true> : k_join_slices<false>)<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                  b.summary, before, after, b.scratch_cap, b.scratch_h, b.scratch_k,
                                                  b.slice_cnt, b.slice_weq);
     k_join_gather<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off,
