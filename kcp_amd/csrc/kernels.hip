@@ -822,13 +822,16 @@ __global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__
     }
 }
 
-// K4b: wave per 64 dirty pairs of this segment; each deferred one's slices are packed in order at the
+// K4b: wave per deferred pair of this segment, found as the first slot of its scratch (so the grid walks
+// only deferred pairs, in parallel: one wave per 64 dirty pairs, walking the deferred ones in turn, took
+// 53 us on config4, profiles/r03o); each deferred pair's slices are packed in order at the
 // start of its scratch slot (moving left, 64 entries at a time: every entry is read before any write
 // can reach it), the sentinel appended, its path count and no-op bits written
 __global__ __launch_bounds__(256) void k_join_gather(const gpudiff_pair_row* __restrict__ rows,
                                                      const uint8_t* __restrict__ flags,
                                                      const uint32_t* __restrict__ dirty_idx,
                                                      const uint32_t* __restrict__ scratch_off,
+                                                     const uint32_t* __restrict__ slot_owner,
                                                      const uint32_t* __restrict__ summary,
                                                      const uint4* __restrict__ tot_before,
                                                      const uint4* __restrict__ tot_after, uint64_t mask,
@@ -840,62 +843,55 @@ __global__ __launch_bounds__(256) void k_join_gather(const gpudiff_pair_row* __r
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     if (summary[6] == 0u || summary[4] != 0u) return;
-    const uint32_t d_begin = tot_before ? tot_before->z : 0u;
-    const uint32_t ndirty = tot_after->z;
-    const uint32_t nchunks = (ndirty - d_begin + 63u) >> 6;
-    for (uint32_t c = wave; c < nchunks; c += nwaves) {
-        const uint32_t d = d_begin + (c << 6) + lane;
-        const bool valid = d < ndirty;
-        const uint32_t p = valid ? dirty_idx[d] : 0u;
-        const uint32_t f = valid ? flags[p] : 0u;
-        for (uint64_t m = ballot(valid && (f & F_DEFER)); m; m &= m - 1) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(m);
-            const uint32_t dk = d_begin + (c << 6) + k;
-            const uint32_t fk = uni(shfl32(f, k)), pk = uni(shfl32(p, k));
-            const uint32_t so = uni(scratch_off[dk]);
-            const gpudiff_pair_row r = rows[pk];
-            const uint32_t Ls = (fk & F_JSPEC) ? r.spec_l_a + r.spec_l_b : 0u;
-            const uint32_t Lt = (fk & F_JSTAT) ? r.stat_l_a + r.stat_l_b : 0u;
-            const uint32_t nsl = (Ls + kJoinSlice - 1u) / kJoinSlice, ntl = (Lt + kJoinSlice - 1u) / kJoinSlice;
-            const uint32_t s_first = so / kJoinSlice;
-            uint32_t n = 0;
-            bool spec_weq = true, stat_weq = true;
-            for (uint32_t i = 0; i < nsl + ntl; i++) {
-                const uint32_t cnt = uni(slice_cnt[s_first + i]);
-                const bool w = uni((uint32_t)slice_weq[s_first + i]) != 0u;
-                if (i < nsl) spec_weq &= w;
-                else stat_weq &= w;
-                const uint32_t src = so + i * kJoinSlice, dst = so + n;
-                if (src != dst)
-                    for (uint32_t q = 0; q < cnt; q += 64u) {
-                        const bool act = q + lane < cnt;
-                        uint64_t h = 0;
-                        uint8_t kk = 0;
-                        if (act) {
-                            h = sh[src + q + lane];
-                            kk = sk[src + q + lane];
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        if (act) {
-                            sh[dst + q + lane] = h;
-                            sk[dst + q + lane] = kk;
-                        }
+    const uint32_t s0 = (tot_before ? tot_before->w : 0u) / kJoinSlice, s1 = tot_after->w / kJoinSlice;
+    for (uint32_t s = s0 + wave; s < s1; s += nwaves) {
+        const uint32_t dk = uni(slot_owner[s]);
+        const uint32_t so = uni(scratch_off[dk]);
+        if (s != so / kJoinSlice) continue;  // not its pair's first slot
+        const uint32_t pk = uni(dirty_idx[dk]);
+        const uint32_t fk = uni((uint32_t)flags[pk]);
+        const gpudiff_pair_row r = rows[pk];
+        const uint32_t Ls = (fk & F_JSPEC) ? r.spec_l_a + r.spec_l_b : 0u;
+        const uint32_t Lt = (fk & F_JSTAT) ? r.stat_l_a + r.stat_l_b : 0u;
+        const uint32_t nsl = (Ls + kJoinSlice - 1u) / kJoinSlice, ntl = (Lt + kJoinSlice - 1u) / kJoinSlice;
+        const uint32_t s_first = so / kJoinSlice;
+        uint32_t n = 0;
+        bool spec_weq = true, stat_weq = true;
+        for (uint32_t i = 0; i < nsl + ntl; i++) {
+            const uint32_t cnt = uni(slice_cnt[s_first + i]);
+            const bool w = uni((uint32_t)slice_weq[s_first + i]) != 0u;
+            if (i < nsl) spec_weq &= w;
+            else stat_weq &= w;
+            const uint32_t src = so + i * kJoinSlice, dst = so + n;
+            if (src != dst)
+                for (uint32_t q = 0; q < cnt; q += 64u) {
+                    const bool act = q + lane < cnt;
+                    uint64_t h = 0;
+                    uint8_t kk = 0;
+                    if (act) {
+                        h = sh[src + q + lane];
+                        kk = sk[src + q + lane];
                     }
-                n += cnt;
-            }
-            if (fk & F_SENT) {
-                if (lane == 0) {
-                    sh[so + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
-                    sk[so + n] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                    __builtin_amdgcn_wave_barrier();
+                    if (act) {
+                        sh[dst + q + lane] = h;
+                        sk[dst + q + lane] = kk;
+                    }
                 }
-                n += 1;
-            }
-            const bool stat_ok = stat_weq && (!(fk & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
+            n += cnt;
+        }
+        if (fk & F_SENT) {
             if (lane == 0) {
-                path_count[dk] = n;
-                noop_d[dk] = (uint8_t)((((fk & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) |
-                                       (((fk & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u));
+                sh[so + n] = status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask);
+                sk[so + n] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
             }
+            n += 1;
+        }
+        const bool stat_ok = stat_weq && (!(fk & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
+        if (lane == 0) {
+            path_count[dk] = n;
+            noop_d[dk] = (uint8_t)((((fk & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) |
+                                   (((fk & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u));
         }
     }
 }
@@ -1658,7 +1654,7 @@ hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_
     (b.k4_pipelined ? k_join_slices<true> : k_join_slices<false>)<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                  b.summary, before, after, b.scratch_cap, b.scratch_h, b.scratch_k,
                                                  b.slice_cnt, b.slice_weq);
-    k_join_gather<<<grid_for(c1 - c0, kPersistBlocks), 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off,
+    k_join_gather<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                                      b.summary, before, after, b.hash_mask,
                                                                      b.scratch_h, b.scratch_k, b.slice_cnt,
                                                                      b.slice_weq, b.path_count, b.noop_d);
