@@ -49,3 +49,18 @@ for chunks in (1, 16):
         ev1.record(s)
     torch.cuda.synchronize()
     print("H2D %d chunk(s) beside a busy stream: %.1f GB/s" % (chunks, n / (ev0.elapsed_time(ev1) * 1e-3) / 1e9))
+
+# the same bytes split over 2 / 4 copy streams at once (several SDMA engines?)
+for ns in (2, 4):
+    streams = [torch.cuda.Stream() for _ in range(ns)]
+    torch.cuda.synchronize()
+    best = 1e9
+    for _ in range(5):
+        t = time.perf_counter()
+        for k, st in enumerate(streams):
+            a, b = n * k // ns, n * (k + 1) // ns
+            with torch.cuda.stream(st):
+                dst[a:b].copy_(src[a:b], non_blocking=True)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    print("H2D over %d streams: %.1f GB/s" % (ns, n / best / 1e9))
