@@ -1648,13 +1648,17 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after) {
     // K4a: a resident grid walks the segment's slices (their number is on the device); exits at once
-    // when K2 deferred nothing
+    // when K2 deferred nothing.  The slices can never outnumber the scratch's slots (a larger need is the
+    // overflow re-run, after the scratch grew), so the grid is at most one wave per slot: an empty K4
+    // over the default 64k-entry scratch costs a 16-block launch, not 2048 blocks (~4 us each)
+    const uint32_t k4_blocks = (uint32_t)std::min<uint64_t>(kPersistBlocks,
+                                                            (b.scratch_cap / kJoinSlice + 3u) / 4u + 1u);
     (void)c0;
     (void)c1;
-    (b.k4_pipelined ? k_join_slices<true> : k_join_slices<false>)<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
+    (b.k4_pipelined ? k_join_slices<true> : k_join_slices<false>)<<<k4_blocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                  b.summary, before, after, b.scratch_cap, b.scratch_h, b.scratch_k,
                                                  b.slice_cnt, b.slice_weq);
-    k_join_gather<<<kPersistBlocks, 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
+    k_join_gather<<<k4_blocks, 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                                      b.summary, before, after, b.hash_mask,
                                                                      b.scratch_h, b.scratch_k, b.slice_cnt,
                                                                      b.slice_weq, b.path_count, b.noop_d);
