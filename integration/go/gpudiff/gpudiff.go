@@ -51,6 +51,11 @@ func Open(device int) (*Engine, error) {
 // OpenWith is Open with GPUDIFF_OPT_* flags, e.g. C.GPUDIFF_OPT_DEVICE_ENCODE to send the
 // batcher's JSON pairs to the GPU tokenizer (kernel K0) instead of the host encoder.
 func OpenWith(device int, flags uint32) (*Engine, error) {
+	// the header this package was built against must match the library loaded at run time (ABI 4: value
+	// heads in the leaf records, no value digests; the digest options are ignored)
+	if v := int(C.gpudiff_abi_version()); v != int(C.GPUDIFF_ABI_VERSION) {
+		return nil, fmt.Errorf("gpudiff: libgpudiff.so has ABI %d, this binding was built for %d", v, int(C.GPUDIFF_ABI_VERSION))
+	}
 	var opts C.gpudiff_opts
 	opts.device = C.int32_t(device)
 	opts.flags = C.uint32_t(flags)
