@@ -180,9 +180,11 @@ __device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, 
 
 // ---------------------------------------------------------------- scans
 // Reduce-then-scan over u32 or 4 x u32 elements in tiles of 4096 (256 threads
-// x 16), three launches: tile sums -> one-workgroup scan of tile sums ->
-// per-tile exclusive scan + base.  The element count comes from the host
-// (n_host) or from device memory (n_dev, e.g. the dirty count).
+// x 16), two launches: tile sums -> per-tile exclusive scan, each workgroup
+// summing the tile sums before its own tile (a few thousand at most, L2-
+// resident) instead of a third, one-workgroup launch scanning them.  The
+// element count comes from the host (n_host) or from device memory (n_dev,
+// e.g. the dirty count).
 constexpr uint32_t SCAN_TILE = 4096;
 
 struct V4 {
@@ -224,52 +226,24 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const V* __restrict__ in, co
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = vadd(vadd(red[0], red[1]), vadd(red[2], red[3]));
 }
 
-// exclusive scan of the tile sums in place, offset by *base_in (the running
-// total of earlier batch segments, nullptr = 0); *total = base + sum
-template <class V>
-__global__ __launch_bounds__(1024) void k_scan_top(V* __restrict__ tile_sums, const uint32_t* __restrict__ n_dev,
-                                                   uint32_t n_host, const V* base_in, V* total) {
-    __shared__ V part[1024];
-    const V base = base_in ? *base_in : vzero<V>();
-    const uint32_t n = scan_n(n_dev, n_host);
-    const uint32_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (ntiles + 1023u) / 1024u;
-    const uint32_t b = min(ntiles, t * per), e = min(ntiles, b + per);
-    V s = vzero<V>();
-    for (uint32_t i = b; i < e; i++) s = vadd(s, tile_sums[i]);
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        V o = t >= d ? part[t - d] : vzero<V>();
-        __syncthreads();
-        part[t] = vadd(part[t], o);
-        __syncthreads();
-    }
-    V run = vadd(base, t ? part[t - 1] : vzero<V>());
-    for (uint32_t i = b; i < e; i++) {
-        const V v = tile_sums[i];
-        tile_sums[i] = run;
-        run = vadd(run, v);
-    }
-    __syncthreads();  // every thread has read base_in before it may be overwritten (total may alias it)
-    if (t == 1023) *total = vadd(base, part[1023]);
-}
-
-// out[i] = exclusive prefix (may alias in); if out_n != nullptr, out[n] = total
+// out[i] = *base_in (nullptr = 0) + exclusive prefix of in (out may alias in).  The workgroup holding the
+// last element (workgroup 0 when n == 0) writes *total = base + sum -- total must not alias base_in -- and,
+// if write_terminal, out[n] = the same.  Launch at least (n ? (n - 1) / SCAN_TILE + 1 : 1) workgroups.
 template <class V>
 __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t* __restrict__ n_dev, uint32_t n_host,
-                                                    const V* __restrict__ tile_base, const V* __restrict__ total,
+                                                    const V* __restrict__ tile_sums, const V* base_in, V* total,
                                                     V* out, bool write_terminal) {
     __shared__ V wsum[4];
+    __shared__ V wpre[4];
     const uint32_t n = scan_n(n_dev, n_host);
+    const uint32_t last = n ? (n - 1) / SCAN_TILE : 0;
+    if (blockIdx.x > last) return;
     const uint32_t base = blockIdx.x * SCAN_TILE;
-    if (base > n) return;
-    if (base == n) {
-        if (write_terminal && threadIdx.x == 0) out[n] = *total;
-        return;
-    }
     const uint32_t t = threadIdx.x;
+    V p = vzero<V>();
+    for (uint32_t i = t; i < blockIdx.x; i += 256) p = vadd(p, tile_sums[i]);
+    p = vshfl(wave_incl_scan_v(p), 63);
+    if (lane_id() == 0) wpre[t >> 6] = p;
     V v[16];
     V s = vzero<V>();
 #pragma unroll
@@ -281,7 +255,8 @@ __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t*
     const V incl = wave_incl_scan_v(s);
     if (lane_id() == 63) wsum[t >> 6] = incl;
     __syncthreads();
-    V run = tile_base[blockIdx.x];
+    V run = vadd(vadd(wpre[0], wpre[1]), vadd(wpre[2], wpre[3]));
+    if (base_in) run = vadd(run, *base_in);
     for (uint32_t w = 0; w < (t >> 6); w++) run = vadd(run, wsum[w]);
     const V excl_thread = vshfl(incl, lane_id() ? lane_id() - 1 : 0);
     if (lane_id()) run = vadd(run, excl_thread);
@@ -291,7 +266,10 @@ __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t*
         if (i < n) out[i] = run;
         run = vadd(run, v[k]);
     }
-    if (write_terminal && base + SCAN_TILE >= n && t == 0) out[n] = *total;
+    if (blockIdx.x == last && t == 255) {  // run = base + every element of the tile (zero past n)
+        *total = run;
+        if (write_terminal) out[n] = run;
+    }
 }
 
 // One wave per chunk: ballot + prefix compaction into the ID lists.
@@ -1635,8 +1613,8 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     V4* cc = (V4*)b.chunk_counts + c0;
     V4* ts = (V4*)b.tile_sums;
     if (ntiles) k_scan_tiles<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts);
-    k_scan_top<V4><<<1, 1024, 0, s>>>(ts, nullptr, n, (const V4*)before, (V4*)after);
-    if (ntiles) k_scan_apply<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts, (const V4*)after, cc, false);
+    k_scan_apply<V4><<<std::max(ntiles, 1u), 256, 0, s>>>(cc, nullptr, n, ts, (const V4*)before, (V4*)after, cc,
+                                                          false);
     k_compact<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
                                                            (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
                                                            b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1,
@@ -1672,11 +1650,11 @@ hipError_t launch_slot_owners(hipStream_t s, const DiffBuffers& b) {
 }
 
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b) {
-    const uint32_t ntiles = b.n_pairs / SCAN_TILE + 1;  // covers base == n for the terminal offset
+    const uint32_t ntiles = b.n_pairs / SCAN_TILE + 1;  // >= (n_dirty - 1) / SCAN_TILE + 1 workgroups
     const uint32_t* nd = b.summary + 2;
     k_scan_tiles<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums);
-    k_scan_top<uint32_t><<<1, 1024, 0, s>>>(b.tile_sums, nd, 0, nullptr, b.summary + 5);
-    k_scan_apply<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums, b.summary + 5, b.path_off, true);
+    k_scan_apply<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums, nullptr, b.summary + 5,
+                                                  b.path_off, true);
     k_copy_paths<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
         b.summary, b.scratch_off, b.path_off, b.path_count, b.scratch_h, b.scratch_k, b.arena_h, b.arena_k, b.out_h,
         b.out_k);
