@@ -413,7 +413,8 @@ def main():
                     pm = json.load(fh)
             except (OSError, ValueError):
                 continue
-            if pm.get("k2_source_hash") == src_hash:
+            # the newest summary of the same K2 sources on this workload (a config4 summary may be newer)
+            if pm.get("k2_source_hash") == src_hash and pm.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
                 cand.append(f)
         tj = cand[-1] if cand else ""
     if tj and tj != "none" and os.path.exists(tj):

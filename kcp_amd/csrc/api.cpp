@@ -571,16 +571,19 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     }
     hipStream_t ms = c->stream;
     static_assert(kMaxSegments <= kK2TailCounters, "K2 item counters per segment");
-    HIPCHK(hipMemsetAsync(d->summary, 0, kSummaryWords * sizeof(uint32_t), ms));  // + K2 item counters
-    if (ev) HIPCHK(hipEventRecord(ev[0], ms));
-    DiffBuffers b = buffers_of(c, d);
     const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);
     const uint32_t S = choose_segments(d->n_pairs, c->flags);
+    // the summary (+ K2 item counters) is zeroed by the single K2 launch's reset kernel, else here: with
+    // segments, k2alt's first launch waits only for what precedes alt_start
+    const bool reset_in_k2 = d->n_pairs != 0 && S == 1;
+    if (ev) HIPCHK(hipEventRecord(ev[0], ms));
+    if (!reset_in_k2) HIPCHK(hipMemsetAsync(d->summary, 0, kSummaryWords * sizeof(uint32_t), ms));
+    DiffBuffers b = buffers_of(c, d);
     uint4* total = (uint4*)d->summary;  // summary[0..3]: n_spec, n_status, n_dirty, scratch cap
     if (d->n_pairs == 0) {
         HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), ms));
     } else if (S == 1) {
-        HIPCHK(launch_compare(ms, b, 0, nchunks, 0, 1));
+        HIPCHK(launch_compare(ms, b, 0, nchunks, 0, 1, true));
         if (ev) HIPCHK(hipEventRecord(ev[1], ms));
         HIPCHK(launch_compact(ms, b, 0, nchunks, nullptr, total));
         if (ev) HIPCHK(hipEventRecord(ev[2], ms));
@@ -603,7 +606,7 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         for (uint32_t s = 0; s <= last; s++) {
             const uint32_t c0 = s * per, c1 = std::min(nchunks, c0 + per);
             k2s = (alt && (s & 1)) ? c->k2alt : ms;
-            HIPCHK(launch_compare(k2s, b, c0, c1, s, last + 1));
+            HIPCHK(launch_compare(k2s, b, c0, c1, s, last + 1, false));
             HIPCHK(hipEventRecord(c->seg_ev[s], k2s));
             HIPCHK(hipStreamWaitEvent(c->side, c->seg_ev[s], 0));
             const uint4* before = s ? d->seg_tot + (s - 1) : nullptr;

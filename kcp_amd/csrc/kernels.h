@@ -76,7 +76,7 @@ struct BlobMove {
 hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, const BlobMove* moves, uint32_t n);
 // K2 (+ fused join) over the 64-pair chunks [c0, c1), batch segment seg of nsegs
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
-                          uint32_t nsegs);
+                          uint32_t nsegs, bool reset_summary);
 // K3 over chunks [c0, c1): running (n_spec, n_status, n_dirty, cap) totals before -> after
 hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                           uint4* after);

@@ -1581,18 +1581,28 @@ uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks) {
     return grid_for(items, k2_cap_blocks(b)) * 4u;
 }
 
+// A pass's zeroing in one launch (hipMemsetAsync is a fill kernel each): the summary words (when the pass
+// starts with this K2 launch) and the chunk counts that split chunks accumulate with atomics
+__global__ __launch_bounds__(256) void k_pass_reset(uint32_t* __restrict__ summary, uint32_t nwords,
+                                                    uint4* __restrict__ cc, uint32_t ncc) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (summary && i < nwords) summary[i] = 0u;
+    for (uint32_t j = i; j < ncc; j += gridDim.x * 256u) cc[j] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
-                          uint32_t nsegs) {
+                          uint32_t nsegs, bool reset_summary) {
     const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
     uint4* cc = (uint4*)b.chunk_counts;
     const uint32_t sub = k2_sub_shift(b, c1 - c0);
     const uint32_t v = b.k2_variant & 15u;
     const uint32_t tq = k2_tail_q(b);
     const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq) : 0u;
-    if (sub || tail) {  // split chunks accumulate their counts with atomics
+    if (sub || tail || reset_summary) {  // split chunks accumulate their counts with atomics
         const uint32_t z0 = sub ? c0 : c1 - tail;
-        hipError_t e = hipMemsetAsync(cc + z0, 0, (size_t)(c1 - z0) * sizeof(uint4), s);
-        if (e != hipSuccess) return e;
+        const uint32_t ncc = c1 - z0;
+        k_pass_reset<<<std::max(1u, std::min(1024u, (ncc + 255u) / 256u)), 256, 0, s>>>(
+            reset_summary ? b.summary : nullptr, kSummaryWords, cc + z0, ncc);
     }
     // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
     const uint32_t slice = b.arena_per_wave / nsegs;
