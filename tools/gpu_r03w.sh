@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 3 close: main's build again after the side-branch A/B -- -m gpu suite, smoke, default bench line
+set -o pipefail
+O=gpurun_out/r03w; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.log || { tail -20 $O/bench.log; exit 1; }
+python -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['traffic'], d['roofline'].get('traffic_source'), d['cpu_baseline']['value'])"
