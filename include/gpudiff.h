@@ -237,7 +237,8 @@ int gpudiff_dbatch_device_view(const gpudiff_dbatch* db, gpudiff_device_view* v)
 /* async device-to-device copy of a diffed batch's results into caller memory
  * (e.g. a tensor handed to an RCCL all-gather), ordered on the context
  * stream; copies min(count, max_elems) elements of `what` */
-#define GPUDIFF_EXPORT_COUNTS 0u      /* 8 x u32: n_spec, n_status, n_dirty, cap, overflow, n_paths, 0, 0 */
+#define GPUDIFF_EXPORT_COUNTS 0u      /* 8 x u32: n_spec, n_status, n_dirty, K4 scratch entries (saturating),
+                                         overflow, n_paths, any join deferred to K3/K4, 0 */
 #define GPUDIFF_EXPORT_SPEC_IDS 1u    /* u32 */
 #define GPUDIFF_EXPORT_STATUS_IDS 2u  /* u32 */
 #define GPUDIFF_EXPORT_DIRTY_IDS 3u   /* u32 */
@@ -248,6 +249,21 @@ int gpudiff_dbatch_export(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint32_t w
 int gpudiff_dbatch_read_pool(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint64_t off, void* dst,
                              uint64_t bytes);
 void gpudiff_dbatch_free(gpudiff_ctx* ctx, gpudiff_dbatch* db);
+
+/* ---- sharding by logical cluster ----
+ * The reference runs one syncer per logical cluster (pkg/reconciler/cluster/cluster.go:125-138), so a
+ * node shards pairs by whole cluster with no data-path exchange.  A rank's step time is its decision
+ * kernel's byte stream, so clusters are balanced by Σ B_pair, not by pair count (object sizes differ by
+ * tenant).  Host-only; no GPU needed.
+ * gpudiff_cluster_bytes adds each row's B_pair -- the bytes K2 streams for it: the 64-B row, the flag
+ * and both objects' compared 16-B chunks (gpudiff_pair_compare_bytes, gpudiff_format.h) -- into
+ * out[row.cluster_id] (out has n_clusters entries; a row with cluster_id >= n_clusters is
+ * GPUDIFF_E_INVAL).  Weights can come from the previous step's encoded rows of each cluster.
+ * gpudiff_shard_lpt: greedy LPT -- clusters by descending weight (ties: lower cluster id) each onto the
+ * least-loaded rank (ties: lower rank); owner[c] = its rank.  The heaviest rank's load is at most
+ * 4/3 of the optimum (Graham's bound) and within one cluster's weight of the mean. */
+int gpudiff_cluster_bytes(const gpudiff_pair_row* rows, size_t n, uint32_t n_clusters, uint64_t* out);
+int gpudiff_shard_lpt(const uint64_t* weights, uint32_t n_clusters, uint32_t world, int32_t* owner);
 
 /* ---- diff (the hot path) ---- */
 /* enqueue K2..K6 on the context stream; returns immediately */
@@ -454,7 +470,12 @@ typedef struct gpudiff_write_plan {
     gpudiff_bodies bodies;       /* n bodies (empty for no-op writes; status GPUDIFF_E_DECODE = undecodable) */
     void* internal;
 } gpudiff_write_plan;
-int gpudiff_write_plan_get(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_write_plan* out); /* = _ex(..., 0, ...) */
+/* gpudiff_write_plan_get = _ex(..., GPUDIFF_PLAN_INFORMER, ...).  ABI 3 rendered a spec write from the
+ * pair's FIRST document (the upstream/downstream reading); since ABI 4 the default is the informer
+ * reading (the NEW document).  Bindings must check gpudiff_abi_version() == GPUDIFF_ABI_VERSION at load
+ * (the Go binding and kcp_amd/gpudiff.py refuse a mismatched library) and pass
+ * GPUDIFF_PLAN_UPSTREAM_DOWNSTREAM to _ex for (A, B) pairs. */
+int gpudiff_write_plan_get(gpudiff_ctx* ctx, gpudiff_ticket ticket, gpudiff_write_plan* out);
 int gpudiff_write_plan_get_ex(gpudiff_ctx* ctx, gpudiff_ticket ticket, uint32_t mode, gpudiff_write_plan* out);
 void gpudiff_write_plan_release(gpudiff_ctx* ctx, gpudiff_write_plan* p);
 

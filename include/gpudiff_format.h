@@ -120,6 +120,28 @@ static inline uint64_t gpudiff_blob_body(uint32_t sl, uint32_t sar, uint32_t tl,
            ~(uint64_t)(GPUDIFF_BLOB_ALIGN - 1u);
 }
 
+/* B_pair: the bytes the decision kernel (K2) reads for one pair -- the 64-B row, the flag byte and, per
+ * object, the compared 16-B chunks: the whole body (segments + zero pad) when both regions' sizes match
+ * and B has status; the spec segment when only the spec sizes match (padded to the line too when neither
+ * side has status leaves); the status segment when only the status sizes match; nothing else (a size
+ * mismatch decides the region without reading it).  The roofline's format bytes and the shard weight. */
+static inline uint64_t gpudiff_pair_compare_bytes(const gpudiff_pair_row* r) {
+    const uint64_t al = GPUDIFF_BLOB_ALIGN - 1u;
+    uint64_t per = 0;
+    if ((r->flags_a | r->flags_b) & GPUDIFF_OBJ_DECODE_ERR) return sizeof(gpudiff_pair_row) + 1u;
+    {
+        const int spec_sz = r->spec_l_a == r->spec_l_b && r->spec_ar_a == r->spec_ar_b;
+        const int stat_sz = (r->flags_b & GPUDIFF_OBJ_HAS_STATUS) && r->stat_l_a == r->stat_l_b &&
+                            r->stat_ar_a == r->stat_ar_b;
+        const uint64_t seg_s = gpudiff_seg_bytes(r->spec_l_a, r->spec_ar_a);
+        const uint64_t seg_t = gpudiff_seg_bytes(r->stat_l_a, r->stat_ar_a);
+        if (spec_sz && stat_sz) per = (seg_s + seg_t + al) & ~al;
+        else if (spec_sz) per = (r->stat_l_a | r->stat_l_b | r->stat_ar_a | r->stat_ar_b) ? seg_s : (seg_s + al) & ~al;
+        else if (stat_sz) per = seg_t;
+    }
+    return sizeof(gpudiff_pair_row) + 1u + 2u * per;
+}
+
 static inline uint32_t gpudiff_meta(uint32_t tag, uint32_t len) { return (len << 3) | tag; }
 static inline uint32_t gpudiff_meta_tag(uint32_t m) { return m & 7u; }
 static inline uint32_t gpudiff_meta_len(uint32_t m) { return m >> 3; }

@@ -41,8 +41,19 @@ typedef struct gpudiff_synth_cfg {
 
 typedef struct gpudiff_synth gpudiff_synth;
 
-/* plans the population and the LPT shard of `rank` among `world` ranks */
+/* plans the population and the LPT shard of `rank` among `world` ranks (clusters by pair count) */
 int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudiff_synth** out);
+/* the same with the clusters LPT-packed by cluster_weight[n_clusters] (NULL = pair count), the rule of
+ * gpudiff_shard_lpt: SURVEY.md §8(e) balances ranks by Σ B_pair (gpudiff_synth_cluster_bytes) */
+int gpudiff_synth_open_ex(const gpudiff_synth_cfg* cfg, int world, int rank, const uint64_t* cluster_weight,
+                          gpudiff_synth** out);
+/* pairs per cluster (out[n_clusters]) */
+int gpudiff_synth_cluster_sizes(const gpudiff_synth_cfg* cfg, uint64_t* out);
+/* exact Σ B_pair (gpudiff_pair_compare_bytes of the encoded pair) of every cluster c with
+ * c % stride == offset into out[c] (others untouched): encodes those clusters' pairs with `threads` host
+ * threads (ranks split the work by stride = world, offset = rank, then sum the vectors) */
+int gpudiff_synth_cluster_bytes(const gpudiff_synth_cfg* cfg, uint32_t stride, uint32_t offset, uint32_t threads,
+                                uint64_t* out);
 void gpudiff_synth_close(gpudiff_synth* s);
 uint64_t gpudiff_synth_local_pairs(const gpudiff_synth* s);
 uint64_t gpudiff_synth_local_clusters(const gpudiff_synth* s);

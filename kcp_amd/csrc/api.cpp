@@ -53,7 +53,10 @@ static int ensure_paths(gpudiff_dbatch* d, uint64_t arena, uint64_t scratch) {
         d->arena_cap = arena;
     }
     if (!ok_s) {
-        scratch = std::max<uint64_t>({scratch + scratch / 8, d->scratch_cap, 1u << 16});
+        // scratch offsets share a u32 with the arena bit (scratch_off): at most 2^31 entries
+        if (scratch > kMaxScratchEntries) return GPUDIFF_E_CAPACITY;
+        scratch = std::min<uint64_t>(std::max<uint64_t>({scratch + scratch / 8, d->scratch_cap, 1u << 16}),
+                                     kMaxScratchEntries);
         scratch = (scratch + kJoinSliceHost - 1) / kJoinSliceHost * kJoinSliceHost;  // whole K4 slice slots
         drop(d->scratch_h);
         drop(d->scratch_k);
@@ -117,7 +120,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     }
     b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
     b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
-    b.avg_pair_bytes = d->n_pairs ? d->compare_bytes / d->n_pairs : 0;
+    b.avg_pair_bytes = d->n_pairs ? (d->compare_bytes ? d->compare_bytes : d->size_hint_bytes) / d->n_pairs : 0;
     return b;
 }
 
@@ -447,7 +450,7 @@ int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
     int rc = set_device(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
-    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = 0;
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->size_hint_bytes = 0;
     d->ticket = 0;
     return GPUDIFF_OK;
 }
@@ -500,6 +503,42 @@ int gpudiff_dbatch_read_pool(gpudiff_ctx* c, const gpudiff_dbatch* d, uint64_t o
     if (off > d->pool_used || bytes > d->pool_used - off) return GPUDIFF_E_INVAL;
     HIPCHK(hipStreamSynchronize(c->stream));
     if (bytes) HIPCHK(hipMemcpy(dst, d->pool + off, bytes, hipMemcpyDeviceToHost));
+    return GPUDIFF_OK;
+}
+
+// ------------------------------------------------------------------ sharding
+int gpudiff_cluster_bytes(const gpudiff_pair_row* rows, size_t n, uint32_t n_clusters, uint64_t* out) {
+    if ((n && !rows) || (n_clusters && !out)) return GPUDIFF_E_INVAL;
+    for (size_t i = 0; i < n; i++)
+        if (rows[i].cluster_id >= n_clusters) return GPUDIFF_E_INVAL;
+    for (size_t i = 0; i < n; i++) out[rows[i].cluster_id] += gpudiff_pair_compare_bytes(&rows[i]);
+    return GPUDIFF_OK;
+}
+
+int gpudiff_shard_lpt(const uint64_t* weights, uint32_t n_clusters, uint32_t world, int32_t* owner) {
+    if (world == 0 || world > 0x7FFFFFFFu || (n_clusters && (!weights || !owner))) return GPUDIFF_E_INVAL;
+    try {
+        std::vector<uint32_t> order(n_clusters);
+        for (uint32_t c = 0; c < n_clusters; c++) order[c] = c;
+        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+            return weights[x] != weights[y] ? weights[x] > weights[y] : x < y;
+        });
+        // least-loaded rank first, ties to the lower rank: a min-heap of (load, rank)
+        std::vector<std::pair<uint64_t, uint32_t>> heap;
+        heap.reserve(world);
+        for (uint32_t r = 0; r < world; r++) heap.emplace_back(0, r);
+        auto gt = [](const std::pair<uint64_t, uint32_t>& a, const std::pair<uint64_t, uint32_t>& b) { return a > b; };
+        std::make_heap(heap.begin(), heap.end(), gt);
+        for (uint32_t c : order) {
+            std::pop_heap(heap.begin(), heap.end(), gt);
+            auto& top = heap.back();
+            owner[c] = (int32_t)top.second;
+            top.first += weights[c];
+            std::push_heap(heap.begin(), heap.end(), gt);
+        }
+    } catch (const std::bad_alloc&) {
+        return GPUDIFF_E_NOMEM;
+    }
     return GPUDIFF_OK;
 }
 
@@ -814,7 +853,7 @@ int gpudiff_submit(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpu
             return rc;
         }
     }
-    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = 0;
+    d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->size_hint_bytes = 0;
     if ((rc = gpudiff_dbatch_append(c, d, hb)) || (rc = gpudiff_diff(c, d, ticket))) {
         gpudiff_hbatch_free(c, hb);
         return rc;

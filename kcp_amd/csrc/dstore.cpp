@@ -621,7 +621,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     std::vector<const uint8_t*> src;
     src.reserve(max_docs);
     uint32_t nd = 0, nh = 0;
-    uint64_t jbytes = 0, bound = 0, floor = 0;
+    uint64_t jbytes = 0, bound = 0, floor = 0, new_json_bytes = 0;
     auto add_doc = [&](const uint8_t* p, size_t len, uint32_t slot, uint32_t row, const gpudiff_event& e) {
         TokDoc& D = docs[nd];
         memset(&D, 0, sizeof(D));
@@ -671,6 +671,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
             s->seen[e.slot] = 1;
         }
         add_doc(e.new_json, e.new_len, e.slot, (uint32_t)i, e);
+        new_json_bytes += e.new_len;
     }
     jbytes += kTokSlack;
     if ((rc = grow_pinned(&R.hjson, &R.hjson_cap, jbytes))) return rc;
@@ -816,6 +817,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     d->n_pairs = n;
     d->leaves = 0;
     d->compare_bytes = d->value_bytes = 0;
+    d->size_hint_bytes = 2 * new_json_bytes;  // k2_sub_shift's size class (engine.h)
     if ((rc = gpudiff_diff(c, d, ticket))) {
         s->broken = true;
         return rc;

@@ -61,6 +61,10 @@ struct gpudiff_dbatch {
     uint64_t pool_cap = 0, pool_used = 0;
     uint64_t max_pairs = 0, n_pairs = 0;
     uint64_t leaves = 0, compare_bytes = 0, value_bytes = 0;
+    // K0-encoded batches (the device-encode store / submit): the rows are built on the device, so
+    // compare_bytes is unknown on the host; this is the batch's JSON bytes per pair side x 2 (config3
+    // objects: 0.85 compare bytes per JSON byte), the size class K2's item split goes by (k2_sub_shift)
+    uint64_t size_hint_bytes = 0;
     uint8_t* pool = nullptr;
     bool pool_borrowed = false;  // pool owned by a gpudiff_store (its current space)
     gpudiff_pair_row* rows = nullptr;
@@ -189,20 +193,6 @@ inline uint64_t blob_value_bytes(const uint8_t* blob, uint32_t spec_l, uint32_t 
     return v;
 }
 
-// bytes the decision kernel must read for this pair (DESIGN.md "Roofline"): the row, the flag, and
-// per object the compared 16-B chunks -- the same rule as k_compare_flat: with both regions compared
-// the stream covers the whole body (segments + zero pad to 128 B); with spec only, the spec segment,
-// padded too when neither side has status leaves; with status only, the status segment
-inline uint64_t pair_compare_bytes(const gpudiff_pair_row& r) {
-    uint64_t b = sizeof(gpudiff_pair_row) + 1;
-    if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) return b;
-    const bool spec_sz = r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b;
-    const bool stat_sz = (r.flags_b & GPUDIFF_OBJ_HAS_STATUS) && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b;
-    const uint64_t seg_s = gpudiff_seg_bytes(r.spec_l_a, r.spec_ar_a), seg_t = gpudiff_seg_bytes(r.stat_l_a, r.stat_ar_a);
-    const uint64_t al = GPUDIFF_BLOB_ALIGN - 1;
-    uint64_t per = 0;
-    if (spec_sz && stat_sz) per = (seg_s + seg_t + al) & ~al;
-    else if (spec_sz) per = (r.stat_l_a | r.stat_l_b | r.stat_ar_a | r.stat_ar_b) ? seg_s : (seg_s + al) & ~al;
-    else if (stat_sz) per = seg_t;
-    return b + 2 * per;
-}
+// bytes the decision kernel must read for this pair (DESIGN.md "Roofline"; the same rule as
+// k_compare_flat's streamed chunks): gpudiff_format.h gpudiff_pair_compare_bytes
+inline uint64_t pair_compare_bytes(const gpudiff_pair_row& r) { return gpudiff_pair_compare_bytes(&r); }

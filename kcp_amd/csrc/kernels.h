@@ -7,11 +7,14 @@
 
 namespace gd {
 
-// K4 slices: a deferred pair's scratch is a whole number of kJoinSlice-entry slots
+// K4 slices: a sliced deferral's scratch is a whole number of kJoinSlice-entry slots
 constexpr uint32_t kJoinSliceHost = 1024;  // = kJoinSlice in kernels.hip
+// the K4 scratch's limit: a deferred pair's offset shares a u32 with the arena bit (scratch_off); a batch
+// whose deferred joins need more (summary[3] saturates at 2^32 - 1 past u32) fails with GPUDIFF_E_CAPACITY
+constexpr uint64_t kMaxScratchEntries = 1ull << 31;
 
 // Device buffers of one diff pass.  summary[]: 0 n_spec, 1 n_status,
-// 2 n_dirty, 3 K4 scratch cap, 4 overflow, 5 n_paths, 6 any pair deferred to K4, 7 -.
+// 2 n_dirty, 3 K4 scratch entries (saturating), 4 overflow, 5 n_paths, 6 any pair deferred to K4, 7 -.
 struct DiffBuffers {
     const gpudiff_pair_row* rows;
     const uint8_t* pool;
@@ -39,7 +42,8 @@ struct DiffBuffers {
     uint64_t* scratch_h;    // K4 scratch for deferred pairs
     uint8_t* scratch_k;
     uint64_t scratch_cap;
-    uint32_t* slot_owner;   // per K4 slice slot of the scratch (kJoinSlice entries): its dirty pair (K3)
+    uint32_t* slot_owner;   // per K4 slice slot of the scratch (kJoinSlice entries): its dirty pair, or
+                            // ~0 inside a whole deferral's entries (K3)
     uint32_t* slice_cnt;    // per slot: paths its slice wrote (K4a)
     uint8_t* slice_weq;     // per slot: every path a wire-equal number change (K4a)
     uint64_t* out_h;

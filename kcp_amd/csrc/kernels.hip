@@ -47,13 +47,26 @@ __device__ __forceinline__ uint32_t deep_join_max(uint32_t sub_arg) {
     return m == 1u ? ~0u : kDeepJoin << (m ? m - 1u : 0u);
 }
 
-// scratch entries of a deferred pair: each region's merged keys rounded up to whole slices, the status
-// region with one more entry for the sentinel
+// Scratch entries of a deferred pair.  need = the merged keys of each joined region + the status-absent
+// sentinel (when the pair has one) bounds its paths.  A pair with need <= kJoinSlice -- one K2 deferred
+// only because its wave arena was full -- is a *whole* deferral: exactly need entries, joined by one
+// wave in K3 (k_compact).  A larger one is *sliced*: each region's merged keys in kJoinSlice-key slices,
+// every slice writing at its own kJoinSlice-entry offset, so the cap is a whole number of slices (and at
+// least need, for the sentinel after the packed paths); a sliced cap is therefore >= 2 * kJoinSlice and
+// cap <= kJoinSlice tells the two kinds apart.
+constexpr uint32_t kNoOwner = 0xFFFFFFFFu;  // slot_owner of a slot inside a whole deferral's entries
 __device__ __forceinline__ uint32_t defer_cap(uint32_t spec_l_a, uint32_t spec_l_b, uint32_t stat_l_a,
                                               uint32_t stat_l_b, uint32_t f) {
     const uint32_t Ls = (f & F_JSPEC) ? spec_l_a + spec_l_b : 0u;
     const uint32_t Lt = (f & F_JSTAT) ? stat_l_a + stat_l_b : 0u;
-    return ((Ls + kJoinSlice - 1u) / kJoinSlice + (Lt + kJoinSlice) / kJoinSlice) * kJoinSlice;
+    const uint32_t need = Ls + Lt + ((f & F_SENT) ? 1u : 0u);
+    if (need <= kJoinSlice) return need;
+    const uint32_t slices = (Ls + kJoinSlice - 1u) / kJoinSlice + (Lt + kJoinSlice - 1u) / kJoinSlice;
+    return max(slices, (need + kJoinSlice - 1u) / kJoinSlice) * kJoinSlice;
+}
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
+    const uint32_t s = a + b;
+    return s < a ? 0xFFFFFFFFu : s;
 }
 
 
@@ -191,7 +204,12 @@ struct V4 {
     uint32_t x, y, z, w;
 };
 __device__ __forceinline__ uint32_t vadd(uint32_t a, uint32_t b) { return a + b; }
-__device__ __forceinline__ V4 vadd(const V4& a, const V4& b) { return V4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+// w (the deferred pairs' scratch entries) saturates at 2^32 - 1 -- saturating addition is associative --
+// so a batch whose deferred joins would need more scratch than u32 offsets address is reported
+// (GPUDIFF_E_CAPACITY) instead of wrapping into overlapping scratch
+__device__ __forceinline__ V4 vadd(const V4& a, const V4& b) {
+    return V4{a.x + b.x, a.y + b.y, a.z + b.z, sat_add(a.w, b.w)};
+}
 template <class V> __device__ __forceinline__ V vzero() { return V{}; }
 __device__ __forceinline__ uint32_t vshfl(uint32_t v, uint32_t src) { return shfl32(v, src); }
 __device__ __forceinline__ V4 vshfl(const V4& v, uint32_t src) {
@@ -269,52 +287,6 @@ __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t*
     if (blockIdx.x == last && t == 255) {  // run = base + every element of the tile (zero past n)
         *total = run;
         if (write_terminal) out[n] = run;
-    }
-}
-
-// One wave per chunk: ballot + prefix compaction into the ID lists.
-__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ flags, const uint32_t* __restrict__ caps,
-                                                 const uint32_t* __restrict__ pair_ids, uint32_t n,
-                                                 const uint4* __restrict__ cbase, uint32_t* __restrict__ spec_ids,
-                                                 uint32_t* __restrict__ status_ids, uint32_t* __restrict__ dirty_ids,
-                                                 uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off,
-                                                 uint32_t c_begin, uint32_t c_end, const uint32_t* __restrict__ path_src,
-                                                 const uint32_t* __restrict__ path_cnt,
-                                                 uint32_t* __restrict__ path_count, const uint8_t* __restrict__ nbits,
-                                                 uint8_t* __restrict__ noop_d, uint32_t* __restrict__ slot_owner,
-                                                 uint64_t scratch_cap) {
-    const uint32_t lane = lane_id();
-    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint64_t lt = mask_lt(lane);
-    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
-        const uint32_t p = (c << 6) + lane;
-        const bool valid = p < n;
-        const uint32_t f = valid ? flags[p] : 0u;
-        const uint64_t bs = ballot(f & F_SPEC), bt = ballot(f & F_STATUS), bd = ballot(f & (F_SPEC | F_STATUS));
-        if (bd == 0) continue;
-        const uint4 base = cbase[c];
-        const bool dirty = (f & (F_SPEC | F_STATUS)) != 0u;
-        const uint32_t id = dirty ? pair_ids[p] : 0u;
-        const uint32_t cap = dirty ? caps[p] : 0u;
-        const uint32_t cincl = wave_incl_scan(cap);
-        if (f & F_SPEC) spec_ids[base.x + popc64(bs & lt)] = id;
-        if (f & F_STATUS) status_ids[base.y + popc64(bt & lt)] = id;
-        if (dirty) {
-            const uint32_t d = base.z + popc64(bd & lt);
-            dirty_ids[d] = id;
-            dirty_idx[d] = p;
-            if (f & F_DEFER) {  // K4 joins it into its scratch slot and writes the count
-                const uint32_t so = base.w + cincl - cap;  // whole K4 slices (defer_cap)
-                scratch_off[d] = so;
-                if ((uint64_t)so + cap <= scratch_cap)  // else K4 reports the overflow, the host re-runs
-                    for (uint32_t q = 0; q < cap / kJoinSlice; q++) slot_owner[so / kJoinSlice + q] = d;
-            } else {            // K2 already wrote its paths into a wave arena (and the no-op bits)
-                scratch_off[d] = path_src[p] | ARENA_BIT;
-                path_count[d] = path_cnt[p];
-                noop_d[d] = nbits[p];
-            }
-        }
     }
 }
 
@@ -648,6 +620,132 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
     return n;
 }
 
+// ---------------------------------------------------------------- K3 compaction
+// A deferred pair's scratch entries [so, so + cap): a sliced deferral owns every kJoinSlice-aligned slot
+// that starts inside them (exactly cap / kJoinSlice slots: its cap is a multiple of kJoinSlice), and its
+// slice i is the i-th of those; a whole deferral's entries hold at most one slot start, marked kNoOwner.
+// The slots of [before, after) are therefore exactly those starting in it, each written once.  Returns
+// whether the entries fit the scratch (else K4 reports the overflow and the host re-runs K4-K6).
+__device__ __forceinline__ bool place_deferred(uint32_t d, uint64_t so, uint32_t cap, uint64_t scratch_cap,
+                                               uint32_t* __restrict__ slot_owner) {
+    if (so > scratch_cap || cap > scratch_cap - so) return false;
+    const uint32_t b0 = (uint32_t)((so + kJoinSlice - 1u) / kJoinSlice);
+    const uint32_t b1 = (uint32_t)((so + cap + kJoinSlice - 1u) / kJoinSlice);  // slots starting before the end
+    if (cap > kJoinSlice) {
+        for (uint32_t q = b0; q < b1; q++) slot_owner[q] = d;
+    } else if (b0 < b1) {
+        slot_owner[b0] = kNoOwner;
+    }
+    return true;
+}
+
+// The whole deferrals among the wave's lanes (bit k: lane k's pair), one at a time: join_pair straight
+// into the pair's exact scratch entries, path count and no-op bits written here (K4 skips them).
+__device__ __forceinline__ void join_whole(uint64_t wm, uint32_t p, uint32_t d, uint32_t so, uint32_t f,
+                                           const gpudiff_pair_row* __restrict__ rows, const uint8_t* __restrict__ pool,
+                                           uint64_t mask, uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
+                                           uint32_t* __restrict__ path_count, uint8_t* __restrict__ noop_d,
+                                           uint32_t lane) {
+    for (; wm; wm &= wm - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(wm);
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)p, (int)k);
+        const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)k);
+        const uint32_t sok = (uint32_t)__builtin_amdgcn_readlane((int)so, (int)k);
+        const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k);
+        const gpudiff_pair_row r = rows[pk];
+        uint32_t nb = 0;
+        const uint32_t cnt = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
+        if (lane == 0) {
+            path_count[dk] = cnt;
+            noop_d[dk] = (uint8_t)nb;
+        }
+    }
+}
+
+// One wave per chunk: ballot + prefix compaction into the ID lists; scratch entries and K4 slots of the
+// deferred pairs (place_deferred), and the whole deferrals joined on the spot.
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ flags, const uint32_t* __restrict__ caps,
+                                                 const uint32_t* __restrict__ pair_ids, uint32_t n,
+                                                 const uint4* __restrict__ cbase, uint32_t* __restrict__ spec_ids,
+                                                 uint32_t* __restrict__ status_ids, uint32_t* __restrict__ dirty_ids,
+                                                 uint32_t* __restrict__ dirty_idx, uint32_t* __restrict__ scratch_off,
+                                                 uint32_t c_begin, uint32_t c_end, const uint32_t* __restrict__ path_src,
+                                                 const uint32_t* __restrict__ path_cnt,
+                                                 uint32_t* __restrict__ path_count, const uint8_t* __restrict__ nbits,
+                                                 uint8_t* __restrict__ noop_d, uint32_t* __restrict__ slot_owner,
+                                                 uint64_t scratch_cap, const gpudiff_pair_row* __restrict__ rows,
+                                                 const uint8_t* __restrict__ pool, uint64_t mask,
+                                                 uint64_t* __restrict__ sh, uint8_t* __restrict__ sk) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint64_t lt = mask_lt(lane);
+    for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
+        const uint32_t p = (c << 6) + lane;
+        const bool valid = p < n;
+        const uint32_t f = valid ? flags[p] : 0u;
+        const uint64_t bs = ballot(f & F_SPEC), bt = ballot(f & F_STATUS), bd = ballot(f & (F_SPEC | F_STATUS));
+        if (bd == 0) continue;
+        const uint4 base = cbase[c];
+        const bool dirty = (f & (F_SPEC | F_STATUS)) != 0u;
+        const uint32_t id = dirty ? pair_ids[p] : 0u;
+        const uint32_t cap = dirty ? caps[p] : 0u;
+        const uint32_t cincl = wave_incl_scan(cap);
+        if (f & F_SPEC) spec_ids[base.x + popc64(bs & lt)] = id;
+        if (f & F_STATUS) status_ids[base.y + popc64(bt & lt)] = id;
+        uint32_t d = 0, so = 0;
+        bool whole = false;
+        if (dirty) {
+            d = base.z + popc64(bd & lt);
+            dirty_ids[d] = id;
+            dirty_idx[d] = p;
+            if (f & F_DEFER) {  // K4 (or, whole, this wave) joins it into its scratch entries
+                // base.w saturates (a batch past u32 scratch offsets): then nothing fits and K4 reports it
+                const uint64_t so64 = base.w == 0xFFFFFFFFu ? ~0ull : (uint64_t)base.w + (cincl - cap);
+                so = (uint32_t)min(so64, (uint64_t)0xFFFFFFFFu);
+                scratch_off[d] = so;
+                whole = place_deferred(d, so64, cap, scratch_cap, slot_owner) && cap <= kJoinSlice;
+            } else {            // K2 already wrote its paths into a wave arena (and the no-op bits)
+                scratch_off[d] = path_src[p] | ARENA_BIT;
+                path_count[d] = path_cnt[p];
+                noop_d[d] = nbits[p];
+            }
+        }
+        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane);
+    }
+}
+
+// The overflow re-run after the scratch grew (K3 placed nothing past the old scratch): every deferred
+// pair placed again and its whole deferrals joined.  Wave per 64 dirty pairs.
+__global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__ flags, const uint32_t* __restrict__ caps,
+                                                     const uint32_t* __restrict__ dirty_idx,
+                                                     const uint32_t* __restrict__ scratch_off,
+                                                     const uint32_t* __restrict__ summary, uint64_t scratch_cap,
+                                                     uint32_t* __restrict__ slot_owner,
+                                                     const gpudiff_pair_row* __restrict__ rows,
+                                                     const uint8_t* __restrict__ pool, uint64_t mask,
+                                                     uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
+                                                     uint32_t* __restrict__ path_count, uint8_t* __restrict__ noop_d) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t ndirty = summary[2];
+    if (summary[6] == 0u) return;
+    for (uint32_t c = wave; c < (ndirty + 63u) >> 6; c += nwaves) {
+        const uint32_t d = (c << 6) + lane;
+        const uint32_t p = d < ndirty ? dirty_idx[d] : 0u;
+        const uint32_t f = d < ndirty ? flags[p] : 0u;
+        bool whole = false;
+        uint32_t so = 0;
+        if (f & F_DEFER) {
+            so = scratch_off[d];
+            const uint32_t cap = caps[p];
+            whole = place_deferred(d, so, cap, scratch_cap, slot_owner) && cap <= kJoinSlice;
+        }
+        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane);
+    }
+}
+
 // ---------------------------------------------------------------- K4: merge-path slices
 // A deferred pair's join -- one K2 could not hold in its wave arena, or one over kDeepJoin keys that
 // would keep a single K2 wave busy long after the others finish (config4's list shifts: thousands of
@@ -687,18 +785,33 @@ __device__ uint32_t merge_split(const uint32_t* __restrict__ ka, uint32_t La, co
     return lo;
 }
 
-// arena bytes of entries [0, n) of a region (long values' tails before entry n)
+// first scratch slot starting at or after entry e
+__device__ __forceinline__ uint32_t slot_ceil(uint32_t e) { return (uint32_t)(((uint64_t)e + kJoinSlice - 1u) / kJoinSlice); }
+
+// arena bytes of entries [0, n) of a region (long values' tails before entry n).  Every slice of a pair
+// sums the metas before its start, so a region of L keys costs O(L^2 / kJoinSlice) meta reads over its
+// slices; they are L2-resident re-reads, and this loop keeps 8 x 16 B (32 metas) per lane in
+// flight -- 2048 metas per wave step, 8x the former 4-byte loop -- so even a 100k-key list (the k8s
+// object size limit) takes ~50 steps per slice, about the slice's own join time.  The metas array starts
+// 4-B aligned (12 L bytes into a 16-B aligned segment): a dword head reaches 16-B alignment first.
 __device__ uint32_t arena_prefix(const uint32_t* __restrict__ metas, uint32_t n, uint32_t lane) {
-    uint32_t acc = 0;
-    for (uint32_t i = 0; i < n; i += 256u) {
-        uint32_t a[4];
+    const uint32_t head = min(n, (uint32_t)((16u - ((uintptr_t)metas & 15u)) & 15u) >> 2);
+    uint32_t acc = lane < head ? meta_arena(metas[lane]) : 0u;
+    const u32x4* m4 = (const u32x4*)(metas + head);
+    const uint32_t n4 = (n - head) >> 2, rest = (n - head) & 3u;
+    constexpr uint32_t PU = 8;
+    for (uint32_t i = 0; i < n4; i += 64u * PU) {
+        u32x4 v[PU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t j = i + (uint32_t)u * 64u + lane;
-            a[u] = j < n ? meta_arena(metas[j]) : 0u;
+        for (uint32_t u = 0; u < PU; u++) {
+            const uint32_t j = i + u * 64u + lane;
+            v[u] = j < n4 ? m4[j] : u32x4{0u, 0u, 0u, 0u};
         }
-        acc += a[0] + a[1] + a[2] + a[3];
+#pragma unroll
+        for (uint32_t u = 0; u < PU; u++)
+            acc += meta_arena(v[u].x) + meta_arena(v[u].y) + meta_arena(v[u].z) + meta_arena(v[u].w);
     }
+    if (lane < rest) acc += meta_arena(metas[head + 4u * n4 + lane]);
     return wave_sum(acc);
 }
 
@@ -730,8 +843,8 @@ __device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_
 
 // K4a (join_region by default; PL, GPUDIFF_OPT_K4_PIPELINED_JOIN: the software-pipelined join_region_pl,
 // measured 15% slower on config4's slices, profiles/r03m)
-// wave per slice of the scratch slots [before.w, after.w) / kJoinSlice (this segment's deferred
-// pairs); writes each slice's path count and whether all its paths are wire-equal number changes
+// wave per scratch slot starting in [before.w, after.w) (this segment's deferred pairs: place_deferred);
+// writes each slice's path count and whether all its paths are wire-equal number changes
 template <bool PL>
 __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __restrict__ rows,
                                                      const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
@@ -751,11 +864,12 @@ __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __r
         if (blockIdx.x == 0 && threadIdx.x == 0) summary[4] = 1u;
         return;
     }
-    const uint32_t s0 = (tot_before ? tot_before->w : 0u) / kJoinSlice, s1 = after.w / kJoinSlice;
+    const uint32_t s0 = slot_ceil(tot_before ? tot_before->w : 0u), s1 = slot_ceil(after.w);
     for (uint32_t s = s0 + wave; s < s1; s += nwaves) {
         const uint32_t d = uni(slot_owner[s]);
+        if (d == kNoOwner) continue;  // inside a whole deferral (K3 joined it)
         const uint32_t so = uni(scratch_off[d]);
-        const uint32_t i = s - so / kJoinSlice;  // slice of this pair
+        const uint32_t i = s - slot_ceil(so);  // slice of this pair
         const uint32_t p = uni(dirty_idx[d]);
         const uint32_t f = uni((uint32_t)flags[p]);
         const gpudiff_pair_row r = rows[p];
@@ -783,23 +897,6 @@ __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __r
     }
 }
 
-// The slot owners of every deferred pair (the overflow re-run: K3 wrote none past the old scratch)
-__global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__ flags, const uint32_t* __restrict__ caps,
-                                                     const uint32_t* __restrict__ dirty_idx,
-                                                     const uint32_t* __restrict__ scratch_off,
-                                                     const uint32_t* __restrict__ summary, uint64_t scratch_cap,
-                                                     uint32_t* __restrict__ slot_owner) {
-    const uint32_t ndirty = summary[2];
-    if (summary[6] == 0u) return;
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < ndirty; d += gridDim.x * blockDim.x) {
-        const uint32_t p = dirty_idx[d];
-        if (!(flags[p] & F_DEFER)) continue;
-        const uint32_t so = scratch_off[d], cap = caps[p];
-        if ((uint64_t)so + cap <= scratch_cap)
-            for (uint32_t q = 0; q < cap / kJoinSlice; q++) slot_owner[so / kJoinSlice + q] = d;
-    }
-}
-
 // K4b: wave per deferred pair of this segment, found as the first slot of its scratch (so the grid walks
 // only deferred pairs, in parallel: one wave per 64 dirty pairs, walking the deferred ones in turn, took
 // 53 us on config4, profiles/r03o); each deferred pair's slices are packed in order at the
@@ -821,18 +918,19 @@ __global__ __launch_bounds__(256) void k_join_gather(const gpudiff_pair_row* __r
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     if (summary[6] == 0u || summary[4] != 0u) return;
-    const uint32_t s0 = (tot_before ? tot_before->w : 0u) / kJoinSlice, s1 = tot_after->w / kJoinSlice;
+    const uint32_t s0 = slot_ceil(tot_before ? tot_before->w : 0u), s1 = slot_ceil(tot_after->w);
     for (uint32_t s = s0 + wave; s < s1; s += nwaves) {
         const uint32_t dk = uni(slot_owner[s]);
+        if (dk == kNoOwner) continue;  // inside a whole deferral
         const uint32_t so = uni(scratch_off[dk]);
-        if (s != so / kJoinSlice) continue;  // not its pair's first slot
+        if (s != slot_ceil(so)) continue;  // not its pair's first slot
         const uint32_t pk = uni(dirty_idx[dk]);
         const uint32_t fk = uni((uint32_t)flags[pk]);
         const gpudiff_pair_row r = rows[pk];
         const uint32_t Ls = (fk & F_JSPEC) ? r.spec_l_a + r.spec_l_b : 0u;
         const uint32_t Lt = (fk & F_JSTAT) ? r.stat_l_a + r.stat_l_b : 0u;
         const uint32_t nsl = (Ls + kJoinSlice - 1u) / kJoinSlice, ntl = (Lt + kJoinSlice - 1u) / kJoinSlice;
-        const uint32_t s_first = so / kJoinSlice;
+        const uint32_t s_first = s;  // = slot_ceil(so): the pair's first slot
         uint32_t n = 0;
         bool spec_weq = true, stat_weq = true;
         for (uint32_t i = 0; i < nsl + ntl; i++) {
@@ -1615,6 +1713,20 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     return hipGetLastError();
 }
 
+// k_compact's grid: one resident block per CU per slot its occupancy allows (it carries the whole-deferral
+// join, so it holds more VGPRs than a plain compaction; a larger grid would only queue blocks)
+static uint32_t compact_cap_blocks() {
+    static int occ = 0;
+    if (!occ) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k_compact), 256, 0) !=
+                hipSuccess || n <= 0)
+            n = 4;
+        occ = n;
+    }
+    return std::min<uint32_t>(kPersistBlocks, 256u * (uint32_t)occ);
+}
+
 // K3 over the chunks [c0, c1) of one segment: running totals before -> after
 hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                           uint4* after) {
@@ -1625,11 +1737,10 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     if (ntiles) k_scan_tiles<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts);
     k_scan_apply<V4><<<std::max(ntiles, 1u), 256, 0, s>>>(cc, nullptr, n, ts, (const V4*)before, (V4*)after, cc,
                                                           false);
-    k_compact<<<grid_for(n, kPersistBlocks), 256, 0, s>>>(b.flags, b.caps, b.pair_ids, b.n_pairs,
-                                                           (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids,
-                                                           b.dirty_ids, b.dirty_idx, b.scratch_off, c0, c1,
-                                                           b.path_src, b.path_cnt, b.path_count, b.nbits, b.noop_d,
-                                                           b.slot_owner, b.scratch_cap);
+    k_compact<<<grid_for(n, compact_cap_blocks()), 256, 0, s>>>(
+        b.flags, b.caps, b.pair_ids, b.n_pairs, (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids, b.dirty_ids,
+        b.dirty_idx, b.scratch_off, c0, c1, b.path_src, b.path_cnt, b.path_count, b.nbits, b.noop_d, b.slot_owner,
+        b.scratch_cap, b.rows, b.pool, b.hash_mask, b.scratch_h, b.scratch_k);
     return hipGetLastError();
 }
 
@@ -1654,8 +1765,9 @@ hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_
 }
 
 hipError_t launch_slot_owners(hipStream_t s, const DiffBuffers& b) {
-    k_slot_owners<<<kPersistBlocks, 256, 0, s>>>(b.flags, b.caps, b.dirty_idx, b.scratch_off, b.summary, b.scratch_cap,
-                                                 b.slot_owner);
+    k_slot_owners<<<compact_cap_blocks(), 256, 0, s>>>(b.flags, b.caps, b.dirty_idx, b.scratch_off, b.summary,
+                                                       b.scratch_cap, b.slot_owner, b.rows, b.pool, b.hash_mask,
+                                                       b.scratch_h, b.scratch_k, b.path_count, b.noop_d);
     return hipGetLastError();
 }
 

@@ -664,24 +664,8 @@ struct gpudiff_synth {
     }
 };
 
-extern "C" {
-
-int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudiff_synth** out) {
-    if (!cfg || !out || world < 1 || rank < 0 || rank >= world || cfg->n_clusters == 0) return -1;
-    std::unique_ptr<gpudiff_synth> s(new (std::nothrow) gpudiff_synth());
-    if (!s) return -2;
-    s->cfg = *cfg;
-    if (s->cfg.crd_leaves == 0) s->cfg.crd_leaves = 200;
-    double w[5] = {cfg->w_configmap, cfg->w_secret, cfg->w_deployment, cfg->w_crd, cfg->w_deep};
-    double tot = 0;
-    for (double x : w) tot += x;
-    if (tot <= 0) return -1;
-    double acc = 0;
-    for (int k = 0; k < 5; k++) {
-        acc += w[k] / tot;
-        s->cum[k] = acc;
-    }
-    // cluster sizes: rank-frequency Zipf(1.1) with offset 10 over a seeded permutation
+// cluster sizes: rank-frequency Zipf(1.1) with offset 10 over a seeded permutation
+static std::vector<uint64_t> cluster_sizes(const gpudiff_synth_cfg* cfg) {
     const uint32_t C = cfg->n_clusters;
     std::vector<uint32_t> perm(C);
     for (uint32_t i = 0; i < C; i++) perm[i] = i;
@@ -700,24 +684,29 @@ int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudif
         assigned += size[c];
     }
     for (uint64_t k = 0; assigned < cfg->n_pairs; k++, assigned++) size[k % C]++;
-    // LPT assignment of clusters to ranks by pair count
-    std::vector<uint32_t> order(C);
-    for (uint32_t i = 0; i < C; i++) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-        return size[x] != size[y] ? size[x] > size[y] : x < y;
-    });
-    std::vector<uint64_t> load(world, 0);
-    std::vector<int> owner(C);
-    for (uint32_t c : order) {
-        int best = 0;
-        for (int k = 1; k < world; k++)
-            if (load[k] < load[best]) best = k;
-        owner[c] = best;
-        load[best] += size[c];
+    return size;
+}
+
+// a population whose local clusters are those with mine(c)
+template <class Mine>
+static int synth_plan(const gpudiff_synth_cfg* cfg, Mine mine, gpudiff_synth** out) {
+    std::unique_ptr<gpudiff_synth> s(new (std::nothrow) gpudiff_synth());
+    if (!s) return -2;
+    s->cfg = *cfg;
+    if (s->cfg.crd_leaves == 0) s->cfg.crd_leaves = 200;
+    double w[5] = {cfg->w_configmap, cfg->w_secret, cfg->w_deployment, cfg->w_crd, cfg->w_deep};
+    double tot = 0;
+    for (double x : w) tot += x;
+    if (tot <= 0) return -1;
+    double acc = 0;
+    for (int k = 0; k < 5; k++) {
+        acc += w[k] / tot;
+        s->cum[k] = acc;
     }
+    const std::vector<uint64_t> size = cluster_sizes(cfg);
     uint64_t g = 0, l = 0;
-    for (uint32_t c = 0; c < C; c++) {
-        if (owner[c] == rank && size[c]) {
+    for (uint32_t c = 0; c < cfg->n_clusters; c++) {
+        if (mine(c) && size[c]) {
             s->local.push_back({g, size[c], l, c});
             l += size[c];
         }
@@ -725,6 +714,42 @@ int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudif
     }
     s->n_local = l;
     *out = s.release();
+    return 0;
+}
+
+extern "C" {
+
+int gpudiff_synth_open_ex(const gpudiff_synth_cfg* cfg, int world, int rank, const uint64_t* cluster_weight,
+                          gpudiff_synth** out) {
+    if (!cfg || !out || world < 1 || rank < 0 || rank >= world || cfg->n_clusters == 0) return -1;
+    // LPT of clusters onto ranks: by the given weights (sum of B_pair,
+    // gpudiff_synth_cluster_bytes), else by pair count; the rule of gpudiff_shard_lpt / shard.lpt_assign
+    const uint32_t C = cfg->n_clusters;
+    const std::vector<uint64_t> size = cluster_sizes(cfg);
+    const uint64_t* wt = cluster_weight ? cluster_weight : size.data();
+    std::vector<uint32_t> order(C);
+    for (uint32_t i = 0; i < C; i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return wt[x] != wt[y] ? wt[x] > wt[y] : x < y; });
+    std::vector<uint64_t> load(world, 0);
+    std::vector<int> owner(C);
+    for (uint32_t c : order) {
+        int best = 0;
+        for (int k = 1; k < world; k++)
+            if (load[k] < load[best]) best = k;
+        owner[c] = best;
+        load[best] += wt[c];
+    }
+    return synth_plan(cfg, [&](uint32_t c) { return owner[c] == rank; }, out);
+}
+
+int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudiff_synth** out) {
+    return gpudiff_synth_open_ex(cfg, world, rank, nullptr, out);
+}
+
+int gpudiff_synth_cluster_sizes(const gpudiff_synth_cfg* cfg, uint64_t* out) {
+    if (!cfg || !out || cfg->n_clusters == 0) return -1;
+    const std::vector<uint64_t> size = cluster_sizes(cfg);
+    memcpy(out, size.data(), size.size() * sizeof(uint64_t));
     return 0;
 }
 
@@ -777,6 +802,24 @@ int gpudiff_synth_encode(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t 
     s->last_n = n;
     if (pool_bytes) *pool_bytes = pb;
     if (total_leaves) *total_leaves = lv;
+    return 0;
+}
+
+int gpudiff_synth_cluster_bytes(const gpudiff_synth_cfg* cfg, uint32_t stride, uint32_t offset, uint32_t threads,
+                                uint64_t* out) {
+    if (!cfg || !out || stride == 0 || offset >= stride || cfg->n_clusters == 0) return -1;
+    gpudiff_synth* raw = nullptr;
+    int rc = synth_plan(cfg, [&](uint32_t c) { return c % stride == offset; }, &raw);
+    if (rc) return rc;
+    std::unique_ptr<gpudiff_synth> s(raw);
+    for (uint32_t c = offset; c < cfg->n_clusters; c += stride) out[c] = 0;
+    const uint64_t step = 1ull << 17;
+    for (uint64_t first = 0; first < s->n_local; first += step) {
+        const uint64_t n = std::min(step, s->n_local - first);
+        if ((rc = gpudiff_synth_encode(s.get(), first, n, threads, nullptr, nullptr))) return rc;
+        for (uint32_t t = 0; t < s->last_threads; t++)
+            for (const gpudiff_pair_row& r : s->workers[t]->rows) out[r.cluster_id] += gpudiff_pair_compare_bytes(&r);
+    }
     return 0;
 }
 

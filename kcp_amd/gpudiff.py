@@ -17,6 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpudiff.so")
 
+ABI_VERSION = 4  # GPUDIFF_ABI_VERSION of include/gpudiff.h
 OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUND = range(-1, -9, -1)
 
@@ -299,6 +300,12 @@ def _load() -> C.CDLL:
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
+    # the structures above and the meaning of unchanged symbols (e.g. gpudiff_write_plan_get's default
+    # mode, ABI 4) follow this ABI: a library built from other headers is refused, not half-used
+    got = lib.gpudiff_abi_version()
+    if got != ABI_VERSION:
+        raise ImportError("%s has ABI %d, this binding needs %d (rebuild with kcp_amd/build.py)"
+                          % (LIB_PATH, got, ABI_VERSION))
     return lib
 
 

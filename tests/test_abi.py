@@ -43,6 +43,17 @@ def test_host_only_context_refuses_device_work():
     e.close()
 
 
+def test_binding_abi_matches_header():
+    """The Python binding's ABI_VERSION is the header's, and its loader checks the library against it
+    (gpudiff_write_plan_get kept its name while its default mode changed in ABI 4)."""
+    from kcp_amd import gpudiff as G
+    src = open(os.path.join(ROOT, "include", "gpudiff.h")).read()
+    assert int(re.search(r"#define GPUDIFF_ABI_VERSION (\d+)", src).group(1)) == G.ABI_VERSION
+    assert G.lib().gpudiff_abi_version() == G.ABI_VERSION
+    import inspect
+    assert "gpudiff_abi_version" in inspect.getsource(G._load)
+
+
 def test_header_compiles_as_c():
     import subprocess
     import tempfile

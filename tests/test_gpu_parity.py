@@ -138,6 +138,51 @@ def test_scratch_overflow_keeps_arena_paths():
     e.close()
 
 
+def test_small_deferrals_take_exact_scratch():
+    """a small pair deferred only because its K2 wave arena is full (here: no arena at all, so
+    every dirty pair is deferred) gets exactly its merged keys + sentinel as K4 scratch and is joined whole
+    by K3 -- not two 1024-entry slices -- and deep pairs in the same batch still go through the slices.
+    The scratch need (summary word 3) must be the exact sum, the first pass overflows the default 64Ki
+    scratch (the grow-and-rejoin path re-places and re-joins whole deferrals), and every flag, ID and path
+    equals the oracle's."""
+    small, _, _ = make_pairs(9000, seed=91, mix=(("cm", 0.6), ("deploy", 0.4)), mutate_frac=0.9, pretty_frac=0)
+    deep = deep_pairs()[:6]
+    pairs = small + deep
+    e = G.Engine(device=0, flags=15 << 21)  # arena_per_wave = 16384 >> 15 = 0
+    hb = e.encode(pairs)
+    rows = hb.rows()
+    db = e.device_batch(hb.info().pool_bytes + 4096, len(pairs))
+    db.append(hb)
+    res = e.wait(e.diff(db))
+    exp = assert_matches(res, pairs)
+    import torch
+    cnt = torch.zeros(8, dtype=torch.int32, device="cuda")
+    db.export(G.EXPORT_COUNTS, cnt.data_ptr(), 8)
+    e.sync()
+    scratch = int(cnt[3].item()) & 0xFFFFFFFF
+    # expected: per dirty pair (not a decode error) need = joined regions' leaves + sentinel, whole when
+    # <= 1024, else whole 1024-entry slices (spec slices + status slices, at least need)
+    want, n_whole = 0, 0
+    for r, x in zip(rows, exp):
+        if not (x["spec_dirty"] or x["status_dirty"]) or x.get("decode_error"):
+            continue
+        ls = int(r["spec_l_a"]) + int(r["spec_l_b"]) if x["spec_dirty"] else 0
+        has_st_b = bool(int(r["flags_b"]) & G.OBJ_HAS_STATUS)
+        lt = int(r["stat_l_a"]) + int(r["stat_l_b"]) if x["status_dirty"] else 0
+        need = ls + lt + (1 if (x["status_dirty"] and not has_st_b) else 0)
+        if need <= 1024:
+            want += need
+            n_whole += 1
+        else:
+            sl = -(-ls // 1024) + -(-lt // 1024)
+            want += max(sl, -(-need // 1024)) * 1024
+    assert n_whole > 5000 and want > 65536
+    assert scratch == want, (scratch, want)
+    db.free()
+    hb.free()
+    e.close()
+
+
 @pytest.mark.parametrize("dev", [False, True], ids=["host_encode", "device_encode"])
 def test_forced_collisions(dev):
     e = G.Engine(device=0, path_hash_bits=8, device_encode=dev)

@@ -124,3 +124,67 @@ def test_equal_keys_on_every_boundary():
     want = join(ka, kb, va, vb)
     for D in (1, 3, 7, 1023, 1024, 1025):
         assert join_sliced(ka, kb, va, vb, D) == want
+
+
+def _defer_cap(ls, lt, sent, slice_=1024):
+    """Restatement of kernels.hip defer_cap: exact entries for a whole deferral (need <= one slice), else
+    whole slices per region and at least need."""
+    need = ls + lt + sent
+    if need <= slice_:
+        return need
+    sl = -(-ls // slice_) + -(-lt // slice_)
+    return max(sl, -(-need // slice_)) * slice_
+
+
+def _place(caps, slice_=1024):
+    """Restatement of kernels.hip place_deferred over a batch's deferred pairs (in dirty order): slot q
+    (starting at entry q * slice) belongs to the pair whose entries contain its start; a whole deferral
+    marks it 'none'."""
+    owner = {}
+    so = 0
+    offs = []
+    for d, cap in enumerate(caps):
+        offs.append(so)
+        b0, b1 = -(-so // slice_), -(-(so + cap) // slice_)
+        for q in range(b0, b1):
+            assert q not in owner
+            owner[q] = d if cap > slice_ else None
+            if cap <= slice_:
+                assert b1 - b0 == 1  # a whole deferral holds at most one slot start
+        so += cap
+    return owner, offs, so
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_deferred_scratch_placement(seed):
+    """whole deferrals take exact entries, sliced ones whole slices at unaligned offsets.  Every
+    slot starting inside the batch's entries is written exactly once; a sliced pair owns exactly cap / 1024
+    consecutive slots starting at slot_ceil(so), and its slice i's window [so + 1024 i, +1024) lies inside
+    its entries -- what K4a (slice i = s - slot_ceil(so)) and K4b (first slot = slot_ceil(so)) rely on."""
+    rnd = random.Random(seed)
+    caps, kinds = [], []
+    for _ in range(rnd.randint(1, 400)):
+        if rnd.random() < 0.8:
+            ls, lt = rnd.randint(0, 600), rnd.randint(0, 400)
+        else:
+            ls, lt = rnd.randint(0, 9000), rnd.randint(0, 5000)
+        sent = rnd.randint(0, 1)
+        if ls + lt + sent == 0:
+            sent = 1
+        cap = _defer_cap(ls, lt, sent)
+        assert cap >= ls + lt + sent
+        if cap > 1024:
+            assert cap % 1024 == 0 and cap >= 2048 and cap // 1024 >= -(-ls // 1024) + -(-lt // 1024)
+        caps.append(cap)
+    owner, offs, total = _place(caps)
+    assert sorted(owner) == list(range(-(-total // 1024)))
+    for d, (cap, so) in enumerate(zip(caps, offs)):
+        mine = sorted(q for q, o in owner.items() if o == d)
+        if cap <= 1024:
+            assert not mine
+            continue
+        first = -(-so // 1024)
+        assert mine == list(range(first, first + cap // 1024))
+        for q in mine:
+            i = q - first
+            assert so <= so + 1024 * i and so + 1024 * (i + 1) <= so + cap
