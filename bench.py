@@ -181,6 +181,24 @@ def main():
                     help="PMC traffic summary to attach as roofline.traffic (default: the newest committed "
                          "profiles/**/pmc_summary.json, used only if it was measured on this workload with the "
                          "same K2 sources; 'none' to skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: nccl = RCCL over xGMI (the product path); gloo = a rehearsal of the same N-rank "
+                         "path on one GPU (every rank on device local_rank %% device_count, counts and IDs staged "
+                         "through host tensors -- RCCL refuses two ranks on one device); timings then measure "
+                         "the rehearsal, not the node")
+    ap.add_argument("--dump-gather", default="",
+                    help="rank 0 writes the last step's node-wide spec / status dirty IDs to this .npz (tests)")
+    ap.add_argument("--shard-weight", default="bytes", choices=["bytes", "pairs"],
+                    help="N > 1 (or --emulate-world): LPT of logical clusters onto ranks by sum of B_pair (SURVEY.md "
+                         "8(e), the bytes K2 streams; default) or by pair count")
+    ap.add_argument("--weights-cache", default="",
+                    help="one GPU (--emulate-world): .npy of the population's per-cluster B_pair sums, reused if it "
+                         "was written for the same population (saves re-encoding 10M pairs between runs)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one GPU: time the share of rank --emulate-rank of an N-rank strong-scaling split of the "
+                         "population (diagnostic line, not the headline)")
+    ap.add_argument("--emulate-rank", type=int, default=-1,
+                    help="with --emulate-world: the rank whose share to time (-1 = the byte-heaviest rank)")
     ap.add_argument("--print-launch", action="store_true",
                     help="print the launch command --gpus N resolves to (one process per GPU) and exit")
     args = ap.parse_args(argv)
@@ -221,23 +239,27 @@ def main():
     from kcp_amd import shard
     from kcp_amd import synth as S
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gloo = args.dist_backend == "gloo"
+    gpu = local_rank % max(1, torch.cuda.device_count()) if gloo else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    comm_dev = torch.device("cpu") if gloo else dev  # where the collectives' tensors live
     collective = world > 1 or args.gather_world1
     if collective:
-        dist.init_process_group("nccl", device_id=dev, world_size=world, rank=rank,
+        dist.init_process_group(args.dist_backend, device_id=None if gloo else dev, world_size=world, rank=rank,
                                 init_method=None if world > 1 or "MASTER_ADDR" in os.environ else
                                 "tcp://127.0.0.1:%d" % free_port())
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(device=dev)  # the engine's stream, made torch's current one: exports,
+    torch.cuda.set_stream(stream)            # copies and collectives all order on it (never the null stream)
     aff, nproc, quota = host_cores()
     threads = args.threads or max(1, min(16, aff))
 
-    eng = G.Engine(device=local_rank, encode_threads=threads, stream=stream.cuda_stream, timing=True,
+    eng = G.Engine(device=gpu, encode_threads=threads, stream=stream.cuda_stream, timing=True,
                    flags=args.engine_flags)
     base = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=args.clusters)
     mult = world if scaling == "weak" else 1
     cfg = S.make_cfg(args.config, n_pairs=base.n_pairs * mult, n_clusters=base.n_clusters * mult)
-    pop = S.Population(cfg, world, rank)
+    shard_info, pop = shard_population(args, cfg, world, rank, threads, comm_dev, dist if collective else None, G, S)
     n = pop.n
     log("config %s (%s scaling): %d pairs / %d clusters node-wide; this rank %d pairs / %d clusters; %d host threads"
         % (args.config, scaling, cfg.n_pairs, cfg.n_clusters, n, pop.n_clusters, threads))
@@ -335,19 +357,29 @@ def main():
     # ---------------- the collective (N > 1): capacities agreed once, untimed
     gather = None
     if collective:
-        counts = torch.zeros(8, dtype=torch.int32, device=dev)
-        db.export(G.EXPORT_COUNTS, counts.data_ptr(), 8)
+        def export_to(t, what, n):
+            """gpudiff_dbatch_export of n elements into t: straight from HBM into a device tensor (RCCL), or
+            through a device staging tensor into the host tensor gloo sends"""
+            if t.device.type == "cuda":
+                db.export(what, t.data_ptr(), n, n)
+            else:
+                tmp = torch.empty(t.numel(), dtype=t.dtype, device=dev)
+                db.export(what, tmp.data_ptr(), n, n)
+                t.copy_(tmp)
+
+        counts = torch.zeros(8, dtype=torch.int32, device=comm_dev)
+        export_to(counts, G.EXPORT_COUNTS, 8)
         torch.cuda.synchronize()
         cap_s, cap_t = shard.DirtyGather.agree_capacity(counts, world, dist)
-        gather = shard.DirtyGather(world, cap_s, cap_t, dev, dist, depth=args.gather_depth)
-        log("collective: capacities agreed (%d spec, %d status IDs per rank), depth %d" % (cap_s, cap_t, args.gather_depth))
+        gather = shard.DirtyGather(world, cap_s, cap_t, comm_dev, dist, depth=args.gather_depth)
+        log("collective: %s, capacities agreed (%d spec, %d status IDs per rank), depth %d"
+            % (args.dist_backend, cap_s, cap_t, args.gather_depth))
 
         def fill_counts(t):
-            db.export(G.EXPORT_COUNTS, t.data_ptr(), 8)
+            export_to(t, G.EXPORT_COUNTS, 8)
 
         def fill_ids(col, buf):
-            db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
-                      buf.numel())
+            export_to(buf, G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.numel())
         gather.step(fill_counts, fill_ids)  # warm the communicator
         gather.finish()
         torch.cuda.synchronize()
@@ -378,12 +410,16 @@ def main():
                             gathered_spec=None if sa is None else int(sa.numel()),
                             gathered_status=None if ta is None else int(ta.numel()),
                             depth=gather.depth, bytes_per_rank=4 * gather.width, regrows=gather.n_regrows)
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        tot = torch.tensor([n], dtype=torch.int64, device=dev)
+        tot = torch.tensor([n], dtype=torch.int64, device=comm_dev)
         dist.all_reduce(tot)
         total_pairs = int(tot.item())
+        if sa is not None:
+            gather_check.update(node_sets_vs_truth(pop, truth, sa, ta, dist, comm_dev, G))
+            if args.dump_gather and rank == 0:
+                np.savez(args.dump_gather, spec=sa.cpu().numpy(), status=ta.cpu().numpy())
     else:
         total_pairs = n
 
@@ -469,13 +505,18 @@ def main():
                 "workload": "%s: %d pairs / %d logical clusters node-wide%s, %.0f%% mutated (%s)" % (
                     args.config, cfg.n_pairs, cfg.n_clusters,
                     " (%d x %d pairs / %d clusters, one per GPU)" % (world, base.n_pairs, base.n_clusters)
-                    if mult > 1 else (" split %d ways by logical cluster" % world if world > 1 else ""),
+                    if mult > 1 else (" split %d ways by logical cluster" % world if world > 1 else
+                                      (" -- EMULATED: rank %d's share (%d pairs) of a %d-way split, timed alone on "
+                                       "one GPU" % (shard_info["emulated_rank"], n, shard_info["world"])
+                                       if "emulated_rank" in shard_info else "")),
                     cfg.mutate_frac * 100,
                     "40% ConfigMap/Secret, 40% Deployment, 20% CRD" if args.config == "config3" else args.config),
-                "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9,
+                "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9, "shard": shard_info,
                 "parallelism": "shard-by-logical-cluster x%d (LPT)%s" % (
-                    world, (", RCCL all-gather of dirty counts+IDs per step (%d in flight)" % args.gather_depth)
-                    if collective else ""),
+                    world, ((", RCCL all-gather of dirty counts+IDs per step (%d in flight)" % args.gather_depth)
+                            if args.dist_backend == "nccl" else
+                            ", gloo all-gather of dirty counts+IDs per step through host tensors (REHEARSAL: "
+                            "every rank on one GPU; not a node measurement)") if collective else ""),
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
@@ -501,6 +542,104 @@ def main():
         print(json.dumps(line), flush=True)
     if collective:
         dist.destroy_process_group()
+
+
+def _mix64(x):
+    """splitmix64 finalizer over a u64 array (the multiset hash of node_sets_vs_truth)"""
+    x = x.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def node_sets_vs_truth(pop, truth, spec_all, status_all, dist, comm_dev, G):
+    """The node-wide dirty sets every rank gathered must equal the union of every rank's generator truth
+    (statussyncer.go:22-26: status-absent objects are status-dirty): per list, the count and a multiset
+    hash (sum of splitmix64 of the global pair IDs, mod 2^64) of the gathered IDs against the same over
+    each rank's expected IDs, summed with one all-reduce.  Checked on every rank."""
+    import torch
+    ids = pop.local_ids().astype(np.uint64)
+    exp = pop.expected_flags(truth)
+    loc = []
+    for bit in (G.SPEC_DIRTY, G.STATUS_DIRTY):
+        e = ids[(exp & bit) != 0]
+        loc += [e.size, int(_mix64(e).sum(dtype=np.uint64).view(np.int64))]
+    t = torch.tensor(loc, dtype=torch.int64, device=comm_dev)
+    dist.all_reduce(t)
+    want = t.cpu().tolist()
+    got = []
+    for g in (spec_all, status_all):
+        a = g.cpu().numpy().astype(np.uint32).astype(np.uint64)
+        got += [a.size, int(_mix64(a).sum(dtype=np.uint64).view(np.int64))]
+    ok = all(int(x) == int(y) for x, y in zip(got, want))
+    ok_all = torch.tensor([1 if ok else 0], dtype=torch.int64, device=comm_dev)
+    dist.all_reduce(ok_all, op=dist.ReduceOp.MIN)
+    return {"node_sets_eq_truth": bool(ok_all.item()), "node_expected_spec": int(want[0]),
+            "node_expected_status": int(want[2])}
+
+
+def shard_population(args, cfg, world, rank, threads, dev, dist, G, S):
+    """This rank's population.  Strong scaling at N > 1 packs whole logical clusters onto ranks by LPT on
+    each cluster's exact sum of B_pair (the bytes K2 streams, so the ranks' step times
+    balance), computed once, untimed: every rank encodes the clusters c % N == rank on the host and the
+    weight vectors are summed over ranks (one all-reduce).  --emulate-world N times one rank's share of
+    an N-way split on one GPU (the byte-heaviest by default).  Returns (shard summary, Population)."""
+    import torch
+    ew = args.emulate_world if world == 1 else 0
+    split = world if world > 1 else ew
+    if split <= 1:
+        return {"rule": "single rank", "world": 1}, S.Population(cfg, 1, 0)
+    t0 = time.time()
+    sizes = S.cluster_sizes(cfg).astype(np.int64)
+    w = None
+    if args.shard_weight == "bytes":
+        if world > 1:
+            part = S.cluster_bytes(cfg, world, rank, threads).astype(np.int64)
+            wt = torch.from_numpy(part).to(dev)
+            dist.all_reduce(wt)
+            w = wt.cpu().numpy().astype(np.uint64)
+        else:
+            key = "%d-%d-%d-%.4f" % (cfg.seed, cfg.n_pairs, cfg.n_clusters, cfg.mutate_frac)
+            cache = getattr(args, "weights_cache", "")
+            if cache and os.path.exists(cache) and os.path.exists(cache + ".key") and \
+                    open(cache + ".key").read() == key:
+                w = np.load(cache).astype(np.uint64)
+            else:
+                w = S.cluster_bytes(cfg, 1, 0, threads)
+                if cache:
+                    np.save(cache, w)
+                    with open(cache + ".key", "w") as f:
+                        f.write(key)
+    t_w = time.time() - t0
+    owner = G.shard_lpt(w if w is not None else sizes.astype(np.uint64), split)
+    # the rank loads on both measures, whichever rule packed them (bytes only when known)
+    load_p = np.bincount(owner, weights=sizes.astype(np.float64), minlength=split)
+    info = {"rule": "LPT by sum of B_pair" if w is not None else "LPT by pair count", "world": split,
+            "weights_s": round(t_w, 2), "max_over_mean_pairs": float(load_p.max() / load_p.mean())}
+    if w is not None:
+        load_b = np.bincount(owner, weights=w.astype(np.float64), minlength=split)
+        info.update(max_over_mean_bytes=float(load_b.max() / load_b.mean()), total_bytes=int(load_b.sum()),
+                    heaviest_rank=int(load_b.argmax()), heaviest_bytes=int(load_b.max()))
+        # the pair-count rule on the same weights, for comparison
+        oc = G.shard_lpt(sizes.astype(np.uint64), split)
+        lc = np.bincount(oc, weights=w.astype(np.float64), minlength=split)
+        info["pair_count_rule_max_over_mean_bytes"] = float(lc.max() / lc.mean())
+    if world > 1:
+        r = rank
+    else:
+        r = args.emulate_rank if args.emulate_rank >= 0 else int(
+            (np.bincount(owner, weights=w.astype(np.float64), minlength=split) if w is not None else load_p).argmax())
+        info["emulated_rank"] = r
+        info["note"] = "one GPU timing rank %d's share of a %d-way split (diagnostic, not the node-wide metric)" % (
+            r, split)
+    if w is not None:
+        info["rank_bytes"] = int(np.bincount(owner, weights=w.astype(np.float64), minlength=split)[r])
+    pop = S.Population(cfg, split, r, cluster_weight=w)
+    assert pop.n == int(load_p[r]), "synth LPT and gpudiff_shard_lpt disagree"
+    info["rank_pairs"] = pop.n
+    log("shard: %s" % json.dumps(info))
+    return info, pop
 
 
 def json_in_rates(G, pop, m, threads, device):

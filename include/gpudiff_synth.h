@@ -59,6 +59,8 @@ uint64_t gpudiff_synth_local_pairs(const gpudiff_synth* s);
 uint64_t gpudiff_synth_local_clusters(const gpudiff_synth* s);
 /* global pair index of local pair i */
 uint64_t gpudiff_synth_global_index(const gpudiff_synth* s, uint64_t i);
+/* the global pair index (= the encoded pair_id, u32) of every local pair, out[local_pairs] */
+int gpudiff_synth_local_ids(const gpudiff_synth* s, uint32_t* out);
 
 /* encodes local pairs [first, first+n) with `threads` host threads into
  * internal buffers; reports the pool bytes and leaves needed */

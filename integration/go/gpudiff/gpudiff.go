@@ -290,6 +290,15 @@ type Batcher struct {
 	ch       chan event
 	maxBatch int
 	window   time.Duration
+	avgBytes float64 // JSON bytes per event, running average: the next flush's jsonBuf size
+}
+
+func (b *Batcher) bytesHint(n int) int { return int(b.avgBytes*float64(n)*1.25) + 4096 }
+
+func (b *Batcher) noteBytes(total, n int) {
+	if n > 0 {
+		b.avgBytes = 0.75*b.avgBytes + 0.25*float64(total)/float64(n)
+	}
 }
 
 func NewBatcher(e *Engine, maxBatch int, window time.Duration) *Batcher {
@@ -310,6 +319,11 @@ func (b *Batcher) UpdateStored(slot uint32, oldObj, newObj interface{}, which Wh
 	b.ch <- event{oldObj, newObj, which, enqueue, int64(slot)}
 }
 
+// loop flushes when maxBatch events are pending or the window has passed since the last flush,
+// whichever comes first; events are decided and enqueued in arrival order.  Before the timer is
+// re-armed it is stopped and, if it had fired while a full batch was being flushed, its tick is
+// drained: Reset does not empty the channel, and a stale tick would flush the next batch at once,
+// shrinking batches exactly when the load is high (tests/goshim.py Batcher restates this loop).
 func (b *Batcher) loop() {
 	var pending []event
 	timer := time.NewTimer(b.window)
@@ -326,9 +340,91 @@ func (b *Batcher) loop() {
 			b.flush(pending)
 			pending = pending[:0]
 		}
+		if !timer.Stop() {
+			select {
+			case <-timer.C: // fired during the flush (or just received above: then empty)
+			default:
+			}
+		}
 		timer.Reset(b.window)
 	}
 }
+
+// jsonBuf holds one flush's objects as JSON in ONE C allocation: appendValue appends straight into
+// a slice whose backing array is the C memory, so each object is written once, where the engine
+// reads it (no jsonOf-then-C.CBytes copy and no allocation per object).  An object that would run
+// past the allocation makes append move the slice to the Go heap; add then grows the C buffer
+// (C.realloc) and copies that object's bytes over -- rare once capHint tracks the flush size.
+// Offsets are handed out, not pointers: the buffer may move until the last object is added.
+type jsonBuf struct {
+	p   unsafe.Pointer
+	n   int // capacity of the C allocation
+	buf []byte
+}
+
+// cslice views n bytes of C memory as a Go slice (Go 1.16, the reference's toolchain: no unsafe.Slice)
+func cslice(p unsafe.Pointer, n int) []byte { return (*[1 << 40]byte)(p)[:n:n] }
+
+func newJSONBuf(capHint int) *jsonBuf {
+	if capHint < 4096 {
+		capHint = 4096
+	}
+	p := C.malloc(C.size_t(capHint))
+	return &jsonBuf{p: p, n: capHint, buf: cslice(p, capHint)[:0]}
+}
+
+func (j *jsonBuf) grow(out []byte, start int) {
+	nn := 2 * cap(out)
+	np := C.realloc(j.p, C.size_t(nn)) // keeps [0, start): the objects already in C memory
+	dst := cslice(np, nn)
+	copy(dst[start:len(out)], out[start:])
+	j.p, j.n, j.buf = np, nn, dst[:len(out)]
+}
+
+// add renders obj (jsonOf's rules) at the end of the buffer: its offset and length, ok = false
+// for a non-transferable object (nothing added).
+func (j *jsonBuf) add(obj interface{}) (off, n int, ok bool) {
+	u, isU := obj.(*unstructured.Unstructured)
+	if !isU || u == nil {
+		return 0, 0, false
+	}
+	var m interface{} = u.Object
+	if u.Object == nil {
+		m = map[string]interface{}{}
+	}
+	start := len(j.buf)
+	out, ok := appendValue(j.buf, m, 0)
+	if !ok { // j.buf is unchanged: the partial object (in C memory or a Go copy) is dropped
+		return 0, 0, false
+	}
+	return start, len(out) - start, j.commit(out, start)
+}
+
+// raw appends literal bytes (the "{}" stand-in of a non-transferable object)
+func (j *jsonBuf) raw(b []byte) (off, n int) {
+	start := len(j.buf)
+	j.commit(append(j.buf, b...), start)
+	return start, len(b)
+}
+
+func (j *jsonBuf) commit(out []byte, start int) bool {
+	if cap(out) > 0 && unsafe.Pointer(&out[:1][0]) != j.p {
+		j.grow(out, start)
+	} else {
+		j.buf = out
+	}
+	return true
+}
+
+// at is the C pointer of the object at offset off (valid until the buffer is freed)
+func (j *jsonBuf) at(off, n int) (*C.uint8_t, C.size_t) {
+	if n == 0 {
+		return nil, 0
+	}
+	return (*C.uint8_t)(unsafe.Pointer(uintptr(j.p) + uintptr(off))), C.size_t(n)
+}
+
+func (j *jsonBuf) free() { C.free(j.p) }
 
 func (b *Batcher) flush(evs []event) {
 	if b.store != nil {
@@ -338,25 +434,33 @@ func (b *Batcher) flush(evs []event) {
 	n := len(evs)
 	pairs := (*[1 << 28]C.gpudiff_json_pair)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_json_pair{}))))[:n:n]
 	defer C.free(unsafe.Pointer(&pairs[0]))
+	jb := newJSONBuf(b.bytesHint(n))
+	defer jb.free()
 	bad := make([]bool, n)
+	offs := make([]int, 4*n) // old off, len, new off, len: pointers only once the buffer stops moving
 	for i, ev := range evs {
-		a, ok1 := jsonOf(ev.old)
-		c, ok2 := jsonOf(ev.new)
+		mark := len(jb.buf)
+		oa, la, ok1 := jb.add(ev.old)
+		var oc, lc int
+		ok2 := false
+		if ok1 {
+			oc, lc, ok2 = jb.add(ev.new)
+		}
 		if !ok1 || !ok2 {
 			bad[i] = true
-			a, c = []byte("{}"), []byte("{}")
+			jb.buf = jb.buf[:mark]
+			oa, la = jb.raw([]byte("{}"))
+			oc, lc = oa, la
 		}
-		pa, la := cmem(a)
-		pc, lc := cmem(c)
+		offs[4*i], offs[4*i+1], offs[4*i+2], offs[4*i+3] = oa, la, oc, lc
+	}
+	b.noteBytes(len(jb.buf), n)
+	for i := range evs {
+		pa, la := jb.at(offs[4*i], offs[4*i+1])
+		pc, lc := jb.at(offs[4*i+2], offs[4*i+3])
 		pairs[i] = C.gpudiff_json_pair{old_json: pa, old_len: la, new_json: pc, new_len: lc,
 			pair_id: C.uint32_t(i)}
 	}
-	defer func() {
-		for i := range pairs {
-			C.free(unsafe.Pointer(pairs[i].old_json))
-			C.free(unsafe.Pointer(pairs[i].new_json))
-		}
-	}()
 	b.e.mu.Lock()
 	var ticket C.gpudiff_ticket
 	rc := C.gpudiff_submit(b.e.ctx, &pairs[0], C.size_t(n), &ticket)
@@ -440,26 +544,28 @@ func (b *Batcher) flushStored(evs []event) {
 	}
 	ce := (*[1 << 27]C.gpudiff_event)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_event{}))))[:n:n]
 	defer C.free(unsafe.Pointer(&ce[0]))
+	jb := newJSONBuf(b.bytesHint(n))
+	defer jb.free()
 	ok := make([]bool, n)
+	offs := make([]int, 4*n) // new off, len, old off, len (len 0: absent)
 	for k, i := range good {
 		ev := evs[i]
-		ce[k] = C.gpudiff_event{slot: C.uint32_t(ev.slot), pair_id: C.uint32_t(k)}
-		if nb, okn := jsonOf(ev.new); okn {
-			ce[k].new_json, ce[k].new_len = cmem(nb)
+		if o, l, okn := jb.add(ev.new); okn {
+			offs[4*k], offs[4*k+1] = o, l
 			ok[k] = true
 		} else {
-			ce[k].new_json, ce[k].new_len = cmem([]byte("{"))  // undecodable: reported dirty, slot emptied
+			offs[4*k], offs[4*k+1] = jb.raw([]byte("{")) // undecodable: reported dirty, slot emptied
 		}
-		if ob, oko := jsonOf(ev.old); oko {
-			ce[k].old_json, ce[k].old_len = cmem(ob)
+		if o, l, oko := jb.add(ev.old); oko {
+			offs[4*k+2], offs[4*k+3] = o, l
 		}
 	}
-	defer func() {
-		for k := range ce {
-			C.free(unsafe.Pointer(ce[k].new_json))
-			C.free(unsafe.Pointer(ce[k].old_json))
-		}
-	}()
+	b.noteBytes(len(jb.buf), n)
+	for k, i := range good {
+		ce[k] = C.gpudiff_event{slot: C.uint32_t(evs[i].slot), pair_id: C.uint32_t(k)}
+		ce[k].new_json, ce[k].new_len = jb.at(offs[4*k], offs[4*k+1])
+		ce[k].old_json, ce[k].old_len = jb.at(offs[4*k+2], offs[4*k+3])
+	}
 	b.e.mu.Lock()
 	var ticket C.gpudiff_ticket
 	rc := C.gpudiff_store_submit(b.e.ctx, b.store.s, &ce[0], C.size_t(n), &ticket)

@@ -757,6 +757,12 @@ void gpudiff_synth_close(gpudiff_synth* s) { delete s; }
 uint64_t gpudiff_synth_local_pairs(const gpudiff_synth* s) { return s ? s->n_local : 0; }
 uint64_t gpudiff_synth_local_clusters(const gpudiff_synth* s) { return s ? s->local.size() : 0; }
 uint64_t gpudiff_synth_global_index(const gpudiff_synth* s, uint64_t i) { return s->spec_of(i).g; }
+int gpudiff_synth_local_ids(const gpudiff_synth* s, uint32_t* out) {
+    if (!s || !out) return -1;
+    for (const ClusterRange& r : s->local)
+        for (uint64_t k = 0; k < r.count; k++) out[r.lstart + k] = (uint32_t)(r.gstart + k);
+    return 0;
+}
 
 int gpudiff_synth_encode(gpudiff_synth* s, uint64_t first, uint64_t n, uint32_t threads, uint64_t* pool_bytes,
                          uint64_t* total_leaves) {

@@ -213,6 +213,8 @@ SIGNATURES = [
     ("gpudiff_dbatch_read_pool", C.c_int, [_P, _P, C.c_uint64, C.c_void_p, C.c_uint64]),
     ("gpudiff_dbatch_export", C.c_int, [_P, _P, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64]),
     ("gpudiff_dbatch_free", None, [_P, _P]),
+    ("gpudiff_cluster_bytes", C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p]),
+    ("gpudiff_shard_lpt", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     ("gpudiff_diff", C.c_int, [_P, _P, C.POINTER(C.c_uint64)]),
     ("gpudiff_wait", C.c_int, [_P, C.c_uint64, C.POINTER(Result)]),
     ("gpudiff_result_release", None, [_P, C.POINTER(Result)]),
@@ -325,6 +327,23 @@ def device_count() -> int:
     n = C.c_int(0)
     _chk(_lib.gpudiff_device_count(C.byref(n)), "gpudiff_device_count")
     return n.value
+
+
+def cluster_bytes(rows: np.ndarray, n_clusters: int) -> np.ndarray:
+    """Σ B_pair per logical cluster of encoded rows (ROW_DTYPE): the bytes K2 streams for each cluster's
+    pairs -- the shard weight of SURVEY.md §8(e) (gpudiff_cluster_bytes)."""
+    rows = np.ascontiguousarray(rows, dtype=ROW_DTYPE)
+    out = np.zeros(n_clusters, dtype=np.uint64)
+    _chk(_lib.gpudiff_cluster_bytes(rows.ctypes.data, rows.size, n_clusters, out.ctypes.data), "gpudiff_cluster_bytes")
+    return out
+
+
+def shard_lpt(weights, world: int) -> np.ndarray:
+    """Owner rank per cluster: greedy LPT by weight (gpudiff_shard_lpt; shard.lpt_assign restates it)."""
+    w = np.ascontiguousarray(weights, dtype=np.uint64)
+    owner = np.zeros(w.size, dtype=np.int32)
+    _chk(_lib.gpudiff_shard_lpt(w.ctypes.data, w.size, world, owner.ctypes.data), "gpudiff_shard_lpt")
+    return owner
 
 
 def to_json_bytes(obj: Union[bytes, bytearray, str, dict]) -> bytes:
@@ -529,6 +548,13 @@ class Engine:
     def __init__(self, device: int = DEVICE_CURRENT, encode_threads: int = 0, stream: Optional[int] = None,
                  timing: bool = False, path_hash_bits: int = PATH_HASH_BITS, flags: int = 0,
                  device_encode: bool = False):
+        if stream is not None and not stream:
+            # 0 is HIP's null stream, which the engine cannot share: gpudiff_open reads NULL as "create your
+            # own (non-blocking) stream", and a non-blocking stream never orders against the null stream --
+            # the caller's copies / collectives would race the engine's exports.  Share a real stream:
+            # s = torch.cuda.Stream(dev); torch.cuda.set_stream(s); Engine(..., stream=s.cuda_stream)
+            raise ValueError("Engine(stream=0): the null stream cannot be shared; make a torch.cuda.Stream current "
+                             "and pass its cuda_stream")
         o = Opts(device=device, encode_threads=encode_threads, stream=stream or None,
                  flags=(OPT_TIMING if timing else 0) | (OPT_DEVICE_ENCODE if device_encode else 0) | flags,
                  path_hash_bits=path_hash_bits)

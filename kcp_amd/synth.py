@@ -26,6 +26,10 @@ class SynthCfg(C.Structure):
 _P = C.c_void_p
 _SIGS = [
     ("gpudiff_synth_open", C.c_int, [C.POINTER(SynthCfg), C.c_int, C.c_int, C.POINTER(_P)]),
+    ("gpudiff_synth_open_ex", C.c_int, [C.POINTER(SynthCfg), C.c_int, C.c_int, C.c_void_p, C.POINTER(_P)]),
+    ("gpudiff_synth_cluster_sizes", C.c_int, [C.POINTER(SynthCfg), C.c_void_p]),
+    ("gpudiff_synth_cluster_bytes", C.c_int, [C.POINTER(SynthCfg), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+    ("gpudiff_synth_local_ids", C.c_int, [_P, C.c_void_p]),
     ("gpudiff_synth_close", None, [_P]),
     ("gpudiff_synth_local_pairs", C.c_uint64, [_P]),
     ("gpudiff_synth_local_clusters", C.c_uint64, [_P]),
@@ -73,12 +77,36 @@ class Chunk:
     leaves: int
 
 
-class Population:
-    """One rank's shard (LPT by logical cluster) of a synthetic population."""
+def cluster_sizes(cfg: SynthCfg) -> np.ndarray:
+    """Pairs per logical cluster of the population (u64 [n_clusters])."""
+    out = np.zeros(cfg.n_clusters, dtype=np.uint64)
+    if _lib.gpudiff_synth_cluster_sizes(C.byref(cfg), out.ctypes.data) != 0:
+        raise RuntimeError("gpudiff_synth_cluster_sizes failed")
+    return out
 
-    def __init__(self, cfg: SynthCfg, world: int = 1, rank: int = 0):
+
+def cluster_bytes(cfg: SynthCfg, stride: int = 1, offset: int = 0, threads: int = 16) -> np.ndarray:
+    """Exact Σ B_pair per logical cluster (u64 [n_clusters]) for the clusters c % stride == offset (zeros
+    elsewhere): their pairs are encoded on the host and gpudiff_pair_compare_bytes summed by cluster.
+    Ranks split the work (stride = world, offset = rank) and sum the vectors."""
+    out = np.zeros(cfg.n_clusters, dtype=np.uint64)
+    if _lib.gpudiff_synth_cluster_bytes(C.byref(cfg), stride, offset, threads, out.ctypes.data) != 0:
+        raise RuntimeError("gpudiff_synth_cluster_bytes failed")
+    return out
+
+
+class Population:
+    """One rank's shard (LPT by logical cluster) of a synthetic population: clusters packed by
+    `cluster_weight` (Σ B_pair, `cluster_bytes`) or, if None, by pair count."""
+
+    def __init__(self, cfg: SynthCfg, world: int = 1, rank: int = 0, cluster_weight=None):
         h = C.c_void_p()
-        rc = _lib.gpudiff_synth_open(C.byref(cfg), world, rank, C.byref(h))
+        wt = None
+        if cluster_weight is not None:
+            wt = np.ascontiguousarray(cluster_weight, dtype=np.uint64)
+            assert wt.size == cfg.n_clusters
+        rc = _lib.gpudiff_synth_open_ex(C.byref(cfg), world, rank, None if wt is None else wt.ctypes.data,
+                                        C.byref(h))
         if rc != 0:
             raise RuntimeError("gpudiff_synth_open failed (%d)" % rc)
         self.h = h
@@ -96,6 +124,13 @@ class Population:
             self.close()
         except Exception:
             pass
+
+    def local_ids(self) -> np.ndarray:
+        """Global pair index (= the pair_id the encoder writes) of every local pair, u32 [n]."""
+        out = np.zeros(max(self.n, 1), dtype=np.uint32)
+        if _lib.gpudiff_synth_local_ids(self.h, out.ctypes.data) != 0:
+            raise RuntimeError("gpudiff_synth_local_ids failed")
+        return out[:self.n]
 
     def global_index(self, i: int) -> int:
         return int(_lib.gpudiff_synth_global_index(self.h, i))

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import decimal
 import math
-from typing import Any, Optional
+from typing import Any, List, Optional, Tuple
 
 from oracle import gpudiff_oracle as O
 from oracle.upsert_oracle import go_marshal
@@ -165,3 +165,109 @@ def shim_pair(a_json: bytes, b_json: bytes):
     if ja is None or jb is None:
         return None
     return ja, jb
+
+
+# ---------------------------------------------------------------- Batcher (gpudiff.go Batcher.loop / flush)
+SPEC_DIRTY, STATUS_DIRTY = 0x1, 0x2  # GPUDIFF_SPEC_DIRTY / GPUDIFF_STATUS_DIRTY: the Which of an event
+
+
+class JsonBuf:
+    """gpudiff.go jsonBuf: every object of one flush rendered into ONE buffer (the Go side's C
+    allocation); objects are addressed by (offset, length), pointers are taken only after the last
+    add (the buffer may move while it grows)."""
+
+    def __init__(self):
+        self.buf = bytearray()
+
+    def add(self, tree) -> Optional[Tuple[int, int]]:
+        if tree is None:  # not an *unstructured.Unstructured: nothing added
+            return None
+        j = shim_json(tree)
+        if j is None:  # not transferable: the partial object is dropped
+            return None
+        off = len(self.buf)
+        self.buf += j
+        return off, len(j)
+
+    def raw(self, b: bytes) -> Tuple[int, int]:
+        off = len(self.buf)
+        self.buf += b
+        return off, len(b)
+
+    def mark(self) -> int:
+        return len(self.buf)
+
+    def truncate(self, m: int):
+        del self.buf[m:]
+
+
+class Batcher:
+    """Restatement of gpudiff.go's Batcher over a simulated clock: events arrive as
+    (t, old_json, new_json, which, name); a flush happens when maxBatch events are pending or `window`
+    has passed since the timer was last armed.  The timer is re-armed after every loop turn; the Go
+    code stops and drains it first, so a tick that fired while a full batch was being flushed does NOT
+    flush the next (small) batch at once.  `drain=False` models the old code (Reset without draining).
+    decide(pairs) -> flags per pair (the engine: gpudiff_submit + gpudiff_wait; the oracle in CPU
+    tests).  Dirty events are enqueued in arrival order; a pair the shim cannot transfer is enqueued
+    without asking the engine (specsyncer.go:20-22)."""
+
+    def __init__(self, decide, max_batch: int, window: float, flush_cost: float = 0.0, drain: bool = True):
+        self.decide, self.max_batch, self.window = decide, max_batch, window
+        self.flush_cost, self.drain = flush_cost, drain
+        self.enqueued: List[str] = []
+        self.flushes: List[int] = []
+        self.buffers: List[bytes] = []
+
+    def flush(self, evs):
+        jb = JsonBuf()
+        bad, offs = [], []
+        for (_t, a, b, _which, _name) in evs:
+            m = jb.mark()
+            oa = jb.add(informer_object(a))
+            ob = jb.add(informer_object(b)) if oa is not None else None
+            if oa is None or ob is None:
+                jb.truncate(m)
+                oa = ob = jb.raw(b"{}")
+                bad.append(True)
+            else:
+                bad.append(False)
+            offs.append((oa, ob))
+        buf = bytes(jb.buf)
+        self.buffers.append(buf)
+        pairs = [(buf[oa[0]:oa[0] + oa[1]], buf[ob[0]:ob[0] + ob[1]]) for oa, ob in offs]
+        flags = self.decide(pairs)
+        for (ev, f, bd) in zip(evs, flags, bad):
+            if bd or (f & ev[3]):
+                self.enqueued.append(ev[4])
+        self.flushes.append(len(evs))
+
+    def run(self, events):
+        """events sorted by arrival time; returns the enqueued names in order."""
+        pending = []
+        now = 0.0
+        deadline = self.window  # timer armed at 0
+        stale_tick = False      # a fired tick left in the channel (the old Reset-without-drain code)
+        i = 0
+        while i < len(events) or pending:
+            nxt = events[i][0] if i < len(events) else float("inf")
+            if stale_tick:  # the channel already holds a tick: the select takes it at once
+                stale_tick = False
+                fire = True
+            elif nxt <= deadline:
+                now = max(now, nxt)
+                pending.append(events[i])
+                i += 1
+                if len(pending) < self.max_batch:
+                    continue
+                fire = False
+            else:
+                now = max(now, deadline)
+                fire = True
+            if pending:
+                self.flush(pending)
+                pending = []
+            now += self.flush_cost
+            if not fire and now >= deadline and not self.drain:
+                stale_tick = True  # the timer fired during the flush and Reset does not drain it
+            deadline = now + self.window
+        return self.enqueued

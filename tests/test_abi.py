@@ -54,6 +54,15 @@ def test_binding_abi_matches_header():
     assert "gpudiff_abi_version" in inspect.getsource(G._load)
 
 
+def test_engine_refuses_the_null_stream():
+    """stream=0 would silently give the engine its own non-blocking stream, which never orders against
+    the caller's null-stream copies and collectives (the r04 gloo rehearsal read exports before they
+    landed): refused."""
+    from kcp_amd import gpudiff as G
+    with pytest.raises(ValueError):
+        G.Engine(device=G.DEVICE_NONE, stream=0)
+
+
 def test_header_compiles_as_c():
     import subprocess
     import tempfile

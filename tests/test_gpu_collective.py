@@ -32,7 +32,8 @@ def test_dirty_gather_over_rccl_world1():
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1,
                             device_id=dev)
     try:
-        stream = torch.cuda.current_stream(dev)
+        stream = torch.cuda.Stream(device=dev)  # shared with the engine and current: exports, copies and the
+        torch.cuda.set_stream(stream)            # collectives order on one stream (the null stream cannot be shared)
         eng = G.Engine(device=0, stream=stream.cuda_stream)
         pairs, _, _ = make_pairs(3000, seed=21, mutate_frac=0.3, pretty_frac=0)
         hb = eng.encode(pairs)
@@ -83,4 +84,5 @@ def test_dirty_gather_over_rccl_world1():
         hb.free()
         eng.close()
     finally:
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
         dist.destroy_process_group()

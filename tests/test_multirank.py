@@ -247,3 +247,120 @@ def test_dirty_gather_fixed_capacity_gloo_world2(shrink, depth):
             # depth 1: a capacity below a rank's count is regrown inside the step, the sets stay exact
             assert ok and s == want_s and t == want_t
             assert regrows == (1 if shrink else 0)
+
+
+# ---------------------------------------------------------------- byte-weighted sharding
+def _pair_compare_bytes_py(r):
+    """Restatement of gpudiff_format.h gpudiff_pair_compare_bytes for one ROW_DTYPE record."""
+    from kcp_amd import gpudiff as G
+    b = 65
+    if (int(r["flags_a"]) | int(r["flags_b"])) & G.OBJ_DECODE_ERR:
+        return b
+    seg = lambda l, ar: 16 * int(l) + int(ar)  # noqa: E731
+    spec_sz = r["spec_l_a"] == r["spec_l_b"] and r["spec_ar_a"] == r["spec_ar_b"]
+    stat_sz = bool(int(r["flags_b"]) & G.OBJ_HAS_STATUS) and r["stat_l_a"] == r["stat_l_b"] and \
+        r["stat_ar_a"] == r["stat_ar_b"]
+    ss, st = seg(r["spec_l_a"], r["spec_ar_a"]), seg(r["stat_l_a"], r["stat_ar_a"])
+    up = lambda x: (x + 127) & ~127  # noqa: E731
+    if spec_sz and stat_sz:
+        per = up(ss + st)
+    elif spec_sz:
+        per = ss if (int(r["stat_l_a"]) | int(r["stat_l_b"]) | int(r["stat_ar_a"]) | int(r["stat_ar_b"])) else up(ss)
+    elif stat_sz:
+        per = st
+    else:
+        per = 0
+    return b + 2 * per
+
+
+def test_shard_lpt_c_equals_restatement():
+    from kcp_amd import gpudiff as G
+    rnd = np.random.default_rng(5)
+    for world in (1, 2, 3, 8, 16):
+        for w in (rnd.integers(0, 1 << 40, 3000), rnd.integers(0, 5, 500), np.zeros(7, np.int64)):
+            assert np.array_equal(G.shard_lpt(w.astype(np.uint64), world), shard.lpt_assign(w, world))
+    with pytest.raises(G.GpuDiffError):
+        G.shard_lpt(np.ones(3, np.uint64), 0)
+
+
+def test_cluster_bytes_equal_row_formula():
+    """gpudiff_cluster_bytes sums gpudiff_pair_compare_bytes by cluster; held to a Python restatement over
+    encoded synthetic rows of every kind (and the engine's own compare_bytes total)."""
+    from kcp_amd import gpudiff as G
+    e = G.Engine(device=G.DEVICE_NONE)
+    for name in ("config3", "config4"):
+        cfg = S.make_cfg(name, n_pairs=3000, n_clusters=40)
+        p = S.Population(cfg)
+        ch = p.chunk(e, 0, p.n, 4)
+        rows = ch.hb.rows()
+        got = G.cluster_bytes(rows, cfg.n_clusters)
+        want = np.zeros(cfg.n_clusters, np.uint64)
+        for r in rows:
+            want[int(r["cluster_id"])] += _pair_compare_bytes_py(r)
+        assert np.array_equal(got, want)
+        # the synth's per-cluster weights are the same sums
+        assert np.array_equal(S.cluster_bytes(cfg, threads=4), want)
+        with pytest.raises(G.GpuDiffError):
+            G.cluster_bytes(rows, 1)  # cluster ids past n_clusters
+        ch.hb.free()
+        p.close()
+    e.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_byte_weighted_shards_partition_and_balance(world):
+    """Ranks packed by Σ B_pair: every pair exactly once, whole clusters, the same owner as gpudiff_shard_lpt,
+    and byte loads at least as balanced as the pair-count rule's."""
+    from kcp_amd import gpudiff as G
+    cfg = S.make_cfg("config3", n_pairs=60000, n_clusters=600)
+    w = S.cluster_bytes(cfg, threads=4)
+    sizes = S.cluster_sizes(cfg)
+    owner = G.shard_lpt(w, world)
+    seen = []
+    for r in range(world):
+        p = S.Population(cfg, world, r, cluster_weight=w)
+        assert p.n == int(sizes[owner == r].sum())
+        seen.append(p.local_ids().astype(np.int64))
+        p.close()
+    allg = np.concatenate(seen)
+    assert allg.size == cfg.n_pairs and np.unique(allg).size == cfg.n_pairs
+    lb = np.bincount(owner, weights=w.astype(float), minlength=world)
+    lc = np.bincount(shard.lpt_assign(sizes, world), weights=w.astype(float), minlength=world)
+    assert lb.max() <= lc.max() and lb.max() / lb.mean() < 1.01
+
+
+def _weights_worker(rank, world, port, q):
+    """bench.py's shard_population at world 2 over gloo: the stride-split weight computation summed by an
+    all-reduce equals one rank computing every cluster."""
+    import argparse
+    import bench
+    from kcp_amd import gpudiff as G
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = S.make_cfg("config3", n_pairs=20000, n_clusters=300)
+    args = argparse.Namespace(emulate_world=0, emulate_rank=-1, shard_weight="bytes")
+    info, pop = bench.shard_population(args, cfg, world, rank, 2, torch.device("cpu"), dist, G, S)
+    q.put((rank, info, pop.local_ids().tolist()))
+    dist.destroy_process_group()
+
+
+def test_bench_shard_population_gloo_world2():
+    from kcp_amd import gpudiff as G
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_weights_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    cfg = S.make_cfg("config3", n_pairs=20000, n_clusters=300)
+    w = S.cluster_bytes(cfg, threads=4)
+    owner = G.shard_lpt(w, world)
+    sizes = S.cluster_sizes(cfg)
+    for r, info, ids in out:
+        assert info["rule"] == "LPT by sum of B_pair" and info["rank_pairs"] == int(sizes[owner == r].sum())
+        assert info["total_bytes"] == int(w.sum())
+    assert sorted(sum((o[2] for o in out), [])) == list(range(cfg.n_pairs))

@@ -36,7 +36,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(device=dev)  # the engine's stream, made torch's current one: exports,
+    torch.cuda.set_stream(stream)            # copies and collectives all order on it (never the null stream)
     cfg = S.make_cfg(args.config, n_pairs=args.pairs, n_clusters=max(1, args.pairs // 100))
     pop = S.Population(cfg, 1, 0)
     n = pop.n
