@@ -242,7 +242,9 @@ class Batcher:
         self.flushes.append(len(evs))
 
     def run(self, events):
-        """events sorted by arrival time; returns the enqueued names in order."""
+        """events sorted by arrival time; returns the enqueued names in order.  Events that arrived while
+        a flush ran wait in the channel (the Go side's buffered chan); when both a queued event and a
+        fired tick are ready, Go's select picks at random -- modeled as: one event, then the tick."""
         pending = []
         now = 0.0
         deadline = self.window  # timer armed at 0
@@ -250,8 +252,11 @@ class Batcher:
         i = 0
         while i < len(events) or pending:
             nxt = events[i][0] if i < len(events) else float("inf")
-            if stale_tick:  # the channel already holds a tick: the select takes it at once
+            if stale_tick:
                 stale_tick = False
+                if nxt <= now:
+                    pending.append(events[i])
+                    i += 1
                 fire = True
             elif nxt <= deadline:
                 now = max(now, nxt)

@@ -15,6 +15,7 @@ from hypothesis import given, settings, strategies as st
 from kcp_amd import gpudiff as G
 from oracle import gpudiff_oracle as O
 from tests import goshim as S
+from tests import goshim as gs
 from tests.golden import fixtures as F
 from tests.golden.kat_cases import cases
 
@@ -144,3 +145,66 @@ def test_round_trip_keeps_go_types(obj):
         return  # lone surrogates: not a Go string (covered above)
     assert txt is not None
     assert _same_typed(O.go_json_decode(txt), obj)
+
+
+# ---------------------------------------------------------------- the Batcher (gpudiff.go loop / flush)
+def _oracle_decide(pairs):
+    from tests.parity import expected_flags
+    return [expected_flags(O.diff_pair(a, b)) for a, b in pairs]
+
+
+def _event_stream(n, seed=3, dt=0.1):
+    """n Update events of mixed kinds: spec-gated (upstream informer) and status-gated (downstream),
+    some dirty for their predicate, some dirty only for the other one, some non-transferable."""
+    import random
+    from tests.workload import make_pairs
+    rnd = random.Random(seed)
+    pairs, _, _ = make_pairs(n, seed=seed, mutate_frac=0.5, pretty_frac=0)
+    evs = []
+    for i, (a, b) in enumerate(pairs):
+        which = gs.SPEC_DIRTY if rnd.random() < 0.5 else gs.STATUS_DIRTY
+        if i % 37 == 5:
+            b = b"[1, 2]"  # not an object: the informer never delivers an Unstructured -> enqueued
+        evs.append((i * dt, a, b, which, "ev%04d" % i))
+    return evs
+
+
+def test_batcher_enqueues_dirty_events_in_arrival_order():
+    """Mixed spec / status events over several flushes (by size and by window): exactly the events dirty
+    for THEIR predicate (or not transferable) are enqueued, in arrival order; all objects of a flush sit
+    in one buffer, addressed by offset (gpudiff.go jsonBuf)."""
+    evs = _event_stream(300)
+    # a dense first half (flushed by size), a sparse second half (flushed by the window)
+    evs = [((e[0] if i < 150 else 15.0 + (i - 150) * 0.4),) + e[1:] for i, e in enumerate(evs)]
+    bt = gs.Batcher(_oracle_decide, max_batch=20, window=2.5)
+    got = bt.run(evs)
+    want = []
+    for (_t, a, b, which, name) in evs:
+        pr = gs.shim_pair(a, b)
+        if pr is None:
+            want.append(name)
+            continue
+        r = O.diff_pair(*pr)
+        f = (gs.SPEC_DIRTY if r["spec_dirty"] else 0) | (gs.STATUS_DIRTY if r["status_dirty"] else 0)
+        if f & which:
+            want.append(name)
+    assert got == want and len(want) > 50
+    assert sum(bt.flushes) == len(evs) and max(bt.flushes) == 20 and min(bt.flushes) < 10
+    assert len(bt.buffers) == len(bt.flushes)
+    # spec-gated events dirty only in status (and vice versa) are NOT enqueued
+    only_other = [e[4] for e in evs if gs.shim_pair(e[1], e[2]) is not None and e[4] not in want]
+    assert only_other
+
+
+def test_batcher_timer_drain_keeps_batches_full():
+    """A burst: events every 0.1, maxBatch 16, window 1.0, each flush 1.5 (longer than the window, so the
+    timer fires while a full batch is flushed).  With the stopped-and-drained timer every flush but the
+    last holds maxBatch events; the old Reset-without-drain loop answers the stale tick at once and
+    flushes 1-2 events -- decisions and enqueue order are the same either way."""
+    evs = _event_stream(200, seed=4, dt=0.1)
+    new = gs.Batcher(_oracle_decide, max_batch=16, window=1.0, flush_cost=1.5, drain=True)
+    old = gs.Batcher(_oracle_decide, max_batch=16, window=1.0, flush_cost=1.5, drain=False)
+    a, b = new.run(evs), old.run(evs)
+    assert a == b
+    assert all(f == 16 for f in new.flushes[1:-1]) and len(new.flushes) > 5  # the first: the window
+    assert min(old.flushes) <= 2 and len(old.flushes) > len(new.flushes)
