@@ -163,6 +163,10 @@ def main():
     ap.add_argument("--gather-depth", type=int, default=1,
                     help="N > 1: all-gathers in flight; 2 = pipelined (step s's collective overlaps step s+1's "
                          "diff; measured 2.4%% slower than serial at world size 1 on MI355X, profiles/r02zd)")
+    ap.add_argument("--no-gather-lookahead", action="store_true",
+                    help="N > 1 (RCCL, depth 1): read each step's gathered counts before enqueueing the next pass "
+                         "(the default checks step s after step s + 1 is queued, regrowing from the engine's "
+                         "alternate result slot, so the GPU never waits for the host between steps)")
     ap.add_argument("--gather-world1", action="store_true",
                     help="run the per-step RCCL collective even at world size 1 (exercises/measures it on one GPU)")
     ap.add_argument("--engine-flags", type=lambda x: int(x, 0), default=0,
@@ -371,7 +375,12 @@ def main():
         export_to(counts, G.EXPORT_COUNTS, 8)
         torch.cuda.synchronize()
         cap_s, cap_t = shard.DirtyGather.agree_capacity(counts, world, dist)
-        gather = shard.DirtyGather(world, cap_s, cap_t, comm_dev, dist, depth=args.gather_depth)
+        # RCCL: the engine's compaction writes each step's counts and IDs straight into the send buffer
+        # (gpudiff_dbatch_bind_gather) -- no export copies per step; gloo's host tensors are filled by copies
+        bind = None if gloo else (lambda send, cs, ct: db.bind_gather(send.data_ptr(), cs, ct))
+        slot = None if (gloo or args.no_gather_lookahead or args.gather_depth != 1) else (lambda k: db.result_slot(k))
+        gather = shard.DirtyGather(world, cap_s, cap_t, comm_dev, dist, depth=args.gather_depth, bind=bind,
+                                   slot=slot)
         log("collective: %s, capacities agreed (%d spec, %d status IDs per rank), depth %d"
             % (args.dist_backend, cap_s, cap_t, args.gather_depth))
 
@@ -380,6 +389,9 @@ def main():
 
         def fill_ids(col, buf):
             export_to(buf, G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.numel())
+        if bind is not None or slot is not None:
+            gather.begin_step()
+            eng.diff(db)
         gather.step(fill_counts, fill_ids)  # warm the communicator
         gather.finish()
         torch.cuda.synchronize()
@@ -391,6 +403,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if gather is not None and (gather.bind is not None or gather.slot is not None):
+            gather.begin_step()
         eng.diff(db)
         if gather is not None:
             gather.step(fill_counts, fill_ids)
@@ -409,7 +423,8 @@ def main():
         gather_check = dict(capacity_ok=ok, node_spec_dirty=int(cc[:, 0].sum()), node_status_dirty=int(cc[:, 1].sum()),
                             gathered_spec=None if sa is None else int(sa.numel()),
                             gathered_status=None if ta is None else int(ta.numel()),
-                            depth=gather.depth, bytes_per_rank=4 * gather.width, regrows=gather.n_regrows)
+                            depth=gather.depth, bytes_per_rank=4 * gather.width, regrows=gather.n_regrows,
+                            engine_writes_send_buffer=gather.bind is not None, lookahead=gather.slot is not None)
         t = torch.tensor([dt], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())

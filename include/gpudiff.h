@@ -245,6 +245,20 @@ int gpudiff_dbatch_device_view(const gpudiff_dbatch* db, gpudiff_device_view* v)
 #define GPUDIFF_EXPORT_FLAGS 4u       /* u8 per pair */
 int gpudiff_dbatch_export(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint32_t what, void* dst_device,
                           uint64_t max_elems, uint64_t known_count);
+/* Gather binding: while bound, every diff of this batch also writes -- from its K3 compaction, no extra
+ * launch or copy -- the buffer a per-step all-gather sends (kcp_amd/shard.py DirtyGather): u32
+ * [8 counts | cap_spec spec-dirty IDs | cap_status status-dirty IDs], counts = (n_spec, n_status, n_dirty,
+ * K4 scratch entries, 0, 0, 0, 0).  The counts are the batch totals even past a capacity; IDs past it are
+ * not written (the caller grows its buffers and exports them with gpudiff_dbatch_export, whose lists are
+ * always complete).  Words 4..7 are zeroed here, on the context stream.  send_dev = NULL unbinds. */
+int gpudiff_dbatch_bind_gather(gpudiff_ctx* ctx, gpudiff_dbatch* db, void* send_dev, uint32_t cap_spec,
+                               uint32_t cap_status);
+/* Result slots: the spec / status dirty-ID lists come in two slots (0 by default; slot 1 allocated on first
+ * use).  Later diffs write, and exports / gpudiff_wait read, the selected slot; the other keeps the lists
+ * of the last diff made under it.  A per-step collective that checks step s's gathered counts only after
+ * step s + 1's diff is enqueued alternates slots by step, so a capacity regrow can still export step s's
+ * complete lists (kcp_amd/shard.py DirtyGather, lookahead).  Host-only state: ordered like every call. */
+int gpudiff_dbatch_result_slot(gpudiff_ctx* ctx, gpudiff_dbatch* db, uint32_t slot);
 /* synchronous D2H copy of resident pool bytes (inspection / tests) */
 int gpudiff_dbatch_read_pool(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint64_t off, void* dst,
                              uint64_t bytes);

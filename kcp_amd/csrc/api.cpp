@@ -120,6 +120,9 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     }
     b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
     b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
+    b.gather_send = d->gather_send;
+    b.gather_cap_spec = d->gather_cap_spec;
+    b.gather_cap_status = d->gather_cap_status;
     b.avg_pair_bytes = d->n_pairs ? (d->compare_bytes ? d->compare_bytes : d->size_hint_bytes) / d->n_pairs : 0;
     return b;
 }
@@ -493,6 +496,33 @@ int gpudiff_dbatch_export(gpudiff_ctx* c, const gpudiff_dbatch* d, uint32_t what
     }
     if (what != GPUDIFF_EXPORT_COUNTS && n > d->n_pairs) n = d->n_pairs;
     if (n) HIPCHK(hipMemcpyAsync(dst, src, n * esz, hipMemcpyDeviceToDevice, c->stream));
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_bind_gather(gpudiff_ctx* c, gpudiff_dbatch* d, void* send_dev, uint32_t cap_spec,
+                               uint32_t cap_status) {
+    if (!c || !d) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    d->gather_send = (uint32_t*)send_dev;
+    d->gather_cap_spec = send_dev ? cap_spec : 0;
+    d->gather_cap_status = send_dev ? cap_status : 0;
+    if (send_dev) HIPCHK(hipMemsetAsync((uint32_t*)send_dev + 4, 0, 4 * sizeof(uint32_t), c->stream));
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_result_slot(gpudiff_ctx* c, gpudiff_dbatch* d, uint32_t slot) {
+    if (!c || !d || slot > 1) return GPUDIFF_E_INVAL;
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (slot == d->res_slot) return GPUDIFF_OK;
+    if (!d->ids_alt[0]) {
+        const uint64_t np = std::max<uint64_t>(d->max_pairs, 1);
+        if ((rc = dalloc(&d->ids_alt[0], np)) || (rc = dalloc(&d->ids_alt[1], np))) return rc;
+    }
+    std::swap(d->spec_ids, d->ids_alt[0]);
+    std::swap(d->status_ids, d->ids_alt[1]);
+    d->res_slot = slot;
     return GPUDIFF_OK;
 }
 

@@ -56,6 +56,8 @@ struct DiffBuffers {
     uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
     uint64_t avg_pair_bytes;    // format bytes K2 reads per pair, averaged over the batch (0: unknown)
     uint32_t k4_pipelined;      // tuning (GPUDIFF_OPT_K4_PIPELINED_JOIN): K4's slices with join_region_pl
+    uint32_t* gather_send;      // gpudiff_dbatch_bind_gather: K3 also writes counts + IDs here (nullptr: unbound)
+    uint32_t gather_cap_spec, gather_cap_status;
     uint32_t k2_deep_mode;      // tuning (GPUDIFF_OPT_K2_DEEP_SHIFT): 0 defer joins over 2048 keys to K4's
                                 // slices, 1 keep every join in K2, 2 / 3 defer over 4096 / 8192
 };

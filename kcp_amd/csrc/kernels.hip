@@ -244,13 +244,22 @@ __global__ __launch_bounds__(256) void k_scan_tiles(const V* __restrict__ in, co
     if (threadIdx.x == 0) tile_sums[blockIdx.x] = vadd(vadd(red[0], red[1]), vadd(red[2], red[3]));
 }
 
+__device__ __forceinline__ void mirror_store(uint32_t* m, const V4& v) {
+    m[0] = v.x;
+    m[1] = v.y;
+    m[2] = v.z;
+    m[3] = v.w;
+}
+__device__ __forceinline__ void mirror_store(uint32_t* m, uint32_t v) { m[0] = v; }
+
 // out[i] = *base_in (nullptr = 0) + exclusive prefix of in (out may alias in).  The workgroup holding the
 // last element (workgroup 0 when n == 0) writes *total = base + sum -- total must not alias base_in -- and,
-// if write_terminal, out[n] = the same.  Launch at least (n ? (n - 1) / SCAN_TILE + 1 : 1) workgroups.
+// if write_terminal, out[n] = the same, and, if mirror, the total's words there too (the bound gather
+// buffer's counts).  Launch at least (n ? (n - 1) / SCAN_TILE + 1 : 1) workgroups.
 template <class V>
 __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t* __restrict__ n_dev, uint32_t n_host,
                                                     const V* __restrict__ tile_sums, const V* base_in, V* total,
-                                                    V* out, bool write_terminal) {
+                                                    V* out, bool write_terminal, uint32_t* __restrict__ mirror) {
     __shared__ V wsum[4];
     __shared__ V wpre[4];
     const uint32_t n = scan_n(n_dev, n_host);
@@ -287,6 +296,7 @@ __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t*
     if (blockIdx.x == last && t == 255) {  // run = base + every element of the tile (zero past n)
         *total = run;
         if (write_terminal) out[n] = run;
+        if (mirror) mirror_store(mirror, run);
     }
 }
 
@@ -675,7 +685,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                                                  uint8_t* __restrict__ noop_d, uint32_t* __restrict__ slot_owner,
                                                  uint64_t scratch_cap, const gpudiff_pair_row* __restrict__ rows,
                                                  const uint8_t* __restrict__ pool, uint64_t mask,
-                                                 uint64_t* __restrict__ sh, uint8_t* __restrict__ sk) {
+                                                 uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
+                                                 uint32_t* __restrict__ gsend, uint32_t gcap_s, uint32_t gcap_t) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -691,8 +702,18 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
         const uint32_t id = dirty ? pair_ids[p] : 0u;
         const uint32_t cap = dirty ? caps[p] : 0u;
         const uint32_t cincl = wave_incl_scan(cap);
-        if (f & F_SPEC) spec_ids[base.x + popc64(bs & lt)] = id;
-        if (f & F_STATUS) status_ids[base.y + popc64(bt & lt)] = id;
+        // the dirty lists, and (gpudiff_dbatch_bind_gather) the same IDs straight into the collective's send
+        // buffer [8 counts | gcap_s spec IDs | gcap_t status IDs]: no export copies per step
+        if (f & F_SPEC) {
+            const uint32_t q = base.x + popc64(bs & lt);
+            spec_ids[q] = id;
+            if (gsend && q < gcap_s) gsend[8u + q] = id;
+        }
+        if (f & F_STATUS) {
+            const uint32_t q = base.y + popc64(bt & lt);
+            status_ids[q] = id;
+            if (gsend && q < gcap_t) gsend[8u + gcap_s + q] = id;
+        }
         uint32_t d = 0, so = 0;
         bool whole = false;
         if (dirty) {
@@ -1735,12 +1756,15 @@ hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     V4* cc = (V4*)b.chunk_counts + c0;
     V4* ts = (V4*)b.tile_sums;
     if (ntiles) k_scan_tiles<V4><<<ntiles, 256, 0, s>>>(cc, nullptr, n, ts);
+    // the bound gather buffer's counts: the batch totals, written with the last segment's (the total's) scan
+    uint32_t* mirror = (b.gather_send && (const void*)after == (const void*)b.summary) ? b.gather_send : nullptr;
     k_scan_apply<V4><<<std::max(ntiles, 1u), 256, 0, s>>>(cc, nullptr, n, ts, (const V4*)before, (V4*)after, cc,
-                                                          false);
+                                                          false, mirror);
     k_compact<<<grid_for(n, compact_cap_blocks()), 256, 0, s>>>(
         b.flags, b.caps, b.pair_ids, b.n_pairs, (const uint4*)b.chunk_counts, b.spec_ids, b.status_ids, b.dirty_ids,
         b.dirty_idx, b.scratch_off, c0, c1, b.path_src, b.path_cnt, b.path_count, b.nbits, b.noop_d, b.slot_owner,
-        b.scratch_cap, b.rows, b.pool, b.hash_mask, b.scratch_h, b.scratch_k);
+        b.scratch_cap, b.rows, b.pool, b.hash_mask, b.scratch_h, b.scratch_k, b.gather_send, b.gather_cap_spec,
+        b.gather_cap_status);
     return hipGetLastError();
 }
 
@@ -1776,7 +1800,7 @@ hipError_t launch_emit(hipStream_t s, const DiffBuffers& b) {
     const uint32_t* nd = b.summary + 2;
     k_scan_tiles<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums);
     k_scan_apply<uint32_t><<<ntiles, 256, 0, s>>>(b.path_count, nd, 0, b.tile_sums, nullptr, b.summary + 5,
-                                                  b.path_off, true);
+                                                  b.path_off, true, nullptr);
     k_copy_paths<<<grid_for((b.n_pairs + 63) / 64, kPersistBlocks), 256, 0, s>>>(
         b.summary, b.scratch_off, b.path_off, b.path_count, b.scratch_h, b.scratch_k, b.arena_h, b.arena_k, b.out_h,
         b.out_k);

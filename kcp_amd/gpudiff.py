@@ -213,6 +213,8 @@ SIGNATURES = [
     ("gpudiff_dbatch_read_pool", C.c_int, [_P, _P, C.c_uint64, C.c_void_p, C.c_uint64]),
     ("gpudiff_dbatch_export", C.c_int, [_P, _P, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64]),
     ("gpudiff_dbatch_free", None, [_P, _P]),
+    ("gpudiff_dbatch_bind_gather", C.c_int, [_P, _P, C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("gpudiff_dbatch_result_slot", C.c_int, [_P, _P, C.c_uint32]),
     ("gpudiff_cluster_bytes", C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p]),
     ("gpudiff_shard_lpt", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     ("gpudiff_diff", C.c_int, [_P, _P, C.POINTER(C.c_uint64)]),
@@ -448,6 +450,16 @@ class DeviceBatch:
         """Async D2D copy of results into caller device memory (ctx stream)."""
         _chk(_lib.gpudiff_dbatch_export(self.engine.ctx, self.h, what, dst_device_ptr, max_elems, known_count),
              "gpudiff_dbatch_export")
+
+    def bind_gather(self, send_device_ptr: int, cap_spec: int, cap_status: int):
+        """K3 of every later diff also writes [8 counts | spec IDs | status IDs] into this device buffer
+        (gpudiff_dbatch_bind_gather); 0 unbinds."""
+        _chk(_lib.gpudiff_dbatch_bind_gather(self.engine.ctx, self.h, send_device_ptr or None, cap_spec, cap_status),
+             "gpudiff_dbatch_bind_gather")
+
+    def result_slot(self, slot: int):
+        """Select result slot 0 / 1 for later diffs, exports and waits (gpudiff_dbatch_result_slot)."""
+        _chk(_lib.gpudiff_dbatch_result_slot(self.engine.ctx, self.h, slot), "gpudiff_dbatch_result_slot")
 
     def read_pool(self, off: int, nbytes: int) -> bytes:
         buf = C.create_string_buffer(max(nbytes, 1))

@@ -108,14 +108,29 @@ class DirtyGather:
     region."""
 
     def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist, depth: int = 1,
-                 grow: float = 1.25):
+                 grow: float = 1.25, bind=None, slot=None):
+        """bind(send, cap_spec, cap_status): optional -- the engine writes each step's counts and IDs into
+        the send buffer itself (gpudiff_dbatch_bind_gather, from its compaction kernel), so a step needs no
+        export copies; call begin_step() before the step's diff so the binding points at that step's
+        buffer.  fill_counts / fill_ids are then used only to re-export after a capacity regrow.
+
+        slot(k): optional, depth 1 only -- LOOKAHEAD: step s's gathered counts are checked only after step
+        s + 1's diff and collective are enqueued (finish() checks the last step), so the host never waits
+        between steps and the GPU always has the next pass queued.  The engine alternates result slots by
+        step (gpudiff_dbatch_result_slot, set by begin_step), so a capacity regrow found late still exports
+        step s's complete lists from its slot, re-gathers it, and re-gathers step s + 1 from the other."""
+        import numpy as np
         import torch
         self.world, self.dist, self.device = world, dist, device
         self.depth = max(1, int(depth))
         self.grow = max(1.0, float(grow))
+        self.bind = bind
         self.n_steps = 0
         self.n_regrows = 0
         self.maxc = torch.zeros((world, 2), dtype=torch.int32, device=device)
+        self.maxc_host = np.zeros((world, 2), dtype=np.int64)  # depth 1: the counts read back every step
+        self.slot = slot if self.depth == 1 else None
+        self.pending = None  # lookahead: the step whose gathered counts are not checked yet
         self._alloc(cap_spec, cap_status)
 
     def _alloc(self, cap_spec: int, cap_status: int):
@@ -129,12 +144,64 @@ class DirtyGather:
         self.used = [False] * self.depth
         pinned = torch.device(self.device).type == "cuda"
         self.host_counts = torch.zeros((self.world, 2), dtype=torch.int32, pin_memory=pinned)
+        # lookahead: per step parity, the gathered counts (pinned), their event and the capacities they had
+        self.la_counts = [torch.zeros((self.world, 2), dtype=torch.int32, pin_memory=pinned) for _ in range(2)]
+        self.la_events = [torch.cuda.Event() if pinned else None for _ in range(2)]
+        self.la_caps = [self.cap, self.cap]
         self._select(0)
 
     def _select(self, b: int):
         self.send, self.all = self.sends[b], self.alls[b]
         self.counts = self.send[:8]
         self.buf = [self.send[8:8 + self.cap[0]], self.send[8 + self.cap[0]:]]
+        if self.bind is not None:
+            self.bind(self.send, self.cap[0], self.cap[1])
+
+    def begin_step(self):
+        """Before the step's diff (with `bind` or `slot`): select this step's send buffer (after the
+        collective that last read it) and point the engine's binding at it; with `slot`, the result slot
+        this step's diff writes."""
+        b = self.n_steps % self.depth
+        self._join(b)
+        if self.bind is not None:
+            self._select(b)
+        if self.slot is not None:
+            self.slot(self.n_steps % 2)
+
+    def _gather_lookahead(self, k: int):
+        """all-gather of the send buffer, then this step's gathered counts copied to pinned slot k behind an
+        event (read later by _check)"""
+        self.dist.all_gather_into_tensor(self.all, self.send)
+        self.la_counts[k].copy_(self._gathered_counts(0), non_blocking=True)
+        self.la_caps[k] = self.cap
+        if self.la_events[k] is not None:
+            self.la_events[k].record()
+
+    def _check(self, s: int, fill_counts, fill_ids):
+        """Lookahead: step s's gathered counts (its collective finished long before: step s + 1's pass was
+        queued behind it).  A capacity exceeded on any rank -- the same on every rank, so all redo it
+        together -- grows the buffers and re-gathers step s from its result slot, then the in-flight step
+        s + 1 (whose send buffer was filled under the old capacities) from the other."""
+        k = s % 2
+        if self.la_events[k] is not None:
+            self.la_events[k].synchronize()
+        hc = self.la_counts[k].clone()
+        cap = self.la_caps[k]
+        self.maxc_host = self.maxc_host.clip(min=hc.numpy())
+        if not bool((hc[:, 0] > cap[0]).any() or (hc[:, 1] > cap[1]).any()):
+            return
+        ms, mt = int(hc[:, 0].max()), int(hc[:, 1].max())
+        self._alloc(max(self.cap[0], int(ms * self.grow) + 1), max(self.cap[1], int(mt * self.grow) + 1))
+        redo = [s] + ([s + 1] if self.pending == s + 1 else [])
+        for t in redo:
+            self.slot(t % 2)
+            fill_counts(self.counts)
+            for col in (0, 1):
+                fill_ids(col, self.buf[col])
+            self._gather_lookahead(t % 2)
+        self.n_regrows += 1
+        if self.pending == s + 1:  # its re-gather may still exceed the grown capacity: checked as usual
+            self.slot((s + 2) % 2)
 
     @staticmethod
     def agree_capacity(counts, world: int, dist, slack: float = 1.0):
@@ -164,14 +231,27 @@ class DirtyGather:
         rank's values into its slots of the send buffer on the device (the GPU
         path: gpudiff_dbatch_export straight from HBM, ordered on the stream
         before the collective).  Both may be called again within one step (a
-        capacity regrow re-exports the same results)."""
+        capacity regrow re-exports the same results).  With `bind` the engine
+        has written them already (begin_step before the diff) and they run only
+        after a regrow."""
         import torch
         b = self.n_steps % self.depth
-        self._join(b)  # the collective that last read this buffer
-        self._select(b)
-        fill_counts(self.counts)
-        for col in (0, 1):
-            fill_ids(col, self.buf[col])
+        if self.bind is None:
+            self._join(b)  # the collective that last read this buffer
+            self._select(b)
+            fill_counts(self.counts)
+            for col in (0, 1):
+                fill_ids(col, self.buf[col])
+        if self.slot is not None:  # lookahead (depth 1)
+            s = self.n_steps
+            self._gather_lookahead(s % 2)
+            prev, self.pending = self.pending, s
+            self.used[0] = True
+            self.n_steps += 1
+            if prev is not None:
+                self._check(prev, fill_counts, fill_ids)
+            self._fills = (fill_counts, fill_ids)
+            return
         if self.depth > 1:
             self.works[b] = self.dist.all_gather_into_tensor(self.all, self.send, async_op=True)
         else:
@@ -186,7 +266,10 @@ class DirtyGather:
                     fill_ids(col, self.buf[col])
                 self.dist.all_gather_into_tensor(self.all, self.send)
                 self.n_regrows += 1
-            torch.maximum(self.maxc, self._gathered_counts(0), out=self.maxc)
+                hc = self._read_counts()
+            # the running maximum on the host: the counts are here already (no device kernel per step)
+            np_hc = hc.numpy()
+            self.maxc_host = self.maxc_host.clip(min=np_hc)
         self.used[b] = True
         self.n_steps += 1
 
@@ -200,9 +283,13 @@ class DirtyGather:
             torch.maximum(self.maxc, self._gathered_counts(b), out=self.maxc)
 
     def finish(self):
-        """Join every outstanding collective (the compute stream waits for them)."""
+        """Join every outstanding collective (the compute stream waits for them); with lookahead, check the
+        last step's counts (and regrow it if needed)."""
         for b in range(self.depth):
             self._join(b)
+        if self.slot is not None and self.pending is not None:
+            s, self.pending = self.pending, None
+            self._check(s, *self._fills)
 
     def _rows(self):
         return self.all.view(self.world, self.width)
@@ -211,8 +298,11 @@ class DirtyGather:
         """-> (ok, host count matrix [world, 8] of the last step); ok only if no
         rank exceeded its capacity in ANY step since the buffers were last sized
         (the device-side running maximum of the gathered counts)."""
+        import torch
         self.finish()
         mx = self.maxc.cpu()
+        if self.depth == 1:
+            mx = torch.maximum(mx, torch.from_numpy(self.maxc_host).to(mx.dtype))
         ok = bool((mx[:, 0] <= self.cap[0]).all() and (mx[:, 1] <= self.cap[1]).all())
         cc = self._rows()[:, :8].cpu()
         return ok, cc
@@ -223,7 +313,8 @@ class DirtyGather:
         import torch
         ok, cc = self.check()
         if not ok:
-            raise RuntimeError("dirty-ID capacity exceeded: %s > %s" % (self.maxc.cpu().tolist(), self.cap))
+            raise RuntimeError("dirty-ID capacity exceeded: %s / %s > %s" % (
+                self.maxc.cpu().tolist(), self.maxc_host.tolist(), self.cap))
         rows = self._rows()
         spec = torch.cat([rows[r, 8:8 + int(cc[r, 0])] for r in range(self.world)])
         stat = torch.cat([rows[r, 8 + self.cap[0]:8 + self.cap[0] + int(cc[r, 1])] for r in range(self.world)])

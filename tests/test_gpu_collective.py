@@ -65,6 +65,47 @@ def test_dirty_gather_over_rccl_world1():
             sa, ta = g.result()
             assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
             assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        # the engine writes counts + IDs into the send buffer itself (gpudiff_dbatch_bind_gather): no export
+        # copies per step; the fills run only after a regrow (capacity below the count: the first step)
+        bind = lambda send, cs, ct: db.bind_gather(send.data_ptr(), cs, ct)  # noqa: E731
+        for depth, caps in ((1, (cap_s, cap_t)), (2, (cap_s, cap_t)), (1, (max(1, cap_s // 2), max(1, cap_t // 3)))):
+            g = shard.DirtyGather(1, caps[0], caps[1], dev, dist, depth=depth, bind=bind)
+            for _ in range(4):
+                g.begin_step()
+                eng.diff(db)
+                g.step(fill_counts, fill_ids)
+            g.finish()
+            torch.cuda.synchronize()
+            sa, ta = g.result()
+            assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+            assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+            assert g.n_regrows == (1 if caps[0] < cap_s else 0)
+            cnt = g._rows()[0, :8].cpu().tolist()
+            assert cnt[:3] == [want.spec_dirty_ids.size, want.status_dirty_ids.size, want.dirty_ids.size]
+            assert cnt[4:] == [0, 0, 0, 0]
+        # lookahead: step s checked after step s + 1 is queued; a capacity below the count is found one step
+        # late and re-gathered from the engine's alternate result slot (and so is the in-flight step)
+        for caps in ((cap_s, cap_t), (max(1, cap_s // 2), max(1, cap_t // 3))):
+            g = shard.DirtyGather(1, caps[0], caps[1], dev, dist, bind=bind, slot=lambda k: db.result_slot(k))
+            for _ in range(5):
+                g.begin_step()
+                eng.diff(db)
+                g.step(fill_counts, fill_ids)
+            g.finish()
+            torch.cuda.synchronize()
+            ok, cc = g.check()
+            assert ok and g.n_regrows == (1 if caps[0] < cap_s else 0)
+            sa, ta = g.result()
+            assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+            assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        db.result_slot(0)
+        # each slot keeps the lists of the last diff made under it
+        r0 = eng.wait(eng.diff(db))
+        db.result_slot(1)
+        r1 = eng.wait(eng.diff(db))
+        assert np.array_equal(r0.spec_dirty_ids, r1.spec_dirty_ids) and np.array_equal(r1.spec_dirty_ids, want.spec_dirty_ids)
+        db.result_slot(0)
+        db.bind_gather(0, 0, 0)
         # a capacity below the dirty count: regrown inside the first step, exact from then on
         g = shard.DirtyGather(1, max(1, cap_s // 2), max(1, cap_t // 3), dev, dist)
         for _ in range(3):
