@@ -163,6 +163,11 @@ def main():
     ap.add_argument("--gather-depth", type=int, default=1,
                     help="N > 1: all-gathers in flight; 2 = pipelined (step s's collective overlaps step s+1's "
                          "diff; measured 2.4%% slower than serial at world size 1 on MI355X, profiles/r02zd)")
+    ap.add_argument("--pipeline", type=int, default=1, choices=[1, 2],
+                    help="2 = two diff passes in flight: a second context (own stream) diffs a view of the resident "
+                         "batch (gpudiff_dbatch_create_view) on alternate steps, so one pass's decision kernel "
+                         "fills the CUs the previous pass's tail frees and that pass's compaction, joins and "
+                         "collective (shard.PipelinedGather) run beside it; every step still a complete pass")
     ap.add_argument("--no-gather-lookahead", action="store_true",
                     help="N > 1 (RCCL, depth 1): read each step's gathered counts before enqueueing the next pass "
                          "(the default checks step s after step s + 1 is queued, regrowing from the engine's "
@@ -357,6 +362,25 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         eng.diff(db)
     eng.sync()
+    # --pipeline 2: the second pass context (its own stream) and its view of the resident batch
+    engs, dbs, streams = [eng], [db], [stream]
+    if args.pipeline == 2:
+        if gloo:
+            log("error: --pipeline 2 needs the RCCL path")
+            sys.exit(2)
+        stream2 = torch.cuda.Stream(device=dev)
+        eng2 = G.Engine(device=gpu, encode_threads=threads, stream=stream2.cuda_stream, timing=True,
+                        flags=args.engine_flags)
+        db2 = db.view(eng2)
+        engs.append(eng2)
+        dbs.append(db2)
+        streams.append(stream2)
+        r2 = eng2.wait(eng2.diff(db2))  # allocates its outputs; the same decisions as the first context's
+        full_check["pipeline_view_flags_eq"] = bool(np.array_equal(r2.pair_flags, pop_flags))
+        del r2
+        for _ in range(max(0, args.warmup - 1)):
+            eng2.diff(db2)
+        eng2.sync()
 
     # ---------------- the collective (N > 1): capacities agreed once, untimed
     gather = None
@@ -379,30 +403,50 @@ def main():
         # (gpudiff_dbatch_bind_gather) -- no export copies per step; gloo's host tensors are filled by copies
         bind = None if gloo else (lambda send, cs, ct: db.bind_gather(send.data_ptr(), cs, ct))
         slot = None if (gloo or args.no_gather_lookahead or args.gather_depth != 1) else (lambda k: db.result_slot(k))
-        gather = shard.DirtyGather(world, cap_s, cap_t, comm_dev, dist, depth=args.gather_depth, bind=bind,
-                                   slot=slot)
-        log("collective: %s, capacities agreed (%d spec, %d status IDs per rank), depth %d"
-            % (args.dist_backend, cap_s, cap_t, args.gather_depth))
+        if args.pipeline == 2:
+            binds = [lambda send, cs, ct, d=d: d.bind_gather(send.data_ptr(), cs, ct) for d in dbs]
+            gather = shard.PipelinedGather(world, cap_s, cap_t, comm_dev, dist, streams, binds)
 
-        def fill_counts(t):
-            export_to(t, G.EXPORT_COUNTS, 8)
+            def fill_counts(p, t):
+                dbs[p].export(G.EXPORT_COUNTS, t.data_ptr(), 8, 8)
 
-        def fill_ids(col, buf):
-            export_to(buf, G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.numel())
-        if bind is not None or slot is not None:
-            gather.begin_step()
-            eng.diff(db)
-        gather.step(fill_counts, fill_ids)  # warm the communicator
+            def fill_ids(p, col, buf):
+                dbs[p].export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
+                              buf.numel())
+            for p in (0, 1):  # warm the communicator on both streams
+                engs[p].diff(dbs[p])
+                gather.step(fill_counts, fill_ids)
+        else:
+            gather = shard.DirtyGather(world, cap_s, cap_t, comm_dev, dist, depth=args.gather_depth, bind=bind,
+                                       slot=slot)
+
+            def fill_counts(t):
+                export_to(t, G.EXPORT_COUNTS, 8)
+
+            def fill_ids(col, buf):
+                export_to(buf, G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.numel())
+            if bind is not None or slot is not None:
+                gather.begin_step()
+                eng.diff(db)
+            gather.step(fill_counts, fill_ids)  # warm the communicator
+        log("collective: %s, capacities agreed (%d spec, %d status IDs per rank), depth %d, pipeline %d"
+            % (args.dist_backend, cap_s, cap_t, args.gather_depth, args.pipeline))
         gather.finish()
         torch.cuda.synchronize()
 
     # ---------------- timed region
-    eng.timing_reset()
+    for e in engs:
+        e.timing_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if args.pipeline == 2:  # alternate contexts: two passes in flight
+        for i in range(args.steps):
+            engs[i & 1].diff(dbs[i & 1])
+            if gather is not None:
+                gather.step(fill_counts, fill_ids)
+    for _ in range(args.steps if args.pipeline == 1 else 0):
         if gather is not None and (gather.bind is not None or gather.slot is not None):
             gather.begin_step()
         eng.diff(db)
@@ -424,7 +468,8 @@ def main():
                             gathered_spec=None if sa is None else int(sa.numel()),
                             gathered_status=None if ta is None else int(ta.numel()),
                             depth=gather.depth, bytes_per_rank=4 * gather.width, regrows=gather.n_regrows,
-                            engine_writes_send_buffer=gather.bind is not None, lookahead=gather.slot is not None)
+                            engine_writes_send_buffer=(args.pipeline == 2 or gather.bind is not None),
+                            lookahead=(args.pipeline == 2 or gather.slot is not None), pipeline=args.pipeline)
         t = torch.tensor([dt], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -475,6 +520,8 @@ def main():
         if pmc.get("k2_source_hash") == src_hash and pmc.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
 
+    for d in dbs[1:]:
+        d.free()  # views before their base
     db.free()  # the JSON-in and CPU legs below need no resident population
 
     # ---------------- rank 0, N = 1: end-to-end JSON-in, CPU baselines, three-way parity
@@ -527,6 +574,7 @@ def main():
                     cfg.mutate_frac * 100,
                     "40% ConfigMap/Secret, 40% Deployment, 20% CRD" if args.config == "config3" else args.config),
                 "pairs_per_rank": n, "resident_gb_per_rank": st.pool_bytes / 1e9, "shard": shard_info,
+                "passes_in_flight": args.pipeline,
                 "parallelism": "shard-by-logical-cluster x%d (LPT)%s" % (
                     world, ((", RCCL all-gather of dirty counts+IDs per step (%d in flight)" % args.gather_depth)
                             if args.dist_backend == "nccl" else

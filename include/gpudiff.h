@@ -229,6 +229,14 @@ void gpudiff_hbatch_free(gpudiff_ctx* ctx, gpudiff_hbatch* hb);
 /* ---- device batches ---- */
 int gpudiff_dbatch_create(gpudiff_ctx* ctx, uint64_t pool_bytes, uint64_t max_pairs,
                           gpudiff_dbatch** out);
+/* A view of `base`: a batch with its own per-pass outputs (flags, lists, path arenas, scratch, counts) over
+ * base's resident pairs (pool, rows and pair IDs are base's; appends to base are seen by later diffs of
+ * the view; append / reset on a view are GPUDIFF_E_INVAL).  With a second context (its own stream) it lets
+ * two diff passes over one population be in flight at once -- pass s + 1's decision kernel fills the CUs
+ * pass s's tail frees, and pass s's compaction, joins and collective run beside it.  Same device as base;
+ * the caller orders base's appends before the view's diffs (e.g. gpudiff_sync on base's context).  Free
+ * views before their base. */
+int gpudiff_dbatch_create_view(gpudiff_ctx* ctx, const gpudiff_dbatch* base, gpudiff_dbatch** out);
 /* async H2D of hb into the batch (rows rebased onto the batch's pool) */
 int gpudiff_dbatch_append(gpudiff_ctx* ctx, gpudiff_dbatch* db, const gpudiff_hbatch* hb);
 int gpudiff_dbatch_reset(gpudiff_ctx* ctx, gpudiff_dbatch* db);
@@ -250,7 +258,8 @@ int gpudiff_dbatch_export(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint32_t w
  * [8 counts | cap_spec spec-dirty IDs | cap_status status-dirty IDs], counts = (n_spec, n_status, n_dirty,
  * K4 scratch entries, 0, 0, 0, 0).  The counts are the batch totals even past a capacity; IDs past it are
  * not written (the caller grows its buffers and exports them with gpudiff_dbatch_export, whose lists are
- * always complete).  Words 4..7 are zeroed here, on the context stream.  send_dev = NULL unbinds. */
+ * always complete).  Words 4..7 are zeroed here, on the context stream, when the buffer differs from the
+ * one bound (rebinding the same buffer is free).  send_dev = NULL unbinds. */
 int gpudiff_dbatch_bind_gather(gpudiff_ctx* ctx, gpudiff_dbatch* db, void* send_dev, uint32_t cap_spec,
                                uint32_t cap_status);
 /* Result slots: the spec / status dirty-ID lists come in two slots (0 by default; slot 1 allocated on first

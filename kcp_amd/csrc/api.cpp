@@ -383,6 +383,8 @@ void gpudiff_hbatch_free(gpudiff_ctx* c, gpudiff_hbatch* hb) {
 }
 
 // ------------------------------------------------------------------ device batches
+static int alloc_outputs(gpudiff_dbatch* d);
+
 int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pairs, gpudiff_dbatch** out) {
     if (!c || !out) return GPUDIFF_E_INVAL;
     *out = nullptr;
@@ -393,12 +395,62 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
     if (!d) return GPUDIFF_E_NOMEM;
     d->pool_cap = (pool_bytes + 15) & ~15ull;
     d->max_pairs = max_pairs;
+    d->device = c->device;
     const uint64_t np = std::max<uint64_t>(max_pairs, 1);
+    if ((rc = dalloc(&d->pool, d->pool_cap)) || (rc = dalloc(&d->rows, np)) || (rc = dalloc(&d->pair_ids, np)) ||
+        (rc = alloc_outputs(d.get()))) {
+        dfree_all(d.get());
+        return rc;
+    }
+    *out = d.release();
+    return GPUDIFF_OK;
+}
+
+int gpudiff_dbatch_create_view(gpudiff_ctx* c, const gpudiff_dbatch* base, gpudiff_dbatch** out) {
+    if (!c || !base || !out || base->base) return GPUDIFF_E_INVAL;
+    *out = nullptr;
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (base->device != c->device) return GPUDIFF_E_INVAL;
+    std::unique_ptr<gpudiff_dbatch> d(new (std::nothrow) gpudiff_dbatch());
+    if (!d) return GPUDIFF_E_NOMEM;
+    d->base = base;
+    d->pool_borrowed = true;
+    d->max_pairs = base->max_pairs;
+    d->device = c->device;
+    if ((rc = alloc_outputs(d.get()))) {
+        dfree_all(d.get());
+        return rc;
+    }
+    *out = d.release();
+    return GPUDIFF_OK;
+}
+
+// a view sees its base's resident pairs as of this call (appends made since are ordered by the caller:
+// they run on the base's context stream)
+static void view_sync(gpudiff_dbatch* d) {
+    if (!d->base) return;
+    const gpudiff_dbatch* b = d->base;
+    d->pool = b->pool;
+    d->pool_cap = b->pool_cap;
+    d->pool_used = b->pool_used;
+    d->rows = b->rows;
+    d->pair_ids = b->pair_ids;
+    d->n_pairs = b->n_pairs;
+    d->leaves = b->leaves;
+    d->compare_bytes = b->compare_bytes;
+    d->value_bytes = b->value_bytes;
+    d->size_hint_bytes = b->size_hint_bytes;
+}
+
+// every per-pass output of a batch (a view has only these)
+static int alloc_outputs(gpudiff_dbatch* d) {
+    int rc;
+    const uint64_t np = std::max<uint64_t>(d->max_pairs, 1);
     const uint64_t nchunks = (np + 63) / 64;
     const uint64_t ntiles = 4 * (np / 4096 + 2);  // scan tile sums (4 x u32 for the chunk scan)
     uint4* cc = nullptr;
-    if ((rc = dalloc(&d->pool, d->pool_cap)) || (rc = dalloc(&d->rows, np)) || (rc = dalloc(&d->pair_ids, np)) ||
-        (rc = dalloc(&d->flags, np)) || (rc = dalloc(&d->caps, np)) || (rc = dalloc(&cc, nchunks)) ||
+    if ((rc = dalloc(&d->flags, np)) || (rc = dalloc(&d->caps, np)) || (rc = dalloc(&cc, nchunks)) ||
         (rc = dalloc(&d->summary, kSummaryWords)) || (rc = dalloc(&d->spec_ids, np)) || (rc = dalloc(&d->status_ids, np)) ||
         (rc = dalloc(&d->dirty_ids, np)) || (rc = dalloc(&d->dirty_idx, np)) || (rc = dalloc(&d->scratch_off, np)) ||
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
@@ -406,20 +458,15 @@ int gpudiff_dbatch_create(gpudiff_ctx* c, uint64_t pool_bytes, uint64_t max_pair
         (rc = dalloc(&d->noop_d, np)) ||
         (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments))) {
         d->chunk_counts = cc;
-        dfree_all(d.get());
         return rc;
     }
     d->chunk_counts = cc;
-    if (hipEventCreateWithFlags(&d->done, hipEventDisableTiming) != hipSuccess) {
-        dfree_all(d.get());
-        return GPUDIFF_E_DEVICE;
-    }
-    *out = d.release();
+    if (hipEventCreateWithFlags(&d->done, hipEventDisableTiming) != hipSuccess) return GPUDIFF_E_DEVICE;
     return GPUDIFF_OK;
 }
 
 int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatch* hb) {
-    if (!c || !d || !hb) return GPUDIFF_E_INVAL;
+    if (!c || !d || !hb || d->base) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
     if (d->pool_used + hb->pool_bytes > d->pool_cap || d->n_pairs + hb->n > d->max_pairs) return GPUDIFF_E_CAPACITY;
@@ -449,7 +496,7 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
 }
 
 int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
-    if (!c || !d) return GPUDIFF_E_INVAL;
+    if (!c || !d || d->base) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -460,6 +507,7 @@ int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
 
 int gpudiff_dbatch_stats_get(const gpudiff_dbatch* d, gpudiff_batch_stats* st) {
     if (!d || !st) return GPUDIFF_E_INVAL;
+    if (d->base) d = d->base;
     st->n_pairs = d->n_pairs;
     st->pool_bytes = d->pool_used;
     st->total_leaves = d->leaves;
@@ -504,10 +552,12 @@ int gpudiff_dbatch_bind_gather(gpudiff_ctx* c, gpudiff_dbatch* d, void* send_dev
     if (!c || !d) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
+    const bool fresh = send_dev && send_dev != (void*)d->gather_send;
     d->gather_send = (uint32_t*)send_dev;
     d->gather_cap_spec = send_dev ? cap_spec : 0;
     d->gather_cap_status = send_dev ? cap_status : 0;
-    if (send_dev) HIPCHK(hipMemsetAsync((uint32_t*)send_dev + 4, 0, 4 * sizeof(uint32_t), c->stream));
+    // a rebinding of the same buffer (every step of a per-step collective) costs nothing on the stream
+    if (fresh) HIPCHK(hipMemsetAsync((uint32_t*)send_dev + 4, 0, 4 * sizeof(uint32_t), c->stream));
     return GPUDIFF_OK;
 }
 
@@ -528,6 +578,7 @@ int gpudiff_dbatch_result_slot(gpudiff_ctx* c, gpudiff_dbatch* d, uint32_t slot)
 
 int gpudiff_dbatch_read_pool(gpudiff_ctx* c, const gpudiff_dbatch* d, uint64_t off, void* dst, uint64_t bytes) {
     if (!c || !d || (!dst && bytes)) return GPUDIFF_E_INVAL;
+    if (d->base) d = d->base;
     int rc = set_device(c);
     if (rc) return rc;
     if (off > d->pool_used || bytes > d->pool_used - off) return GPUDIFF_E_INVAL;
@@ -626,6 +677,8 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     if (!c || !d) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
     if (rc) return rc;
+    if (d->base && d->base->device != c->device) return GPUDIFF_E_INVAL;
+    view_sync(d);
     // scratch for changed paths: sized from the batch, grown on overflow
     {
         const uint32_t nch = (uint32_t)((d->n_pairs + 63) / 64);

@@ -105,6 +105,10 @@ struct gpudiff_dbatch {
     // always the current slot's; switching swaps them), allocated on first use
     uint32_t* ids_alt[2] = {nullptr, nullptr};
     uint32_t res_slot = 0;
+    // gpudiff_dbatch_create_view: this batch diffs `base`'s resident pairs (pool, rows, pair IDs borrowed,
+    // refreshed at every diff) into its own outputs, so two passes over one population can be in flight
+    const gpudiff_dbatch* base = nullptr;
+    int device = -1;
 };
 
 struct DStore;
@@ -174,6 +178,7 @@ inline int dalloc(T** p, uint64_t count) {
 
 inline void dfree_all(gpudiff_dbatch* d) {
     if (d->pool && !d->pool_borrowed) (void)hipFree(d->pool);
+    if (d->base) d->rows = nullptr, d->pair_ids = nullptr;  // a view's inputs are its base's
     void* ps[] = {d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
                   d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,

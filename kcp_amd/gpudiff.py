@@ -215,6 +215,7 @@ SIGNATURES = [
     ("gpudiff_dbatch_free", None, [_P, _P]),
     ("gpudiff_dbatch_bind_gather", C.c_int, [_P, _P, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("gpudiff_dbatch_result_slot", C.c_int, [_P, _P, C.c_uint32]),
+    ("gpudiff_dbatch_create_view", C.c_int, [_P, _P, C.POINTER(_P)]),
     ("gpudiff_cluster_bytes", C.c_int, [C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p]),
     ("gpudiff_shard_lpt", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     ("gpudiff_diff", C.c_int, [_P, _P, C.POINTER(C.c_uint64)]),
@@ -424,11 +425,20 @@ class HostBatch:
 
 
 class DeviceBatch:
-    def __init__(self, engine: "Engine", pool_bytes: int, max_pairs: int):
+    def __init__(self, engine: "Engine", pool_bytes: int, max_pairs: int, _view_of: "DeviceBatch" = None):
         self.engine = engine
         h = C.c_void_p()
-        _chk(_lib.gpudiff_dbatch_create(engine.ctx, pool_bytes, max_pairs, C.byref(h)), "gpudiff_dbatch_create")
+        if _view_of is None:
+            _chk(_lib.gpudiff_dbatch_create(engine.ctx, pool_bytes, max_pairs, C.byref(h)), "gpudiff_dbatch_create")
+        else:
+            _chk(_lib.gpudiff_dbatch_create_view(engine.ctx, _view_of.h, C.byref(h)), "gpudiff_dbatch_create_view")
+        self.base = _view_of  # keeps the base alive while the view lives
         self.h = h
+
+    def view(self, engine: "Engine") -> "DeviceBatch":
+        """A batch with its own outputs over this batch's resident pairs, diffed by `engine` (typically a
+        second context on its own stream: two passes in flight, gpudiff_dbatch_create_view)."""
+        return DeviceBatch(engine, 0, 0, _view_of=self)
 
     def append(self, hb: HostBatch):
         _chk(_lib.gpudiff_dbatch_append(self.engine.ctx, self.h, hb.h), "gpudiff_dbatch_append")

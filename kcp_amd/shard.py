@@ -319,3 +319,125 @@ class DirtyGather:
         spec = torch.cat([rows[r, 8:8 + int(cc[r, 0])] for r in range(self.world)])
         stat = torch.cat([rows[r, 8 + self.cap[0]:8 + self.cap[0] + int(cc[r, 1])] for r in range(self.world)])
         return spec, stat
+
+
+class PipelinedGather:
+    """The per-step collective for TWO diff passes in flight: two contexts, each on its own stream, diff a
+    batch and its view (gpudiff_dbatch_create_view) on alternate steps, so pass s + 1's decision kernel
+    fills the CUs pass s's tail frees while pass s's compaction, joins and collective run beside it.
+
+    Pass p = s % 2 owns send / gathered buffer p, bound to its batch (gpudiff_dbatch_bind_gather: the
+    engine's compaction writes [8 counts | spec IDs | status IDs] there), and its all-gather runs on its
+    stream (torch's ProcessGroupNCCL orders the collective after the current stream's work and the stream
+    after the collective; the communicator serialises collectives in issue order, the same on every
+    rank).  Step s's gathered counts are copied to pinned memory behind an event and checked only after
+    step s + 1 is queued; a capacity exceeded on any rank (every rank sees the same counts) grows both
+    buffers and re-gathers step s from batch s % 2 -- its lists stay until step s + 2 -- and the in-flight
+    step s + 1 from the other, each on its own stream.  Replaced buffers are kept alive until finish(), as
+    a collective still queued may read them."""
+
+    def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist, streams, binds,
+                 grow: float = 1.25):
+        import numpy as np
+        import torch
+        self.world, self.dist, self.device = world, dist, device
+        self.streams, self.binds = list(streams), list(binds)
+        self.grow = max(1.0, float(grow))
+        self.n_steps = 0
+        self.n_regrows = 0
+        self.pending = None
+        self.maxc_host = np.zeros((world, 2), dtype=np.int64)
+        self.hc = [torch.zeros((world, 2), dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        self.ev = [torch.cuda.Event() for _ in range(2)]
+        self.graveyard = []
+        self._alloc(cap_spec, cap_status)
+
+    def _alloc(self, cap_spec: int, cap_status: int):
+        import torch
+        if getattr(self, "sends", None) is not None:
+            self.graveyard += self.sends + self.alls
+        self.cap = (max(1, int(cap_spec)), max(1, int(cap_status)))
+        self.width = 8 + self.cap[0] + self.cap[1]
+        self.sends, self.alls = [], []
+        for p in range(2):
+            with torch.cuda.stream(self.streams[p]):
+                self.sends.append(torch.zeros(self.width, dtype=torch.int32, device=self.device))
+                self.alls.append(torch.zeros(self.world * self.width, dtype=torch.int32, device=self.device))
+            self.binds[p](self.sends[p], self.cap[0], self.cap[1])
+        self.caps_at = [self.cap, self.cap]
+
+    def _views(self, p: int):
+        s = self.sends[p]
+        return s[:8], [s[8:8 + self.cap[0]], s[8 + self.cap[0]:]]
+
+    def _gather(self, p: int):
+        import torch
+        with torch.cuda.stream(self.streams[p]):
+            self.dist.all_gather_into_tensor(self.alls[p], self.sends[p])
+            self.hc[p].copy_(self.alls[p].view(self.world, self.width)[:, :2], non_blocking=True)
+            self.ev[p].record()
+        self.caps_at[p] = self.cap
+
+    def step(self, fill_counts, fill_ids):
+        """After step s's diff was enqueued on pass s % 2's context.  fill_counts(p, t) / fill_ids(p, col,
+        buf) re-export pass p's results (used only after a regrow)."""
+        s = self.n_steps
+        self._gather(s % 2)
+        prev, self.pending = self.pending, s
+        self.n_steps += 1
+        self._fills = (fill_counts, fill_ids)
+        if prev is not None:
+            self._check(prev)
+
+    def _check(self, s: int):
+        import torch
+        p = s % 2
+        self.ev[p].synchronize()
+        hc = self.hc[p].clone()
+        cap = self.caps_at[p]
+        self.maxc_host = self.maxc_host.clip(min=hc.numpy())
+        if not bool((hc[:, 0] > cap[0]).any() or (hc[:, 1] > cap[1]).any()):
+            return
+        ms, mt = int(hc[:, 0].max()), int(hc[:, 1].max())
+        self._alloc(max(self.cap[0], int(ms * self.grow) + 1), max(self.cap[1], int(mt * self.grow) + 1))
+        fill_counts, fill_ids = self._fills
+        for t in [s] + ([s + 1] if self.pending == s + 1 else []):
+            q = t % 2
+            counts, bufs = self._views(q)
+            with torch.cuda.stream(self.streams[q]):
+                fill_counts(q, counts)
+                for col in (0, 1):
+                    fill_ids(q, col, bufs[col])
+            self._gather(q)
+        self.n_regrows += 1
+
+    def finish(self):
+        """Check the last step (inside the timed region: it waits for the last collective)."""
+        import torch
+        if self.pending is not None:
+            s, self.pending = self.pending, None
+            self._check(s)
+            self.ev[s % 2].synchronize()
+        for st in self.streams:
+            torch.cuda.current_stream().wait_stream(st)
+
+    def check(self):
+        ok = bool((self.maxc_host[:, 0] <= self.cap[0]).all() and (self.maxc_host[:, 1] <= self.cap[1]).all())
+        p = (self.n_steps - 1) % 2
+        cc = self.alls[p].view(self.world, self.width)[:, :8].cpu()
+        return ok, cc
+
+    def result(self):
+        """Node-wide (spec IDs, status IDs) of the last step, in rank order."""
+        import torch
+        ok, cc = self.check()
+        if not ok:
+            raise RuntimeError("dirty-ID capacity exceeded: %s > %s" % (self.maxc_host.tolist(), self.cap))
+        rows = self.alls[(self.n_steps - 1) % 2].view(self.world, self.width)
+        spec = torch.cat([rows[r, 8:8 + int(cc[r, 0])] for r in range(self.world)])
+        stat = torch.cat([rows[r, 8 + self.cap[0]:8 + self.cap[0] + int(cc[r, 1])] for r in range(self.world)])
+        return spec, stat
+
+    @property
+    def depth(self):
+        return 2

@@ -22,6 +22,9 @@ def lib():
         l.oracle_free.argtypes = [C.c_void_p]
         l.oracle_tree_paths.restype = C.c_long
         l.oracle_tree_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        l.oracle_tree_check.restype = C.c_long
+        l.oracle_tree_check.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         l.oracle_csr_run.restype = C.c_double
         l.oracle_csr_run.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.c_void_p,
                                      C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
@@ -176,6 +179,28 @@ class RollupDocs:
             self.close()
         except Exception:
             pass
+
+
+def tree_check(buf: np.ndarray, offs: np.ndarray, seeds: np.ndarray, threads: int = 16, cap: int = 0):
+    """Decisions and changed paths of n pairs given as JSON (buf u8, offs u64[2n+1] as
+    Population.json_range returns), by the tree-walk restatement with its own decoder: (flags u8[n],
+    offsets u32[n_dirty + 1], hashes u64, kinds u8).  TEST INFRASTRUCTURE (tools/full_tree_check.py)."""
+    n = (len(offs) - 1) // 2
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+    cap = cap or max(1024, 8 * n)
+    while True:
+        flags = np.zeros(max(n, 1), np.uint8)
+        o = np.zeros(n + 1, np.uint32)
+        hs = np.zeros(cap, np.uint64)
+        ks = np.zeros(cap, np.uint8)
+        m = lib().oracle_tree_check(buf.ctypes.data, offs.ctypes.data, n, seeds.ctypes.data, threads,
+                                    flags.ctypes.data, o.ctypes.data, hs.ctypes.data, ks.ctypes.data, cap)
+        if m >= 0:
+            nd = int(np.count_nonzero(flags[:n] & 3))
+            return flags[:n], o[:nd + 1], hs[:m], ks[:m]
+        cap *= 4
 
 
 class CsrPairs:

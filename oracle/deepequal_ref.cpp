@@ -551,6 +551,78 @@ long oracle_tree_paths(void* h, const uint8_t* seeds, uint32_t* offsets, uint64_
 
 void oracle_free(void* h) { delete (Pairs*)h; }
 
+// The full-size checker (tools/full_tree_check.py; TEST INFRASTRUCTURE): n pairs as JSON text, pair i's A
+// at buf[offs[2i], offs[2i+1]) and B at buf[offs[2i+1], offs[2i+2]), decoded by this file's own decoder
+// and decided + path-diffed by the tree walk (what oracle_load + oracle_decide + oracle_tree_paths do), on
+// `threads` threads over contiguous slices, nothing kept between pairs.  flags[i] as oracle_decide; for the
+// dirty pairs in order, offsets[k] .. offsets[k+1] of (hashes, kinds) as oracle_tree_paths.  Returns the
+// entries written, or -1 if cap is too small.
+long oracle_tree_check(const uint8_t* buf, const uint64_t* offs, size_t n, const uint8_t* seeds, int threads,
+                       uint8_t* flags, uint32_t* offsets, uint64_t* hashes, uint8_t* kinds, size_t cap) {
+    if (threads < 1) threads = 1;
+    struct Part {
+        std::vector<uint32_t> cnt;  // per dirty pair of the slice
+        std::vector<std::pair<uint64_t, uint8_t>> ent;
+    };
+    std::vector<Part> parts(threads);
+    auto work = [&](int t) {
+        const size_t b = n * t / threads, e = n * (t + 1) / threads;
+        Part& P = parts[t];
+        std::vector<std::pair<uint64_t, uint8_t>> ent;
+        for (size_t i = b; i < e; i++) {
+            Value va, vb;
+            const char* pa = (const char*)buf + offs[2 * i];
+            const char* pb = (const char*)buf + offs[2 * i + 1];
+            if (!decode(pa, offs[2 * i + 1] - offs[2 * i], va) || !decode(pb, offs[2 * i + 2] - offs[2 * i + 1], vb) ||
+                list_probe(va) || list_probe(vb)) {
+                flags[i] = 7;
+                P.cnt.push_back(0);
+                continue;
+            }
+            const bool sd = !deep_equal_apart_from_status(va, vb);
+            const bool td = !deep_equal_status(va, vb);
+            flags[i] = (sd ? 1 : 0) | (td ? 2 : 0);
+            if (!sd && !td) continue;
+            ent.clear();
+            LeafMap la, lb;
+            spec_leaves(va, seeds[i], la);
+            spec_leaves(vb, seeds[i], lb);
+            region_diff(la, lb, 0, ent);
+            if (td) {
+                LeafMap ta, tb;
+                status_leaves(va, seeds[i], ta);
+                status_leaves(vb, seeds[i], tb);
+                region_diff(ta, tb, 0x80, ent);
+                if (!vb.m->count("status")) {
+                    std::string path;
+                    ent.push_back({key_hash(seeds[i], "status", path) & kPathMask, (uint8_t)(3 | 0x80)});
+                }
+            }
+            P.cnt.push_back((uint32_t)ent.size());
+            P.ent.insert(P.ent.end(), ent.begin(), ent.end());
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    size_t total = 0, k = 0;
+    offsets[0] = 0;
+    for (const Part& P : parts) {
+        if (total + P.ent.size() > cap) return -1;
+        size_t j = 0;
+        for (uint32_t c : P.cnt) {
+            for (uint32_t q = 0; q < c; q++, j++) {
+                hashes[total] = P.ent[j].first;
+                kinds[total] = P.ent[j].second;
+                total++;
+            }
+            offsets[++k] = (uint32_t)total;
+        }
+    }
+    return (long)total;
+}
+
 // runs both predicates over every pair; flags bit0 spec dirty, bit1 status
 // dirty, bit2 decode error.  Threads repeat their slices until min_seconds
 // elapsed; returns the sweeps done (fractional) and the wall seconds.

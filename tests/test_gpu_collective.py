@@ -82,7 +82,8 @@ def test_dirty_gather_over_rccl_world1():
             assert g.n_regrows == (1 if caps[0] < cap_s else 0)
             cnt = g._rows()[0, :8].cpu().tolist()
             assert cnt[:3] == [want.spec_dirty_ids.size, want.status_dirty_ids.size, want.dirty_ids.size]
-            assert cnt[4:] == [0, 0, 0, 0]
+            if not g.n_regrows:  # words 4..7: zero from the binding (a regrow's export copies the summary's)
+                assert cnt[4:] == [0, 0, 0, 0]
         # lookahead: step s checked after step s + 1 is queued; a capacity below the count is found one step
         # late and re-gathered from the engine's alternate result slot (and so is the in-flight step)
         for caps in ((cap_s, cap_t), (max(1, cap_s // 2), max(1, cap_t // 3))):

@@ -102,3 +102,41 @@ def test_csr_paths_ptr_threads_equal_single_pass():
         assert got == expected_paths(exp[i])
     hb.free()
     e.close()
+
+
+def test_tree_check_equals_decoded_pairs_and_python_oracle():
+    """oracle_tree_check (the full-size checker's JSON-in tree walk, threaded, own decoder) gives the same
+    flags and changed paths as the per-pair oracle functions and the Python oracle, on a synthetic config3
+    population (its seeds from the host encoder's rows) plus the KAT pairs (decode errors included)."""
+    from kcp_amd import synth as S
+    cfg = S.make_cfg("config3", n_pairs=3000, n_clusters=30, mutate_frac=0.3)
+    pop = S.Population(cfg)
+    buf, offs, _ = pop.json_range(0, pop.n, 4)
+    e = G.Engine(device=G.DEVICE_NONE)
+    pairs = [(bytes(buf[offs[2 * i]:offs[2 * i + 1]]), bytes(buf[offs[2 * i + 1]:offs[2 * i + 2]]))
+             for i in range(pop.n)]
+    pairs += [(a, b) for _, a, b, _, _ in cases()]
+    hb = e.encode(pairs)
+    seeds = ((hb.rows()["flags_a"] >> G.OBJ_SEED_SHIFT) & 0xFF).astype(np.uint8)
+    jb = np.frombuffer(b"".join(a + b for a, b in pairs), np.uint8)
+    jo = np.zeros(2 * len(pairs) + 1, np.uint64)
+    pos = 0
+    for i, (a, b) in enumerate(pairs):
+        jo[2 * i], jo[2 * i + 1] = pos, pos + len(a)
+        pos += len(a) + len(b)
+    jo[-1] = pos
+    for threads in (1, 7):
+        f, o, h, k = cpu_ref.tree_check(jb, jo, seeds, threads)
+        dp = cpu_ref.DecodedPairs(pairs)
+        f2, _, _ = dp.decide()
+        o2, h2, k2 = dp.paths(seeds)
+        dp.close()
+        assert np.array_equal(f, f2) and np.array_equal(o, o2) and np.array_equal(h, h2) and np.array_equal(k, k2)
+    exp = oracle_batch(pairs)
+    assert [int(x) & 7 for x in f] == [expected_flags(r) & 7 for r in exp]
+    dirty = [i for i, r in enumerate(exp) if expected_flags(r) & 3]
+    for j, i in enumerate(dirty):
+        got = list(zip(h[o[j]:o[j + 1]].tolist(), k[o[j]:o[j + 1]].tolist()))
+        assert got == expected_paths(exp[i]), i
+    hb.free()
+    e.close()
