@@ -157,6 +157,7 @@ def test_small_deferrals_take_exact_scratch():
     exp = assert_matches(res, pairs)
     import torch
     cnt = torch.zeros(8, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the engine's stream does not order against torch's null stream
     db.export(G.EXPORT_COUNTS, cnt.data_ptr(), 8)
     e.sync()
     scratch = int(cnt[3].item()) & 0xFFFFFFFF
