@@ -98,11 +98,9 @@ enum {
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
 #define GPUDIFF_OPT_K4_PIPELINED_JOIN 0x8u /* tuning: K4's merge-path slices prefetch the next window's keys and
                                               metas (software-pipelined join) */
-/* bits 0x2 and 0x4: until ABI 3 they (and 0x8, bits 30-31) chose where long-value digests were computed (the
-   format has had no digests since ABI 4); now a 2-bit tuning field: */
-#define GPUDIFF_OPT_K2_RANGE_SHIFT 1u    /* 2 bits: the decision kernel's range tail (its last ~round of work handed
-                                            out as K ranges per pair): 0 = for large pairs (>= 16 KiB compared
-                                            bytes on average), 1 = off, 2 / 3 = on with K = 4 / 8 */
+/* bits 0x2 and 0x4 are reserved: until ABI 3 they (and 0x8, bits 30-31) chose where long-value digests were
+   computed (host encoder or kernel K1); since ABI 4 the format has no digests (include/gpudiff_format.h:
+   a long string's first 8 bytes sit in its leaf record, the rest in the arena) and they are ignored */
 /* tuning knobs (A/B measurements; 0 = defaults) */
 #define GPUDIFF_OPT_K2_VARIANT_SHIFT 8u  /* 4 bits: decision-kernel load policy / unroll */
 #define GPUDIFF_OPT_K2_BLOCKS_SHIFT 12u  /* 4 bits: resident blocks per CU for the decision kernel */

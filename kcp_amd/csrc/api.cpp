@@ -120,7 +120,6 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     }
     b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
     b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
-    b.k2_range_mode = (c->flags >> GPUDIFF_OPT_K2_RANGE_SHIFT) & 3u;
     b.gather_send = d->gather_send;
     b.gather_cap_spec = d->gather_cap_spec;
     b.gather_cap_status = d->gather_cap_status;

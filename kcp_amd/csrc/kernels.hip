@@ -1100,17 +1100,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // DYN variants: chunks at the end of a launch handed out as 8-pair items (about
 // four per wave), unless the whole launch is split already
 // a tail of q quarters of the launch's wave count, in 64-pair chunks
-// Range tail (sub_arg bits 20-22 = log2 K, 0 = off; large pairs): the launch's last chunks -- about one round of
-// main items -- are handed out as K range items per pair, each streaming 1/K of the pair's compared chunks,
-// so the launch ends with pieces of a few KiB instead of whole 16-256 KiB deep pairs (config4: the last wave
-// ended 140 us after the median one with 2-pair items).  The ranges' mismatch bits meet in one per-pair
-// counter word (caps[p], zeroed by the pass's reset kernel: done count | spec / status mismatch counts); the
-// wave that completes the last range decides the pair and joins or defers it like any other dirty pair.
-__host__ __device__ inline uint32_t k2_range_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift) {
-    const uint64_t pairs = (uint64_t)nwaves * (64u >> sub_shift);  // one round of main items
-    const uint64_t c = (pairs + 63u) / 64u;
-    return (uint32_t)(c < nch / 2u ? c : nch / 2u);
-}
 __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t q) {
     return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * q);
 }
@@ -1219,11 +1208,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     [[maybe_unused]] uint64_t tp_rows = 0, tp_pre = 0, tp_post = 0, tp_adv = 0, tp_e = 0, tp_r = 0, tp_je = 0;
     if constexpr (PROF) tp_start = wall_clock64();
     const uint32_t nch = c_end - c_begin;
-    const uint32_t rsh = (DYN && !RPF) ? (sub_arg >> 20) & 7u : 0u;  // range tail: K = 2^rsh ranges per pair
-    const uint32_t tail_c = !DYN ? 0u : rsh ? k2_range_tail_chunks(nch, nwaves, sub_shift)
-                                            : k2_tail_chunks(nch, nwaves, sub_shift, tail_q);
+    const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
-    const uint32_t nitems = n_full + (rsh ? (tail_c << (6u + rsh)) : (tail_c << tail_ish));
+    const uint32_t nitems = n_full + (tail_c << tail_ish);
     // Two ticket counters per segment: main items are taken with a prefetch (the next main ticket as an
     // item starts, waited for only at its end); tail items from their own counter only when a wave is
     // free. With one counter a prefetch made as a long main item started could reserve a tail item,
@@ -1263,15 +1250,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_last = tp_i;
             tp_items++;
         }
-        // a range item (range tail, k2_range_tail_chunks): 1/K of one pair's compared chunks; it counts its
-        // chunk's results with atomics like a split item (ish != 0)
-        const bool rng = rsh && tail;
+        const uint32_t ish = tail ? tail_ish : sub_shift;
         const uint32_t j = tail ? it - n_full : it;
-        const uint32_t ish = rng ? 1u : tail ? tail_ish : sub_shift;
-        const uint32_t p_r = ((c_begin + nch - tail_c) << 6) + (j >> rsh);
-        const uint32_t c = rng ? (p_r >> 6) : c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
-        const uint32_t per = rng ? 1u : 64u >> ish;
-        const uint32_t p0 = rng ? p_r : (c << 6) + (j & ((1u << ish) - 1u)) * per;
+        const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
+        const uint32_t per = 64u >> ish;
+        const uint32_t p0 = (c << 6) + (j & ((1u << ish) - 1u)) * per;
         if (p0 >= n) {
             if constexpr (DYN && RPF) {
                 if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
@@ -1334,19 +1317,14 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_s0 = wall_clock64();
             tp_pre += tp_s0 - tp_r;
         }
-        // a range item streams chunks [gs, ge) of its one pair (lane 0's row: every lane's prefix is that
-        // pair's count, so each chunk's owner is lane 0); a pair item streams all its pairs' chunks
-        const uint32_t K = 1u << rsh, rr = j & (K - 1u);
-        const uint32_t gs = rng ? (uint32_t)((uint64_t)total * rr / K) : 0u;
-        const uint32_t ge = rng ? (uint32_t)((uint64_t)total * (rr + 1u) / K) : total;
-        for (uint32_t base = gs; base < ge; base += 64u * U) {
+        for (uint32_t base = 0; base < total; base += 64u * U) {
             u32x4 va[U], vb[U];
             uint32_t own[U];
             bool st[U], act[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t g = base + (uint32_t)u * 64u + lane;
-                act[u] = g < ge;
+                act[u] = g < total;
                 uint32_t o = 0;  // owner = number of lanes whose inclusive prefix is <= g
 #pragma unroll
                 for (uint32_t s = 32; s >= 1; s >>= 1)
@@ -1393,17 +1371,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     }
                 }
             }
-        }
-        if (rng) {
-            // the ranges' mismatch bits meet in the pair's counter word caps[p] (done count | spec mismatches
-            // << 10 | status mismatches << 20; zeroed by the reset kernel); the wave that completes the last
-            // range decides and joins the pair below
-            uint32_t old = 0;
-            if (lane == 0) old = atomicAdd(caps + p0, 1u | ((uint32_t)(mis_s & 1ull) << 10) | ((uint32_t)(mis_t & 1ull) << 20));
-            old = uni(__builtin_amdgcn_readlane(old, 0));
-            if ((old & 0x3FFu) != K - 1u) continue;  // another range of the pair is still streaming
-            mis_s |= ((old >> 10) & 0x3FFu) ? 1ull : 0ull;
-            mis_t |= ((old >> 20) & 0x3FFu) ? 1ull : 0ull;
         }
         [[maybe_unused]] uint64_t tp_s1 = 0;
         if constexpr (PROF) {
@@ -1712,20 +1679,6 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
 constexpr uint64_t kK2BigPairBytes = 16384;
 constexpr uint32_t kK2ItemsPerWaveBig = 8, kK2MaxSubShiftBig = 6;
 
-// the range tail's log2 K for this launch (0 = off): DYN variants without the LDS row prefetch; by default
-// for large pairs (>= kK2BigPairBytes compared bytes on average: config4), K = 4; GPUDIFF_OPT_K2_RANGE_SHIFT
-// (tuning) turns it off or forces K = 4 / 8 for any batch
-static uint32_t k2_range_shift(const DiffBuffers& b, uint32_t v) {
-    if (!(v == 0 || v == 14 || v == 15)) return 0;
-    switch (b.k2_range_mode) {
-        case 1: return 0;
-        case 2: return 2;
-        case 3: return 3;
-        default: return b.avg_pair_bytes >= kK2BigPairBytes ? 2u : 0u;
-    }
-}
-
-
 // 64-pair chunks split into 2^k items until there are >= kK2ItemsPerWave items per resident wave
 // (config3's 156k chunks: k = 0; deep pairs: see above)
 static uint32_t k2_sub_shift(const DiffBuffers& b, uint32_t nchunks) {
@@ -1750,12 +1703,10 @@ uint32_t k2_grid_waves(const DiffBuffers& b, uint32_t nchunks) {
 // A pass's zeroing in one launch (hipMemsetAsync is a fill kernel each): the summary words (when the pass
 // starts with this K2 launch) and the chunk counts that split chunks accumulate with atomics
 __global__ __launch_bounds__(256) void k_pass_reset(uint32_t* __restrict__ summary, uint32_t nwords,
-                                                    uint4* __restrict__ cc, uint32_t ncc, uint32_t* __restrict__ caps,
-                                                    uint32_t ncaps) {
+                                                    uint4* __restrict__ cc, uint32_t ncc) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (summary && i < nwords) summary[i] = 0u;
     for (uint32_t j = i; j < ncc; j += gridDim.x * 256u) cc[j] = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t j = i; j < ncaps; j += gridDim.x * 256u) caps[j] = 0u;  // range tail: the per-pair counters
 }
 
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
@@ -1765,24 +1716,19 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const uint32_t sub = k2_sub_shift(b, c1 - c0);
     const uint32_t v = b.k2_variant & 15u;
     const uint32_t tq = k2_tail_q(b);
-    const uint32_t rsh = k2_range_shift(b, v);
-    const uint32_t tail = !k2_is_dyn(v) ? 0u : rsh ? k2_range_tail_chunks(c1 - c0, grid.x * 4u, sub)
-                                                   : k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq);
+    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq) : 0u;
     if (sub || tail || reset_summary) {  // split chunks accumulate their counts with atomics
         const uint32_t z0 = sub ? c0 : c1 - tail;
         const uint32_t ncc = c1 - z0;
-        // range tail: the tail pairs' counter words (caps) start at zero
-        const uint32_t p0 = (c1 - tail) << 6, p1 = std::min<uint32_t>(c1 << 6, b.n_pairs);
-        const uint32_t ncaps = (rsh && p1 > p0) ? p1 - p0 : 0u;
-        k_pass_reset<<<std::max(1u, std::min(1024u, (std::max(ncc, ncaps) + 255u) / 256u)), 256, 0, s>>>(
-            reset_summary ? b.summary : nullptr, kSummaryWords, cc + z0, ncc, b.caps + p0, ncaps);
+        k_pass_reset<<<std::max(1u, std::min(1024u, (ncc + 255u) / 256u)), 256, 0, s>>>(
+            reset_summary ? b.summary : nullptr, kSummaryWords, cc + z0, ncc);
     }
     // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
     const uint32_t slice = b.arena_per_wave / nsegs;
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
-                   ((b.k2_deep_mode & 3u) << 18) | (rsh << 20)
+                   ((b.k2_deep_mode & 3u) << 18)
     k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();

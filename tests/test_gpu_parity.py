@@ -341,13 +341,10 @@ def test_k2_variants_bit_exact(variant):
         e.close()
 
 
-@pytest.mark.parametrize("tail_flags", [0x10, 0x50, 0x80, 0x10 | (1 << 28), 2 << 1, 3 << 1, (3 << 1) | (3 << 21)],
-                         ids=["no_tail_late", "tail4q", "tail8", "no_tail_ipw4", "range4", "range8", "range8_defer"])
+@pytest.mark.parametrize("tail_flags", [0x10, 0x50, 0x80, 0x10 | (1 << 28)], ids=["no_tail_late", "tail4q", "tail8", "no_tail_ipw4"])
 def test_k2_tail_tunings_bit_exact(tail_flags):
     """K2's work hand-out variants (GPUDIFF_OPT_K2_TAIL_SHIFT / _K2_TAIL8 / items per wave): main and
-    tail tickets, late fetch, 8-pair or half-size tail items, the range tail (K = 4 / 8 ranges per tail pair,
-    their mismatches merged through the pair's counter word; also with every join deferred) -- identical
-    results, against the oracle."""
+    tail tickets, late fetch, 8-pair or half-size tail items -- identical results, against the oracle."""
     pairs, _, _ = make_pairs(6000, seed=33, mutate_frac=0.2, pretty_frac=0)
     e = G.Engine(device=0, flags=tail_flags)
     res = e.diff_pairs(pairs)
@@ -355,15 +352,14 @@ def test_k2_tail_tunings_bit_exact(tail_flags):
     e.close()
 
 
-@pytest.mark.parametrize("mode", ["slices", "fused", "slices_all", "range4", "range_off"])
+@pytest.mark.parametrize("mode", ["slices", "fused", "slices_all"])
 def test_deep_joins_merge_path(mode):
     """Joins over 2048 keys go to K4's merge-path slices (1024 merged keys each: several slices per
     region, equal keys straddling slice boundaries, list shifts with thousands of changed paths);
     "fused": GPUDIFF_OPT_K2_FUSE_DEEP keeps them in K2; "slices_all": a shrunken K2 arena sends every
     dirty pair, small ones included, through the slices.  Flags, IDs and paths equal the oracle's."""
     pairs = deep_pairs() + make_pairs(300, seed=43, mutate_frac=0.4)[0]
-    # range4 / range_off: the decision kernel's range tail forced on (K = 4) / off (GPUDIFF_OPT_K2_RANGE_SHIFT)
-    flags = {"slices": 0, "fused": G.OPT_K2_FUSE_DEEP, "slices_all": 14 << 21, "range4": 2 << 1, "range_off": 1 << 1}[mode]
+    flags = {"slices": 0, "fused": G.OPT_K2_FUSE_DEEP, "slices_all": 14 << 21}[mode]
     e = G.Engine(device=0, flags=flags)
     assert_matches(e.diff_pairs(pairs), pairs)
     e.close()
