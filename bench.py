@@ -163,11 +163,15 @@ def main():
     ap.add_argument("--gather-depth", type=int, default=1,
                     help="N > 1: all-gathers in flight; 2 = pipelined (step s's collective overlaps step s+1's "
                          "diff; measured 2.4%% slower than serial at world size 1 on MI355X, profiles/r02zd)")
-    ap.add_argument("--pipeline", type=int, default=1, choices=[1, 2],
-                    help="2 = two diff passes in flight: a second context (own stream) diffs a view of the resident "
-                         "batch (gpudiff_dbatch_create_view) on alternate steps, so one pass's decision kernel "
-                         "fills the CUs the previous pass's tail frees and that pass's compaction, joins and "
-                         "collective (shard.PipelinedGather) run beside it; every step still a complete pass")
+    ap.add_argument("--pipeline", type=int, default=2, choices=[1, 2],
+                    help="2 (default) = two diff passes in flight: a second context (own stream) diffs a view of the "
+                         "resident batch (gpudiff_dbatch_create_view) on alternate steps, so one pass's decision "
+                         "kernel fills the CUs the previous pass's tail frees and that pass's compaction, joins and "
+                         "collective (shard.PipelinedGather) run beside it; every step is still a complete pass.  "
+                         "The roofline's kernel times then come from isolated passes after the timed loop.  "
+                         "1 = one pass at a time (the kernel times are the timed loop's)")
+    ap.add_argument("--calib-passes", type=int, default=6,
+                    help="--pipeline 2: isolated diff passes after the timed loop that time the kernels (roofline)")
     ap.add_argument("--no-gather-lookahead", action="store_true",
                     help="N > 1 (RCCL, depth 1): read each step's gathered counts before enqueueing the next pass "
                          "(the default checks step s after step s + 1 is queued, regrowing from the engine's "
@@ -458,6 +462,13 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if args.pipeline == 2:
+        # the timed loop overlaps passes, so a kernel's event span there includes waiting for CUs the other
+        # pass holds: the roofline's kernel times come from isolated passes of the same batch (untimed)
+        eng.timing_reset()
+        for _ in range(args.calib_passes):
+            eng.diff(db)
+            eng.sync()
     tm = eng.timings()
     log("timed region: %d steps in %.3f s" % (args.steps, dt))
     gather_check = None
@@ -513,12 +524,14 @@ def main():
             if pm.get("k2_source_hash") == src_hash and pm.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
                 cand.append(f)
         tj = cand[-1] if cand else ""
+    traffic_box = traffic_rocprof_ms = None
     if tj and tj != "none" and os.path.exists(tj):
         with open(tj) as f:
             pmc = json.load(f)
         # comparable only on the same K2 sources and the same workload (format bytes per launch)
         if pmc.get("k2_source_hash") == src_hash and pmc.get("algorithmic_bytes_per_launch") == fmt_bytes / launches:
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), os.path.relpath(tj, ROOT)
+            traffic_box, traffic_rocprof_ms = pmc.get("box"), pmc.get("rocprof_avg_ms")
 
     for d in dbs[1:]:
         d.free()  # views before their base
@@ -592,8 +605,17 @@ def main():
                                            "size-matched segments (16 B per leaf record: value u64 = the value's first 8 bytes, 32-bit path hash, meta; + the arena: long strings' tails past 8 bytes, 4-B aligned, padded to 16)"},
                          "diff_pass": {"ms": pass_ms, "achieved": achieved_pass, "frac": achieved_pass / HBM_PEAK_GBPS,
                                        "def": "SURVEY bytes over the whole diff pass (K2..K6)"},
-                         "k2_source_hash": src_hash},
-            "kernels_ms": {"compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,
+                         "k2_source_hash": src_hash,
+                         # the physical rate: HBM counter bytes (FETCH_SIZE x 2 + WRITE_SIZE per K2 launch) over
+                         # this run's K2 time -- what the memory system moved, whatever the byte definition
+                         "frac_physical": (traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic and k2_ms else None,
+                         "frac_physical_def": "PMC traffic per K2 launch / K2 HIP-event time / 8 TB/s",
+                         "survey_over_format_bytes": survey_bytes / fmt_bytes if fmt_bytes else None,
+                         "traffic_box": traffic_box, "traffic_rocprof_k2_ms": traffic_rocprof_ms,
+                         "box": box_id()},
+            "kernels_ms": {"source": ("%d isolated passes after the timed loop (the loop overlaps two passes)"
+                                      % args.calib_passes) if args.pipeline == 2 else "the timed loop's passes",
+                           "compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,
                            "join_exposed": tm.join_ms, "emit": tm.emit_ms, "diff_pass": tm.total_ms,
                            "passes": tm.n_passes},
             "cpu_baseline": cpu,
@@ -601,10 +623,24 @@ def main():
             "checks": {"full_size": full_check, "sample": sample_check, "three_way": three_way,
                        "gather": gather_check},
             "ingest_s": t_gen,
+            "box": box_id(),
         }
         print(json.dumps(line), flush=True)
     if collective:
         dist.destroy_process_group()
+
+
+def box_id():
+    """The machine this run measured on (hostname + the GPU's PCI bus id): a roofline whose counters were
+    taken on another box says so."""
+    import socket
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(torch.cuda.current_device())
+        bus = "%s/%s" % (getattr(p, "pci_bus_id", "?"), getattr(p, "pci_device_id", "?"))
+    except Exception:
+        bus = "?"
+    return "%s:%s" % (socket.gethostname(), bus)
 
 
 def _mix64(x):
@@ -727,8 +763,32 @@ def json_in_rates(G, pop, m, threads, device):
         best = min(times)
         out[mode] = dict(pairs_per_s=m / best, ms=best * 1e3, json_gb_per_s=int(offs[-1]) / best / 1e9)
         e.close()
+        if mode == "device_encode":
+            out[mode]["phases_ms"] = json_in_phases(G, arr, m, threads, device)
     out["modes_agree"] = bool(np.array_equal(flags["host_encode"], flags["device_encode"]))
     return out
+
+
+def json_in_phases(G, arr, m, threads, device):
+    """Where a device-encoded JSON-in batch's time goes (separate runs with GPUDIFF_OPT_TIMING; the events
+    are not in the timed runs above): the host side of gpudiff_submit (document tables, the JSON copy into
+    pinned staging, the enqueue), the H2D copy, K0 (tokenize + encode), K0c + K0x, the diff pass (K2..K6)
+    and the store's part of gpudiff_wait.  Copy stream and kernels overlap by chunk, so the GPU phases can
+    sum to more than the end-to-end time."""
+    e = G.Engine(device=device, encode_threads=threads, device_encode=True, timing=True)
+    e.wait(e.submit_array(arr))
+    e.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        e.wait(e.submit_array(arr))
+    wall = (time.perf_counter() - t0) / 3 * 1e3
+    st = e.submit_stats()
+    tm = e.timings()
+    e.close()
+    return dict(end_to_end=wall, host_submit=st.host_submit_ms, host_tables=st.submit_docs_ms,
+                host_staging_copy=st.submit_copy_ms, host_enqueue=st.submit_enqueue_ms, h2d=st.h2d_ms,
+                k0_encode=st.encode_ms, k0c_k0x=st.link_ms, diff_pass=tm.total_ms, wait_finish=st.finish_ms,
+                batches=int(st.timing_batches), deferred_to_host=int(st.deferred))
 
 
 def cpu_legs(G, eng, pop, n, pop_flags, args, aff, nproc, quota):

@@ -381,6 +381,10 @@ int gpudiff_store_submit(gpudiff_ctx* ctx, gpudiff_store* st, const gpudiff_even
 /* Delete event: the slot is empty again */
 int gpudiff_store_forget(gpudiff_ctx* ctx, gpudiff_store* st, uint32_t slot);
 int gpudiff_store_stats_get(const gpudiff_store* st, gpudiff_store_stats* out);
+/* The same statistics for gpudiff_submit's device-encode path (GPUDIFF_OPT_DEVICE_ENCODE: the context's
+ * pair-mode store), e.g. the per-phase times of JSON-in with GPUDIFF_OPT_TIMING; GPUDIFF_E_STATE before the
+ * context's first device-encoded submit. */
+int gpudiff_submit_stats_get(gpudiff_ctx* ctx, gpudiff_store_stats* out);
 void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
 
 /* ---- object encoding in the device-store format (inspection / parity) ----

@@ -773,6 +773,7 @@ int gpudiff_timing_reset(gpudiff_ctx* c) {
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->n_pass = 0;
+    if (c->pair_store) dstore_timing_reset(c->pair_store);
     return GPUDIFF_OK;
 }
 

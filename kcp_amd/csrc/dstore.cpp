@@ -904,6 +904,18 @@ int dstore_submit_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n
     return dstore_submit(c, s, ev.data(), n, ticket);
 }
 
+void dstore_timing_reset(DStore* s) {
+    for (double& x : s->t_sum) x = 0;
+    for (double& x : s->t_sub) x = 0;
+    s->t_n = 0;
+}
+
+extern "C" int gpudiff_submit_stats_get(gpudiff_ctx* c, gpudiff_store_stats* out) {
+    if (!c || !out) return GPUDIFF_E_INVAL;
+    if (!c->pair_store) return GPUDIFF_E_STATE;
+    return dstore_stats(c->pair_store, out);
+}
+
 int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot) {
     HIPCHK(launch_forget(c->stream, s->slots, slot, s->ctr));
     s->seen[slot] = 0;

@@ -12,6 +12,7 @@ int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot);
 // GPUDIFF_E_CAPACITY = take the host-encode path for this batch
 int dstore_submit_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n, gpudiff_ticket* ticket);
 int dstore_stats(const DStore* s, gpudiff_store_stats* out);
+void dstore_timing_reset(DStore* s);  // gpudiff_timing_reset: the submit path's phase sums too
 void dstore_free(gpudiff_ctx* c, DStore* s);
 
 // The staged JSON of a waited pair-mode batch (gpudiff_submit with GPUDIFF_OPT_DEVICE_ENCODE): pair i's

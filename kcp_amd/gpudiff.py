@@ -234,6 +234,7 @@ SIGNATURES = [
     ("gpudiff_store_submit", C.c_int, [_P, _P, C.POINTER(Event), C.c_size_t, C.POINTER(C.c_uint64)]),
     ("gpudiff_store_forget", C.c_int, [_P, _P, C.c_uint32]),
     ("gpudiff_store_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
+    ("gpudiff_submit_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
     ("gpudiff_store_free", None, [_P, _P]),
     ("gpudiff_encode_objects", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                                          C.c_size_t, C.c_void_p, C.c_uint64, C.POINTER(ObjInfo)]),
@@ -674,6 +675,12 @@ class Engine:
         held[ticket] = bufs
         for t in sorted(held)[:-2]:
             del held[t]
+
+    def submit_stats(self) -> StoreStats:
+        """gpudiff_submit_stats_get: the device-encode submit path's statistics (phase times with timing)."""
+        st = StoreStats()
+        _chk(_lib.gpudiff_submit_stats_get(self.ctx, C.byref(st)), "gpudiff_submit_stats_get")
+        return st
 
     def submit_array(self, arr: np.ndarray) -> int:
         """gpudiff_submit over a JSON_PAIR_DTYPE table (json_pair_array)."""

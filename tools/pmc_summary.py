@@ -66,6 +66,10 @@ def main():
         hbm_bytes_per_launch=k2.get("hbm_bytes"),
         traffic_over_algorithmic=(k2["hbm_bytes"] / alg) if k2.get("hbm_bytes") else None,
         rocprof_avg_ms=k2.get("avg_ms"),
+        # the physical rate: counter bytes over rocprof's kernel time (the box that measured both)
+        frac_physical=((k2["hbm_bytes"] / (k2["avg_ms"] * 1e-3) / 1e9 / 8000.0)
+                       if k2.get("hbm_bytes") and k2.get("avg_ms") else None),
+        box=bench.get("box"),
         bench_hip_event_avg_ms=bench["roofline"]["avg_launch_ms"],
         note="FETCH_SIZE x2 (gfx950 half-count of 16-B/lane reads) + WRITE_SIZE, KiB -> bytes; "
              "separate --pmc passes; scalar row loads are counted at the doubled rate too",

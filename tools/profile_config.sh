@@ -10,11 +10,11 @@ export TMPDIR=/tmp
 B="$ROOT/bench.py"
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
-    python3 "$B" --config "$CFG" --no-cpu-baseline --sample 0 --json-in-pairs 0 --steps 10 > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
+    python3 "$B" --pipeline 1 --config "$CFG" --no-cpu-baseline --sample 0 --json-in-pairs 0 --steps 10 > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 "$B" --config "$CFG" --no-cpu-baseline --sample 0 --json-in-pairs 0 --steps 2 --warmup 1 > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.log"
+    python3 "$B" --pipeline 1 --config "$CFG" --no-cpu-baseline --sample 0 --json-in-pairs 0 --steps 2 --warmup 1 > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.log"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
-    python3 "$B" --config "$CFG" --no-cpu-baseline --sample 0 --json-in-pairs 0 --steps 2 --warmup 1 > "$OUT/write_bench.json" 2> "$OUT/write_bench.log"
+    python3 "$B" --pipeline 1 --config "$CFG" --no-cpu-baseline --sample 0 --json-in-pairs 0 --steps 2 --warmup 1 > "$OUT/write_bench.json" 2> "$OUT/write_bench.log"
 cd "$ROOT"
 for d in kt fetch write; do
     f=$(find "$OUT/$d" -name 'run_*.csv' | head -n 1 || true)

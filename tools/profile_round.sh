@@ -20,11 +20,11 @@ timeout -k 10 600 python3 "$B" > "$OUT/bench.json" 2> "$OUT/bench.log"
 cat "$OUT/bench.json"
 cd /tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- \
-    python3 "$B" --no-cpu-baseline --sample 0 --steps 10 > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
+    python3 "$B" --pipeline 1 --no-cpu-baseline --sample 0 --steps 10 > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.log"
 timeout -k 10 500 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 "$B" --no-cpu-baseline --sample 0 --steps 2 --warmup 1 > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.log"
+    python3 "$B" --pipeline 1 --no-cpu-baseline --sample 0 --steps 2 --warmup 1 > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.log"
 timeout -k 10 500 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
-    python3 "$B" --no-cpu-baseline --sample 0 --steps 2 --warmup 1 > "$OUT/write_bench.json" 2> "$OUT/write_bench.log"
+    python3 "$B" --pipeline 1 --no-cpu-baseline --sample 0 --steps 2 --warmup 1 > "$OUT/write_bench.json" 2> "$OUT/write_bench.log"
 cd "$ROOT"
 # rocprofv3 may nest its files under host/pid directories: flatten
 for d in kt fetch write; do
