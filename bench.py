@@ -163,13 +163,13 @@ def main():
     ap.add_argument("--gather-depth", type=int, default=1,
                     help="N > 1: all-gathers in flight; 2 = pipelined (step s's collective overlaps step s+1's "
                          "diff; measured 2.4%% slower than serial at world size 1 on MI355X, profiles/r02zd)")
-    ap.add_argument("--pipeline", type=int, default=2, choices=[1, 2],
+    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1, 2],
                     help="2 (default) = two diff passes in flight: a second context (own stream) diffs a view of the "
                          "resident batch (gpudiff_dbatch_create_view) on alternate steps, so one pass's decision "
                          "kernel fills the CUs the previous pass's tail frees and that pass's compaction, joins and "
                          "collective (shard.PipelinedGather) run beside it; every step is still a complete pass.  "
                          "The roofline's kernel times then come from isolated passes after the timed loop.  "
-                         "1 = one pass at a time (the kernel times are the timed loop's)")
+                         "1 = one pass at a time (the kernel times are the timed loop's); 0 = 2, or 1 with gloo")
     ap.add_argument("--calib-passes", type=int, default=6,
                     help="--pipeline 2: isolated diff passes after the timed loop that time the kernels (roofline)")
     ap.add_argument("--no-gather-lookahead", action="store_true",
@@ -215,6 +215,8 @@ def main():
     ap.add_argument("--print-launch", action="store_true",
                     help="print the launch command --gpus N resolves to (one process per GPU) and exit")
     args = ap.parse_args(argv)
+    if not args.pipeline:
+        args.pipeline = 1 if args.dist_backend == "gloo" else 2
     self_launch(args, argv)
     claim_stdout()
     if args.gpus > 1 and args.config not in ("config1", "config2", "config3", "config4"):
