@@ -120,6 +120,9 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     }
     b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
     b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
+    b.tail_perm = d->tail_perm;
+    b.tail_perm_key = &d->tail_perm_key;
+    b.k2_no_lpt = (c->flags & GPUDIFF_OPT_K2_NO_LPT) ? 1u : 0u;
     b.gather_send = d->gather_send;
     b.gather_cap_spec = d->gather_cap_spec;
     b.gather_cap_status = d->gather_cap_status;
@@ -456,7 +459,8 @@ static int alloc_outputs(gpudiff_dbatch* d) {
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
         (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) || (rc = dalloc(&d->nbits, np)) ||
         (rc = dalloc(&d->noop_d, np)) ||
-        (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments))) {
+        (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments)) ||
+        (rc = dalloc(&d->tail_perm, 8192))) {
         d->chunk_counts = cc;
         return rc;
     }

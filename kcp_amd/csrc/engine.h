@@ -109,6 +109,8 @@ struct gpudiff_dbatch {
     // refreshed at every diff) into its own outputs, so two passes over one population can be in flight
     const gpudiff_dbatch* base = nullptr;
     int device = -1;
+    uint32_t* tail_perm = nullptr;  // K2's largest-first final round (kernels.h DiffBuffers)
+    uint64_t tail_perm_key = ~0ull;
 };
 
 struct DStore;
@@ -183,7 +185,7 @@ inline void dfree_all(gpudiff_dbatch* d) {
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
                   d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
                   d->scratch_h, d->scratch_k, d->out_h, d->out_k, d->nbits, d->noop_d, d->slot_owner,
-                  d->slice_cnt, d->slice_weq, d->ids_alt[0], d->ids_alt[1]};
+                  d->slice_cnt, d->slice_weq, d->ids_alt[0], d->ids_alt[1], d->tail_perm};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);

@@ -54,6 +54,9 @@ struct DiffBuffers {
     uint32_t k2_blocks_per_cu;  // tuning: 0 = the variant's occupancy (4 resident 256-thread blocks per CU)
     uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default
     uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
+    uint32_t* tail_perm;        // K2's largest-first final round: its order (device, kK2LptMax u32)
+    uint64_t* tail_perm_key;    // (host) the launch shape tail_perm was computed for
+    uint32_t k2_no_lpt;         // tuning (GPUDIFF_OPT_K2_NO_LPT): the final round in index order
     uint64_t avg_pair_bytes;    // format bytes K2 reads per pair, averaged over the batch (0: unknown)
     uint32_t k4_pipelined;      // tuning (GPUDIFF_OPT_K4_PIPELINED_JOIN): K4's slices with join_region_pl
     uint32_t* gather_send;      // gpudiff_dbatch_bind_gather: K3 also writes counts + IDs here (nullptr: unbound)

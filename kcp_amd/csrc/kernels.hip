@@ -1010,7 +1010,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
                                                  uint32_t arena_off, uint32_t arena_per_wave, uint32_t arena_stride,
                                                  uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
                                                  uint8_t* __restrict__ nbits, uint64_t mask,
-                                                 uint32_t* __restrict__ summary, uint32_t sub_arg) {
+                                                 uint32_t* __restrict__ summary, uint32_t sub_arg,
+                                                 const uint32_t* __restrict__ tail_perm) {
+    (void)tail_perm;
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -1100,6 +1102,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // DYN variants: chunks at the end of a launch handed out as 8-pair items (about
 // four per wave), unless the whole launch is split already
 // a tail of q quarters of the launch's wave count, in 64-pair chunks
+// items of the largest-first final round: one per resident wave, at most half the launch's main items
+__host__ __device__ inline uint32_t k2_lpt_round(uint32_t n_full, uint32_t nwaves) {
+    const uint32_t r = nwaves < n_full / 2u ? nwaves : n_full / 2u;
+    return r < 2u ? 0u : r;
+}
 __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t q) {
     return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * q);
 }
@@ -1150,7 +1157,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                                                       uint32_t arena_per_wave, uint32_t arena_stride,
                                                       uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
                                                       uint8_t* __restrict__ nbits, uint64_t mask,
-                                                      uint32_t* __restrict__ summary, uint32_t sub_arg) {
+                                                      uint32_t* __restrict__ summary, uint32_t sub_arg,
+                                                      const uint32_t* __restrict__ tail_perm) {
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -1211,6 +1219,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
     const uint32_t nitems = n_full + (tail_c << tail_ish);
+    // largest-first final round (k2_lpt_round; large pairs): the last lpt_r main items are handed out by the
+    // tail counter in tail_perm's order -- by descending bytes -- so the launch ends with its smallest items;
+    // the bulk stays in index order (neighbouring waves stream neighbouring pool bytes)
+    const uint32_t lpt_r = (DYN && !RPF && tail_perm && tail_c == 0u) ? k2_lpt_round(n_full, nwaves) : 0u;
+    const uint32_t n_main = n_full - lpt_r;
     // Two ticket counters per segment: main items are taken with a prefetch (the next main ticket as an
     // item starts, waited for only at its end); tail items from their own counter only when a wave is
     // free. With one counter a prefetch made as a long main item started could reserve a tail item,
@@ -1218,18 +1231,18 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     // (the last ~0.13 ms of a 10M-pair pass, tools/k2_wave_profile.py).
     uint32_t* const ctr = summary + 8u + (arena_per_wave ? arena_off / arena_per_wave : 0u);
     uint32_t* const ctr_tail = ctr + kK2TailCounters;
-    const uint32_t tail0 = max(n_full, nwaves);  // the first item the tail counter hands out
+    const uint32_t tail0 = max(n_main, nwaves);  // the first item the tail counter hands out
     // late fetch: the last two rounds of main items take their next ticket when they are done, so
     // no ticket waits behind a long item at the end of the pass (the others prefetch as they start)
-    const uint32_t pf_end = late ? (n_full > 2u * nwaves ? n_full - 2u * nwaves : 0u) : n_full;
+    const uint32_t pf_end = late ? (n_main > 2u * nwaves ? n_main - 2u * nwaves : 0u) : n_main;
     auto advance = [&](uint32_t cur, uint32_t tk) -> uint32_t {
         if constexpr (!DYN) {
             return cur + nwaves;
         } else {
-            if (cur < n_full) {
+            if (cur < n_main) {
                 if (cur >= pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
                 const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
-                if (nx < n_full) return nx;
+                if (nx < n_main) return nx;
             }
             uint32_t tt = 0;
             if (lane == 0) tt = atomicAdd(ctr_tail, 1u);
@@ -1237,7 +1250,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         }
     };
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
-        const bool tail = it >= n_full;
+        // the item this ticket stands for: in the largest-first round, the permuted main item
+        const uint32_t im = (lpt_r && it >= n_main && it < n_full) ? n_main + tail_perm[it - n_main] : it;
+        const bool tail = im >= n_full;
         // the next main ticket: fetched while this item streams (with RPF only after this item's rows are
         // read from LDS -- the LDS read waits on vmcnt, which would otherwise wait for the atomic's return)
         if constexpr (DYN && !RPF) {
@@ -1251,7 +1266,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_items++;
         }
         const uint32_t ish = tail ? tail_ish : sub_shift;
-        const uint32_t j = tail ? it - n_full : it;
+        const uint32_t j = tail ? im - n_full : im;
         const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
         const uint32_t per = 64u >> ish;
         const uint32_t p0 = (c << 6) + (j & ((1u << ish) - 1u)) * per;
@@ -1620,7 +1635,7 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
 // The decision kernel of each tuning variant (GPUDIFF_OPT_K2_VARIANT_SHIFT; 0 = the default).
 typedef void (*K2Fn)(const gpudiff_pair_row*, const uint8_t*, uint32_t, uint8_t*, uint32_t*, uint4*, uint32_t, uint32_t,
                      uint64_t*, uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t*, uint32_t*, uint8_t*, uint64_t,
-                     uint32_t*, uint32_t);
+                     uint32_t*, uint32_t, const uint32_t*);
 static K2Fn k2_kernel(uint32_t variant) {
     switch (variant) {
         case 1: return k_compare<false, 4, 1>;
@@ -1651,6 +1666,7 @@ static bool k2_is_dyn(uint32_t variant) {
     }
 }
 
+constexpr uint32_t kK2LptMax = 8192;  // largest-first round: at most this many items (one per resident wave)
 constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
 constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
@@ -1709,6 +1725,68 @@ __global__ __launch_bounds__(256) void k_pass_reset(uint32_t* __restrict__ summa
     for (uint32_t j = i; j < ncc; j += gridDim.x * 256u) cc[j] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// bytes K2 streams for a pair (the rule of its n1 / n2 chunk counts; gpudiff_pair_compare_bytes on the host)
+__device__ __forceinline__ uint64_t pair_stream_bytes(const gpudiff_pair_row& r) {
+    if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) return 65u;
+    const bool spec_sz = r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b;
+    const bool stat_sz = (r.flags_b & GPUDIFF_OBJ_HAS_STATUS) && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b;
+    const uint64_t seg_s = seg_bytes(r.spec_l_a, r.spec_ar_a), seg_t = seg_bytes(r.stat_l_a, r.stat_ar_a);
+    uint64_t per = 0;
+    if (spec_sz && stat_sz) per = (seg_s + seg_t + 127u) & ~127ull;
+    else if (spec_sz) per = (r.stat_l_a | r.stat_l_b | r.stat_ar_a | r.stat_ar_b) ? seg_s : (seg_s + 127u) & ~127ull;
+    else if (stat_sz) per = seg_t;
+    return 65u + 2u * per;
+}
+
+// The largest-first final round's order (items of large pairs): one block sorts the last round's main items
+// by their compared bytes, descending (ties by index), into perm (offsets from the round's first item).
+// Cached per batch by the host (launch_compare): the order depends only on the rows and the launch shape, and
+// any permutation is correct -- a stale one only orders the round less well.
+__global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __restrict__ rows, uint32_t n,
+                                                     uint32_t c_begin, uint32_t n_main, uint32_t r,
+                                                     uint32_t sub_shift, uint32_t* __restrict__ perm) {
+    __shared__ uint64_t key[kK2LptMax];
+    const uint32_t per = 64u >> sub_shift;
+    uint32_t m2 = 1;
+    while (m2 < r) m2 <<= 1;
+    for (uint32_t t = threadIdx.x; t < m2; t += blockDim.x) {
+        uint64_t bytes = 0;
+        if (t < r) {
+            const uint32_t m = n_main + t;
+            const uint32_t p0 = ((c_begin + (m >> sub_shift)) << 6) + (m & ((1u << sub_shift) - 1u)) * per;
+            for (uint32_t p = p0; p < min(p0 + per, n); p++) bytes += pair_stream_bytes(rows[p]);
+        }
+        // descending bytes, ascending index: sort ascending on (~bytes, t); padding sorts last
+        key[t] = t < r ? ((~bytes & 0xFFFFFFFFFFull) << 20) | t : ~0ull;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= m2; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < m2; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = key[i], bb = key[l];
+                    if (((i & k) == 0) == (a > bb)) {
+                        key[i] = bb;
+                        key[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t t = threadIdx.x; t < r; t += blockDim.x) perm[t] = (uint32_t)(key[t] & 0xFFFFFu);
+}
+
+// the launch's largest-first round (0 = none): large pairs only, DYN variants without the LDS row prefetch,
+// no pair-split tail (k2_tail_chunks() == 0: the items of large pairs are split to 1-2 pairs already)
+static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uint32_t nwaves, uint32_t sub,
+                             uint32_t tail) {
+    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 0 || v == 14 || v == 15)) return 0;
+    if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
+    const uint32_t r = k2_lpt_round(nch << sub, nwaves);
+    return r <= kK2LptMax ? r : 0;
+}
+
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
                           uint32_t nsegs, bool reset_summary) {
     const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
@@ -1717,6 +1795,18 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const uint32_t v = b.k2_variant & 15u;
     const uint32_t tq = k2_tail_q(b);
     const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq) : 0u;
+    const uint32_t lpt = nsegs == 1 ? k2_lpt_items(b, v, c1 - c0, grid.x * 4u, sub, tail) : 0u;
+    const uint32_t* perm = nullptr;
+    if (lpt) {
+        const uint32_t n_full = (c1 - c0) << sub;
+        const uint64_t key = ((uint64_t)b.n_pairs << 32) ^ ((uint64_t)lpt << 12) ^ ((uint64_t)sub << 8) ^ c0 ^
+                             ((uint64_t)(uintptr_t)b.rows << 7);
+        if (*b.tail_perm_key != key) {
+            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, c0, n_full - lpt, lpt, sub, b.tail_perm);
+            *b.tail_perm_key = key;
+        }
+        perm = b.tail_perm;
+    }
     if (sub || tail || reset_summary) {  // split chunks accumulate their counts with atomics
         const uint32_t z0 = sub ? c0 : c1 - tail;
         const uint32_t ncc = c1 - z0;
@@ -1728,7 +1818,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
-                   ((b.k2_deep_mode & 3u) << 18)
+                   ((b.k2_deep_mode & 3u) << 18), perm
     k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();

@@ -352,6 +352,30 @@ def test_k2_tail_tunings_bit_exact(tail_flags):
     e.close()
 
 
+@pytest.mark.parametrize("lpt", [True, False], ids=["largest_first", "index_order"])
+def test_k2_largest_first_round(lpt):
+    """Large pairs (>= 16 KiB compared on average): K2's final round of items is handed out largest first
+    (k_tail_order's permutation, cached per batch) or in index order (GPUDIFF_OPT_K2_NO_LPT); repeated
+    passes over the same batch (the cached order) and over a view (its own order): identical results,
+    against the oracle."""
+    pairs, _, _ = make_pairs(900, seed=61, mix=(("crd", 1.0),), mutate_frac=0.4, crd_leaves=2500, pretty_frac=0)
+    e = G.Engine(device=0, flags=0 if lpt else G.OPT_K2_NO_LPT)
+    hb = e.encode(pairs)
+    assert hb.info().pool_bytes / len(pairs) > 2 * 16384  # the large-pair path
+    db = e.device_batch(hb.info().pool_bytes + 4096, len(pairs))
+    db.append(hb)
+    exp = assert_matches(e.wait(e.diff(db)), pairs)
+    assert_matches(e.wait(e.diff(db)), pairs, exp=exp)
+    e2 = G.Engine(device=0, flags=0 if lpt else G.OPT_K2_NO_LPT)
+    v = db.view(e2)
+    assert_matches(e2.wait(e2.diff(v)), pairs, exp=exp)
+    v.free()
+    db.free()
+    hb.free()
+    e2.close()
+    e.close()
+
+
 @pytest.mark.parametrize("mode", ["slices", "fused", "slices_all"])
 def test_deep_joins_merge_path(mode):
     """Joins over 2048 keys go to K4's merge-path slices (1024 merged keys each: several slices per
