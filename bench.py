@@ -753,8 +753,10 @@ def json_in_rates(G, pop, m, threads, device):
     arr = G.json_pair_array(buf, offs)
     out = dict(sample_pairs=m, json_bytes=int(offs[-1]), threads=threads)
     flags = {}
-    for mode in ("host_encode", "device_encode"):
-        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode == "device_encode"))
+    # device_encode_h2d2: the same with GPUDIFF_OPT_H2D_TWO_STREAMS (JSON chunks alternate two copy streams)
+    for mode in ("host_encode", "device_encode", "device_encode_h2d2"):
+        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode != "host_encode"),
+                     flags=G.OPT_H2D_TWO_STREAMS if mode == "device_encode_h2d2" else 0)
         r = e.wait(e.submit_array(arr))  # warm: staging and scratch allocations
         times = []
         for _ in range(3):
@@ -767,7 +769,8 @@ def json_in_rates(G, pop, m, threads, device):
         e.close()
         if mode == "device_encode":
             out[mode]["phases_ms"] = json_in_phases(G, arr, m, threads, device)
-    out["modes_agree"] = bool(np.array_equal(flags["host_encode"], flags["device_encode"]))
+    out["modes_agree"] = bool(np.array_equal(flags["host_encode"], flags["device_encode"]) and
+                              np.array_equal(flags["host_encode"], flags["device_encode_h2d2"]))
     return out
 
 

@@ -98,9 +98,11 @@ enum {
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
 #define GPUDIFF_OPT_K4_PIPELINED_JOIN 0x8u /* tuning: K4's merge-path slices prefetch the next window's keys and
                                               metas (software-pipelined join) */
-/* bit 0x2 is reserved: until ABI 3 it (and 0x4, 0x8, bits 30-31) chose where long-value digests were computed;
-   since ABI 4 the format has no digests (include/gpudiff_format.h: a long string's first 8 bytes sit in its
-   leaf record, the rest in the arena) and it is ignored */
+/* bits 0x2 / 0x4: until ABI 3 they (and 0x8, bits 30-31) chose where long-value digests were computed; since ABI
+   4 the format has no digests (include/gpudiff_format.h: a long string's first 8 bytes sit in its leaf record,
+   the rest in the arena); now two tuning bits: */
+#define GPUDIFF_OPT_H2D_TWO_STREAMS 0x2u /* tuning: device-encode uploads alternate JSON chunks between two copy
+                                           streams (DMA queues) */
 #define GPUDIFF_OPT_K2_NO_LPT 0x4u      /* tuning: the decision kernel's final round of items in index order (the
                                            default hands it out largest first when pairs are large) */
 /* tuning knobs (A/B measurements; 0 = defaults) */

@@ -86,6 +86,8 @@ struct DStore {
     DSlot* slots = nullptr;
     uint32_t* ctr = nullptr;  // kCtrLive, kCtrLiveBytes
     hipStream_t cs = nullptr;  // H2D of the next batch overlaps K0 of the current one
+    hipStream_t cs2 = nullptr; // GPUDIFF_OPT_H2D_TWO_STREAMS: odd JSON chunks upload here (a second DMA queue)
+    hipEvent_t cs2_done = nullptr;
     uint64_t* sizes = nullptr;
     uint64_t* tile_sums = nullptr;
     uint8_t* scratch = nullptr;
@@ -578,6 +580,10 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
             return fail(GPUDIFF_E_DEVICE);
     }
     if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+    if ((c->flags & GPUDIFF_OPT_H2D_TWO_STREAMS) &&
+        (hipStreamCreateWithFlags(&s->cs2, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&s->cs2_done, hipEventDisableTiming) != hipSuccess))
+        return fail(GPUDIFF_E_DEVICE);
     if ((rc = gpudiff_dbatch_create(c, 16, 1024, &s->res_d))) return fail(rc);
     (void)hipFree(s->res_d->pool);
     s->res_d->pool = nullptr;
@@ -730,6 +736,11 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     // the upload runs on the copy stream, behind this ring slot's previous K0 (which read the
     // same device buffers), so it overlaps the other batch's K0 / diff pass
     if (R.k0_recorded) HIPCHK(hipStreamWaitEvent(cs, R.k0_done, 0));
+    hipStream_t cs2 = s->cs2 ? s->cs2 : cs;
+    if (s->cs2) {  // the second copy stream starts behind the same dependencies
+        HIPCHK(hipEventRecord(s->cs2_done, cs));
+        HIPCHK(hipStreamWaitEvent(cs2, s->cs2_done, 0));
+    }
     if (timing) HIPCHK(hipEventRecord(R.t_ev[0], cs));
     // the tables' used parts only (their device offsets are sized for 2n documents)
     HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, (uint64_t)nd * sizeof(TokDoc), hipMemcpyHostToDevice, cs));
@@ -749,8 +760,9 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     auto upload = [&](uint32_t q) {
         const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
         if (q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
-        if (hipMemcpyAsync(R.djson + b0, R.hjson + b0, b1 - b0, hipMemcpyHostToDevice, cs) != hipSuccess ||
-            hipEventRecord(R.chunk_ev[q], cs) != hipSuccess)
+        hipStream_t qs = (q & 1u) ? cs2 : cs;
+        if (hipMemcpyAsync(R.djson + b0, R.hjson + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
+            hipEventRecord(R.chunk_ev[q], qs) != hipSuccess)
             up_err.store(1);
     };
     workers(c).run(T, [&](uint32_t t) {
@@ -779,6 +791,10 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     });
     if (up_err.load()) return GPUDIFF_E_DEVICE;
     lap(2);
+    if (s->cs2) {  // staged = both copy streams done
+        HIPCHK(hipEventRecord(s->cs2_done, cs2));
+        HIPCHK(hipStreamWaitEvent(cs, s->cs2_done, 0));
+    }
     HIPCHK(hipEventRecord(R.staged, cs));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[1], cs));
     HIPCHK(hipStreamWaitEvent(st, R.chunk_ev[0], 0));
@@ -972,6 +988,11 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
             if (e) (void)hipEventDestroy(e);
     }
     if (s->res_d) gpudiff_dbatch_free(c, s->res_d);
+    if (s->cs2) {
+        (void)hipStreamSynchronize(s->cs2);
+        (void)hipStreamDestroy(s->cs2);
+    }
+    if (s->cs2_done) (void)hipEventDestroy(s->cs2_done);
     if (s->cs) {
         (void)hipStreamSynchronize(s->cs);
         (void)hipStreamDestroy(s->cs);

@@ -27,6 +27,7 @@ PATH_REGION_STATUS = 0x80
 OPT_TIMING = 0x1
 OPT_DEVICE_ENCODE = 0x2000000
 OPT_K2_FUSE_DEEP = 0x40000000  # tuning: deep joins stay in K2 (no K4 merge-path slices)
+OPT_H2D_TWO_STREAMS = 0x2  # tuning: device-encode uploads alternate JSON chunks between two copy streams
 OPT_K2_NO_LPT = 0x4  # tuning: K2's final round in index order (default: largest first for large pairs)
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 

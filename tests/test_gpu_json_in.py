@@ -1,0 +1,50 @@
+"""JSON-in batches large enough for several upload chunks (gpudiff_submit's device-encode path splits the JSON
+into up to 4 chunks of >= 16 MiB, each uploaded and encoded as soon as it is staged): the default single copy
+stream and GPUDIFF_OPT_H2D_TWO_STREAMS give the same flags and changed paths as host encoding and as the
+oracle's tree walk over the same JSON (oracle/deepequal_ref.cpp, specsyncer.go:17-41 / statussyncer.go:15-27)."""
+import numpy as np
+import pytest
+
+from kcp_amd import gpudiff as G
+from kcp_amd import synth as S
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b):
+    return (np.array_equal(a.pair_flags & 7, b.pair_flags & 7) and np.array_equal(a.path_offsets, b.path_offsets)
+            and np.array_equal(a.path_hashes, b.path_hashes) and np.array_equal(a.path_kinds, b.path_kinds))
+
+
+def test_multi_chunk_upload_one_and_two_copy_streams():
+    cfg = S.make_cfg("config3", n_pairs=12000, mutate_frac=0.3)
+    pop = S.Population(cfg)
+    buf, offs, _ = pop.json_range(0, pop.n, 8)
+    assert int(offs[-1]) >= 3 * (16 << 20)  # at least three upload chunks
+    arr = G.json_pair_array(buf, offs)
+    host = G.Engine(device=0, encode_threads=8)
+    want = host.wait(host.submit_array(arr))
+    host.close()
+    seeds = np.zeros(pop.n, np.uint8)  # tree-walk seeds: the host encoder's, from a host-encoded copy
+    enc = G.Engine(device=G.DEVICE_NONE)
+    pairs = [(bytes(buf[offs[2 * i]:offs[2 * i + 1]]), bytes(buf[offs[2 * i + 1]:offs[2 * i + 2]]))
+             for i in range(pop.n)]
+    hb = enc.encode(pairs)
+    seeds[:] = ((hb.rows()["flags_a"] >> G.OBJ_SEED_SHIFT) & 0xFF).astype(np.uint8)
+    hb.free()
+    enc.close()
+    f, o, h, k = cpu_ref.tree_check(buf, offs, seeds, 8)
+    assert np.array_equal(want.pair_flags & 7, f)
+    assert np.array_equal(want.path_offsets.astype(np.int64), o.astype(np.int64))
+    assert np.array_equal(want.path_hashes, h) and np.array_equal(want.path_kinds, k)
+    for flags in (0, G.OPT_H2D_TWO_STREAMS):
+        e = G.Engine(device=0, encode_threads=8, device_encode=True, flags=flags)
+        # two batches in flight (both ring slots), then the same batch again on a reused slot
+        t1 = e.submit_array(arr)
+        t2 = e.submit_array(arr)
+        r1, r2 = e.wait(t1), e.wait(t2)
+        r3 = e.wait(e.submit_array(arr))
+        e.close()
+        for r in (r1, r2, r3):
+            assert _same(r, want), "device encode (flags %#x) differs from host encode" % flags

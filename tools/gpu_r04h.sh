@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/r04h; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_collective.py tests/test_gpu_dist_rehearsal.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_collective.py tests/test_gpu_dist_rehearsal.py tests/test_gpu_json_in.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for v in "c4_lpt:--engine-flags 0" "c4_idx:--engine-flags 0x4" "c4_lpt2:--engine-flags 0" "c4_idx2:--engine-flags 0x4"; do
   n=${v%%:*}; a=${v#*:}
@@ -12,6 +12,7 @@ for v in "c4_lpt:--engine-flags 0" "c4_idx:--engine-flags 0x4" "c4_lpt2:--engine
   python -c "import json; d=json.load(open('$O/$n.json')); print('$n', d['value'], d['ms_per_step'], d['roofline']['format']['frac'], d['kernels_ms']['compare_all_launches'])"
 done
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.log || { tail -30 $O/bench.log; exit 1; }
-python -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['format']['frac'], d['kernels_ms']); print(d['json_in'])"
+python -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['format']['frac'], d['kernels_ms']); print(json.dumps(d['json_in']))"
 timeout -k 10 900 python tools/full_tree_check.py --k0 > $O/full_tree_check.json 2> $O/full_tree_check.log || { tail -30 $O/full_tree_check.log; exit 1; }
 cat $O/full_tree_check.json
+timeout -k 10 200 python tools/h2d_probe.py > $O/h2d_probe.txt 2>&1 && cat $O/h2d_probe.txt
