@@ -753,11 +753,16 @@ def json_in_rates(G, pop, m, threads, device):
     arr = G.json_pair_array(buf, offs)
     out = dict(sample_pairs=m, json_bytes=int(offs[-1]), threads=threads)
     flags = {}
-    # device_encode_h2d2: the same with GPUDIFF_OPT_H2D_TWO_STREAMS (JSON chunks alternate two copy streams)
-    for mode in ("host_encode", "device_encode", "device_encode_h2d2"):
-        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode != "host_encode"),
-                     flags=G.OPT_H2D_TWO_STREAMS if mode == "device_encode_h2d2" else 0)
-        r = e.wait(e.submit_array(arr))  # warm: staging and scratch allocations
+    # A/B variants of device encode: device_encode_h2d2 with GPUDIFF_OPT_H2D_TWO_STREAMS (JSON chunks alternate
+    # two copy streams); device_encode_4chunks with round 3's staging (at most 4 upload chunks)
+    modes = (("host_encode", 0, None), ("device_encode", 0, None),
+             ("device_encode_h2d2", G.OPT_H2D_TWO_STREAMS, None), ("device_encode_4chunks", 0, "4"))
+    for mode, mflags, max_chunks in modes:
+        if max_chunks:
+            os.environ["GPUDIFF_H2D_MAX_CHUNKS"] = max_chunks  # read when the context's store is created
+        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode != "host_encode"), flags=mflags)
+        r = e.wait(e.submit_array(arr))  # warm: staging and scratch allocations (and the device-encode store)
+        os.environ.pop("GPUDIFF_H2D_MAX_CHUNKS", None)
         times = []
         for _ in range(3):
             t0 = time.perf_counter()
@@ -769,8 +774,7 @@ def json_in_rates(G, pop, m, threads, device):
         e.close()
         if mode == "device_encode":
             out[mode]["phases_ms"] = json_in_phases(G, arr, m, threads, device)
-    out["modes_agree"] = bool(np.array_equal(flags["host_encode"], flags["device_encode"]) and
-                              np.array_equal(flags["host_encode"], flags["device_encode_h2d2"]))
+    out["modes_agree"] = all(bool(np.array_equal(flags["host_encode"], f)) for f in flags.values())
     return out
 
 

@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <new>
 #include <thread>
 #include <unordered_map>
@@ -43,6 +44,12 @@ using namespace gd;
 namespace {
 
 constexpr uint64_t kScratchCap = 2ull << 30;  // K0 working area, reused across launches
+// a device-encoded batch's JSON is staged, uploaded and encoded in up to kMaxUpChunks chunks of at least
+// kUpChunkBytes (whole documents): the smaller the chunks, the sooner the first upload starts and the shorter
+// the last chunk's K0 after the copy stream is done.  GPUDIFF_H2D_CHUNK_MIB / GPUDIFF_H2D_MAX_CHUNKS (read once
+// per store, A/B tuning only) override them; round 3 used 4 chunks of >= 16 MiB.
+constexpr uint32_t kMaxUpChunks = 16;
+constexpr uint64_t kUpChunkBytes = 16ull << 20;
 
 struct Ring {
     gpudiff_dbatch* d = nullptr;  // rows, pair_ids, results; pool = the store's current space
@@ -63,7 +70,7 @@ struct Ring {
     hipEvent_t k0_done = nullptr;  // its K0..K0x finished reading the device JSON / document table
     bool k0_recorded = false;
     hipEvent_t t_ev[5] = {};      // GPUDIFF_OPT_TIMING: H2D begin/end (copy stream), K0 begin/end, K0c+K0x end
-    hipEvent_t chunk_ev[8] = {};  // each JSON chunk's H2D done: its K0 launches may start
+    hipEvent_t chunk_ev[kMaxUpChunks] = {};  // each JSON chunk's H2D done: its K0 launches may start
     std::vector<gpudiff_event> events;
     std::vector<uint8_t> final_flags;  // the waited batch's result flags (deferred events resolved)
     bool waited = false;
@@ -88,6 +95,8 @@ struct DStore {
     hipStream_t cs = nullptr;  // H2D of the next batch overlaps K0 of the current one
     hipStream_t cs2 = nullptr; // GPUDIFF_OPT_H2D_TWO_STREAMS: odd JSON chunks upload here (a second DMA queue)
     hipEvent_t cs2_done = nullptr;
+    uint64_t up_chunk_bytes = kUpChunkBytes;
+    uint32_t up_max_chunks = kMaxUpChunks;
     uint64_t* sizes = nullptr;
     uint64_t* tile_sums = nullptr;
     uint8_t* scratch = nullptr;
@@ -580,6 +589,10 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
             return fail(GPUDIFF_E_DEVICE);
     }
     if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+    if (const char* v = getenv("GPUDIFF_H2D_CHUNK_MIB"))
+        s->up_chunk_bytes = std::max<uint64_t>(1, strtoull(v, nullptr, 10)) << 20;
+    if (const char* v = getenv("GPUDIFF_H2D_MAX_CHUNKS"))
+        s->up_max_chunks = (uint32_t)std::min<unsigned long long>(kMaxUpChunks, std::max(1ull, strtoull(v, nullptr, 10)));
     if ((c->flags & GPUDIFF_OPT_H2D_TWO_STREAMS) &&
         (hipStreamCreateWithFlags(&s->cs2, hipStreamNonBlocking) != hipSuccess ||
          hipEventCreateWithFlags(&s->cs2_done, hipEventDisableTiming) != hipSuccess))
@@ -694,8 +707,8 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         }
         return lo;
     };
-    const uint32_t C = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, jbytes >> 24));
-    uint32_t cdoc[9];
+    const uint32_t C = (uint32_t)std::min<uint64_t>(s->up_max_chunks, std::max<uint64_t>(1, jbytes / s->up_chunk_bytes));
+    uint32_t cdoc[kMaxUpChunks + 1];
     for (uint32_t q = 0; q <= C; q++) cdoc[q] = q == C ? nd : first_doc(jbytes * q / C);
     auto cbyte = [&](uint32_t q) -> uint64_t { return q == C || cdoc[q] >= nd ? jbytes : docs[cdoc[q]].json_off; };
     // K0 scratch: per-document areas within launches of at most kScratchCap, never across a chunk
@@ -753,7 +766,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     // 1, ... and counts each chunk done; the calling thread (worker 0) enqueues a chunk's upload as
     // soon as every worker has counted it, then goes on with its own share of the next chunk.
     const uint32_t T = (uint32_t)std::min<uint64_t>(std::max(1u, c->threads), std::max<uint64_t>(1, jbytes >> 20));
-    std::atomic<uint32_t> chunk_done[8];
+    std::atomic<uint32_t> chunk_done[kMaxUpChunks];
     for (auto& x : chunk_done) x.store(0, std::memory_order_relaxed);
     std::atomic<int> up_err{0};
     uint32_t uploaded = 0;

@@ -2,6 +2,8 @@
 into up to 4 chunks of >= 16 MiB, each uploaded and encoded as soon as it is staged): the default single copy
 stream and GPUDIFF_OPT_H2D_TWO_STREAMS give the same flags and changed paths as host encoding and as the
 oracle's tree walk over the same JSON (oracle/deepequal_ref.cpp, specsyncer.go:17-41 / statussyncer.go:15-27)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -38,13 +40,21 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
     assert np.array_equal(want.pair_flags & 7, f)
     assert np.array_equal(want.path_offsets.astype(np.int64), o.astype(np.int64))
     assert np.array_equal(want.path_hashes, h) and np.array_equal(want.path_kinds, k)
-    for flags in (0, G.OPT_H2D_TWO_STREAMS):
+    # the default chunks, two copy streams, one chunk, and the most chunks (1 MiB minimum: capped at 16)
+    variants = ((0, {}), (G.OPT_H2D_TWO_STREAMS, {}), (0, {"GPUDIFF_H2D_MAX_CHUNKS": "1"}),
+                (G.OPT_H2D_TWO_STREAMS, {"GPUDIFF_H2D_CHUNK_MIB": "1"}))
+    for flags, env in variants:
+        os.environ.update(env)
         e = G.Engine(device=0, encode_threads=8, device_encode=True, flags=flags)
         # two batches in flight (both ring slots), then the same batch again on a reused slot
-        t1 = e.submit_array(arr)
+        try:
+            t1 = e.submit_array(arr)  # creates the device-encode store (reads the environment)
+        finally:
+            for k in env:
+                os.environ.pop(k)
         t2 = e.submit_array(arr)
         r1, r2 = e.wait(t1), e.wait(t2)
         r3 = e.wait(e.submit_array(arr))
         e.close()
         for r in (r1, r2, r3):
-            assert _same(r, want), "device encode (flags %#x) differs from host encode" % flags
+            assert _same(r, want), "device encode (flags %#x, %s) differs from host encode" % (flags, env)
