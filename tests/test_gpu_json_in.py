@@ -1,5 +1,5 @@
 """JSON-in batches large enough for several upload chunks (gpudiff_submit's device-encode path splits the JSON
-into up to 4 chunks of >= 16 MiB, each uploaded and encoded as soon as it is staged): the default single copy
+into up to 16 chunks of >= 16 MiB, each uploaded and encoded as soon as it is staged): the default single copy
 stream and GPUDIFF_OPT_H2D_TWO_STREAMS give the same flags and changed paths as host encoding and as the
 oracle's tree walk over the same JSON (oracle/deepequal_ref.cpp, specsyncer.go:17-41 / statussyncer.go:15-27)."""
 import os
@@ -50,8 +50,8 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
         try:
             t1 = e.submit_array(arr)  # creates the device-encode store (reads the environment)
         finally:
-            for k in env:
-                os.environ.pop(k)
+            for name in env:
+                os.environ.pop(name)
         t2 = e.submit_array(arr)
         r1, r2 = e.wait(t1), e.wait(t2)
         r3 = e.wait(e.submit_array(arr))
