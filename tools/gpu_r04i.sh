@@ -7,3 +7,5 @@ export TMPDIR=/tmp
 timeout -k 10 1000 python -u tools/full_tree_check.py --k0 > $O/full_tree_check.json 2> $O/full_tree_check.log || { tail -30 $O/full_tree_check.log; exit 1; }
 cat $O/full_tree_check.json
 timeout -k 10 150 python tools/h2d_probe.py > $O/h2d_probe.txt 2>&1 && cat $O/h2d_probe.txt
+timeout -k 10 200 python tools/json_in_probe.py > $O/json_in.json 2> $O/json_in.log || { tail -20 $O/json_in.log; exit 1; }
+cat $O/json_in.json
