@@ -671,7 +671,68 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         src.push_back(p);
         nd++;
     };
-    for (size_t i = 0; i < n; i++) {
+    if (s->pair_mode) {
+        // gpudiff_submit's pairs: event i is slot i with documents 2i (old) and 2i + 1 (new), so the tables
+        // are filled by the workers -- a per-thread byte sum, then each thread writes its range from its
+        // offset.  Same tables as add_doc builds (it is the order-dependent path for store events).
+        static const uint8_t kNone[1] = {0};
+        const uint32_t T = (uint32_t)std::min<size_t>(std::max(1u, c->threads), std::max<size_t>(1, n / 4096));
+        std::vector<uint64_t> part(4 * (size_t)T + 4, 0);  // per thread: JSON bytes, bound, floor, new bytes
+        std::atomic<int> bad{0};
+        src.resize(2 * n);
+        auto step = [](size_t len) -> uint64_t { return (len + kTokSlack + 15) & ~15ull; };
+        workers(c).run(T, [&](uint32_t t) {
+            uint64_t jb = 0, bd = 0, fl = 0, nj = 0;
+            for (size_t i = n * t / T, i1 = n * (t + 1) / T; i < i1; i++) {
+                const gpudiff_event& e = ev[i];
+                if (e.slot != i || e.slot >= s->max_slots || !e.new_json || e.new_len > kTokMaxLen ||
+                    e.old_len > kTokMaxLen)
+                    bad.store(1, std::memory_order_relaxed);
+                const size_t lo = e.old_json ? e.old_len : 0;
+                jb += step(lo) + step(e.new_len);
+                bd += (5 * (uint64_t)lo) / 2 + (5 * (uint64_t)e.new_len) / 2 + 768;
+                fl += lo + e.new_len;
+                nj += e.new_len;
+            }
+            uint64_t* q = &part[4 * (size_t)(t + 1)];
+            q[0] = jb, q[1] = bd, q[2] = fl, q[3] = nj;
+        });
+        if (bad.load()) return GPUDIFF_E_INVAL;
+        for (uint32_t t = 1; t <= T; t++)
+            for (int k = 0; k < 4; k++) part[4 * (size_t)t + k] += part[4 * (size_t)(t - 1) + k];
+        workers(c).run(T, [&](uint32_t t) {
+            uint64_t off = part[4 * (size_t)t];
+            for (size_t i = n * t / T, i1 = n * (t + 1) / T; i < i1; i++) {
+                const gpudiff_event& e = ev[i];
+                const uint8_t* pj[2] = {e.old_json ? e.old_json : kNone, e.new_json};
+                const size_t len[2] = {e.old_json ? e.old_len : 0, e.new_len};
+                for (uint32_t h = 0; h < 2; h++) {
+                    const size_t k = 2 * i + h;
+                    TokDoc& D = docs[k];
+                    memset(&D, 0, sizeof(D));
+                    D.json_off = off;
+                    D.json_len = (uint32_t)len[h];
+                    off += step(len[h]);
+                    DocLink& L = links[k];
+                    memset(&L, 0, sizeof(L));
+                    L.slot = e.slot;
+                    L.row = h ? (uint32_t)i : kNoRow;
+                    L.pair_id = e.pair_id;
+                    L.cluster_id = e.cluster_id;
+                    L.prev = h ? (int32_t)(2 * i) : -1;
+                    L.next = h ? -1 : (int32_t)(2 * i + 1);
+                    src[k] = pj[h];
+                }
+                heads[i] = (uint32_t)(2 * i);
+                s->sstate[e.slot] = DStore::SlotState{batch, (int32_t)(2 * i + 1)};
+            }
+        });
+        const uint64_t* tot = &part[4 * (size_t)T];
+        nd = (uint32_t)(2 * n);
+        nh = (uint32_t)n;
+        jbytes = tot[0], bound = tot[1], floor = tot[2], new_json_bytes = tot[3];
+    }
+    for (size_t i = 0; i < n && !s->pair_mode; i++) {
         const gpudiff_event& e = ev[i];
         if (i + 16 < n && ev[i + 16].slot < s->max_slots) {  // the slot state 16 events ahead
             __builtin_prefetch(&s->sstate[ev[i + 16].slot], 1);
