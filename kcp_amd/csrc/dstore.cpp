@@ -831,13 +831,33 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     for (auto& x : chunk_done) x.store(0, std::memory_order_relaxed);
     std::atomic<int> up_err{0};
     uint32_t uploaded = 0;
+    if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
+    const TokDoc* ddocs = (const TokDoc*)R.dmeta;
+    const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
+    const uint32_t* dheads = (const uint32_t*)(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
+    uint8_t* space = s->space[s->cur];
+    size_t li = 0;  // next K0 launch
+    // chunk q's K0 launches go on the kernel stream as soon as its upload is enqueued (behind its copy
+    // event), so K0 of chunk q runs while chunk q + 1 is on the link -- not after the host has staged them all
     auto upload = [&](uint32_t q) {
         const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
         if (q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
         hipStream_t qs = (q & 1u) ? cs2 : cs;
         if (hipMemcpyAsync(R.djson + b0, R.hjson + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
-            hipEventRecord(R.chunk_ev[q], qs) != hipSuccess)
+            hipEventRecord(R.chunk_ev[q], qs) != hipSuccess || hipStreamWaitEvent(st, R.chunk_ev[q], 0) != hipSuccess ||
+            (q == 0 && timing && hipEventRecord(R.t_ev[2], st) != hipSuccess)) {
             up_err.store(1);
+            return;
+        }
+        for (; li < launches.size() && chunk_of_launch[li] == q; li++) {
+            const auto& L = launches[li];
+            if (launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
+                                   s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
+                                   (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u) != hipSuccess) {
+                up_err.store(1);
+                return;
+            }
+        }
     };
     workers(c).run(T, [&](uint32_t t) {
         for (uint32_t q = 0; q < C; q++) {
@@ -871,24 +891,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     }
     HIPCHK(hipEventRecord(R.staged, cs));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[1], cs));
-    HIPCHK(hipStreamWaitEvent(st, R.chunk_ev[0], 0));
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[2], st));
-    if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
-    const TokDoc* ddocs = (const TokDoc*)R.dmeta;
-    const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
-    const uint32_t* dheads = (const uint32_t*)(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
-    uint8_t* space = s->space[s->cur];
-    uint32_t waited_chunk = 0;
-    for (size_t li = 0; li < launches.size(); li++) {
-        const auto& L = launches[li];
-        if (chunk_of_launch[li] != waited_chunk) {
-            waited_chunk = chunk_of_launch[li];
-            HIPCHK(hipStreamWaitEvent(st, R.chunk_ev[waited_chunk], 0));
-        }
-        HIPCHK(launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
-                                  s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
-                                  (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
-    }
+    if (li != launches.size()) return GPUDIFF_E_STATE;  // every launch belongs to an uploaded chunk
     HIPCHK(hipStreamWaitEvent(st, R.staged, 0));  // every chunk (and the tables) landed
     if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
     HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
