@@ -88,8 +88,11 @@ struct DStore {
     uint64_t space_bytes = 0;
     uint8_t* space[2] = {nullptr, nullptr};
     uint32_t cur = 0;
-    unsigned long long* used_dev = nullptr;
+    unsigned long long* used_dev = nullptr;  // the current space's append point (one of used_base[0..1])
+    unsigned long long* used_base = nullptr;
     uint64_t used_ub = 0;  // host upper bound of *used_dev
+    // gpudiff_submit's pair mode: ring slot r's batches own space[r] and used_base[r] (each batch starts it
+    // empty: the batch two submits back is dropped), so neither a compaction nor its host sync is ever needed
     DSlot* slots = nullptr;
     uint32_t* ctr = nullptr;  // kCtrLive, kCtrLiveBytes
     hipStream_t cs = nullptr;  // H2D of the next batch overlaps K0 of the current one
@@ -193,6 +196,8 @@ int compact(DStore* s) {
 // compacts when `want` bytes may not fit; fails only when not even `need` bytes fit after it
 int ensure_space(DStore* s, uint64_t want, uint64_t need) {
     if (s->used_ub + want <= s->space_bytes) return GPUDIFF_OK;
+    if (s->pair_mode)  // the other space is the other ring slot's batch: no compaction into it
+        return s->used_ub + need <= s->space_bytes ? GPUDIFF_OK : GPUDIFF_E_CAPACITY;
     int rc = compact(s);
     if (rc) return rc;
     return s->used_ub + need <= s->space_bytes ? GPUDIFF_OK : GPUDIFF_E_CAPACITY;
@@ -571,11 +576,12 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
     if (!s->enc) return fail(GPUDIFF_E_NOMEM);
     for (auto& sp : s->space)
         if ((rc = dalloc(&sp, s->space_bytes))) return fail(rc);
-    if ((rc = dalloc(&s->used_dev, 1)) || (rc = dalloc(&s->slots, max_slots)) || (rc = dalloc(&s->ctr, 4)) ||
+    if ((rc = dalloc(&s->used_base, 2)) || (rc = dalloc(&s->slots, max_slots)) || (rc = dalloc(&s->ctr, 4)) ||
         (rc = dalloc(&s->sizes, max_slots)) || (rc = dalloc(&s->tile_sums, (max_slots + 1023) / 1024 + 1)) ||
         (rc = dalloc(&s->res_err, 1)))
         return fail(rc);
-    if (hipMemset(s->used_dev, 0, 8) != hipSuccess || hipMemset(s->slots, 0, sizeof(DSlot) * (size_t)max_slots) ||
+    s->used_dev = s->used_base;
+    if (hipMemset(s->used_base, 0, 16) != hipSuccess || hipMemset(s->slots, 0, sizeof(DSlot) * (size_t)max_slots) ||
         hipMemset(s->ctr, 0, 16) != hipSuccess)
         return fail(GPUDIFF_E_DEVICE);
     for (Ring& R : s->ring) {
@@ -621,6 +627,12 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     }
     int rc;
     if (R.staged) HIPCHK(hipEventSynchronize(R.staged));
+    if (s->pair_mode) {  // this ring slot's space, emptied behind its previous batch (stream order)
+        s->cur = s->ring_next;
+        s->used_dev = s->used_base + s->ring_next;
+        s->used_ub = 0;
+        HIPCHK(hipMemsetAsync(s->used_dev, 0, 8, c->stream));
+    }
     auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
         if (!timing) return;
         const auto now = std::chrono::steady_clock::now();
@@ -933,12 +945,16 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         }
         uint32_t ndef = 0;
         uint64_t used = 0;
+        if (s->pair_mode) {  // resolution appends to this batch's own space
+            s->cur = (uint32_t)(Rp - s->ring);
+            s->used_dev = s->used_base + s->cur;
+        }
         HIPCHK(hipMemcpyAsync(&ndef, RR.dcnt, 4, hipMemcpyDeviceToHost, s->c->rb));  // behind K0x: d->done waited
         HIPCHK(hipMemcpyAsync(&used, s->used_dev, 8, hipMemcpyDeviceToHost, s->c->rb));
         HIPCHK(hipStreamSynchronize(s->c->rb));
         // exact append point + what the other batch in flight may still add
         const Ring& other = s->ring[(Rp - s->ring) ^ 1];
-        s->used_ub = std::max<uint64_t>(used, used + (other.outstanding ? other.bound : 0));
+        s->used_ub = s->pair_mode ? used : std::max<uint64_t>(used, used + (other.outstanding ? other.bound : 0));
         if (RR.t_ev[0] && (s->c->flags & GPUDIFF_OPT_TIMING)) {
             float ms[3];
             HIPCHK(hipEventElapsedTime(&ms[0], RR.t_ev[0], RR.t_ev[1]));  // H2D
@@ -972,8 +988,11 @@ int dstore_submit_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n
     DStore*& s = c->pair_store;
     uint64_t json = 0;
     for (size_t i = 0; i < n; i++) json += pairs[i].old_len + pairs[i].new_len;
-    const uint64_t space = std::max<uint64_t>(512ull << 20, 4 * (json + json / 2 + 128 * n));
-    if (!s || s->max_events < n || s->space_bytes < space / 2) {
+    // one space per ring slot, each taking a whole batch: dstore_submit's bound (5/2 of the JSON + 384 B a
+    // document), with half again as headroom so a growing batch does not recreate the store every time
+    const uint64_t need = (5 * json) / 2 + 768 * (uint64_t)n + (1ull << 20);
+    const uint64_t space = std::max<uint64_t>(512ull << 20, need + need / 2);
+    if (!s || s->max_events < n || s->space_bytes < need) {
         if (s && (s->ring[0].outstanding || s->ring[1].outstanding))
             return GPUDIFF_E_CAPACITY;  // grows only between batches: gpudiff_submit encodes this one on the host
         if (s) dstore_free(c, s);
@@ -1074,7 +1093,7 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         (void)hipStreamSynchronize(s->cs);
         (void)hipStreamDestroy(s->cs);
     }
-    for (void* p : {(void*)s->space[0], (void*)s->space[1], (void*)s->used_dev, (void*)s->slots, (void*)s->ctr,
+    for (void* p : {(void*)s->space[0], (void*)s->space[1], (void*)s->used_base, (void*)s->slots, (void*)s->ctr,
                     (void*)s->sizes, (void*)s->tile_sums, (void*)s->scratch, (void*)s->res_stage, (void*)s->res_ups,
                     (void*)s->res_err})
         if (p) (void)hipFree(p);

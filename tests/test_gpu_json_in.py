@@ -58,3 +58,30 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
         e.close()
         for r in (r1, r2, r3):
             assert _same(r, want), "device encode (flags %#x, %s) differs from host encode" % (flags, env)
+
+
+def test_two_in_flight_with_host_resolution():
+    """Pair-mode submits keep one space per ring slot: batches of varying size, two in flight, each waited
+    after the next is submitted, with 8-bit path hashes so that K0 hands colliding documents to the host
+    resolution (which appends into the waited batch's own space while the next batch's K0 fills the other)
+    -- every result equals the host-encoded engine's with the same hash width."""
+    from tests.workload import make_pairs
+    batches = [make_pairs(n, seed=40 + i, mutate_frac=0.4)[0] for i, n in enumerate((200, 200, 900, 900, 2000, 300))]
+    host = G.Engine(device=0, encode_threads=8, path_hash_bits=8)
+    wants = [host.wait(host.submit(p)) for p in batches]
+    host.close()
+    e = G.Engine(device=0, encode_threads=8, device_encode=True, path_hash_bits=8)
+    prev = None
+    deferred = 0
+    for i, p in enumerate(batches):
+        if i == 4:  # the store grows only between batches: drain first
+            e.wait(prev[1])
+            prev = None
+        t = e.submit(p)
+        if prev is not None:
+            assert _same(e.wait(prev[1]), wants[prev[0]])
+        prev = (i, t)
+    assert _same(e.wait(prev[1]), wants[prev[0]])
+    deferred = e.submit_stats().deferred
+    e.close()
+    assert deferred > 0  # the host resolution ran
