@@ -50,6 +50,9 @@ constexpr uint64_t kScratchCap = 2ull << 30;  // K0 working area, reused across 
 // per store, A/B tuning only) override them; round 3 used 4 chunks of >= 16 MiB.
 constexpr uint32_t kMaxUpChunks = 16;
 constexpr uint64_t kUpChunkBytes = 16ull << 20;
+// ... and of at least kMinChunkDocs documents: each chunk's K0 launch (a wave per document) should fill the
+// chip's ~8k resident waves twice over (r04m: 12 chunks of 5.4k documents made config5's K0 6.4 ms, from 4.1)
+constexpr uint64_t kMinChunkDocs = 16384;
 
 struct Ring {
     gpudiff_dbatch* d = nullptr;  // rows, pair_ids, results; pool = the store's current space
@@ -780,7 +783,9 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         }
         return lo;
     };
-    const uint32_t C = (uint32_t)std::min<uint64_t>(s->up_max_chunks, std::max<uint64_t>(1, jbytes / s->up_chunk_bytes));
+    const uint32_t C = (uint32_t)std::min<uint64_t>(
+        std::min<uint64_t>(s->up_max_chunks, std::max<uint64_t>(1, nd / kMinChunkDocs)),
+        std::max<uint64_t>(1, jbytes / s->up_chunk_bytes));
     uint32_t cdoc[kMaxUpChunks + 1];
     for (uint32_t q = 0; q <= C; q++) cdoc[q] = q == C ? nd : first_doc(jbytes * q / C);
     auto cbyte = [&](uint32_t q) -> uint64_t { return q == C || cdoc[q] >= nd ? jbytes : docs[cdoc[q]].json_off; };
