@@ -1647,8 +1647,8 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 7: return k_compare<true, 2, 6>;
         case 8: return k_compare_flat<4, 1>;
         case 9: return k_compare_flat<2, 1>;
-        case 11: return k_compare_flat<2, 5>;
-        case 12: return k_compare_flat<4, 5>;
+        case 11: return k_compare_flat<8, 4, true>;   // x8 held to 4 waves/SIMD
+        case 12: return k_compare_flat<16, 1, true>;  // x16
         case 13: return k_compare_flat<4, 1, true, false, true>;  // + next rows prefetched into LDS (RPF)
         case 10: return k_compare_flat<8, 1, true>;  // the default with 8 chunks a side in flight (tail rate)
         case 14: return k_compare_flat<4, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
@@ -1661,7 +1661,7 @@ static K2Fn k2_kernel(uint32_t variant) {
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 10: case 13: case 14: case 15: return true;
+        case 0: case 10: case 11: case 12: case 13: case 14: case 15: return true;
         default: return false;
     }
 }
@@ -1781,7 +1781,7 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
 // no pair-split tail (k2_tail_chunks() == 0: the items of large pairs are split to 1-2 pairs already)
 static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uint32_t nwaves, uint32_t sub,
                              uint32_t tail) {
-    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 0 || v == 10 || v == 14 || v == 15)) return 0;
+    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 0 || (v >= 10 && v <= 12) || v == 14 || v == 15)) return 0;
     if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
     const uint32_t r = k2_lpt_round(nch << sub, nwaves);
     return r <= kK2LptMax ? r : 0;
