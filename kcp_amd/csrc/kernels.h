@@ -49,7 +49,7 @@ struct DiffBuffers {
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
-    uint32_t k2_variant;        // tuning: 0 default = k_compare_flat, 4 x 16-B chunks in flight per lane per object
+    uint32_t k2_variant;        // tuning: 0 = by batch shape (k2_variant_of: 8 or 16 x 16-B chunks in flight per lane per object)
     uint32_t k2_items_per_wave; // tuning: 0 = default; 64-pair chunks split until each resident wave has this many items
     uint32_t k2_blocks_per_cu;  // tuning: 0 = the variant's occupancy (4 resident 256-thread blocks per CU)
     uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default

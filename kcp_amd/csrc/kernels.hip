@@ -1644,26 +1644,37 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 4: return k_compare<true, 2, 1>;
         case 5: return k_compare<true, 4, 6>;  // <= 80 VGPRs
         case 6: return k_compare<true, 2, 8>;  // <= 64 VGPRs
-        case 7: return k_compare<true, 2, 6>;
+        case 7: return k_compare_flat<4, 1, true>;  // round 3's default: 4 chunks a side in flight, 4 waves/SIMD
         case 8: return k_compare_flat<4, 1>;
         case 9: return k_compare_flat<2, 1>;
         case 11: return k_compare_flat<8, 4, true>;   // x8 held to 4 waves/SIMD
         case 12: return k_compare_flat<16, 1, true>;  // x16
         case 13: return k_compare_flat<4, 1, true, false, true>;  // + next rows prefetched into LDS (RPF)
-        case 10: return k_compare_flat<8, 1, true>;  // the default with 8 chunks a side in flight (tail rate)
+        case 10: return k_compare_flat<8, 1, true>;  // 8 chunks a side in flight, 3 waves/SIMD
         case 14: return k_compare_flat<4, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
         case 15: return k_compare_flat<2, 1, true>;
-        // 0: 105 VGPRs, 4 waves/SIMD, no spills; items handed out dynamically (5% shorter than static
+        // 0 is resolved by k2_variant_of (10 or 12); items handed out dynamically (5% shorter than static
         // striding = variant 8 on config3, tools/ab_k2.py on MI355X)
-        default: return k_compare_flat<4, 1, true>;
+        default: return k_compare_flat<8, 1, true>;
     }
 }
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 10: case 11: case 12: case 13: case 14: case 15: return true;
+        case 0: case 7: case 10: case 11: case 12: case 13: case 14: case 15: return true;
         default: return false;
     }
+}
+
+// The default decision kernel by batch shape (variant 0; in-process A/B, profiles/r04p): the kernel keeps 8 x 16-B
+// chunks a side in flight per lane at 3 waves/SIMD (139 VGPRs) -- config3 10M K2 8.21 vs 8.28 ms, the N = 8 share
+// 1.147 vs 1.164, config4 1.080 vs 1.091 against round 3's 4 in flight at 4 waves -- and 16 in flight at 2 waves
+// for deep pairs (>= kK2BigPairBytes a pair: config4 1.043 ms, but config3 8.44 and the share 1.195): when the
+// items are 16-256 KiB the last round's waves stream alone and their own loads in flight set the tail's rate.
+constexpr uint64_t kK2BigPairBytes = 16384;
+static uint32_t k2_variant_of(const DiffBuffers& b) {
+    const uint32_t v = b.k2_variant & 15u;
+    return v ? v : (b.avg_pair_bytes >= kK2BigPairBytes ? 12u : 10u);
 }
 
 constexpr uint32_t kK2LptMax = 8192;  // largest-first round: at most this many items (one per resident wave)
@@ -1676,7 +1687,7 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     // kernel (its measured occupancy, hipOccupancyMaxActiveBlocksPerMultiprocessor):
     // a larger grid would leave blocks waiting for a free slot, i.e. a tail
     static int occ[16] = {0};
-    const uint32_t v = b.k2_variant & 15u;
+    const uint32_t v = k2_variant_of(b);
     if (!occ[v]) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k2_kernel(v)), 256, 0) !=
@@ -1692,7 +1703,6 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
 // ~0.5 MB each and the pass ended ~0.5 ms after the median wave (tools/k2_wave_profile.py,
 // profiles/r03e/wave_c4.json: 68% of the span busy); in-process A/B on config4 (profiles/r03h,
 // r03i ab_c4.json): 1-pair items 1.56 ms, 2-pair 1.21, 4-pair 1.26-1.28 -- 8 per wave gives 2-pair
-constexpr uint64_t kK2BigPairBytes = 16384;
 constexpr uint32_t kK2ItemsPerWaveBig = 8, kK2MaxSubShiftBig = 6;
 
 // 64-pair chunks split into 2^k items until there are >= kK2ItemsPerWave items per resident wave
@@ -1781,7 +1791,7 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
 // no pair-split tail (k2_tail_chunks() == 0: the items of large pairs are split to 1-2 pairs already)
 static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uint32_t nwaves, uint32_t sub,
                              uint32_t tail) {
-    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 0 || (v >= 10 && v <= 12) || v == 14 || v == 15)) return 0;
+    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v == 14 || v == 15)) return 0;
     if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
     const uint32_t r = k2_lpt_round(nch << sub, nwaves);
     return r <= kK2LptMax ? r : 0;
@@ -1792,7 +1802,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
     uint4* cc = (uint4*)b.chunk_counts;
     const uint32_t sub = k2_sub_shift(b, c1 - c0);
-    const uint32_t v = b.k2_variant & 15u;
+    const uint32_t v = k2_variant_of(b);
     const uint32_t tq = k2_tail_q(b);
     const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq) : 0u;
     const uint32_t lpt = nsegs == 1 ? k2_lpt_items(b, v, c1 - c0, grid.x * 4u, sub, tail) : 0u;
@@ -1819,7 +1829,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
                    ((b.k2_deep_mode & 3u) << 18), perm
-    k2_kernel(b.k2_variant)<<<grid, 256, 0, s>>>(K2ARGS);
+    k2_kernel(v)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
 }
