@@ -1651,7 +1651,8 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 12: return k_compare_flat<16, 1, true>;  // x16
         case 13: return k_compare_flat<4, 1, true, false, true>;  // + next rows prefetched into LDS (RPF)
         case 10: return k_compare_flat<8, 1, true>;  // 8 chunks a side in flight, 3 waves/SIMD
-        case 14: return k_compare_flat<4, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
+        case 14: return k_compare_flat<8, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
+        case 16: return k_compare_flat<16, 1, true, true>;  // (variant 14 on deep pairs, by k2_variant_of)
         case 15: return k_compare_flat<2, 1, true>;
         // 0 is resolved by k2_variant_of (10 or 12); items handed out dynamically (5% shorter than static
         // striding = variant 8 on config3, tools/ab_k2.py on MI355X)
@@ -1661,7 +1662,7 @@ static K2Fn k2_kernel(uint32_t variant) {
 
 static bool k2_is_dyn(uint32_t variant) {
     switch (variant) {
-        case 0: case 7: case 10: case 11: case 12: case 13: case 14: case 15: return true;
+        case 0: case 7: case 10: case 11: case 12: case 13: case 14: case 15: case 16: return true;
         default: return false;
     }
 }
@@ -1674,7 +1675,9 @@ static bool k2_is_dyn(uint32_t variant) {
 constexpr uint64_t kK2BigPairBytes = 16384;
 static uint32_t k2_variant_of(const DiffBuffers& b) {
     const uint32_t v = b.k2_variant & 15u;
-    return v ? v : (b.avg_pair_bytes >= kK2BigPairBytes ? 12u : 10u);
+    const bool big = b.avg_pair_bytes >= kK2BigPairBytes;
+    if (v == 14) return big ? 16u : 14u;  // the profiled kernel follows the default's shape choice
+    return v ? v : (big ? 12u : 10u);
 }
 
 constexpr uint32_t kK2LptMax = 8192;  // largest-first round: at most this many items (one per resident wave)
@@ -1686,7 +1689,7 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     // one resident 256-thread block per CU per wave slot a SIMD offers the
     // kernel (its measured occupancy, hipOccupancyMaxActiveBlocksPerMultiprocessor):
     // a larger grid would leave blocks waiting for a free slot, i.e. a tail
-    static int occ[16] = {0};
+    static int occ[17] = {0};
     const uint32_t v = k2_variant_of(b);
     if (!occ[v]) {
         int n = 0;
@@ -1791,7 +1794,7 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
 // no pair-split tail (k2_tail_chunks() == 0: the items of large pairs are split to 1-2 pairs already)
 static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uint32_t nwaves, uint32_t sub,
                              uint32_t tail) {
-    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v == 14 || v == 15)) return 0;
+    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v >= 14)) return 0;
     if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
     const uint32_t r = k2_lpt_round(nch << sub, nwaves);
     return r <= kK2LptMax ? r : 0;
