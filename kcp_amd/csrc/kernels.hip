@@ -1218,12 +1218,13 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     const uint32_t nch = c_end - c_begin;
     const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
-    const uint32_t nitems = n_full + (tail_c << tail_ish);
-    // largest-first final round (k2_lpt_round; large pairs): the last lpt_r main items are handed out by the
-    // tail counter in tail_perm's order -- by descending bytes -- so the launch ends with its smallest items;
-    // the bulk stays in index order (neighbouring waves stream neighbouring pool bytes)
+    // largest-first final round (k2_lpt_round; large pairs): the pairs of the last lpt_r main items are handed
+    // out one pair an item by the tail counter in tail_perm's order -- by descending bytes -- so the launch ends
+    // with its smallest pairs; the bulk stays in index order (neighbouring waves stream neighbouring pool bytes)
     const uint32_t lpt_r = (DYN && !RPF && tail_perm && tail_c == 0u) ? k2_lpt_round(n_full, nwaves) : 0u;
     const uint32_t n_main = n_full - lpt_r;
+    const uint32_t lpt_p0 = ((c_begin + (n_main >> sub_shift)) << 6) + (n_main & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
+    const uint32_t nitems = lpt_r ? n_main + (lpt_r << (6u - sub_shift)) : n_full + (tail_c << tail_ish);
     // Two ticket counters per segment: main items are taken with a prefetch (the next main ticket as an
     // item starts, waited for only at its end); tail items from their own counter only when a wave is
     // free. With one counter a prefetch made as a long main item started could reserve a tail item,
@@ -1250,9 +1251,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         }
     };
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
-        // the item this ticket stands for: in the largest-first round, the permuted main item
-        const uint32_t im = (lpt_r && it >= n_main && it < n_full) ? n_main + tail_perm[it - n_main] : it;
-        const bool tail = im >= n_full;
+        // the item this ticket stands for: in the largest-first round, one pair (the permuted order)
+        const bool lpt = lpt_r && it >= n_main;
+        const uint32_t im = lpt ? 0u : it;
+        const bool tail = !lpt && im >= n_full;
         // the next main ticket: fetched while this item streams (with RPF only after this item's rows are
         // read from LDS -- the LDS read waits on vmcnt, which would otherwise wait for the atomic's return)
         if constexpr (DYN && !RPF) {
@@ -1265,11 +1267,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_last = tp_i;
             tp_items++;
         }
-        const uint32_t ish = tail ? tail_ish : sub_shift;
+        const uint32_t ish = lpt ? 6u : tail ? tail_ish : sub_shift;
         const uint32_t j = tail ? im - n_full : im;
-        const uint32_t c = c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
+        const uint32_t lp = lpt ? lpt_p0 + tail_perm[it - n_main] : 0u;
+        const uint32_t c = lpt ? lp >> 6 : c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
         const uint32_t per = 64u >> ish;
-        const uint32_t p0 = (c << 6) + (j & ((1u << ish) - 1u)) * per;
+        const uint32_t p0 = lpt ? lp : (c << 6) + (j & ((1u << ish) - 1u)) * per;
         if (p0 >= n) {
             if constexpr (DYN && RPF) {
                 if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
@@ -1751,24 +1754,18 @@ __device__ __forceinline__ uint64_t pair_stream_bytes(const gpudiff_pair_row& r)
     return 65u + 2u * per;
 }
 
-// The largest-first final round's order (items of large pairs): one block sorts the last round's main items
-// by their compared bytes, descending (ties by index), into perm (offsets from the round's first item).
+// The largest-first final round's order (large pairs): one block sorts the pairs of the last round's main items
+// by their compared bytes, descending (ties by index), into perm (offsets from the round's first pair).
 // Cached per batch by the host (launch_compare): the order depends only on the rows and the launch shape, and
 // any permutation is correct -- a stale one only orders the round less well.
 __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __restrict__ rows, uint32_t n,
-                                                     uint32_t c_begin, uint32_t n_main, uint32_t r,
-                                                     uint32_t sub_shift, uint32_t* __restrict__ perm) {
+                                                     uint32_t p_first, uint32_t r, uint32_t* __restrict__ perm) {
     __shared__ uint64_t key[kK2LptMax];
-    const uint32_t per = 64u >> sub_shift;
     uint32_t m2 = 1;
     while (m2 < r) m2 <<= 1;
     for (uint32_t t = threadIdx.x; t < m2; t += blockDim.x) {
-        uint64_t bytes = 0;
-        if (t < r) {
-            const uint32_t m = n_main + t;
-            const uint32_t p0 = ((c_begin + (m >> sub_shift)) << 6) + (m & ((1u << sub_shift) - 1u)) * per;
-            for (uint32_t p = p0; p < min(p0 + per, n); p++) bytes += pair_stream_bytes(rows[p]);
-        }
+        const uint32_t p = p_first + t;
+        const uint64_t bytes = t < r && p < n ? pair_stream_bytes(rows[p]) : 0u;
         // descending bytes, ascending index: sort ascending on (~bytes, t); padding sorts last
         key[t] = t < r ? ((~bytes & 0xFFFFFFFFFFull) << 20) | t : ~0ull;
     }
@@ -1797,7 +1794,7 @@ static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uin
     if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v >= 14)) return 0;
     if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
     const uint32_t r = k2_lpt_round(nch << sub, nwaves);
-    return r <= kK2LptMax ? r : 0;
+    return (r << (6u - sub)) <= kK2LptMax ? r : 0;  // the round's pairs are sorted in one block's LDS
 }
 
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
@@ -1811,17 +1808,18 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     const uint32_t lpt = nsegs == 1 ? k2_lpt_items(b, v, c1 - c0, grid.x * 4u, sub, tail) : 0u;
     const uint32_t* perm = nullptr;
     if (lpt) {
-        const uint32_t n_full = (c1 - c0) << sub;
+        const uint32_t n_main = ((c1 - c0) << sub) - lpt;
+        const uint32_t p_first = ((c0 + (n_main >> sub)) << 6) + (n_main & ((1u << sub) - 1u)) * (64u >> sub);
         const uint64_t key = ((uint64_t)b.n_pairs << 32) ^ ((uint64_t)lpt << 12) ^ ((uint64_t)sub << 8) ^ c0 ^
                              ((uint64_t)(uintptr_t)b.rows << 7);
         if (*b.tail_perm_key != key) {
-            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, c0, n_full - lpt, lpt, sub, b.tail_perm);
+            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, p_first, lpt << (6u - sub), b.tail_perm);
             *b.tail_perm_key = key;
         }
         perm = b.tail_perm;
     }
-    if (sub || tail || reset_summary) {  // split chunks accumulate their counts with atomics
-        const uint32_t z0 = sub ? c0 : c1 - tail;
+    if (sub || tail || lpt || reset_summary) {  // split chunks accumulate their counts with atomics
+        const uint32_t z0 = sub ? c0 : lpt ? c0 + ((((c1 - c0) << sub) - lpt) >> sub) : c1 - tail;
         const uint32_t ncc = c1 - z0;
         k_pass_reset<<<std::max(1u, std::min(1024u, (ncc + 255u) / 256u)), 256, 0, s>>>(
             reset_summary ? b.summary : nullptr, kSummaryWords, cc + z0, ncc);
