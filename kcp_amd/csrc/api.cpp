@@ -460,7 +460,7 @@ static int alloc_outputs(gpudiff_dbatch* d) {
         (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) || (rc = dalloc(&d->nbits, np)) ||
         (rc = dalloc(&d->noop_d, np)) ||
         (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments)) ||
-        (rc = dalloc(&d->tail_perm, 8192))) {
+        (rc = dalloc(&d->tail_perm, 16384))) {
         d->chunk_counts = cc;
         return rc;
     }

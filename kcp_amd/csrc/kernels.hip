@@ -1103,8 +1103,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* _
 // four per wave), unless the whole launch is split already
 // a tail of q quarters of the launch's wave count, in 64-pair chunks
 // items of the largest-first final round: one per resident wave, at most half the launch's main items
-__host__ __device__ inline uint32_t k2_lpt_round(uint32_t n_full, uint32_t nwaves) {
-    const uint32_t r = nwaves < n_full / 2u ? nwaves : n_full / 2u;
+__host__ __device__ inline uint32_t k2_lpt_round(uint32_t n_full, uint32_t nwaves, uint32_t rounds) {
+    const uint32_t want = rounds * nwaves;
+    const uint32_t r = want < n_full / 2u ? want : n_full / 2u;
     return r < 2u ? 0u : r;
 }
 __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t q) {
@@ -1221,7 +1222,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     // largest-first final round (k2_lpt_round; large pairs): the pairs of the last lpt_r main items are handed
     // out one pair an item by the tail counter in tail_perm's order -- by descending bytes -- so the launch ends
     // with its smallest pairs; the bulk stays in index order (neighbouring waves stream neighbouring pool bytes)
-    const uint32_t lpt_r = (DYN && !RPF && tail_perm && tail_c == 0u) ? k2_lpt_round(n_full, nwaves) : 0u;
+    const uint32_t lpt_rounds = (sub_arg >> 20) & 3u;  // launch_compare: 0 when the round is off
+    const uint32_t lpt_r = (DYN && !RPF && tail_perm && tail_c == 0u && lpt_rounds) ? k2_lpt_round(n_full, nwaves, lpt_rounds) : 0u;
     const uint32_t n_main = n_full - lpt_r;
     const uint32_t lpt_p0 = ((c_begin + (n_main >> sub_shift)) << 6) + (n_main & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
     const uint32_t nitems = lpt_r ? n_main + (lpt_r << (6u - sub_shift)) : n_full + (tail_c << tail_ish);
@@ -1683,7 +1685,9 @@ static uint32_t k2_variant_of(const DiffBuffers& b) {
     return v ? v : (big ? 12u : 10u);
 }
 
-constexpr uint32_t kK2LptMax = 8192;  // largest-first round: at most this many items (one per resident wave)
+constexpr uint32_t kK2LptMax = 16384;  // largest-first rounds: at most this many pairs (one block sorts them in LDS)
+// largest-first rounds for deep pairs (GPUDIFF_OPT_K2_TAIL8 there: one instead of two)
+static uint32_t k2_lpt_rounds(const DiffBuffers& b) { return b.k2_tail8 ? 1u : 2u; }
 constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
 constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
@@ -1760,14 +1764,16 @@ __device__ __forceinline__ uint64_t pair_stream_bytes(const gpudiff_pair_row& r)
 // any permutation is correct -- a stale one only orders the round less well.
 __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __restrict__ rows, uint32_t n,
                                                      uint32_t p_first, uint32_t r, uint32_t* __restrict__ perm) {
-    __shared__ uint64_t key[kK2LptMax];
+    __shared__ uint32_t key[kK2LptMax];  // 64 KiB
     uint32_t m2 = 1;
     while (m2 < r) m2 <<= 1;
     for (uint32_t t = threadIdx.x; t < m2; t += blockDim.x) {
         const uint32_t p = p_first + t;
         const uint64_t bytes = t < r && p < n ? pair_stream_bytes(rows[p]) : 0u;
-        // descending bytes, ascending index: sort ascending on (~bytes, t); padding sorts last
-        key[t] = t < r ? ((~bytes & 0xFFFFFFFFFFull) << 20) | t : ~0ull;
+        // descending bytes (in 16-B units, saturating at 1 MiB), ascending index: sort ascending on
+        // (~bytes16, t); padding sorts last
+        const uint32_t b16 = (uint32_t)min(bytes >> 4, (uint64_t)0xFFFFu);
+        key[t] = t < r ? ((0xFFFFu - b16) << 16) | t : ~0u;
     }
     __syncthreads();
     for (uint32_t k = 2; k <= m2; k <<= 1)
@@ -1775,7 +1781,7 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
             for (uint32_t i = threadIdx.x; i < m2; i += blockDim.x) {
                 const uint32_t l = i ^ j;
                 if (l > i) {
-                    const uint64_t a = key[i], bb = key[l];
+                    const uint32_t a = key[i], bb = key[l];
                     if (((i & k) == 0) == (a > bb)) {
                         key[i] = bb;
                         key[l] = a;
@@ -1784,7 +1790,7 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
             }
             __syncthreads();
         }
-    for (uint32_t t = threadIdx.x; t < r; t += blockDim.x) perm[t] = (uint32_t)(key[t] & 0xFFFFFu);
+    for (uint32_t t = threadIdx.x; t < r; t += blockDim.x) perm[t] = key[t] & 0xFFFFu;
 }
 
 // the launch's largest-first round (0 = none): large pairs only, DYN variants without the LDS row prefetch,
@@ -1793,7 +1799,7 @@ static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uin
                              uint32_t tail) {
     if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v >= 14)) return 0;
     if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
-    const uint32_t r = k2_lpt_round(nch << sub, nwaves);
+    const uint32_t r = k2_lpt_round(nch << sub, nwaves, k2_lpt_rounds(b));
     return (r << (6u - sub)) <= kK2LptMax ? r : 0;  // the round's pairs are sorted in one block's LDS
 }
 
@@ -1829,7 +1835,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
-                   ((b.k2_deep_mode & 3u) << 18), perm
+                   ((b.k2_deep_mode & 3u) << 18) | (lpt ? k2_lpt_rounds(b) << 20 : 0u), perm
     k2_kernel(v)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();
