@@ -1686,8 +1686,9 @@ static uint32_t k2_variant_of(const DiffBuffers& b) {
 }
 
 constexpr uint32_t kK2LptMax = 16384;  // largest-first rounds: at most this many pairs (one block sorts them in LDS)
-// largest-first rounds for deep pairs (GPUDIFF_OPT_K2_TAIL8 there: one instead of two)
-static uint32_t k2_lpt_rounds(const DiffBuffers& b) { return b.k2_tail8 ? 1u : 2u; }
+// largest-first rounds for deep pairs: one (GPUDIFF_OPT_K2_TAIL8 there: two -- config4 K2 1.093 ms vs 1.060 with
+// one and 1.070 in index order, profiles/r04w: twice the single-pair items scatter the stream further)
+static uint32_t k2_lpt_rounds(const DiffBuffers& b) { return b.k2_tail8 ? 2u : 1u; }
 constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
 constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
