@@ -291,6 +291,11 @@ type Batcher struct {
 	maxBatch int
 	window   time.Duration
 	avgBytes float64 // JSON bytes per event, running average: the next flush's jsonBuf size
+	// pipelined (NewBatcherPipelined): batch k + 1 is submitted before batch k is waited, so the engine
+	// overlaps their host staging, upload, K0 and diff pass; an event's enqueue can then come up to two
+	// windows after its arrival.  The engine keeps two pair batches in flight and a third submit drops the
+	// oldest, so a pipelined batcher must be the engine's only gpudiff_submit user (no one-pair helpers on it).
+	pipelined bool
 }
 
 func (b *Batcher) bytesHint(n int) int { return int(b.avgBytes*float64(n)*1.25) + 4096 }
@@ -303,6 +308,15 @@ func (b *Batcher) noteBytes(total, n int) {
 
 func NewBatcher(e *Engine, maxBatch int, window time.Duration) *Batcher {
 	b := &Batcher{e: e, ch: make(chan event, 4*maxBatch), maxBatch: maxBatch, window: window}
+	go b.loop()
+	return b
+}
+
+// NewBatcherPipelined is NewBatcher with two batches in flight (see Batcher.pipelined): at 131k config3
+// pairs a batch the engine then streams at the PCIe link's rate (DESIGN.md §6, 7.45M pairs/s vs 6.2-6.6M
+// waiting each batch before the next).  tests/goshim.py Batcher(engine=...) restates it.
+func NewBatcherPipelined(e *Engine, maxBatch int, window time.Duration) *Batcher {
+	b := &Batcher{e: e, ch: make(chan event, 4*maxBatch), maxBatch: maxBatch, window: window, pipelined: true}
 	go b.loop()
 	return b
 }
@@ -326,6 +340,7 @@ func (b *Batcher) UpdateStored(slot uint32, oldObj, newObj interface{}, which Wh
 // shrinking batches exactly when the load is high (tests/goshim.py Batcher restates this loop).
 func (b *Batcher) loop() {
 	var pending []event
+	var inflight *flight // pipelined: the batch submitted last, not yet waited
 	timer := time.NewTimer(b.window)
 	for {
 		select {
@@ -336,9 +351,19 @@ func (b *Batcher) loop() {
 			}
 		case <-timer.C:
 		}
-		if len(pending) > 0 {
+		if len(pending) > 0 && b.pipelined {
+			f := b.submitFlight(pending) // the engine works on it while the previous batch is settled
+			if inflight != nil {
+				b.finishFlight(inflight)
+			}
+			inflight = f
+			pending = make([]event, 0, b.maxBatch) // f keeps the old slice
+		} else if len(pending) > 0 {
 			b.flush(pending)
 			pending = pending[:0]
+		} else if inflight != nil { // a window with no new events: settle the batch in flight
+			b.finishFlight(inflight)
+			inflight = nil
 		}
 		if !timer.Stop() {
 			select {
@@ -426,19 +451,35 @@ func (j *jsonBuf) at(off, n int) (*C.uint8_t, C.size_t) {
 
 func (j *jsonBuf) free() { C.free(j.p) }
 
-func (b *Batcher) flush(evs []event) {
+// flight is one submitted batch: its events, which pair each event became (-1: enqueued without asking
+// the engine, e.g. a non-transferable object), the C memory the engine reads until gpudiff_wait, the ticket.
+type flight struct {
+	evs    []event
+	pairOf []int
+	ok     []bool // per pair: transferable (false: reported dirty whatever the engine says)
+	n      int
+	rc     C.int
+	ticket C.gpudiff_ticket
+	jb     *jsonBuf
+	cmem   unsafe.Pointer
+}
+
+func (b *Batcher) flush(evs []event) { b.finishFlight(b.submitFlight(evs)) }
+
+// submitFlight stages a batch and submits it (gpudiff_submit or gpudiff_store_submit) without waiting.
+func (b *Batcher) submitFlight(evs []event) *flight {
 	if b.store != nil {
-		b.flushStored(evs)
-		return
+		return b.submitStored(evs)
 	}
 	n := len(evs)
+	f := &flight{evs: evs, pairOf: make([]int, n), ok: make([]bool, n), n: n}
 	pairs := (*[1 << 28]C.gpudiff_json_pair)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_json_pair{}))))[:n:n]
-	defer C.free(unsafe.Pointer(&pairs[0]))
-	jb := newJSONBuf(b.bytesHint(n))
-	defer jb.free()
-	bad := make([]bool, n)
+	f.cmem = unsafe.Pointer(&pairs[0])
+	f.jb = newJSONBuf(b.bytesHint(n))
+	jb := f.jb
 	offs := make([]int, 4*n) // old off, len, new off, len: pointers only once the buffer stops moving
 	for i, ev := range evs {
+		f.pairOf[i] = i
 		mark := len(jb.buf)
 		oa, la, ok1 := jb.add(ev.old)
 		var oc, lc int
@@ -446,8 +487,8 @@ func (b *Batcher) flush(evs []event) {
 		if ok1 {
 			oc, lc, ok2 = jb.add(ev.new)
 		}
-		if !ok1 || !ok2 {
-			bad[i] = true
+		f.ok[i] = ok1 && ok2
+		if !f.ok[i] {
 			jb.buf = jb.buf[:mark]
 			oa, la = jb.raw([]byte("{}"))
 			oc, lc = oa, la
@@ -462,24 +503,40 @@ func (b *Batcher) flush(evs []event) {
 			pair_id: C.uint32_t(i)}
 	}
 	b.e.mu.Lock()
-	var ticket C.gpudiff_ticket
-	rc := C.gpudiff_submit(b.e.ctx, &pairs[0], C.size_t(n), &ticket)
-	var res C.gpudiff_result
-	if rc == C.GPUDIFF_OK {
-		rc = C.gpudiff_wait(b.e.ctx, ticket, &res)
-	}
-	flags := make([]uint8, n)
-	if rc == C.GPUDIFF_OK {
-		copy(flags, (*[1 << 30]uint8)(unsafe.Pointer(res.pair_flags))[:n:n])
-		C.gpudiff_result_release(b.e.ctx, &res)
-	}
+	f.rc = C.gpudiff_submit(b.e.ctx, &pairs[0], C.size_t(n), &f.ticket)
 	b.e.mu.Unlock()
-	for i, ev := range evs {
-		// device or encode failure: conservative, like the reference's type
-		// assertion failure -> enqueue
-		if rc != C.GPUDIFF_OK || bad[i] || flags[i]&uint8(ev.which) != 0 {
+	return f
+}
+
+// finishFlight waits for a submitted batch and calls its events' enqueue in arrival order: the dirty ones
+// for their own predicate, the non-transferable ones, and every one if the engine failed (conservative,
+// like the reference's failed type assertion -> enqueue, specsyncer.go:20-22).
+func (b *Batcher) finishFlight(f *flight) {
+	flags := make([]uint8, f.n)
+	rc := f.rc
+	if f.n > 0 {
+		b.e.mu.Lock()
+		var res C.gpudiff_result
+		if rc == C.GPUDIFF_OK {
+			rc = C.gpudiff_wait(b.e.ctx, f.ticket, &res)
+		}
+		if rc == C.GPUDIFF_OK {
+			copy(flags, (*[1 << 30]uint8)(unsafe.Pointer(res.pair_flags))[:f.n:f.n])
+			C.gpudiff_result_release(b.e.ctx, &res)
+		}
+		b.e.mu.Unlock()
+	}
+	for i, ev := range f.evs {
+		k := f.pairOf[i]
+		if k < 0 || rc != C.GPUDIFF_OK || !f.ok[k] || flags[k]&uint8(ev.which) != 0 {
 			ev.enqueue(ev.new)
 		}
+	}
+	if f.jb != nil {
+		f.jb.free()
+	}
+	if f.cmem != nil {
+		C.free(f.cmem)
 	}
 }
 
@@ -526,33 +583,35 @@ func (b *Batcher) WithStore(st *Store) *Batcher {
 	return b
 }
 
-func (b *Batcher) flushStored(evs []event) {
+func (b *Batcher) submitStored(evs []event) *flight {
 	// events whose objects are not Unstructured never reach the store (its slot
 	// state must only see real versions); they are enqueued, as the reference's
-	// failed type assertion would (specsyncer.go:20-22)
+	// failed type assertion would (specsyncer.go:20-22) -- in arrival order, when the batch finishes
+	f := &flight{evs: evs, pairOf: make([]int, len(evs))}
 	good := make([]int, 0, len(evs))
 	for i, ev := range evs {
 		if _, ok := ev.new.(*unstructured.Unstructured); ok && ev.slot >= 0 {
+			f.pairOf[i] = len(good)
 			good = append(good, i)
 		} else {
-			ev.enqueue(ev.new)
+			f.pairOf[i] = -1
 		}
 	}
 	n := len(good)
+	f.n, f.ok = n, make([]bool, n)
 	if n == 0 {
-		return
+		return f
 	}
 	ce := (*[1 << 27]C.gpudiff_event)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_event{}))))[:n:n]
-	defer C.free(unsafe.Pointer(&ce[0]))
-	jb := newJSONBuf(b.bytesHint(n))
-	defer jb.free()
-	ok := make([]bool, n)
+	f.cmem = unsafe.Pointer(&ce[0])
+	f.jb = newJSONBuf(b.bytesHint(n))
+	jb := f.jb
 	offs := make([]int, 4*n) // new off, len, old off, len (len 0: absent)
 	for k, i := range good {
 		ev := evs[i]
 		if o, l, okn := jb.add(ev.new); okn {
 			offs[4*k], offs[4*k+1] = o, l
-			ok[k] = true
+			f.ok[k] = true
 		} else {
 			offs[4*k], offs[4*k+1] = jb.raw([]byte("{")) // undecodable: reported dirty, slot emptied
 		}
@@ -567,24 +626,9 @@ func (b *Batcher) flushStored(evs []event) {
 		ce[k].old_json, ce[k].old_len = jb.at(offs[4*k+2], offs[4*k+3])
 	}
 	b.e.mu.Lock()
-	var ticket C.gpudiff_ticket
-	rc := C.gpudiff_store_submit(b.e.ctx, b.store.s, &ce[0], C.size_t(n), &ticket)
-	var res C.gpudiff_result
-	if rc == C.GPUDIFF_OK {
-		rc = C.gpudiff_wait(b.e.ctx, ticket, &res)
-	}
-	flags := make([]uint8, n)
-	if rc == C.GPUDIFF_OK {
-		copy(flags, (*[1 << 30]uint8)(unsafe.Pointer(res.pair_flags))[:n:n])
-		C.gpudiff_result_release(b.e.ctx, &res)
-	}
+	f.rc = C.gpudiff_store_submit(b.e.ctx, b.store.s, &ce[0], C.size_t(n), &f.ticket)
 	b.e.mu.Unlock()
-	for k, i := range good {
-		ev := evs[i]
-		if rc != C.GPUDIFF_OK || !ok[k] || flags[k]&uint8(ev.which) != 0 {
-			ev.enqueue(ev.new)
-		}
-	}
+	return f
 }
 
 var errNoEngine = errors.New("gpudiff: engine not initialised")

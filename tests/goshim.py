@@ -211,14 +211,19 @@ class Batcher:
     tests).  Dirty events are enqueued in arrival order; a pair the shim cannot transfer is enqueued
     without asking the engine (specsyncer.go:20-22)."""
 
-    def __init__(self, decide, max_batch: int, window: float, flush_cost: float = 0.0, drain: bool = True):
+    def __init__(self, decide, max_batch: int, window: float, flush_cost: float = 0.0, drain: bool = True,
+                 engine=None):
+        """engine (NewBatcherPipelined): an object with submit(pairs) -> ticket and wait(ticket) -> flags; batch
+        k + 1 is submitted before batch k is waited and enqueued, and a window with no new events settles the
+        batch in flight."""
         self.decide, self.max_batch, self.window = decide, max_batch, window
-        self.flush_cost, self.drain = flush_cost, drain
+        self.flush_cost, self.drain, self.engine = flush_cost, drain, engine
         self.enqueued: List[str] = []
         self.flushes: List[int] = []
         self.buffers: List[bytes] = []
+        self.inflight = None
 
-    def flush(self, evs):
+    def _stage(self, evs):
         jb = JsonBuf()
         bad, offs = [], []
         for (_t, a, b, _which, _name) in evs:
@@ -234,12 +239,29 @@ class Batcher:
             offs.append((oa, ob))
         buf = bytes(jb.buf)
         self.buffers.append(buf)
-        pairs = [(buf[oa[0]:oa[0] + oa[1]], buf[ob[0]:ob[0] + ob[1]]) for oa, ob in offs]
-        flags = self.decide(pairs)
+        return bad, [(buf[oa[0]:oa[0] + oa[1]], buf[ob[0]:ob[0] + ob[1]]) for oa, ob in offs]
+
+    def _enqueue(self, evs, flags, bad):
         for (ev, f, bd) in zip(evs, flags, bad):
             if bd or (f & ev[3]):
                 self.enqueued.append(ev[4])
+
+    def flush(self, evs):
+        bad, pairs = self._stage(evs)
         self.flushes.append(len(evs))
+        if self.engine is None:
+            self._enqueue(evs, self.decide(pairs), bad)
+            return
+        # pipelined (gpudiff.go submitFlight / finishFlight): submit this batch, then settle the one before
+        flight = (list(evs), bad, self.engine.submit(pairs))
+        self.settle()
+        self.inflight = flight
+
+    def settle(self):
+        if self.inflight is not None:
+            evs, bad, ticket = self.inflight
+            self.inflight = None
+            self._enqueue(evs, self.engine.wait(ticket), bad)
 
     def run(self, events):
         """events sorted by arrival time; returns the enqueued names in order.  Events that arrived while
@@ -250,7 +272,7 @@ class Batcher:
         deadline = self.window  # timer armed at 0
         stale_tick = False      # a fired tick left in the channel (the old Reset-without-drain code)
         i = 0
-        while i < len(events) or pending:
+        while i < len(events) or pending or self.inflight is not None:
             nxt = events[i][0] if i < len(events) else float("inf")
             if stale_tick:
                 stale_tick = False
@@ -271,6 +293,8 @@ class Batcher:
             if pending:
                 self.flush(pending)
                 pending = []
+            elif fire:
+                self.settle()  # a window with no new events: the batch in flight is waited and enqueued
             now += self.flush_cost
             if not fire and now >= deadline and not self.drain:
                 stale_tick = True  # the timer fired during the flush and Reset does not drain it

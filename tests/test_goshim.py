@@ -208,3 +208,43 @@ def test_batcher_timer_drain_keeps_batches_full():
     assert a == b
     assert all(f == 16 for f in new.flushes[1:-1]) and len(new.flushes) > 5  # the first: the window
     assert min(old.flushes) <= 2 and len(old.flushes) > len(new.flushes)
+
+
+class _RingEngine:
+    """gpudiff_submit / gpudiff_wait with the pair path's ring rule: at most two batches outstanding (a third
+    submit drops the oldest ticket, whose wait then fails); records the call order."""
+
+    def __init__(self):
+        self.next, self.out, self.calls = 1, {}, []
+
+    def submit(self, pairs):
+        t = self.next
+        self.next += 1
+        self.out[t] = _oracle_decide(pairs)
+        assert len(self.out) <= 2, "more than two batches in flight"
+        self.calls.append(("submit", t))
+        return t
+
+    def wait(self, t):
+        self.calls.append(("wait", t))
+        return self.out.pop(t)
+
+
+def test_pipelined_batcher_same_queue_two_in_flight():
+    """NewBatcherPipelined: batch k + 1 is submitted before batch k is waited (the engine overlaps their
+    staging, upload, K0 and diff), never more than two outstanding; the queue is the synchronous batcher's,
+    in arrival order, and an idle window settles the last batch."""
+    evs = _event_stream(300, seed=5)
+    evs = [((e[0] if i < 150 else 15.0 + (i - 150) * 0.4),) + e[1:] for i, e in enumerate(evs)]
+    sync = gs.Batcher(_oracle_decide, max_batch=20, window=2.5)
+    eng = _RingEngine()
+    pipe = gs.Batcher(None, max_batch=20, window=2.5, engine=eng)
+    want, got = sync.run(evs), pipe.run(evs)
+    assert got == want and len(want) > 50
+    assert pipe.flushes == sync.flushes and not eng.out
+    subs = [t for k, t in eng.calls if k == "submit"]
+    assert subs == list(range(1, len(subs) + 1))
+    # every wait but the last comes right after the next batch's submit
+    for k, (kind, t) in enumerate(eng.calls[:-1]):
+        if kind == "wait":
+            assert eng.calls[k - 1] == ("submit", t + 1)
