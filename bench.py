@@ -610,8 +610,13 @@ def main():
                          "k2_source_hash": src_hash,
                          # the physical rate: HBM counter bytes (FETCH_SIZE x 2 + WRITE_SIZE per K2 launch) over
                          # this run's K2 time -- what the memory system moved, whatever the byte definition
-                         "frac_physical": (traffic / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS) if traffic and k2_ms else None,
-                         "frac_physical_def": "PMC traffic per K2 launch / K2 HIP-event time / 8 TB/s",
+                         # (with no PMC summary of these K2 sources and this workload, the bytes K2's format
+                         # reads stand in -- a lower bound of what it moves, never the definitional SURVEY count)
+                         "frac_physical": ((traffic if traffic else fmt_bytes / launches) / (k2_ms * 1e-3) / 1e9 /
+                                           HBM_PEAK_GBPS) if k2_ms else None,
+                         "frac_physical_def": ("PMC traffic per K2 launch / K2 HIP-event time / 8 TB/s" if traffic else
+                                               "format bytes per K2 launch / K2 HIP-event time / 8 TB/s (no PMC "
+                                               "summary of these K2 sources on this workload)"),
                          "survey_over_format_bytes": survey_bytes / fmt_bytes if fmt_bytes else None,
                          "traffic_box": traffic_box, "traffic_rocprof_k2_ms": traffic_rocprof_ms,
                          "box": box_id()},
