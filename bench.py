@@ -781,15 +781,34 @@ def json_in_rates(G, pop, m, threads, device):
         if mode == "device_encode":
             out[mode]["phases_ms"] = json_in_phases(G, arr, m, threads, device)
             out["device_encode_streaming"] = json_in_streaming(G, arr, m, threads, device)
+    # zero copy: the pairs rendered into a gpudiff_host_alloc buffer in the upload layout (what the batcher does
+    # when it renders a flush into engine-pinned memory; the layout copy here is untimed), uploaded without the
+    # staging copy
+    e = G.Engine(device=device, encode_threads=threads, device_encode=True)
+    pj = G.PinnedJson(e, buf, offs)
+    for _ in range(2):
+        r = e.wait(e.submit_array(pj.pairs))
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        r = e.wait(e.submit_array(pj.pairs))
+        times.append(time.perf_counter() - t0)
+    flags["device_encode_zero_copy"] = r.pair_flags
+    best = min(times)
+    out["device_encode_zero_copy"] = dict(pairs_per_s=m / best, ms=best * 1e3, json_gb_per_s=int(offs[-1]) / best / 1e9,
+                                          zero_copy_batches=int(e.submit_stats().zero_copy_batches),
+                                          streaming=json_in_streaming(G, pj.pairs, m, threads, device, engine=e))
+    pj.free()
+    e.close()
     out["modes_agree"] = all(bool(np.array_equal(flags["host_encode"], f)) for f in flags.values())
     return out
 
 
-def json_in_streaming(G, arr, m, threads, device, batches=6):
+def json_in_streaming(G, arr, m, threads, device, batches=6, engine=None):
     """Device-encoded JSON-in as an informer stream feeds it: batch k + 1 is submitted before batch k is waited
     (the engine keeps two in flight), so host staging, the PCIe upload, K0 and the diff pass of neighbouring
     batches overlap.  pairs/s over `batches` batches of the same m pairs, first submit to last wait."""
-    e = G.Engine(device=device, encode_threads=threads, device_encode=True)
+    e = engine or G.Engine(device=device, encode_threads=threads, device_encode=True)
     for _ in range(2):
         e.wait(e.submit_array(arr))
     flags_ok = True
@@ -805,7 +824,8 @@ def json_in_streaming(G, arr, m, threads, device, batches=6):
     r = e.wait(tk)
     dt = time.perf_counter() - t0
     flags_ok &= bool(np.array_equal(r.pair_flags, want))
-    e.close()
+    if engine is None:
+        e.close()
     return dict(pairs_per_s=m * batches / dt, ms_per_batch=dt / batches * 1e3, batches=batches,
                 json_gb_per_s=int(arr["old_len"].sum() + arr["new_len"].sum()) * batches / dt / 1e9,
                 batches_agree=flags_ok)

@@ -360,7 +360,7 @@ typedef struct gpudiff_store_stats {
      * enqueue of copies and kernels; and the store's part of gpudiff_wait */
     float submit_wait_ms, submit_docs_ms, submit_copy_ms, submit_enqueue_ms, finish_ms;
     uint32_t timing_batches; /* batches the means are over */
-    uint32_t pad;
+    uint32_t zero_copy_batches; /* gpudiff_submit batches uploaded straight from a gpudiff_host_alloc buffer */
     uint64_t space_conservative; /* device-encode: deferred events reported dirty (GPUDIFF_DECODE_ERROR, slot
                                     emptied) because the space could not take their re-encoded blobs */
 } gpudiff_store_stats;
@@ -390,6 +390,16 @@ int gpudiff_store_stats_get(const gpudiff_store* st, gpudiff_store_stats* out);
  * context's first device-encoded submit. */
 int gpudiff_submit_stats_get(gpudiff_ctx* ctx, gpudiff_store_stats* out);
 void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
+/* Pinned host memory for gpudiff_submit's JSON on a device-encode context (no reference counterpart: the syncer
+ * batcher renders each flush's objects into it).  A batch whose documents all lie in ONE such
+ * buffer, in pair order (old_0, new_0, old_1, new_1, ...), each at a 16-B aligned address and followed by at
+ * least its staged span -- len + 32 bytes rounded up to 16 -- before the next document (the last one's span and
+ * 32 more bytes inside the buffer) is uploaded straight from it: no staging copy.  The engine zeroes each
+ * document's padding up to that span (those bytes are its to write).  Any other layout takes the staging copy;
+ * results are identical either way (gpudiff_store_stats.zero_copy_batches counts the zero-copy ones).  The
+ * buffer must stay untouched until gpudiff_wait on the ticket returns; free it before gpudiff_close. */
+int gpudiff_host_alloc(gpudiff_ctx* ctx, size_t bytes, void** out);
+int gpudiff_host_free(gpudiff_ctx* ctx, void* p);
 
 /* ---- object encoding in the device-store format (inspection / parity) ----
  * An object's blob followed by its path table (gpudiff_format.h: the node

@@ -32,6 +32,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <unordered_map>
@@ -82,6 +83,27 @@ struct Ring {
     gpudiff_ticket ticket = 0;
     bool outstanding = false;
 };
+
+// gpudiff_host_alloc's pinned buffers: a gpudiff_submit batch laid out in one of them (gpudiff.h) is uploaded
+// straight from it, without the staging copy
+struct HostBuf {
+    gpudiff_ctx* c;
+    uint8_t* p;
+    uint64_t n;
+};
+std::mutex g_hb_mu;
+std::vector<HostBuf> g_hb;
+
+bool find_host_buf(gpudiff_ctx* c, const void* q, uint8_t** base, uint64_t* size) {
+    std::lock_guard<std::mutex> lk(g_hb_mu);
+    for (const HostBuf& h : g_hb)
+        if (h.c == c && (const uint8_t*)q >= h.p && (const uint8_t*)q < h.p + h.n) {
+            *base = h.p;
+            *size = h.n;
+            return true;
+        }
+    return false;
+}
 
 }  // namespace
 
@@ -654,6 +676,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     uint32_t* heads = (uint32_t*)(R.hmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
     std::vector<const uint8_t*> src;
     src.reserve(max_docs);
+    const uint8_t* zsrc = nullptr;  // zero copy: the caller's pinned buffer holds the staged layout (offset 0 here)
     uint32_t nd = 0, nh = 0;
     uint64_t jbytes = 0, bound = 0, floor = 0, new_json_bytes = 0;
     auto add_doc = [&](const uint8_t* p, size_t len, uint32_t slot, uint32_t row, const gpudiff_event& e) {
@@ -696,6 +719,13 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         std::atomic<int> bad{0};
         src.resize(2 * n);
         auto step = [](size_t len) -> uint64_t { return (len + kTokSlack + 15) & ~15ull; };
+        // Zero copy: every document in one gpudiff_host_alloc buffer, 16-B aligned, in pair order, each followed
+        // by its staged span (step) before the next -- then the buffer's range is the staged layout itself
+        uint8_t* zb = nullptr;
+        uint64_t zn = 0;
+        bool zc = ev[0].old_json && find_host_buf(c, ev[0].old_json, &zb, &zn);
+        std::atomic<int> zc_bad{0};
+        const uint8_t* zend = zb + zn - kTokSlack;  // the upload runs kTokSlack past the last document's span
         workers(c).run(T, [&](uint32_t t) {
             uint64_t jb = 0, bd = 0, fl = 0, nj = 0;
             for (size_t i = n * t / T, i1 = n * (t + 1) / T; i < i1; i++) {
@@ -703,6 +733,13 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
                 if (e.slot != i || e.slot >= s->max_slots || !e.new_json || e.new_len > kTokMaxLen ||
                     e.old_len > kTokMaxLen)
                     bad.store(1, std::memory_order_relaxed);
+                if (zc) {
+                    const uint8_t* next = i + 1 < n ? ev[i + 1].old_json : zend;
+                    if (!e.old_json || e.old_json < zb || (((uintptr_t)e.old_json | (uintptr_t)e.new_json) & 15u) ||
+                        e.new_json < e.old_json + step(e.old_len) || !next || next < e.new_json + step(e.new_len) ||
+                        next > zend)
+                        zc_bad.store(1, std::memory_order_relaxed);
+                }
                 const size_t lo = e.old_json ? e.old_len : 0;
                 jb += step(lo) + step(e.new_len);
                 bd += (5 * (uint64_t)lo) / 2 + (5 * (uint64_t)e.new_len) / 2 + 768;
@@ -713,6 +750,8 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
             q[0] = jb, q[1] = bd, q[2] = fl, q[3] = nj;
         });
         if (bad.load()) return GPUDIFF_E_INVAL;
+        zc = zc && !zc_bad.load();
+        const uint8_t* zlo = ev[0].old_json;
         for (uint32_t t = 1; t <= T; t++)
             for (int k = 0; k < 4; k++) part[4 * (size_t)t + k] += part[4 * (size_t)(t - 1) + k];
         workers(c).run(T, [&](uint32_t t) {
@@ -725,9 +764,11 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
                     const size_t k = 2 * i + h;
                     TokDoc& D = docs[k];
                     memset(&D, 0, sizeof(D));
-                    D.json_off = off;
+                    D.json_off = zc ? (uint64_t)(pj[h] - zlo) : off;
                     D.json_len = (uint32_t)len[h];
                     off += step(len[h]);
+                    if (zc)  // the staged span's padding, as the staging copy writes it (gpudiff.h: engine-owned)
+                        memset((uint8_t*)pj[h] + len[h], 0, step(len[h]) - len[h]);
                     DocLink& L = links[k];
                     memset(&L, 0, sizeof(L));
                     L.slot = e.slot;
@@ -746,6 +787,11 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         nd = (uint32_t)(2 * n);
         nh = (uint32_t)n;
         jbytes = tot[0], bound = tot[1], floor = tot[2], new_json_bytes = tot[3];
+        if (zc) {
+            zsrc = zlo;
+            jbytes = (uint64_t)(ev[n - 1].new_json + step(ev[n - 1].new_len) - zlo);
+            s->st.zero_copy_batches++;
+        }
     }
     for (size_t i = 0; i < n && !s->pair_mode; i++) {
         const gpudiff_event& e = ev[i];
@@ -769,7 +815,8 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         new_json_bytes += e.new_len;
     }
     jbytes += kTokSlack;
-    if ((rc = grow_pinned(&R.hjson, &R.hjson_cap, jbytes))) return rc;
+    if (!zsrc && (rc = grow_pinned(&R.hjson, &R.hjson_cap, jbytes))) return rc;
+    const uint8_t* hsrc = zsrc ? zsrc : R.hjson;
     lap(1);
     // Chunks of the batch's JSON (by bytes, whole documents): the host copies chunk c into pinned
     // staging while chunk c - 1 is uploading, and K0 starts on a chunk as soon as it has landed, so
@@ -858,9 +905,9 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     // event), so K0 of chunk q runs while chunk q + 1 is on the link -- not after the host has staged them all
     auto upload = [&](uint32_t q) {
         const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
-        if (q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
+        if (!zsrc && q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
         hipStream_t qs = (q & 1u) ? cs2 : cs;
-        if (hipMemcpyAsync(R.djson + b0, R.hjson + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
+        if (hipMemcpyAsync(R.djson + b0, hsrc + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
             hipEventRecord(R.chunk_ev[q], qs) != hipSuccess || hipStreamWaitEvent(st, R.chunk_ev[q], 0) != hipSuccess ||
             (q == 0 && timing && hipEventRecord(R.t_ev[2], st) != hipSuccess)) {
             up_err.store(1);
@@ -876,6 +923,9 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
             }
         }
     };
+    if (zsrc)  // nothing to stage: every chunk's upload (and its K0 launches) goes out at once
+        while (uploaded < C) upload(uploaded++);
+    else
     workers(c).run(T, [&](uint32_t t) {
         for (uint32_t q = 0; q < C; q++) {
             const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
@@ -1031,6 +1081,32 @@ extern "C" int gpudiff_submit_stats_get(gpudiff_ctx* c, gpudiff_store_stats* out
     if (!c || !out) return GPUDIFF_E_INVAL;
     if (!c->pair_store) return GPUDIFF_E_STATE;
     return dstore_stats(c->pair_store, out);
+}
+
+extern "C" int gpudiff_host_alloc(gpudiff_ctx* c, size_t bytes, void** out) {
+    if (!c || !out || !bytes) return GPUDIFF_E_INVAL;
+    if (!c->has_device) return GPUDIFF_E_NODEVICE;
+    HIPCHK(hipSetDevice(c->device));
+    uint8_t* p = nullptr;
+    if (hipHostMalloc((void**)&p, bytes, hipHostMallocDefault) != hipSuccess) return GPUDIFF_E_NOMEM;
+    {
+        std::lock_guard<std::mutex> lk(g_hb_mu);
+        g_hb.push_back(HostBuf{c, p, (uint64_t)bytes});
+    }
+    *out = p;
+    return GPUDIFF_OK;
+}
+
+extern "C" int gpudiff_host_free(gpudiff_ctx* c, void* p) {
+    if (!c || !p) return GPUDIFF_E_INVAL;
+    {
+        std::lock_guard<std::mutex> lk(g_hb_mu);
+        auto it = std::find_if(g_hb.begin(), g_hb.end(), [&](const HostBuf& h) { return h.c == c && h.p == p; });
+        if (it == g_hb.end()) return GPUDIFF_E_INVAL;
+        g_hb.erase(it);
+    }
+    if (c->has_device) (void)hipSetDevice(c->device);
+    return hipHostFree(p) == hipSuccess ? GPUDIFF_OK : GPUDIFF_E_DEVICE;
 }
 
 int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot) {

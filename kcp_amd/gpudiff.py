@@ -76,6 +76,50 @@ def json_pair_array(buf: np.ndarray, offs: np.ndarray, ids=None, clusters=None) 
     return arr
 
 
+ZC_SLACK = 32  # gpudiff.h gpudiff_host_alloc: a document's staged span is len + 32 rounded up to 16
+
+
+def zero_copy_layout(lens: np.ndarray):
+    """Offsets of documents laid out for gpudiff_submit's zero-copy upload (gpudiff.h gpudiff_host_alloc): each
+    at a 16-B aligned offset, followed by its staged span; returns (offsets, bytes the buffer needs)."""
+    span = (lens.astype(np.uint64) + ZC_SLACK + 15) & ~np.uint64(15)
+    offs = np.zeros(lens.size, np.uint64)
+    np.cumsum(span[:-1], out=offs[1:])
+    return offs, int(offs[-1] + span[-1]) + ZC_SLACK if lens.size else ZC_SLACK
+
+
+class PinnedJson:
+    """A gpudiff_host_alloc buffer holding JSON pairs in the zero-copy layout, with its pair table: what the
+    syncer batcher produces when it renders a flush straight into engine-pinned memory.
+    Free it (or the engine) when done; every submit of `pairs` must be waited first."""
+
+    def __init__(self, eng: "Engine", buf: np.ndarray, offs: np.ndarray, ids=None, clusters=None):
+        n = (len(offs) - 1) // 2
+        o = offs.astype(np.int64)
+        lens = np.diff(o)
+        doffs, nbytes = zero_copy_layout(lens)
+        p = C.c_void_p()
+        _chk(_lib.gpudiff_host_alloc(eng.ctx, nbytes, C.byref(p)), "gpudiff_host_alloc")
+        self.eng, self.ptr, self.nbytes = eng, p.value, nbytes
+        dst = np.ctypeslib.as_array(C.cast(self.ptr, C.POINTER(C.c_uint8)), (nbytes,))
+        src = np.ascontiguousarray(buf)
+        for k in range(2 * n):  # the render step of the batcher (untimed in the benches)
+            a, ln, d = int(o[k]), int(lens[k]), int(doffs[k])
+            dst[d:d + ln] = src[a:a + ln]
+        self.pairs = np.zeros(n, dtype=JSON_PAIR_DTYPE)
+        self.pairs["old_json"] = self.ptr + doffs[0:2 * n:2]
+        self.pairs["old_len"] = lens[0:2 * n:2]
+        self.pairs["new_json"] = self.ptr + doffs[1:2 * n:2]
+        self.pairs["new_len"] = lens[1:2 * n:2]
+        self.pairs["pair_id"] = np.arange(n, dtype=np.uint32) if ids is None else ids
+        self.pairs["cluster_id"] = 0 if clusters is None else clusters
+
+    def free(self):
+        if self.ptr:
+            _chk(_lib.gpudiff_host_free(self.eng.ctx, self.ptr), "gpudiff_host_free")
+            self.ptr = None
+
+
 class PairRow(C.Structure):
     _fields_ = [("off_a", C.c_uint64), ("off_b", C.c_uint64),
                 ("spec_l_a", C.c_uint32), ("spec_l_b", C.c_uint32),
@@ -106,7 +150,7 @@ class StoreStats(C.Structure):
                 ("host_submit_ms", C.c_float), ("h2d_ms", C.c_float), ("encode_ms", C.c_float),
                 ("link_ms", C.c_float), ("submit_wait_ms", C.c_float), ("submit_docs_ms", C.c_float),
                 ("submit_copy_ms", C.c_float), ("submit_enqueue_ms", C.c_float), ("finish_ms", C.c_float),
-                ("timing_batches", C.c_uint32), ("pad", C.c_uint32), ("space_conservative", C.c_uint64)]
+                ("timing_batches", C.c_uint32), ("zero_copy_batches", C.c_uint32), ("space_conservative", C.c_uint64)]
 
 
 class ObjInfo(C.Structure):
@@ -237,6 +281,8 @@ SIGNATURES = [
     ("gpudiff_store_forget", C.c_int, [_P, _P, C.c_uint32]),
     ("gpudiff_store_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
     ("gpudiff_submit_stats_get", C.c_int, [_P, C.POINTER(StoreStats)]),
+    ("gpudiff_host_alloc", C.c_int, [_P, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("gpudiff_host_free", C.c_int, [_P, C.c_void_p]),
     ("gpudiff_store_free", None, [_P, _P]),
     ("gpudiff_encode_objects", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                                          C.c_size_t, C.c_void_p, C.c_uint64, C.POINTER(ObjInfo)]),

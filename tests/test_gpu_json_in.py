@@ -20,7 +20,7 @@ def _same(a, b):
 
 
 def test_multi_chunk_upload_one_and_two_copy_streams():
-    cfg = S.make_cfg("config3", n_pairs=12000, mutate_frac=0.3)
+    cfg = S.make_cfg("config3", n_pairs=40000, mutate_frac=0.3)  # >= 64k documents: 4 chunks (kMinChunkDocs)
     pop = S.Population(cfg)
     buf, offs, _ = pop.json_range(0, pop.n, 8)
     assert int(offs[-1]) >= 3 * (16 << 20)  # at least three upload chunks
@@ -43,18 +43,25 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
     # the default chunks, two copy streams, one chunk, and the most chunks (1 MiB minimum: capped at 16)
     variants = ((0, {}), (G.OPT_H2D_TWO_STREAMS, {}), (0, {"GPUDIFF_H2D_MAX_CHUNKS": "1"}),
                 (G.OPT_H2D_TWO_STREAMS, {"GPUDIFF_H2D_CHUNK_MIB": "1"}))
-    for flags, env in variants:
+    for flags, env in variants + ((0, {"zero_copy": True}),):
+        zero_copy = env.pop("zero_copy", False)
         os.environ.update(env)
         e = G.Engine(device=0, encode_threads=8, device_encode=True, flags=flags)
+        # zero copy: the pairs laid out in a gpudiff_host_alloc buffer, uploaded straight from it
+        pj = G.PinnedJson(e, buf, offs) if zero_copy else None
+        a = pj.pairs if zero_copy else arr
         # two batches in flight (both ring slots), then the same batch again on a reused slot
         try:
-            t1 = e.submit_array(arr)  # creates the device-encode store (reads the environment)
+            t1 = e.submit_array(a)  # creates the device-encode store (reads the environment)
         finally:
             for name in env:
                 os.environ.pop(name)
-        t2 = e.submit_array(arr)
+        t2 = e.submit_array(a)
         r1, r2 = e.wait(t1), e.wait(t2)
-        r3 = e.wait(e.submit_array(arr))
+        r3 = e.wait(e.submit_array(a))
+        assert e.submit_stats().zero_copy_batches == (3 if zero_copy else 0)
+        if pj is not None:
+            pj.free()
         e.close()
         for r in (r1, r2, r3):
             assert _same(r, want), "device encode (flags %#x, %s) differs from host encode" % (flags, env)
@@ -85,3 +92,48 @@ def test_two_in_flight_with_host_resolution():
     deferred = e.submit_stats().deferred
     e.close()
     assert deferred > 0  # the host resolution ran
+
+
+def test_zero_copy_layout_rules():
+    """gpudiff_host_alloc buffers: a batch uploaded straight from one only when every document is 16-B aligned,
+    in pair order and followed by its staged span (and the last by 32 more bytes inside the buffer); packed
+    documents, documents in another buffer or a span running past the buffer's end take the staging copy --
+    results are the host encoder's every time."""
+    from tests.workload import make_pairs
+    pairs, _, _ = make_pairs(600, seed=21, mutate_frac=0.4)
+    flat = b"".join(a + b for a, b in pairs)
+    lens = np.array([len(x) for p in pairs for x in p], np.int64)
+    offs = np.zeros(lens.size + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    buf = np.frombuffer(flat, np.uint8)
+    host = G.Engine(device=0, encode_threads=4)
+    want = host.wait(host.submit_array(G.json_pair_array(buf, offs)))
+    host.close()
+    e = G.Engine(device=0, encode_threads=4, device_encode=True)
+    pj = G.PinnedJson(e, buf, offs)
+    assert _same(e.wait(e.submit_array(pj.pairs)), want)
+    zc = e.submit_stats().zero_copy_batches
+    assert zc == 1
+    # packed into the same pinned buffer (no spans): staged
+    raw = np.ctypeslib.as_array(G.C.cast(pj.ptr, G.C.POINTER(G.C.c_uint8)), (pj.nbytes,))
+    raw[:flat.__len__()] = buf
+    packed = G.json_pair_array(raw, offs)
+    assert _same(e.wait(e.submit_array(packed)), want)
+    assert e.submit_stats().zero_copy_batches == zc
+    pj.free()
+    # the last document's span + 32 bytes past the buffer's end: staged
+    pj = G.PinnedJson(e, buf, offs)
+    short = pj.pairs.copy()
+    last = int(short["new_json"][-1]) - pj.ptr
+    assert last + int(short["new_len"][-1]) <= pj.nbytes
+    tail = pj.nbytes - last  # move the last new object to the very end of the buffer
+    raw = np.ctypeslib.as_array(G.C.cast(pj.ptr, G.C.POINTER(G.C.c_uint8)), (pj.nbytes,))
+    n_last = int(short["new_len"][-1])
+    dst = (pj.nbytes - n_last) & ~15
+    raw[dst:dst + n_last] = raw[last:last + n_last].copy()
+    short["new_json"][-1] = pj.ptr + dst
+    assert tail >= 0
+    assert _same(e.wait(e.submit_array(short)), want)
+    assert e.submit_stats().zero_copy_batches == zc
+    pj.free()
+    e.close()
