@@ -32,8 +32,9 @@ import (
 // reentrant, so every call goes through mu; the Batcher is the intended
 // single submitter.
 type Engine struct {
-	mu  sync.Mutex
-	ctx *C.gpudiff_ctx
+	mu     sync.Mutex
+	ctx    *C.gpudiff_ctx
+	devEnc bool // GPUDIFF_OPT_DEVICE_ENCODE: the batcher renders flushes into engine-pinned memory
 }
 
 func errOf(rc C.int) error {
@@ -63,7 +64,7 @@ func OpenWith(device int, flags uint32) (*Engine, error) {
 	if err := errOf(C.gpudiff_open(&opts, &ctx)); err != nil {
 		return nil, err
 	}
-	return &Engine{ctx: ctx}, nil
+	return &Engine{ctx: ctx, devEnc: flags&uint32(C.GPUDIFF_OPT_DEVICE_ENCODE) != 0}, nil
 }
 
 func (e *Engine) Close() {
@@ -296,9 +297,31 @@ type Batcher struct {
 	// windows after its arrival.  The engine keeps two pair batches in flight and a third submit drops the
 	// oldest, so a pipelined batcher must be the engine's only gpudiff_submit user (no one-pair helpers on it).
 	pipelined bool
+	bufs      []*jsonBuf // idle flush buffers (getJSONBuf)
 }
 
 func (b *Batcher) bytesHint(n int) int { return int(b.avgBytes*float64(n)*1.25) + 4096 }
+
+// getJSONBuf / putJSONBuf keep up to three flush buffers (pinned ones are costly to allocate; a pipelined
+// batcher has two batches' buffers alive at once)
+func (b *Batcher) getJSONBuf(hint int) *jsonBuf {
+	for k, jb := range b.bufs {
+		if jb.n >= hint {
+			b.bufs = append(b.bufs[:k], b.bufs[k+1:]...)
+			jb.buf = jb.buf[:0]
+			return jb
+		}
+	}
+	return newJSONBuf(b.e, hint)
+}
+
+func (b *Batcher) putJSONBuf(jb *jsonBuf) {
+	if jb.e == nil || len(b.bufs) >= 3 {
+		jb.free()
+		return
+	}
+	b.bufs = append(b.bufs, jb)
+}
 
 func (b *Batcher) noteBytes(total, n int) {
 	if n > 0 {
@@ -383,16 +406,28 @@ func (b *Batcher) loop() {
 // Offsets are handed out, not pointers: the buffer may move until the last object is added.
 type jsonBuf struct {
 	p   unsafe.Pointer
-	n   int // capacity of the C allocation
+	n   int // capacity of the allocation
 	buf []byte
+	e   *Engine // non-nil: p is engine-pinned memory (gpudiff_host_alloc) in the zero-copy layout:
+	// every object 16-B aligned and followed by its staged span (len + 32 rounded up to 16, zeroed), so
+	// gpudiff_submit uploads the flush straight from it (gpudiff.h)
 }
 
 // cslice views n bytes of C memory as a Go slice (Go 1.16, the reference's toolchain: no unsafe.Slice)
 func cslice(p unsafe.Pointer, n int) []byte { return (*[1 << 40]byte)(p)[:n:n] }
 
-func newJSONBuf(capHint int) *jsonBuf {
+func newJSONBuf(e *Engine, capHint int) *jsonBuf {
 	if capHint < 4096 {
 		capHint = 4096
+	}
+	if e != nil && e.devEnc {
+		var p unsafe.Pointer
+		e.mu.Lock()
+		rc := C.gpudiff_host_alloc(e.ctx, C.size_t(capHint), &p)
+		e.mu.Unlock()
+		if rc == C.GPUDIFF_OK {
+			return &jsonBuf{p: p, n: capHint, buf: cslice(p, capHint)[:0], e: e}
+		}
 	}
 	p := C.malloc(C.size_t(capHint))
 	return &jsonBuf{p: p, n: capHint, buf: cslice(p, capHint)[:0]}
@@ -400,10 +435,50 @@ func newJSONBuf(capHint int) *jsonBuf {
 
 func (j *jsonBuf) grow(out []byte, start int) {
 	nn := 2 * cap(out)
-	np := C.realloc(j.p, C.size_t(nn)) // keeps [0, start): the objects already in C memory
+	if j.e == nil {
+		np := C.realloc(j.p, C.size_t(nn)) // keeps [0, start): the objects already in C memory
+		dst := cslice(np, nn)
+		copy(dst[start:len(out)], out[start:])
+		j.p, j.n, j.buf = np, nn, dst[:len(out)]
+		return
+	}
+	var np unsafe.Pointer
+	j.e.mu.Lock()
+	rc := C.gpudiff_host_alloc(j.e.ctx, C.size_t(nn), &np)
+	j.e.mu.Unlock()
+	if rc != C.GPUDIFF_OK { // pinned memory exhausted: continue in malloc'd memory (the staged upload)
+		np = C.malloc(C.size_t(nn))
+	}
 	dst := cslice(np, nn)
+	copy(dst[:start], cslice(j.p, j.n)[:start])
 	copy(dst[start:len(out)], out[start:])
+	j.free()
+	if rc != C.GPUDIFF_OK {
+		j.e = nil
+	}
 	j.p, j.n, j.buf = np, nn, dst[:len(out)]
+}
+
+// span closes the object at [start, len(buf)) in the zero-copy layout: zeros up to its staged span
+func (j *jsonBuf) span(start int) {
+	if j.e == nil {
+		return
+	}
+	n := len(j.buf) - start
+	pad := ((n+32+15)&^15) - n
+	out := j.buf
+	for k := 0; k < pad; k++ {
+		out = append(out, 0)
+	}
+	j.commit(out, len(j.buf))
+}
+
+// tail: the 32 bytes the upload reads past the last object's span
+func (j *jsonBuf) tail() {
+	if j.e != nil {
+		out := append(j.buf, make([]byte, 32)...)
+		j.commit(out, len(j.buf))
+	}
 }
 
 // add renders obj (jsonOf's rules) at the end of the buffer: its offset and length, ok = false
@@ -422,13 +497,17 @@ func (j *jsonBuf) add(obj interface{}) (off, n int, ok bool) {
 	if !ok { // j.buf is unchanged: the partial object (in C memory or a Go copy) is dropped
 		return 0, 0, false
 	}
-	return start, len(out) - start, j.commit(out, start)
+	j.commit(out, start)
+	n := len(j.buf) - start
+	j.span(start)
+	return start, n, true
 }
 
 // raw appends literal bytes (the "{}" stand-in of a non-transferable object)
 func (j *jsonBuf) raw(b []byte) (off, n int) {
 	start := len(j.buf)
 	j.commit(append(j.buf, b...), start)
+	j.span(start)
 	return start, len(b)
 }
 
@@ -449,7 +528,15 @@ func (j *jsonBuf) at(off, n int) (*C.uint8_t, C.size_t) {
 	return (*C.uint8_t)(unsafe.Pointer(uintptr(j.p) + uintptr(off))), C.size_t(n)
 }
 
-func (j *jsonBuf) free() { C.free(j.p) }
+func (j *jsonBuf) free() {
+	if j.e != nil {
+		j.e.mu.Lock()
+		C.gpudiff_host_free(j.e.ctx, j.p)
+		j.e.mu.Unlock()
+	} else {
+		C.free(j.p)
+	}
+}
 
 // flight is one submitted batch: its events, which pair each event became (-1: enqueued without asking
 // the engine, e.g. a non-transferable object), the C memory the engine reads until gpudiff_wait, the ticket.
@@ -475,7 +562,7 @@ func (b *Batcher) submitFlight(evs []event) *flight {
 	f := &flight{evs: evs, pairOf: make([]int, n), ok: make([]bool, n), n: n}
 	pairs := (*[1 << 28]C.gpudiff_json_pair)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_json_pair{}))))[:n:n]
 	f.cmem = unsafe.Pointer(&pairs[0])
-	f.jb = newJSONBuf(b.bytesHint(n))
+	f.jb = b.getJSONBuf(b.bytesHint(n))
 	jb := f.jb
 	offs := make([]int, 4*n) // old off, len, new off, len: pointers only once the buffer stops moving
 	for i, ev := range evs {
@@ -491,11 +578,12 @@ func (b *Batcher) submitFlight(evs []event) *flight {
 		if !f.ok[i] {
 			jb.buf = jb.buf[:mark]
 			oa, la = jb.raw([]byte("{}"))
-			oc, lc = oa, la
+			oc, lc = jb.raw([]byte("{}")) // its own copy: the zero-copy layout wants pair order
 		}
 		offs[4*i], offs[4*i+1], offs[4*i+2], offs[4*i+3] = oa, la, oc, lc
 	}
 	b.noteBytes(len(jb.buf), n)
+	jb.tail()
 	for i := range evs {
 		pa, la := jb.at(offs[4*i], offs[4*i+1])
 		pc, lc := jb.at(offs[4*i+2], offs[4*i+3])
@@ -533,7 +621,7 @@ func (b *Batcher) finishFlight(f *flight) {
 		}
 	}
 	if f.jb != nil {
-		f.jb.free()
+		b.putJSONBuf(f.jb)
 	}
 	if f.cmem != nil {
 		C.free(f.cmem)
@@ -604,7 +692,7 @@ func (b *Batcher) submitStored(evs []event) *flight {
 	}
 	ce := (*[1 << 27]C.gpudiff_event)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.gpudiff_event{}))))[:n:n]
 	f.cmem = unsafe.Pointer(&ce[0])
-	f.jb = newJSONBuf(b.bytesHint(n))
+	f.jb = newJSONBuf(nil, b.bytesHint(n)) // the store path stages (its events upload only new objects)
 	jb := f.jb
 	offs := make([]int, 4*n) // new off, len, old off, len (len 0: absent)
 	for k, i := range good {

@@ -176,8 +176,17 @@ class JsonBuf:
     allocation); objects are addressed by (offset, length), pointers are taken only after the last
     add (the buffer may move while it grows)."""
 
-    def __init__(self):
+    def __init__(self, pinned: bool = False):
+        """pinned: the engine-pinned buffer of a device-encode engine (gpudiff_host_alloc) in the zero-copy
+        layout -- each object followed by zeros up to its staged span, len + 32 rounded up to 16 (span),
+        and 32 more bytes after the last (tail)"""
         self.buf = bytearray()
+        self.pinned = pinned
+
+    def _span(self, start: int):
+        if self.pinned:
+            n = len(self.buf) - start
+            self.buf += bytes(((n + 32 + 15) & ~15) - n)
 
     def add(self, tree) -> Optional[Tuple[int, int]]:
         if tree is None:  # not an *unstructured.Unstructured: nothing added
@@ -187,12 +196,18 @@ class JsonBuf:
             return None
         off = len(self.buf)
         self.buf += j
+        self._span(off)
         return off, len(j)
 
     def raw(self, b: bytes) -> Tuple[int, int]:
         off = len(self.buf)
         self.buf += b
+        self._span(off)
         return off, len(b)
+
+    def tail(self):
+        if self.pinned:
+            self.buf += bytes(32)
 
     def mark(self) -> int:
         return len(self.buf)
@@ -222,9 +237,11 @@ class Batcher:
         self.flushes: List[int] = []
         self.buffers: List[bytes] = []
         self.inflight = None
+        self.pinned = False  # a device-encode engine: flush buffers in the zero-copy layout (gpudiff.go jsonBuf.e)
+        self.layouts: List[list] = []
 
     def _stage(self, evs):
-        jb = JsonBuf()
+        jb = JsonBuf(self.pinned)
         bad, offs = [], []
         for (_t, a, b, _which, _name) in evs:
             m = jb.mark()
@@ -232,13 +249,15 @@ class Batcher:
             ob = jb.add(informer_object(b)) if oa is not None else None
             if oa is None or ob is None:
                 jb.truncate(m)
-                oa = ob = jb.raw(b"{}")
+                oa, ob = jb.raw(b"{}"), jb.raw(b"{}")  # two copies: the zero-copy layout wants pair order
                 bad.append(True)
             else:
                 bad.append(False)
             offs.append((oa, ob))
+        jb.tail()
         buf = bytes(jb.buf)
         self.buffers.append(buf)
+        self.layouts.append(offs)
         return bad, [(buf[oa[0]:oa[0] + oa[1]], buf[ob[0]:ob[0] + ob[1]]) for oa, ob in offs]
 
     def _enqueue(self, evs, flags, bad):

@@ -248,3 +248,22 @@ def test_pipelined_batcher_same_queue_two_in_flight():
     for k, (kind, t) in enumerate(eng.calls[:-1]):
         if kind == "wait":
             assert eng.calls[k - 1] == ("submit", t + 1)
+
+
+def test_pinned_flush_buffers_meet_the_zero_copy_layout():
+    """On a device-encode engine the Go batcher renders each flush into engine-pinned memory in the layout
+    gpudiff_submit uploads without a staging copy (gpudiff.h gpudiff_host_alloc): pair order, 16-B aligned
+    objects, zeros up to each staged span, 32 bytes after the last -- non-transferable pairs included (two
+    "{}" copies).  The queue is the unpadded batcher's."""
+    evs = _event_stream(120, seed=6)
+    plain = gs.Batcher(_oracle_decide, max_batch=40, window=5.0)
+    pinned = gs.Batcher(_oracle_decide, max_batch=40, window=5.0)
+    pinned.pinned = True
+    assert pinned.run(evs) == plain.run(evs)
+    for buf, offs in zip(pinned.buffers, pinned.layouts):
+        docs = [d for pair in offs for d in pair]
+        for k, (off, n) in enumerate(docs):
+            span = (n + 32 + 15) & ~15
+            nxt = docs[k + 1][0] if k + 1 < len(docs) else len(buf) - 32
+            assert off % 16 == 0 and nxt >= off + span and not any(buf[off + n:off + span])
+        assert len(buf) == docs[-1][0] + ((docs[-1][1] + 47) & ~15) + 32
