@@ -397,7 +397,7 @@ void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
  * 32 more bytes inside the buffer) is uploaded straight from it: no staging copy.  The engine zeroes each
  * document's padding up to that span (those bytes are its to write).  Any other layout takes the staging copy;
  * results are identical either way (gpudiff_store_stats.zero_copy_batches counts the zero-copy ones).  The
- * buffer must stay untouched until gpudiff_wait on the ticket returns; free it before gpudiff_close. */
+ * buffer must stay untouched until gpudiff_wait on the ticket returns; gpudiff_close frees what is left. */
 int gpudiff_host_alloc(gpudiff_ctx* ctx, size_t bytes, void** out);
 int gpudiff_host_free(gpudiff_ctx* ctx, void* p);
 

@@ -207,6 +207,7 @@ void gpudiff_close(gpudiff_ctx* c) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
         if (c->pair_store) dstore_free(c, c->pair_store);
+        dstore_host_bufs_release(c);  // gpudiff_host_alloc buffers the caller did not free
         for (int i = 0; i < 2; i++) {
             if (c->ring[i]) gpudiff_dbatch_free(c, c->ring[i]);
             if (c->ring_hb[i]) gpudiff_hbatch_free(c, c->ring_hb[i]);

@@ -1109,6 +1109,17 @@ extern "C" int gpudiff_host_free(gpudiff_ctx* c, void* p) {
     return hipHostFree(p) == hipSuccess ? GPUDIFF_OK : GPUDIFF_E_DEVICE;
 }
 
+void dstore_host_bufs_release(gpudiff_ctx* c) {
+    std::lock_guard<std::mutex> lk(g_hb_mu);
+    for (auto it = g_hb.begin(); it != g_hb.end();)
+        if (it->c == c) {
+            (void)hipHostFree(it->p);
+            it = g_hb.erase(it);
+        } else {
+            ++it;
+        }
+}
+
 int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot) {
     HIPCHK(launch_forget(c->stream, s->slots, slot, s->ctr));
     s->seen[slot] = 0;

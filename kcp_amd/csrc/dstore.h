@@ -14,6 +14,7 @@ int dstore_submit_pairs(gpudiff_ctx* c, const gpudiff_json_pair* pairs, size_t n
 int dstore_stats(const DStore* s, gpudiff_store_stats* out);
 void dstore_timing_reset(DStore* s);  // gpudiff_timing_reset: the submit path's phase sums too
 void dstore_free(gpudiff_ctx* c, DStore* s);
+void dstore_host_bufs_release(gpudiff_ctx* c);  // gpudiff_close: the context's remaining gpudiff_host_alloc buffers
 
 // The staged JSON of a waited pair-mode batch (gpudiff_submit with GPUDIFF_OPT_DEVICE_ENCODE): pair i's
 // old object is document 2i, its new one 2i + 1; hdocs[] holds their offsets into djson (HBM) and hjson
