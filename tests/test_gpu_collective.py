@@ -122,6 +122,39 @@ def test_dirty_gather_over_rccl_world1():
             G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(), k), 0, 1, dist, dev)
         assert np.array_equal(s2.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
         assert np.array_equal(t2.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        # two passes in flight (shard.PipelinedGather, the bench's default): a second context on its own stream
+        # diffs a view of the batch on alternate steps, each pass's compaction writes its own bound send buffer,
+        # its collective runs on its stream; a capacity below the count is found one step late and both
+        # passes' steps are re-gathered from their still-intact lists
+        stream2 = torch.cuda.Stream(device=dev)
+        eng2 = G.Engine(device=0, stream=stream2.cuda_stream)
+        db2 = db.view(eng2)
+        engs, dbs = [eng, eng2], [db, db2]
+        binds = [lambda send, cs, ct, d=d: d.bind_gather(send.data_ptr(), cs, ct) for d in dbs]
+
+        def fill_counts2(p, t):
+            dbs[p].export(G.EXPORT_COUNTS, t.data_ptr(), 8, 8)
+
+        def fill_ids2(p, col, buf):
+            dbs[p].export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
+                          buf.numel())
+        for caps in ((cap_s, cap_t), (max(1, cap_s // 2), max(1, cap_t // 3))):
+            g = shard.PipelinedGather(1, caps[0], caps[1], dev, dist, [stream, stream2], binds)
+            for s in range(6):
+                engs[s % 2].diff(dbs[s % 2])
+                g.step(fill_counts2, fill_ids2)
+            g.finish()
+            torch.cuda.synchronize()
+            ok, cc = g.check()
+            assert ok and g.n_regrows == (1 if caps[0] < cap_s else 0)
+            assert [int(x) for x in cc[0, :2]] == [want.spec_dirty_ids.size, want.status_dirty_ids.size]
+            sa, ta = g.result()
+            assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want.spec_dirty_ids)
+            assert np.array_equal(ta.cpu().numpy().astype(np.uint32), want.status_dirty_ids)
+        for d in dbs:
+            d.bind_gather(0, 0, 0)
+        db2.free()  # the view before its base
+        eng2.close()
         db.free()
         hb.free()
         eng.close()
