@@ -123,6 +123,11 @@ struct DStore {
     hipStream_t cs = nullptr;  // H2D of the next batch overlaps K0 of the current one
     hipStream_t cs2 = nullptr; // GPUDIFF_OPT_H2D_TWO_STREAMS: odd JSON chunks upload here (a second DMA queue)
     hipEvent_t cs2_done = nullptr;
+    // K0 of odd chunks runs on a second stream (its own half of the scratch), so one chunk's launch tail
+    // overlaps the next chunk's start instead of idling the CUs between back-to-back launches on one stream
+    // (GPUDIFF_K0_ONE_STREAM=1, read once per store: all on the kernel stream, A/B tuning only)
+    hipStream_t ks = nullptr;
+    hipEvent_t ks_ev = nullptr;
     uint64_t up_chunk_bytes = kUpChunkBytes;
     uint32_t up_max_chunks = kMaxUpChunks;
     uint64_t* sizes = nullptr;
@@ -620,6 +625,10 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
             return fail(GPUDIFF_E_DEVICE);
     }
     if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+    if (!getenv("GPUDIFF_K0_ONE_STREAM") &&
+        (hipStreamCreateWithFlags(&s->ks, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&s->ks_ev, hipEventDisableTiming) != hipSuccess))
+        return fail(GPUDIFF_E_DEVICE);
     if (const char* v = getenv("GPUDIFF_H2D_CHUNK_MIB"))
         s->up_chunk_bytes = std::max<uint64_t>(1, strtoull(v, nullptr, 10)) << 20;
     if (const char* v = getenv("GPUDIFF_H2D_MAX_CHUNKS"))
@@ -839,6 +848,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     // K0 scratch: per-document areas within launches of at most kScratchCap, never across a chunk
     std::vector<std::pair<uint32_t, uint32_t>> launches;
     std::vector<uint32_t> chunk_of_launch;
+    uint64_t max_sb = 0;  // the largest launch's scratch: one such area per K0 stream
     for (uint32_t q = 0; q < C; q++) {
         uint64_t sb = 0;
         uint32_t first = cdoc[q];
@@ -852,13 +862,15 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
             }
             docs[k].scratch_off = sb;
             sb += need;
-            if ((rc = grow_dev(&s->scratch, &s->scratch_cap, sb))) return rc;
+            max_sb = std::max(max_sb, sb);
         }
         if (cdoc[q + 1] > first) {
             launches.emplace_back(first, cdoc[q + 1]);
             chunk_of_launch.push_back(q);
         }
     }
+    const uint64_t scratch_half = (max_sb + 255u) & ~255ull;
+    if ((rc = grow_dev(&s->scratch, &s->scratch_cap, s->ks ? 2 * scratch_half : scratch_half))) return rc;
     // 2. capacity (compaction is stream-ordered after every earlier batch)
     if ((rc = ensure_space(s, bound, floor))) return rc;
     // 3. upload + kernels
@@ -896,6 +908,10 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     std::atomic<int> up_err{0};
     uint32_t uploaded = 0;
     if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
+    if (s->ks) {  // the second K0 stream starts behind everything before this batch's K0 on the kernel stream
+        HIPCHK(hipEventRecord(s->ks_ev, st));
+        HIPCHK(hipStreamWaitEvent(s->ks, s->ks_ev, 0));
+    }
     const TokDoc* ddocs = (const TokDoc*)R.dmeta;
     const DocLink* dlinks = (const DocLink*)(R.dmeta + max_docs * sizeof(TokDoc));
     const uint32_t* dheads = (const uint32_t*)(R.dmeta + max_docs * (sizeof(TokDoc) + sizeof(DocLink)));
@@ -907,15 +923,18 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
         if (!zsrc && q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
         hipStream_t qs = (q & 1u) ? cs2 : cs;
+        const bool odd = s->ks && (q & 1u);
+        hipStream_t kq = odd ? s->ks : st;  // this chunk's K0 stream, and its half of the scratch
+        uint8_t* scr = s->scratch + (odd ? scratch_half : 0);
         if (hipMemcpyAsync(R.djson + b0, hsrc + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
-            hipEventRecord(R.chunk_ev[q], qs) != hipSuccess || hipStreamWaitEvent(st, R.chunk_ev[q], 0) != hipSuccess ||
+            hipEventRecord(R.chunk_ev[q], qs) != hipSuccess || hipStreamWaitEvent(kq, R.chunk_ev[q], 0) != hipSuccess ||
             (q == 0 && timing && hipEventRecord(R.t_ev[2], st) != hipSuccess)) {
             up_err.store(1);
             return;
         }
         for (; li < launches.size() && chunk_of_launch[li] == q; li++) {
             const auto& L = launches[li];
-            if (launch_encode_docs(st, ddocs + L.first, L.second - L.first, R.djson, s->scratch, space, s->space_bytes,
+            if (launch_encode_docs(kq, ddocs + L.first, L.second - L.first, R.djson, scr, space, s->space_bytes,
                                    s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
                                    (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u) != hipSuccess) {
                 up_err.store(1);
@@ -959,6 +978,10 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     HIPCHK(hipEventRecord(R.staged, cs));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[1], cs));
     if (li != launches.size()) return GPUDIFF_E_STATE;  // every launch belongs to an uploaded chunk
+    if (s->ks) {  // K0c waits for the odd chunks' K0 too
+        HIPCHK(hipEventRecord(s->ks_ev, s->ks));
+        HIPCHK(hipStreamWaitEvent(st, s->ks_ev, 0));
+    }
     HIPCHK(hipStreamWaitEvent(st, R.staged, 0));  // every chunk (and the tables) landed
     if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
     HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
@@ -1181,6 +1204,11 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         (void)hipStreamDestroy(s->cs2);
     }
     if (s->cs2_done) (void)hipEventDestroy(s->cs2_done);
+    if (s->ks) {
+        (void)hipStreamSynchronize(s->ks);
+        (void)hipStreamDestroy(s->ks);
+    }
+    if (s->ks_ev) (void)hipEventDestroy(s->ks_ev);
     if (s->cs) {
         (void)hipStreamSynchronize(s->cs);
         (void)hipStreamDestroy(s->cs);

@@ -40,9 +40,10 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
     assert np.array_equal(want.pair_flags & 7, f)
     assert np.array_equal(want.path_offsets.astype(np.int64), o.astype(np.int64))
     assert np.array_equal(want.path_hashes, h) and np.array_equal(want.path_kinds, k)
-    # the default chunks, two copy streams, one chunk, and the most chunks (1 MiB minimum: capped at 16)
+    # the default chunks, two copy streams, one chunk, the most chunks (1 MiB minimum: capped at 16), and every
+    # chunk's K0 on the kernel stream (the default alternates two K0 streams)
     variants = ((0, {}), (G.OPT_H2D_TWO_STREAMS, {}), (0, {"GPUDIFF_H2D_MAX_CHUNKS": "1"}),
-                (G.OPT_H2D_TWO_STREAMS, {"GPUDIFF_H2D_CHUNK_MIB": "1"}))
+                (G.OPT_H2D_TWO_STREAMS, {"GPUDIFF_H2D_CHUNK_MIB": "1"}), (0, {"GPUDIFF_K0_ONE_STREAM": "1"}))
     for flags, env in variants + ((0, {"zero_copy": True}),):
         zero_copy = env.pop("zero_copy", False)
         os.environ.update(env)
