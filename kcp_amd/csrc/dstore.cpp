@@ -73,6 +73,8 @@ struct Ring {
     hipEvent_t staged = nullptr;  // its H2D copies finished (pinned buffers reusable)
     hipEvent_t k0_done = nullptr;  // its K0..K0x finished reading the device JSON / document table
     bool k0_recorded = false;
+    hipEvent_t pass_done = nullptr;  // pair mode: its diff pass finished reading its space (K0 may refill it)
+    bool pass_recorded = false;
     hipEvent_t t_ev[5] = {};      // GPUDIFF_OPT_TIMING: H2D begin/end (copy stream), K0 begin/end, K0c+K0x end
     hipEvent_t chunk_ev[kMaxUpChunks] = {};  // each JSON chunk's H2D done: its K0 launches may start
     std::vector<gpudiff_event> events;
@@ -128,6 +130,11 @@ struct DStore {
     // (GPUDIFF_K0_ONE_STREAM=1, read once per store: all on the kernel stream, A/B tuning only)
     hipStream_t ks = nullptr;
     hipEvent_t ks_ev = nullptr;
+    // pair mode with two K0 streams: the whole K0 stage (slot reset, K0 of even chunks, K0c, K0x) runs on ks0 and
+    // waits only for what it reuses -- the previous batch's K0x (the shared slot table) and this ring slot's
+    // previous diff pass (its space) -- so a batch's K0 overlaps the previous batch's diff pass on the kernel stream
+    hipStream_t ks0 = nullptr;
+    int last_ring = -1;  // the ring slot of the previous submit
     uint64_t up_chunk_bytes = kUpChunkBytes;
     uint32_t up_max_chunks = kMaxUpChunks;
     uint64_t* sizes = nullptr;
@@ -627,8 +634,11 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
     if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
     if (!getenv("GPUDIFF_K0_ONE_STREAM") &&
         (hipStreamCreateWithFlags(&s->ks, hipStreamNonBlocking) != hipSuccess ||
-         hipEventCreateWithFlags(&s->ks_ev, hipEventDisableTiming) != hipSuccess))
+         hipEventCreateWithFlags(&s->ks_ev, hipEventDisableTiming) != hipSuccess ||
+         hipStreamCreateWithFlags(&s->ks0, hipStreamNonBlocking) != hipSuccess))
         return fail(GPUDIFF_E_DEVICE);
+    for (Ring& R : s->ring)
+        if (hipEventCreateWithFlags(&R.pass_done, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
     if (const char* v = getenv("GPUDIFF_H2D_CHUNK_MIB"))
         s->up_chunk_bytes = std::max<uint64_t>(1, strtoull(v, nullptr, 10)) << 20;
     if (const char* v = getenv("GPUDIFF_H2D_MAX_CHUNKS"))
@@ -661,11 +671,13 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     }
     int rc;
     if (R.staged) HIPCHK(hipEventSynchronize(R.staged));
+    // pair mode with the K0 stage on its own streams (ks0 / ks): decoupled from the kernel stream
+    const bool dec = s->pair_mode && s->ks0;
     if (s->pair_mode) {  // this ring slot's space, emptied behind its previous batch (stream order)
         s->cur = s->ring_next;
         s->used_dev = s->used_base + s->ring_next;
         s->used_ub = 0;
-        HIPCHK(hipMemsetAsync(s->used_dev, 0, 8, c->stream));
+        if (!dec) HIPCHK(hipMemsetAsync(s->used_dev, 0, 8, c->stream));  // (dec: on ks0, below)
     }
     auto lap = [&, t = std::chrono::steady_clock::now()](int k) mutable {
         if (!timing) return;
@@ -879,6 +891,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         return rc;
     if ((rc = grow_dev(&R.dcoll, &R.coll_cap, nd + 1)) || (rc = grow_dev(&R.ddef, &R.def_cap, n + 1))) return rc;
     hipStream_t st = c->stream, cs = s->cs;
+    hipStream_t k0s = dec ? s->ks0 : st;  // the K0 stage's stream (even chunks, K0c, K0x)
     if (timing && !R.t_ev[0])
         for (auto& e : R.t_ev) HIPCHK(hipEventCreate(&e));
     if (!R.chunk_ev[0])
@@ -907,9 +920,16 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     for (auto& x : chunk_done) x.store(0, std::memory_order_relaxed);
     std::atomic<int> up_err{0};
     uint32_t uploaded = 0;
-    if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, st));  // every pair starts empty
-    if (s->ks) {  // the second K0 stream starts behind everything before this batch's K0 on the kernel stream
-        HIPCHK(hipEventRecord(s->ks_ev, st));
+    if (dec) {  // what this batch's K0 stage reuses: the slot table (the previous batch's K0x read it) and this
+                // ring slot's space, douts and rows (its previous batch's diff pass read them)
+        if (s->last_ring >= 0 && s->ring[s->last_ring].k0_recorded)
+            HIPCHK(hipStreamWaitEvent(k0s, s->ring[s->last_ring].k0_done, 0));
+        if (R.pass_recorded) HIPCHK(hipStreamWaitEvent(k0s, R.pass_done, 0));
+        HIPCHK(hipMemsetAsync(s->used_dev, 0, 8, k0s));
+    }
+    if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, k0s));  // every pair starts empty
+    if (s->ks) {  // the second K0 stream starts behind everything before this batch's K0 on the K0 stage's stream
+        HIPCHK(hipEventRecord(s->ks_ev, k0s));
         HIPCHK(hipStreamWaitEvent(s->ks, s->ks_ev, 0));
     }
     const TokDoc* ddocs = (const TokDoc*)R.dmeta;
@@ -924,11 +944,11 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         if (!zsrc && q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
         hipStream_t qs = (q & 1u) ? cs2 : cs;
         const bool odd = s->ks && (q & 1u);
-        hipStream_t kq = odd ? s->ks : st;  // this chunk's K0 stream, and its half of the scratch
+        hipStream_t kq = odd ? s->ks : k0s;  // this chunk's K0 stream, and its half of the scratch
         uint8_t* scr = s->scratch + (odd ? scratch_half : 0);
         if (hipMemcpyAsync(R.djson + b0, hsrc + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
             hipEventRecord(R.chunk_ev[q], qs) != hipSuccess || hipStreamWaitEvent(kq, R.chunk_ev[q], 0) != hipSuccess ||
-            (q == 0 && timing && hipEventRecord(R.t_ev[2], st) != hipSuccess)) {
+            (q == 0 && timing && hipEventRecord(R.t_ev[2], k0s) != hipSuccess)) {
             up_err.store(1);
             return;
         }
@@ -980,18 +1000,19 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     if (li != launches.size()) return GPUDIFF_E_STATE;  // every launch belongs to an uploaded chunk
     if (s->ks) {  // K0c waits for the odd chunks' K0 too
         HIPCHK(hipEventRecord(s->ks_ev, s->ks));
-        HIPCHK(hipStreamWaitEvent(st, s->ks_ev, 0));
+        HIPCHK(hipStreamWaitEvent(k0s, s->ks_ev, 0));
     }
-    HIPCHK(hipStreamWaitEvent(st, R.staged, 0));  // every chunk (and the tables) landed
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[3], st));
-    HIPCHK(launch_collide(st, dlinks, R.douts, s->slots, nd, space, R.dcoll));
-    HIPCHK(hipMemsetAsync(R.dcnt, 0, 4, st));
+    HIPCHK(hipStreamWaitEvent(k0s, R.staged, 0));  // every chunk (and the tables) landed
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[3], k0s));
+    HIPCHK(launch_collide(k0s, dlinks, R.douts, s->slots, nd, space, R.dcoll));
+    HIPCHK(hipMemsetAsync(R.dcnt, 0, 4, k0s));
     gpudiff_dbatch* d = R.d;
-    HIPCHK(launch_link(st, dheads, nh, dlinks, R.douts, R.dcoll, s->slots, d->rows, d->pair_ids, R.ddef, batch,
+    HIPCHK(launch_link(k0s, dheads, nh, dlinks, R.douts, R.dcoll, s->slots, d->rows, d->pair_ids, R.ddef, batch,
                        R.dcnt, s->ctr));
-    HIPCHK(hipEventRecord(R.k0_done, st));
+    HIPCHK(hipEventRecord(R.k0_done, k0s));
     R.k0_recorded = true;
-    if (timing) HIPCHK(hipEventRecord(R.t_ev[4], st));
+    if (timing) HIPCHK(hipEventRecord(R.t_ev[4], k0s));
+    if (dec) HIPCHK(hipStreamWaitEvent(st, R.k0_done, 0));  // the diff pass reads the rows K0x wrote
     s->used_ub += bound;
     // 4. the diff pass over the batch's rows
     d->pool = space;
@@ -1005,6 +1026,11 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         s->broken = true;
         return rc;
     }
+    if (dec) {  // this ring slot's next K0 stage may refill its space once this pass has read it
+        HIPCHK(hipEventRecord(R.pass_done, st));
+        R.pass_recorded = true;
+    }
+    s->last_ring = (int)(&R - s->ring);
     R.events.assign(ev, ev + n);
     R.waited = false;
     R.batch = batch;
@@ -1204,10 +1230,13 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         (void)hipStreamDestroy(s->cs2);
     }
     if (s->cs2_done) (void)hipEventDestroy(s->cs2_done);
-    if (s->ks) {
-        (void)hipStreamSynchronize(s->ks);
-        (void)hipStreamDestroy(s->ks);
-    }
+    for (hipStream_t* k : {&s->ks, &s->ks0})
+        if (*k) {
+            (void)hipStreamSynchronize(*k);
+            (void)hipStreamDestroy(*k);
+        }
+    for (Ring& R : s->ring)
+        if (R.pass_done) (void)hipEventDestroy(R.pass_done);
     if (s->ks_ev) (void)hipEventDestroy(s->ks_ev);
     if (s->cs) {
         (void)hipStreamSynchronize(s->cs);
