@@ -632,10 +632,11 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
             return fail(GPUDIFF_E_DEVICE);
     }
     if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+    // (GPUDIFF_K0_COUPLED=1, A/B tuning only: the pair-mode K0 stage stays on the kernel stream)
     if (!getenv("GPUDIFF_K0_ONE_STREAM") &&
         (hipStreamCreateWithFlags(&s->ks, hipStreamNonBlocking) != hipSuccess ||
          hipEventCreateWithFlags(&s->ks_ev, hipEventDisableTiming) != hipSuccess ||
-         hipStreamCreateWithFlags(&s->ks0, hipStreamNonBlocking) != hipSuccess))
+         (!getenv("GPUDIFF_K0_COUPLED") && hipStreamCreateWithFlags(&s->ks0, hipStreamNonBlocking) != hipSuccess)))
         return fail(GPUDIFF_E_DEVICE);
     for (Ring& R : s->ring)
         if (hipEventCreateWithFlags(&R.pass_done, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
