@@ -1652,7 +1652,7 @@ static K2Fn k2_kernel(uint32_t variant) {
         case 7: return k_compare_flat<4, 1, true>;  // round 3's default: 4 chunks a side in flight, 4 waves/SIMD
         case 8: return k_compare_flat<4, 1>;
         case 9: return k_compare_flat<2, 1>;
-        case 11: return k_compare_flat<6, 1, true>;  // x6 (4 waves/SIMD if it fits 128 VGPRs)
+        case 11: return k_compare_flat<12, 3, true>;  // x12 held to 3 waves/SIMD
         case 12: return k_compare_flat<16, 1, true>;  // x16
         case 13: return k_compare_flat<4, 1, true, false, true>;  // + next rows prefetched into LDS (RPF)
         case 10: return k_compare_flat<8, 1, true>;  // 8 chunks a side in flight, 3 waves/SIMD
