@@ -1108,6 +1108,9 @@ __host__ __device__ inline uint32_t k2_lpt_round(uint32_t n_full, uint32_t nwave
     const uint32_t r = want < n_full / 2u ? want : n_full / 2u;
     return r < 2u ? 0u : r;
 }
+__host__ __device__ inline uint32_t k2_item_round(uint32_t n_main, uint32_t nwaves) {
+    return n_main >= 3u * nwaves ? nwaves : 0u;  // one item per resident wave, when the bulk keeps two rounds
+}
 __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t q) {
     return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * q);
 }
@@ -1225,6 +1228,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     const uint32_t lpt_rounds = (sub_arg >> 20) & 3u;  // launch_compare: 0 when the round is off
     const uint32_t lpt_r = (DYN && !RPF && tail_perm && tail_c == 0u && lpt_rounds) ? k2_lpt_round(n_full, nwaves, lpt_rounds) : 0u;
     const uint32_t n_main = n_full - lpt_r;
+    // ... and the round before it in whole items, also largest first (sub_arg bit 22): its biggest items then start
+    // a round earlier instead of running past the pair round's end
+    const uint32_t r2 = (lpt_r && ((sub_arg >> 22) & 1u)) ? k2_item_round(n_main, nwaves) : 0u;
+    const uint32_t n_main2 = n_main - r2;
+    const uint32_t lpt_pairs = lpt_r << (6u - sub_shift);
     const uint32_t lpt_p0 = ((c_begin + (n_main >> sub_shift)) << 6) + (n_main & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
     const uint32_t nitems = lpt_r ? n_main + (lpt_r << (6u - sub_shift)) : n_full + (tail_c << tail_ish);
     // Two ticket counters per segment: main items are taken with a prefetch (the next main ticket as an
@@ -1255,7 +1263,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
         // the item this ticket stands for: in the largest-first round, one pair (the permuted order)
         const bool lpt = lpt_r && it >= n_main;
-        const uint32_t im = lpt ? 0u : it;
+        const uint32_t im = lpt ? 0u : (r2 && it >= n_main2) ? n_main2 + tail_perm[lpt_pairs + (it - n_main2)] : it;
         const bool tail = !lpt && im >= n_full;
         // the next main ticket: fetched while this item streams (with RPF only after this item's rows are
         // read from LDS -- the LDS read waits on vmcnt, which would otherwise wait for the atomic's return)
@@ -1686,9 +1694,11 @@ static uint32_t k2_variant_of(const DiffBuffers& b) {
 }
 
 constexpr uint32_t kK2LptMax = 16384;  // largest-first rounds: at most this many pairs (one block sorts them in LDS)
-// largest-first rounds for deep pairs: one (GPUDIFF_OPT_K2_TAIL8 there: two -- config4 K2 1.093 ms vs 1.060 with
-// one and 1.070 in index order, profiles/r04w: twice the single-pair items scatter the stream further)
-static uint32_t k2_lpt_rounds(const DiffBuffers& b) { return b.k2_tail8 ? 2u : 1u; }
+// largest-first rounds for deep pairs: one round of single pairs (two scatter the stream further: config4 K2
+// 1.093 ms vs 1.060 with one and 1.070 in index order, profiles/r04w), after one round of whole items sorted the
+// same way (GPUDIFF_OPT_K2_TAIL8 there: without that item round, the A/B)
+static uint32_t k2_lpt_rounds(const DiffBuffers&) { return 1u; }
+static bool k2_item_round_on(const DiffBuffers& b) { return !b.k2_tail8; }
 constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
 constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
@@ -1763,19 +1773,11 @@ __device__ __forceinline__ uint64_t pair_stream_bytes(const gpudiff_pair_row& r)
 // by their compared bytes, descending (ties by index), into perm (offsets from the round's first pair).
 // Cached per batch by the host (launch_compare): the order depends only on the rows and the launch shape, and
 // any permutation is correct -- a stale one only orders the round less well.
-__global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __restrict__ rows, uint32_t n,
-                                                     uint32_t p_first, uint32_t r, uint32_t* __restrict__ perm) {
-    __shared__ uint32_t key[kK2LptMax];  // 64 KiB
+// one block: sorts key[0, r) ascending (bitonic, padded to a power of two with ~0)
+__device__ void block_sort_u32(uint32_t* key, uint32_t r) {
     uint32_t m2 = 1;
     while (m2 < r) m2 <<= 1;
-    for (uint32_t t = threadIdx.x; t < m2; t += blockDim.x) {
-        const uint32_t p = p_first + t;
-        const uint64_t bytes = t < r && p < n ? pair_stream_bytes(rows[p]) : 0u;
-        // descending bytes (in 16-B units, saturating at 1 MiB), ascending index: sort ascending on
-        // (~bytes16, t); padding sorts last
-        const uint32_t b16 = (uint32_t)min(bytes >> 4, (uint64_t)0xFFFFu);
-        key[t] = t < r ? ((0xFFFFu - b16) << 16) | t : ~0u;
-    }
+    for (uint32_t t = r + threadIdx.x; t < m2; t += blockDim.x) key[t] = ~0u;
     __syncthreads();
     for (uint32_t k = 2; k <= m2; k <<= 1)
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -1791,7 +1793,37 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
             }
             __syncthreads();
         }
+}
+
+__global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __restrict__ rows, uint32_t n,
+                                                     uint32_t p_first, uint32_t r, uint32_t c_begin, uint32_t n_main2,
+                                                     uint32_t r2, uint32_t sub_shift, uint32_t* __restrict__ perm) {
+    __shared__ uint32_t key[kK2LptMax];  // 64 KiB
+    // the last round's pairs: descending bytes (in 16-B units, saturating at 1 MiB), ascending index -- sort
+    // ascending on (~bytes16, t); padding sorts last
+    for (uint32_t t = threadIdx.x; t < r; t += blockDim.x) {
+        const uint32_t p = p_first + t;
+        const uint64_t bytes = p < n ? pair_stream_bytes(rows[p]) : 0u;
+        const uint32_t b16 = (uint32_t)min(bytes >> 4, (uint64_t)0xFFFFu);
+        key[t] = ((0xFFFFu - b16) << 16) | t;
+    }
+    block_sort_u32(key, r);
     for (uint32_t t = threadIdx.x; t < r; t += blockDim.x) perm[t] = key[t] & 0xFFFFu;
+    __syncthreads();
+    // the round before, in whole items of 64 >> sub_shift pairs (32-B units, saturating at 2 MiB)
+    const uint32_t per = 64u >> sub_shift;
+    for (uint32_t t = threadIdx.x; t < r2; t += blockDim.x) {
+        const uint32_t m = n_main2 + t;
+        const uint32_t p0 = ((c_begin + (m >> sub_shift)) << 6) + (m & ((1u << sub_shift) - 1u)) * per;
+        uint64_t bytes = 0;
+        for (uint32_t p = p0; p < min(p0 + per, n); p++) bytes += pair_stream_bytes(rows[p]);
+        const uint32_t b32 = (uint32_t)min(bytes >> 5, (uint64_t)0xFFFFu);
+        key[t] = ((0xFFFFu - b32) << 16) | t;
+    }
+    if (r2) {
+        block_sort_u32(key, r2);
+        for (uint32_t t = threadIdx.x; t < r2; t += blockDim.x) perm[r + t] = key[t] & 0xFFFFu;
+    }
 }
 
 // the launch's largest-first round (0 = none): large pairs only, DYN variants without the LDS row prefetch,
@@ -1801,7 +1833,8 @@ static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uin
     if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v >= 14)) return 0;
     if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
     const uint32_t r = k2_lpt_round(nch << sub, nwaves, k2_lpt_rounds(b));
-    return (r << (6u - sub)) <= kK2LptMax ? r : 0;  // the round's pairs are sorted in one block's LDS
+    // the round's pairs and the item round before it are sorted in one block's LDS / kept in tail_perm
+    return (r << (6u - sub)) + k2_item_round((nch << sub) - r, nwaves) <= kK2LptMax ? r : 0;
 }
 
 hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
@@ -1817,10 +1850,12 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
     if (lpt) {
         const uint32_t n_main = ((c1 - c0) << sub) - lpt;
         const uint32_t p_first = ((c0 + (n_main >> sub)) << 6) + (n_main & ((1u << sub) - 1u)) * (64u >> sub);
+        const uint32_t r2 = k2_item_round_on(b) ? k2_item_round(n_main, grid.x * 4u) : 0u;
         const uint64_t key = ((uint64_t)b.n_pairs << 32) ^ ((uint64_t)lpt << 12) ^ ((uint64_t)sub << 8) ^ c0 ^
-                             ((uint64_t)(uintptr_t)b.rows << 7);
+                             ((uint64_t)(uintptr_t)b.rows << 7) ^ ((uint64_t)r2 << 40);
         if (*b.tail_perm_key != key) {
-            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, p_first, lpt << (6u - sub), b.tail_perm);
+            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, p_first, lpt << (6u - sub), c0, n_main - r2, r2, sub,
+                                            b.tail_perm);
             *b.tail_perm_key = key;
         }
         perm = b.tail_perm;
@@ -1836,7 +1871,8 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
 #define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
-                   ((b.k2_deep_mode & 3u) << 18) | (lpt ? k2_lpt_rounds(b) << 20 : 0u), perm
+                   ((b.k2_deep_mode & 3u) << 18) | (lpt ? k2_lpt_rounds(b) << 20 : 0u) | \
+                   (lpt && k2_item_round_on(b) ? 1u << 22 : 0u), perm
     k2_kernel(v)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();

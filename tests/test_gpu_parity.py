@@ -387,3 +387,31 @@ def test_deep_joins_merge_path(mode):
     e = G.Engine(device=0, flags=flags)
     assert_matches(e.diff_pairs(pairs), pairs)
     e.close()
+
+
+def test_k2_hand_out_orders_agree_on_deep_batches():
+    """A deep batch large enough for every K2 hand-out stage (config4 shape, 40k pairs: 4-pair main items, a
+    round of whole items and a round of single pairs both handed out largest first): the default, index order
+    (GPUDIFF_OPT_K2_NO_LPT) and no item round (GPUDIFF_OPT_K2_TAIL8 on deep batches) give identical flags, ID
+    lists and changed paths, and the flags equal the generator's ground truth."""
+    from kcp_amd import synth as S
+    pop = S.Population(S.make_cfg("config4", n_pairs=40000))
+    res = {}
+    for name, flags in (("default", 0), ("index", G.OPT_K2_NO_LPT), ("no_item_round", 0x80)):
+        e = G.Engine(device=0, encode_threads=16, flags=flags)
+        ch = pop.chunk(e, 0, pop.n, 16)
+        db = e.device_batch(ch.hb.info().pool_bytes + 4096, pop.n)
+        db.append(ch.hb)
+        r = e.wait(e.diff(db))
+        r2 = e.wait(e.diff(db))  # the cached order
+        assert np.array_equal(r.pair_flags, r2.pair_flags) and np.array_equal(r.path_hashes, r2.path_hashes)
+        res[name] = r
+        truth = ch.truth
+        db.free()
+        ch.hb.free()
+        e.close()
+    want = res["default"]
+    assert np.array_equal(want.pair_flags & (G.SPEC_DIRTY | G.STATUS_DIRTY), pop.expected_flags(truth))
+    for name, r in res.items():
+        for f in ("pair_flags", "spec_dirty_ids", "status_dirty_ids", "path_offsets", "path_hashes", "path_kinds"):
+            assert np.array_equal(getattr(r, f), getattr(want, f)), (name, f)
