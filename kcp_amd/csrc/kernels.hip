@@ -42,6 +42,7 @@ constexpr uint32_t kJoinSlice = 1024;  // merged keys per slice (<= 16 windows o
 constexpr uint32_t kDeepJoin = 2048;   // K2 defers a dirty pair whose join covers more keys
 // the deep-join bound of a K2 launch (sub_arg bits 18-19 = GPUDIFF_OPT_K2_DEEP_SHIFT's field: 0 the
 // default, 1 none -- every join the wave arena holds stays in K2 --, 2 and 3: 2x and 4x the default)
+constexpr uint32_t kTailJoinMax = 256;  // K2's largest-first rounds: joins over this many keys go to K4
 __device__ __forceinline__ uint32_t deep_join_max(uint32_t sub_arg) {
     const uint32_t m = (sub_arg >> 18) & 3u;
     return m == 1u ? ~0u : kDeepJoin << (m ? m - 1u : 0u);
@@ -1231,6 +1232,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     // ... and the round before it in whole items, also largest first (sub_arg bit 22): its biggest items then start
     // a round earlier instead of running past the pair round's end
     const uint32_t r2 = (lpt_r && ((sub_arg >> 22) & 1u)) ? k2_item_round(n_main, nwaves) : 0u;
+    const bool tail_defer = (sub_arg >> 23) & 1u;
     const uint32_t n_main2 = n_main - r2;
     const uint32_t lpt_pairs = lpt_r << (6u - sub_shift);
     const uint32_t lpt_p0 = ((c_begin + (n_main >> sub_shift)) << 6) + (n_main & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
@@ -1263,6 +1265,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
         // the item this ticket stands for: in the largest-first round, one pair (the permuted order)
         const bool lpt = lpt_r && it >= n_main;
+        // the largest-first rounds' dirty pairs join only up to kTailJoinMax keys here (bigger ones go to K4's
+        // slices, spread over the whole grid): a deep join late in the launch would run past everyone's end
+        const bool tail_round = tail_defer && lpt_r && it >= n_main2;
         const uint32_t im = lpt ? 0u : (r2 && it >= n_main2) ? n_main2 + tail_perm[lpt_pairs + (it - n_main2)] : it;
         const bool tail = !lpt && im >= n_full;
         // the next main ticket: fetched while this item streams (with RPF only after this item's rows are
@@ -1424,7 +1429,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
             uint32_t src = 0, pc = 0, nb = 0;
             bool defer = false;
-            if (used + ck <= arena_per_wave && ck <= deep_max) {
+            if (used + ck <= arena_per_wave && ck <= (tail_round ? min(deep_max, kTailJoinMax) : deep_max)) {
                 src = wbase + used;
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
@@ -1696,9 +1701,11 @@ static uint32_t k2_variant_of(const DiffBuffers& b) {
 constexpr uint32_t kK2LptMax = 16384;  // largest-first rounds: at most this many pairs (one block sorts them in LDS)
 // largest-first rounds for deep pairs: one round of single pairs (two scatter the stream further: config4 K2
 // 1.093 ms vs 1.060 with one and 1.070 in index order, profiles/r04w), after one round of whole items sorted the
-// same way (GPUDIFF_OPT_K2_TAIL8 there: without that item round, the A/B)
+// same way (-0.4%, profiles/r04zk); in both, joins over kTailJoinMax keys are deferred to K4 (GPUDIFF_OPT_K2_TAIL8
+// on deep batches: not, the A/B)
 static uint32_t k2_lpt_rounds(const DiffBuffers&) { return 1u; }
-static bool k2_item_round_on(const DiffBuffers& b) { return !b.k2_tail8; }
+static bool k2_item_round_on(const DiffBuffers&) { return true; }
+static bool k2_tail_defer_on(const DiffBuffers& b) { return !b.k2_tail8; }
 constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
 constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
@@ -1872,7 +1879,7 @@ hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint
                b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
                sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
                    ((b.k2_deep_mode & 3u) << 18) | (lpt ? k2_lpt_rounds(b) << 20 : 0u) | \
-                   (lpt && k2_item_round_on(b) ? 1u << 22 : 0u), perm
+                   (lpt && k2_item_round_on(b) ? 1u << 22 : 0u) | (lpt && k2_tail_defer_on(b) ? 1u << 23 : 0u), perm
     k2_kernel(v)<<<grid, 256, 0, s>>>(K2ARGS);
 #undef K2ARGS
     return hipGetLastError();

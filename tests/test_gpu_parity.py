@@ -392,12 +392,13 @@ def test_deep_joins_merge_path(mode):
 def test_k2_hand_out_orders_agree_on_deep_batches():
     """A deep batch large enough for every K2 hand-out stage (config4 shape, 40k pairs: 4-pair main items, a
     round of whole items and a round of single pairs both handed out largest first): the default, index order
-    (GPUDIFF_OPT_K2_NO_LPT) and no item round (GPUDIFF_OPT_K2_TAIL8 on deep batches) give identical flags, ID
-    lists and changed paths, and the flags equal the generator's ground truth."""
+    (GPUDIFF_OPT_K2_NO_LPT) and the rounds' joins kept in K2 (GPUDIFF_OPT_K2_TAIL8 on deep batches; the default
+    defers their joins over 256 keys to K4) give identical flags, ID lists and changed paths, and the flags equal
+    the generator's ground truth."""
     from kcp_amd import synth as S
     pop = S.Population(S.make_cfg("config4", n_pairs=40000))
     res = {}
-    for name, flags in (("default", 0), ("index", G.OPT_K2_NO_LPT), ("no_item_round", 0x80)):
+    for name, flags in (("default", 0), ("index", G.OPT_K2_NO_LPT), ("tail_joins_in_k2", 0x80)):
         e = G.Engine(device=0, encode_threads=16, flags=flags)
         ch = pop.chunk(e, 0, pop.n, 16)
         db = e.device_batch(ch.hb.info().pool_bytes + 4096, pop.n)

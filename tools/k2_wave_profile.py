@@ -103,6 +103,11 @@ def main():
             # the end of the pass: how many waves are still running at each point of the last 20%
             grid = np.linspace(0.8 * span, span, 11)
             rec["running_at"] = {"%.1f" % g: int(((start <= g) & (end > g)).sum()) for g in grid}
+            # the 40 waves that end last: when their last item started, and their totals
+            late = np.argsort(end)[-40:]
+            rec["late_waves"] = [dict(last_item_start_us=round(float(us(r[k, 3] - t0)), 1), end_us=round(float(end[k]), 1),
+                                      items=int(r[k, 2]), stream_us=round(float(us(r[k, 5])), 1),
+                                      join_us=round(float(us(r[k, 6])), 1)) for k in late]
         out["variant%d" % variant] = rec
         db.free()
         eng.close()
