@@ -42,7 +42,7 @@ constexpr uint32_t kJoinSlice = 1024;  // merged keys per slice (<= 16 windows o
 constexpr uint32_t kDeepJoin = 2048;   // K2 defers a dirty pair whose join covers more keys
 // the deep-join bound of a K2 launch (sub_arg bits 18-19 = GPUDIFF_OPT_K2_DEEP_SHIFT's field: 0 the
 // default, 1 none -- every join the wave arena holds stays in K2 --, 2 and 3: 2x and 4x the default)
-constexpr uint32_t kTailJoinMax = 256;  // K2's largest-first rounds: joins over this many keys go to K4
+constexpr uint32_t kTailJoinMax = 1024;  // K2's largest-first rounds: joins over this many keys go to K4's slices
 __device__ __forceinline__ uint32_t deep_join_max(uint32_t sub_arg) {
     const uint32_t m = (sub_arg >> 18) & 3u;
     return m == 1u ? ~0u : kDeepJoin << (m ? m - 1u : 0u);
