@@ -1422,31 +1422,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                      (stat_dirty && !has_st_b ? F_SENT : 0u) | (((v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu) ? F_SEED : 0u);
             mycap = (spec_dirty ? v1.x + v1.y : 0u) + (stat_dirty ? v2.x + v2.y + (has_st_b ? 0u : 1u) : 0u);
         }
-        // ---- changed paths of the dirty pairs into this wave's arena.  Status-absent-only pairs (every
-        // ConfigMap / Secret update: ~40% of config3's pairs) take one entry each, written lane-parallel here;
-        // the joins follow, one pair at a time in pair order
-        bool sent_done = false;
-        if constexpr (!RPF) {
-            const bool sent_only = (myflag & F_SENT) && !(myflag & (F_JSPEC | F_JSTAT));
-            const uint64_t sm = ballot(sent_only);
-            const uint32_t nsent = popc64(sm);
-            if (nsent && used + nsent <= arena_per_wave) {
-                if (sent_only) {
-                    const uint32_t src = wbase + used +
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-                    ah[src] = (myflag & F_SEED) ? status_sentinel_hash((v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
-                                                : sent0;
-                    ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
-                    mynoop = sentinel_noop_bits(v3.x);
-                    mysrc = src;
-                    mycnt = 1;
-                    mycap = 0;
-                    sent_done = true;
-                }
-                used += nsent;
-            }
-        }
-        for (uint64_t dm = ballot((myflag & (F_SPEC | F_STATUS)) != 0u && !sent_done); dm; dm &= dm - 1) {
+        // ---- changed paths of the dirty pairs, in pair order, into this wave's arena
+        for (uint64_t dm = ballot((myflag & (F_SPEC | F_STATUS)) != 0u); dm; dm &= dm - 1) {
             const uint32_t k = (uint32_t)__builtin_ctzll(dm);
             const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)myflag, (int)k);
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
