@@ -40,6 +40,13 @@ def test_host_only_context_refuses_device_work():
         e.submit([(b"{}", b"{}")])
     assert ei.value.code == G.E_NODEVICE
     assert G.lib().gpudiff_abi_version() == 4
+    # pinned zero-copy buffers need a device; freeing a pointer the context never handed out is refused
+    import ctypes as C
+    p = C.c_void_p()
+    assert G.lib().gpudiff_host_alloc(e.ctx, 4096, C.byref(p)) == G.E_NODEVICE and not p.value
+    assert G.lib().gpudiff_host_alloc(e.ctx, 0, C.byref(p)) == G.E_INVAL
+    buf = C.create_string_buffer(64)
+    assert G.lib().gpudiff_host_free(e.ctx, C.cast(buf, C.c_void_p)) == G.E_INVAL
     e.close()
 
 
