@@ -135,6 +135,12 @@ struct DStore {
     // previous diff pass (its space) -- so a batch's K0 overlaps the previous batch's diff pass on the kernel stream
     hipStream_t ks0 = nullptr;
     int last_ring = -1;  // the ring slot of the previous submit
+    // store mode, GPUDIFF_K0_DECOUPLE_STORE=1 (opt-in): the K0 stage on ks0 there too; whatever the kernel stream
+    // does to the slot table or the space between submits (compaction, Delete, the host resolution's placement)
+    // first waits for the last K0 stage and sets st_slot_ops, and the next K0 stage then waits for the kernel stream
+    bool dec_store = false;
+    bool st_slot_ops = false;
+    hipEvent_t st_ev = nullptr;
     uint64_t up_chunk_bytes = kUpChunkBytes;
     uint32_t up_max_chunks = kMaxUpChunks;
     uint64_t* sizes = nullptr;
@@ -215,10 +221,21 @@ int grow_dev(T** p, uint64_t* cap, uint64_t need) {
     return GPUDIFF_OK;
 }
 
+// a kernel-stream operation on the slot table or the space (store mode with the K0 stage on its own stream):
+// after the last K0 stage, and the next K0 stage waits for it
+int before_st_slot_op(DStore* s) {
+    if (!s->dec_store) return GPUDIFF_OK;
+    if (s->last_ring >= 0 && s->ring[s->last_ring].k0_recorded)
+        HIPCHK(hipStreamWaitEvent(s->c->stream, s->ring[s->last_ring].k0_done, 0));
+    s->st_slot_ops = true;
+    return GPUDIFF_OK;
+}
+
 // packs the live blobs into the other space (stream-ordered), then reads the
 // exact append point back
 int compact(DStore* s) {
     gpudiff_ctx* c = s->c;
+    if (int rc = before_st_slot_op(s)) return rc;
     HIPCHK(launch_compact_store(c->stream, s->slots, s->max_slots, s->space[s->cur], s->space[1 - s->cur], s->sizes,
                                 s->tile_sums, s->used_dev));
     s->cur = 1 - s->cur;
@@ -292,6 +309,10 @@ void set_tab(HostSlot& H, const FlatObject& o) {
 int resolve(DStore* s, Ring& R, ResultStore& rs) {
     gpudiff_ctx* c = s->c;
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (s->dec_store) {  // the slot reads below see every K0 stage submitted so far, and the placement follows them
+        HIPCHK(hipStreamSynchronize(s->ks0));
+        s->st_slot_ops = true;
+    }
     std::vector<uint8_t> def(R.nev);
     if (R.nev) HIPCHK(hipMemcpy(def.data(), R.ddef, R.nev, hipMemcpyDeviceToHost));
     std::vector<uint32_t> drows;
@@ -640,6 +661,10 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
         return fail(GPUDIFF_E_DEVICE);
     for (Ring& R : s->ring)
         if (hipEventCreateWithFlags(&R.pass_done, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+    if (s->ks0 && getenv("GPUDIFF_K0_DECOUPLE_STORE")) {
+        if (hipEventCreateWithFlags(&s->st_ev, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
+        s->dec_store = true;
+    }
     if (const char* v = getenv("GPUDIFF_H2D_CHUNK_MIB"))
         s->up_chunk_bytes = std::max<uint64_t>(1, strtoull(v, nullptr, 10)) << 20;
     if (const char* v = getenv("GPUDIFF_H2D_MAX_CHUNKS"))
@@ -673,7 +698,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     int rc;
     if (R.staged) HIPCHK(hipEventSynchronize(R.staged));
     // pair mode with the K0 stage on its own streams (ks0 / ks): decoupled from the kernel stream
-    const bool dec = s->pair_mode && s->ks0;
+    const bool dec = (s->pair_mode || s->dec_store) && s->ks0;
     if (s->pair_mode) {  // this ring slot's space, emptied behind its previous batch (stream order)
         s->cur = s->ring_next;
         s->used_dev = s->used_base + s->ring_next;
@@ -926,7 +951,12 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         if (s->last_ring >= 0 && s->ring[s->last_ring].k0_recorded)
             HIPCHK(hipStreamWaitEvent(k0s, s->ring[s->last_ring].k0_done, 0));
         if (R.pass_recorded) HIPCHK(hipStreamWaitEvent(k0s, R.pass_done, 0));
-        HIPCHK(hipMemsetAsync(s->used_dev, 0, 8, k0s));
+        if (s->pair_mode) HIPCHK(hipMemsetAsync(s->used_dev, 0, 8, k0s));
+        if (s->st_slot_ops) {  // store mode: a compaction, Delete or placement since the last K0 stage
+            HIPCHK(hipEventRecord(s->st_ev, st));
+            HIPCHK(hipStreamWaitEvent(k0s, s->st_ev, 0));
+            s->st_slot_ops = false;
+        }
     }
     if (s->pair_mode) HIPCHK(hipMemsetAsync(s->slots, 0, sizeof(DSlot) * n, k0s));  // every pair starts empty
     if (s->ks) {  // the second K0 stream starts behind everything before this batch's K0 on the K0 stage's stream
@@ -1171,6 +1201,7 @@ void dstore_host_bufs_release(gpudiff_ctx* c) {
 }
 
 int dstore_forget(gpudiff_ctx* c, DStore* s, uint32_t slot) {
+    if (int rc = before_st_slot_op(s)) return rc;
     HIPCHK(launch_forget(c->stream, s->slots, slot, s->ctr));
     s->seen[slot] = 0;
     s->forgotten[slot] = s->batch_seq;
@@ -1238,6 +1269,7 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
         }
     for (Ring& R : s->ring)
         if (R.pass_done) (void)hipEventDestroy(R.pass_done);
+    if (s->st_ev) (void)hipEventDestroy(s->st_ev);
     if (s->ks_ev) (void)hipEventDestroy(s->ks_ev);
     if (s->cs) {
         (void)hipStreamSynchronize(s->cs);
