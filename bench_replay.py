@@ -53,9 +53,11 @@ def run(args):
 
     assert G.Event.__sizeof__ is not None and C.sizeof(G.Event) == EVENT_DTYPE.itemsize
     torch.cuda.set_device(0)
-    ncpu = len(os.sched_getaffinity(0))
+    from bench import cpu_threads, host_cores
+    aff, nproc, quota = host_cores()
+    ncpu = cpu_threads(aff, quota)  # the cores this process may run at once (affinity capped by the cgroup quota)
     threads = args.threads or max(1, min(16, ncpu))
-    M = args.pairs or 1_000_000
+    M = args.pairs or (1 << 20)  # 16 batches of 65,536 per epoch
     B = args.batch
     cfg = S.make_cfg("config3", n_pairs=M, n_clusters=args.clusters or max(1, M // 100))
     pop = S.Population(cfg)
@@ -109,68 +111,89 @@ def run(args):
     log("initial list: %d objects in %.1f s (%.0f objects/s), %.2f GB resident" % (
         M, t_load, M / t_load, ss.live_bytes / 1e9))
 
-    # ---- timed replay: each batch = B distinct objects, each advanced one version
+    # ---- timed replay (>= 10 s sustained).  The batches come from a cycle built before the
+    # clock: two epochs, each a permutation of every resident object cut into batches of B distinct objects; the
+    # first epoch advances each object A -> B, the second B -> A, so the cycle can repeat for as long as the run
+    # lasts and every event is a real Update of the object's current version (same 5% mutation rate as config3)
     rng = np.random.default_rng(20211004 + 5)
-    on_b = np.zeros(M, dtype=bool)  # current version of each object
-    n_batches = args.batches
-    batches = []
-    for k in range(args.warmup_batches + n_batches):
-        sl = rng.choice(M, size=B, replace=False).astype(np.uint32)
-        new_is_b = ~on_b[sl]
-        on_b[sl] = new_is_b
-        batches.append((sl, new_is_b, events(sl, new_is_b)))
-    lat, gpu_ms, bytes_up = [], [], 0
-    results = []
-    up_bytes = [int(b[2]["new_len"].sum()) for b in batches]
+    cycle = []
+    for epoch in range(2):
+        perm = rng.permutation(M).astype(np.uint32)
+        for s0 in range(0, M, B):
+            sl = perm[s0:s0 + B]
+            new_is_b = np.full(sl.size, epoch == 0)
+            cycle.append((sl, new_is_b, events(sl, new_is_b)))
+    up_bytes = [int(c[2]["new_len"].sum()) for c in cycle]
+    min_batches = args.batches if args.seconds <= 0 else 0
+    lat, bytes_up = [], 0
+    results = []  # (pair flags, cycle index) of every timed batch: checked after the clock stops
     t_sub, t_wait = [], []  # host time inside submit / wait per timed batch
+    done_at = []  # completion time of every timed batch (the throughput series)
     ss0 = None
     mism = 0
     checked = 0
     sample_ok = None
     first_res = None
-    inflight = []  # (ticket, t_submit, batch index)
+    inflight = []  # (ticket, t_submit, cycle index, timed)
     eng.timing_reset()
     t_start = None
-    for k, (sl, new_is_b, ev) in enumerate(batches):
+    k = 0
+    n_timed = ev_total = 0
+    while True:
         if k == args.warmup_batches:
             # drain the warmup batches, then start the clock
             while inflight:
-                tk, ts, kk = inflight.pop(0)
-                eng.wait(tk)
+                eng.wait(inflight.pop(0)[0])
             eng.timing_reset()
             ss0 = st.stats()
             t_start = time.time()
+        timed = k >= args.warmup_batches
+        if timed:
+            el = time.time() - t_start
+            if (args.seconds > 0 and el >= args.seconds) or (args.seconds <= 0 and n_timed >= min_batches):
+                break
+        ci = k % len(cycle)
         ts = time.time()
-        tk = submit(ev)
-        if k >= args.warmup_batches:
+        tk = submit(cycle[ci][2])
+        if timed:
             t_sub.append(time.time() - ts)
-            # device encoding uploads the events' JSON (summed per batch before the clock); host
-            # encoding the encoded blobs
-            bytes_up += up_bytes[k] if dev_enc else st.stats().last_batch_bytes
-        inflight.append((tk, ts, k))
+            # device encoding uploads the events' JSON; host encoding the encoded blobs
+            bytes_up += up_bytes[ci] if dev_enc else st.stats().last_batch_bytes
+            n_timed += 1
+            ev_total += cycle[ci][0].size
+        inflight.append((tk, ts, ci, timed))
         if len(inflight) == 2:
-            tk0, ts0, k0 = inflight.pop(0)
+            tk0, ts0, c0, tm0 = inflight.pop(0)
             tw = time.time()
             r = eng.wait(tk0)
-            if k0 >= args.warmup_batches:
-                t_wait.append(time.time() - tw)
-                lat.append(time.time() - ts0)
-                results.append((r, k0))  # checked against the ground truth after the clock stops
+            if tm0:
+                now = time.time()
+                t_wait.append(now - tw)
+                lat.append(now - ts0)
+                done_at.append(now - t_start)
+                results.append((r.pair_flags, c0))
+                if first_res is None:
+                    first_res = (r, cycle[c0])
+        k += 1
     while inflight:
-        tk0, ts0, k0 = inflight.pop(0)
+        tk0, ts0, c0, tm0 = inflight.pop(0)
         r = eng.wait(tk0)
-        lat.append(time.time() - ts0)
-        results.append((r, k0))
+        now = time.time()
+        lat.append(now - ts0)
+        done_at.append(now - t_start)
+        results.append((r.pair_flags, c0))
     t_end = time.time()
     el = t_end - t_start
-    for r, k0 in results:  # every timed decision against the generator's ground truth
-        f = r.pair_flags & 3
-        mism += int((f != (exp_ab[batches[k0][0]] & 3)).sum())
+    n_batches = n_timed
+    for f, c0 in results:  # every timed decision against the generator's ground truth
+        f = f & 3
+        mism += int((f != (exp_ab[cycle[c0][0]] & 3)).sum())
         checked += f.size
-        if first_res is None:
-            first_res = (r, batches[k0])
+    # sustained rate per whole second of the run (batches completed in each 1-s window x B)
+    done_at = np.array(done_at)
+    per_s = [int(((done_at >= w) & (done_at < w + 1)).sum()) * B for w in range(int(el))]
+    batches = cycle
     tm = eng.timings()
-    ev_total = n_batches * B
     ss = st.stats()
 
     def window(f):  # the mean of a per-batch store timing over the timed batches only
@@ -187,7 +210,7 @@ def run(args):
             sample_ok = _sample_check(first_res[0], first_res[1], buf, offs, args.sample)
             log("sample bit-exact vs oracle:", sample_ok)
         from oracle import cpu_ref
-        sl, new_is_b, _ = batches[args.warmup_batches]
+        sl, new_is_b, _ = first_res[1]
         m = min(args.cpu_sample, sl.size)
         pairs = []
         for i in range(m):
@@ -217,11 +240,16 @@ def run(args):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (config3 object mix; each event alternates an object's two seeded versions)",
-        "config": {"workload": "config5: %d resident objects, batches of %d events, 2 in flight" % (M, B),
+        "config": {"workload": "config5: %d resident objects, batches of %d events, 2 in flight, %s" % (
+            M, B, ("time-based: >= %.0f s sustained" % args.seconds) if args.seconds > 0 else "%d batches" % n_batches),
                    "encode": "device (K0 JSON tokenizer/encoder in HBM)" if dev_enc else "host (%d threads)" % threads,
                    "host_threads": threads},
+        "duration_s": el,
         "latency_ms": {"p50": float(np.percentile(lat_ms, 50)), "p99": float(np.percentile(lat_ms, 99)),
-                       "max": float(lat_ms.max())},
+                       "max": float(lat_ms.max()), "def": "submit call -> results on the host, per batch of %d" % B},
+        "events_per_second_window": {"series": per_s, "min": min(per_s) if per_s else None,
+                                     "max": max(per_s) if per_s else None,
+                                     "def": "events of the batches completed in each whole second of the run"},
         "h2d_gbps": bytes_up / el / 1e9,
         "gpu_ms_per_batch": {"diff_pass": tm.total_ms, "k2": tm.compare_ms},
         "store": {"resident_gb": ss.live_bytes / 1e9, "compactions": ss.compactions, "reseeded": ss.reseeded,
@@ -231,7 +259,12 @@ def run(args):
                      "submit_split": {f: window(f) for f in ("submit_wait_ms", "submit_docs_ms", "submit_copy_ms",
                                                              "submit_enqueue_ms")},
                      "store_finish": window("finish_ms"),
-                     "submit_call": float(np.mean(t_sub) * 1e3), "wait_call": float(np.mean(t_wait) * 1e3)}
+                     "submit_call": float(np.mean(t_sub) * 1e3), "wait_call": float(np.mean(t_wait) * 1e3),
+                     "share_of_step": {"k0_encode": window("encode_ms") / (el / n_batches * 1e3),
+                                       "host_staging_copy": window("submit_copy_ms") / (el / n_batches * 1e3),
+                                       "h2d": window("h2d_ms") / (el / n_batches * 1e3),
+                                       "def": "per-batch phase time / the sustained time per batch (phases of "
+                                              "neighbouring batches overlap, so shares can sum past 1)"}}
         if dev_enc else None,
         "initial_list_objects_per_s": M / t_load,
         "checks": {"events_checked": checked, "decision_mismatches_vs_ground_truth": mism,

@@ -266,9 +266,9 @@ int gpudiff_dbatch_export(gpudiff_ctx* ctx, const gpudiff_dbatch* db, uint32_t w
  * one bound (rebinding the same buffer is free).  send_dev = NULL unbinds. */
 int gpudiff_dbatch_bind_gather(gpudiff_ctx* ctx, gpudiff_dbatch* db, void* send_dev, uint32_t cap_spec,
                                uint32_t cap_status);
-/* Result slots: the spec / status dirty-ID lists come in two slots (0 by default; slot 1 allocated on first
- * use).  Later diffs write, and exports / gpudiff_wait read, the selected slot; the other keeps the lists
- * of the last diff made under it.  A per-step collective that checks step s's gathered counts only after
+/* Result slots: the spec / status dirty-ID lists and the counts (GPUDIFF_EXPORT_COUNTS) come in two slots
+ * (0 by default; slot 1 allocated on first use).  Later diffs write, and exports / gpudiff_wait read, the
+ * selected slot; the other keeps the lists and counts of the last diff made under it.  A per-step collective that checks step s's gathered counts only after
  * step s + 1's diff is enqueued alternates slots by step, so a capacity regrow can still export step s's
  * complete lists (kcp_amd/shard.py DirtyGather, lookahead).  Host-only state: ordered like every call. */
 int gpudiff_dbatch_result_slot(gpudiff_ctx* ctx, gpudiff_dbatch* db, uint32_t slot);

@@ -571,12 +571,25 @@ int gpudiff_dbatch_result_slot(gpudiff_ctx* c, gpudiff_dbatch* d, uint32_t slot)
     int rc = set_device(c);
     if (rc) return rc;
     if (slot == d->res_slot) return GPUDIFF_OK;
-    if (!d->ids_alt[0]) {
+    if (!d->summary_alt) {  // all three buffers or none (a half-allocated slot would swap in a null list)
         const uint64_t np = std::max<uint64_t>(d->max_pairs, 1);
-        if ((rc = dalloc(&d->ids_alt[0], np)) || (rc = dalloc(&d->ids_alt[1], np))) return rc;
+        uint32_t *a = nullptr, *b = nullptr, *sm = nullptr;
+        if ((rc = dalloc(&a, np)) || (rc = dalloc(&b, np)) || (rc = dalloc(&sm, kSummaryWords))) {
+            for (uint32_t* p : {a, b, sm})
+                if (p) (void)hipFree(p);
+            return rc;
+        }
+        if (hipMemset(sm, 0, kSummaryWords * sizeof(uint32_t)) != hipSuccess) {
+            for (uint32_t* p : {a, b, sm}) (void)hipFree(p);
+            return GPUDIFF_E_DEVICE;
+        }
+        d->ids_alt[0] = a, d->ids_alt[1] = b, d->summary_alt = sm;
     }
+    // the counts are per slot too: a lookahead regrow re-exports step s's counts after step s + 1 ran
+    // (one shared summary paired step s + 1's counts with step s's lists)
     std::swap(d->spec_ids, d->ids_alt[0]);
     std::swap(d->status_ids, d->ids_alt[1]);
+    std::swap(d->summary, d->summary_alt);
     d->res_slot = slot;
     return GPUDIFF_OK;
 }

@@ -1292,7 +1292,6 @@ int dstore_staged_pairs(gpudiff_ctx* c, gpudiff_ticket t, StagedPairs* out) {
         (void)max_docs;
         out->hdocs = (const TokDoc*)R.hmeta;
         out->djson = R.djson;
-        out->hjson = R.hjson;
         out->n = R.nev;
         out->flags = &R.final_flags;
         out->events = &R.events;

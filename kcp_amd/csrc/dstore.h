@@ -17,13 +17,14 @@ void dstore_free(gpudiff_ctx* c, DStore* s);
 void dstore_host_bufs_release(gpudiff_ctx* c);  // gpudiff_close: the context's remaining gpudiff_host_alloc buffers
 
 // The staged JSON of a waited pair-mode batch (gpudiff_submit with GPUDIFF_OPT_DEVICE_ENCODE): pair i's
-// old object is document 2i, its new one 2i + 1; hdocs[] holds their offsets into djson (HBM) and hjson
-// (pinned host copy); flags = the batch's final result flags (host-deferred pairs resolved).  Valid until
-// the ring slot is reused by the submit after the next one.
+// old object is document 2i, its new one 2i + 1; hdocs[] holds their offsets into djson (HBM); flags = the
+// batch's final result flags (host-deferred pairs resolved).  Valid until the ring slot is reused by the
+// submit after the next one.  There is no host copy to offer: a zero-copy batch was uploaded from the
+// caller's buffer (reusable once gpudiff_wait returned), so host work on a staged document reads it back
+// from djson.
 struct StagedPairs {
     const gd::TokDoc* hdocs = nullptr;
     const uint8_t* djson = nullptr;
-    const uint8_t* hjson = nullptr;
     uint32_t n = 0;
     const std::vector<uint8_t>* flags = nullptr;
     const std::vector<gpudiff_event>* events = nullptr;

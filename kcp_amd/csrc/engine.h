@@ -101,9 +101,11 @@ struct gpudiff_dbatch {
     gpudiff_ticket ticket = 0;
     uint32_t* gather_send = nullptr;  // gpudiff_dbatch_bind_gather
     uint32_t gather_cap_spec = 0, gather_cap_status = 0;
-    // gpudiff_dbatch_result_slot: the spec / status lists of the other slot (spec_ids / status_ids are
-    // always the current slot's; switching swaps them), allocated on first use
+    // gpudiff_dbatch_result_slot: the spec / status lists and the summary (counts) of the other slot
+    // (spec_ids / status_ids / summary are always the current slot's; switching swaps them), allocated on
+    // first use -- all three or none
     uint32_t* ids_alt[2] = {nullptr, nullptr};
+    uint32_t* summary_alt = nullptr;
     uint32_t res_slot = 0;
     // gpudiff_dbatch_create_view: this batch diffs `base`'s resident pairs (pool, rows, pair IDs borrowed,
     // refreshed at every diff) into its own outputs, so two passes over one population can be in flight
@@ -185,7 +187,7 @@ inline void dfree_all(gpudiff_dbatch* d) {
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
                   d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
                   d->scratch_h, d->scratch_k, d->out_h, d->out_k, d->nbits, d->noop_d, d->slot_owner,
-                  d->slice_cnt, d->slice_weq, d->ids_alt[0], d->ids_alt[1], d->tail_perm};
+                  d->slice_cnt, d->slice_weq, d->ids_alt[0], d->ids_alt[1], d->summary_alt, d->tail_perm};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     if (d->done) (void)hipEventDestroy(d->done);

@@ -638,10 +638,27 @@ int gpudiff_write_plan_get_ex(gpudiff_ctx* c, gpudiff_ticket ticket, uint32_t mo
             return GPUDIFF_E_DEVICE;
         }
     }
-    // K10's deferrals: the host path over the pinned host copy of the same staged JSON
+    // K10's deferrals: the host path over the same staged JSON, read back from HBM (the batch may have been
+    // uploaded zero-copy from a caller's buffer that is reusable since gpudiff_wait returned, and a staging
+    // copy in the ring slot may belong to another batch)
     std::vector<uint32_t> def;
     for (size_t k = 0; k < nd; k++)
         if (to[k].status != GPUDIFF_TOK_OK) def.push_back((uint32_t)k);
+    std::vector<uint64_t> hoff(def.size() + 1, 0);
+    for (size_t k = 0; k < def.size(); k++) hoff[k + 1] = hoff[k] + docs[def[k]].json_len;
+    std::vector<uint8_t> hjson(hoff.back());
+    if (!def.empty()) {
+        hipError_t e = hipSuccess;
+        for (size_t k = 0; k < def.size() && e == hipSuccess; k++)
+            if (docs[def[k]].json_len)
+                e = hipMemcpyAsync(hjson.data() + hoff[k], sp.djson + docs[def[k]].json_off, docs[def[k]].json_len,
+                                   hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            gd::g_last_hip_error = hipGetErrorString(e);
+            return GPUDIFF_E_DEVICE;
+        }
+    }
     std::vector<std::string> hb(def.size());
     std::vector<uint8_t> hok(def.size(), 0);
     const uint32_t mode_split = n_spec_docs;
@@ -650,7 +667,7 @@ int gpudiff_write_plan_get_ex(gpudiff_ctx* c, gpudiff_ticket ticket, uint32_t mo
         auto work = [&](uint32_t t) {
             for (size_t k = t; k < def.size(); k += T) {
                 const TokDoc& d = docs[def[k]];
-                hok[k] = host_body(sp.hjson + d.json_off, d.json_len,
+                hok[k] = host_body(hjson.data() + hoff[k], d.json_len,
                                    def[k] < mode_split ? GPUDIFF_UPSERT_SPEC : GPUDIFF_UPSERT_STATUS, hb[k])
                              ? 1
                              : 0;

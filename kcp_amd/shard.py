@@ -131,6 +131,8 @@ class DirtyGather:
         self.maxc_host = np.zeros((world, 2), dtype=np.int64)  # depth 1: the counts read back every step
         self.slot = slot if self.depth == 1 else None
         self.pending = None  # lookahead: the step whose gathered counts are not checked yet
+        self.gathered = []  # tests (trace): (step, capacities, gathered rows) of every lookahead gather
+        self.trace = False
         self._alloc(cap_spec, cap_status)
 
     def _alloc(self, cap_spec: int, cap_status: int):
@@ -168,7 +170,7 @@ class DirtyGather:
         if self.slot is not None:
             self.slot(self.n_steps % 2)
 
-    def _gather_lookahead(self, k: int):
+    def _gather_lookahead(self, k: int, step: int = -1):
         """all-gather of the send buffer, then this step's gathered counts copied to pinned slot k behind an
         event (read later by _check)"""
         self.dist.all_gather_into_tensor(self.all, self.send)
@@ -176,6 +178,8 @@ class DirtyGather:
         self.la_caps[k] = self.cap
         if self.la_events[k] is not None:
             self.la_events[k].record()
+        if self.trace:  # synchronises: tests only
+            self.gathered.append((step, self.cap, self.all.view(self.world, self.width).cpu().clone()))
 
     def _check(self, s: int, fill_counts, fill_ids):
         """Lookahead: step s's gathered counts (its collective finished long before: step s + 1's pass was
@@ -198,7 +202,7 @@ class DirtyGather:
             fill_counts(self.counts)
             for col in (0, 1):
                 fill_ids(col, self.buf[col])
-            self._gather_lookahead(t % 2)
+            self._gather_lookahead(t % 2, t)
         self.n_regrows += 1
         if self.pending == s + 1:  # its re-gather may still exceed the grown capacity: checked as usual
             self.slot((s + 2) % 2)
@@ -244,7 +248,7 @@ class DirtyGather:
                 fill_ids(col, self.buf[col])
         if self.slot is not None:  # lookahead (depth 1)
             s = self.n_steps
-            self._gather_lookahead(s % 2)
+            self._gather_lookahead(s % 2, s)
             prev, self.pending = self.pending, s
             self.used[0] = True
             self.n_steps += 1
@@ -334,13 +338,21 @@ class PipelinedGather:
     step s + 1 is queued; a capacity exceeded on any rank (every rank sees the same counts) grows both
     buffers and re-gathers step s from batch s % 2 -- its lists stay until step s + 2 -- and the in-flight
     step s + 1 from the other, each on its own stream.  Replaced buffers are kept alive until finish(), as
-    a collective still queued may read them."""
+    a collective still queued may read them.
+
+    comm_device = cpu (the gloo rehearsal of this path on one GPU, where RCCL refuses two ranks per device):
+    the send buffers stay on the GPU -- the engines still write them from their compaction -- and each
+    step's buffer is staged into a pinned host tensor on its pass's stream after that pass, then gathered
+    by gloo on the host.  Binding, views, lookahead and regrow are the RCCL path's; only the transport
+    differs (and the host waits for pass s before gathering it, so the rehearsal's timings are not the
+    node's)."""
 
     def __init__(self, world: int, cap_spec: int, cap_status: int, device, dist, streams, binds,
-                 grow: float = 1.25):
+                 grow: float = 1.25, comm_device=None):
         import numpy as np
         import torch
         self.world, self.dist, self.device = world, dist, device
+        self.host = comm_device is not None and torch.device(comm_device).type == "cpu"
         self.streams, self.binds = list(streams), list(binds)
         self.grow = max(1.0, float(grow))
         self.n_steps = 0
@@ -350,6 +362,8 @@ class PipelinedGather:
         self.hc = [torch.zeros((world, 2), dtype=torch.int32, pin_memory=True) for _ in range(2)]
         self.ev = [torch.cuda.Event() for _ in range(2)]
         self.graveyard = []
+        self.gathered = []  # (step, rank-0 rows [world, 8] as gathered) -- every gather, regrows included
+        self.trace = False
         self._alloc(cap_spec, cap_status)
 
     def _alloc(self, cap_spec: int, cap_status: int):
@@ -359,10 +373,14 @@ class PipelinedGather:
         self.cap = (max(1, int(cap_spec)), max(1, int(cap_status)))
         self.width = 8 + self.cap[0] + self.cap[1]
         self.sends, self.alls = [], []
+        # gloo: the host mirrors the collective reads and writes (the send buffers stay device memory)
+        self.hsends = [torch.zeros(self.width, dtype=torch.int32, pin_memory=True) for _ in range(2)] \
+            if self.host else None
         for p in range(2):
             with torch.cuda.stream(self.streams[p]):
                 self.sends.append(torch.zeros(self.width, dtype=torch.int32, device=self.device))
-                self.alls.append(torch.zeros(self.world * self.width, dtype=torch.int32, device=self.device))
+                self.alls.append(torch.zeros(self.world * self.width, dtype=torch.int32,
+                                             device="cpu" if self.host else self.device))
             self.binds[p](self.sends[p], self.cap[0], self.cap[1])
         self.caps_at = [self.cap, self.cap]
 
@@ -370,19 +388,32 @@ class PipelinedGather:
         s = self.sends[p]
         return s[:8], [s[8:8 + self.cap[0]], s[8 + self.cap[0]:]]
 
-    def _gather(self, p: int):
+    def _gather(self, p: int, step: int = -1):
         import torch
-        with torch.cuda.stream(self.streams[p]):
-            self.dist.all_gather_into_tensor(self.alls[p], self.sends[p])
-            self.hc[p].copy_(self.alls[p].view(self.world, self.width)[:, :2], non_blocking=True)
-            self.ev[p].record()
+        if self.host:
+            # pass p's send buffer (written by its compaction, on its stream) -> pinned host -> gloo
+            with torch.cuda.stream(self.streams[p]):
+                self.hsends[p].copy_(self.sends[p], non_blocking=True)
+            self.streams[p].synchronize()
+            self.dist.all_gather_into_tensor(self.alls[p], self.hsends[p])
+            self.hc[p].copy_(self.alls[p].view(self.world, self.width)[:, :2])
+            self.ev[p].record(self.streams[p])  # already complete: keeps _check's wait uniform
+        else:
+            with torch.cuda.stream(self.streams[p]):
+                self.dist.all_gather_into_tensor(self.alls[p], self.sends[p])
+                self.hc[p].copy_(self.alls[p].view(self.world, self.width)[:, :2], non_blocking=True)
+                self.ev[p].record()
         self.caps_at[p] = self.cap
+        if self.trace:  # tests: what each gather delivered (synchronises; never in a timed run)
+            self.streams[p].synchronize()
+            rows = self.alls[p].view(self.world, self.width)
+            self.gathered.append((step, self.cap, rows.cpu().clone()))
 
     def step(self, fill_counts, fill_ids):
         """After step s's diff was enqueued on pass s % 2's context.  fill_counts(p, t) / fill_ids(p, col,
         buf) re-export pass p's results (used only after a regrow)."""
         s = self.n_steps
-        self._gather(s % 2)
+        self._gather(s % 2, s)
         prev, self.pending = self.pending, s
         self.n_steps += 1
         self._fills = (fill_counts, fill_ids)
@@ -408,7 +439,7 @@ class PipelinedGather:
                 fill_counts(q, counts)
                 for col in (0, 1):
                     fill_ids(q, col, bufs[col])
-            self._gather(q)
+            self._gather(q, t)
         self.n_regrows += 1
 
     def finish(self):

@@ -161,3 +161,74 @@ def test_dirty_gather_over_rccl_world1():
     finally:
         torch.cuda.set_stream(torch.cuda.default_stream(dev))
         dist.destroy_process_group()
+
+
+def test_lookahead_regrow_with_changing_counts():
+    """with lookahead, a capacity overflow found one step late re-gathers step s from its result
+    slot after step s + 1 has run.  The counts must be step s's too (the summary is per result slot): here step
+    0 diffs 3000 pairs, then 1000 more are appended, so step 1's counts differ from step 0's; every gather --
+    the regrow's re-gathers included -- must carry its own step's counts and exactly its own step's IDs."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
+        eng = G.Engine(device=0, stream=stream.cuda_stream)
+        pa, _, _ = make_pairs(3000, seed=31, mutate_frac=0.3, pretty_frac=0)
+        pb, _, _ = make_pairs(1000, seed=32, mutate_frac=0.6, pretty_frac=0)
+        ha, hb = eng.encode(pa), eng.encode(pb)
+        cap = ha.info().pool_bytes + hb.info().pool_bytes + 8192
+        want = []
+        for parts in ((ha,), (ha, hb)):
+            d = eng.device_batch(cap, len(pa) + len(pb))
+            for h in parts:
+                d.append(h)
+            r = eng.wait(eng.diff(d))
+            want.append((r.spec_dirty_ids.copy(), r.status_dirty_ids.copy()))
+            d.free()
+        # pair IDs of the appended batch continue after the first one's
+        assert want[1][0].size > want[0][0].size and want[1][1].size > want[0][1].size
+        db = eng.device_batch(cap, len(pa) + len(pb))
+        db.append(ha)
+        bind = lambda send, cs, ct: db.bind_gather(send.data_ptr(), cs, ct)  # noqa: E731
+
+        def fill_counts(t):
+            db.export(G.EXPORT_COUNTS, t.data_ptr(), 8)
+
+        def fill_ids(col, buf):
+            db.export(G.EXPORT_SPEC_IDS if col == 0 else G.EXPORT_STATUS_IDS, buf.data_ptr(), buf.numel(),
+                      buf.numel())
+        caps = (max(1, want[0][0].size // 2), max(1, want[0][1].size // 2))
+        g = shard.DirtyGather(1, caps[0], caps[1], dev, dist, bind=bind, slot=lambda k: db.result_slot(k))
+        g.trace = True
+        for s in range(4):
+            if s == 1:
+                db.append(hb)
+            g.begin_step()
+            eng.diff(db)
+            g.step(fill_counts, fill_ids)
+        g.finish()
+        torch.cuda.synchronize()
+        assert g.n_regrows >= 1
+        seen = set()
+        for step, (cs, ct), rows in g.gathered:
+            w = want[0] if step == 0 else want[1]
+            n_s, n_t = int(rows[0, 0]), int(rows[0, 1])
+            assert (n_s, n_t) == (w[0].size, w[1].size), (step, n_s, n_t)
+            if n_s <= cs and n_t <= ct:  # a complete gather: exactly that step's lists
+                seen.add(step)
+                assert np.array_equal(rows[0, 8:8 + n_s].numpy().astype(np.uint32), w[0]), step
+                assert np.array_equal(rows[0, 8 + cs:8 + cs + n_t].numpy().astype(np.uint32), w[1]), step
+        assert {0, 1, 2, 3} <= seen  # step 0 was re-gathered complete after step 1 ran
+        sa, ta = g.result()
+        assert np.array_equal(sa.cpu().numpy().astype(np.uint32), want[1][0])
+        db.bind_gather(0, 0, 0)
+        db.free()
+        ha.free()
+        hb.free()
+        eng.close()
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+        dist.destroy_process_group()

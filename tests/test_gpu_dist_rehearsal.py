@@ -2,9 +2,13 @@
 
 RCCL refuses two ranks on one device, so `bench.py --dist-backend gloo` runs the real multi-rank path --
 the self-launch child (torch.distributed.run), byte-weighted LPT shards with the weight all-reduce,
-per-rank engines on GPU 0, DirtyGather's one all-gather per step, the max-dt and total-pairs all-reduces,
-rank 0's relayed line -- with counts and IDs staged through host tensors.  The node-wide dirty sets rank
-0 gathered must equal a single-rank diff of the whole population."""
+per-rank engines on GPU 0, the one all-gather per step, the max-dt and total-pairs all-reduces, rank 0's
+relayed line -- with counts and IDs staged through host tensors.  Both collectives run: one pass in flight
+(DirtyGather, export copies into the host tensors) and the default two passes in flight (PipelinedGather:
+two contexts, a view of the resident batch, the engine-written send buffer of each pass staged to the host
+after it, lookahead count checks), the latter also with capacities forced below the counts so the lookahead
+regrow re-gathers steps s and s + 1 at world 2.  The node-wide dirty sets rank 0 gathered must equal a
+single-rank diff of the whole population."""
 import json
 import os
 import subprocess
@@ -20,17 +24,22 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_ranks_gloo_on_one_gpu(tmp_path):
+@pytest.mark.parametrize("pipeline,cap_frac", [(1, 1.0), (2, 1.0), (2, 0.5)])
+def test_bench_two_ranks_gloo_on_one_gpu(tmp_path, pipeline, cap_frac):
     dump = str(tmp_path / "gather.npz")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--pairs", "100000", "--clusters", "1000",
-           "--dist-backend", "gloo", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--sample", "0",
-           "--json-in-pairs", "0", "--threads", "8", "--dump-gather", dump]
+           "--dist-backend", "gloo", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--sample", "0",
+           "--json-in-pairs", "0", "--threads", "8", "--dump-gather", dump, "--pipeline", str(pipeline),
+           "--gather-cap-frac", str(cap_frac), "--calib-passes", "1"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["shard"]["rule"] == "LPT by sum of B_pair"
+    assert line["config"]["passes_in_flight"] == pipeline
     g = line["checks"]["gather"]
+    assert g["pipeline"] == pipeline and g["engine_writes_send_buffer"] == (pipeline == 2)
+    assert g["regrows"] == (1 if cap_frac < 1 else 0), g
     assert g["capacity_ok"] and g["node_sets_eq_truth"], json.dumps(line["checks"]) + r.stderr[-2000:]
     assert g["gathered_spec"] == g["node_spec_dirty"] == g["node_expected_spec"]
     assert g["gathered_status"] == g["node_status_dirty"] == g["node_expected_status"]

@@ -148,3 +148,70 @@ def test_write_plan_informer_renders_new_object():
             if side == 1:
                 assert b'"replicas":%d' % (i + 100) in body
     eng.close()
+
+
+def _escaped_key_pairs(n, seed):
+    """Pairs whose new object has a key that needs unescaping (K10 hands such documents to the host path)
+    beside plain edits."""
+    rnd = random.Random(seed)
+    out = []
+    for i in range(n):
+        a = json.loads(J(BASE))
+        a["spec"]["replicas"] = rnd.randint(0, 50)
+        ja = J(a)
+        a["spec"]["replicas"] += 1
+        jb = J(a)
+        if i % 3 == 0:  # a key written with an escape: "maxSurge"-style, same decoded key
+            jb = jb.replace(b'"replicas"', b'"r\\u0065plicas"')
+            jb = jb.replace(b'"revisionHistoryLimit":10', b'"revisionHistoryLimit":%d' % (11 + i))
+        out.append((ja, jb))
+    return out
+
+
+def test_write_plan_zero_copy_batches_host_deferrals():
+    """a zero-copy batch (gpudiff_host_alloc buffer) has no copy in the ring slot's pinned
+    staging, so the write plan's host path for the documents K10 defers must not read the staging (null on a
+    slot that never staged; another batch's JSON otherwise).  Fresh engine: the first batch is zero-copy (its
+    slot never staged); then staged batches fill both slots with other JSON before another zero-copy batch."""
+    import numpy as np
+    eng = G.Engine(device=0, device_encode=True)
+
+    def pinned(pairs):
+        lens = [len(x) for p in pairs for x in p]
+        offs = np.zeros(len(lens) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum(lens)
+        buf = np.frombuffer(b"".join(x for p in pairs for x in p), dtype=np.uint8)
+        return G.PinnedJson(eng, buf, offs)
+
+    def check_plan(t, pairs):
+        plan = eng.write_plan(t)
+        want = U.write_plan(pairs)
+        got = list(zip(plan.pair_index.tolist(), plan.kind.tolist(), [bool(x) for x in plan.noop], plan.bodies))
+        assert got == want
+        return plan
+
+    zc1 = _escaped_key_pairs(60, 1)
+    pj = pinned(zc1)
+    t = eng.submit_array(pj.pairs)
+    res = eng.wait(t)
+    assert_matches(res, zc1)
+    plan = check_plan(t, zc1)
+    assert (plan.source == G.BODY_HOST).sum() >= 20  # the escaped-key documents went to the host path
+    assert eng.submit_stats().zero_copy_batches >= 1
+    # the caller may reuse its buffer once wait returned: scribble over it, the plan must not see it
+    np.ctypeslib.as_array(G.C.cast(pj.ptr, G.C.POINTER(G.C.c_uint8)), (pj.nbytes,))[:] = ord("x")
+    plan2 = eng.write_plan(t)
+    assert plan2.bodies == plan.bodies
+    pj.free()
+    for seed in (2, 3):  # staged batches into both ring slots
+        st = _escaped_key_pairs(40, 10 + seed)
+        t2 = eng.submit(st)
+        eng.wait(t2)
+        check_plan(t2, st)
+    zc2 = _escaped_key_pairs(50, 4)
+    pj2 = pinned(zc2)
+    t3 = eng.submit_array(pj2.pairs)
+    eng.wait(t3)
+    check_plan(t3, zc2)
+    pj2.free()
+    eng.close()
