@@ -773,19 +773,10 @@ def json_in_rates(G, pop, m, threads, device):
     arr = G.json_pair_array(buf, offs)
     out = dict(sample_pairs=m, json_bytes=int(offs[-1]), threads=threads)
     flags = {}
-    # A/B variants of device encode: device_encode_h2d2 with GPUDIFF_OPT_H2D_TWO_STREAMS (JSON chunks alternate
-    # two copy streams); device_encode_4chunks with round 3's staging (at most 4 upload chunks)
-    # device_encode_one_k0_stream: every chunk's K0 on the kernel stream (round 4's r04k-r04z pipeline)
-    modes = (("host_encode", 0, {}), ("device_encode", 0, {}),
-             ("device_encode_h2d2", G.OPT_H2D_TWO_STREAMS, {}), ("device_encode_4chunks", 0, {"GPUDIFF_H2D_MAX_CHUNKS": "4"}),
-             ("device_encode_one_k0_stream", 0, {"GPUDIFF_K0_ONE_STREAM": "1"}))
-    for mode, mflags, env in modes:
-        os.environ.update(env)  # read when the context's store is created (its first submit)
-        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode != "host_encode"), flags=mflags)
+    for mode in ("host_encode", "device_encode"):
+        e = G.Engine(device=device, encode_threads=threads, device_encode=(mode != "host_encode"))
         for _ in range(2):  # warm: both ring slots' staging, the scratch (and the device-encode store)
             r = e.wait(e.submit_array(arr))
-        for k in env:
-            os.environ.pop(k, None)
         times = []
         for _ in range(5):
             t0 = time.perf_counter()

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GPUDIFF_ABI_VERSION 4
+#define GPUDIFF_ABI_VERSION 5  /* 5: the tuning option bits removed (GPUDIFF_OPT_KNOWN); result slots own their counts */
 
 enum {
     GPUDIFF_OK = 0,
@@ -94,38 +94,19 @@ enum {
 #define GPUDIFF_PATH_STATUS_ABSENT 3u  /* new has no "status" key (statussyncer.go:22-26) */
 #define GPUDIFF_PATH_REGION_STATUS 0x80u
 
-/* context option flags */
-#define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times */
-#define GPUDIFF_OPT_K4_PIPELINED_JOIN 0x8u /* tuning: K4's merge-path slices prefetch the next window's keys and
-                                              metas (software-pipelined join) */
-/* bits 0x2 / 0x4: until ABI 3 they (and 0x8, bits 30-31) chose where long-value digests were computed; since ABI
-   4 the format has no digests (include/gpudiff_format.h: a long string's first 8 bytes sit in its leaf record,
-   the rest in the arena); now two tuning bits: */
-#define GPUDIFF_OPT_H2D_TWO_STREAMS 0x2u /* tuning: device-encode uploads alternate JSON chunks between two copy
-                                           streams (DMA queues) */
-#define GPUDIFF_OPT_K2_NO_LPT 0x4u      /* tuning: the decision kernel's final round of items in index order (the
-                                           default hands it out largest first when pairs are large) */
-/* tuning knobs (A/B measurements; 0 = defaults) */
-#define GPUDIFF_OPT_K2_VARIANT_SHIFT 8u  /* 4 bits: decision-kernel load policy / unroll */
-#define GPUDIFF_OPT_K2_BLOCKS_SHIFT 12u  /* 4 bits: resident blocks per CU for the decision kernel */
-#define GPUDIFF_OPT_SEGMENTS_SHIFT 16u   /* 4 bits: force the number of pipelined batch segments */
-#define GPUDIFF_OPT_NO_K2_ALT 0x100000u  /* keep every K2 segment on the main stream */
-#define GPUDIFF_OPT_ARENA_SHIFT 21u      /* 4 bits: shrink the per-wave path arena 2^k-fold
-                                            (tests: forces pairs through the deferred K4 path) */
+/* context option flags (any other bit: gpudiff_open returns GPUDIFF_E_INVAL).  Round 5 removed the A/B tuning
+ * bits of earlier rounds whose measurements rejected them (DESIGN.md §5-§6 keep the numbers):
+ * 0x2 two upload streams, 0x4 index-order final round, 0x8 pipelined K4 join, 0x10-0x80 tail shapes, bits 9-20
+ * kernel variants / blocks per CU / segmented passes, bits 26-31 K0 occupancy, items per wave, deep-join bounds. */
+#define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times (gpudiff_last_timings) */
+#define GPUDIFF_OPT_K2_TIMELINE 0x100u   /* profiling hook: the decision kernel's per-wave timeline build
+                                            (gpudiff_k2_profile buffer; tools/k2_wave_profile.py) */
+#define GPUDIFF_OPT_ARENA_SHIFT 21u      /* 4 bits, test hook: shrink the per-wave path arena 2^k-fold (forces
+                                            pairs through the deferred K4 path) */
 #define GPUDIFF_OPT_DEVICE_ENCODE 0x2000000u /* gpudiff_submit / single-pair helpers: raw JSON up, kernel K0
                                                 encodes (as GPUDIFF_STORE_DEVICE_ENCODE does for the store) */
-#define GPUDIFF_OPT_K0_VARIANT_SHIFT 26u /* 2 bits: K0 / K10 occupancy variant (0: 8 waves/SIMD, 1: unconstrained;
-                                           K10 also 2: 5 waves, 3: 6 waves) */
-#define GPUDIFF_OPT_K2_TAIL_SHIFT 4u    /* 3 bits t: decision-kernel tail of t - 1 quarters of its wave count
-                                           in 64-pair chunks (0: the default, 2 quarters; t = 1: no tail,
-                                           the last two rounds of tickets fetched late) */
-#define GPUDIFF_OPT_K2_TAIL8 0x80u      /* tuning: tail items of 8 pairs instead of half a main item */
-#define GPUDIFF_OPT_K2_DEEP_SHIFT 30u     /* 2 bits, tuning: 0 = K2 defers joins over 2048 keys to K4's merge-path
-                                            slices (the default), 1 = K2 joins every dirty pair its wave arena
-                                            holds, 2 / 3 = defer joins over 4096 / 8192 keys */
-#define GPUDIFF_OPT_K2_FUSE_DEEP (1u << GPUDIFF_OPT_K2_DEEP_SHIFT)
-#define GPUDIFF_OPT_K2_ITEMS_SHIFT 28u   /* 2 bits: decision-kernel items per resident wave before 64-pair
-                                            chunks are split (0: default 8, 1: 4, 2: 8, 3: 16) */
+#define GPUDIFF_OPT_KNOWN (GPUDIFF_OPT_TIMING | GPUDIFF_OPT_K2_TIMELINE | (0xFu << GPUDIFF_OPT_ARENA_SHIFT) | \
+                           GPUDIFF_OPT_DEVICE_ENCODE)
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */
@@ -423,12 +404,12 @@ int gpudiff_encode_objects(gpudiff_ctx* ctx, const uint8_t* const* docs, const s
                            size_t n, uint8_t* out, uint64_t out_cap, gpudiff_obj_info* info);
 int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, uint32_t path_hash_bits, uint8_t* out,
                                uint64_t out_cap, gpudiff_obj_info* info);
-/* tuning: K0 per-phase wall-clock ticks (100 MHz, summed over waves) since the
+/* profiling hook: K0 per-phase wall-clock ticks (100 MHz, summed over waves) since the
  * previous call (scan, tree, values, hashes, sort, blob, -, -); enable != 0
  * keeps recording */
 int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
-/* tuning: the decision kernel's per-wave timeline, recorded by K2 tuning variant 14 (the default
- * kernel plus timestamps; GPUDIFF_OPT_K2_VARIANT_SHIFT): 12 u64 per wave (start, end of the first
+/* profiling hook: the decision kernel's per-wave timeline, recorded by the GPUDIFF_OPT_K2_TIMELINE build of
+ * the default kernel (the same kernel plus timestamps): 12 u64 per wave (start, end of the first
  * item, items, start of the last item, end, streaming ticks, join ticks, hardware CU id, then ticks
  * spent per item on its rows, between its rows and its first pass, after its joins, and from one
  * item's end to the next one's start; 100 MHz) into device memory dev_buf of cap_waves records;

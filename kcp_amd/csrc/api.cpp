@@ -109,20 +109,11 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.slot_owner = d->slot_owner;
     b.slice_cnt = d->slice_cnt;
     b.slice_weq = d->slice_weq;
-    b.k2_deep_mode = (c->flags >> GPUDIFF_OPT_K2_DEEP_SHIFT) & 3u;
-    b.k4_pipelined = (c->flags & GPUDIFF_OPT_K4_PIPELINED_JOIN) ? 1u : 0u;
     b.hash_mask = c->hash_mask;
-    b.k2_variant = (c->flags >> GPUDIFF_OPT_K2_VARIANT_SHIFT) & 0xFu;
-    b.k2_blocks_per_cu = (c->flags >> GPUDIFF_OPT_K2_BLOCKS_SHIFT) & 0xFu;
-    {
-        const uint32_t it = (c->flags >> GPUDIFF_OPT_K2_ITEMS_SHIFT) & 3u;
-        b.k2_items_per_wave = it ? 2u << it : 0u;
-    }
-    b.k2_tail_quarters = (c->flags >> GPUDIFF_OPT_K2_TAIL_SHIFT) & 7u;
-    b.k2_tail8 = (c->flags & GPUDIFF_OPT_K2_TAIL8) ? 1u : 0u;
+    b.k2_timeline = (c->flags & GPUDIFF_OPT_K2_TIMELINE) ? 1u : 0u;
     b.tail_perm = d->tail_perm;
     b.tail_perm_key = &d->tail_perm_key;
-    b.k2_no_lpt = (c->flags & GPUDIFF_OPT_K2_NO_LPT) ? 1u : 0u;
+    b.rows_gen = d->rows_gen;
     b.gather_send = d->gather_send;
     b.gather_cap_spec = d->gather_cap_spec;
     b.gather_cap_status = d->gather_cap_status;
@@ -166,6 +157,7 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
     gpudiff_opts o{};
     o.device = GPUDIFF_DEVICE_CURRENT;
     if (opts) o = *opts;
+    if (o.flags & ~GPUDIFF_OPT_KNOWN) return GPUDIFF_E_INVAL;  // a removed tuning bit, or a typo
     std::unique_ptr<gpudiff_ctx> c(new (std::nothrow) gpudiff_ctx());
     if (!c) return GPUDIFF_E_NOMEM;
     uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
@@ -190,12 +182,7 @@ int gpudiff_open(const gpudiff_opts* opts, gpudiff_ctx** out) {
             HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             c->own_stream = true;
         }
-        HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->k2alt, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&c->rb, hipStreamNonBlocking));
-        for (auto& e : c->seg_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->side_done, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&c->alt_start, hipEventDisableTiming));
     }
     *out = c.release();
     return GPUDIFF_OK;
@@ -214,15 +201,10 @@ void gpudiff_close(gpudiff_ctx* c) {
         }
         for (auto& a : c->pass_ev)
             for (auto& e : a) (void)hipEventDestroy(e);
-        for (auto& e : c->seg_ev)
-            if (e) (void)hipEventDestroy(e);
-        if (c->side_done) (void)hipEventDestroy(c->side_done);
-        if (c->alt_start) (void)hipEventDestroy(c->alt_start);
-        for (hipStream_t s : {c->side, c->k2alt, c->rb})
-            if (s) {
-                (void)hipStreamSynchronize(s);
-                (void)hipStreamDestroy(s);
-            }
+        if (c->rb) {
+            (void)hipStreamSynchronize(c->rb);
+            (void)hipStreamDestroy(c->rb);
+        }
         if (c->own_stream) (void)hipStreamDestroy(c->stream);
     }
     delete c;
@@ -445,6 +427,7 @@ static void view_sync(gpudiff_dbatch* d) {
     d->compare_bytes = b->compare_bytes;
     d->value_bytes = b->value_bytes;
     d->size_hint_bytes = b->size_hint_bytes;
+    d->rows_gen = b->rows_gen;
 }
 
 // every per-pass output of a batch (a view has only these)
@@ -460,7 +443,7 @@ static int alloc_outputs(gpudiff_dbatch* d) {
         (rc = dalloc(&d->path_count, np)) || (rc = dalloc(&d->path_off, np + 1)) ||
         (rc = dalloc(&d->path_src, np)) || (rc = dalloc(&d->path_cnt, np)) || (rc = dalloc(&d->nbits, np)) ||
         (rc = dalloc(&d->noop_d, np)) ||
-        (rc = dalloc(&d->tile_sums, ntiles)) || (rc = dalloc(&d->seg_tot, kMaxSegments)) ||
+        (rc = dalloc(&d->tile_sums, ntiles)) ||
         (rc = dalloc(&d->tail_perm, 16384))) {
         d->chunk_counts = cc;
         return rc;
@@ -496,6 +479,7 @@ int gpudiff_dbatch_append(gpudiff_ctx* c, gpudiff_dbatch* d, const gpudiff_hbatc
     d->value_bytes += vb;
     d->pool_used += hb->pool_bytes;
     d->n_pairs = end;
+    d->rows_gen++;
     d->leaves += hb->leaves;
     return GPUDIFF_OK;
 }
@@ -507,6 +491,7 @@ int gpudiff_dbatch_reset(gpudiff_ctx* c, gpudiff_dbatch* d) {
     HIPCHK(hipStreamSynchronize(c->stream));
     d->pool_used = d->n_pairs = d->leaves = d->compare_bytes = d->value_bytes = d->size_hint_bytes = 0;
     d->ticket = 0;
+    d->rows_gen++;
     return GPUDIFF_OK;
 }
 
@@ -676,21 +661,6 @@ static int enqueue_join_emit(gpudiff_ctx* c, gpudiff_dbatch* d) {
     return GPUDIFF_OK;
 }
 
-// Segments of the diff pass.  K2 is HBM-bound and K3/K4 latency-bound, so a
-// large batch is cut into segments: K2 of segment s+1 streams on the main
-// stream while K3 (compaction) and K4 (merge-join) of segment s run on the
-// side stream; only the last segment's K3/K4 and the global K5/K6 are exposed.
-static uint32_t choose_segments(uint64_t n_pairs, uint32_t flags) {
-    const uint64_t nchunks = (n_pairs + 63) / 64;
-    const uint32_t forced = (flags >> GPUDIFF_OPT_SEGMENTS_SHIFT) & 0xFu;  // tests / tuning
-    if (forced) return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({forced, kMaxSegments, nchunks}));
-    // Measured (tools/ab_k2.py, config3 10M pairs): the overlapped K3/K4 take as
-    // much HBM/issue time from K2 as they hide at 5% dirty pairs, so one
-    // segment is the default; segmenting pays off when dirty pairs dominate.
-    (void)n_pairs;
-    return 1;
-}
-
 int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     if (!c || !d) return GPUDIFF_E_INVAL;
     int rc = set_device(c);
@@ -710,20 +680,15 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         if (!ev) return GPUDIFF_E_DEVICE;
     }
     hipStream_t ms = c->stream;
-    static_assert(kMaxSegments <= kK2TailCounters, "K2 item counters per segment");
-    const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);
-    const uint32_t S = choose_segments(d->n_pairs, c->flags);
-    // the summary (+ K2 item counters) is zeroed by the single K2 launch's reset kernel, else here: with
-    // segments, k2alt's first launch waits only for what precedes alt_start
-    const bool reset_in_k2 = d->n_pairs != 0 && S == 1;
-    if (ev) HIPCHK(hipEventRecord(ev[0], ms));
-    if (!reset_in_k2) HIPCHK(hipMemsetAsync(d->summary, 0, kSummaryWords * sizeof(uint32_t), ms));
     DiffBuffers b = buffers_of(c, d);
     uint4* total = (uint4*)d->summary;  // summary[0..3]: n_spec, n_status, n_dirty, scratch cap
+    if (ev) HIPCHK(hipEventRecord(ev[0], ms));
     if (d->n_pairs == 0) {
+        HIPCHK(hipMemsetAsync(d->summary, 0, kSummaryWords * sizeof(uint32_t), ms));
         HIPCHK(hipMemsetAsync(d->path_off, 0, sizeof(uint32_t), ms));
-    } else if (S == 1) {
-        HIPCHK(launch_compare(ms, b, 0, nchunks, 0, 1, true));
+    } else {
+        const uint32_t nchunks = (uint32_t)((d->n_pairs + 63) / 64);
+        HIPCHK(launch_compare(ms, b));  // zeroes the summary (+ K2's item counters) first
         if (ev) HIPCHK(hipEventRecord(ev[1], ms));
         HIPCHK(launch_compact(ms, b, 0, nchunks, nullptr, total));
         if (ev) HIPCHK(hipEventRecord(ev[2], ms));
@@ -731,44 +696,8 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
         if (ev) HIPCHK(hipEventRecord(ev[3], ms));
         HIPCHK(launch_emit(ms, b));
         if (ev) HIPCHK(hipEventRecord(ev[4], ms));
-    } else {
-        const uint32_t per = (nchunks + S - 1) / S;
-        uint32_t last = 0;
-        for (uint32_t s = 0; s < S && s * per < nchunks; s++) last = s;
-        // K2 segments alternate between the main stream and k2alt so a segment's
-        // waves fill the CUs while the previous segment's last waves drain
-        const bool alt = !(c->flags & GPUDIFF_OPT_NO_K2_ALT);
-        if (alt) {
-            HIPCHK(hipEventRecord(c->alt_start, ms));
-            HIPCHK(hipStreamWaitEvent(c->k2alt, c->alt_start, 0));
-        }
-        hipStream_t k2s = ms;
-        for (uint32_t s = 0; s <= last; s++) {
-            const uint32_t c0 = s * per, c1 = std::min(nchunks, c0 + per);
-            k2s = (alt && (s & 1)) ? c->k2alt : ms;
-            HIPCHK(launch_compare(k2s, b, c0, c1, s, last + 1, false));
-            HIPCHK(hipEventRecord(c->seg_ev[s], k2s));
-            HIPCHK(hipStreamWaitEvent(c->side, c->seg_ev[s], 0));
-            const uint4* before = s ? d->seg_tot + (s - 1) : nullptr;
-            uint4* after = s == last ? total : d->seg_tot + s;
-            HIPCHK(launch_compact(c->side, b, c0, c1, before, after));
-            HIPCHK(launch_join(c->side, b, c0, c1, before, after));
-        }
-        if (ev) {  // ev[1] after both K2 streams' last segments
-            if (alt && last > 0) HIPCHK(hipStreamWaitEvent(k2s, c->seg_ev[last - 1], 0));
-            HIPCHK(hipEventRecord(ev[1], k2s));
-            HIPCHK(hipEventRecord(ev[2], k2s));
-            HIPCHK(hipEventRecord(ev[3], c->side));
-        }
-        HIPCHK(hipEventRecord(c->side_done, c->side));
-        HIPCHK(hipStreamWaitEvent(ms, c->side_done, 0));
-        HIPCHK(launch_emit(ms, b));
-        if (ev) HIPCHK(hipEventRecord(ev[4], ms));
     }
-    if (ev) {
-        c->pass_k2_launches = S;
-        c->n_pass++;
-    }
+    if (ev) c->n_pass++;
     HIPCHK(hipEventRecord(d->done, c->stream));
     if (d->ticket) c->tickets.erase(d->ticket);
     d->ticket = c->next_ticket++;
@@ -802,7 +731,7 @@ int gpudiff_last_timings(gpudiff_ctx* c, gpudiff_timings* t) {
     if (!(c->flags & GPUDIFF_OPT_TIMING)) return GPUDIFF_E_STATE;
     HIPCHK(hipStreamSynchronize(c->stream));
     t->n_passes = (uint32_t)c->n_pass;
-    t->k2_launches = c->pass_k2_launches;
+    t->k2_launches = 1;
     if (!c->n_pass) return GPUDIFF_OK;
     double s[5] = {0, 0, 0, 0, 0};
     for (size_t i = 0; i < c->n_pass; i++) {

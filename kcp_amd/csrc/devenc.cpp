@@ -91,7 +91,7 @@ int gpudiff_encode_objects(gpudiff_ctx* c, const uint8_t* const* docs, const siz
     HIPCHK(hipMemsetAsync(dsp.p, 0xA5, cap, c->stream));  // poison: every blob byte must be written by K0
     HIPCHK(launch_encode_docs(c->stream, (const TokDoc*)dd.p, (uint32_t)n, (const uint8_t*)dj.p, (uint8_t*)ds.p,
                               (uint8_t*)dsp.p, cap, (unsigned long long*)du.p, c->hash_mask, (TokOut*)dout.p,
-                              nullptr, nullptr, (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
+                              nullptr, nullptr));
     std::vector<TokOut> to(n);
     uint64_t used = 0;
     HIPCHK(hipMemcpyAsync(to.data(), dout.p, n * sizeof(TokOut), hipMemcpyDeviceToHost, c->stream));

@@ -54,6 +54,10 @@ constexpr uint64_t kUpChunkBytes = 16ull << 20;
 // ... and of at least kMinChunkDocs documents: each chunk's K0 launch (a wave per document) should fill the
 // chip's ~8k resident waves twice over (r04m: 12 chunks of 5.4k documents made config5's K0 6.4 ms, from 4.1)
 constexpr uint64_t kMinChunkDocs = 16384;
+// store mode: the K0 stage on the kernel stream.  The decoupled form (K0 stage on its own stream; compaction,
+// Delete and the host resolution's placement ordered against it) measured within box noise on config 5
+// (profiles/r04zs) and stays compiled out until a measurement shows a gain
+constexpr bool kDecoupleStore = false;
 
 struct Ring {
     gpudiff_dbatch* d = nullptr;  // rows, pair_ids, results; pool = the store's current space
@@ -123,11 +127,9 @@ struct DStore {
     DSlot* slots = nullptr;
     uint32_t* ctr = nullptr;  // kCtrLive, kCtrLiveBytes
     hipStream_t cs = nullptr;  // H2D of the next batch overlaps K0 of the current one
-    hipStream_t cs2 = nullptr; // GPUDIFF_OPT_H2D_TWO_STREAMS: odd JSON chunks upload here (a second DMA queue)
-    hipEvent_t cs2_done = nullptr;
     // K0 of odd chunks runs on a second stream (its own half of the scratch), so one chunk's launch tail
     // overlaps the next chunk's start instead of idling the CUs between back-to-back launches on one stream
-    // (GPUDIFF_K0_ONE_STREAM=1, read once per store: all on the kernel stream, A/B tuning only)
+    // (interleaved A/B, profiles/r04ze: one K0 stream 7.44-7.51M pairs/s vs 7.90-8.37M)
     hipStream_t ks = nullptr;
     hipEvent_t ks_ev = nullptr;
     // pair mode with two K0 streams: the whole K0 stage (slot reset, K0 of even chunks, K0c, K0x) runs on ks0 and
@@ -135,14 +137,12 @@ struct DStore {
     // previous diff pass (its space) -- so a batch's K0 overlaps the previous batch's diff pass on the kernel stream
     hipStream_t ks0 = nullptr;
     int last_ring = -1;  // the ring slot of the previous submit
-    // store mode, GPUDIFF_K0_DECOUPLE_STORE=1 (opt-in): the K0 stage on ks0 there too; whatever the kernel stream
+    // store mode with kDecoupleStore (off): the K0 stage on ks0 there too; whatever the kernel stream
     // does to the slot table or the space between submits (compaction, Delete, the host resolution's placement)
     // first waits for the last K0 stage and sets st_slot_ops, and the next K0 stage then waits for the kernel stream
     bool dec_store = false;
     bool st_slot_ops = false;
     hipEvent_t st_ev = nullptr;
-    uint64_t up_chunk_bytes = kUpChunkBytes;
-    uint32_t up_max_chunks = kMaxUpChunks;
     uint64_t* sizes = nullptr;
     uint64_t* tile_sums = nullptr;
     uint8_t* scratch = nullptr;
@@ -552,6 +552,7 @@ int resolve(DStore* s, Ring& R, ResultStore& rs) {
     d->pool = s->space[s->cur];
     d->pool_cap = s->space_bytes;
     d->n_pairs = rows.size();
+    d->rows_gen++;
     gpudiff_ticket t2;
     if ((rc = gpudiff_diff(c, d, &t2))) return rc;
     ResultStore r2;
@@ -653,26 +654,18 @@ DStore* dstore_create(gpudiff_ctx* c, uint32_t max_slots, uint64_t space_bytes, 
             return fail(GPUDIFF_E_DEVICE);
     }
     if (hipStreamCreateWithFlags(&s->cs, hipStreamNonBlocking) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
-    // (GPUDIFF_K0_COUPLED=1, A/B tuning only: the pair-mode K0 stage stays on the kernel stream)
-    if (!getenv("GPUDIFF_K0_ONE_STREAM") &&
-        (hipStreamCreateWithFlags(&s->ks, hipStreamNonBlocking) != hipSuccess ||
-         hipEventCreateWithFlags(&s->ks_ev, hipEventDisableTiming) != hipSuccess ||
-         (!getenv("GPUDIFF_K0_COUPLED") && hipStreamCreateWithFlags(&s->ks0, hipStreamNonBlocking) != hipSuccess)))
+    // the pair-mode K0 stage on its own stream (interleaved A/B, profiles/r04zf: on the kernel stream 7.71-7.79M
+    // pairs/s staged vs 7.90-8.37M)
+    if (hipStreamCreateWithFlags(&s->ks, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ks_ev, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&s->ks0, hipStreamNonBlocking) != hipSuccess)
         return fail(GPUDIFF_E_DEVICE);
     for (Ring& R : s->ring)
         if (hipEventCreateWithFlags(&R.pass_done, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
-    if (s->ks0 && getenv("GPUDIFF_K0_DECOUPLE_STORE")) {
+    if (kDecoupleStore) {
         if (hipEventCreateWithFlags(&s->st_ev, hipEventDisableTiming) != hipSuccess) return fail(GPUDIFF_E_DEVICE);
         s->dec_store = true;
     }
-    if (const char* v = getenv("GPUDIFF_H2D_CHUNK_MIB"))
-        s->up_chunk_bytes = std::max<uint64_t>(1, strtoull(v, nullptr, 10)) << 20;
-    if (const char* v = getenv("GPUDIFF_H2D_MAX_CHUNKS"))
-        s->up_max_chunks = (uint32_t)std::min<unsigned long long>(kMaxUpChunks, std::max(1ull, strtoull(v, nullptr, 10)));
-    if ((c->flags & GPUDIFF_OPT_H2D_TWO_STREAMS) &&
-        (hipStreamCreateWithFlags(&s->cs2, hipStreamNonBlocking) != hipSuccess ||
-         hipEventCreateWithFlags(&s->cs2_done, hipEventDisableTiming) != hipSuccess))
-        return fail(GPUDIFF_E_DEVICE);
     if ((rc = gpudiff_dbatch_create(c, 16, 1024, &s->res_d))) return fail(rc);
     (void)hipFree(s->res_d->pool);
     s->res_d->pool = nullptr;
@@ -878,8 +871,8 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         return lo;
     };
     const uint32_t C = (uint32_t)std::min<uint64_t>(
-        std::min<uint64_t>(s->up_max_chunks, std::max<uint64_t>(1, nd / kMinChunkDocs)),
-        std::max<uint64_t>(1, jbytes / s->up_chunk_bytes));
+        std::min<uint64_t>(kMaxUpChunks, std::max<uint64_t>(1, nd / kMinChunkDocs)),
+        std::max<uint64_t>(1, jbytes / kUpChunkBytes));
     uint32_t cdoc[kMaxUpChunks + 1];
     for (uint32_t q = 0; q <= C; q++) cdoc[q] = q == C ? nd : first_doc(jbytes * q / C);
     auto cbyte = [&](uint32_t q) -> uint64_t { return q == C || cdoc[q] >= nd ? jbytes : docs[cdoc[q]].json_off; };
@@ -925,11 +918,6 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     // the upload runs on the copy stream, behind this ring slot's previous K0 (which read the
     // same device buffers), so it overlaps the other batch's K0 / diff pass
     if (R.k0_recorded) HIPCHK(hipStreamWaitEvent(cs, R.k0_done, 0));
-    hipStream_t cs2 = s->cs2 ? s->cs2 : cs;
-    if (s->cs2) {  // the second copy stream starts behind the same dependencies
-        HIPCHK(hipEventRecord(s->cs2_done, cs));
-        HIPCHK(hipStreamWaitEvent(cs2, s->cs2_done, 0));
-    }
     if (timing) HIPCHK(hipEventRecord(R.t_ev[0], cs));
     // the tables' used parts only (their device offsets are sized for 2n documents)
     HIPCHK(hipMemcpyAsync(R.dmeta, R.hmeta, (uint64_t)nd * sizeof(TokDoc), hipMemcpyHostToDevice, cs));
@@ -973,8 +961,8 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     auto upload = [&](uint32_t q) {
         const uint64_t b0 = cbyte(q), b1 = cbyte(q + 1);
         if (!zsrc && q + 1 == C && cdoc[q] >= nd) memset(R.hjson + b0, 0, b1 - b0);  // no documents: the slack only
-        hipStream_t qs = (q & 1u) ? cs2 : cs;
-        const bool odd = s->ks && (q & 1u);
+        hipStream_t qs = cs;  // one DMA queue saturates the link (two measured slower, profiles/r04z)
+        const bool odd = (q & 1u) != 0u;
         hipStream_t kq = odd ? s->ks : k0s;  // this chunk's K0 stream, and its half of the scratch
         uint8_t* scr = s->scratch + (odd ? scratch_half : 0);
         if (hipMemcpyAsync(R.djson + b0, hsrc + b0, b1 - b0, hipMemcpyHostToDevice, qs) != hipSuccess ||
@@ -986,8 +974,8 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         for (; li < launches.size() && chunk_of_launch[li] == q; li++) {
             const auto& L = launches[li];
             if (launch_encode_docs(kq, ddocs + L.first, L.second - L.first, R.djson, scr, space, s->space_bytes,
-                                   s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first,
-                                   (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u) != hipSuccess) {
+                                   s->used_dev, c->hash_mask, R.douts + L.first, s->slots, dlinks + L.first) !=
+                hipSuccess) {
                 up_err.store(1);
                 return;
             }
@@ -1022,10 +1010,6 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     });
     if (up_err.load()) return GPUDIFF_E_DEVICE;
     lap(2);
-    if (s->cs2) {  // staged = both copy streams done
-        HIPCHK(hipEventRecord(s->cs2_done, cs2));
-        HIPCHK(hipStreamWaitEvent(cs, s->cs2_done, 0));
-    }
     HIPCHK(hipEventRecord(R.staged, cs));
     if (timing) HIPCHK(hipEventRecord(R.t_ev[1], cs));
     if (li != launches.size()) return GPUDIFF_E_STATE;  // every launch belongs to an uploaded chunk
@@ -1050,6 +1034,7 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
     d->pool_cap = s->space_bytes;
     d->pool_used = s->used_ub;
     d->n_pairs = n;
+    d->rows_gen++;
     d->leaves = 0;
     d->compare_bytes = d->value_bytes = 0;
     d->size_hint_bytes = 2 * new_json_bytes;  // k2_sub_shift's size class (engine.h)
@@ -1257,11 +1242,6 @@ void dstore_free(gpudiff_ctx* c, DStore* s) {
             if (e) (void)hipEventDestroy(e);
     }
     if (s->res_d) gpudiff_dbatch_free(c, s->res_d);
-    if (s->cs2) {
-        (void)hipStreamSynchronize(s->cs2);
-        (void)hipStreamDestroy(s->cs2);
-    }
-    if (s->cs2_done) (void)hipEventDestroy(s->cs2_done);
     for (hipStream_t* k : {&s->ks, &s->ks0})
         if (*k) {
             (void)hipStreamSynchronize(*k);

@@ -40,7 +40,6 @@ struct Part {
 };
 }  // namespace gd
 
-inline constexpr uint32_t kMaxSegments = 8;
 // changed-path arena entries per K2 wave (a pair whose worst case does not
 // fit the wave's remaining arena is deferred to K4)
 inline constexpr uint32_t kArenaPerWave = 16384;
@@ -81,7 +80,6 @@ struct gpudiff_dbatch {
     uint32_t* path_count = nullptr;
     uint32_t* path_off = nullptr;
     uint32_t* tile_sums = nullptr;
-    uint4* seg_tot = nullptr;  // running totals after each diff segment
     uint32_t* path_src = nullptr;
     uint32_t* path_cnt = nullptr;
     uint8_t* nbits = nullptr;   // per pair: no-op bits of K2's joins
@@ -112,7 +110,8 @@ struct gpudiff_dbatch {
     const gpudiff_dbatch* base = nullptr;
     int device = -1;
     uint32_t* tail_perm = nullptr;  // K2's largest-first final round (kernels.h DiffBuffers)
-    uint64_t tail_perm_key = ~0ull;
+    gd::TailPermKey tail_perm_key;
+    uint64_t rows_gen = 0;  // bumped whenever the rows change (appends, resets, store batches): K2's cached order
 };
 
 struct DStore;
@@ -139,14 +138,7 @@ struct gpudiff_ctx {
     std::unordered_map<gpudiff_ticket, gpudiff_dbatch*> tickets;
     std::vector<std::array<hipEvent_t, 5>> pass_ev;
     size_t n_pass = 0;
-    uint32_t pass_k2_launches = 1;
-    // segmented diff pass: side stream for K3/K4, one event per segment
-    hipStream_t side = nullptr;
-    hipStream_t k2alt = nullptr;  // second K2 stream (odd segments)
     hipStream_t rb = nullptr;     // result readback (never behind work queued after the batch)
-    hipEvent_t seg_ev[kMaxSegments] = {};
-    hipEvent_t side_done = nullptr;
-    hipEvent_t alt_start = nullptr;
     // per-ticket completion hooks run by gpudiff_wait before results are
     // published (the device-encode store resolves its host-deferred events)
     std::unordered_map<gpudiff_ticket, std::function<int(ResultStore&)>> finishers;
@@ -185,7 +177,7 @@ inline void dfree_all(gpudiff_dbatch* d) {
     if (d->base) d->rows = nullptr, d->pair_ids = nullptr;  // a view's inputs are its base's
     void* ps[] = {d->rows, d->pair_ids, d->flags, d->caps, d->chunk_counts, d->summary, d->spec_ids,
                   d->status_ids, d->dirty_ids, d->dirty_idx, d->scratch_off, d->path_count, d->path_off,
-                  d->tile_sums, d->seg_tot, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
+                  d->tile_sums, d->path_src, d->path_cnt, d->arena_h, d->arena_k,
                   d->scratch_h, d->scratch_k, d->out_h, d->out_k, d->nbits, d->noop_d, d->slot_owner,
                   d->slice_cnt, d->slice_weq, d->ids_alt[0], d->ids_alt[1], d->summary_alt, d->tail_perm};
     for (void* p : ps)

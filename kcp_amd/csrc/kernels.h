@@ -49,24 +49,27 @@ struct DiffBuffers {
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
-    uint32_t k2_variant;        // tuning: 0 = by batch shape (k2_variant_of: 8 or 16 x 16-B chunks in flight per lane per object)
-    uint32_t k2_items_per_wave; // tuning: 0 = default; 64-pair chunks split until each resident wave has this many items
-    uint32_t k2_blocks_per_cu;  // tuning: 0 = the variant's occupancy (4 resident 256-thread blocks per CU)
-    uint32_t k2_tail_quarters;  // tuning: a tail of (this - 1) / 4 x the launch's waves chunks; 0 = default
-    uint32_t k2_tail8;          // tuning: tail items of 8 pairs instead of half a main item
+    uint32_t k2_timeline;       // GPUDIFF_OPT_K2_TIMELINE: the per-wave timeline build of K2 (profiling hook)
     uint32_t* tail_perm;        // K2's largest-first final round: its order (device, kK2LptMax u32)
-    uint64_t* tail_perm_key;    // (host) the launch shape tail_perm was computed for
-    uint32_t k2_no_lpt;         // tuning (GPUDIFF_OPT_K2_NO_LPT): the final round in index order
+    struct TailPermKey* tail_perm_key;  // (host) the rows and launch shape tail_perm was computed for
+    uint64_t rows_gen;          // bumped whenever the batch's rows change (appends, resets, store batches)
     uint64_t avg_pair_bytes;    // format bytes K2 reads per pair, averaged over the batch (0: unknown)
-    uint32_t k4_pipelined;      // tuning (GPUDIFF_OPT_K4_PIPELINED_JOIN): K4's slices with join_region_pl
     uint32_t* gather_send;      // gpudiff_dbatch_bind_gather: K3 also writes counts + IDs here (nullptr: unbound)
     uint32_t gather_cap_spec, gather_cap_status;
-    uint32_t k2_deep_mode;      // tuning (GPUDIFF_OPT_K2_DEEP_SHIFT): 0 defer joins over 2048 keys to K4's
-                                // slices, 1 keep every join in K2, 2 / 3 defer over 4096 / 8192
 };
 
-// summary[8 + seg]: K2's main item counter of segment seg; summary[8 + kK2TailCounters + seg]: its tail
-// item counter (zeroed with the pass)
+// the exact launch a cached largest-first order was computed for (kernels.hip launch_compare)
+struct TailPermKey {
+    const void* rows = nullptr;
+    uint64_t rows_gen = ~0ull;
+    uint32_t n_pairs = 0, lpt = 0, sub = 0, r2 = 0;
+    bool operator==(const TailPermKey& o) const {
+        return rows == o.rows && rows_gen == o.rows_gen && n_pairs == o.n_pairs && lpt == o.lpt && sub == o.sub &&
+               r2 == o.r2;
+    }
+};
+
+// summary[8]: K2's main item counter; summary[8 + kK2TailCounters]: its tail item counter (zeroed with the pass)
 constexpr uint32_t kK2TailCounters = 8, kSummaryWords = 8 + 2 * kK2TailCounters;
 // default tail: half a chunk per resident wave, in items of half a main item (in-process A/B on MI355X,
 // profiles/r02zj-r02zm: 8-pair tail items cost more than the imbalance they remove; with no tail at all
@@ -83,9 +86,8 @@ struct BlobMove {
     uint64_t src, dst, bytes;
 };
 hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, const BlobMove* moves, uint32_t n);
-// K2 (+ fused join) over the 64-pair chunks [c0, c1), batch segment seg of nsegs
-hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
-                          uint32_t nsegs, bool reset_summary);
+// K2 (+ fused join) over the whole batch; zeroes the pass's summary first
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b);
 // K3 over chunks [c0, c1): running (n_spec, n_status, n_dirty, cap) totals before -> after
 hipError_t launch_compact(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                           uint4* after);
@@ -95,8 +97,9 @@ hipError_t launch_slot_owners(hipStream_t s, const DiffBuffers& b);
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after);
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
-// tuning: K2 variant 14 writes 8 u64 per wave (start, first item end, items, last item start, end,
-// streaming ticks, join ticks, hw id) into dev_buf (cap_waves waves); nullptr disables
+// profiling hook: the GPUDIFF_OPT_K2_TIMELINE build of K2 writes 12 u64 per wave (start, first item end, items,
+// last item start, end, streaming ticks, join ticks, hw id, rows, pre, post, ticket ticks) into dev_buf
+// (cap_waves waves); nullptr disables
 hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves);
 
 }  // namespace gd

@@ -40,13 +40,7 @@ constexpr uint32_t ARENA_BIT = 0x80000000u;  // scratch_off[d]: paths live in th
 // K4 merge-path slices (k_join_slices below)
 constexpr uint32_t kJoinSlice = 1024;  // merged keys per slice (<= 16 windows of 64 + 64)
 constexpr uint32_t kDeepJoin = 2048;   // K2 defers a dirty pair whose join covers more keys
-// the deep-join bound of a K2 launch (sub_arg bits 18-19 = GPUDIFF_OPT_K2_DEEP_SHIFT's field: 0 the
-// default, 1 none -- every join the wave arena holds stays in K2 --, 2 and 3: 2x and 4x the default)
 constexpr uint32_t kTailJoinMax = 1024;  // K2's largest-first rounds: joins over this many keys go to K4's slices
-__device__ __forceinline__ uint32_t deep_join_max(uint32_t sub_arg) {
-    const uint32_t m = (sub_arg >> 18) & 3u;
-    return m == 1u ? ~0u : kDeepJoin << (m ? m - 1u : 0u);
-}
 
 // Scratch entries of a deferred pair.  need = the merged keys of each joined region + the status-absent
 // sentinel (when the pair has one) bounds its paths.  A pair with need <= kJoinSlice -- one K2 deferred
@@ -123,74 +117,6 @@ __device__ __forceinline__ bool neq16(const u32x4& a, const u32x4& b) {
     const u32x4 x = a ^ b;
     return (x.x | x.y | x.z | x.w) != 0u;
 }
-
-// ---------------------------------------------------------------- K2
-struct PairDecision {
-    uint32_t flag;
-    uint32_t cap;
-};
-
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
-    if (NT) return __builtin_nontemporal_load(p);
-    return *p;
-}
-
-template <bool NT, int U>
-__device__ __forceinline__ PairDecision compare_pair(const gpudiff_pair_row& r, const uint8_t* __restrict__ pool,
-                                                     uint32_t lane) {
-    PairDecision d{0u, 0u};
-    if ((r.flags_a | r.flags_b) & GPUDIFF_OBJ_DECODE_ERR) {
-        d.flag = F_SPEC | F_STATUS | F_ERR;
-        return d;
-    }
-    const bool spec_sz = r.spec_l_a == r.spec_l_b && r.spec_ar_a == r.spec_ar_b;
-    const bool has_st_b = (r.flags_b & GPUDIFF_OBJ_HAS_STATUS) != 0u;
-    const bool stat_sz = has_st_b && r.stat_l_a == r.stat_l_b && r.stat_ar_a == r.stat_ar_b;
-    const uint64_t seg_a = seg_bytes(r.spec_l_a, r.spec_ar_a);
-    const uint64_t seg_b = seg_bytes(r.spec_l_b, r.spec_ar_b);
-    const uint32_t n1 = spec_sz ? (uint32_t)(seg_a >> 4) : 0u;
-    const uint32_t n2 = stat_sz ? (uint32_t)(seg_bytes(r.stat_l_a, r.stat_ar_a) >> 4) : 0u;
-    const u32x4* a1 = (const u32x4*)(pool + r.off_a);
-    const u32x4* b1 = (const u32x4*)(pool + r.off_b);
-    const u32x4* a2 = (const u32x4*)(pool + r.off_a + seg_a);
-    const u32x4* b2 = (const u32x4*)(pool + r.off_b + seg_b);
-    const uint32_t ntot = n1 + n2;
-    bool mis1 = false, mis2 = false;
-    for (uint32_t base = 0; base < ntot; base += 64 * U) {
-        u32x4 va[U], vb[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t i = base + u * 64 + lane;
-            if (i < ntot) {
-                const bool in1 = i < n1;
-                const u32x4* pa = in1 ? a1 + i : a2 + (i - n1);
-                const u32x4* pb = in1 ? b1 + i : b2 + (i - n1);
-                va[u] = ld16<NT>(pa);
-                vb[u] = ld16<NT>(pb);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t i = base + u * 64 + lane;
-            if (i < ntot) {
-                const bool ne = neq16(va[u], vb[u]);
-                if (i < n1) mis1 |= ne;
-                else mis2 |= ne;
-            }
-        }
-    }
-    const bool spec_dirty = !spec_sz || ballot(mis1) != 0;
-    const bool stat_dirty = !stat_sz || ballot(mis2) != 0;
-    const bool stat_join = stat_dirty && (r.stat_l_a + r.stat_l_b) != 0u;
-    d.flag = (spec_dirty ? F_SPEC | F_JSPEC : 0u) | (stat_dirty ? F_STATUS : 0u) | (stat_join ? F_JSTAT : 0u) |
-             (stat_dirty && !has_st_b ? F_SENT : 0u) |
-             (((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu) ? F_SEED : 0u);
-    d.cap = (spec_dirty ? r.spec_l_a + r.spec_l_b : 0u) +
-            (stat_dirty ? r.stat_l_a + r.stat_l_b + (has_st_b ? 0u : 1u) : 0u);
-    return d;
-}
-
 
 // ---------------------------------------------------------------- scans
 // Reduce-then-scan over u32 or 4 x u32 elements in tiles of 4096 (256 threads
@@ -476,113 +402,6 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
     return outpos;
 }
 
-// One side's 64-key window of the pipelined merge-join: lane l holds entry start + l's key and meta
-// (zeros past the region).
-struct JWin {
-    uint32_t k, m;
-};
-__device__ __forceinline__ JWin jwin_load(const RegionView& R, uint32_t start, uint32_t lane) {
-    JWin w = {0u, 0u};
-    if (start + lane < R.L) {
-        w.k = R.keys[start + lane];
-        w.m = R.metas[start + lane];
-    }
-    return w;
-}
-// the window c entries later, from the current window and the prefetched next one: lane l < 64 - c
-// takes cur[l + c], the others pre[l + c - 64] -- a source lane s offers cur[s] when s >= c and pre[s]
-// otherwise, and everything rotates left by c (one bpermute per value)
-__device__ __forceinline__ JWin jwin_shift(const JWin& cur, const JWin& pre, uint32_t c, uint32_t lane) {
-    const bool own = lane >= c;
-    const uint32_t src = (lane + c) & 63u;
-    JWin w;
-    w.k = shfl32(own ? cur.k : pre.k, src);
-    w.m = shfl32(own ? cur.m : pre.m, src);
-    return w;
-}
-
-// join_region, software-pipelined: each side keeps its current 64-entry window of keys and metas and
-// the next 64 in registers; once a window is resolved the current one moves forward by the entries
-// consumed (a register rotate) and the following 64 are loaded, so those loads fly while the next
-// window is resolved (and its tails confirmed) instead of opening every window with a dependent HBM
-// round trip.  The values (first 8 bytes) are loaded per window as it opens: they are needed only
-// after the binary searches.  Same results as join_region.  A tuning variant of K4's slices
-// (GPUDIFF_OPT_K4_PIPELINED_JOIN): it measured slower than join_region there (profiles/r03m) and no
-// faster inside K2 (profiles/r03j) -- a window is bound by its instructions (cross-lane searches,
-// scans, the tail confirmation), not by the key loads it would hide.
-template <bool EMIT>
-__device__ uint32_t join_region_pl(const RegionView& A, const RegionView& B, uint8_t region_bit,
-                                   uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
-                                   uint32_t lane, bool* weq_all) {
-    uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
-    bool weq = true;
-    const uint64_t lt = mask_lt(lane);
-    JWin curA = jwin_load(A, 0u, lane), curB = jwin_load(B, 0u, lane);
-    JWin preA = jwin_load(A, 64u, lane), preB = jwin_load(B, 64u, lane);
-    while (ia < A.L || ib < B.L) {
-        const uint32_t na = min(64u, A.L - ia), nb = min(64u, B.L - ib);
-        const bool va = lane < na, vb = lane < nb;
-        const uint64_t xa = va ? A.vals[ia + lane] : 0ull;
-        const uint64_t xb = vb ? B.vals[ib + lane] : 0ull;
-        const uint32_t ka = curA.k, kb = curB.k, ma = curA.m, mb = curB.m;  // zeros past the regions
-        const bool endA = ia + na == A.L, endB = ib + nb == B.L;
-        const uint32_t lastA = na ? shfl32(ka, na - 1) : 0u;
-        const uint32_t lastB = nb ? shfl32(kb, nb - 1) : 0u;
-        bool inf = true;
-        uint32_t bound = 0;
-        if (!endA) { bound = lastA; inf = false; }
-        if (!endB) { bound = inf ? lastB : min(bound, lastB); inf = false; }
-        const bool inA = va && (inf || ka <= bound);
-        const bool inB = vb && (inf || kb <= bound);
-        const uint32_t asA = va ? meta_arena(ma) : 0u, asB = vb ? meta_arena(mb) : 0u;
-        const uint32_t incA = wave_incl_scan(asA), incB = wave_incl_scan(asB);
-        const uint32_t offA = arA + incA - asA, offB = arB + incB - asB;
-        const uint32_t jA = tile_lower_bound(ka, kb, nb);
-        const uint32_t kbj = shfl32(kb, min(jA, 63u));
-        const uint32_t mbj = shfl32(mb, min(jA, 63u));
-        const uint32_t obj = shfl32(offB, min(jA, 63u));
-        const uint32_t iB = tile_lower_bound(kb, ka, na);
-        const uint32_t kai = shfl32(ka, min(iB, 63u));
-        const uint64_t xbj = shfl64(xb, min(jA, 63u));
-        const bool matchA = inA && jA < nb && kbj == ka;
-        bool differ = matchA && (ma != mbj || xa != xbj);
-        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
-        const bool matchB = inB && iB < na && kai == kb;
-        const bool emitA = inA && (!matchA || differ);
-        const bool emitB = inB && !matchB;
-        const uint64_t balA = ballot(emitA), balB = ballot(emitB);
-        if (ballot((emitA && !(matchA && wire_equal_number(ma, xa, mbj, xbj))) || emitB)) weq = false;
-        if (EMIT) {
-            if (emitA) {
-                const uint32_t pos = popc64(balA & lt) + popc64(balB & mask_lt(jA));
-                out_h[out_base + outpos + pos] = ka;
-                out_k[out_base + outpos + pos] = region_bit | (matchA ? GPUDIFF_PATH_CHANGED : GPUDIFF_PATH_REMOVED);
-            }
-            if (emitB) {
-                const uint32_t pos = popc64(balB & lt) + popc64(balA & mask_lt(iB));
-                out_h[out_base + outpos + pos] = kb;
-                out_k[out_base + outpos + pos] = region_bit | GPUDIFF_PATH_ADDED;
-            }
-        }
-        outpos += popc64(balA) + popc64(balB);
-        const uint32_t ca = popc64(ballot(inA)), cb = popc64(ballot(inB));
-        arA += ca ? shfl32(incA, ca - 1) : 0u;
-        arB += cb ? shfl32(incB, cb - 1) : 0u;
-        ia += ca;
-        ib += cb;
-        if (ca) {
-            curA = jwin_shift(curA, preA, ca, lane);
-            preA = jwin_load(A, ia + 64u, lane);
-        }
-        if (cb) {
-            curB = jwin_shift(curB, preB, cb, lane);
-            preB = jwin_load(B, ib + 64u, lane);
-        }
-    }
-    *weq_all = weq;
-    return outpos;
-}
-
 __device__ uint64_t status_sentinel_hash(uint32_t seed, uint64_t mask) {
     // XXH64 of the 11 path bytes 01 06 00 00 00 's' 't' 'a' 't' 'u' 's'
     // bytes: [0]=01 [1]=06 [2..4]=00 [5]='s' [6]='t' [7]='a' | [8]='t' [9]='u' [10]='s'
@@ -838,7 +657,6 @@ __device__ uint32_t arena_prefix(const uint32_t* __restrict__ metas, uint32_t n,
 }
 
 // one slice [dg0, dg1) of a region's merge path, joined into out[base ...]; returns the paths written
-template <bool PL>
 __device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_t dg0, uint32_t dg1,
                                uint8_t region_bit, uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k,
                                uint32_t base, uint32_t lane, bool* weq) {
@@ -859,15 +677,11 @@ __device__ uint32_t join_slice(const RegionView& A, const RegionView& B, uint32_
     Bs.metas += ib0;
     Bs.arena += arena_prefix(B.metas, ib0, lane);
     Bs.L = ib1 > ib0 ? ib1 - ib0 : 0u;
-    return PL ? join_region_pl<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq)
-              : join_region<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq);
+    return join_region<true>(As, Bs, region_bit, out_h, out_k, base, lane, weq);
 }
 
-// K4a (join_region by default; PL, GPUDIFF_OPT_K4_PIPELINED_JOIN: the software-pipelined join_region_pl,
-// measured 15% slower on config4's slices, profiles/r03m)
-// wave per scratch slot starting in [before.w, after.w) (this segment's deferred pairs: place_deferred);
+// K4a: wave per scratch slot starting in [before.w, after.w) (this segment's deferred pairs: place_deferred);
 // writes each slice's path count and whether all its paths are wire-equal number changes
-template <bool PL>
 __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __restrict__ rows,
                                                      const uint8_t* __restrict__ pool, const uint8_t* __restrict__ flags,
                                                      const uint32_t* __restrict__ dirty_idx,
@@ -904,12 +718,12 @@ __global__ __launch_bounds__(256) void k_join_slices(const gpudiff_pair_row* __r
             const RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
             const RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
             const uint32_t dg0 = i * kJoinSlice;
-            cnt = join_slice<PL>(A, B, dg0, min(dg0 + kJoinSlice, Ls), 0, sh, sk, so + i * kJoinSlice, lane, &weq);
+            cnt = join_slice(A, B, dg0, min(dg0 + kJoinSlice, Ls), 0, sh, sk, so + i * kJoinSlice, lane, &weq);
         } else if (i - nsl < ntl) {
             const RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
             const RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
             const uint32_t dg0 = (i - nsl) * kJoinSlice;
-            cnt = join_slice<PL>(A, B, dg0, min(dg0 + kJoinSlice, Lt), GPUDIFF_PATH_REGION_STATUS, sh, sk,
+            cnt = join_slice(A, B, dg0, min(dg0 + kJoinSlice, Lt), GPUDIFF_PATH_REGION_STATUS, sh, sk,
                              so + i * kJoinSlice, lane, &weq);
         }
         if (lane == 0) {
@@ -994,115 +808,9 @@ __global__ __launch_bounds__(256) void k_join_gather(const gpudiff_pair_row* __r
     }
 }
 
-// ---------------------------------------------------------------- K2 (+ fused K4)
-// One wave per chunk of 64 consecutive pairs; the wave walks its pairs in
-// order, all 64 lanes streaming both objects of a pair with 16-byte loads
-// (NT: non-temporal; U: 16-B chunks in flight per lane per object).  A dirty
-// pair is merge-joined right away by the same wave while its bytes are hot in
-// the XCD's L2, its changed paths appended to this wave's private arena (no
-// atomics, no second HBM read of dirty pairs); a pair whose worst case does
-// not fit the arena's remaining space is flagged F_DEFER for K4.
-template <bool NT, int U, int MINB>
-__global__ __launch_bounds__(256, MINB) void k_compare(const gpudiff_pair_row* __restrict__ rows,
-                                                 const uint8_t* __restrict__ pool, uint32_t n,
-                                                 uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
-                                                 uint4* __restrict__ chunk_counts, uint32_t c_begin,
-                                                 uint32_t c_end, uint64_t* __restrict__ ah, uint8_t* __restrict__ ak,
-                                                 uint32_t arena_off, uint32_t arena_per_wave, uint32_t arena_stride,
-                                                 uint32_t* __restrict__ path_src, uint32_t* __restrict__ path_cnt,
-                                                 uint8_t* __restrict__ nbits, uint64_t mask,
-                                                 uint32_t* __restrict__ summary, uint32_t sub_arg,
-                                                 const uint32_t* __restrict__ tail_perm) {
-    (void)tail_perm;
-    const uint32_t lane = lane_id();
-    const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    const uint32_t sub_shift = sub_arg & 0xFFu;
-    const uint32_t deep_max = deep_join_max(sub_arg);  // joins over this many keys go to K4's slices
-    const uint32_t wbase = arena_off + wave * arena_stride;
-    uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
-    bool deferred = false;
-    const uint64_t sent0 = status_sentinel_hash(0, mask);
-    // work item = 1/2^sub_shift of a 64-pair chunk: small batches of large pairs spread over
-    // the whole grid; items of one chunk add their counts into chunk_counts atomically
-    const uint32_t per = 64u >> sub_shift;
-    const uint32_t nitems = (c_end - c_begin) << sub_shift;
-    for (uint32_t it = wave; it < nitems; it += nwaves) {
-        const uint32_t c = c_begin + (it >> sub_shift);
-        const uint32_t p0 = (c << 6) + (it & ((1u << sub_shift) - 1u)) * per;
-        if (p0 >= n) continue;
-        const uint32_t cnt = min(per, n - p0);
-        uint32_t myflag = 0, mycap = 0, mysrc = 0, mycnt = 0, mynoop = 0;
-        for (uint32_t k = 0; k < cnt; k++) {
-            const gpudiff_pair_row r = rows[p0 + k];
-            PairDecision d = compare_pair<NT, U>(r, pool, lane);
-            uint32_t src = 0, pc = 0, nb = 0;
-            if (d.flag & (F_SPEC | F_STATUS)) {
-                if (used + d.cap <= arena_per_wave && d.cap <= deep_max) {
-                    src = wbase + used;
-                    if (d.flag & (F_JSPEC | F_JSTAT)) {
-                        pc = join_pair<true>(r, d.flag, pool, mask, ah, ak, src, lane, &nb);
-                    } else if (d.flag & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
-                        nb = sentinel_noop_bits(r.flags_a);
-                        if (lane == 0) {
-                            ah[src] = (d.flag & F_SEED)
-                                          ? status_sentinel_hash((r.flags_a >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
-                                          : sent0;
-                            ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
-                        }
-                        pc = 1;
-                    }
-                    used += pc;
-                    d.cap = 0;  // no K4 scratch slot needed
-                } else {
-                    d.flag |= F_DEFER;
-                    d.cap = defer_cap(r.spec_l_a, r.spec_l_b, r.stat_l_a, r.stat_l_b, d.flag);
-                    deferred = true;
-                }
-            }
-            if (lane == k) {
-                myflag = d.flag;
-                mycap = d.cap;
-                mysrc = src;
-                mycnt = pc;
-                mynoop = nb;
-            }
-        }
-        const bool dirty = (myflag & (F_SPEC | F_STATUS)) != 0u;
-        if (lane < cnt) {
-            flags[p0 + lane] = (uint8_t)myflag;
-            if (dirty) {
-                caps[p0 + lane] = mycap;
-                path_src[p0 + lane] = mysrc;
-                path_cnt[p0 + lane] = mycnt;
-                nbits[p0 + lane] = (uint8_t)mynoop;
-            }
-        }
-        const uint32_t ns = popc64(ballot(myflag & F_SPEC));
-        const uint32_t nt = popc64(ballot(myflag & F_STATUS));
-        const uint32_t nd = popc64(ballot(dirty));
-        const uint32_t cs = wave_sum(dirty ? mycap : 0u);
-        if (lane == 0) {
-            if (!sub_shift) {
-                chunk_counts[c] = make_uint4(ns, nt, nd, cs);
-            } else if (ns | nt | nd | cs) {
-                uint32_t* cc = (uint32_t*)(chunk_counts + c);
-                atomicAdd(cc + 0, ns);
-                atomicAdd(cc + 1, nt);
-                atomicAdd(cc + 2, nd);
-                atomicAdd(cc + 3, cs);
-            }
-        }
-    }
-    // one plain store per wave (a same-address atomic per deferred pair
-    // serialises across the XCDs)
-    if (deferred && lane == 0) summary[6] = 1u;
-}
-
 // ---------------------------------------------------------------- K2, flattened stream
-// DYN variants: chunks at the end of a launch handed out as 8-pair items (about
-// four per wave), unless the whole launch is split already
-// a tail of q quarters of the launch's wave count, in 64-pair chunks
+// the chunks at the end of a launch handed out as smaller items (half a main item, at least 8 pairs), unless
+// the whole launch is split already: a tail of q quarters of the launch's wave count, in 64-pair chunks
 // items of the largest-first final round: one per resident wave, at most half the launch's main items
 __host__ __device__ inline uint32_t k2_lpt_round(uint32_t n_full, uint32_t nwaves, uint32_t rounds) {
     const uint32_t want = rounds * nwaves;
@@ -1115,11 +823,6 @@ __host__ __device__ inline uint32_t k2_item_round(uint32_t n_main, uint32_t nwav
 __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves, uint32_t sub_shift, uint32_t q) {
     return sub_shift >= 3u ? 0u : min(nch, nwaves / 4u * q);
 }
-// the tail quarters a launch uses (GPUDIFF_OPT_K2_TAIL_SHIFT: 0 = default, else t - 1)
-static inline uint32_t k2_tail_q(const DiffBuffers& b) {
-    return b.k2_tail_quarters ? b.k2_tail_quarters - 1u : kK2TailQuarters;
-}
-
 // One wave per work item of P = 64 >> sub_shift consecutive pairs.  Lane k
 // loads pair k's 64-B row with four coalesced 16-B loads (one 4 KiB read per
 // item instead of a scalar row load per pair).  The item's compared segments
@@ -1131,28 +834,20 @@ static inline uint32_t k2_tail_q(const DiffBuffers& b) {
 // average ~200 chunks a side: a wave-per-pair pass leaves 1/5 of its loads
 // unused and pays a row + data latency per pair).  A mismatching chunk marks
 // its pair (spec or status region); then the wave merge-joins its dirty pairs
-// one at a time into its arena, exactly as k_compare does (same flags, caps,
-// arena order and F_DEFER rule).
-// DYN: after its first item a wave takes the next one from a per-launch counter
-// (summary[8 + segment], zeroed with the pass), fetched while it streams the
+// one at a time into its arena (flags, caps, arena order and the F_DEFER rule:
+// DESIGN.md §5).
+// After its first item a wave takes the next one from a per-launch counter
+// (summary[8], zeroed with the pass), fetched while it streams the
 // current item, so the launch ends when the work does, not when the wave with
 // the heaviest static share of items does; the last k2_tail_chunks() chunks are
 // handed out as 8-pair items, so the final round of items is short too.
-// K2 per-wave timeline (tuning variant 14 only, tools/k2_wave_profile.py): 8 u64 per wave --
+// K2 per-wave timeline (PROF: the GPUDIFF_OPT_K2_TIMELINE build only, tools/k2_wave_profile.py): 12 u64 per wave --
 // start, end of the first item, items, start of the last item, end, streaming ticks, join ticks,
 // hardware id (wall clock: 100 MHz)
 __device__ uint64_t* g_k2_prof;
 __device__ uint32_t g_k2_prof_cap;
 
-// RPF (with DYN): the next main item's 64 rows are fetched into LDS by direct-to-LDS loads
-// (global_load_lds_dwordx4: no VGPRs held) as soon as its ticket is known -- after the current
-// item's first streaming pass -- so an item no longer starts with a dependent HBM round trip for
-// its rows (under a saturated memory system that round trip costs several microseconds: a
-// config4 pair's single-pair item spent ~14% of its time outside streaming and joining,
-// profiles/r03g/wave_c4.json). One 4 KiB buffer per wave suffices: an item's rows are read from it
-// before its first loads issue (their addresses depend on them), and the next prefetch into it is
-// issued only after that first pass.
-template <int U, int MINB, bool DYN = false, bool PROF = false, bool RPF = false>
+template <int U, int MINB, bool PROF = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -1167,72 +862,28 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     const uint32_t lane = lane_id();
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    // (launch_compare packs: sub_shift | tail quarters << 8 | late fetch << 16)
+    // (launch_compare packs: sub_shift | tail quarters << 8 | largest-first rounds << 20 | item round << 22)
     const uint32_t sub_shift = sub_arg & 0xFFu, tail_q = (sub_arg >> 8) & 0xFFu;
-    const bool late = (sub_arg >> 16) & 1u;
-    const uint32_t deep_max = deep_join_max(sub_arg);  // joins over this many keys go to K4's slices
-    const uint32_t tail_ish = ((sub_arg >> 17) & 1u) ? 3u : min(sub_shift + 1u, 3u);  // tail items: half or 8 pairs
+    const uint32_t tail_ish = min(sub_shift + 1u, 3u);  // tail items: half a main item, at least 8 pairs
     const uint32_t wbase = arena_off + wave * arena_stride;
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
-    typedef __attribute__((address_space(3))) void* lds_ptr;
-    __shared__ u32x4 rowbuf[RPF ? 4 * 4 * 64 : 1];  // [wave in block][16-B piece][lane]
-    const uint32_t wv = threadIdx.x >> 6;
-    uint32_t pf_item = ~0u;     // the item whose rows are in this wave's rowbuf (wave-uniform)
-    // RPF: an item's result stores are issued after the next item's rows are read, so no item waits for
-    // the previous item's stores to complete (gfx9 counts stores in vmcnt, and both the ticket read and
-    // the LDS read of prefetched rows wait on vmcnt): per lane its flag, cap, path source / count,
-    // no-op bits and seed; per wave the item's first pair, size, 64-pair chunk, split shift and counts
-    uint32_t q_flag = 0, q_cap = 0, q_src = 0, q_cnt = 0, q_noop = 0, q_seed = 0;
-    uint32_t q_p0 = 0, q_n = 0, q_c = 0, q_ish = 0, q_ns = 0, q_nt = 0, q_nd = 0, q_cs = 0;
-    bool q_pending = false;
-    auto flush = [&]() {
-        if (!q_pending) return;
-        q_pending = false;
-        const bool dirty = (q_flag & (F_SPEC | F_STATUS)) != 0u;
-        if (lane < q_n) {
-            flags[q_p0 + lane] = (uint8_t)q_flag;
-            if (dirty) {
-                caps[q_p0 + lane] = q_cap;
-                path_src[q_p0 + lane] = q_src;
-                path_cnt[q_p0 + lane] = q_cnt;
-                nbits[q_p0 + lane] = (uint8_t)q_noop;
-                // a status-absent-only pair's one path (the sentinel), written lane-parallel here
-                if ((q_flag & F_SENT) && !(q_flag & (F_JSPEC | F_JSTAT | F_DEFER))) {
-                    ah[q_src] = (q_flag & F_SEED) ? status_sentinel_hash(q_seed, mask) : sent0;
-                    ak[q_src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
-                }
-            }
-        }
-        if (lane == 0) {
-            if (!q_ish) {
-                chunk_counts[q_c] = make_uint4(q_ns, q_nt, q_nd, q_cs);
-            } else if (q_ns | q_nt | q_nd | q_cs) {
-                uint32_t* cc = (uint32_t*)(chunk_counts + q_c);
-                atomicAdd(cc + 0, q_ns);
-                atomicAdd(cc + 1, q_nt);
-                atomicAdd(cc + 2, q_nd);
-                atomicAdd(cc + 3, q_cs);
-            }
-        }
-    };
     [[maybe_unused]] uint64_t tp_start = 0, tp_first = 0, tp_last = 0, tp_stream = 0, tp_join = 0, tp_items = 0;
     [[maybe_unused]] uint64_t tp_rows = 0, tp_pre = 0, tp_post = 0, tp_adv = 0, tp_e = 0, tp_r = 0, tp_je = 0;
     if constexpr (PROF) tp_start = wall_clock64();
     const uint32_t nch = c_end - c_begin;
-    const uint32_t tail_c = DYN ? k2_tail_chunks(nch, nwaves, sub_shift, tail_q) : 0u;
+    const uint32_t tail_c = k2_tail_chunks(nch, nwaves, sub_shift, tail_q);
     const uint32_t n_full = (nch - tail_c) << sub_shift;  // items of 64 >> sub_shift pairs, then 8-pair items
     // largest-first final round (k2_lpt_round; large pairs): the pairs of the last lpt_r main items are handed
     // out one pair an item by the tail counter in tail_perm's order -- by descending bytes -- so the launch ends
     // with its smallest pairs; the bulk stays in index order (neighbouring waves stream neighbouring pool bytes)
     const uint32_t lpt_rounds = (sub_arg >> 20) & 3u;  // launch_compare: 0 when the round is off
-    const uint32_t lpt_r = (DYN && !RPF && tail_perm && tail_c == 0u && lpt_rounds) ? k2_lpt_round(n_full, nwaves, lpt_rounds) : 0u;
+    const uint32_t lpt_r = (tail_perm && tail_c == 0u && lpt_rounds) ? k2_lpt_round(n_full, nwaves, lpt_rounds) : 0u;
     const uint32_t n_main = n_full - lpt_r;
     // ... and the round before it in whole items, also largest first (sub_arg bit 22): its biggest items then start
     // a round earlier instead of running past the pair round's end
     const uint32_t r2 = (lpt_r && ((sub_arg >> 22) & 1u)) ? k2_item_round(n_main, nwaves) : 0u;
-    const bool tail_defer = (sub_arg >> 23) & 1u;
     const uint32_t n_main2 = n_main - r2;
     const uint32_t lpt_pairs = lpt_r << (6u - sub_shift);
     const uint32_t lpt_p0 = ((c_begin + (n_main >> sub_shift)) << 6) + (n_main & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
@@ -1245,36 +896,25 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     uint32_t* const ctr = summary + 8u + (arena_per_wave ? arena_off / arena_per_wave : 0u);
     uint32_t* const ctr_tail = ctr + kK2TailCounters;
     const uint32_t tail0 = max(n_main, nwaves);  // the first item the tail counter hands out
-    // late fetch: the last two rounds of main items take their next ticket when they are done, so
-    // no ticket waits behind a long item at the end of the pass (the others prefetch as they start)
-    const uint32_t pf_end = late ? (n_main > 2u * nwaves ? n_main - 2u * nwaves : 0u) : n_main;
     auto advance = [&](uint32_t cur, uint32_t tk) -> uint32_t {
-        if constexpr (!DYN) {
-            return cur + nwaves;
-        } else {
-            if (cur < n_main) {
-                if (cur >= pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
-                const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
-                if (nx < n_main) return nx;
-            }
-            uint32_t tt = 0;
-            if (lane == 0) tt = atomicAdd(ctr_tail, 1u);
-            return tail0 + uni(__builtin_amdgcn_readlane(tt, 0));
+        if (cur < n_main) {
+            const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
+            if (nx < n_main) return nx;
         }
+        uint32_t tt = 0;
+        if (lane == 0) tt = atomicAdd(ctr_tail, 1u);
+        return tail0 + uni(__builtin_amdgcn_readlane(tt, 0));
     };
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
         // the item this ticket stands for: in the largest-first round, one pair (the permuted order)
         const bool lpt = lpt_r && it >= n_main;
         // the largest-first rounds' dirty pairs join only up to kTailJoinMax keys here (bigger ones go to K4's
         // slices, spread over the whole grid): a deep join late in the launch would run past everyone's end
-        const bool tail_round = tail_defer && lpt_r && it >= n_main2;
+        const bool tail_round = lpt_r && it >= n_main2;
         const uint32_t im = lpt ? 0u : (r2 && it >= n_main2) ? n_main2 + tail_perm[lpt_pairs + (it - n_main2)] : it;
         const bool tail = !lpt && im >= n_full;
-        // the next main ticket: fetched while this item streams (with RPF only after this item's rows are
-        // read from LDS -- the LDS read waits on vmcnt, which would otherwise wait for the atomic's return)
-        if constexpr (DYN && !RPF) {
-            if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
-        }
+        // the next main ticket: fetched while this item streams
+        if (it < n_main && lane == 0) tk = atomicAdd(ctr, 1u);
         [[maybe_unused]] uint64_t tp_i = 0;
         if constexpr (PROF) {
             tp_i = wall_clock64();
@@ -1288,36 +928,18 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t c = lpt ? lp >> 6 : c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
         const uint32_t per = 64u >> ish;
         const uint32_t p0 = lpt ? lp : (c << 6) + (j & ((1u << ish) - 1u)) * per;
-        if (p0 >= n) {
-            if constexpr (DYN && RPF) {
-                if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
-            }
-            continue;
-        }
+        if (p0 >= n) continue;
         const uint32_t cnt = min(per, n - p0);
         const bool valid = lane < cnt;
         // ---- rows: lane k holds pair p0 + k
         u32x4 v0 = {0, 0, 0, 0}, v1 = v0, v2 = v0, v3 = v0;
-        if (RPF && it == pf_item) {  // prefetched into LDS during the previous item
-            if (valid) {
-                const u32x4* rb = rowbuf + wv * 256u + lane;
-                v0 = rb[0];
-                v1 = rb[64];
-                v2 = rb[128];
-                v3 = rb[192];
-            }
-        } else if (valid) {
+        if (valid) {
             const u32x4* rp = (const u32x4*)(rows + p0 + lane);
             v0 = rp[0];  // off_a, off_b
             v1 = rp[1];  // spec_l_a, spec_l_b, spec_ar_a, spec_ar_b
             v2 = rp[2];  // stat_l_a, stat_l_b, stat_ar_a, stat_ar_b
             v3 = rp[3];  // flags_a, flags_b, pair_id, cluster_id
         }
-        pf_item = ~0u;
-        if constexpr (DYN && RPF) {
-            if (it < pf_end && lane == 0) tk = atomicAdd(ctr, 1u);
-        }
-        if constexpr (RPF) flush();  // the previous item's results
         if constexpr (PROF) {
             tp_r = wall_clock64();
             tp_rows += tp_r - tp_i;
@@ -1384,26 +1006,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     else mis_s |= bit;
                 }
             }
-            if constexpr (RPF && DYN) {
-                // after the first pass the next main ticket (fetched as this item started, before its
-                // rows and first loads) is back: start its rows' trip into LDS
-                if (base == 0u && it < pf_end) {
-                    const uint32_t nx = uni(__builtin_amdgcn_readlane(tk, 0)) + nwaves;
-                    const uint32_t q0 = ((c_begin + (nx >> sub_shift)) << 6) +
-                                        (nx & ((1u << sub_shift) - 1u)) * (64u >> sub_shift);
-                    if (nx < n_full && q0 < n) {
-                        if (lane < min(64u >> sub_shift, n - q0)) {
-                            const u32x4* rp = (const u32x4*)(rows + q0 + lane);
-                            u32x4* rb = rowbuf + wv * 256u;
-                            __builtin_amdgcn_global_load_lds(rp + 0, (lds_ptr)(rb + 0), 16, 0, 0);
-                            __builtin_amdgcn_global_load_lds(rp + 1, (lds_ptr)(rb + 64), 16, 0, 0);
-                            __builtin_amdgcn_global_load_lds(rp + 2, (lds_ptr)(rb + 128), 16, 0, 0);
-                            __builtin_amdgcn_global_load_lds(rp + 3, (lds_ptr)(rb + 192), 16, 0, 0);
-                        }
-                        pf_item = nx;
-                    }
-                }
-            }
         }
         [[maybe_unused]] uint64_t tp_s1 = 0;
         if constexpr (PROF) {
@@ -1429,7 +1031,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
             uint32_t src = 0, pc = 0, nb = 0;
             bool defer = false;
-            if (used + ck <= arena_per_wave && ck <= (tail_round ? min(deep_max, kTailJoinMax) : deep_max)) {
+            if (used + ck <= arena_per_wave && ck <= (tail_round ? kTailJoinMax : kDeepJoin)) {
                 src = wbase + used;
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
@@ -1439,7 +1041,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
                     const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
                     nb = sentinel_noop_bits(fa);
-                    if (!RPF && lane == 0) {  // RPF: written lane-parallel by flush()
+                    if (lane == 0) {
                         ah[src] = (fk & F_SEED) ? status_sentinel_hash((fa >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask)
                                                 : sent0;
                         ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
@@ -1474,28 +1076,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t nt = popc64(ballot(myflag & F_STATUS));
         const uint32_t nd = popc64(ballot(dirty));
         const uint32_t cs = wave_sum(dirty ? mycap : 0u);
-        if constexpr (RPF) {
-            q_flag = myflag;
-            q_cap = mycap;
-            q_src = mysrc;
-            q_cnt = mycnt;
-            q_noop = mynoop;
-            q_seed = (v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu;
-            q_p0 = p0;
-            q_n = cnt;
-            q_c = c;
-            q_ish = ish;
-            q_ns = ns;
-            q_nt = nt;
-            q_nd = nd;
-            q_cs = cs;
-            q_pending = true;
-            if constexpr (PROF) {
-                tp_e = wall_clock64();
-                tp_post += tp_e - tp_je;
-            }
-            continue;
-        }
         if (valid) {
             flags[p0 + lane] = (uint8_t)myflag;
             if (dirty) {
@@ -1521,7 +1101,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_post += tp_e - tp_je;
         }
     }
-    if constexpr (RPF) flush();  // the last item's results
     if (deferred && lane == 0) summary[6] = 1u;
     if constexpr (PROF) {
         const uint64_t t_end = wall_clock64();
@@ -1650,63 +1229,38 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
     return hipGetLastError();
 }
 
-// The decision kernel of each tuning variant (GPUDIFF_OPT_K2_VARIANT_SHIFT; 0 = the default).
+// The decision kernels: 8 x 16-B chunks a side in flight per lane at 3 waves/SIMD (139 VGPRs) by default, 16 at
+// 2 waves/SIMD for deep pairs (>= kK2BigPairBytes a pair on average), each also as the per-wave timeline build
+// (GPUDIFF_OPT_K2_TIMELINE, tools/k2_wave_profile.py).  In-process A/B (profiles/r04p): 8 in flight beat round
+// 3's 4 at 4 waves on every shape -- config3 10M K2 8.21 vs 8.28 ms, the N = 8 share 1.147 vs 1.164, config4 1.080
+// vs 1.091 -- and 16 wins only on deep pairs (config4 1.043 ms, but config3 8.44 and the share 1.195): when the
+// items are 16-256 KiB the last round's waves stream alone and their own loads in flight set the tail's rate.
+// Rejected and removed in round 5 (measurements in DESIGN.md §5, §6): a wave per pair (k_compare),
+// 2 / 4 / 12 chunks in flight, plain loads, rows prefetched into LDS, static striding.
 typedef void (*K2Fn)(const gpudiff_pair_row*, const uint8_t*, uint32_t, uint8_t*, uint32_t*, uint4*, uint32_t, uint32_t,
                      uint64_t*, uint8_t*, uint32_t, uint32_t, uint32_t, uint32_t*, uint32_t*, uint8_t*, uint64_t,
                      uint32_t*, uint32_t, const uint32_t*);
-static K2Fn k2_kernel(uint32_t variant) {
-    switch (variant) {
-        case 1: return k_compare<false, 4, 1>;
-        case 2: return k_compare<true, 8, 1>;
-        case 3: return k_compare<false, 8, 1>;
-        case 4: return k_compare<true, 2, 1>;
-        case 5: return k_compare<true, 4, 6>;  // <= 80 VGPRs
-        case 6: return k_compare<true, 2, 8>;  // <= 64 VGPRs
-        case 7: return k_compare_flat<4, 1, true>;  // round 3's default: 4 chunks a side in flight, 4 waves/SIMD
-        case 8: return k_compare_flat<4, 1>;
-        case 9: return k_compare_flat<2, 1>;
-        case 11: return k_compare_flat<12, 3, true>;  // x12 held to 3 waves/SIMD
-        case 12: return k_compare_flat<16, 1, true>;  // x16
-        case 13: return k_compare_flat<4, 1, true, false, true>;  // + next rows prefetched into LDS (RPF)
-        case 10: return k_compare_flat<8, 1, true>;  // 8 chunks a side in flight, 3 waves/SIMD
-        case 14: return k_compare_flat<8, 1, true, true>;  // the default + per-wave timeline (g_k2_prof)
-        case 16: return k_compare_flat<16, 1, true, true>;  // (variant 14 on deep pairs, by k2_variant_of)
-        case 15: return k_compare_flat<2, 1, true>;
-        // 0 is resolved by k2_variant_of (10 or 12); items handed out dynamically (5% shorter than static
-        // striding = variant 8 on config3, tools/ab_k2.py on MI355X)
-        default: return k_compare_flat<8, 1, true>;
+constexpr uint32_t kK2Kernels = 4;
+static K2Fn k2_kernel(uint32_t k) {
+    switch (k) {
+        case 1: return k_compare_flat<16, 1>;
+        case 2: return k_compare_flat<8, 1, true>;
+        case 3: return k_compare_flat<16, 1, true>;
+        default: return k_compare_flat<8, 1>;
     }
 }
 
-static bool k2_is_dyn(uint32_t variant) {
-    switch (variant) {
-        case 0: case 7: case 10: case 11: case 12: case 13: case 14: case 15: case 16: return true;
-        default: return false;
-    }
-}
-
-// The default decision kernel by batch shape (variant 0; in-process A/B, profiles/r04p): the kernel keeps 8 x 16-B
-// chunks a side in flight per lane at 3 waves/SIMD (139 VGPRs) -- config3 10M K2 8.21 vs 8.28 ms, the N = 8 share
-// 1.147 vs 1.164, config4 1.080 vs 1.091 against round 3's 4 in flight at 4 waves -- and 16 in flight at 2 waves
-// for deep pairs (>= kK2BigPairBytes a pair: config4 1.043 ms, but config3 8.44 and the share 1.195): when the
-// items are 16-256 KiB the last round's waves stream alone and their own loads in flight set the tail's rate.
 constexpr uint64_t kK2BigPairBytes = 16384;
 static uint32_t k2_variant_of(const DiffBuffers& b) {
-    const uint32_t v = b.k2_variant & 15u;
-    const bool big = b.avg_pair_bytes >= kK2BigPairBytes;
-    if (v == 14) return big ? 16u : 14u;  // the profiled kernel follows the default's shape choice
-    return v ? v : (big ? 12u : 10u);
+    return (b.avg_pair_bytes >= kK2BigPairBytes ? 1u : 0u) | (b.k2_timeline ? 2u : 0u);
 }
 
 constexpr uint32_t kK2LptMax = 16384;  // largest-first rounds: at most this many pairs (one block sorts them in LDS)
 // largest-first rounds for deep pairs: one round of single pairs (two scatter the stream further: config4 K2
 // 1.093 ms vs 1.060 with one and 1.070 in index order, profiles/r04w), after one round of whole items sorted the
-// same way (-0.4%, profiles/r04zk); in both, joins over kTailJoinMax keys are deferred to K4 (GPUDIFF_OPT_K2_TAIL8
-// on deep batches: not, the A/B)
-static uint32_t k2_lpt_rounds(const DiffBuffers&) { return 1u; }
-static bool k2_item_round_on(const DiffBuffers&) { return true; }
-static bool k2_tail_defer_on(const DiffBuffers& b) { return !b.k2_tail8; }
-constexpr uint32_t kK2MaxSubShift = 3;  // tuning: items of >= 64 >> 3 = 8 pairs
+// same way (-0.4%, profiles/r04zk); in both, joins over kTailJoinMax keys are deferred to K4
+constexpr uint32_t kK2LptRounds = 1;
+constexpr uint32_t kK2MaxSubShift = 3;  // items of >= 64 >> 3 = 8 pairs
 // 64-pair chunks are split into 2^k items until every resident K2 wave has at least this many
 constexpr uint32_t kK2ItemsPerWave = 6;  // >= 6 items per resident wave: config3 at the N = 8 share (19.5k chunks) and config2 (15.6k) both split to 32-pair items, the best of 4 / 8 on each (profiles/r02zz3)
 
@@ -1714,7 +1268,7 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
     // one resident 256-thread block per CU per wave slot a SIMD offers the
     // kernel (its measured occupancy, hipOccupancyMaxActiveBlocksPerMultiprocessor):
     // a larger grid would leave blocks waiting for a free slot, i.e. a tail
-    static int occ[17] = {0};
+    static int occ[kK2Kernels] = {0};
     const uint32_t v = k2_variant_of(b);
     if (!occ[v]) {
         int n = 0;
@@ -1723,7 +1277,7 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
             n = 4;
         occ[v] = n;
     }
-    return 256u * (b.k2_blocks_per_cu ? b.k2_blocks_per_cu : (uint32_t)occ[v]);
+    return 256u * (uint32_t)occ[v];
 }
 
 // Deep pairs (>= 16 KiB of compared bytes on average: config4's 8-64 KiB objects) are split below
@@ -1737,9 +1291,7 @@ constexpr uint32_t kK2ItemsPerWaveBig = 8, kK2MaxSubShiftBig = 6;
 // (config3's 156k chunks: k = 0; deep pairs: see above)
 static uint32_t k2_sub_shift(const DiffBuffers& b, uint32_t nchunks) {
     const bool big = b.avg_pair_bytes >= kK2BigPairBytes;
-    const uint64_t want = (uint64_t)(b.k2_items_per_wave ? b.k2_items_per_wave
-                                                         : (big ? kK2ItemsPerWaveBig : kK2ItemsPerWave)) *
-                          4u * k2_cap_blocks(b);
+    const uint64_t want = (uint64_t)(big ? kK2ItemsPerWaveBig : kK2ItemsPerWave) * 4u * k2_cap_blocks(b);
     const uint32_t max_shift = big ? kK2MaxSubShiftBig : kK2MaxSubShift;
     // items of at least 8 pairs: a small batch (a watch-replay batch of 64k events: 1k chunks) split
     // further than that pays a row load, a prefix sum and a ticket per 2-4 pairs (config5: K2 0.42 ms
@@ -1833,55 +1385,50 @@ __global__ __launch_bounds__(1024) void k_tail_order(const gpudiff_pair_row* __r
     }
 }
 
-// the launch's largest-first round (0 = none): large pairs only, DYN variants without the LDS row prefetch,
-// no pair-split tail (k2_tail_chunks() == 0: the items of large pairs are split to 1-2 pairs already)
-static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t v, uint32_t nch, uint32_t nwaves, uint32_t sub,
-                             uint32_t tail) {
-    if (b.k2_no_lpt || !b.tail_perm || tail || !(v == 7 || (v >= 10 && v <= 12) || v >= 14)) return 0;
-    if (b.avg_pair_bytes < kK2BigPairBytes) return 0;
-    const uint32_t r = k2_lpt_round(nch << sub, nwaves, k2_lpt_rounds(b));
+// the launch's largest-first round (0 = none): large pairs only, no pair-split tail (k2_tail_chunks() == 0: the
+// items of large pairs are split to 1-2 pairs already)
+static uint32_t k2_lpt_items(const DiffBuffers& b, uint32_t nch, uint32_t nwaves, uint32_t sub, uint32_t tail) {
+    if (!b.tail_perm || tail || b.avg_pair_bytes < kK2BigPairBytes) return 0;
+    const uint32_t r = k2_lpt_round(nch << sub, nwaves, kK2LptRounds);
     // the round's pairs and the item round before it are sorted in one block's LDS / kept in tail_perm
     return (r << (6u - sub)) + k2_item_round((nch << sub) - r, nwaves) <= kK2LptMax ? r : 0;
 }
 
-hipError_t launch_compare(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, uint32_t seg,
-                          uint32_t nsegs, bool reset_summary) {
-    const dim3 grid(k2_grid_waves(b, c1 - c0) / 4u);
+hipError_t launch_compare(hipStream_t s, const DiffBuffers& b) {
+    const uint32_t nch = (b.n_pairs + 63u) / 64u;
+    const dim3 grid(k2_grid_waves(b, nch) / 4u);
     uint4* cc = (uint4*)b.chunk_counts;
-    const uint32_t sub = k2_sub_shift(b, c1 - c0);
+    const uint32_t sub = k2_sub_shift(b, nch);
     const uint32_t v = k2_variant_of(b);
-    const uint32_t tq = k2_tail_q(b);
-    const uint32_t tail = k2_is_dyn(v) ? k2_tail_chunks(c1 - c0, grid.x * 4u, sub, tq) : 0u;
-    const uint32_t lpt = nsegs == 1 ? k2_lpt_items(b, v, c1 - c0, grid.x * 4u, sub, tail) : 0u;
+    const uint32_t tq = kK2TailQuarters;
+    const uint32_t tail = k2_tail_chunks(nch, grid.x * 4u, sub, tq);
+    const uint32_t lpt = k2_lpt_items(b, nch, grid.x * 4u, sub, tail);
     const uint32_t* perm = nullptr;
     if (lpt) {
-        const uint32_t n_main = ((c1 - c0) << sub) - lpt;
-        const uint32_t p_first = ((c0 + (n_main >> sub)) << 6) + (n_main & ((1u << sub) - 1u)) * (64u >> sub);
-        const uint32_t r2 = k2_item_round_on(b) ? k2_item_round(n_main, grid.x * 4u) : 0u;
-        const uint64_t key = ((uint64_t)b.n_pairs << 32) ^ ((uint64_t)lpt << 12) ^ ((uint64_t)sub << 8) ^ c0 ^
-                             ((uint64_t)(uintptr_t)b.rows << 7) ^ ((uint64_t)r2 << 40);
-        if (*b.tail_perm_key != key) {
-            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, p_first, lpt << (6u - sub), c0, n_main - r2, r2, sub,
+        const uint32_t n_main = (nch << sub) - lpt;
+        const uint32_t p_first = ((n_main >> sub) << 6) + (n_main & ((1u << sub) - 1u)) * (64u >> sub);
+        const uint32_t r2 = k2_item_round(n_main, grid.x * 4u);
+        // the order depends on the rows and the launch shape: cached under the exact tuple (a permutation made
+        // for another round size would visit pairs outside the round, or one twice -- ADVICE r4)
+        const TailPermKey key{b.rows, b.rows_gen, b.n_pairs, lpt, sub, r2};
+        if (!(*b.tail_perm_key == key)) {
+            k_tail_order<<<1, 1024, 0, s>>>(b.rows, b.n_pairs, p_first, lpt << (6u - sub), 0u, n_main - r2, r2, sub,
                                             b.tail_perm);
             *b.tail_perm_key = key;
         }
         perm = b.tail_perm;
     }
-    if (sub || tail || lpt || reset_summary) {  // split chunks accumulate their counts with atomics
-        const uint32_t z0 = sub ? c0 : lpt ? c0 + ((((c1 - c0) << sub) - lpt) >> sub) : c1 - tail;
-        const uint32_t ncc = c1 - z0;
-        k_pass_reset<<<std::max(1u, std::min(1024u, (ncc + 255u) / 256u)), 256, 0, s>>>(
-            reset_summary ? b.summary : nullptr, kSummaryWords, cc + z0, ncc);
+    {  // one launch zeroes the summary and the chunk counts split items accumulate with atomics
+        const uint32_t z0 = sub ? 0u : lpt ? (((nch << sub) - lpt) >> sub) : nch - tail;
+        const uint32_t ncc = nch - z0;
+        k_pass_reset<<<std::max(1u, std::min(1024u, (ncc + 255u) / 256u)), 256, 0, s>>>(b.summary, kSummaryWords,
+                                                                                        cc + z0, ncc);
     }
-    // each wave owns arena entries [wave*stride + seg*slice, +slice) in this segment
-    const uint32_t slice = b.arena_per_wave / nsegs;
-#define K2ARGS b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, c0, c1, b.arena_h, b.arena_k, seg * slice, slice, \
-               b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask, b.summary, \
-               sub | (k2_is_dyn(v) ? (tq << 8) | (tq ? 0u : 1u << 16) | (b.k2_tail8 ? 1u << 17 : 0u) : 0u) | \
-                   ((b.k2_deep_mode & 3u) << 18) | (lpt ? k2_lpt_rounds(b) << 20 : 0u) | \
-                   (lpt && k2_item_round_on(b) ? 1u << 22 : 0u) | (lpt && k2_tail_defer_on(b) ? 1u << 23 : 0u), perm
-    k2_kernel(v)<<<grid, 256, 0, s>>>(K2ARGS);
-#undef K2ARGS
+    // sub_arg: sub_shift | tail quarters << 8 | largest-first rounds << 20 | item round << 22
+    const uint32_t sub_arg = sub | (tq << 8) | (lpt ? kK2LptRounds << 20 | 1u << 22 : 0u);
+    k2_kernel(v)<<<grid, 256, 0, s>>>(b.rows, b.pool, b.n_pairs, b.flags, b.caps, cc, 0u, nch, b.arena_h, b.arena_k, 0u,
+                                      b.arena_per_wave, b.arena_per_wave, b.path_src, b.path_cnt, b.nbits, b.hash_mask,
+                                      b.summary, sub_arg, perm);
     return hipGetLastError();
 }
 
@@ -1929,7 +1476,7 @@ hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_
                                                             (b.scratch_cap / kJoinSlice + 3u) / 4u + 1u);
     (void)c0;
     (void)c1;
-    (b.k4_pipelined ? k_join_slices<true> : k_join_slices<false>)<<<k4_blocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
+    k_join_slices<<<k4_blocks, 256, 0, s>>>(b.rows, b.pool, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,
                                                  b.summary, before, after, b.scratch_cap, b.scratch_h, b.scratch_k,
                                                  b.slice_cnt, b.slice_weq);
     k_join_gather<<<k4_blocks, 256, 0, s>>>(b.rows, b.flags, b.dirty_idx, b.scratch_off, b.slot_owner,

@@ -423,6 +423,7 @@ int gpudiff_store_submit(gpudiff_ctx* c, gpudiff_store* s, const gpudiff_event* 
     d->pool_cap = s->space_bytes;
     d->pool_used = s->used;
     d->n_pairs = n;
+    d->rows_gen++;
     d->leaves = leaves;
     d->compare_bytes = cb;
     d->value_bytes = 0;

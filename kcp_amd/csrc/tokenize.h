@@ -206,13 +206,12 @@ hipError_t k0_profile(int enable, uint64_t* out8);
 // slots/links (optional): the seed is the slot's (DSlot.flags >> 8).
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
-                              TokOut* out, const DSlot* slots = nullptr, const DocLink* links = nullptr,
-                              uint32_t variant = 0);
+                              TokOut* out, const DSlot* slots = nullptr, const DocLink* links = nullptr);
 // K10: the write path's request bodies (GPUDIFF_UPSERT_*): docs[i].pad holds
 // the body's u64 offset in `bodies` (room: marshal_out_cap(json_len)); out[i]
 // gets {off, bytes, status}.  A nonzero status leaves the document to the host.
 hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
-                               uint8_t* bodies, uint32_t mode, TokOut* out, uint32_t variant = 0);
+                               uint8_t* bodies, uint32_t mode, TokOut* out);
 // K11: roll-up fields per document into outs (RollOut[n]); scratch per document at docs[i].scratch_off
 hipError_t launch_rollup_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               RollOut* outs);

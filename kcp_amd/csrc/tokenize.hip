@@ -760,34 +760,22 @@ hipError_t k0_profile(int enable, uint64_t* out8) {
 
 hipError_t launch_encode_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
                               uint8_t* space, uint64_t space_cap, unsigned long long* used, uint64_t mask,
-                              TokOut* out, const DSlot* slots, const DocLink* links, uint32_t variant) {
+                              TokOut* out, const DSlot* slots, const DocLink* links) {
     if (!n) return hipSuccess;
     const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    // variant (tuning, GPUDIFF_OPT_K0_VARIANT_SHIFT): 0 = 8 waves/SIMD (<= 64 VGPRs), 1 = unconstrained
-    if (variant == 1)
-        k_encode_docs<1><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask,
-                                                                out, slots, links);
-    else
-        k_encode_docs<8><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask,
-                                                                out, slots, links);
+    // 8 waves/SIMD (<= 64 VGPRs): unconstrained occupancy measured slower (round 2)
+    k_encode_docs<8><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, space, space_cap, used, mask, out,
+                                                            slots, links);
     return hipGetLastError();
 }
 
 hipError_t launch_marshal_docs(hipStream_t s, const TokDoc* docs, uint32_t n, const uint8_t* json, uint8_t* scratch,
-                               uint8_t* bodies, uint32_t mode, TokOut* out, uint32_t variant) {
+                               uint8_t* bodies, uint32_t mode, TokOut* out) {
     if (!n) return hipSuccess;
     const uint32_t blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    // variant (tuning, GPUDIFF_OPT_K0_VARIANT_SHIFT): 0 = 8 waves/SIMD (<= 64 VGPRs, a few spills:
-    // fastest, A/B on config3 documents), 1 = unconstrained (4 waves), 2 = 5 waves (no spills), 3 = 6 waves
-#define K10_LAUNCH(W)                                                                                   \
-    k_encode_docs<W, kModeMarshal><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, bodies, 0, \
-                                                                          nullptr, (uint64_t)mode, out,      \
-                                                                          nullptr, nullptr)
-    if (variant == 1) K10_LAUNCH(1);
-    else if (variant == 2) K10_LAUNCH(5);
-    else if (variant == 3) K10_LAUNCH(6);
-    else K10_LAUNCH(8);
-#undef K10_LAUNCH
+    // 8 waves/SIMD (<= 64 VGPRs, a few spills): faster than 4, 5 or 6 waves on config3 documents (round 2 A/B)
+    k_encode_docs<8, kModeMarshal><<<blocks, 64 * kWavesPerBlock, 0, s>>>(docs, n, json, scratch, bodies, 0, nullptr,
+                                                                          (uint64_t)mode, out, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -435,8 +435,7 @@ int gpudiff_wbatch_run(gpudiff_ctx* c, gpudiff_wbatch* wb) {
     }
     if (wb->ev[0]) HIPCHK(hipEventRecord(wb->ev[0], c->stream));
     HIPCHK(launch_marshal_docs(c->stream, (const TokDoc*)wb->d_docs, wb->n, (const uint8_t*)wb->d_json,
-                               (uint8_t*)wb->d_scratch, (uint8_t*)wb->d_out, wb->mode, (TokOut*)wb->d_res,
-                               (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u));
+                               (uint8_t*)wb->d_scratch, (uint8_t*)wb->d_out, wb->mode, (TokOut*)wb->d_res));
     if (wb->ev[1]) {
         HIPCHK(hipEventRecord(wb->ev[1], c->stream));
         wb->pending_timing = true;
@@ -619,15 +618,14 @@ int gpudiff_write_plan_get_ex(gpudiff_ctx* c, gpudiff_ticket ticket, uint32_t mo
             cleanup();
             return e == hipErrorOutOfMemory ? GPUDIFF_E_CAPACITY : GPUDIFF_E_DEVICE;
         }
-        const uint32_t var = (c->flags >> GPUDIFF_OPT_K0_VARIANT_SHIFT) & 3u;
         hipError_t le = hipMemcpyAsync(d_docs, docs.data(), nd * sizeof(TokDoc), hipMemcpyHostToDevice, c->stream);
         if (le == hipSuccess && n_spec_docs)
             le = launch_marshal_docs(c->stream, (const TokDoc*)d_docs, n_spec_docs, sp.djson, (uint8_t*)d_scratch,
-                                     (uint8_t*)d_out, GPUDIFF_UPSERT_SPEC, (TokOut*)d_res, var);
+                                     (uint8_t*)d_out, GPUDIFF_UPSERT_SPEC, (TokOut*)d_res);
         if (le == hipSuccess && nd > n_spec_docs)
             le = launch_marshal_docs(c->stream, (const TokDoc*)d_docs + n_spec_docs, (uint32_t)(nd - n_spec_docs),
                                      sp.djson, (uint8_t*)d_scratch, (uint8_t*)d_out, GPUDIFF_UPSERT_STATUS,
-                                     (TokOut*)d_res + n_spec_docs, var);
+                                     (TokOut*)d_res + n_spec_docs);
         if (le == hipSuccess && (rc = dstore_staged_mark_read(c, ticket))) le = hipErrorUnknown;
         if (le == hipSuccess) le = hipMemcpyAsync(to.data(), d_res, nd * sizeof(TokOut), hipMemcpyDeviceToHost, c->stream);
         if (le == hipSuccess) le = hipMemcpyAsync(raw.data(), d_out, ob, hipMemcpyDeviceToHost, c->stream);

@@ -17,7 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpudiff.so")
 
-ABI_VERSION = 4  # GPUDIFF_ABI_VERSION of include/gpudiff.h
+ABI_VERSION = 5  # GPUDIFF_ABI_VERSION of include/gpudiff.h
 OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUND = range(-1, -9, -1)
 
@@ -26,9 +26,8 @@ PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
 OPT_TIMING = 0x1
 OPT_DEVICE_ENCODE = 0x2000000
-OPT_K2_FUSE_DEEP = 0x40000000  # tuning: deep joins stay in K2 (no K4 merge-path slices)
-OPT_H2D_TWO_STREAMS = 0x2  # tuning: device-encode uploads alternate JSON chunks between two copy streams
-OPT_K2_NO_LPT = 0x4  # tuning: K2's final round in index order (default: largest first for large pairs)
+OPT_K2_TIMELINE = 0x100  # profiling hook: K2's per-wave timeline build (k2_profile)
+OPT_ARENA_SHIFT = 21  # test hook: 4 bits, the K2 wave arenas shrunk 2^k-fold (forces the deferred K4 path)
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
 PATH_HASH_BITS = 32  # GPUDIFF_PATH_HASH_BITS: segment keys and reported path hashes

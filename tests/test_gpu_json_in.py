@@ -1,8 +1,7 @@
 """JSON-in batches large enough for several upload chunks (gpudiff_submit's device-encode path splits the JSON
-into up to 16 chunks of >= 16 MiB, each uploaded and encoded as soon as it is staged): the default single copy
-stream and GPUDIFF_OPT_H2D_TWO_STREAMS give the same flags and changed paths as host encoding and as the
-oracle's tree walk over the same JSON (oracle/deepequal_ref.cpp, specsyncer.go:17-41 / statussyncer.go:15-27)."""
-import os
+into up to 16 chunks of >= 16 MiB, each uploaded and encoded as soon as it is staged), staged or zero-copy,
+give the same flags and changed paths as host encoding and as the oracle's tree walk over the same JSON
+(oracle/deepequal_ref.cpp, specsyncer.go:17-41 / statussyncer.go:15-27)."""
 
 import numpy as np
 import pytest
@@ -19,7 +18,7 @@ def _same(a, b):
             and np.array_equal(a.path_hashes, b.path_hashes) and np.array_equal(a.path_kinds, b.path_kinds))
 
 
-def test_multi_chunk_upload_one_and_two_copy_streams():
+def test_multi_chunk_upload_staged_and_zero_copy():
     cfg = S.make_cfg("config3", n_pairs=40000, mutate_frac=0.3)  # >= 64k documents: 4 chunks (kMinChunkDocs)
     pop = S.Population(cfg)
     buf, offs, _ = pop.json_range(0, pop.n, 8)
@@ -40,23 +39,15 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
     assert np.array_equal(want.pair_flags & 7, f)
     assert np.array_equal(want.path_offsets.astype(np.int64), o.astype(np.int64))
     assert np.array_equal(want.path_hashes, h) and np.array_equal(want.path_kinds, k)
-    # the default chunks, two copy streams, one chunk, the most chunks (1 MiB minimum: capped at 16), and every
-    # chunk's K0 on the kernel stream (the default alternates two K0 streams)
-    variants = ((0, {}), (G.OPT_H2D_TWO_STREAMS, {}), (0, {"GPUDIFF_H2D_MAX_CHUNKS": "1"}),
-                (G.OPT_H2D_TWO_STREAMS, {"GPUDIFF_H2D_CHUNK_MIB": "1"}), (0, {"GPUDIFF_K0_ONE_STREAM": "1"}))
-    for flags, env in variants + ((0, {"zero_copy": True}),):
-        zero_copy = env.pop("zero_copy", False)
-        os.environ.update(env)
-        e = G.Engine(device=0, encode_threads=8, device_encode=True, flags=flags)
+    # the default chunks (three here: >= 16 MiB and >= 16k documents each), staged and zero copy; K0 of odd
+    # chunks on the second K0 stream
+    for zero_copy in (False, True):
+        e = G.Engine(device=0, encode_threads=8, device_encode=True)
         # zero copy: the pairs laid out in a gpudiff_host_alloc buffer, uploaded straight from it
         pj = G.PinnedJson(e, buf, offs) if zero_copy else None
         a = pj.pairs if zero_copy else arr
         # two batches in flight (both ring slots), then the same batch again on a reused slot
-        try:
-            t1 = e.submit_array(a)  # creates the device-encode store (reads the environment)
-        finally:
-            for name in env:
-                os.environ.pop(name)
+        t1 = e.submit_array(a)
         t2 = e.submit_array(a)
         r1, r2 = e.wait(t1), e.wait(t2)
         r3 = e.wait(e.submit_array(a))
@@ -65,7 +56,7 @@ def test_multi_chunk_upload_one_and_two_copy_streams():
             pj.free()
         e.close()
         for r in (r1, r2, r3):
-            assert _same(r, want), "device encode (flags %#x, %s) differs from host encode" % (flags, env)
+            assert _same(r, want), "device encode (zero copy %s) differs from host encode" % zero_copy
 
 
 def test_two_in_flight_with_host_resolution():

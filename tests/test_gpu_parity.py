@@ -85,32 +85,13 @@ def test_long_values_and_list_shift(eng):
     assert_matches(res, pairs)
 
 
-@pytest.mark.parametrize("segments", [2, 3, 8])
-def test_segmented_pipeline(segments):
-    """K2 of segment s+1 overlapped with K3/K4 of segment s on the side stream:
-    identical results to the single-segment pass."""
-    pairs, cl, _ = make_pairs(2600, seed=13, mutate_frac=0.3, pretty_frac=0)
-    e = G.Engine(device=0, flags=segments << 16, timing=True)
-    hb = e.encode(pairs)
-    db = e.device_batch(hb.info().pool_bytes + 4096, len(pairs))
-    db.append(hb)
-    res = e.wait(e.diff(db))
-    assert_matches(res, pairs)
-    assert e.timings().k2_launches == segments
-    res2 = e.wait(e.diff(db))
-    assert np.array_equal(res.path_hashes, res2.path_hashes)
-    db.free()
-    hb.free()
-    e.close()
-
-
-@pytest.mark.parametrize("shrink,segments", [(10, 1), (12, 1), (9, 3), (14, 2)])
-def test_deferred_join_path(shrink, segments):
+@pytest.mark.parametrize("shrink", [9, 10, 12, 14])
+def test_deferred_join_path(shrink):
     """Wave arenas shrunk until most dirty pairs do not fit: those pairs take the
     deferred K4 path (and with shrink 14 every pair with a path does);
     results must not change."""
     pairs, _, _ = make_pairs(1500, seed=14, mutate_frac=0.4, crd_leaves=300, pretty_frac=0)
-    e = G.Engine(device=0, flags=(shrink << 21) | (segments << 16))
+    e = G.Engine(device=0, flags=shrink << G.OPT_ARENA_SHIFT)
     res = e.diff_pairs(pairs)
     assert_matches(res, pairs)
     e.close()
@@ -327,63 +308,71 @@ def test_submit_pipelining(eng):
     assert_matches(eng.wait(t1), p1)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 7, 8, 9, 10, 11, 12, 13, 14, 15])
-def test_k2_variants_bit_exact(variant):
-    """Every decision-kernel variant (k_compare: wave per pair; k_compare_flat:
-    flattened chunk stream, several unrolls / occupancies) against the oracle on
-    mixed and deep populations, with joins in K2 and with deferred joins."""
+@pytest.mark.parametrize("timeline", [False, True], ids=["default", "timeline_build"])
+def test_k2_kernels_bit_exact(timeline):
+    """The four decision kernels -- 8 chunks a side in flight (mixed pairs) and 16 (deep pairs, >= 16 KiB a pair),
+    each also as the per-wave timeline build (GPUDIFF_OPT_K2_TIMELINE) -- against the oracle, with joins in K2
+    and with every join deferred to K4."""
     pairs, _, _ = make_pairs(1200, seed=31, mutate_frac=0.3, pretty_frac=0)
-    deep, _, _ = make_pairs(120, seed=32, mix=(("crd", 1.0),), mutate_frac=0.5, crd_leaves=1500)
+    deep, _, _ = make_pairs(120, seed=32, mix=(("crd", 1.0),), mutate_frac=0.5, crd_leaves=2500, pretty_frac=0)
     for shrink in (0, 12):
-        e = G.Engine(device=0, flags=(variant << 8) | (shrink << 21))
+        e = G.Engine(device=0, flags=(G.OPT_K2_TIMELINE if timeline else 0) | (shrink << G.OPT_ARENA_SHIFT))
         assert_matches(e.diff_pairs(pairs), pairs)
+        hb = e.encode(deep)
+        assert hb.info().pool_bytes / len(deep) > 2 * 16384  # the deep-pair kernel
+        hb.free()
         assert_matches(e.diff_pairs(deep), deep)
         e.close()
 
 
-@pytest.mark.parametrize("tail_flags", [0x10, 0x50, 0x80, 0x10 | (1 << 28)], ids=["no_tail_late", "tail4q", "tail8", "no_tail_ipw4"])
-def test_k2_tail_tunings_bit_exact(tail_flags):
-    """K2's work hand-out variants (GPUDIFF_OPT_K2_TAIL_SHIFT / _K2_TAIL8 / items per wave): main and
-    tail tickets, late fetch, 8-pair or half-size tail items -- identical results, against the oracle."""
-    pairs, _, _ = make_pairs(6000, seed=33, mutate_frac=0.2, pretty_frac=0)
-    e = G.Engine(device=0, flags=tail_flags)
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4095, 6000, 20000])
+def test_k2_hand_out_shapes_bit_exact(n):
+    """Batch sizes around the chunk and item boundaries: 64-pair chunks split into items, the tail of half-size
+    items, dynamic tickets -- against the oracle."""
+    pairs, _, _ = make_pairs(n, seed=33 + n, mutate_frac=0.2, pretty_frac=0)
+    e = G.Engine(device=0)
     res = e.diff_pairs(pairs)
     assert_matches(res, pairs)
     e.close()
 
 
-@pytest.mark.parametrize("lpt", [True, False], ids=["largest_first", "index_order"])
-def test_k2_largest_first_round(lpt):
+def test_k2_largest_first_round():
     """Large pairs (>= 16 KiB compared on average): K2's final round of items is handed out largest first
-    (k_tail_order's permutation, cached per batch) or in index order (GPUDIFF_OPT_K2_NO_LPT); repeated
-    passes over the same batch (the cached order) and over a view (its own order): identical results,
-    against the oracle."""
+    (k_tail_order's permutation, cached per batch under the exact launch shape and the rows' generation);
+    repeated passes over the same batch (the cached order), over a view (its own order) and after the batch
+    was reset and refilled with other pairs of the same count (a new order): identical to the oracle."""
     pairs, _, _ = make_pairs(900, seed=61, mix=(("crd", 1.0),), mutate_frac=0.4, crd_leaves=2500, pretty_frac=0)
-    e = G.Engine(device=0, flags=0 if lpt else G.OPT_K2_NO_LPT)
+    other, _, _ = make_pairs(900, seed=62, mix=(("crd", 1.0),), mutate_frac=0.6, crd_leaves=3000, pretty_frac=0)
+    e = G.Engine(device=0)
     hb = e.encode(pairs)
+    ho = e.encode(other)
     assert hb.info().pool_bytes / len(pairs) > 2 * 16384  # the large-pair path
-    db = e.device_batch(hb.info().pool_bytes + 4096, len(pairs))
+    db = e.device_batch(max(hb.info().pool_bytes, ho.info().pool_bytes) + 4096, len(pairs))
     db.append(hb)
     exp = assert_matches(e.wait(e.diff(db)), pairs)
     assert_matches(e.wait(e.diff(db)), pairs, exp=exp)
-    e2 = G.Engine(device=0, flags=0 if lpt else G.OPT_K2_NO_LPT)
+    e2 = G.Engine(device=0)
     v = db.view(e2)
     assert_matches(e2.wait(e2.diff(v)), pairs, exp=exp)
     v.free()
+    db.reset()
+    db.append(ho)
+    assert_matches(e.wait(e.diff(db)), other)
     db.free()
     hb.free()
+    ho.free()
     e2.close()
     e.close()
 
 
-@pytest.mark.parametrize("mode", ["slices", "fused", "slices_all"])
+@pytest.mark.parametrize("mode", ["slices", "slices_all"])
 def test_deep_joins_merge_path(mode):
     """Joins over 2048 keys go to K4's merge-path slices (1024 merged keys each: several slices per
     region, equal keys straddling slice boundaries, list shifts with thousands of changed paths);
-    "fused": GPUDIFF_OPT_K2_FUSE_DEEP keeps them in K2; "slices_all": a shrunken K2 arena sends every
-    dirty pair, small ones included, through the slices.  Flags, IDs and paths equal the oracle's."""
+    "slices_all": a shrunken K2 arena sends every dirty pair, small ones included, through the slices.
+    Flags, IDs and paths equal the oracle's."""
     pairs = deep_pairs() + make_pairs(300, seed=43, mutate_frac=0.4)[0]
-    flags = {"slices": 0, "fused": G.OPT_K2_FUSE_DEEP, "slices_all": 14 << 21}[mode]
+    flags = {"slices": 0, "slices_all": 14 << G.OPT_ARENA_SHIFT}[mode]
     e = G.Engine(device=0, flags=flags)
     assert_matches(e.diff_pairs(pairs), pairs)
     e.close()
@@ -391,14 +380,13 @@ def test_deep_joins_merge_path(mode):
 
 def test_k2_hand_out_orders_agree_on_deep_batches():
     """A deep batch large enough for every K2 hand-out stage (config4 shape, 40k pairs: 4-pair main items, a
-    round of whole items and a round of single pairs both handed out largest first): the default, index order
-    (GPUDIFF_OPT_K2_NO_LPT) and the rounds' joins kept in K2 (GPUDIFF_OPT_K2_TAIL8 on deep batches; the default
-    defers their joins over 256 keys to K4) give identical flags, ID lists and changed paths, and the flags equal
-    the generator's ground truth."""
+    round of whole items and a round of single pairs both handed out largest first, their joins over 1024 keys
+    deferred to K4): the default and every join deferred to K4's slices (a shrunken arena) give identical flags,
+    ID lists and changed paths, and the flags equal the generator's ground truth."""
     from kcp_amd import synth as S
     pop = S.Population(S.make_cfg("config4", n_pairs=40000))
     res = {}
-    for name, flags in (("default", 0), ("index", G.OPT_K2_NO_LPT), ("tail_joins_in_k2", 0x80)):
+    for name, flags in (("default", 0), ("all_joins_in_k4", 14 << G.OPT_ARENA_SHIFT)):
         e = G.Engine(device=0, encode_threads=16, flags=flags)
         ch = pop.chunk(e, 0, pop.n, 16)
         db = e.device_batch(ch.hb.info().pool_bytes + 4096, pop.n)

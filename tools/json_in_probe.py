@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """JSON-in end-to-end rates and phase split alone (bench.py's json_in block without the 10M resident
 population): the first --pairs pairs of config3 as JSON in host memory -> gpudiff_submit -> gpudiff_wait, with
-host encoding, device encoding and its A/B variants.  Prints one JSON object.
+host encoding, device encoding (staged, streaming, zero copy).  Prints one JSON object.
 
     python tools/json_in_probe.py [--pairs 131072] [--threads 16]
 """

@@ -20,7 +20,7 @@ docs = [bytes(buf[offs[2 * i + 1]:offs[2 * i + 2]]) for i in range(n)]
 print("docs %d, mean %.0f B" % (n, np.mean([len(d) for d in docs])))
 variants = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0"])]
 for var in variants:
-    eng = G.Engine(device=0, flags=var << 26)
+    eng = G.Engine(device=0, flags=0)
     eng.encode_objects(docs[:256])  # warm
     for on in (False, True):
         eng.k0_profile(on)

@@ -23,7 +23,7 @@ for d in docs:
     kinds[k] = kinds.get(k, 0) + 1
 print("docs %d, mean %.0f B, kinds %s" % (n, np.mean([len(d) for d in docs]), kinds))
 variant = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-eng = G.Engine(device=0, timing=True, flags=variant << 26)
+eng = G.Engine(device=0, timing=True, flags=0)
 print("K10 variant", variant)
 wb = eng.wbatch(docs)
 wb.run()

@@ -1,7 +1,8 @@
 """K2's per-wave timeline on MI355X: where a diff pass loses time against a pure stream.
 
-Ingests config3 (optionally resized) like bench.py, times the default K2 (variant 0) and then runs
-variant 14 -- the same kernel plus wall-clock stamps (100 MHz) -- recording per wave: start, end of
+Ingests config3 (optionally resized) like bench.py, times the default K2 ("variant0") and then runs its
+timeline build ("variant14", GPUDIFF_OPT_K2_TIMELINE: the same kernel plus wall-clock stamps, 100 MHz), recording
+per wave: start, end of
 its first item, items taken, start of its last item, end, ticks spent streaming and in the join.
 
     python tools/k2_wave_profile.py --pairs 1250000 [--passes 5] [--config config4 --flags 0xF00000] > out.json
@@ -42,9 +43,9 @@ def main():
     pop = S.Population(cfg, 1, 0)
     n = pop.n
     out = {"pairs": n}
-    for variant in (0, 14):
+    for variant in (0, 14):  # 14: the timeline build (GPUDIFF_OPT_K2_TIMELINE; the record names of earlier rounds)
         eng = G.Engine(device=0, encode_threads=args.threads, stream=stream.cuda_stream, timing=True,
-                       flags=(variant << 8) | args.flags)
+                       flags=(G.OPT_K2_TIMELINE if variant == 14 else 0) | args.flags)
         first = pop.chunk(eng, 0, min(262144, n), args.threads)
         per_pair = first.pool_bytes / max(1, min(262144, n))
         db = eng.device_batch(int(per_pair * n * (1.4 if args.config == "config4" else 1.15)) + (64 << 20), n)
