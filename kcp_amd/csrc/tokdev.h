@@ -39,6 +39,7 @@ constexpr uint32_t kMaxDepth = 255;
 constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kLdsPerWave = 5120;
 constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
+constexpr uint32_t kLdsOrder = 768;  // phase 3b's depth order in LDS up to this many nodes (4 B each, behind 2 KiB)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -274,8 +275,9 @@ __device__ int decode_string(const uint8_t* p, const uint8_t* q, const uint8_t* 
     return (int)(o - dst);
 }
 
-// literal / number at p (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error
-__device__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+// literal / number at p (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error; byte by
+// byte from memory (parse_atom's path for atoms that do not fit its register window)
+__device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
     const uint32_t c = *p;
     *val = 0;
     if (c == 't' || c == 'f' || c == 'n') {
@@ -372,6 +374,47 @@ __device__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* t
     uint64_t bits;
     if (!decimal_to_double(w, e10, neg, &bits)) return GPUDIFF_TOK_NUMBER;
     *val = bits;
+    return GPUDIFF_TOK_OK;
+}
+
+// parse_atom: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or
+// the document's end -- from a 16-byte register window (three aligned-word loads issued together instead of a
+// dependent load per byte); everything else (floats, exponents, longer numbers, any syntax doubt) goes to
+// parse_atom_mem, so results are parse_atom_mem's by construction.  kTokSlack >= 32 keeps the loads inside the
+// staged buffer.  K0 (encode mode) only.
+__device__ __forceinline__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
+    const uint64_t w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+    const uint64_t w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+    const uint64_t left = (uint64_t)(end - p);
+    const uint32_t avail = left < 16u ? (uint32_t)left : 16u;
+    auto at = [&](uint32_t k) -> uint32_t { return (uint32_t)(((k < 8u ? w0 : w1) >> (8u * (k & 7u))) & 0xFFu); };
+    const uint32_t c = (uint32_t)(w0 & 0xFFu);
+    if (c == 't' || c == 'f' || c == 'n') {
+        const uint32_t n = c == 'f' ? 5u : 4u;
+        const uint64_t want = c == 't' ? 0x65757274ull : c == 'f' ? 0x65736c6166ull : 0x6c6c756eull;
+        if (avail >= n && (w0 & ((1ull << (8 * n)) - 1ull)) == want && (avail == n ? left == n : is_delim(at(n)))) {
+            *val = 0;
+            *tag = c == 't' ? GPUDIFF_TAG_TRUE : c == 'f' ? GPUDIFF_TAG_FALSE : GPUDIFF_TAG_NULL;
+            return GPUDIFF_TOK_OK;
+        }
+        return parse_atom_mem(p, end, tag, val);
+    }
+    const uint32_t d0 = c == '-' ? 1u : 0u;
+    uint32_t k = d0;
+    uint64_t v = 0;
+    while (k < avail && is_digit(at(k))) v = v * 10u + (at(k++) - '0');
+    const uint32_t nd = k - d0;
+    // accepted: 1..15 digits, no leading zero unless alone, then the document's end or a delimiter that is not
+    // the start of a fraction or an exponent ('.', 'e', 'E' are no delimiters)
+    const bool at_end = k == avail && left == avail;
+    if (nd == 0 || nd > 15 || (at(d0) == '0' && nd > 1) || !(at_end || (k < avail && is_delim(at(k)))))
+        return parse_atom_mem(p, end, tag, val);
+    *tag = GPUDIFF_TAG_INT;
+    *val = d0 ? 0ull - v : v;
     return GPUDIFF_TOK_OK;
 }
 
@@ -565,6 +608,28 @@ __device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* 
             if (nb > 1) q[1] = (uint8_t)(w >> 8);
             if (nb > 2) q[2] = (uint8_t)(w >> 16);
             if (nb > 3) q[3] = (uint8_t)(w >> 24);
+        }
+    }
+}
+
+// copies this lane's n bytes at s into 4-byte aligned o as whole dwords, the last one zero past n (K0's arena
+// tails), flattened over the wave like wave_copy_flat
+__device__ void wave_copy_dwords0(bool has, const uint8_t* s, uint32_t n, uint32_t* o) {
+    const uint32_t lane = __lane_id();
+    const FlatUnits f = flat_units(has, n);
+    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const uint64_t sp = (uint64_t)(uintptr_t)s, dp = (uint64_t)(uintptr_t)o;
+    for (uint32_t b = 0; b < f.total; b += 64) {
+        const uint32_t g = b + lane;
+        const uint32_t ow = flat_owner(f, g);
+        const uint32_t first = shfl32(f.incl - units, ow), on = shfl32(n, ow);
+        const uint64_t op = shfl64(sp, ow), od = shfl64(dp, ow);
+        if (g < f.total) {
+            const uint32_t u = g - first;
+            uint32_t w = (uint32_t)ld8u((const uint8_t*)(uintptr_t)op + 4u * u);
+            const uint32_t rem = on - 4u * u;
+            if (rem < 4u) w &= (1u << (8u * rem)) - 1u;
+            ((uint32_t*)(uintptr_t)od)[u] = w;
         }
     }
 }

@@ -441,12 +441,14 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint32_t i = i0 + lane;
             if (i >= nn) break;
             const uint4 r = S.rec[i];
-            if (r.x == 0 && (r.y & KEYBIT)) {
-                // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key
-                // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
+            if (r.y & KEYBIT) {
+                // a member's key span for phase 3b's hash (kept in the sort-key area, unused until phase 4)
                 const uint32_t kt = r.y & ~KEYBIT;
                 const uint32_t op = S.tok[kt] & POS_MASK, cp = S.tok[kt + 1] & POS_MASK;
-                if (cp - op - 1 == 5u && (ld8u(d + op + 1) & 0xDFDFDFDFDFull) == 0x534D455449ull) {
+                S.skey[i] = ((uint64_t)(cp - op - 1) << 32) | (op + 1);
+                // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key
+                // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
+                if (r.x == 0 && cp - op - 1 == 5u && (ld8u(d + op + 1) & 0xDFDFDFDFDFull) == 0x534D455449ull) {
                     err = GPUDIFF_TOK_LIST;
                     continue;
                 }
@@ -490,7 +492,10 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
 
     mark(2);
     // ------------------------------------------------------------ phase 3b: path hashes by depth
+    // nodes counting-sorted by depth (the order in LDS up to kLdsOrder nodes), then level by level a lane per
+    // node: its record and key span (phase 3a) in one round trip, its parent's hash and its key bytes in the next
     if (status == GPUDIFF_TOK_OK && nn > 1) {
+        uint32_t* order = nn - 1 <= kLdsOrder ? (uint32_t*)(lds + 2048) : S.order;
         // counting sort of nodes by depth
         for (uint32_t i = lane; i <= kMaxDepth; i += 64) hist[i] = 0;
         wave_sync();
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             if (i < nn) {
                 const uint32_t dep = (S.rec[i].w >> NI_DEPTH_SHIFT) & 0xFFu;
                 const uint32_t p = atomicAdd(&cur[dep], 1u);
-                S.order[p] = i;
+                order[p] = i;  // nodes 1 .. nn - 1 (the root is not sorted): depths >= 1
             }
         }
         wave_sync();
@@ -522,18 +527,12 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint32_t cnt = hist[dep];
             for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
                 if (j0 + lane < cnt) {
-                    const uint32_t i = S.order[beg + j0 + lane];
+                    const uint32_t i = order[beg + j0 + lane];
                     const uint4 r = S.rec[i];
+                    const uint64_t ks = S.skey[i];
                     const uint64_t ph = r.x == 0 ? seed : S.h[r.x];
-                    uint64_t hh;
-                    if (r.y & KEYBIT) {
-                        const uint32_t kt = r.y & ~KEYBIT;
-                        const uint32_t op = S.tok[kt] & POS_MASK, cp = S.tok[kt + 1] & POS_MASK;
-                        hh = hash_key(ph, d + op + 1, cp - op - 1);
-                    } else {
-                        hh = hash_index(ph, r.y);
-                    }
-                    S.h[i] = hh;
+                    S.h[i] = (r.y & KEYBIT) ? hash_key(ph, d + (uint32_t)ks, (uint32_t)(ks >> 32))
+                                            : hash_index(ph, r.y);
                 }
             }
             beg += cnt;
@@ -695,37 +694,31 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 // the path-table entry: hash, parent hash, component (+ key bytes)
                 const uint64_t tbal = ballot(t);
                 const uint32_t kinc = wave_incl_scan(kl);
+                const uint32_t ko = tko + kinc - kl;  // this entry's key bytes
                 if (t) {
                     const uint32_t tr = trank + popc64(tbal & mask_lt(lane));
-                    const uint32_t ko = tko + kinc - kl;
                     hs[tr] = skey[j];
                     phs[tr] = r.x == 0 ? root : (S.h[r.x] & mask);
                     cs[tr] = (r.y & KEYBIT) ? (((uint64_t)kl << 32) | ko) : (GPUDIFF_TAB_INDEX | r.y);
-                    for (uint32_t q = 0; q < kl; q++) keys[ko + q] = d[kop + q];
                 }
                 trank += popc64(tbal);
                 tko += rdlane(kinc, 63);
-                // long strings: wave-cooperative dword copies of the tail (the bytes after the
-                // first 8, which sit in the leaf record) into the arena (tails at 4-byte aligned
-                // offsets; the last dword's bytes past the value are zero)
-                for (uint64_t bl = ballot(ar != 0); bl; bl &= bl - 1) {
-                    const uint32_t src_lane = (uint32_t)__builtin_ctzll(bl);
-                    const uint32_t si = rdlane(i, src_lane);
-                    const uint32_t sm = rdlane(m, src_lane);
-                    const uint32_t sg = rdlane(rg, src_lane) - 1u;
-                    const uint32_t sa = rdlane(my_aoff, src_lane);
-                    const uint4 rr = S.rec[si];
-                    const uint32_t op = S.tok[rr.z] & POS_MASK;
-                    const uint8_t* src = ((rr.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1)) + GPUDIFF_INLINE_MAX;
-                    const uint32_t slen = (sm >> 3) - GPUDIFF_INLINE_MAX;
-                    uint32_t* dst = (uint32_t*)(segp[sg] + 16ull * Lr[sg] + sa);
-                    for (uint32_t c4 = lane; c4 * 4u < slen; c4 += 64) {
-                        uint32_t w = (uint32_t)ld8u(src + 4u * c4);
-                        const uint32_t rem = slen - 4u * c4;
-                        if (rem < 4) w &= (1u << (8 * rem)) - 1u;
-                        dst[c4] = w;
-                    }
+                // key bytes of the path-table entries and the long strings' tails (the bytes after the first 8,
+                // which sit in the leaf record; 4-byte aligned arena offsets, the last dword zero past the value):
+                // wave-cooperative flattened copies over every lane's span at once (one copy loop per string,
+                // each a chain of dependent loads, cost this phase a quarter of K0's time, profiles/r05a)
+                wave_copy_flat(t && kl, d + kop, kl, keys + ko);
+                const bool tail = ar != 0u;
+                const uint8_t* tsrc = nullptr;
+                uint32_t* tdst = nullptr;
+                uint32_t tlen = 0;
+                if (tail) {
+                    const uint32_t op = S.tok[r.z] & POS_MASK;
+                    tsrc = ((r.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1)) + GPUDIFF_INLINE_MAX;
+                    tlen = (m >> 3) - GPUDIFF_INLINE_MAX;
+                    tdst = (uint32_t*)(segp[rg - 1u] + 16ull * Lr[rg - 1u] + my_aoff);
                 }
+                wave_copy_dwords0(tail, tsrc, tlen, tdst);
             }
             // zero each arena's tail pad (its values end 4-byte aligned; the arena is a multiple of 16)
             for (uint32_t g = 0; g < 2; g++) {
