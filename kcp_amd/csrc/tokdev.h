@@ -40,6 +40,7 @@ constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kLdsPerWave = 5120;
 constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
 constexpr uint32_t kLdsOrder = 768;  // phase 3b's depth order in LDS up to this many nodes (4 B each, behind 2 KiB)
+constexpr uint32_t kLdsHash = 256;   // ... and up to this many nodes their hashes too (order 1 KiB + hashes 2 KiB)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -382,13 +383,18 @@ __device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_
 // dependent load per byte); everything else (floats, exponents, longer numbers, any syntax doubt) goes to
 // parse_atom_mem, so results are parse_atom_mem's by construction.  kTokSlack >= 32 keeps the loads inside the
 // staged buffer.  K0 (encode mode) only.
-__device__ __forceinline__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+// the 16 bytes at p in two registers (three aligned-word loads issued together; p + 23 must be readable)
+__device__ __forceinline__ void ld16u(const uint8_t* p, uint64_t* w0, uint64_t* w1) {
     const uintptr_t a = (uintptr_t)p;
     const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
     const uint32_t sh = (uint32_t)(a & 7u) * 8u;
     const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
-    const uint64_t w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
-    const uint64_t w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+    *w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+    *w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+}
+// parse_atom over its window w0, w1 = the 16 bytes at p (ld16u), loaded by the caller with its other loads
+__device__ __forceinline__ uint32_t parse_atom_w(const uint8_t* p, const uint8_t* end, uint64_t w0, uint64_t w1,
+                                                 uint32_t* tag, uint64_t* val) {
     const uint64_t left = (uint64_t)(end - p);
     const uint32_t avail = left < 16u ? (uint32_t)left : 16u;
     auto at = [&](uint32_t k) -> uint32_t { return (uint32_t)(((k < 8u ? w0 : w1) >> (8u * (k & 7u))) & 0xFFu); };
@@ -416,6 +422,11 @@ __device__ __forceinline__ uint32_t parse_atom(const uint8_t* p, const uint8_t* 
     *tag = GPUDIFF_TAG_INT;
     *val = d0 ? 0ull - v : v;
     return GPUDIFF_TOK_OK;
+}
+__device__ __forceinline__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+    uint64_t w0, w1;
+    ld16u(p, &w0, &w1);
+    return parse_atom_w(p, end, w0, w1, tag, val);
 }
 
 // ---- K10 (write path) helpers: Go 1.16 encodeState.string(s, escapeHTML=true)

@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                                                      const DocLink* __restrict__ links) {
     // per wave, one LDS area reused phase by phase (5 KiB -> 8 workgroups of 4 waves per CU):
     //   phase 1: [0, 2048) byte ring; phase 2: [2048, 4096) container stack;
-    //   phase 3b: [0, 2048) depth histogram + cursors; phase 4: [0, 4608) sort (ns <= kLdsSort)
+    //   phase 3b: [0, 2048) depth histogram + cursors, [2048, ..) depth order (<= kLdsOrder nodes) or order +
+    //   hashes [3072, 5120) (<= kLdsHash nodes); phase 4: [0, 4608) sort (ns <= kLdsSort)
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[kWavesPerBlock][kLdsPerWave];
 
     const uint32_t lane = lane_id();
@@ -156,6 +157,84 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     if (nchunks > 4) pre = ld_chunk(4);
     lds_order();
     auto ring32 = [&](uint32_t p) -> uint32_t { return *(const uint32_t*)(ring + (p & 4095u)); };
+    // the token code of an opening quote at pos: a region keyword when the exact string follows (the 16 bytes
+    // after the quote, from five LDS words; bytes past the document cannot fake a match: a string that closes
+    // inside the document puts its quote inside the compared span), else the quote itself
+    auto keyword = [&](uint32_t pos) -> uint32_t {
+        const uint32_t a = (pos + 1u) & ~3u, sh = (pos + 1u) & 3u;
+        const uint32_t w0 = ring32(a), w1 = ring32(a + 4u), w2 = ring32(a + 8u), w3 = ring32(a + 12u);
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh), x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        const uint32_t x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        uint32_t kw = '"';
+        kw = (x0 == 0x6174656du && x1 == 0x61746164u && (x2 & 0xFFu) == 0x22u) ? TK_KEY_META : kw;  // metadata"
+        kw = (x0 == 0x74617473u && (x1 & 0xFFFFFFu) == 0x227375u) ? TK_KEY_STATUS : kw;          // status"
+        kw = (x0 == 0x6562616cu && (x1 & 0xFFFFFFu) == 0x22736cu) ? TK_KEY_LABELS : kw;          // labels"
+        kw = (x0 == 0x6f6e6e61u && x1 == 0x69746174u && x2 == 0x22736e6fu) ? TK_KEY_ANNOT : kw;  // annotations"
+        return kw;
+    };
+    // 256 bytes in one step, 4 per lane, when the block holds no backslash and no byte >= 0x80 (and no escape
+    // carries into it): no escapes, so the unescaped quotes are the quotes; a lane's in-string state is the parity
+    // of the quotes in the lanes below it (one ballot + mbcnt) and its own prefix parity; tokens are compacted with
+    // a 3-ballot prefix of the per-lane counts.  The same tokens, codes and state as four 64-byte steps (below).
+    // Returns false (nothing done) otherwise.
+    auto fast_block = [&](uint32_t b) -> bool {
+        const uint32_t p4 = b + 4u * lane;
+        uint32_t x = *(const uint32_t*)(ring + (p4 & 4095u));
+        if (p4 + 4u > len) {  // bytes past the document read as spaces
+            const uint32_t nv = p4 >= len ? 0u : len - p4;
+            const uint32_t keep = (1u << (8u * nv)) - 1u;
+            x = (x & keep) | (0x20202020u & ~keep);
+        }
+        uint32_t Qn = 0, Sn = 0, Wn = 0, Cn = 0, Mn = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t c = (x >> (8u * j)) & 0xFFu, cb = c & 0xDFu;
+            Qn |= (c == '"' ? 1u : 0u) << j;
+            Sn |= (cb == '[' || cb == ']' || c == ':' || c == ',' ? 1u : 0u) << j;
+            Wn |= (c == ' ' || c == '\n' || c == '\r' || c == '\t' ? 1u : 0u) << j;
+            Cn |= (c < 0x20u ? 1u : 0u) << j;
+            Mn |= (c == '\\' || c >= 0x80u ? 1u : 0u) << j;
+        }
+        if (esc_carry || ballot(Mn != 0u)) return false;
+        const uint64_t odd = ballot(__builtin_popcount(Qn) & 1u);
+        const uint32_t P = (str_par + mbcnt64(odd)) & 1u;  // parity of the quotes before this lane
+        uint32_t px = Qn ^ (Qn << 1);
+        px = (px ^ (px << 2)) & 0xFu;                      // inclusive prefix parity within the lane
+        const uint32_t In = px ^ (P ? 0xFu : 0u);          // in a string (opening quote in, closing out)
+        str_par = (str_par + popc64(odd)) & 1u;
+        const uint32_t opens = Qn & In, closes = Qn & ~In & 0xFu;
+        const uint32_t atom = ~In & ~Qn & ~Sn & ~Wn & 0xFu;
+        const uint32_t prev = wave_shr1((atom >> 3) & 1u, (uint32_t)atom_carry);  // byte 3 of the lane below
+        const uint32_t astart = atom & ~(((atom << 1) | prev) & 0xFu);
+        atom_carry = rdlane((atom >> 3) & 1u, 63);
+        if (ballot((Cn & In & ~opens) != 0u)) ctl_in_string = true;
+        const uint32_t Tn = (Sn & ~In) | Qn | astart;
+        const uint32_t tc = __builtin_popcount(Tn);
+        const uint64_t c0 = ballot(tc & 1u), c1 = ballot(tc & 2u), c2 = ballot(tc & 4u);
+        const uint32_t pre = mbcnt64(c0) + 2u * mbcnt64(c1) + 4u * mbcnt64(c2);
+        const uint32_t j1 = opens ? (uint32_t)__builtin_ctz(opens) : 4u;  // most lanes hold at most one opening
+        const uint32_t kw1 = opens ? keyword(p4 + j1) : 0u;
+        const uint32_t op2 = opens & (opens - 1u);
+        const uint32_t kw2 = ballot(op2 != 0u) && op2 ? keyword(p4 + (uint32_t)__builtin_ctz(op2)) : 0u;
+        uint32_t k = ntok + pre;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            if ((Tn >> j) & 1u) {
+                const uint32_t code = ((closes >> j) & 1u) ? TK_CLOSEQ
+                                      : ((opens >> j) & 1u) ? (j == j1 ? kw1 : kw2) : (x >> (8u * j)) & 0xFFu;
+                S.tok[k++] = (code << 24) | (p4 + j);
+            }
+        }
+        const uint64_t om = ballot(opens != 0u);
+        if (om) {  // the last opening quote of the block (a later step may mark its string slow)
+            const uint32_t L = 63u - (uint32_t)__builtin_clzll(om);
+            const uint32_t jl = opens ? 31u - (uint32_t)__builtin_clz(opens) : 0u;
+            last_open_idx = rdlane(ntok + pre + __builtin_popcount(Tn & ((1u << jl) - 1u)), L);
+            last_open_pos = b + 4u * L + rdlane(jl, L);
+        }
+        ntok += popc64(c0) + 2u * popc64(c1) + 4u * popc64(c2);
+        return true;
+    };
     for (uint32_t ch = 0; ch < nchunks; ch++) {
         if (ch >= 3 && ch + 1 < nchunks) {  // the lookahead chunk, loaded during chunk ch - 1
             put_chunk(ch + 1, pre);
@@ -163,7 +242,10 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             lds_order();
         }
         const uint32_t bend = min(len, (ch + 1) << 10);
-        for (uint32_t b = ch << 10; b < bend; b += 64) {
+        for (uint32_t b4 = ch << 10; b4 < bend; b4 += 256) {
+          if (fast_block(b4)) continue;
+          for (uint32_t b = b4; b < min(bend, b4 + 256u); b += 64) {  // the block holds an escape or a
+                                                                        // non-ASCII byte: 64 bytes a step
             const uint32_t pos = b + lane;
             const uint32_t c = pos < len ? (uint32_t)ring[pos & 4095u] : 0x20u;
             const uint64_t bs = ballot(c == '\\');
@@ -241,6 +323,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 if ((slow_opens >> ob) & 1ull) last_marked = last_open_idx;
             }
             ntok += popc64(tokens);
+          }
         }
     }
     if (str_par) status = GPUDIFF_TOK_SYNTAX;  // unterminated string
@@ -437,46 +520,56 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
         uint32_t err = GPUDIFF_TOK_OK;
+        // three dependent rounds of loads per 64 nodes, each issued for every lane before any is waited for:
+        // the record; the token positions of its key and value; 16 bytes at the value and 8 at a root key
         for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
             const uint32_t i = i0 + lane;
             if (i >= nn) break;
             const uint4 r = S.rec[i];
-            if (r.y & KEYBIT) {
+            const bool key = (r.y & KEYBIT) != 0u, leaf = (r.w & NI_LEAF) != 0u;
+            const bool str = leaf && (r.w & NI_STR), atom = leaf && (r.w & NI_ATOM);
+            const uint32_t kt = r.y & ~KEYBIT;
+            uint32_t kop = 0, kcp = 0, vop = 0, vcp = 0;
+            if (key) {
+                kop = S.tok[kt] & POS_MASK;
+                kcp = S.tok[kt + 1] & POS_MASK;
+            }
+            if (str || atom) vop = S.tok[r.z] & POS_MASK;
+            if (str) vcp = S.tok[r.z + 1] & POS_MASK;
+            const uint8_t* vp = d + vop + (str ? 1u : 0u);
+            uint64_t w0 = 0, w1 = 0, kw = 0;
+            if (str || atom) ld16u(vp, &w0, &w1);
+            if (key && r.x == 0) kw = ld8u(d + kop + 1);
+            if (key) {
                 // a member's key span for phase 3b's hash (kept in the sort-key area, unused until phase 4)
-                const uint32_t kt = r.y & ~KEYBIT;
-                const uint32_t op = S.tok[kt] & POS_MASK, cp = S.tok[kt + 1] & POS_MASK;
-                S.skey[i] = ((uint64_t)(cp - op - 1) << 32) | (op + 1);
+                S.skey[i] = ((uint64_t)(kcp - kop - 1) << 32) | (kop + 1);
                 // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key
                 // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
-                if (r.x == 0 && cp - op - 1 == 5u && (ld8u(d + op + 1) & 0xDFDFDFDFDFull) == 0x534D455449ull) {
+                if (r.x == 0 && kcp - kop - 1 == 5u && (kw & 0xDFDFDFDFDFull) == 0x534D455449ull) {
                     err = GPUDIFF_TOK_LIST;
                     continue;
                 }
             }
-            if (!(r.w & NI_LEAF)) continue;
+            if (!leaf) continue;
             uint32_t tag = r.w & NI_TAG, mlen = 0;
             uint64_t v = 0;
-            if (r.w & NI_STR) {
-                const uint32_t op = S.tok[r.z] & POS_MASK, cp = S.tok[r.z + 1] & POS_MASK;
-                const uint8_t* src = d + op + 1;
-                uint32_t sl = cp - op - 1;
+            if (str) {
+                uint32_t sl = vcp - vop - 1;
                 if (r.w & NI_SLOW) {
-                    uint8_t* dst = S.str + op + 1;
-                    const int dl = decode_string(src, d + cp, d + len, dst);
+                    uint8_t* dst = S.str + vop + 1;
+                    const int dl = decode_string(vp, d + vcp, d + len, dst);
                     if (dl < 0) {
                         err = GPUDIFF_TOK_STRING;
                         continue;
                     }
-                    src = dst;
                     sl = (uint32_t)dl;
+                    w0 = ld8u(dst);
                 }
                 mlen = sl;
                 // the value's first 8 bytes (a long string's tail goes to the arena in phase 5)
-                if (sl <= GPUDIFF_INLINE_MAX) v = sl ? (ld8u(src) & (~0ull >> (64u - 8u * sl))) : 0ull;
-                else v = ld8u(src);
-            } else if (r.w & NI_ATOM) {
-                const uint32_t ap = S.tok[r.z] & POS_MASK;
-                const uint32_t e = parse_atom(d + ap, d + len, &tag, &v);
+                v = sl >= GPUDIFF_INLINE_MAX ? w0 : sl ? (w0 & (~0ull >> (64u - 8u * sl))) : 0ull;
+            } else if (atom) {
+                const uint32_t e = parse_atom_w(vp, d + len, w0, w1, &tag, &v);
                 if (e) {
                     err = e;
                     continue;
@@ -494,6 +587,10 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     // ------------------------------------------------------------ phase 3b: path hashes by depth
     // nodes counting-sorted by depth (the order in LDS up to kLdsOrder nodes), then level by level a lane per
     // node: its record and key span (phase 3a) in one round trip, its parent's hash and its key bytes in the next
+    // Up to kLdsHash nodes their hashes stay in LDS too (behind the order): a level reads its parents' hashes there,
+    // with no fence on the global stores between levels
+    const bool h_in_lds = nn <= kLdsHash;
+    uint64_t* const hl = (uint64_t*)(lds + 2048 + 4 * kLdsHash);
     if (status == GPUDIFF_TOK_OK && nn > 1) {
         uint32_t* order = nn - 1 <= kLdsOrder ? (uint32_t*)(lds + 2048) : S.order;
         // counting sort of nodes by depth
@@ -530,14 +627,18 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t i = order[beg + j0 + lane];
                     const uint4 r = S.rec[i];
                     const uint64_t ks = S.skey[i];
-                    const uint64_t ph = r.x == 0 ? seed : S.h[r.x];
-                    S.h[i] = (r.y & KEYBIT) ? hash_key(ph, d + (uint32_t)ks, (uint32_t)(ks >> 32))
-                                            : hash_index(ph, r.y);
+                    const uint64_t ph = r.x == 0 ? seed : h_in_lds ? hl[r.x] : S.h[r.x];
+                    const uint64_t hh = (r.y & KEYBIT) ? hash_key(ph, d + (uint32_t)ks, (uint32_t)(ks >> 32))
+                                                       : hash_index(ph, r.y);
+                    S.h[i] = hh;
+                    if (h_in_lds) hl[i] = hh;
                 }
             }
             beg += cnt;
-            wave_sync();
+            if (h_in_lds) lds_order();  // the next level reads these hashes from LDS (in order within the wave)
+            else wave_sync();
         }
+        wave_sync();  // phases 4-5 read S.h
     }
 
     mark(3);
@@ -546,8 +647,12 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     uint64_t* skey = ns <= kLdsSort ? (uint64_t*)lds : S.skey;
     uint32_t* sidx = ns <= kLdsSort ? (uint32_t*)(lds + 8 * kLdsSort) : S.sidx;
     if (status == GPUDIFF_TOK_OK && ns) {
+        // (from LDS when phase 3b kept the hashes there: batch b reads hl[64b + 1 ..] before it writes sidx over
+        // hl entries below 32 (b + 1), all read by earlier batches)
         for (uint32_t j = lane; j < ns; j += 64) {
-            skey[j] = S.h[j + 1] & mask;
+            const uint64_t hj = h_in_lds ? hl[j + 1] : S.h[j + 1];
+            lds_order();
+            skey[j] = hj & mask;
             sidx[j] = j + 1;
         }
         wave_sync();

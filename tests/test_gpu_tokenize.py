@@ -177,6 +177,24 @@ def test_block_boundaries():
     eng.close()
 
 
+def test_fast_scan_block_boundaries():
+    """K0's scan takes 256 bytes a step (4 per lane) when a block holds no backslash and no non-ASCII byte, and
+    64 bytes a step otherwise: quotes, atoms, whitespace, escapes and UTF-8 around and across every position of
+    the 256-byte blocks (the in-string parity carried from lane to lane and block to block, atoms straddling
+    lanes and blocks, a fast block after a slow one and the reverse, a block ending inside a string)."""
+    eng = G.Engine(device=0)
+    docs = []
+    for pad in range(0, 300):
+        docs.append(b'{"p":"' + b'a' * pad + b'","q":[1,22,333,true,false,null,{"r":"s"}],"t":"' + b'z' * (pad % 7) + b'"}')
+        docs.append(b'{"a":' + b' ' * pad + b'12345678901' + b' ' * (pad % 3) + b',"b":[' + b'7,' * (pad % 5) + b'8]}')
+        docs.append(b'{"e":"' + b'b' * pad + b'\\"x\\"","f":"' + b'c' * (300 - pad) + b'"}')
+        docs.append(('{"u":"' + 'd' * pad + 'é","v":"' + 'e' * (pad % 11) + '"}').encode())
+        docs.append(b'{"metadata":{"labels":{"' + b'k' * (pad % 40) + b'":"v"},"annotations":{"n":"' + b'w' * pad +
+                    b'"}},"status":{"x":[' + b'{},' * (pad % 4) + b'[]]}}')
+    _check(eng, docs)
+    eng.close()
+
+
 def test_short_hashes_defer_or_match():
     """8-bit path hashes: most objects collide (K0 defers them); the rest are
     still byte-identical to the host encoder with the same mask."""
