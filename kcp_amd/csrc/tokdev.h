@@ -36,7 +36,10 @@ enum : uint32_t { R_NONE = 0, R_SPEC = 1, R_META = 2, R_LABELS = 3, R_ANNOT = 4,
 enum : uint32_t { E_ROOT, E_KEY, E_KEYCLOSE, E_COLON, E_VALUE, E_STRCLOSE, E_NEXT, E_END };
 
 constexpr uint32_t kMaxDepth = 255;
-constexpr uint32_t kWavesPerBlock = 4;
+#ifndef K0_WPB
+#define K0_WPB 4
+#endif
+constexpr uint32_t kWavesPerBlock = K0_WPB;  // waves (documents) per K0 workgroup
 constexpr uint32_t kLdsPerWave = 5120;
 constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
 constexpr uint32_t kLdsOrder = 768;  // phase 3b's depth order in LDS up to this many nodes (4 B each, behind 2 KiB)

@@ -22,9 +22,13 @@ def main():
     ap.add_argument("--docs", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--lib", default="", help="A/B: another build of libgpudiff.so (e.g. a K0 launch shape)")
     args = ap.parse_args()
     from kcp_amd import gpudiff as G
     from kcp_amd import synth as S
+    if args.lib:
+        G.LIB_PATH = os.path.abspath(args.lib)
+        G._lib = G._load()
 
     n = args.docs
     cfg = S.make_cfg("config3", n_pairs=n, n_clusters=max(1, n // 100))
@@ -40,7 +44,7 @@ def main():
         t = time.perf_counter()
         res = eng.encode_objects(docs)
         times.append(time.perf_counter() - t)
-    out = dict(docs=n, json_bytes_per_launch=nbytes, mean_doc_bytes=nbytes / n,
+    out = dict(lib=args.lib or "kcp_amd/libgpudiff.so", docs=n, json_bytes_per_launch=nbytes, mean_doc_bytes=nbytes / n,
                call_ms_min=min(times) * 1e3, deferred=sum(1 for i, _ in res if i["status"] != 0))
     if args.profile:
         eng.k0_profile(True)
