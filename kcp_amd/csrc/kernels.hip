@@ -847,7 +847,32 @@ __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves
 __device__ uint64_t* g_k2_prof;
 __device__ uint32_t g_k2_prof_cap;
 
-template <int U, int MINB, bool PROF = false>
+// HELP (the deep-pair kernel): the four waves of a workgroup share their current items through LDS.  An owner
+// publishes its item (first pair, pairs, chunks) and claims its passes from the item's chunk cursor; a wave that
+// finds no ticket left streams passes of a sibling's item from the same cursor and ORs its mismatch bits into the
+// item's masks; the owner decides once every helper has left.  So the launch's last items -- single deep pairs
+// streaming at a few GB/s each under full load -- end up to 4x sooner instead of holding the launch open while
+// the other waves of their workgroups idle (profiles/r05a/wave_c4.json: 32% of the waves still running 20 us
+// after the first ones ran out of work).  Waves only help after their own work is done, so the bulk is unchanged.
+struct HelpSlot {
+    uint32_t gen;      // odd while the owner (re)publishes
+    uint32_t cursor;   // next unclaimed chunk of the item
+    uint32_t total;    // chunks of the item
+    uint32_t helpers;  // waves attached to the item
+    uint32_t p0, cnt;  // its pairs
+    uint64_t mis_s, mis_t;
+};
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint64_t lds_ld64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int U, int MINB, bool PROF = false, bool HELP = false>
 __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_row* __restrict__ rows,
                                                       const uint8_t* __restrict__ pool, uint32_t n,
                                                       uint8_t* __restrict__ flags, uint32_t* __restrict__ caps,
@@ -869,6 +894,54 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     uint32_t used = 0;  // entries of this wave's arena in use (wave-uniform)
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
+    __shared__ HelpSlot help_slots[HELP ? 4 : 1];
+    [[maybe_unused]] HelpSlot* const my = &help_slots[HELP ? (threadIdx.x >> 6) : 0];
+    if constexpr (HELP) {
+        if (lane == 0) {
+            my->gen = my->cursor = my->total = my->helpers = my->p0 = my->cnt = 0u;
+            my->mis_s = my->mis_t = 0ull;
+        }
+        __syncthreads();  // every slot initialised before a sibling reads it
+    }
+    // one pass of a wave over chunks [base, base + 64 U) of an item's flattened stream (lane k's registers: pair k's
+    // inclusive chunk prefix, first chunk, spec chunks, arena adjustments and blob offsets); mismatching chunks mark
+    // their pairs in mis_s / mis_t
+    auto stream_pass = [&](uint32_t base, uint32_t total, uint32_t incl, uint32_t first, uint32_t n1, uint32_t adj_a,
+                           uint32_t adj_b, uint64_t off_a, uint64_t off_b, uint64_t& mis_s, uint64_t& mis_t) {
+        u32x4 va[U], vb[U];
+        uint32_t own[U];
+        bool st[U], act[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t g = base + (uint32_t)u * 64u + lane;
+            act[u] = g < total;
+            uint32_t o = 0;  // owner = number of lanes whose inclusive prefix is <= g
+#pragma unroll
+            for (uint32_t s = 32; s >= 1; s >>= 1)
+                if (shfl32(incl, o + s - 1u) <= g) o += s;
+            const uint32_t k = g - shfl32(first, o);
+            st[u] = k >= shfl32(n1, o);
+            const uint32_t xa = shfl32(adj_a, o), xb = shfl32(adj_b, o);
+            const uint64_t oa = shfl64(off_a, o), ob = shfl64(off_b, o);
+            own[u] = o;
+            const uint64_t rel = 16ull * k;
+            if (act[u]) {
+                va[u] = __builtin_nontemporal_load((const u32x4*)(pool + oa + rel + (st[u] ? xa : 0u)));
+                vb[u] = __builtin_nontemporal_load((const u32x4*)(pool + ob + rel + (st[u] ? xb : 0u)));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint64_t m = ballot(act[u] && neq16(va[u], vb[u]));
+            while (m) {  // differing chunks: only in dirty pairs
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                const uint64_t bit = 1ull << (uint32_t)__builtin_amdgcn_readlane((int)own[u], (int)j);
+                if (__builtin_amdgcn_readlane((int)(st[u] ? 1 : 0), (int)j)) mis_t |= bit;
+                else mis_s |= bit;
+            }
+        }
+    };
     [[maybe_unused]] uint64_t tp_start = 0, tp_first = 0, tp_last = 0, tp_stream = 0, tp_join = 0, tp_items = 0;
     [[maybe_unused]] uint64_t tp_rows = 0, tp_pre = 0, tp_post = 0, tp_adv = 0, tp_e = 0, tp_r = 0, tp_je = 0;
     if constexpr (PROF) tp_start = wall_clock64();
@@ -972,40 +1045,37 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             tp_s0 = wall_clock64();
             tp_pre += tp_s0 - tp_r;
         }
-        for (uint32_t base = 0; base < total; base += 64u * U) {
-            u32x4 va[U], vb[U];
-            uint32_t own[U];
-            bool st[U], act[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t g = base + (uint32_t)u * 64u + lane;
-                act[u] = g < total;
-                uint32_t o = 0;  // owner = number of lanes whose inclusive prefix is <= g
-#pragma unroll
-                for (uint32_t s = 32; s >= 1; s >>= 1)
-                    if (shfl32(incl, o + s - 1u) <= g) o += s;
-                const uint32_t k = g - shfl32(first, o);
-                st[u] = k >= shfl32(n1, o);
-                const uint32_t xa = shfl32(adj_a, o), xb = shfl32(adj_b, o);
-                const uint64_t oa = shfl64(off_a, o), ob = shfl64(off_b, o);
-                own[u] = o;
-                const uint64_t rel = 16ull * k;
-                if (act[u]) {
-                    va[u] = __builtin_nontemporal_load((const u32x4*)(pool + oa + rel + (st[u] ? xa : 0u)));
-                    vb[u] = __builtin_nontemporal_load((const u32x4*)(pool + ob + rel + (st[u] ? xb : 0u)));
-                }
+        if constexpr (HELP) {
+            // publish the item (gen odd while the fields change; helpers of the previous item have left), then
+            // claim passes from its cursor -- the first one up front, each next one while the current one streams
+            if (lane == 0) lds_st(&my->gen, lds_ld(&my->gen) + 1u);
+            while (uni(lds_ld(&my->helpers)) != 0u) __builtin_amdgcn_s_sleep(1);
+            if (lane == 0) {
+                lds_st(&my->p0, p0);
+                lds_st(&my->cnt, cnt);
+                lds_st(&my->total, total);
+                __hip_atomic_store(&my->mis_s, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&my->mis_t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                lds_st(&my->cursor, 64u * U);
+                lds_st(&my->gen, lds_ld(&my->gen) + 1u);
             }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                uint64_t m = ballot(act[u] && neq16(va[u], vb[u]));
-                while (m) {  // differing chunks: only in dirty pairs
-                    const uint32_t j = (uint32_t)__builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint64_t bit = 1ull << (uint32_t)__builtin_amdgcn_readlane((int)own[u], (int)j);
-                    if (__builtin_amdgcn_readlane((int)(st[u] ? 1 : 0), (int)j)) mis_t |= bit;
-                    else mis_s |= bit;
-                }
+            for (uint32_t base = 0; base < total;) {
+                uint32_t nb = 0;
+                if (lane == 0) nb = atomicAdd(&my->cursor, 64u * U);
+                stream_pass(base, total, incl, first, n1, adj_a, adj_b, off_a, off_b, mis_s, mis_t);
+                base = uni(__builtin_amdgcn_readlane(nb, 0));
             }
+            if (lane == 0) {
+                atomicOr((unsigned long long*)&my->mis_s, (unsigned long long)mis_s);
+                atomicOr((unsigned long long*)&my->mis_t, (unsigned long long)mis_t);
+            }
+            while (uni(lds_ld(&my->helpers)) != 0u) __builtin_amdgcn_s_sleep(1);
+            const uint64_t ms = lds_ld64(&my->mis_s), mt = lds_ld64(&my->mis_t);
+            mis_s = ((uint64_t)uni((uint32_t)(ms >> 32)) << 32) | uni((uint32_t)ms);
+            mis_t = ((uint64_t)uni((uint32_t)(mt >> 32)) << 32) | uni((uint32_t)mt);
+        } else {
+            for (uint32_t base = 0; base < total; base += 64u * U)
+                stream_pass(base, total, incl, first, n1, adj_a, adj_b, off_a, off_b, mis_s, mis_t);
         }
         [[maybe_unused]] uint64_t tp_s1 = 0;
         if constexpr (PROF) {
@@ -1099,6 +1169,64 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         if constexpr (PROF) {
             tp_e = wall_clock64();
             tp_post += tp_e - tp_je;
+        }
+    }
+    if constexpr (HELP) {
+        // no ticket left: stream passes of the siblings' items until none has an unclaimed chunk
+        const uint32_t wib = threadIdx.x >> 6;
+        for (bool any = true; any;) {
+            any = false;
+            for (uint32_t q = 1; q < 4; q++) {
+                HelpSlot* const h = &help_slots[(wib + q) & 3u];
+                const uint32_t g = uni(lds_ld(&h->gen));
+                if ((g & 1u) || uni(lds_ld(&h->cursor)) >= uni(lds_ld(&h->total))) continue;
+                any = true;
+                if (lane == 0) atomicAdd(&h->helpers, 1u);
+                __asm__ volatile("" ::: "memory");
+                const uint32_t g1 = uni(lds_ld(&h->gen));
+                const uint32_t hp0 = uni(lds_ld(&h->p0)), hcnt = uni(lds_ld(&h->cnt)), htot = uni(lds_ld(&h->total));
+                const uint32_t g2 = uni(lds_ld(&h->gen));
+                if (g1 == g && g2 == g) {  // the item published at gen g: its geometry from its rows
+                    u32x4 v0 = {0, 0, 0, 0}, v1 = v0, v2 = v0, v3 = v0;
+                    const bool valid = lane < hcnt;
+                    if (valid) {
+                        const u32x4* rp = (const u32x4*)(rows + hp0 + lane);
+                        v0 = rp[0];
+                        v1 = rp[1];
+                        v2 = rp[2];
+                        v3 = rp[3];
+                    }
+                    const uint64_t off_a = ((uint64_t)v0.y << 32) | v0.x, off_b = ((uint64_t)v0.w << 32) | v0.z;
+                    const bool ok = valid && ((v3.x | v3.y) & GPUDIFF_OBJ_DECODE_ERR) == 0u;
+                    const bool spec_sz = v1.x == v1.y && v1.z == v1.w;
+                    const bool stat_sz = (v3.y & GPUDIFF_OBJ_HAS_STATUS) != 0u && v2.x == v2.y && v2.z == v2.w;
+                    const uint32_t seg_a = (uint32_t)seg_bytes(v1.x, v1.z), seg_b = (uint32_t)seg_bytes(v1.y, v1.w);
+                    const uint32_t seg_t = (uint32_t)seg_bytes(v2.x, v2.z);
+                    const uint32_t r128 = ((seg_a + seg_t + 127u) & ~127u);
+                    const bool no_stat = (v2.x | v2.y | v2.z | v2.w) == 0u;
+                    const uint32_t n1 =
+                        (ok && spec_sz) ? ((!stat_sz && no_stat) ? ((seg_a + 127u) & ~127u) : seg_a) >> 4 : 0u;
+                    const uint32_t n2 = (ok && stat_sz) ? (spec_sz ? r128 - seg_a : seg_t) >> 4 : 0u;
+                    const uint32_t tot = n1 + n2;
+                    const uint32_t incl = wave_incl_scan(tot);
+                    const uint32_t first = incl - tot;
+                    const uint32_t adj_a = seg_a - 16u * n1, adj_b = seg_b - 16u * n1;
+                    uint64_t ms = 0, mt = 0;
+                    for (;;) {
+                        uint32_t nb = 0;
+                        if (lane == 0) nb = atomicAdd(&h->cursor, 64u * U);
+                        nb = uni(__builtin_amdgcn_readlane(nb, 0));
+                        if (nb >= htot) break;
+                        stream_pass(nb, htot, incl, first, n1, adj_a, adj_b, off_a, off_b, ms, mt);
+                    }
+                    if (lane == 0) {
+                        if (ms) atomicOr((unsigned long long*)&h->mis_s, (unsigned long long)ms);
+                        if (mt) atomicOr((unsigned long long*)&h->mis_t, (unsigned long long)mt);
+                    }
+                }
+                __asm__ volatile("" ::: "memory");
+                if (lane == 0) atomicSub(&h->helpers, 1u);
+            }
         }
     }
     if (deferred && lane == 0) summary[6] = 1u;
@@ -1243,9 +1371,9 @@ typedef void (*K2Fn)(const gpudiff_pair_row*, const uint8_t*, uint32_t, uint8_t*
 constexpr uint32_t kK2Kernels = 4;
 static K2Fn k2_kernel(uint32_t k) {
     switch (k) {
-        case 1: return k_compare_flat<16, 1>;
+        case 1: return k_compare_flat<16, 1, false, true>;
         case 2: return k_compare_flat<8, 1, true>;
-        case 3: return k_compare_flat<16, 1, true>;
+        case 3: return k_compare_flat<16, 1, true, true>;
         default: return k_compare_flat<8, 1>;
     }
 }
