@@ -13,3 +13,10 @@ r=[x for x in csv.DictReader(open('$O/kt_w${w}_r$r/k0_kernel_trace.csv')) if 'en
 print('wpb $w round $r', [round((int(x['End_Timestamp'])-int(x['Start_Timestamp']))/1e6,3) for x in r])"
 done
 done
+# the deep-pair K2 with in-workgroup helpers: parity on deep batches, then config4 (isolated K2, wave timeline)
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_golden.py -x -q --timeout 300 --timeout-method thread > $O/pytest_parity.log 2>&1 || { tail -40 $O/pytest_parity.log; exit 1; }
+tail -1 $O/pytest_parity.log
+timeout -k 10 300 python tools/k2_wave_profile.py --config config4 --pairs 100000 --passes 5 > $O/wave_c4.json 2> $O/wave_c4.log || { tail -20 $O/wave_c4.log; exit 1; }
+python3 -c "
+import json; d=json.load(open('$O/wave_c4.json')); v=d['variant0']; w=d['variant14']
+print('config4 K2 ms', v['k2_ms'], 'frac', v['format_bytes']/v['k2_ms']/1e6/8000, 'timeline', w['k2_ms'], w['end_us'], w['running_at'])"
