@@ -37,7 +37,7 @@ enum : uint32_t { E_ROOT, E_KEY, E_KEYCLOSE, E_COLON, E_VALUE, E_STRCLOSE, E_NEX
 
 constexpr uint32_t kMaxDepth = 255;
 #ifndef K0_WPB
-#define K0_WPB 4
+#define K0_WPB 1  // one document a workgroup (profiles/r05e: 2.04 ms vs 2.30 with 2 and 2.55 with 4 per 65,536 documents)
 #endif
 constexpr uint32_t kWavesPerBlock = K0_WPB;  // waves (documents) per K0 workgroup
 constexpr uint32_t kLdsPerWave = 5120;
@@ -279,69 +279,70 @@ __device__ int decode_string(const uint8_t* p, const uint8_t* q, const uint8_t* 
     return (int)(o - dst);
 }
 
-// literal / number at p (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error; byte by
-// byte from memory (parse_atom's path for atoms that do not fit its register window)
-__device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
-    const uint32_t c = *p;
+// literal / number (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error.  at(k) is the
+// atom's k-th byte, read only for k < left (the bytes to the document's end)
+template <class At>
+__device__ __forceinline__ uint32_t parse_atom_core(At at, uint64_t left, uint32_t* tag, uint64_t* val) {
+    const uint32_t c = at(0);
     *val = 0;
     if (c == 't' || c == 'f' || c == 'n') {
         const uint32_t n = c == 'f' ? 5u : 4u;
-        if ((uint64_t)(end - p) < n) return GPUDIFF_TOK_SYNTAX;
-        const uint64_t w = ld8u(p) & ((1ull << (8 * n)) - 1ull);
+        if (left < n) return GPUDIFF_TOK_SYNTAX;
+        uint64_t w = 0;
+        for (uint32_t k = 0; k < n; k++) w |= (uint64_t)at(k) << (8u * k);
         const uint64_t want = c == 't' ? 0x65757274ull : c == 'f' ? 0x65736c6166ull : 0x6c6c756eull;
         if (w != want) return GPUDIFF_TOK_SYNTAX;
-        if (p + n < end && !is_delim(p[n])) return GPUDIFF_TOK_SYNTAX;
+        if (n < left && !is_delim(at(n))) return GPUDIFF_TOK_SYNTAX;
         *tag = c == 't' ? GPUDIFF_TAG_TRUE : c == 'f' ? GPUDIFF_TAG_FALSE : GPUDIFF_TAG_NULL;
         return GPUDIFF_TOK_OK;
     }
     // number grammar: -? (0 | [1-9][0-9]*) (. [0-9]+)? ([eE] [+-]? [0-9]+)?
-    const uint8_t* q = p;
+    uint64_t q = 0;
     const bool neg = c == '-';
     if (neg) q++;
-    if (q >= end) return GPUDIFF_TOK_SYNTAX;
-    if (*q == '0') {
+    if (q >= left) return GPUDIFF_TOK_SYNTAX;
+    if (at(q) == '0') {
         q++;
-    } else if (*q >= '1' && *q <= '9') {
-        while (q < end && is_digit(*q)) q++;
+    } else if (at(q) >= '1' && at(q) <= '9') {
+        while (q < left && is_digit(at(q))) q++;
     } else {
         return GPUDIFF_TOK_SYNTAX;
     }
-    const uint8_t* int_end = q;
-    const uint8_t* frac_beg = q;
-    const uint8_t* frac_end = q;
+    const uint64_t d0 = neg ? 1u : 0u;
+    const uint64_t int_end = q;
+    uint64_t frac_beg = q, frac_end = q;
     bool is_int = true;
-    if (q < end && *q == '.') {
+    if (q < left && at(q) == '.') {
         is_int = false;
         q++;
         frac_beg = q;
-        if (q >= end || !is_digit(*q)) return GPUDIFF_TOK_SYNTAX;
-        while (q < end && is_digit(*q)) q++;
+        if (q >= left || !is_digit(at(q))) return GPUDIFF_TOK_SYNTAX;
+        while (q < left && is_digit(at(q))) q++;
         frac_end = q;
     }
     int64_t ex = 0;
-    if (q < end && (*q == 'e' || *q == 'E')) {
+    if (q < left && (at(q) == 'e' || at(q) == 'E')) {
         is_int = false;
         q++;
         bool eneg = false;
-        if (q < end && (*q == '+' || *q == '-')) {
-            eneg = *q == '-';
+        if (q < left && (at(q) == '+' || at(q) == '-')) {
+            eneg = at(q) == '-';
             q++;
         }
-        if (q >= end || !is_digit(*q)) return GPUDIFF_TOK_SYNTAX;
-        while (q < end && is_digit(*q)) {
-            if (ex < 100000) ex = ex * 10 + (*q - '0');
+        if (q >= left || !is_digit(at(q))) return GPUDIFF_TOK_SYNTAX;
+        while (q < left && is_digit(at(q))) {
+            if (ex < 100000) ex = ex * 10 + (at(q) - '0');
             q++;
         }
         if (eneg) ex = -ex;
     }
-    if (q < end && !is_delim(*q)) return GPUDIFF_TOK_SYNTAX;
-    const uint8_t* d0 = p + (neg ? 1 : 0);
+    if (q < left && !is_delim(at(q))) return GPUDIFF_TOK_SYNTAX;
     if (is_int) {  // strconv.ParseInt(s, 10, 64)
         const uint64_t lim = neg ? (1ull << 63) : ((1ull << 63) - 1ull);
         uint64_t v = 0;
         bool ovf = false;
-        for (const uint8_t* d = d0; d < int_end; d++) {
-            const uint64_t dig = (uint64_t)(*d - '0');
+        for (uint64_t k = d0; k < int_end; k++) {
+            const uint64_t dig = (uint64_t)(at(k) - '0');
             if (v > (lim - dig) / 10) {
                 ovf = true;
                 break;
@@ -359,7 +360,7 @@ __device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_
     // <= 19 of them: decfloat.h (Clinger's exact path, else Eisel-Lemire)
     const uint32_t n_int = (uint32_t)(int_end - d0), n_frac = (uint32_t)(frac_end - frac_beg);
     const uint32_t n_all = n_int + n_frac;
-    auto digit = [&](uint32_t k) -> uint32_t { return (k < n_int ? d0[k] : frac_beg[k - n_int]) - '0'; };
+    auto digit = [&](uint32_t k) -> uint32_t { return at(k < n_int ? d0 + k : frac_beg + (k - n_int)) - '0'; };
     uint32_t first = n_all, last = 0;
     for (uint32_t k = 0; k < n_all; k++)
         if (digit(k)) {
@@ -379,6 +380,10 @@ __device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_
     if (!decimal_to_double(w, e10, neg, &bits)) return GPUDIFF_TOK_NUMBER;
     *val = bits;
     return GPUDIFF_TOK_OK;
+}
+// byte by byte from memory (K10 / K11 / K13: their larger kernels keep no window)
+__device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+    return parse_atom_core([&](uint64_t k) -> uint32_t { return p[k]; }, (uint64_t)(end - p), tag, val);
 }
 
 // parse_atom: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or
@@ -400,7 +405,10 @@ __device__ __forceinline__ uint32_t parse_atom_w(const uint8_t* p, const uint8_t
                                                  uint32_t* tag, uint64_t* val) {
     const uint64_t left = (uint64_t)(end - p);
     const uint32_t avail = left < 16u ? (uint32_t)left : 16u;
-    auto at = [&](uint32_t k) -> uint32_t { return (uint32_t)(((k < 8u ? w0 : w1) >> (8u * (k & 7u))) & 0xFFu); };
+    auto at = [&](uint32_t k) -> uint32_t {  // a select by mask (a ternary became a private array and scratch loads)
+        const uint64_t m = 0ull - (uint64_t)((k >> 3) & 1u);
+        return (uint32_t)((((w0 & ~m) | (w1 & m)) >> (8u * (k & 7u))) & 0xFFu);
+    };
     const uint32_t c = (uint32_t)(w0 & 0xFFu);
     if (c == 't' || c == 'f' || c == 'n') {
         const uint32_t n = c == 'f' ? 5u : 4u;
@@ -421,7 +429,19 @@ __device__ __forceinline__ uint32_t parse_atom_w(const uint8_t* p, const uint8_t
     // the start of a fraction or an exponent ('.', 'e', 'E' are no delimiters)
     const bool at_end = k == avail && left == avail;
     if (nd == 0 || nd > 15 || (at(d0) == '0' && nd > 1) || !(at_end || (k < avail && is_delim(at(k)))))
-        return parse_atom_mem(p, end, tag, val);
+    {
+        // floats, exponents, longer numbers, errors: the general parser over the window; an atom that runs past it
+        // (the parser asked for byte 16 or later) is parsed again from memory
+        bool spill = false;
+        const uint32_t e = parse_atom_core(
+            [&](uint64_t j) -> uint32_t {
+                if (j < 16u) return at((uint32_t)j);
+                spill = true;
+                return 0xFFu;  // neither a digit, a sign, '.', 'e' nor a delimiter: the parse stops here
+            },
+            left, tag, val);
+        return spill ? parse_atom_mem(p, end, tag, val) : e;
+    }
     *tag = GPUDIFF_TAG_INT;
     *val = d0 ? 0ull - v : v;
     return GPUDIFF_TOK_OK;
