@@ -517,17 +517,45 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
 
     const uint64_t seed = slots ? ((slots[links[doc_i].slot].flags >> 8) & 0xFFu) : D.seed;
     mark(1);
+    // which leaves the blob encodes, and which nodes its path table lists (phases 3a and 5)
+    auto region_of = [&](uint32_t w) -> uint32_t {  // 1 spec, 2 status, 0 not encoded
+        if (!(w & NI_LEAF)) return 0u;
+        const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
+        if (reg == R_SPEC || (reg == R_LABELS && labels_ok) || (reg == R_ANNOT && annot_ok)) return 1u;
+        return reg == R_STATUS ? 2u : 0u;
+    };
+    // path-table nodes: the region leaves and their ancestors but the root -- every container of the spec / status
+    // subtrees, and metadata, metadata.labels and metadata.annotations when label / annotation leaves are encoded
+    const bool lab_in = status == GPUDIFF_TOK_OK && labels_node != NONE && labels_ok && !(S.rec[labels_node].w & NI_LEAF);
+    const bool ann_in = status == GPUDIFF_TOK_OK && annot_node != NONE && annot_ok && !(S.rec[annot_node].w & NI_LEAF);
+    const bool meta_in = lab_in || ann_in;
+    auto in_tab = [&](uint32_t i, uint32_t w) -> bool {
+        if (region_of(w)) return true;
+        const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
+        if (!(w & NI_LEAF) && (reg == R_SPEC || reg == R_STATUS)) return true;
+        return (i == meta_node && meta_in) || (i == labels_node && lab_in) || (i == annot_node && ann_in);
+    };
+    // per lane: spec / status leaves, their arena bytes, path-table nodes and key bytes (summed for phase 5)
+    uint32_t c_ls = 0, c_lt = 0, c_ar[2] = {0u, 0u}, c_nt = 0, c_kb = 0;
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
         uint32_t err = GPUDIFF_TOK_OK;
         // three dependent rounds of loads per 64 nodes, each issued for every lane before any is waited for:
-        // the record; the token positions of its key and value; 16 bytes at the value and 8 at a root key
+        // the record; the token positions of its key and value; 16 bytes at the value and 8 at a root key.
+        // Strings that need decoding (an escape, a non-ASCII byte) are decoded after the batch, one at a time by
+        // the whole wave: their raw bytes staged into LDS with coalesced loads, then unescaped from there (a
+        // lane's byte-by-byte loop over global memory paid a dependent round trip per byte -- config3's
+        // Deployments carry one such 50-byte command string each, profiles/r05f)
         for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
             const uint32_t i = i0 + lane;
-            if (i >= nn) break;
-            const uint4 r = S.rec[i];
-            const bool key = (r.y & KEYBIT) != 0u, leaf = (r.w & NI_LEAF) != 0u;
+            const bool live = i < nn;
+            uint4 r = make_uint4(0u, 0u, 0u, 0u);
+            if (live) r = S.rec[i];
+            const uint32_t rg = live ? region_of(r.w) : 0u;
+            const bool tb = live && in_tab(i, r.w);
+            const bool key = live && (r.y & KEYBIT) != 0u, leaf = live && (r.w & NI_LEAF) != 0u;
             const bool str = leaf && (r.w & NI_STR), atom = leaf && (r.w & NI_ATOM);
+            const bool slow = str && (r.w & NI_SLOW);
             const uint32_t kt = r.y & ~KEYBIT;
             uint32_t kop = 0, kcp = 0, vop = 0, vcp = 0;
             if (key) {
@@ -538,8 +566,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             if (str) vcp = S.tok[r.z + 1] & POS_MASK;
             const uint8_t* vp = d + vop + (str ? 1u : 0u);
             uint64_t w0 = 0, w1 = 0, kw = 0;
-            if (str || atom) ld16u(vp, &w0, &w1);
+            if ((str && !slow) || atom) ld16u(vp, &w0, &w1);
             if (key && r.x == 0) kw = ld8u(d + kop + 1);
+            bool store = leaf && !slow;
             if (key) {
                 // a member's key span for phase 3b's hash (kept in the sort-key area, unused until phase 4)
                 S.skey[i] = ((uint64_t)(kcp - kop - 1) << 32) | (kop + 1);
@@ -547,37 +576,69 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
                 if (r.x == 0 && kcp - kop - 1 == 5u && (kw & 0xDFDFDFDFDFull) == 0x534D455449ull) {
                     err = GPUDIFF_TOK_LIST;
-                    continue;
+                    store = false;
                 }
             }
-            if (!leaf) continue;
             uint32_t tag = r.w & NI_TAG, mlen = 0;
             uint64_t v = 0;
-            if (str) {
-                uint32_t sl = vcp - vop - 1;
-                if (r.w & NI_SLOW) {
-                    uint8_t* dst = S.str + vop + 1;
-                    const int dl = decode_string(vp, d + vcp, d + len, dst);
-                    if (dl < 0) {
-                        err = GPUDIFF_TOK_STRING;
-                        continue;
-                    }
-                    sl = (uint32_t)dl;
-                    w0 = ld8u(dst);
-                }
+            if (store && str) {
+                const uint32_t sl = vcp - vop - 1;
                 mlen = sl;
                 // the value's first 8 bytes (a long string's tail goes to the arena in phase 5)
                 v = sl >= GPUDIFF_INLINE_MAX ? w0 : sl ? (w0 & (~0ull >> (64u - 8u * sl))) : 0ull;
-            } else if (atom) {
+            } else if (store && atom) {
                 const uint32_t e = parse_atom_w(vp, d + len, w0, w1, &tag, &v);
                 if (e) {
                     err = e;
-                    continue;
+                    store = false;
                 }
                 mlen = (tag == GPUDIFF_TAG_INT || tag == GPUDIFF_TAG_FLOAT) ? 8u : 0u;
             }
-            S.val[i] = v;
-            S.meta[i] = (mlen << 3) | tag;
+            if (store) {
+                S.val[i] = v;
+                S.meta[i] = (mlen << 3) | tag;
+            }
+            // the blob's sizes (phase 5), counted here where every operand is in registers
+            if (rg == 1u) c_ls++;
+            if (rg == 2u) c_lt++;
+            if (rg && store) c_ar[rg - 1u] += meta_arena((mlen << 3) | tag);
+            if (tb) {
+                c_nt++;
+                if (key) c_kb += kcp - kop - 1;
+            }
+            for (uint64_t sm = ballot(slow); sm; sm &= sm - 1) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(sm);
+                const uint32_t sop = rdlane(vop, k), scp = rdlane(vcp, k);
+                const uint32_t raw = scp - sop - 1;  // bytes between the quotes
+                uint8_t* dst = S.str + sop + 1;
+                int dl;
+                if (raw + 1u <= kLdsPerWave - 16u) {
+                    // the raw bytes and the closing quote into LDS (16 B a lane, up to 1 KiB a step); a \u escape
+                    // never reads past the quote (its fourth digit position holds it), so [p, quote + 1) suffices
+                    const uint8_t* src = d + sop + 1;
+                    for (uint32_t o = 16u * lane; o < raw + 1u; o += 1024u) {
+                        const uint64_t a0 = ld8u(src + o), a1 = ld8u(src + o + 8u);
+                        *(uint64_t*)(lds + o) = a0;
+                        *(uint64_t*)(lds + o + 8u) = a1;
+                    }
+                    lds_order();
+                    dl = lane == k ? decode_string(lds, lds + raw, lds + raw + 1u, dst) : 0;
+                    lds_order();
+                } else {
+                    dl = lane == k ? decode_string(d + sop + 1, d + scp, d + len, dst) : 0;
+                }
+                if (lane == k) {
+                    if (dl < 0) {
+                        err = GPUDIFF_TOK_STRING;
+                    } else {
+                        const uint32_t sl = (uint32_t)dl;
+                        const uint64_t h8 = ld8u(dst);
+                        S.val[i] = sl >= GPUDIFF_INLINE_MAX ? h8 : sl ? (h8 & (~0ull >> (64u - 8u * sl))) : 0ull;
+                        S.meta[i] = (sl << 3) | GPUDIFF_TAG_STR;
+                        if (rg) c_ar[rg - 1u] += meta_arena((sl << 3) | GPUDIFF_TAG_STR);
+                    }
+                }
+            }
         }
         const uint32_t e = wave_max(err);  // any error: SYNTAX < NUMBER < ... all nonzero
         if (e) status = e;
@@ -691,51 +752,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     o.n_nodes = nn;
     o.oflags = has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
     if (status == GPUDIFF_TOK_OK) {
-        auto region_of = [&](uint32_t w) -> uint32_t {  // 1 spec, 2 status, 0 not encoded
-            if (!(w & NI_LEAF)) return 0u;
-            const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
-            if (reg == R_SPEC || (reg == R_LABELS && labels_ok) || (reg == R_ANNOT && annot_ok)) return 1u;
-            return reg == R_STATUS ? 2u : 0u;
-        };
-        // path-table nodes: the region leaves and their ancestors but the root -- every
-        // container of the spec / status subtrees, and metadata, metadata.labels and
-        // metadata.annotations when label / annotation leaves are encoded
-        const bool lab_in = labels_node != NONE && labels_ok && !(S.rec[labels_node].w & NI_LEAF);
-        const bool ann_in = annot_node != NONE && annot_ok && !(S.rec[annot_node].w & NI_LEAF);
-        const bool meta_in = lab_in || ann_in;
-        auto in_tab = [&](uint32_t i, uint32_t w) -> bool {
-            if (region_of(w)) return true;
-            const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
-            if (!(w & NI_LEAF) && (reg == R_SPEC || reg == R_STATUS)) return true;
-            return (i == meta_node && meta_in) || (i == labels_node && lab_in) || (i == annot_node && ann_in);
-        };
-        auto key_span = [&](const uint4& r, uint32_t* op) -> uint32_t {  // key bytes of a member node
-            if (!(r.y & KEYBIT)) return 0u;
-            const uint32_t kt = r.y & ~KEYBIT;
-            *op = (S.tok[kt] & POS_MASK) + 1u;
-            return (S.tok[kt + 1] & POS_MASK) - *op;
-        };
-        uint32_t Ls = 0, Lt = 0, ARs = 0, ARt = 0, Nt = 0, KB = 0;
-        for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
-            const uint32_t j = j0 + lane;
-            uint32_t rg = 0, ar = 0, kl = 0;
-            bool t = false;
-            if (j < ns) {
-                const uint32_t i = sidx[j];
-                const uint4 r = S.rec[i];
-                rg = region_of(r.w);
-                if (rg) ar = meta_arena(S.meta[i]);
-                t = in_tab(i, r.w);
-                uint32_t op;
-                if (t) kl = key_span(r, &op);
-            }
-            Ls += popc64(ballot(rg == 1));
-            Lt += popc64(ballot(rg == 2));
-            Nt += popc64(ballot(t));
-            ARs += wave_sum(rg == 1 ? ar : 0u);
-            ARt += wave_sum(rg == 2 ? ar : 0u);
-            KB += wave_sum(kl);
-        }
+        // the sizes counted in phase 3a (sums over the nodes: the sort order does not change them)
+        const uint32_t Ls = wave_sum(c_ls), Lt = wave_sum(c_lt), Nt = wave_sum(c_nt), KB = wave_sum(c_kb);
+        uint32_t ARs = wave_sum(c_ar[0]), ARt = wave_sum(c_ar[1]);
         ARs = (ARs + 15u) & ~15u;  // gpudiff_arena_bytes: each arena a multiple of 16
         ARt = (ARt + 15u) & ~15u;
         const uint64_t seg_s = seg_bytes(Ls, ARs), seg_t = seg_bytes(Lt, ARt);
@@ -765,16 +784,33 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 uint32_t rg = 0, i = 0, m = 0, ar = 0, kl = 0, kop = 0;
                 uint4 r = make_uint4(0u, 0u, 0u, 0u);
                 bool t = false;
+                uint64_t val = 0, ph = root, ks = 0;
+                uint32_t vop = 0;
                 if (j < ns) {
                     i = sidx[j];
                     r = S.rec[i];
                     rg = region_of(r.w);
+                    t = in_tab(i, r.w);
+                    // one round of loads for everything this node needs: its value, its parent's hash, its key span
+                    // (phase 3a's, still in the sort-key area when the sort ran in LDS) and its string's position
                     if (rg) {
                         m = S.meta[i];
-                        ar = meta_arena(m);
+                        val = S.val[i];
                     }
-                    t = in_tab(i, r.w);
-                    if (t) kl = key_span(r, &kop);
+                    if (t && r.x != 0) ph = S.h[r.x] & mask;
+                    if (t && (r.y & KEYBIT)) {
+                        if (ns <= kLdsSort) {
+                            ks = S.skey[i];
+                        } else {
+                            const uint32_t kt = r.y & ~KEYBIT;
+                            const uint32_t kp = S.tok[kt] & POS_MASK, kq = S.tok[kt + 1] & POS_MASK;
+                            ks = ((uint64_t)(kq - kp - 1) << 32) | (kp + 1);
+                        }
+                    }
+                    if (rg && (r.w & NI_STR)) vop = S.tok[r.z] & POS_MASK;
+                    ar = meta_arena(m);
+                    kop = (uint32_t)ks;
+                    kl = (uint32_t)(ks >> 32);
                 }
                 uint32_t my_rank = 0, my_aoff = 0;
                 for (uint32_t g = 0; g < 2; g++) {
@@ -792,7 +828,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     const uint32_t L = Lr[g];
                     uint8_t* sp8 = segp[g];
                     // vals u64 | keys u32 | metas u32 (include/gpudiff_format.h); keys masked to <= 32 bits
-                    ((uint64_t*)sp8)[my_rank] = S.val[i];
+                    ((uint64_t*)sp8)[my_rank] = val;
                     ((uint32_t*)(sp8 + 8ull * L))[my_rank] = (uint32_t)skey[j];
                     ((uint32_t*)(sp8 + 12ull * L))[my_rank] = m;
                 }
@@ -803,7 +839,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 if (t) {
                     const uint32_t tr = trank + popc64(tbal & mask_lt(lane));
                     hs[tr] = skey[j];
-                    phs[tr] = r.x == 0 ? root : (S.h[r.x] & mask);
+                    phs[tr] = ph;
                     cs[tr] = (r.y & KEYBIT) ? (((uint64_t)kl << 32) | ko) : (GPUDIFF_TAB_INDEX | r.y);
                 }
                 trank += popc64(tbal);
@@ -818,8 +854,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 uint32_t* tdst = nullptr;
                 uint32_t tlen = 0;
                 if (tail) {
-                    const uint32_t op = S.tok[r.z] & POS_MASK;
-                    tsrc = ((r.w & NI_SLOW) ? (S.str + op + 1) : (d + op + 1)) + GPUDIFF_INLINE_MAX;
+                    tsrc = ((r.w & NI_SLOW) ? (S.str + vop + 1) : (d + vop + 1)) + GPUDIFF_INLINE_MAX;
                     tlen = (m >> 3) - GPUDIFF_INLINE_MAX;
                     tdst = (uint32_t*)(segp[rg - 1u] + 16ull * Lr[rg - 1u] + my_aoff);
                 }
