@@ -535,15 +535,15 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         if (!(w & NI_LEAF) && (reg == R_SPEC || reg == R_STATUS)) return true;
         return (i == meta_node && meta_in) || (i == labels_node && lab_in) || (i == annot_node && ann_in);
     };
-    // per lane: spec / status leaves, their arena bytes, path-table nodes and key bytes (summed for phase 5)
-    uint32_t c_ls = 0, c_lt = 0, c_ar[2] = {0u, 0u}, c_nt = 0, c_kb = 0;
+    // phase 5's sizes: spec / status leaves, their arena bytes, path-table nodes and their key bytes
+    uint32_t n_ls = 0, n_lt = 0, n_as = 0, n_at = 0, n_nt = 0, n_kb = 0;
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
-        uint32_t err = GPUDIFF_TOK_OK;
+        uint32_t err = GPUDIFF_TOK_OK, nslow = 0;
         // three dependent rounds of loads per 64 nodes, each issued for every lane before any is waited for:
         // the record; the token positions of its key and value; 16 bytes at the value and 8 at a root key.
         // Strings that need decoding (an escape, a non-ASCII byte) are decoded after the batch, one at a time by
-        // the whole wave: their raw bytes staged into LDS with coalesced loads, then unescaped from there (a
+        // the whole wave: their raw bytes staged into LDS with coalesced loads, then unescaped from there by lane 0 (a
         // lane's byte-by-byte loop over global memory paid a dependent round trip per byte -- config3's
         // Deployments carry one such 50-byte command string each, profiles/r05f)
         for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
@@ -598,47 +598,58 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 S.val[i] = v;
                 S.meta[i] = (mlen << 3) | tag;
             }
-            // the blob's sizes (phase 5), counted here where every operand is in registers
-            if (rg == 1u) c_ls++;
-            if (rg == 2u) c_lt++;
-            if (rg && store) c_ar[rg - 1u] += meta_arena((mlen << 3) | tag);
-            if (tb) {
-                c_nt++;
-                if (key) c_kb += kcp - kop - 1;
+            // the blob's sizes (phase 5), counted here where every operand is in registers (wave totals, scalar)
+            const uint32_t a = store ? meta_arena((mlen << 3) | tag) : 0u;
+            n_ls += popc64(ballot(rg == 1u));
+            n_lt += popc64(ballot(rg == 2u));
+            n_nt += popc64(ballot(tb));
+            n_as += wave_sum(rg == 1u ? a : 0u);
+            n_at += wave_sum(rg == 2u ? a : 0u);
+            n_kb += wave_sum(tb && key ? kcp - kop - 1 : 0u);
+            // strings that need decoding: listed (in the depth-order area, free until phase 3b) for after the loop
+            const uint64_t sm = ballot(slow);
+            if (slow) S.order[nslow + mbcnt64(sm)] = i;
+            nslow += popc64(sm);
+        }
+        if (nslow) wave_sync();
+        for (uint32_t j = 0; j < nslow; j++) {
+            const uint32_t i = S.order[j];
+            const uint4 r = S.rec[i];
+            const uint32_t sop = S.tok[r.z] & POS_MASK, scp = S.tok[r.z + 1] & POS_MASK;
+            const uint32_t raw = scp - sop - 1;  // bytes between the quotes
+            uint8_t* dst = S.str + sop + 1;
+            const uint8_t *sp = d + sop + 1, *se = d + scp, *sl_ = d + len;
+            if (raw + 1u <= kLdsPerWave - 16u) {
+                // the raw bytes and the closing quote into LDS (16 B a lane, up to 1 KiB a step); a \u escape never
+                // reads past the quote (its fourth digit position holds it), so [p, quote + 1) suffices
+                for (uint32_t o = 16u * lane; o < raw + 1u; o += 1024u) {
+                    const uint64_t a0 = ld8u(sp + o), a1 = ld8u(sp + o + 8u);
+                    *(uint64_t*)(lds + o) = a0;
+                    *(uint64_t*)(lds + o + 8u) = a1;
+                }
+                lds_order();
+                sp = lds;
+                se = lds + raw;
+                sl_ = lds + raw + 1u;
             }
-            for (uint64_t sm = ballot(slow); sm; sm &= sm - 1) {
-                const uint32_t k = (uint32_t)__builtin_ctzll(sm);
-                const uint32_t sop = rdlane(vop, k), scp = rdlane(vcp, k);
-                const uint32_t raw = scp - sop - 1;  // bytes between the quotes
-                uint8_t* dst = S.str + sop + 1;
-                int dl;
-                if (raw + 1u <= kLdsPerWave - 16u) {
-                    // the raw bytes and the closing quote into LDS (16 B a lane, up to 1 KiB a step); a \u escape
-                    // never reads past the quote (its fourth digit position holds it), so [p, quote + 1) suffices
-                    const uint8_t* src = d + sop + 1;
-                    for (uint32_t o = 16u * lane; o < raw + 1u; o += 1024u) {
-                        const uint64_t a0 = ld8u(src + o), a1 = ld8u(src + o + 8u);
-                        *(uint64_t*)(lds + o) = a0;
-                        *(uint64_t*)(lds + o + 8u) = a1;
-                    }
-                    lds_order();
-                    dl = lane == k ? decode_string(lds, lds + raw, lds + raw + 1u, dst) : 0;
-                    lds_order();
+            uint32_t sa = 0;
+            if (lane == 0) {
+                const int dl = decode_string(sp, se, sl_, dst);
+                if (dl < 0) {
+                    err = GPUDIFF_TOK_STRING;
                 } else {
-                    dl = lane == k ? decode_string(d + sop + 1, d + scp, d + len, dst) : 0;
-                }
-                if (lane == k) {
-                    if (dl < 0) {
-                        err = GPUDIFF_TOK_STRING;
-                    } else {
-                        const uint32_t sl = (uint32_t)dl;
-                        const uint64_t h8 = ld8u(dst);
-                        S.val[i] = sl >= GPUDIFF_INLINE_MAX ? h8 : sl ? (h8 & (~0ull >> (64u - 8u * sl))) : 0ull;
-                        S.meta[i] = (sl << 3) | GPUDIFF_TAG_STR;
-                        if (rg) c_ar[rg - 1u] += meta_arena((sl << 3) | GPUDIFF_TAG_STR);
-                    }
+                    const uint32_t sl = (uint32_t)dl;
+                    const uint64_t h8 = ld8u(dst);
+                    S.val[i] = sl >= GPUDIFF_INLINE_MAX ? h8 : sl ? (h8 & (~0ull >> (64u - 8u * sl))) : 0ull;
+                    S.meta[i] = (sl << 3) | GPUDIFF_TAG_STR;
+                    sa = meta_arena((sl << 3) | GPUDIFF_TAG_STR);
                 }
             }
+            sa = rdlane(sa, 0);
+            const uint32_t rg = region_of(r.w);
+            if (rg == 1u) n_as += sa;
+            if (rg == 2u) n_at += sa;
+            lds_order();
         }
         const uint32_t e = wave_max(err);  // any error: SYNTAX < NUMBER < ... all nonzero
         if (e) status = e;
@@ -753,10 +764,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     o.oflags = has_status ? GPUDIFF_OBJ_HAS_STATUS : 0u;
     if (status == GPUDIFF_TOK_OK) {
         // the sizes counted in phase 3a (sums over the nodes: the sort order does not change them)
-        const uint32_t Ls = wave_sum(c_ls), Lt = wave_sum(c_lt), Nt = wave_sum(c_nt), KB = wave_sum(c_kb);
-        uint32_t ARs = wave_sum(c_ar[0]), ARt = wave_sum(c_ar[1]);
-        ARs = (ARs + 15u) & ~15u;  // gpudiff_arena_bytes: each arena a multiple of 16
-        ARt = (ARt + 15u) & ~15u;
+        const uint32_t Ls = n_ls, Lt = n_lt, Nt = n_nt, KB = n_kb;
+        const uint32_t ARs = (n_as + 15u) & ~15u;  // gpudiff_arena_bytes: each arena a multiple of 16
+        const uint32_t ARt = (n_at + 15u) & ~15u;
         const uint64_t seg_s = seg_bytes(Ls, ARs), seg_t = seg_bytes(Lt, ARt);
         const uint64_t body = (seg_s + seg_t + 127u) & ~127ull;  // gpudiff_blob_body: 128-B line multiples
         const uint64_t tab = (24ull * Nt + KB + 127u) & ~127ull; // gpudiff_tab_bytes
