@@ -355,12 +355,18 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         lds_order();
         int32_t lvl_c = 0;                   // level at the batch start
         uint32_t pc1 = 0, pc2 = 0, pc3 = 0;  // codes of the three tokens before the batch (0: none)
+        // tokens two batches deep in registers: a batch needs the next one's first two (lookahead), and the load of
+        // the batch after that is issued a whole batch before it is used
+        uint32_t t_cur = lane < ntok ? S.tok[lane] : 0u;
+        uint32_t t_nxt = 64u + lane < ntok ? S.tok[64u + lane] : 0u;
         for (uint32_t tb = 0; tb < ntok; tb += 64) {
             const bool live = tb + lane < ntok;
-            const uint32_t t = live ? S.tok[tb + lane] : 0u;
+            const uint32_t t = t_cur;
+            const uint32_t t_far = tb + 128u + lane < ntok ? S.tok[tb + 128u + lane] : 0u;
             const uint32_t code = t >> 24;
-            const uint32_t tx = (lane < 2u && tb + 64u + lane < ntok) ? S.tok[tb + 64u + lane] : 0u;
-            const uint32_t nx0 = rdlane(tx, 0) >> 24, nx1 = rdlane(tx, 1) >> 24;
+            const uint32_t nx0 = rdlane(t_nxt, 0) >> 24, nx1 = rdlane(t_nxt, 1) >> 24;
+            t_cur = t_nxt;
+            t_nxt = t_far;
             const uint32_t cp1 = wave_shr1(code, pc1), cp2 = wave_shr1(cp1, pc2), cp3 = wave_shr1(cp2, pc3);
             const uint32_t cn1 = wave_shl1(code, nx0), cn2 = wave_shl1(cn1, nx1);
             const bool is_o = live && (code == '{' || code == '[');
