@@ -53,8 +53,11 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                                                      const DocLink* __restrict__ links) {
     // per wave, one LDS area reused phase by phase (5 KiB -> 8 workgroups of 4 waves per CU):
     //   phase 1: [0, 2048) byte ring; phase 2: [2048, 4096) container stack;
-    //   phase 3b: [0, 2048) depth histogram + cursors, [2048, ..) depth order (<= kLdsOrder nodes) or order +
-    //   hashes [3072, 5120) (<= kLdsHash nodes); phase 4: [0, 4608) sort (ns <= kLdsSort)
+    //   phases 3a-3b, small documents (<= kLdsHash nodes, depth < 32): [0, 256) depth histogram + cursors,
+    //   [256, 2304) the nodes' hash inputs, [2304, 2816) depth order (u16), [3072, 5120) hashes; phase 3a's decoded
+    //   strings staged at [2304, 5120) after its loop;
+    //   phase 3b, other documents: [0, 2048) depth histogram + cursors, [2048, ..) depth order (<= kLdsOrder nodes);
+    //   phase 4: [0, 4608) sort (ns <= kLdsSort)
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[kWavesPerBlock][kLdsPerWave];
 
     const uint32_t lane = lane_id();
@@ -62,8 +65,6 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     const uint32_t doc_i = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wib);
     if (doc_i >= n_docs) return;
     uint8_t* lds = s_lds[wib];
-    uint32_t* stk_node = (uint32_t*)(lds + 2048);
-    uint32_t* stk_meta = (uint32_t*)(lds + 3072);
     uint32_t* hist = (uint32_t*)lds;
     uint32_t* cur = (uint32_t*)(lds + 1024);
 
@@ -543,6 +544,16 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     };
     // phase 5's sizes: spec / status leaves, their arena bytes, path-table nodes and their key bytes
     uint32_t n_ls = 0, n_lt = 0, n_as = 0, n_at = 0, n_nt = 0, n_kb = 0;
+    // small documents: phase 3a also counts the nodes per depth and leaves each node's hash inputs in LDS (key bytes'
+    // offset or array index; parent, depth, key length), so phase 3b orders and hashes them without reloading records
+    bool small = nn <= kLdsHash && max_depth < 32u;
+    uint32_t* const h32 = (uint32_t*)lds;           // nodes per depth
+    uint32_t* const c32 = (uint32_t*)(lds + 128);   // depth cursors
+    uint2* const hin = (uint2*)(lds + 256);         // x: key offset or index; y: parent | depth << 8 | key << 13 | klen << 16
+    uint16_t* const ord16 = (uint16_t*)(lds + 2304);
+    constexpr uint32_t kStage = 2304;               // phase 3a's decoded strings are staged from here
+    if (small && lane < 32u) h32[lane] = 0u;
+    lds_order();
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
         uint32_t err = GPUDIFF_TOK_OK, nslow = 0;
@@ -604,6 +615,12 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 S.val[i] = v;
                 S.meta[i] = (mlen << 3) | tag;
             }
+            if (small && live) {
+                const uint32_t dep = (r.w >> NI_DEPTH_SHIFT) & 0xFFu, kl = kcp - kop - 1;
+                atomicAdd(&h32[dep], 1u);
+                hin[i] = make_uint2(key ? kop + 1 : r.y, r.x | (dep << 8) | (key ? (1u << 13) | (kl << 16) : 0u));
+            }
+            if (ballot(key && kcp - kop - 1 > 0xFFFFu)) small = false;  // a key length the inputs cannot hold
             // the blob's sizes (phase 5), counted here where every operand is in registers (wave totals, scalar)
             const uint32_t a = store ? meta_arena((mlen << 3) | tag) : 0u;
             n_ls += popc64(ballot(rg == 1u));
@@ -625,18 +642,19 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint32_t raw = scp - sop - 1;  // bytes between the quotes
             uint8_t* dst = S.str + sop + 1;
             const uint8_t *sp = d + sop + 1, *se = d + scp, *sl_ = d + len;
-            if (raw + 1u <= kLdsPerWave - 16u) {
+            if (raw + 1u <= kLdsPerWave - kStage - 16u) {
                 // the raw bytes and the closing quote into LDS (16 B a lane, up to 1 KiB a step); a \u escape never
                 // reads past the quote (its fourth digit position holds it), so [p, quote + 1) suffices
+                uint8_t* const st = lds + kStage;
                 for (uint32_t o = 16u * lane; o < raw + 1u; o += 1024u) {
                     const uint64_t a0 = ld8u(sp + o), a1 = ld8u(sp + o + 8u);
-                    *(uint64_t*)(lds + o) = a0;
-                    *(uint64_t*)(lds + o + 8u) = a1;
+                    *(uint64_t*)(st + o) = a0;
+                    *(uint64_t*)(st + o + 8u) = a1;
                 }
                 lds_order();
-                sp = lds;
-                se = lds + raw;
-                sl_ = lds + raw + 1u;
+                sp = st;
+                se = st + raw;
+                sl_ = st + raw + 1u;
             }
             uint32_t sa = 0;
             if (lane == 0) {
@@ -669,7 +687,40 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     // with no fence on the global stores between levels
     const bool h_in_lds = nn <= kLdsHash;
     uint64_t* const hl = (uint64_t*)(lds + 2048 + 4 * kLdsHash);
-    if (status == GPUDIFF_TOK_OK && nn > 1) {
+    if (status == GPUDIFF_TOK_OK && nn > 1 && small) {
+        // small documents: everything but the key bytes is in LDS -- the depth order from phase 3a's counts, then
+        // level by level a lane per node: its inputs and its parent's hash from LDS, its key bytes from the JSON
+        const uint32_t cnt = lane <= max_depth ? h32[lane] : 0u;
+        const uint32_t inc = wave_incl_scan(cnt);
+        if (lane <= max_depth) c32[lane] = inc - cnt;
+        lds_order();
+        for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            if (i < nn) {
+                const uint32_t p = atomicAdd(&c32[(hin[i].y >> 8) & 31u], 1u);
+                ord16[p] = (uint16_t)i;
+            }
+        }
+        lds_order();
+        uint32_t beg = 0;
+        for (uint32_t dep = 1; dep <= max_depth; dep++) {
+            const uint32_t n_d = rdlane(cnt, dep);
+            for (uint32_t j0 = 0; j0 < n_d; j0 += 64) {
+                if (j0 + lane < n_d) {
+                    const uint32_t i = ord16[beg + j0 + lane];
+                    const uint2 in = hin[i];
+                    const uint32_t par = in.y & 0xFFu;
+                    const uint64_t ph = par == 0u ? seed : hl[par];
+                    const uint64_t hh = (in.y & (1u << 13)) ? hash_key(ph, d + in.x, in.y >> 16) : hash_index(ph, in.x);
+                    S.h[i] = hh;
+                    hl[i] = hh;
+                }
+            }
+            beg += n_d;
+            lds_order();  // the next level reads these hashes
+        }
+        wave_sync();  // phases 4-5 read S.h
+    } else if (status == GPUDIFF_TOK_OK && nn > 1) {
         uint32_t* order = nn - 1 <= kLdsOrder ? (uint32_t*)(lds + 2048) : S.order;
         // counting sort of nodes by depth
         for (uint32_t i = lane; i <= kMaxDepth; i += 64) hist[i] = 0;
