@@ -386,12 +386,7 @@ __device__ uint32_t parse_atom_mem(const uint8_t* p, const uint8_t* end, uint32_
     return parse_atom_core([&](uint64_t k) -> uint32_t { return p[k]; }, (uint64_t)(end - p), tag, val);
 }
 
-// parse_atom: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or
-// the document's end -- from a 16-byte register window (three aligned-word loads issued together instead of a
-// dependent load per byte); everything else (floats, exponents, longer numbers, any syntax doubt) goes to
-// parse_atom_mem, so results are parse_atom_mem's by construction.  kTokSlack >= 32 keeps the loads inside the
-// staged buffer.  K0 (encode mode) only.
-// the 16 bytes at p in two registers (three aligned-word loads issued together; p + 23 must be readable)
+// the bytes at p in two / four registers (aligned-word loads issued together; p + 23 must be readable)
 __device__ __forceinline__ void ld16u(const uint8_t* p, uint64_t* w0, uint64_t* w1) {
     const uintptr_t a = (uintptr_t)p;
     const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
@@ -400,56 +395,131 @@ __device__ __forceinline__ void ld16u(const uint8_t* p, uint64_t* w0, uint64_t* 
     *w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
     *w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
 }
-// parse_atom over its window w0, w1 = the 16 bytes at p (ld16u), loaded by the caller with its other loads
-__device__ __forceinline__ uint32_t parse_atom_w(const uint8_t* p, const uint8_t* end, uint64_t w0, uint64_t w1,
-                                                 uint32_t* tag, uint64_t* val) {
-    const uint64_t left = (uint64_t)(end - p);
+// (ld32u: only the words wholly before lim are read, the others are zero -- a document is readable to kTokSlack = 32
+// bytes past its end, and a 32-byte window at its last bytes reaches up to 40)
+__device__ __forceinline__ void ld32u(const uint8_t* p, const uint8_t* lim, uint64_t& w0, uint64_t& w1, uint64_t& w2,
+                                      uint64_t& w3) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint64_t* ql = (const uint64_t*)lim;
+    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q + 4 <= ql ? q[3] : 0ull, x4 = q + 5 <= ql ? q[4] : 0ull;
+    w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
+    w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+    w2 = sh ? (x2 >> sh) | (x3 << (64u - sh)) : x2;
+    w3 = sh ? (x3 >> sh) | (x4 << (64u - sh)) : x3;
+}
+// byte k of a 16-byte window: a select by mask (a ternary became a private array and scratch loads)
+__device__ __forceinline__ uint32_t win16_at(uint64_t w0, uint64_t w1, uint32_t k) {
+    const uint64_t m = 0ull - (uint64_t)((k >> 3) & 1u);
+    return (uint32_t)((((w0 & ~m) | (w1 & m)) >> (8u * (k & 7u))) & 0xFFu);
+}
+// K0's sort of up to 192 node keys held in LDS (skey, with sidx = position + 1): lane k ranks keys k, k + 64, k + 128
+// by counting the keys below each -- all ns read two at a time by a broadcast ds_read_b128 -- then writes each key
+// and its node to its rank. Ranks are a permutation when the keys are distinct; an equal pair (a duplicate or a
+// collision under the seed) or a key equal to the root's hash sets GPUDIFF_TOK_HASH, as the bitonic path's check
+template <int NK>
+__device__ __forceinline__ void rank_sort_n(uint64_t* skey, uint32_t* sidx, uint32_t ns, uint32_t lane, uint64_t root,
+                                            uint32_t& status) {
+    uint64_t k[NK];
+    uint32_t r[NK], e[NK];
+#pragma unroll
+    for (int q = 0; q < NK; q++) {
+        k[q] = lane + 64u * q < ns ? skey[lane + 64u * q] : 0ull;
+        r[q] = 0u;
+        e[q] = 0u;
+    }
+    const uint32_t np = ns & ~1u;
+    for (uint32_t j = 0; j < np; j += 2) {
+        const uint64_t a = skey[j], b = skey[j + 1];
+#pragma unroll
+        for (int q = 0; q < NK; q++) {
+            r[q] += (uint32_t)(a < k[q]) + (uint32_t)(b < k[q]);
+            e[q] += (uint32_t)(a == k[q]) + (uint32_t)(b == k[q]);
+        }
+    }
+    if (np < ns) {
+        const uint64_t a = skey[np];
+#pragma unroll
+        for (int q = 0; q < NK; q++) {
+            r[q] += (uint32_t)(a < k[q]);
+            e[q] += (uint32_t)(a == k[q]);
+        }
+    }
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < NK; q++)
+        if (lane + 64u * q < ns && (e[q] > 1u || k[q] == root)) dup = true;
+    if (__builtin_amdgcn_ballot_w64(dup)) {
+        status = GPUDIFF_TOK_HASH;
+        return;
+    }
+    __asm__ volatile("" ::: "memory");  // every read above is issued before a write below (LDS runs in order)
+#pragma unroll
+    for (int q = 0; q < NK; q++)
+        if (lane + 64u * q < ns) {
+            skey[r[q]] = k[q];
+            sidx[r[q]] = lane + 64u * q + 1u;
+        }
+    __asm__ volatile("" ::: "memory");
+}
+__device__ __forceinline__ void rank_sort(uint64_t* skey, uint32_t* sidx, uint32_t ns, uint32_t lane, uint64_t root,
+                                          uint32_t& status) {
+    if (ns <= 64u) rank_sort_n<1>(skey, sidx, ns, lane, root, status);
+    else rank_sort_n<2>(skey, sidx, ns, lane, root, status);
+}
+
+// K0's values pass: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or
+// the document's end -- from the 16-byte register window w0, w1 at the atom (left: bytes to the document's end).
+// 0: decided (tag, val); 1: not decided here -- floats, exponents, longer numbers, any syntax doubt go to
+// parse_atom_win (K0's slow-atom pass), whose answers are parse_atom_mem's, so results are by construction.
+__device__ __forceinline__ uint32_t parse_atom_fast(uint64_t w0, uint64_t w1, uint64_t left, uint32_t* tag,
+                                                    uint64_t* val) {
     const uint32_t avail = left < 16u ? (uint32_t)left : 16u;
-    auto at = [&](uint32_t k) -> uint32_t {  // a select by mask (a ternary became a private array and scratch loads)
-        const uint64_t m = 0ull - (uint64_t)((k >> 3) & 1u);
-        return (uint32_t)((((w0 & ~m) | (w1 & m)) >> (8u * (k & 7u))) & 0xFFu);
-    };
     const uint32_t c = (uint32_t)(w0 & 0xFFu);
     if (c == 't' || c == 'f' || c == 'n') {
         const uint32_t n = c == 'f' ? 5u : 4u;
         const uint64_t want = c == 't' ? 0x65757274ull : c == 'f' ? 0x65736c6166ull : 0x6c6c756eull;
-        if (avail >= n && (w0 & ((1ull << (8 * n)) - 1ull)) == want && (avail == n ? left == n : is_delim(at(n)))) {
+        if (avail >= n && (w0 & ((1ull << (8 * n)) - 1ull)) == want &&
+            (avail == n ? left == n : is_delim(win16_at(w0, w1, n)))) {
             *val = 0;
             *tag = c == 't' ? GPUDIFF_TAG_TRUE : c == 'f' ? GPUDIFF_TAG_FALSE : GPUDIFF_TAG_NULL;
-            return GPUDIFF_TOK_OK;
+            return 0u;
         }
-        return parse_atom_mem(p, end, tag, val);
+        return 1u;
     }
     const uint32_t d0 = c == '-' ? 1u : 0u;
     uint32_t k = d0;
     uint64_t v = 0;
-    while (k < avail && is_digit(at(k))) v = v * 10u + (at(k++) - '0');
+    while (k < avail && is_digit(win16_at(w0, w1, k))) v = v * 10u + (win16_at(w0, w1, k++) - '0');
     const uint32_t nd = k - d0;
     // accepted: 1..15 digits, no leading zero unless alone, then the document's end or a delimiter that is not
     // the start of a fraction or an exponent ('.', 'e', 'E' are no delimiters)
     const bool at_end = k == avail && left == avail;
-    if (nd == 0 || nd > 15 || (at(d0) == '0' && nd > 1) || !(at_end || (k < avail && is_delim(at(k)))))
-    {
-        // floats, exponents, longer numbers, errors: the general parser over the window; an atom that runs past it
-        // (the parser asked for byte 16 or later) is parsed again from memory
-        bool spill = false;
-        const uint32_t e = parse_atom_core(
-            [&](uint64_t j) -> uint32_t {
-                if (j < 16u) return at((uint32_t)j);
-                spill = true;
-                return 0xFFu;  // neither a digit, a sign, '.', 'e' nor a delimiter: the parse stops here
-            },
-            left, tag, val);
-        return spill ? parse_atom_mem(p, end, tag, val) : e;
-    }
+    if (nd == 0 || nd > 15 || (win16_at(w0, w1, d0) == '0' && nd > 1) ||
+        !(at_end || (k < avail && is_delim(win16_at(w0, w1, k)))))
+        return 1u;
     *tag = GPUDIFF_TAG_INT;
     *val = d0 ? 0ull - v : v;
-    return GPUDIFF_TOK_OK;
+    return 0u;
 }
-__device__ __forceinline__ uint32_t parse_atom(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
-    uint64_t w0, w1;
-    ld16u(p, &w0, &w1);
-    return parse_atom_w(p, end, w0, w1, tag, val);
+// any atom from the 32-byte register window w at p (ld32u); one that runs past the window is parsed from memory
+__device__ __forceinline__ uint32_t parse_atom_win(const uint8_t* p, const uint8_t* end, uint64_t w0, uint64_t w1,
+                                                   uint64_t w2, uint64_t w3, uint32_t* tag, uint64_t* val) {
+    bool spill = false;
+    const uint32_t e = parse_atom_core(
+        [&](uint64_t j) -> uint32_t {
+            if (j >= 32u) {
+                spill = true;
+                return 0xFFu;  // neither a digit, a sign, '.', 'e' nor a delimiter: the parse stops here
+            }
+            const uint32_t k = (uint32_t)j;  // selects by mask, as win16_at
+            const uint64_t m8 = 0ull - (uint64_t)((k >> 3) & 1u), m16 = 0ull - (uint64_t)((k >> 4) & 1u);
+            const uint64_t lo = (w0 & ~m8) | (w1 & m8), hi = (w2 & ~m8) | (w3 & m8);
+            return (uint32_t)((((lo & ~m16) | (hi & m16)) >> (8u * (k & 7u))) & 0xFFu);
+        },
+        (uint64_t)(end - p), tag, val);
+    return spill ? parse_atom_mem(p, end, tag, val) : e;
 }
 
 // ---- K10 (write path) helpers: Go 1.16 encodeState.string(s, escapeHTML=true)

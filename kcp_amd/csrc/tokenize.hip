@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     lds_order();
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
-        uint32_t err = GPUDIFF_TOK_OK, nslow = 0;
+        uint32_t err = GPUDIFF_TOK_OK, nslow = 0, natom = 0;
         // three dependent rounds of loads per 64 nodes, each issued for every lane before any is waited for:
         // the record; the token positions of its key and value; 16 bytes at the value and 8 at a root key.
         // Strings that need decoding (an escape, a non-ASCII byte) are decoded after the batch, one at a time by
@@ -598,15 +598,15 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             }
             uint32_t tag = r.w & NI_TAG, mlen = 0;
             uint64_t v = 0;
+            bool slow_atom = false;
             if (store && str) {
                 const uint32_t sl = vcp - vop - 1;
                 mlen = sl;
                 // the value's first 8 bytes (a long string's tail goes to the arena in phase 5)
                 v = sl >= GPUDIFF_INLINE_MAX ? w0 : sl ? (w0 & (~0ull >> (64u - 8u * sl))) : 0ull;
             } else if (store && atom) {
-                const uint32_t e = parse_atom_w(vp, d + len, w0, w1, &tag, &v);
-                if (e) {
-                    err = e;
+                if (parse_atom_fast(w0, w1, len - vop, &tag, &v)) {
+                    slow_atom = true;  // parsed after the loop
                     store = false;
                 }
                 mlen = (tag == GPUDIFF_TAG_INT || tag == GPUDIFF_TAG_FLOAT) ? 8u : 0u;
@@ -629,51 +629,96 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             n_as += wave_sum(rg == 1u ? a : 0u);
             n_at += wave_sum(rg == 2u ? a : 0u);
             n_kb += wave_sum(tb && key ? kcp - kop - 1 : 0u);
-            // strings that need decoding: listed (in the depth-order area, free until phase 3b) for after the loop
+            // strings that need decoding and atoms the window did not decide: listed for after the loop, the strings
+            // from the front of the depth-order area, the atoms from its back, each with its value's token positions
+            // in the hash area (both free until phase 3b)
             const uint64_t sm = ballot(slow);
-            if (slow) S.order[nslow + mbcnt64(sm)] = i;
+            if (slow) {
+                const uint32_t q = nslow + mbcnt64(sm);
+                S.order[q] = i;
+                S.h[q] = ((uint64_t)rg << 56) | ((uint64_t)vcp << 32) | vop;  // positions < 2^24
+            }
             nslow += popc64(sm);
+            const uint64_t am = ballot(slow_atom);
+            if (slow_atom) {
+                const uint32_t q = nn - 1u - (natom + mbcnt64(am));
+                S.order[q] = i;
+                S.h[q] = vop;
+            }
+            natom += popc64(am);
         }
-        if (nslow) wave_sync();
+        if (nslow | natom) wave_sync();
+        // atoms: a lane each, from a 32-byte window
+        for (uint32_t j0 = 0; j0 < natom; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            if (j < natom) {
+                const uint32_t q = nn - 1u - j;
+                const uint32_t i = S.order[q], aop = (uint32_t)S.h[q];
+                uint64_t w0, w1, w2, w3;
+                ld32u(d + aop, d + len + kTokSlack, w0, w1, w2, w3);
+                uint32_t tag = GPUDIFF_TAG_NULL;
+                uint64_t v = 0;
+                const uint32_t e = parse_atom_win(d + aop, d + len, w0, w1, w2, w3, &tag, &v);
+                if (e) {
+                    err = e;
+                } else {
+                    S.val[i] = v;
+                    S.meta[i] = (((tag == GPUDIFF_TAG_INT || tag == GPUDIFF_TAG_FLOAT) ? 8u : 0u) << 3) | tag;
+                }
+            }
+        }
+        // strings: one at a time by the wave (the next entry's loads issued while this one decodes)
+        uint32_t ni = nslow ? S.order[0] : 0u;
+        uint64_t npos = nslow ? S.h[0] : 0ull;
         for (uint32_t j = 0; j < nslow; j++) {
-            const uint32_t i = S.order[j];
-            const uint4 r = S.rec[i];
-            const uint32_t sop = S.tok[r.z] & POS_MASK, scp = S.tok[r.z + 1] & POS_MASK;
+            const uint32_t i = rdlane(ni, 0), sop = rdlane((uint32_t)npos, 0), hi = rdlane((uint32_t)(npos >> 32), 0);
+            const uint32_t scp = hi & 0xFFFFFFu, rg = hi >> 24;
+            if (j + 1u < nslow) {
+                ni = S.order[j + 1u];
+                npos = S.h[j + 1u];
+            }
             const uint32_t raw = scp - sop - 1;  // bytes between the quotes
-            uint8_t* dst = S.str + sop + 1;
-            const uint8_t *sp = d + sop + 1, *se = d + scp, *sl_ = d + len;
-            if (raw + 1u <= kLdsPerWave - kStage - 16u) {
-                // the raw bytes and the closing quote into LDS (16 B a lane, up to 1 KiB a step); a \u escape never
-                // reads past the quote (its fourth digit position holds it), so [p, quote + 1) suffices
+            uint8_t* const dst = S.str + sop + 1;
+            const uint32_t ob = (raw + 16u) & ~15u;  // the decoded bytes' offset in the staging area (<= raw of them)
+            int dl;
+            uint64_t h8 = 0;
+            if (ob + raw + 16u <= kLdsPerWave - kStage) {
+                // the raw bytes and the closing quote into LDS (16 B a lane, up to 1 KiB a step; a \u escape never
+                // reads past the quote: its fourth digit position holds it), unescaped there by lane 0, then the
+                // decoded bytes copied out by the wave
                 uint8_t* const st = lds + kStage;
+                const uint8_t* const sp = d + sop + 1;
                 for (uint32_t o = 16u * lane; o < raw + 1u; o += 1024u) {
                     const uint64_t a0 = ld8u(sp + o), a1 = ld8u(sp + o + 8u);
                     *(uint64_t*)(st + o) = a0;
                     *(uint64_t*)(st + o + 8u) = a1;
                 }
                 lds_order();
-                sp = st;
-                se = st + raw;
-                sl_ = st + raw + 1u;
-            }
-            uint32_t sa = 0;
-            if (lane == 0) {
-                const int dl = decode_string(sp, se, sl_, dst);
-                if (dl < 0) {
-                    err = GPUDIFF_TOK_STRING;
-                } else {
-                    const uint32_t sl = (uint32_t)dl;
-                    const uint64_t h8 = ld8u(dst);
-                    S.val[i] = sl >= GPUDIFF_INLINE_MAX ? h8 : sl ? (h8 & (~0ull >> (64u - 8u * sl))) : 0ull;
-                    S.meta[i] = (sl << 3) | GPUDIFF_TAG_STR;
-                    sa = meta_arena((sl << 3) | GPUDIFF_TAG_STR);
+                dl = lane == 0 ? decode_string(st, st + raw, st + raw + 1u, st + ob) : 0;
+                lds_order();
+                dl = (int)rdlane((uint32_t)dl, 0);
+                if (dl > 0) {
+                    for (uint32_t o = lane; o < (uint32_t)dl; o += 64u) dst[o] = st[ob + o];
+                    h8 = *(const uint64_t*)(st + ob);
                 }
+                lds_order();
+            } else {
+                dl = lane == 0 ? decode_string(d + sop + 1, d + scp, d + len, dst) : 0;
+                dl = (int)rdlane((uint32_t)dl, 0);
+                if (dl > 0 && lane == 0) h8 = ld8u(dst);
             }
-            sa = rdlane(sa, 0);
-            const uint32_t rg = region_of(r.w);
-            if (rg == 1u) n_as += sa;
-            if (rg == 2u) n_at += sa;
-            lds_order();
+            if (dl < 0) {
+                err = GPUDIFF_TOK_STRING;
+            } else if (lane == 0) {
+                const uint32_t sl = (uint32_t)dl;
+                S.val[i] = sl >= GPUDIFF_INLINE_MAX ? h8 : sl ? (h8 & (~0ull >> (64u - 8u * sl))) : 0ull;
+                S.meta[i] = (sl << 3) | GPUDIFF_TAG_STR;
+            }
+            if (dl > 0) {
+                const uint32_t sa = meta_arena(((uint32_t)dl << 3) | GPUDIFF_TAG_STR);
+                if (rg == 1u) n_as += sa;
+                if (rg == 2u) n_at += sa;
+            }
         }
         const uint32_t e = wave_max(err);  // any error: SYNTAX < NUMBER < ... all nonzero
         if (e) status = e;
@@ -785,34 +830,42 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             sidx[j] = j + 1;
         }
         wave_sync();
-        // bitonic sort, all comparators ascending (flip + half-cleaners):
-        // indices >= ns act as +inf and never move
-        for (uint32_t kk = 2; (kk >> 1) < ns; kk <<= 1) {
-            for (uint32_t dd = kk; dd >= 2; dd >>= 1) {
-                const bool flip = dd == kk;
-                for (uint32_t i = lane; i < ns; i += 64) {
-                    const uint32_t j = flip ? (i ^ (kk - 1u)) : (i ^ (dd >> 1));
-                    if (j > i && j < ns) {
-                        const uint64_t a = skey[i], b = skey[j];
-                        if (a > b) {
-                            const uint32_t ia = sidx[i], ib = sidx[j];
-                            skey[i] = b;
-                            skey[j] = a;
-                            sidx[i] = ib;
-                            sidx[j] = ia;
+        const uint64_t root = seed & mask;
+        if (ns <= 2u * 64u) {
+            // rank sort: a lane ranks its keys (up to three) against all ns keys, read two at a time by broadcast
+            // from LDS -- no barrier, no divergent exchange; an equal key (a duplicate or a collision under the seed)
+            // or the root's hash hands the document to the host, as below
+            rank_sort(skey, sidx, ns, lane, root, status);
+        } else {
+            // bitonic sort, all comparators ascending (flip + half-cleaners):
+            // indices >= ns act as +inf and never move
+            for (uint32_t kk = 2; (kk >> 1) < ns; kk <<= 1) {
+                for (uint32_t dd = kk; dd >= 2; dd >>= 1) {
+                    const bool flip = dd == kk;
+#pragma unroll 1
+                    for (uint32_t i = lane; i < ns; i += 64) {
+                        const uint32_t j = flip ? (i ^ (kk - 1u)) : (i ^ (dd >> 1));
+                        if (j > i && j < ns) {
+                            const uint64_t a = skey[i], b = skey[j];
+                            if (a > b) {
+                                const uint32_t ia = sidx[i], ib = sidx[j];
+                                skey[i] = b;
+                                skey[j] = a;
+                                sidx[i] = ib;
+                                sidx[j] = ia;
+                            }
                         }
                     }
+                    wave_sync();
                 }
-                wave_sync();
             }
+            // unique node hashes, none the root's: a parent hash in the path table
+            // then names exactly one node (include/gpudiff_format.h)
+            bool dup = false;
+            for (uint32_t j = lane; j < ns; j += 64)
+                if ((j && skey[j] == skey[j - 1]) || skey[j] == root) dup = true;
+            if (ballot(dup)) status = GPUDIFF_TOK_HASH;
         }
-        // unique node hashes, none the root's: a parent hash in the path table
-        // then names exactly one node (include/gpudiff_format.h)
-        const uint64_t root = seed & mask;
-        bool dup = false;
-        for (uint32_t j = lane; j < ns; j += 64)
-            if ((j && skey[j] == skey[j - 1]) || skey[j] == root) dup = true;
-        if (ballot(dup)) status = GPUDIFF_TOK_HASH;
     }
 
     mark(4);
