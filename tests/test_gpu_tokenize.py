@@ -102,7 +102,7 @@ EDGE_OK = [
     # atoms past the 16-byte window (K0's slow-atom pass: 32-byte window) and past 32 bytes (from memory)
     b'{"spec":{"n":[0.000000000000000000000000000000000001,-123456789.12345678900000000000000000,'
     b'1.00000000000000000000000000000000000000000000e-3,12345678901234.5,2.5]}}', b'{"a":2.5}', b'{"a":-7e-1}',
-    b'{"spec":{"t":1.5,"u":"x\ty","v":3.25e1,"w":"\u00e9","x":[0.5,true,"q\"r",-0.25]}}',
+    b'{"spec":{"t":1.5,"u":"x\\ty","v":3.25e1,"w":"\\u00e9","x":[0.5,true,"q\\"r",-0.25]}}',
     b'{"spec":{"t":true,"f":false,"z":null,"a":[true,false,null]}}',
     b'{"a":null,"b":1,"metadata":{"labels":{"x":"1","y":"2"},"annotations":{"k":"v","k2":"long value here"}}}',
     b'{"metadata":{"labels":{"x":"1","y":2}},"spec":1}', b'{"metadata":{"labels":{}},"spec":1}',
@@ -126,7 +126,7 @@ EDGE_DEFER = [
     (b'{"spec":{"i":123456789012345678901}}', G.TOK_NUMBER), (b'{"i":18446744073709551615}', G.TOK_NUMBER),
     (b'{"spec":{"f":1e400}}', G.TOK_NUMBER), (b'{"spec":{"f":0.12345678901234567890123}}', G.TOK_NUMBER),
     (b'{"spec":{"i":1234567890123456789012345678901234567890}}', G.TOK_NUMBER),
-    (b'{"spec":{"f":1.5,"g":1e23,"s":"a\nb"}}', G.TOK_NUMBER), (b'{"a":1.5e}', G.TOK_SYNTAX),
+    (b'{"spec":{"f":1.5,"g":1e23,"s":"a\\nb"}}', G.TOK_NUMBER), (b'{"a":1.5e}', G.TOK_SYNTAX),
     (b'{"sp\\u0065c":1}', G.TOK_KEY), ('{"spéc":{"a":1}}'.encode(), G.TOK_KEY),
     (b'{"spec":{"x":"\xff\xfe"}}', G.TOK_STRING), (b'{"spec":{"x":"a\x01b"}}', G.TOK_STRING),
     (b'{"spec":{"x":"a\\qb"}}', G.TOK_STRING), (b'{"spec":{"x":"\\u12"}}', G.TOK_STRING),
