@@ -146,6 +146,46 @@ __device__ __forceinline__ uint64_t hash_key(uint64_t seed, const uint8_t* k, ui
         return ld8u(k + 8u * i - 5u);
     });
 }
+// XXH64 of a stream of at most 32 bytes held in four registers (W0..W3: its 8-byte little-endian words), straight
+// code without loops or arrays: the same value as xxh64_words over those words
+__device__ __forceinline__ uint64_t xxh64_small(uint64_t seed, uint32_t L, uint64_t W0, uint64_t W1, uint64_t W2,
+                                                uint64_t W3) {
+    uint64_t h;
+    if (L >= 32u) {  // exactly one stripe
+        const uint64_t v1 = xround(seed + XP1 + XP2, W0), v2 = xround(seed + XP2, W1), v3 = xround(seed, W2),
+                       v4 = xround(seed - XP1, W3);
+        h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+        h = xmerge(xmerge(xmerge(xmerge(h, v1), v2), v3), v4);
+    } else {
+        h = seed + XP5;
+    }
+    h += L;
+    const uint32_t rem = L & 31u, n8 = rem >> 3;
+    if (n8 > 0u) h = xrotl(h ^ xround(0, W0), 27) * XP1 + XP4;
+    if (n8 > 1u) h = xrotl(h ^ xround(0, W1), 27) * XP1 + XP4;
+    if (n8 > 2u) h = xrotl(h ^ xround(0, W2), 27) * XP1 + XP4;
+    uint64_t wr = n8 == 0u ? W0 : n8 == 1u ? W1 : n8 == 2u ? W2 : W3;
+    uint32_t r = rem & 7u;
+    if (r >= 4u) {
+        h = xrotl(h ^ ((uint64_t)(uint32_t)wr * XP1), 23) * XP2 + XP3;
+        wr >>= 32;
+        r -= 4u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 3u; k++)
+        if (k < r) h = xrotl(h ^ (((wr >> (8u * k)) & 0xFFu) * XP5), 11) * XP1;
+    return xavalanche(h);
+}
+// hash_key over a key of at most 27 bytes held in registers: w0..w3 = the 32 bytes at the key (ld32u); word i >= 1
+// of the component holds key bytes [8i - 5, 8i + 3), the high five bytes of w[i - 1] and the low three of w[i]
+__device__ __forceinline__ uint64_t hash_key_w(uint64_t seed, uint32_t klen, uint64_t w0, uint64_t w1, uint64_t w2,
+                                               uint64_t w3) {
+    return xxh64_small(seed, klen + 5u, 0x01ull | ((uint64_t)klen << 8) | (w0 << 40), (w0 >> 24) | (w1 << 40),
+                       (w1 >> 24) | (w2 << 40), (w2 >> 24) | (w3 << 40));
+}
+__device__ __forceinline__ uint64_t hash_index_w(uint64_t seed, uint32_t idx) {
+    return xxh64_small(seed, 5u, 0x02ull | ((uint64_t)idx << 8), 0ull, 0ull, 0ull);
+}
 __device__ __forceinline__ uint64_t hash_index(uint64_t seed, uint32_t idx) {
     return xxh64_words(seed, 5u, [&](uint32_t) -> uint64_t { return 0x02ull | ((uint64_t)idx << 8); });
 }

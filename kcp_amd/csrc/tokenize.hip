@@ -356,6 +356,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         lds_order();
         int32_t lvl_c = 0;                   // level at the batch start
         uint32_t pc1 = 0, pc2 = 0, pc3 = 0;  // codes of the three tokens before the batch (0: none)
+        uint32_t pp1 = 0, pp2 = 0, pp3 = 0;  // ... and their positions
         // tokens two batches deep in registers: a batch needs the next one's first two (lookahead), and the load of
         // the batch after that is issued a whole batch before it is used
         uint32_t t_cur = lane < ntok ? S.tok[lane] : 0u;
@@ -365,11 +366,15 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint32_t t = t_cur;
             const uint32_t t_far = tb + 128u + lane < ntok ? S.tok[tb + 128u + lane] : 0u;
             const uint32_t code = t >> 24;
-            const uint32_t nx0 = rdlane(t_nxt, 0) >> 24, nx1 = rdlane(t_nxt, 1) >> 24;
+            const uint32_t tn0 = rdlane(t_nxt, 0), nx0 = tn0 >> 24, nx1 = rdlane(t_nxt, 1) >> 24;
             t_cur = t_nxt;
             t_nxt = t_far;
             const uint32_t cp1 = wave_shr1(code, pc1), cp2 = wave_shr1(cp1, pc2), cp3 = wave_shr1(cp2, pc3);
             const uint32_t cn1 = wave_shl1(code, nx0), cn2 = wave_shl1(cn1, nx1);
+            // positions of the key's quotes (two and three tokens back) and of a string's closing quote (next token)
+            const uint32_t pos = t & POS_MASK;
+            const uint32_t pm1 = wave_shr1(pos, pp1), pm2 = wave_shr1(pm1, pp2), pm3 = wave_shr1(pm2, pp3);
+            const uint32_t pn1 = wave_shl1(pos, tn0 & POS_MASK);
             const bool is_o = live && (code == '{' || code == '[');
             const bool is_c = live && (code == '}' || code == ']');
             const bool is_qo = live && (code == '"' || (code >= TK_OPENQ_SLOW && code <= TK_KEY_ANNOT));
@@ -485,6 +490,11 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     info |= (uint32_t)lvl << NI_DEPTH_SHIFT;
                 }
                 S.rec[id] = make_uint4(tb + lane == 0u ? NONE : e_id, comp, tb + lane, info);
+                if constexpr (MODE == kModeEncode) {
+                    // for phase 3a: a member's key span, a leaf's value positions (its slot until 3a fills it)
+                    if (comp & KEYBIT) S.skey[id] = ((uint64_t)(pm2 - pm3 - 1u) << 32) | (pm3 + 1u);
+                    S.val[id] = ((uint64_t)pn1 << 32) | pos;
+                }
             }
             const uint64_t ok_node = m_node & upto;
             const uint64_t m_meta = ballot(is_node && lvl == 1 && cp3 == TK_KEY_META && code == '{') & upto;
@@ -503,10 +513,13 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             }
             lvl_c += (int32_t)popc64(m_o) - (int32_t)popc64(m_c);
             const uint32_t kend = min(64u, ntok - tb);
-            const uint32_t o1 = pc1, o2 = pc2;
+            const uint32_t o1 = pc1, o2 = pc2, q1 = pp1, q2 = pp2;
             pc1 = rdlane(code, kend - 1u);
             pc2 = kend >= 2u ? rdlane(code, kend - 2u) : o1;
             pc3 = kend >= 3u ? rdlane(code, kend - 3u) : kend == 2u ? o1 : o2;
+            pp1 = rdlane(pos, kend - 1u);
+            pp2 = kend >= 2u ? rdlane(pos, kend - 2u) : q1;
+            pp3 = kend >= 3u ? rdlane(pos, kend - 3u) : kend == 2u ? q1 : q2;
         }
         if (status == GPUDIFF_TOK_OK && (ntok == 0u || lvl_c != 0)) status = GPUDIFF_TOK_SYNTAX;
     }
@@ -557,8 +570,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     // ------------------------------------------------------------ phase 3a: values (lane per node)
     if (status == GPUDIFF_TOK_OK) {
         uint32_t err = GPUDIFF_TOK_OK, nslow = 0, natom = 0;
-        // three dependent rounds of loads per 64 nodes, each issued for every lane before any is waited for:
-        // the record; the token positions of its key and value; 16 bytes at the value and 8 at a root key.
+        // two dependent rounds of loads per 64 nodes, each issued for every lane before any is waited for: the
+        // record with the key span and value positions the tree phase left beside it; 16 bytes at the value and 8
+        // at a root key.
         // Strings that need decoding (an escape, a non-ASCII byte) are decoded after the batch, one at a time by
         // the whole wave: their raw bytes staged into LDS with coalesced loads, then unescaped from there by lane 0 (a
         // lane's byte-by-byte loop over global memory paid a dependent round trip per byte -- config3's
@@ -573,22 +587,23 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const bool key = live && (r.y & KEYBIT) != 0u, leaf = live && (r.w & NI_LEAF) != 0u;
             const bool str = leaf && (r.w & NI_STR), atom = leaf && (r.w & NI_ATOM);
             const bool slow = str && (r.w & NI_SLOW);
-            const uint32_t kt = r.y & ~KEYBIT;
             uint32_t kop = 0, kcp = 0, vop = 0, vcp = 0;
             if (key) {
-                kop = S.tok[kt] & POS_MASK;
-                kcp = S.tok[kt + 1] & POS_MASK;
+                const uint64_t ks = S.skey[i];  // the tree phase's key span
+                kop = (uint32_t)ks - 1u;
+                kcp = kop + 1u + (uint32_t)(ks >> 32);
             }
-            if (str || atom) vop = S.tok[r.z] & POS_MASK;
-            if (str) vcp = S.tok[r.z + 1] & POS_MASK;
+            if (str || atom) {
+                const uint64_t pv = S.val[i];  // the tree phase's value positions
+                vop = (uint32_t)pv;
+                vcp = (uint32_t)(pv >> 32);
+            }
             const uint8_t* vp = d + vop + (str ? 1u : 0u);
             uint64_t w0 = 0, w1 = 0, kw = 0;
             if ((str && !slow) || atom) ld16u(vp, &w0, &w1);
             if (key && r.x == 0) kw = ld8u(d + kop + 1);
             bool store = leaf && !slow;
             if (key) {
-                // a member's key span for phase 3b's hash (kept in the sort-key area, unused until phase 4)
-                S.skey[i] = ((uint64_t)(kcp - kop - 1) << 32) | (kop + 1);
                 // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key
                 // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
                 if (r.x == 0 && kcp - kop - 1 == 5u && (kw & 0xDFDFDFDFDFull) == 0x534D455449ull) {
@@ -620,7 +635,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 atomicAdd(&h32[dep], 1u);
                 hin[i] = make_uint2(key ? kop + 1 : r.y, r.x | (dep << 8) | (key ? (1u << 13) | (kl << 16) : 0u));
             }
-            if (ballot(key && kcp - kop - 1 > 0xFFFFu)) small = false;  // a key length the inputs cannot hold
+            if (ballot(key && kcp - kop - 1 > 27u)) small = false;  // keys hashed from registers: <= 27 bytes
             // the blob's sizes (phase 5), counted here where every operand is in registers (wave totals, scalar)
             const uint32_t a = store ? meta_arena((mlen << 3) | tag) : 0u;
             n_ls += popc64(ballot(rg == 1u));
@@ -747,22 +762,34 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             }
         }
         lds_order();
-        uint32_t beg = 0;
-        for (uint32_t dep = 1; dep <= max_depth; dep++) {
-            const uint32_t n_d = rdlane(cnt, dep);
-            for (uint32_t j0 = 0; j0 < n_d; j0 += 64) {
-                if (j0 + lane < n_d) {
-                    const uint32_t i = ord16[beg + j0 + lane];
-                    const uint2 in = hin[i];
+        // 64 nodes of the depth order at a time: their key bytes loaded once (one round trip for every depth the
+        // batch spans), then a step per depth present -- a node's parent is at a smaller depth, so earlier in the
+        // order: hashed by an earlier batch or step
+        for (uint32_t c0 = 0; c0 + 1u < nn; c0 += 64) {
+            const uint32_t p = c0 + lane;
+            const bool live = p + 1u < nn;
+            uint32_t i = 0;
+            uint2 in = make_uint2(0u, 0u);
+            if (live) {
+                i = ord16[p];
+                in = hin[i];
+            }
+            const bool isk = live && (in.y & (1u << 13)) != 0u;
+            const uint32_t kl = in.y >> 16;
+            uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+            if (isk) ld32u(d + in.x, d + len + kTokSlack, w0, w1, w2, w3);
+            const uint32_t dep = (in.y >> 8) & 31u;
+            const uint32_t dlo = rdlane(dep, 0), dhi = rdlane(dep, min(63u, nn - 2u - c0));
+            for (uint32_t dd = dlo; dd <= dhi; dd++) {
+                if (live && dep == dd) {
                     const uint32_t par = in.y & 0xFFu;
                     const uint64_t ph = par == 0u ? seed : hl[par];
-                    const uint64_t hh = (in.y & (1u << 13)) ? hash_key(ph, d + in.x, in.y >> 16) : hash_index(ph, in.x);
+                    const uint64_t hh = isk ? hash_key_w(ph, kl, w0, w1, w2, w3) : hash_index_w(ph, in.x);
                     S.h[i] = hh;
                     hl[i] = hh;
                 }
+                lds_order();  // the next step reads these hashes
             }
-            beg += n_d;
-            lds_order();  // the next level reads these hashes
         }
         wave_sync();  // phases 4-5 read S.h
     } else if (status == GPUDIFF_TOK_OK && nn > 1) {
