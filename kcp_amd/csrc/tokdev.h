@@ -44,6 +44,7 @@ constexpr uint32_t kLdsPerWave = 5120;
 constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
 constexpr uint32_t kLdsOrder = 768;  // phase 3b's depth order in LDS up to this many nodes (4 B each, behind 2 KiB)
 constexpr uint32_t kLdsHash = 256;   // ... and up to this many nodes their hashes too (order 1 KiB + hashes 2 KiB)
+constexpr uint32_t kRank = 128;      // phase 4 ranks up to this many node keys in LDS (no sort arrays)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -454,24 +455,25 @@ __device__ __forceinline__ uint32_t win16_at(uint64_t w0, uint64_t w1, uint32_t 
     const uint64_t m = 0ull - (uint64_t)((k >> 3) & 1u);
     return (uint32_t)((((w0 & ~m) | (w1 & m)) >> (8u * (k & 7u))) & 0xFFu);
 }
-// K0's sort of up to 192 node keys held in LDS (skey, with sidx = position + 1): lane k ranks keys k, k + 64, k + 128
-// by counting the keys below each -- all ns read two at a time by a broadcast ds_read_b128 -- then writes each key
-// and its node to its rank. Ranks are a permutation when the keys are distinct; an equal pair (a duplicate or a
-// collision under the seed) or a key equal to the root's hash sets GPUDIFF_TOK_HASH, as the bitonic path's check
+// K0's sort of up to kRank node keys: keys[j] & mask (j < ns) are node j + 1's key, in LDS (phase 3b's hashes).
+// Lane k ranks keys k and k + 64 by counting the keys below each -- all ns read two at a time by broadcast -- and
+// writes its nodes' ids to their ranks in ids. Ranks are a permutation when the keys are distinct; an equal pair (a
+// duplicate or a collision under the seed) or a key equal to the root's hash sets GPUDIFF_TOK_HASH instead, as the
+// bitonic path's check does
 template <int NK>
-__device__ __forceinline__ void rank_sort_n(uint64_t* skey, uint32_t* sidx, uint32_t ns, uint32_t lane, uint64_t root,
-                                            uint32_t& status) {
+__device__ __forceinline__ void rank_sort_n(const uint64_t* keys, uint64_t mask, uint16_t* ids, uint32_t ns,
+                                            uint32_t lane, uint64_t root, uint32_t& status) {
     uint64_t k[NK];
     uint32_t r[NK], e[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) {
-        k[q] = lane + 64u * q < ns ? skey[lane + 64u * q] : 0ull;
+        k[q] = lane + 64u * q < ns ? keys[lane + 64u * q] & mask : 0ull;
         r[q] = 0u;
         e[q] = 0u;
     }
     const uint32_t np = ns & ~1u;
     for (uint32_t j = 0; j < np; j += 2) {
-        const uint64_t a = skey[j], b = skey[j + 1];
+        const uint64_t a = keys[j] & mask, b = keys[j + 1] & mask;
 #pragma unroll
         for (int q = 0; q < NK; q++) {
             r[q] += (uint32_t)(a < k[q]) + (uint32_t)(b < k[q]);
@@ -479,7 +481,7 @@ __device__ __forceinline__ void rank_sort_n(uint64_t* skey, uint32_t* sidx, uint
         }
     }
     if (np < ns) {
-        const uint64_t a = skey[np];
+        const uint64_t a = keys[np] & mask;
 #pragma unroll
         for (int q = 0; q < NK; q++) {
             r[q] += (uint32_t)(a < k[q]);
@@ -494,19 +496,15 @@ __device__ __forceinline__ void rank_sort_n(uint64_t* skey, uint32_t* sidx, uint
         status = GPUDIFF_TOK_HASH;
         return;
     }
-    __asm__ volatile("" ::: "memory");  // every read above is issued before a write below (LDS runs in order)
 #pragma unroll
     for (int q = 0; q < NK; q++)
-        if (lane + 64u * q < ns) {
-            skey[r[q]] = k[q];
-            sidx[r[q]] = lane + 64u * q + 1u;
-        }
+        if (lane + 64u * q < ns) ids[r[q]] = (uint16_t)(lane + 64u * q + 1u);
     __asm__ volatile("" ::: "memory");
 }
-__device__ __forceinline__ void rank_sort(uint64_t* skey, uint32_t* sidx, uint32_t ns, uint32_t lane, uint64_t root,
-                                          uint32_t& status) {
-    if (ns <= 64u) rank_sort_n<1>(skey, sidx, ns, lane, root, status);
-    else rank_sort_n<2>(skey, sidx, ns, lane, root, status);
+__device__ __forceinline__ void rank_sort(const uint64_t* keys, uint64_t mask, uint16_t* ids, uint32_t ns,
+                                          uint32_t lane, uint64_t root, uint32_t& status) {
+    if (ns <= 64u) rank_sort_n<1>(keys, mask, ids, ns, lane, root, status);
+    else rank_sort_n<2>(keys, mask, ids, ns, lane, root, status);
 }
 
 // K0's values pass: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or

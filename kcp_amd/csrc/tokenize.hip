@@ -562,7 +562,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     bool small = nn <= kLdsHash && max_depth < 32u;
     uint32_t* const h32 = (uint32_t*)lds;           // nodes per depth
     uint32_t* const c32 = (uint32_t*)(lds + 128);   // depth cursors
-    uint2* const hin = (uint2*)(lds + 256);         // x: key offset or index; y: parent | depth << 8 | key << 13 | klen << 16
+    // hin: x = key offset or index; y = parent | depth << 8 | key << 13 | region << 14 | klen << 16 | path-table
+    // node << 21 | string << 22 | decoded string << 23
+    uint2* const hin = (uint2*)(lds + 256);
     uint16_t* const ord16 = (uint16_t*)(lds + 2304);
     constexpr uint32_t kStage = 2304;               // phase 3a's decoded strings are staged from here
     if (small && lane < 32u) h32[lane] = 0u;
@@ -633,7 +635,10 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             if (small && live) {
                 const uint32_t dep = (r.w >> NI_DEPTH_SHIFT) & 0xFFu, kl = kcp - kop - 1;
                 atomicAdd(&h32[dep], 1u);
-                hin[i] = make_uint2(key ? kop + 1 : r.y, r.x | (dep << 8) | (key ? (1u << 13) | (kl << 16) : 0u));
+                hin[i] = make_uint2(key ? kop + 1 : r.y, r.x | (dep << 8) | (key ? (1u << 13) | ((kl & 31u) << 16) : 0u) |
+                                                             (rg << 14) | (tb ? 1u << 21 : 0u) | (str ? 1u << 22 : 0u) |
+                                                             (slow ? 1u << 23 : 0u));
+                if (str && nn <= kRank + 1u) S.sidx[i] = vop;  // for phase 5 (the sort area is free up to kLdsSort)
             }
             if (ballot(key && kcp - kop - 1 > 27u)) small = false;  // keys hashed from registers: <= 27 bytes
             // the blob's sizes (phase 5), counted here where every operand is in registers (wave totals, scalar)
@@ -775,7 +780,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 in = hin[i];
             }
             const bool isk = live && (in.y & (1u << 13)) != 0u;
-            const uint32_t kl = in.y >> 16;
+            const uint32_t kl = (in.y >> 16) & 31u;
             uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
             if (isk) ld32u(d + in.x, d + len + kTokSlack, w0, w1, w2, w3);
             const uint32_t dep = (in.y >> 8) & 31u;
@@ -847,23 +852,27 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     const uint32_t ns = nn > 1 ? nn - 1 : 0;  // every node but the root
     uint64_t* skey = ns <= kLdsSort ? (uint64_t*)lds : S.skey;
     uint32_t* sidx = ns <= kLdsSort ? (uint32_t*)(lds + 8 * kLdsSort) : S.sidx;
+    // up to kRank nodes: ranked straight from phase 3b's hashes in LDS into a u16 node order (the node records and
+    // hash inputs stay in LDS for phase 5); more: the keys sorted with their node ids
+    const bool rk = ns <= kRank;
+    uint16_t* const ids16 = (uint16_t*)(lds + 2304);
     if (status == GPUDIFF_TOK_OK && ns) {
-        // (from LDS when phase 3b kept the hashes there: batch b reads hl[64b + 1 ..] before it writes sidx over
-        // hl entries below 32 (b + 1), all read by earlier batches)
-        for (uint32_t j = lane; j < ns; j += 64) {
-            const uint64_t hj = h_in_lds ? hl[j + 1] : S.h[j + 1];
-            lds_order();
-            skey[j] = hj & mask;
-            sidx[j] = j + 1;
-        }
-        wave_sync();
         const uint64_t root = seed & mask;
-        if (ns <= 2u * 64u) {
-            // rank sort: a lane ranks its keys (up to three) against all ns keys, read two at a time by broadcast
-            // from LDS -- no barrier, no divergent exchange; an equal key (a duplicate or a collision under the seed)
-            // or the root's hash hands the document to the host, as below
-            rank_sort(skey, sidx, ns, lane, root, status);
+        if (rk) {
+            // rank sort: a lane ranks its keys (up to two) against all ns keys, read by broadcast from LDS -- no
+            // barrier, no divergent exchange; an equal key (a duplicate or a collision under the seed) or the root's
+            // hash hands the document to the host, as below
+            rank_sort(hl + 1, mask, ids16, ns, lane, root, status);
         } else {
+            // (from LDS when phase 3b kept the hashes there: batch b reads hl[64b + 1 ..] before it writes sidx over
+            // hl entries below 32 (b + 1), all read by earlier batches)
+            for (uint32_t j = lane; j < ns; j += 64) {
+                const uint64_t hj = h_in_lds ? hl[j + 1] : S.h[j + 1];
+                lds_order();
+                skey[j] = hj & mask;
+                sidx[j] = j + 1;
+            }
+            wave_sync();
             // bitonic sort, all comparators ascending (flip + half-cleaners):
             // indices >= ns act as +inf and never move
             for (uint32_t kk = 2; (kk >> 1) < ns; kk <<= 1) {
@@ -925,27 +934,52 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             for (uint32_t q = lane; q < tab - 24ull * Nt - KB; q += 64) keys[KB + q] = 0;
             if (lane < (body - seg_s - seg_t) / 16u) ((u32x4*)(blob + seg_s + seg_t))[lane] = u32x4{0u, 0u, 0u, 0u};
             const uint64_t root = seed & mask;
+            const bool tiny = small && rk;  // phases 3a-4 left every input of this pass in LDS
             uint32_t rank[2] = {0, 0}, aoff[2] = {0, 0}, trank = 0, tko = 0;
             for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
                 const uint32_t j = j0 + lane;
-                uint32_t rg = 0, i = 0, m = 0, ar = 0, kl = 0, kop = 0;
-                uint4 r = make_uint4(0u, 0u, 0u, 0u);
-                bool t = false;
-                uint64_t val = 0, ph = root, ks = 0;
+                uint32_t rg = 0, i = 0, m = 0, ar = 0, kl = 0, kop = 0, idx = 0;
+                bool t = false, isk = false, dec = false;
+                uint64_t val = 0, ph = root, key = 0;
                 uint32_t vop = 0;
-                if (j < ns) {
-                    i = sidx[j];
-                    r = S.rec[i];
+                if (j < ns && tiny) {
+                    // a small document: the node's inputs, its hash and its parent's from LDS; its value, metadata
+                    // and string position in one round of loads
+                    i = ids16[j];
+                    const uint2 in = hin[i];
+                    rg = (in.y >> 14) & 3u;
+                    t = (in.y >> 21) & 1u;
+                    isk = (in.y >> 13) & 1u;
+                    dec = (in.y >> 23) & 1u;
+                    kop = in.x;
+                    idx = in.x;
+                    kl = isk ? (in.y >> 16) & 31u : 0u;
+                    key = hl[i] & mask;
+                    if (t && (in.y & 0xFFu)) ph = hl[in.y & 0xFFu] & mask;
+                    if (rg) {
+                        m = S.meta[i];
+                        val = S.val[i];
+                        if ((in.y >> 22) & 1u) vop = S.sidx[i];
+                    }
+                    ar = meta_arena(m);
+                } else if (j < ns) {
+                    i = rk ? ids16[j] : sidx[j];
+                    const uint4 r = S.rec[i];
                     rg = region_of(r.w);
                     t = in_tab(i, r.w);
+                    isk = (r.y & KEYBIT) != 0u;
+                    dec = (r.w & NI_SLOW) != 0u;
+                    idx = r.y;
+                    key = rk ? (h_in_lds ? hl[i] : S.h[i]) & mask : skey[j];
                     // one round of loads for everything this node needs: its value, its parent's hash, its key span
-                    // (phase 3a's, still in the sort-key area when the sort ran in LDS) and its string's position
+                    // (the tree phase's, still in the sort-key area when the sort ran in LDS) and its string's position
+                    uint64_t ks = 0;
                     if (rg) {
                         m = S.meta[i];
                         val = S.val[i];
                     }
                     if (t && r.x != 0) ph = S.h[r.x] & mask;
-                    if (t && (r.y & KEYBIT)) {
+                    if (t && isk) {
                         if (ns <= kLdsSort) {
                             ks = S.skey[i];
                         } else {
@@ -976,7 +1010,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     uint8_t* sp8 = segp[g];
                     // vals u64 | keys u32 | metas u32 (include/gpudiff_format.h); keys masked to <= 32 bits
                     ((uint64_t*)sp8)[my_rank] = val;
-                    ((uint32_t*)(sp8 + 8ull * L))[my_rank] = (uint32_t)skey[j];
+                    ((uint32_t*)(sp8 + 8ull * L))[my_rank] = (uint32_t)key;
                     ((uint32_t*)(sp8 + 12ull * L))[my_rank] = m;
                 }
                 // the path-table entry: hash, parent hash, component (+ key bytes)
@@ -985,9 +1019,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 const uint32_t ko = tko + kinc - kl;  // this entry's key bytes
                 if (t) {
                     const uint32_t tr = trank + popc64(tbal & mask_lt(lane));
-                    hs[tr] = skey[j];
+                    hs[tr] = key;
                     phs[tr] = ph;
-                    cs[tr] = (r.y & KEYBIT) ? (((uint64_t)kl << 32) | ko) : (GPUDIFF_TAB_INDEX | r.y);
+                    cs[tr] = isk ? (((uint64_t)kl << 32) | ko) : (GPUDIFF_TAB_INDEX | idx);
                 }
                 trank += popc64(tbal);
                 tko += rdlane(kinc, 63);
@@ -1001,7 +1035,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 uint32_t* tdst = nullptr;
                 uint32_t tlen = 0;
                 if (tail) {
-                    tsrc = ((r.w & NI_SLOW) ? (S.str + vop + 1) : (d + vop + 1)) + GPUDIFF_INLINE_MAX;
+                    tsrc = (dec ? (S.str + vop + 1) : (d + vop + 1)) + GPUDIFF_INLINE_MAX;
                     tlen = (m >> 3) - GPUDIFF_INLINE_MAX;
                     tdst = (uint32_t*)(segp[rg - 1u] + 16ull * Lr[rg - 1u] + my_aoff);
                 }
