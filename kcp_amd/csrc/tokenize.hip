@@ -953,7 +953,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     dec = (in.y >> 23) & 1u;
                     kop = in.x;
                     idx = in.x;
-                    kl = isk ? (in.y >> 16) & 31u : 0u;
+                    kl = t && isk ? (in.y >> 16) & 31u : 0u;  // key bytes only for path-table entries
                     key = hl[i] & mask;
                     if (t && (in.y & 0xFFu)) ph = hl[in.y & 0xFFu] & mask;
                     if (rg) {

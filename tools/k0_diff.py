@@ -39,7 +39,8 @@ def diff(info, db, hb):
     for name, (o, w, n) in sections(info, hb).items():
         bad = [k for k in range(n) if db[o + w * k:o + w * (k + 1)] != hb[o + w * k:o + w * (k + 1)]]
         if bad:
-            res.append((name, len(bad), bad[:6]))
+            ex = [(k, db[o + w * k:o + w * (k + 1)].hex(), hb[o + w * k:o + w * (k + 1)].hex()) for k in bad[:3]]
+            res.append((name, len(bad), bad[:6], ex if w > 1 else None))
     return res
 
 
@@ -74,7 +75,8 @@ def main():
                 if len(shown) < 4:
                     shown.append(dict(doc=k, n_nodes=di.get("n_nodes"), fields={f: (di[f], hi[f]) for f in
                                       ("spec_l", "spec_ar", "stat_l", "stat_ar", "n_tab", "bytes") if di[f] != hi[f]},
-                                      sections=diff(hi, db, hb) if len(db) == len(hb) else "length"))
+                                      sections=diff(hi, db, hb) if len(db) == len(hb) else "length",
+                                      json=docs[k][:400].decode("utf-8", "replace")))
         print(lib or "kcp_amd/libgpudiff.so", "docs", len(docs), "differing", nd, shown, flush=True)
 
 
