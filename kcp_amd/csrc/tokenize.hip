@@ -767,34 +767,65 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             }
         }
         lds_order();
-        // 64 nodes of the depth order at a time: their key bytes loaded once (one round trip for every depth the
-        // batch spans), then a step per depth present -- a node's parent is at a smaller depth, so earlier in the
-        // order: hashed by an earlier batch or step
-        for (uint32_t c0 = 0; c0 + 1u < nn; c0 += 64) {
-            const uint32_t p = c0 + lane;
-            const bool live = p + 1u < nn;
-            uint32_t i = 0;
-            uint2 in = make_uint2(0u, 0u);
-            if (live) {
-                i = ord16[p];
-                in = hin[i];
+        // level by level, 64 nodes of a level at a time, a lane per node: its inputs and its parent's hash from LDS,
+        // its key bytes in registers -- loaded one step ahead (the next step's nodes are known from the order alone,
+        // so their key loads fly while this step hashes)
+        uint32_t dep = 1, j0 = 0, beg = 0;  // the step being hashed: depth, offset in its level, level start (depth 1
+                                            // holds the root's members: never empty)
+        auto next_step = [&](uint32_t& d_, uint32_t& j_, uint32_t& b_) {
+            j_ += 64u;
+            while (d_ <= max_depth && j_ >= rdlane(cnt, d_)) {
+                b_ += rdlane(cnt, d_);
+                d_++;
+                j_ = 0;
             }
-            const bool isk = live && (in.y & (1u << 13)) != 0u;
-            const uint32_t kl = (in.y >> 16) & 31u;
-            uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-            if (isk) ld32u(d + in.x, d + len + kTokSlack, w0, w1, w2, w3);
-            const uint32_t dep = (in.y >> 8) & 31u;
-            const uint32_t dlo = rdlane(dep, 0), dhi = rdlane(dep, min(63u, nn - 2u - c0));
-            for (uint32_t dd = dlo; dd <= dhi; dd++) {
-                if (live && dep == dd) {
-                    const uint32_t par = in.y & 0xFFu;
-                    const uint64_t ph = par == 0u ? seed : hl[par];
-                    const uint64_t hh = isk ? hash_key_w(ph, kl, w0, w1, w2, w3) : hash_index_w(ph, in.x);
-                    S.h[i] = hh;
-                    hl[i] = hh;
-                }
-                lds_order();  // the next step reads these hashes
+        };
+        uint32_t ci = 0, cy = 0, cx = 0;
+        uint64_t c0w = 0, c1w = 0, c2w = 0, c3w = 0;
+        bool clive = false;
+        auto load_step = [&](uint32_t d_, uint32_t j_, uint32_t b_, uint32_t& i_, uint32_t& y_, uint32_t& x_,
+                             uint64_t& w0_, uint64_t& w1_, uint64_t& w2_, uint64_t& w3_, bool& live_) {
+            live_ = d_ <= max_depth && j_ + lane < rdlane(cnt, d_);
+            i_ = 0u;
+            y_ = 0u;
+            x_ = 0u;
+            w0_ = w1_ = w2_ = w3_ = 0ull;
+            if (live_) {
+                i_ = ord16[b_ + j_ + lane];
+                const uint2 in = hin[i_];
+                y_ = in.y;
+                x_ = in.x;
+                if (in.y & (1u << 13)) ld32u(d + in.x, d + len + kTokSlack, w0_, w1_, w2_, w3_);
             }
+        };
+        load_step(dep, j0, beg, ci, cy, cx, c0w, c1w, c2w, c3w, clive);
+        while (dep <= max_depth) {
+            uint32_t nd = dep, nj = j0, nb = beg;
+            next_step(nd, nj, nb);
+            uint32_t ni, ny, nx;
+            uint64_t n0w, n1w, n2w, n3w;
+            bool nlive;
+            load_step(nd, nj, nb, ni, ny, nx, n0w, n1w, n2w, n3w, nlive);
+            if (clive) {
+                const uint32_t par = cy & 0xFFu;
+                const uint64_t ph = par == 0u ? seed : hl[par];
+                const uint64_t hh = (cy & (1u << 13)) ? hash_key_w(ph, (cy >> 16) & 31u, c0w, c1w, c2w, c3w)
+                                                      : hash_index_w(ph, cx);
+                S.h[ci] = hh;
+                hl[ci] = hh;
+            }
+            lds_order();  // the next level reads these hashes
+            dep = nd;
+            j0 = nj;
+            beg = nb;
+            ci = ni;
+            cy = ny;
+            cx = nx;
+            c0w = n0w;
+            c1w = n1w;
+            c2w = n2w;
+            c3w = n3w;
+            clive = nlive;
         }
         wave_sync();  // phases 4-5 read S.h
     } else if (status == GPUDIFF_TOK_OK && nn > 1) {
