@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 5 (q): the whole -m gpu suite and smoke at the round's sources.
+set -o pipefail
+O=gpurun_out/r05q; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
