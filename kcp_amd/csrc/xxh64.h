@@ -1,5 +1,5 @@
 // XXH64 (published algorithm, Yann Collet), shared by the host encoder (path
-// hashes, optional host value hashes) and kernel K1.  Known answers pinned in
+// hashes) and K0's path hashes (tokdev.h).  Known answers pinned in
 // tests/test_oracle_kat.py against the Python xxhash 3.8.1 package.
 #pragma once
 #include <hip/hip_runtime.h>
