@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 (q): the whole -m gpu suite and smoke at the round's sources.
+# Round 5 (q): the whole -m gpu suite and smoke at the round's sources, then config 5's 12-s replay with this K0.
 set -o pipefail
 O=gpurun_out/r05q; mkdir -p $O
 export TMPDIR=/tmp
