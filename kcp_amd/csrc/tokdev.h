@@ -70,12 +70,25 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     }
     return v;
 }
+// wave reductions: every lane ends with the total, so the result is returned through readfirstlane -- a scalar the
+// compiler knows to be uniform (loop bounds and branches on it stay scalar instead of becoming exec-mask loops)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+// the same reductions left in vector registers (K10 / K11 / K13's phases: their register allocation was tuned so)
+__device__ __forceinline__ uint32_t wave_sum_v(uint32_t v) {
 #pragma unroll
     for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
     return v;
 }
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_max_v(uint32_t v) {
 #pragma unroll
     for (uint32_t d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
     return v;
@@ -984,10 +997,15 @@ __device__ __forceinline__ int bytes_cmp(const uint8_t* a, uint32_t al, const ui
         if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
     return al < bl ? -1 : al > bl ? 1 : 0;
 }
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_min_v(uint32_t v) {
 #pragma unroll
     for (uint32_t d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
     return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (uint32_t d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u, MF_FLOAT = 16u;
 constexpr uint32_t MF_VCLEAN = 32u, MF_KCLEAN = 64u;  // string value / key written as its own bytes

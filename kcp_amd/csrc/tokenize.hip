@@ -858,7 +858,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         wave_sync();
         uint32_t beg = 0;
         for (uint32_t dep = 1; dep <= max_depth; dep++) {
-            const uint32_t cnt = hist[dep];
+            const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)hist[dep]);  // uniform: a scalar loop
             for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
                 if (j0 + lane < cnt) {
                     const uint32_t i = order[beg + j0 + lane];
