@@ -116,9 +116,8 @@ __device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {
     const uintptr_t a = (uintptr_t)p;
     const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
     const uint32_t sh = (uint32_t)(a & 7u) * 8u;
-    const uint64_t lo = q[0];
-    if (!sh) return lo;
-    return (lo >> sh) | (q[1] << (64u - sh));
+    const uint64_t lo = q[0], hi = q[1];  // both words always (a branch around the second cost a mask switch)
+    return (lo >> sh) | ((hi << 1) << (63u - sh));  // = hi << (64 - sh), and 0 when sh = 0, without a select
 }
 
 // XXH64 over a virtual byte stream given as 8-byte little-endian words
@@ -175,19 +174,24 @@ __device__ __forceinline__ uint64_t xxh64_small(uint64_t seed, uint32_t L, uint6
     }
     h += L;
     const uint32_t rem = L & 31u, n8 = rem >> 3;
-    if (n8 > 0u) h = xrotl(h ^ xround(0, W0), 27) * XP1 + XP4;
-    if (n8 > 1u) h = xrotl(h ^ xround(0, W1), 27) * XP1 + XP4;
-    if (n8 > 2u) h = xrotl(h ^ xround(0, W2), 27) * XP1 + XP4;
+    uint64_t hn = xrotl(h ^ xround(0, W0), 27) * XP1 + XP4;
+    h = n8 > 0u ? hn : h;
+    hn = xrotl(h ^ xround(0, W1), 27) * XP1 + XP4;
+    h = n8 > 1u ? hn : h;
+    hn = xrotl(h ^ xround(0, W2), 27) * XP1 + XP4;
+    h = n8 > 2u ? hn : h;
     uint64_t wr = n8 == 0u ? W0 : n8 == 1u ? W1 : n8 == 2u ? W2 : W3;
     uint32_t r = rem & 7u;
-    if (r >= 4u) {
-        h = xrotl(h ^ ((uint64_t)(uint32_t)wr * XP1), 23) * XP2 + XP3;
-        wr >>= 32;
-        r -= 4u;
-    }
+    const uint64_t h4 = xrotl(h ^ ((uint64_t)(uint32_t)wr * XP1), 23) * XP2 + XP3;
+    const bool four = r >= 4u;
+    h = four ? h4 : h;
+    wr = four ? wr >> 32 : wr;
+    r = four ? r - 4u : r;
 #pragma unroll
-    for (uint32_t k = 0; k < 3u; k++)
-        if (k < r) h = xrotl(h ^ (((wr >> (8u * k)) & 0xFFu) * XP5), 11) * XP1;
+    for (uint32_t k = 0; k < 3u; k++) {
+        const uint64_t hk = xrotl(h ^ (((wr >> (8u * k)) & 0xFFu) * XP5), 11) * XP1;
+        h = k < r ? hk : h;  // a select, not a branch
+    }
     return xavalanche(h);
 }
 // hash_key over a key of at most 27 bytes held in registers: w0..w3 = the 32 bytes at the key (ld32u); word i >= 1
@@ -446,8 +450,8 @@ __device__ __forceinline__ void ld16u(const uint8_t* p, uint64_t* w0, uint64_t* 
     const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
     const uint32_t sh = (uint32_t)(a & 7u) * 8u;
     const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
-    *w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
-    *w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
+    *w0 = (x0 >> sh) | ((x1 << 1) << (63u - sh));
+    *w1 = (x1 >> sh) | ((x2 << 1) << (63u - sh));
 }
 // (ld32u: only the words wholly before lim are read, the others are zero -- a document is readable to kTokSlack = 32
 // bytes past its end, and a 32-byte window at its last bytes reaches up to 40)
@@ -457,11 +461,14 @@ __device__ __forceinline__ void ld32u(const uint8_t* p, const uint8_t* lim, uint
     const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
     const uint32_t sh = (uint32_t)(a & 7u) * 8u;
     const uint64_t* ql = (const uint64_t*)lim;
-    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q + 4 <= ql ? q[3] : 0ull, x4 = q + 5 <= ql ? q[4] : 0ull;
-    w0 = sh ? (x0 >> sh) | (x1 << (64u - sh)) : x0;
-    w1 = sh ? (x1 >> sh) | (x2 << (64u - sh)) : x1;
-    w2 = sh ? (x2 >> sh) | (x3 << (64u - sh)) : x2;
-    w3 = sh ? (x3 >> sh) | (x4 << (64u - sh)) : x3;
+    // the words past lim read as zero: their loads go to q[0] instead (a select of addresses, not a branch)
+    const bool r3 = q + 4 <= ql, r4 = q + 5 <= ql;
+    const uint64_t y3 = *(r3 ? q + 3 : q), y4 = *(r4 ? q + 4 : q);
+    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = r3 ? y3 : 0ull, x4 = r4 ? y4 : 0ull;
+    w0 = (x0 >> sh) | ((x1 << 1) << (63u - sh));
+    w1 = (x1 >> sh) | ((x2 << 1) << (63u - sh));
+    w2 = (x2 >> sh) | ((x3 << 1) << (63u - sh));
+    w3 = (x3 >> sh) | ((x4 << 1) << (63u - sh));
 }
 // byte k of a 16-byte window: a select by mask (a ternary became a private array and scratch loads)
 __device__ __forceinline__ uint32_t win16_at(uint64_t w0, uint64_t w1, uint32_t k) {
@@ -560,14 +567,14 @@ __device__ __forceinline__ uint32_t parse_atom_win(const uint8_t* p, const uint8
     bool spill = false;
     const uint32_t e = parse_atom_core(
         [&](uint64_t j) -> uint32_t {
-            if (j >= 32u) {
-                spill = true;
-                return 0xFFu;  // neither a digit, a sign, '.', 'e' nor a delimiter: the parse stops here
-            }
-            const uint32_t k = (uint32_t)j;  // selects by mask, as win16_at
+            // past the window: 0xFF, neither a digit, a sign, '.', 'e' nor a delimiter -- the parse stops there and
+            // the atom is parsed again from memory (selects, no branch)
+            const bool past = j >= 32u;
+            spill |= past;
+            const uint32_t k = (uint32_t)j & 31u;  // selects by mask, as win16_at
             const uint64_t m8 = 0ull - (uint64_t)((k >> 3) & 1u), m16 = 0ull - (uint64_t)((k >> 4) & 1u);
             const uint64_t lo = (w0 & ~m8) | (w1 & m8), hi = (w2 & ~m8) | (w3 & m8);
-            return (uint32_t)((((lo & ~m16) | (hi & m16)) >> (8u * (k & 7u))) & 0xFFu);
+            return past ? 0xFFu : (uint32_t)((((lo & ~m16) | (hi & m16)) >> (8u * (k & 7u))) & 0xFFu);
         },
         (uint64_t)(end - p), tag, val);
     return spill ? parse_atom_mem(p, end, tag, val) : e;

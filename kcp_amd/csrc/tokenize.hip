@@ -190,11 +190,12 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
             const uint32_t c = (x >> (8u * j)) & 0xFFu, cb = c & 0xDFu;
-            Qn |= (c == '"' ? 1u : 0u) << j;
-            Sn |= (cb == '[' || cb == ']' || c == ':' || c == ',' ? 1u : 0u) << j;
-            Wn |= (c == ' ' || c == '\n' || c == '\r' || c == '\t' ? 1u : 0u) << j;
-            Cn |= (c < 0x20u ? 1u : 0u) << j;
-            Mn |= (c == '\\' || c >= 0x80u ? 1u : 0u) << j;
+            // (bitwise | of the compares: a short-circuit || became a branch per term)
+            Qn |= (uint32_t)(c == '"') << j;
+            Sn |= (uint32_t)((cb == '[') | (cb == ']') | (c == ':') | (c == ',')) << j;
+            Wn |= (uint32_t)((c == ' ') | (c == '\n') | (c == '\r') | (c == '\t')) << j;
+            Cn |= (uint32_t)(c < 0x20u) << j;
+            Mn |= (uint32_t)((c == '\\') | (c >= 0x80u)) << j;
         }
         if (esc_carry || ballot(Mn != 0u)) return false;
         const uint64_t odd = ballot(__builtin_popcount(Qn) & 1u);
@@ -217,14 +218,16 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         const uint32_t kw1 = opens ? keyword(p4 + j1) : 0u;
         const uint32_t op2 = opens & (opens - 1u);
         const uint32_t kw2 = ballot(op2 != 0u) && op2 ? keyword(p4 + (uint32_t)__builtin_ctz(op2)) : 0u;
+        // every lane stores four words: a byte that starts no token writes slot len + 1, which no token uses (a
+        // document of len bytes has at most len tokens, tok_cap = len + 2) -- stores without a branch each
         uint32_t k = ntok + pre;
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
-            if ((Tn >> j) & 1u) {
-                const uint32_t code = ((closes >> j) & 1u) ? TK_CLOSEQ
-                                      : ((opens >> j) & 1u) ? (j == j1 ? kw1 : kw2) : (x >> (8u * j)) & 0xFFu;
-                S.tok[k++] = (code << 24) | (p4 + j);
-            }
+            const bool tj = (Tn >> j) & 1u;
+            const uint32_t code = ((closes >> j) & 1u) ? TK_CLOSEQ
+                                  : ((opens >> j) & 1u) ? (j == j1 ? kw1 : kw2) : (x >> (8u * j)) & 0xFFu;
+            S.tok[tj ? k : len + 1u] = (code << 24) | (p4 + j);
+            k += tj ? 1u : 0u;
         }
         const uint64_t om = ballot(opens != 0u);
         if (om) {  // the last opening quote of the block (a later step may mark its string slow)
@@ -252,8 +255,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint64_t bs = ballot(c == '\\');
             const uint64_t qt = ballot(c == '"');
             const uint32_t cb = c & 0xDFu;  // '[' ']' and '{' '}' fold together
-            const uint64_t st = ballot(cb == '[' || cb == ']' || c == ':' || c == ',');
-            const uint64_t wsm = ballot(c == ' ' || c == '\n' || c == '\r' || c == '\t');
+            const uint64_t st = ballot((cb == '[') | (cb == ']') | (c == ':') | (c == ','));
+            const uint64_t wsm = ballot((c == ' ') | (c == '\n') | (c == '\r') | (c == '\t'));
             const uint64_t ctl = ballot(c < 0x20u);  // inside a string every control byte is an error
             const uint64_t hi = ballot(c >= 0x80u);
             // escaped characters: an unescaped backslash escapes the next byte
@@ -538,11 +541,11 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     const uint64_t seed = slots ? ((slots[links[doc_i].slot].flags >> 8) & 0xFFu) : D.seed;
     mark(1);
     // which leaves the blob encodes, and which nodes its path table lists (phases 3a and 5)
-    auto region_of = [&](uint32_t w) -> uint32_t {  // 1 spec, 2 status, 0 not encoded
-        if (!(w & NI_LEAF)) return 0u;
+    auto region_of = [&](uint32_t w) -> uint32_t {  // 1 spec, 2 status, 0 not encoded (selects, no branches)
         const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
-        if (reg == R_SPEC || (reg == R_LABELS && labels_ok) || (reg == R_ANNOT && annot_ok)) return 1u;
-        return reg == R_STATUS ? 2u : 0u;
+        const bool sp = (reg == R_SPEC) | ((reg == R_LABELS) & labels_ok) | ((reg == R_ANNOT) & annot_ok);
+        const uint32_t r = sp ? 1u : reg == R_STATUS ? 2u : 0u;
+        return (w & NI_LEAF) ? r : 0u;
     };
     // path-table nodes: the region leaves and their ancestors but the root -- every container of the spec / status
     // subtrees, and metadata, metadata.labels and metadata.annotations when label / annotation leaves are encoded
@@ -550,10 +553,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     const bool ann_in = status == GPUDIFF_TOK_OK && annot_node != NONE && annot_ok && !(S.rec[annot_node].w & NI_LEAF);
     const bool meta_in = lab_in || ann_in;
     auto in_tab = [&](uint32_t i, uint32_t w) -> bool {
-        if (region_of(w)) return true;
         const uint32_t reg = (w >> NI_REG_SHIFT) & 7u;
-        if (!(w & NI_LEAF) && (reg == R_SPEC || reg == R_STATUS)) return true;
-        return (i == meta_node && meta_in) || (i == labels_node && lab_in) || (i == annot_node && ann_in);
+        return (region_of(w) != 0u) | (!(w & NI_LEAF) & ((reg == R_SPEC) | (reg == R_STATUS))) |
+               ((i == meta_node) & meta_in) | ((i == labels_node) & lab_in) | ((i == annot_node) & ann_in);
     };
     // phase 5's sizes: spec / status leaves, their arena bytes, path-table nodes and their key bytes
     uint32_t n_ls = 0, n_lt = 0, n_as = 0, n_at = 0, n_nt = 0, n_kb = 0;
