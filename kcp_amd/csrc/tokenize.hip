@@ -406,37 +406,40 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 const uint64_t below = m_ol & mask_lt(lane);
                 const uint32_t e = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
                 const uint32_t x_id = shfl32(id, e), x_info = shfl32(my_info, e), x_base = shfl32(my_base, e);
-                if (at1) {
-                    e_id = below ? x_id : st.id;
-                    e_info = below ? x_info : st.info;
-                    if (is_node) {
-                        const uint32_t e_base = below ? x_base : st.base;
-                        const bool earr = e_info & LF_ARR;
-                        const uint32_t preg = (e_info >> 1) & 7u;
-                        const uint32_t depth = (uint32_t)L + 1u;
-                        comp = earr ? nb - e_base : ((tb + lane - 3u) | KEYBIT);
-                        reg = preg;
-                        uint32_t fl = 0;
-                        if (depth == 1u) {
-                            if (cp3 == TK_KEY_META) {
-                                reg = R_META;
-                                if (code == '{') fl = LF_META;
-                            } else {
-                                reg = code == 'n' ? R_NONE : cp3 == TK_KEY_STATUS ? R_STATUS : R_SPEC;
-                            }
-                        } else if (depth == 2u && !earr && (e_info & LF_META)) {
-                            if (code == '{') fl = cp3 == TK_KEY_LABELS ? LF_LAB : cp3 == TK_KEY_ANNOT ? LF_ANN : 0u;
-                        } else if (depth == 3u && (e_info & LF_LAB)) {
-                            reg = R_LABELS;
-                            bad_lab = !is_qo;
-                        } else if (depth == 3u && (e_info & LF_ANN)) {
-                            reg = R_ANNOT;
-                            bad_ann = !is_qo;
-                        } else if (preg == R_LABELS || preg == R_ANNOT) {
-                            reg = R_META;
-                        }
-                        my_info = (code == '[' ? LF_ARR : 0u) | (reg << 1) | fl;
+                // the parent of this level's tokens (selects; the depth tests are uniform: L is a scalar)
+                const uint32_t p_id = below ? x_id : st.id, p_info = below ? x_info : st.info;
+                const uint32_t p_base = below ? x_base : st.base;
+                e_id = at1 ? p_id : e_id;
+                e_info = at1 ? p_info : e_info;
+                {
+                    const bool nd = at1 & is_node;
+                    const bool p_arr = (p_info & LF_ARR) != 0u;
+                    const uint32_t preg = (p_info >> 1) & 7u;
+                    const uint32_t depth = (uint32_t)L + 1u;
+                    const uint32_t comp_n = p_arr ? nb - p_base : ((tb + lane - 3u) | KEYBIT);
+                    uint32_t reg_n, fl = 0u;
+                    bool bl = false, ba = false;
+                    if (depth == 1u) {
+                        const bool km = cp3 == TK_KEY_META;
+                        reg_n = km ? R_META : code == 'n' ? R_NONE : cp3 == TK_KEY_STATUS ? R_STATUS : R_SPEC;
+                        fl = (km & (code == '{')) ? LF_META : 0u;
+                    } else {
+                        // metadata's members (labels / annotations objects), their members, anything below them
+                        const bool c2 = (depth == 2u) & !p_arr & ((p_info & LF_META) != 0u);
+                        const bool c3l = !c2 & (depth == 3u) & ((p_info & LF_LAB) != 0u);
+                        const bool c3a = !c2 & !c3l & (depth == 3u) & ((p_info & LF_ANN) != 0u);
+                        const uint32_t f2 = cp3 == TK_KEY_LABELS ? LF_LAB : cp3 == TK_KEY_ANNOT ? LF_ANN : 0u;
+                        fl = (c2 & (code == '{')) ? f2 : 0u;
+                        const bool below_meta = (preg == R_LABELS) | (preg == R_ANNOT);
+                        reg_n = c2 ? preg : c3l ? R_LABELS : c3a ? R_ANNOT : below_meta ? R_META : preg;
+                        bl = c3l & !is_qo;
+                        ba = c3a & !is_qo;
                     }
+                    comp = nd ? comp_n : comp;
+                    reg = nd ? reg_n : reg;
+                    bad_lab = nd ? bl : bad_lab;
+                    bad_ann = nd ? ba : bad_ann;
+                    my_info = nd ? ((code == '[' ? LF_ARR : 0u) | (reg_n << 1) | fl) : my_info;
                 }
                 // the table entry for level L
                 if (m_ol) {
@@ -452,46 +455,40 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             }
             // grammar: each token against its predecessor (cp1; 0 before the first token)
             const bool earr = e_info & LF_ARR;
-            const bool p_qo = cp1 == '"' || (cp1 >= TK_OPENQ_SLOW && cp1 <= TK_KEY_ANNOT);
-            const bool p_end = cp1 == TK_CLOSEQ || cp1 == '}' || cp1 == ']' ||
-                               (cp1 != 0u && !p_qo && cp1 != '{' && cp1 != '[' && cp1 != ':' && cp1 != ',');
-            uint32_t err = 0;
-            if (live) {
-                if (tb + lane == 0u) {
-                    if (code != '{') err = GPUDIFF_TOK_SYNTAX;
-                } else if (lvl <= 0) {
-                    err = GPUDIFF_TOK_SYNTAX;  // after the root closed
-                } else if (is_key) {
-                    if (!(cp1 == '{' || (cp1 == ',' && !earr))) err = GPUDIFF_TOK_SYNTAX;
-                    else if (code == TK_OPENQ_SLOW) err = GPUDIFF_TOK_KEY;
-                } else if (is_node) {
-                    if (!(cp1 == ':' || cp1 == '[' || (cp1 == ',' && earr))) err = GPUDIFF_TOK_SYNTAX;
-                    else if (is_o && !empty && lvl >= (int32_t)kMaxDepth) err = GPUDIFF_TOK_DEPTH;
-                    else if (id + 3u > ncap) err = GPUDIFF_TOK_SIZE;
-                } else if (code == ':') {
-                    if (cp1 != TK_CLOSEQ) err = GPUDIFF_TOK_SYNTAX;
-                } else if (code == ',') {
-                    if (!p_end) err = GPUDIFF_TOK_SYNTAX;
-                } else if (code == '}') {
-                    if (!(cp1 == '{' || (p_end && !earr))) err = GPUDIFF_TOK_SYNTAX;
-                } else if (code == ']') {
-                    if (!(cp1 == '[' || (p_end && earr))) err = GPUDIFF_TOK_SYNTAX;
-                }
-            }
+            const bool p_qo = (cp1 == '"') | ((cp1 >= TK_OPENQ_SLOW) & (cp1 <= TK_KEY_ANNOT));
+            const bool p_end = (cp1 == TK_CLOSEQ) | (cp1 == '}') | (cp1 == ']') |
+                               ((cp1 != 0u) & !p_qo & (cp1 != '{') & (cp1 != '[') & (cp1 != ':') & (cp1 != ','));
+            // the first failing check per token class, as selects (the grammar of a sequential parser)
+            const bool first_tok = tb + lane == 0u;
+            const uint32_t e_key = !((cp1 == '{') | ((cp1 == ',') & !earr)) ? GPUDIFF_TOK_SYNTAX
+                                   : code == TK_OPENQ_SLOW                  ? GPUDIFF_TOK_KEY
+                                                                            : 0u;
+            const uint32_t e_node = !((cp1 == ':') | (cp1 == '[') | ((cp1 == ',') & earr)) ? GPUDIFF_TOK_SYNTAX
+                                    : (is_o & !empty & (lvl >= (int32_t)kMaxDepth))          ? GPUDIFF_TOK_DEPTH
+                                    : id + 3u > ncap                                        ? GPUDIFF_TOK_SIZE
+                                                                                            : 0u;
+            const bool bad_p = code == ':'   ? cp1 != TK_CLOSEQ
+                               : code == ',' ? !p_end
+                               : code == '}' ? !((cp1 == '{') | (p_end & !earr))
+                               : code == ']' ? !((cp1 == '[') | (p_end & earr))
+                                             : false;
+            const uint32_t err = !live      ? 0u
+                                 : first_tok ? (code != '{' ? GPUDIFF_TOK_SYNTAX : 0u)
+                                 : lvl <= 0  ? GPUDIFF_TOK_SYNTAX  // after the root closed
+                                 : is_key    ? e_key
+                                 : is_node   ? e_node
+                                 : bad_p     ? GPUDIFF_TOK_SYNTAX
+                                             : 0u;
             const uint64_t m_err = ballot(err != 0u);
             const uint64_t upto = m_err ? mask_lt((uint32_t)__builtin_ctzll(m_err)) : ~0ull;
             // node records (the root: no parent, no key, never a leaf)
             if (is_node && ((upto >> lane) & 1ull) && id < ncap) {
-                uint32_t info;
-                if (tb + lane == 0u) {
-                    info = R_NONE << NI_REG_SHIFT;
-                } else {
-                    info = reg << NI_REG_SHIFT;
-                    if (is_o && empty) info |= NI_LEAF | (code == '{' ? GPUDIFF_TAG_EOBJ : GPUDIFF_TAG_EARR);
-                    else if (is_qo) info |= NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u);
-                    else if (is_at) info |= NI_LEAF | NI_ATOM;
-                    info |= (uint32_t)lvl << NI_DEPTH_SHIFT;
-                }
+                const uint32_t leaf = (is_o & empty) ? NI_LEAF | (code == '{' ? GPUDIFF_TAG_EOBJ : GPUDIFF_TAG_EARR)
+                                      : is_qo ? NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u)
+                                      : is_at ? NI_LEAF | NI_ATOM
+                                              : 0u;
+                const uint32_t info = tb + lane == 0u ? R_NONE << NI_REG_SHIFT
+                                                      : (reg << NI_REG_SHIFT) | leaf | ((uint32_t)lvl << NI_DEPTH_SHIFT);
                 S.rec[id] = make_uint4(tb + lane == 0u ? NONE : e_id, comp, tb + lane, info);
                 if constexpr (MODE == kModeEncode) {
                     // for phase 3a: a member's key span, a leaf's value positions (its slot until 3a fills it)
