@@ -784,18 +784,13 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         bool clive = false;
         auto load_step = [&](uint32_t d_, uint32_t j_, uint32_t b_, uint32_t& i_, uint32_t& y_, uint32_t& x_,
                              uint64_t& w0_, uint64_t& w1_, uint64_t& w2_, uint64_t& w3_, bool& live_) {
-            live_ = d_ <= max_depth && j_ + lane < rdlane(cnt, d_);
-            i_ = 0u;
-            y_ = 0u;
-            x_ = 0u;
-            w0_ = w1_ = w2_ = w3_ = 0ull;
-            if (live_) {
-                i_ = ord16[b_ + j_ + lane];
-                const uint2 in = hin[i_];
-                y_ = in.y;
-                x_ = in.x;
-                if (in.y & (1u << 13)) ld32u(d + in.x, d + len + kTokSlack, w0_, w1_, w2_, w3_);
-            }
+            // every lane loads (a lane past the step reads entry 0 and the document's first bytes): no branch
+            live_ = (d_ <= max_depth) && (j_ + lane < rdlane(cnt, min(d_, 31u)));
+            i_ = ord16[live_ ? b_ + j_ + lane : 0u];
+            const uint2 in = hin[i_];
+            y_ = live_ ? in.y : 0u;
+            x_ = in.x;
+            ld32u(d + ((in.y & (1u << 13)) ? in.x : 0u), d + len + kTokSlack, w0_, w1_, w2_, w3_);
         };
         load_step(dep, j0, beg, ci, cy, cx, c0w, c1w, c2w, c3w, clive);
         while (dep <= max_depth) {
@@ -805,13 +800,16 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             uint64_t n0w, n1w, n2w, n3w;
             bool nlive;
             load_step(nd, nj, nb, ni, ny, nx, n0w, n1w, n2w, n3w, nlive);
-            if (clive) {
+            {
+                // every lane hashes; a lane past the step writes slot 0 (the root's, read by nothing after this)
                 const uint32_t par = cy & 0xFFu;
-                const uint64_t ph = par == 0u ? seed : hl[par];
-                const uint64_t hh = (cy & (1u << 13)) ? hash_key_w(ph, (cy >> 16) & 31u, c0w, c1w, c2w, c3w)
-                                                      : hash_index_w(ph, cx);
-                S.h[ci] = hh;
-                hl[ci] = hh;
+                const uint64_t hp = hl[par];
+                const uint64_t ph = par == 0u ? seed : hp;
+                const uint64_t hk = hash_key_w(ph, (cy >> 16) & 31u, c0w, c1w, c2w, c3w), hx = hash_index_w(ph, cx);
+                const uint64_t hh = (cy & (1u << 13)) ? hk : hx;
+                const uint32_t wi = clive ? ci : 0u;
+                S.h[wi] = hh;
+                hl[wi] = hh;
             }
             lds_order();  // the next level reads these hashes
             dep = nd;
@@ -972,25 +970,30 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 bool t = false, isk = false, dec = false;
                 uint64_t val = 0, ph = root, key = 0;
                 uint32_t vop = 0;
-                if (j < ns && tiny) {
+                if (tiny) {
                     // a small document: the node's inputs, its hash and its parent's from LDS; its value, metadata
-                    // and string position in one round of loads
-                    i = ids16[j];
+                    // and string position in one round of loads -- every lane loads (a lane past the order reads
+                    // node 0's words and keeps nothing), so no branch
+                    const bool jl = j < ns;
+                    i = ids16[jl ? j : 0u];
                     const uint2 in = hin[i];
-                    rg = (in.y >> 14) & 3u;
-                    t = (in.y >> 21) & 1u;
-                    isk = (in.y >> 13) & 1u;
-                    dec = (in.y >> 23) & 1u;
+                    const uint32_t y = jl ? in.y : 0u;
+                    rg = (y >> 14) & 3u;
+                    t = (y >> 21) & 1u;
+                    isk = (y >> 13) & 1u;
+                    dec = (y >> 23) & 1u;
                     kop = in.x;
                     idx = in.x;
-                    kl = t && isk ? (in.y >> 16) & 31u : 0u;  // key bytes only for path-table entries
-                    key = hl[i] & mask;
-                    if (t && (in.y & 0xFFu)) ph = hl[in.y & 0xFFu] & mask;
-                    if (rg) {
-                        m = S.meta[i];
-                        val = S.val[i];
-                        if ((in.y >> 22) & 1u) vop = S.sidx[i];
-                    }
+                    kl = t && isk ? (y >> 16) & 31u : 0u;  // key bytes only for path-table entries
+                    const uint64_t hi_ = hl[i], hp = hl[y & 0xFFu];
+                    key = hi_ & mask;
+                    ph = (t && (y & 0xFFu)) ? hp & mask : root;
+                    const uint32_t m_ = S.meta[i];
+                    const uint64_t v_ = S.val[i];
+                    const uint32_t p_ = S.sidx[i];
+                    m = rg ? m_ : 0u;
+                    val = rg ? v_ : 0ull;
+                    vop = (rg && ((y >> 22) & 1u)) ? p_ : 0u;
                     ar = meta_arena(m);
                 } else if (j < ns) {
                     i = rk ? ids16[j] : sidx[j];
@@ -1027,10 +1030,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 for (uint32_t g = 0; g < 2; g++) {
                     const uint64_t bal = ballot(rg == g + 1);
                     const uint32_t inc = wave_incl_scan(rg == g + 1 ? ar : 0u);
-                    if (rg == g + 1) {
-                        my_rank = rank[g] + popc64(bal & mask_lt(lane));
-                        my_aoff = aoff[g] + inc - ar;
-                    }
+                    my_rank = rg == g + 1 ? rank[g] + mbcnt64(bal) : my_rank;
+                    my_aoff = rg == g + 1 ? aoff[g] + inc - ar : my_aoff;
                     rank[g] += popc64(bal);
                     aoff[g] += rdlane(inc, 63);
                 }
