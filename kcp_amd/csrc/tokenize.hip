@@ -581,63 +581,50 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         for (uint32_t i0 = 1; i0 < nn; i0 += 64) {
             const uint32_t i = i0 + lane;
             const bool live = i < nn;
-            uint4 r = make_uint4(0u, 0u, 0u, 0u);
-            if (live) r = S.rec[i];
+            // no per-lane branches in this loop: every lane loads (a lane past the nodes reads node 0's words) and
+            // every lane stores (what a lane keeps nothing of goes to node 0's slots, the root's, which no later
+            // phase reads; list entries past the lists go to slot ncap - 1, never a node)
+            const uint32_t ii = live ? i : 0u;
+            const uint4 r0 = S.rec[ii];
+            const uint64_t ks = S.skey[ii], pv = S.val[ii];  // the tree phase's key span and value positions
+            const uint4 r = live ? r0 : make_uint4(0u, 0u, 0u, 0u);
             const uint32_t rg = live ? region_of(r.w) : 0u;
-            const bool tb = live && in_tab(i, r.w);
-            const bool key = live && (r.y & KEYBIT) != 0u, leaf = live && (r.w & NI_LEAF) != 0u;
-            const bool str = leaf && (r.w & NI_STR), atom = leaf && (r.w & NI_ATOM);
-            const bool slow = str && (r.w & NI_SLOW);
-            uint32_t kop = 0, kcp = 0, vop = 0, vcp = 0;
-            if (key) {
-                const uint64_t ks = S.skey[i];  // the tree phase's key span
-                kop = (uint32_t)ks - 1u;
-                kcp = kop + 1u + (uint32_t)(ks >> 32);
-            }
-            if (str || atom) {
-                const uint64_t pv = S.val[i];  // the tree phase's value positions
-                vop = (uint32_t)pv;
-                vcp = (uint32_t)(pv >> 32);
-            }
-            const uint8_t* vp = d + vop + (str ? 1u : 0u);
-            uint64_t w0 = 0, w1 = 0, kw = 0;
-            if ((str && !slow) || atom) ld16u(vp, &w0, &w1);
-            if (key && r.x == 0) kw = ld8u(d + kop + 1);
-            bool store = leaf && !slow;
-            if (key) {
-                // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key
-                // equal to "items" under ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
-                if (r.x == 0 && kcp - kop - 1 == 5u && (kw & 0xDFDFDFDFDFull) == 0x534D455449ull) {
-                    err = GPUDIFF_TOK_LIST;
-                    store = false;
-                }
-            }
-            uint32_t tag = r.w & NI_TAG, mlen = 0;
-            uint64_t v = 0;
-            bool slow_atom = false;
-            if (store && str) {
-                const uint32_t sl = vcp - vop - 1;
-                mlen = sl;
-                // the value's first 8 bytes (a long string's tail goes to the arena in phase 5)
-                v = sl >= GPUDIFF_INLINE_MAX ? w0 : sl ? (w0 & (~0ull >> (64u - 8u * sl))) : 0ull;
-            } else if (store && atom) {
-                if (parse_atom_fast(w0, w1, len - vop, &tag, &v)) {
-                    slow_atom = true;  // parsed after the loop
-                    store = false;
-                }
-                mlen = (tag == GPUDIFF_TAG_INT || tag == GPUDIFF_TAG_FLOAT) ? 8u : 0u;
-            }
-            if (store) {
-                S.val[i] = v;
-                S.meta[i] = (mlen << 3) | tag;
-            }
-            if (small && live) {
-                const uint32_t dep = (r.w >> NI_DEPTH_SHIFT) & 0xFFu, kl = kcp - kop - 1;
-                atomicAdd(&h32[dep], 1u);
-                hin[i] = make_uint2(key ? kop + 1 : r.y, r.x | (dep << 8) | (key ? (1u << 13) | ((kl & 31u) << 16) : 0u) |
-                                                             (rg << 14) | (tb ? 1u << 21 : 0u) | (str ? 1u << 22 : 0u) |
-                                                             (slow ? 1u << 23 : 0u));
-                if (str && nn <= kRank + 1u) S.sidx[i] = vop;  // for phase 5 (the sort area is free up to kLdsSort)
+            const bool tb = live & in_tab(i, r.w);
+            const bool key = live & ((r.y & KEYBIT) != 0u), leaf = live & ((r.w & NI_LEAF) != 0u);
+            const bool str = leaf & ((r.w & NI_STR) != 0u), atom = leaf & ((r.w & NI_ATOM) != 0u);
+            const bool slow = str & ((r.w & NI_SLOW) != 0u);
+            const uint32_t kop = key ? (uint32_t)ks - 1u : 0u;
+            const uint32_t kcp = key ? kop + 1u + (uint32_t)(ks >> 32) : 0u;
+            const uint32_t vop = (str | atom) ? (uint32_t)pv : 0u, vcp = (str | atom) ? (uint32_t)(pv >> 32) : 0u;
+            uint64_t w0, w1;
+            ld16u(d + vop + (str ? 1u : 0u), &w0, &w1);
+            const uint64_t kw = ld8u(d + kop + 1u);
+            // the list probe of the informer's decoder (json.cpp decodes_as_list): a root key equal to "items" under
+            // ASCII case folding (a non-ASCII key is a slow key: TOK_KEY)
+            const bool items = key & (r.x == 0u) & (kcp - kop - 1u == 5u) & ((kw & 0xDFDFDFDFDFull) == 0x534D455449ull);
+            err = items ? GPUDIFF_TOK_LIST : err;
+            uint32_t atag = r.w & NI_TAG;
+            uint64_t av = 0;
+            const bool aslow = parse_atom_fast(w0, w1, len - vop, &atag, &av) != 0u;
+            const bool store0 = leaf & !slow & !items;
+            const bool slow_atom = store0 & atom & aslow;  // parsed after the loop
+            const bool store = store0 & !slow_atom;
+            const uint32_t sl = vcp - vop - 1u;
+            // the value's first 8 bytes (a long string's tail goes to the arena in phase 5)
+            const uint64_t sv = sl >= GPUDIFF_INLINE_MAX ? w0 : sl ? (w0 & (~0ull >> (64u - 8u * sl))) : 0ull;
+            const uint32_t tag = atom ? atag : r.w & NI_TAG;
+            const uint32_t mlen = str ? sl : ((tag == GPUDIFF_TAG_INT) | (tag == GPUDIFF_TAG_FLOAT)) ? 8u : 0u;
+            const uint64_t v = str ? sv : atom ? av : 0ull;
+            S.val[store ? i : 0u] = v;
+            S.meta[store ? i : 0u] = (mlen << 3) | tag;
+            if (small) {
+                const uint32_t dep = (r.w >> NI_DEPTH_SHIFT) & 0xFFu, kl = kcp - kop - 1u;
+                atomicAdd(&h32[live ? dep : 31u], live ? 1u : 0u);
+                hin[ii] = make_uint2(key ? kop + 1 : r.y, r.x | (dep << 8) | (key ? (1u << 13) | ((kl & 31u) << 16) : 0u) |
+                                                              (rg << 14) | (tb ? 1u << 21 : 0u) | (str ? 1u << 22 : 0u) |
+                                                              (slow ? 1u << 23 : 0u));
+                // for phase 5 (the sort area is free up to kLdsSort)
+                S.sidx[(str & (nn <= kRank + 1u)) ? i : 0u] = vop;
             }
             if (ballot(key && kcp - kop - 1 > 27u)) small = false;  // keys hashed from registers: <= 27 bytes
             // the blob's sizes (phase 5), counted here where every operand is in registers (wave totals, scalar)
@@ -651,19 +638,12 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             // strings that need decoding and atoms the window did not decide: listed for after the loop, the strings
             // from the front of the depth-order area, the atoms from its back, each with its value's token positions
             // in the hash area (both free until phase 3b)
-            const uint64_t sm = ballot(slow);
-            if (slow) {
-                const uint32_t q = nslow + mbcnt64(sm);
-                S.order[q] = i;
-                S.h[q] = ((uint64_t)rg << 56) | ((uint64_t)vcp << 32) | vop;  // positions < 2^24
-            }
+            const uint64_t sm = ballot(slow), am = ballot(slow_atom);
+            const uint32_t qs = nslow + mbcnt64(sm), qa = nn - 1u - (natom + mbcnt64(am));
+            const uint32_t q = slow ? qs : slow_atom ? qa : ncap - 1u;
+            S.order[q] = i;
+            S.h[q] = slow ? ((uint64_t)rg << 56) | ((uint64_t)vcp << 32) | vop : (uint64_t)vop;  // positions < 2^24
             nslow += popc64(sm);
-            const uint64_t am = ballot(slow_atom);
-            if (slow_atom) {
-                const uint32_t q = nn - 1u - (natom + mbcnt64(am));
-                S.order[q] = i;
-                S.h[q] = vop;
-            }
             natom += popc64(am);
         }
         if (nslow | natom) wave_sync();
