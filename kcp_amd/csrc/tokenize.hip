@@ -482,28 +482,31 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint64_t m_err = ballot(err != 0u);
             const uint64_t upto = m_err ? mask_lt((uint32_t)__builtin_ctzll(m_err)) : ~0ull;
             // node records (the root: no parent, no key, never a leaf)
-            if (is_node && ((upto >> lane) & 1ull) && id < ncap) {
+            {
+                // every lane stores: a token that makes no node here writes slot ncap - 1, which no node uses
+                const bool wr = is_node & (((upto >> lane) & 1ull) != 0ull) & (id < ncap);
+                const uint32_t wid = wr ? id : ncap - 1u;
                 const uint32_t leaf = (is_o & empty) ? NI_LEAF | (code == '{' ? GPUDIFF_TAG_EOBJ : GPUDIFF_TAG_EARR)
                                       : is_qo ? NI_LEAF | NI_STR | GPUDIFF_TAG_STR | (code == TK_OPENQ_SLOW ? NI_SLOW : 0u)
                                       : is_at ? NI_LEAF | NI_ATOM
                                               : 0u;
                 const uint32_t info = tb + lane == 0u ? R_NONE << NI_REG_SHIFT
                                                       : (reg << NI_REG_SHIFT) | leaf | ((uint32_t)lvl << NI_DEPTH_SHIFT);
-                S.rec[id] = make_uint4(tb + lane == 0u ? NONE : e_id, comp, tb + lane, info);
+                S.rec[wid] = make_uint4(tb + lane == 0u ? NONE : e_id, comp, tb + lane, info);
                 if constexpr (MODE == kModeEncode) {
                     // for phase 3a: a member's key span, a leaf's value positions (its slot until 3a fills it)
-                    if (comp & KEYBIT) S.skey[id] = ((uint64_t)(pm2 - pm3 - 1u) << 32) | (pm3 + 1u);
-                    S.val[id] = ((uint64_t)pn1 << 32) | pos;
+                    S.skey[(comp & KEYBIT) ? wid : ncap - 1u] = ((uint64_t)(pm2 - pm3 - 1u) << 32) | (pm3 + 1u);
+                    S.val[wid] = ((uint64_t)pn1 << 32) | pos;
                 }
             }
             const uint64_t ok_node = m_node & upto;
-            const uint64_t m_meta = ballot(is_node && lvl == 1 && cp3 == TK_KEY_META && code == '{') & upto;
-            const uint64_t m_lab = ballot(is_node && (my_info & LF_LAB)) & upto;
-            const uint64_t m_ann = ballot(is_node && (my_info & LF_ANN)) & upto;
+            const uint64_t m_meta = ballot(is_node & (lvl == 1) & (cp3 == TK_KEY_META) & (code == '{')) & upto;
+            const uint64_t m_lab = ballot(is_node & ((my_info & LF_LAB) != 0u)) & upto;
+            const uint64_t m_ann = ballot(is_node & ((my_info & LF_ANN) != 0u)) & upto;
             if (m_meta) meta_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_meta));
             if (m_lab) labels_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_lab));
             if (m_ann) annot_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_ann));
-            if (ballot(is_node && lvl == 1 && cp3 == TK_KEY_STATUS) & upto) has_status = true;
+            if (ballot(is_node & (lvl == 1) & (cp3 == TK_KEY_STATUS)) & upto) has_status = true;
             if (ballot(bad_lab) & upto) labels_ok = false;
             if (ballot(bad_ann) & upto) annot_ok = false;
             nn += popc64(ok_node);
