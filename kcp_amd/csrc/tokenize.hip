@@ -215,9 +215,12 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         const uint64_t c0 = ballot(tc & 1u), c1 = ballot(tc & 2u), c2 = ballot(tc & 4u);
         const uint32_t pre = mbcnt64(c0) + 2u * mbcnt64(c1) + 4u * mbcnt64(c2);
         const uint32_t j1 = opens ? (uint32_t)__builtin_ctz(opens) : 4u;  // most lanes hold at most one opening
-        const uint32_t kw1 = opens ? keyword(p4 + j1) : 0u;
+        // (every lane reads its keyword window -- LDS reads and compares, no branch; the result is used only at an
+        // opening quote)
+        const uint32_t kw1 = keyword(p4 + j1);
         const uint32_t op2 = opens & (opens - 1u);
-        const uint32_t kw2 = ballot(op2 != 0u) && op2 ? keyword(p4 + (uint32_t)__builtin_ctz(op2)) : 0u;
+        uint32_t kw2 = 0u;
+        if (ballot(op2 != 0u)) kw2 = keyword(p4 + (op2 ? (uint32_t)__builtin_ctz(op2) : 0u));  // uniform test
         // every lane stores four words: a byte that starts no token writes slot len + 1, which no token uses (a
         // document of len bytes has at most len tokens, tok_cap = len + 2) -- stores without a branch each
         uint32_t k = ntok + pre;
