@@ -549,7 +549,16 @@ __device__ __forceinline__ uint32_t parse_atom_fast(uint64_t w0, uint64_t w1, ui
     const uint32_t d0 = c == '-' ? 1u : 0u;
     uint32_t k = d0;
     uint64_t v = 0;
-    while (k < avail && is_digit(win16_at(w0, w1, k))) v = v * 10u + (win16_at(w0, w1, k++) - '0');
+    bool run = true;
+    // the digit run, 16 predicated steps (a loop with a per-lane trip count switched the exec mask every step)
+#pragma unroll
+    for (uint32_t s = 0; s < 16u; s++) {
+        const uint32_t cs = (uint32_t)(((s < 8u ? w0 : w1) >> (8u * (s & 7u))) & 0xFFu);
+        const bool dig = run & (s >= d0) & (s < avail) & is_digit(cs);
+        v = dig ? v * 10u + (cs - '0') : v;
+        k = dig ? s + 1u : k;
+        run = run & ((s < d0) | dig);
+    }
     const uint32_t nd = k - d0;
     // accepted: 1..15 digits, no leading zero unless alone, then the document's end or a delimiter that is not
     // the start of a fraction or an exponent ('.', 'e', 'E' are no delimiters)
