@@ -699,9 +699,45 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     *(uint64_t*)(st + o + 8u) = a1;
                 }
                 lds_order();
-                dl = lane == 0 ? decode_string(st, st + raw, st + raw + 1u, st + ob) : 0;
+                // the common case by the whole wave, a lane per byte: only ASCII bytes and the escapes \" \\ \/ \b \f
+                // \n \r \t -- an escaped byte maps to its character, its backslash emits nothing. Anything else (a \u
+                // escape, a non-ASCII byte, an invalid escape) is left to lane 0's decode_string, which also decides
+                // its errors (lane 0 alone paid ~14 scalar instructions a byte on the CU's one scalar unit)
+                bool simple = true;
+                uint32_t outn = 0, carry = 0;
+                for (uint32_t o = 0; o < raw; o += 64u) {
+                    const uint32_t p = o + lane;
+                    const bool in = p < raw;
+                    const uint32_t c = in ? st[p] : 0x20u;
+                    const uint64_t bs = ballot(in & (c == '\\'));
+                    uint64_t esc = carry;  // byte 0 of this chunk escaped by the previous chunk's last byte
+                    carry = 0;
+                    for (uint64_t m = bs; m; m &= m - 1) {
+                        const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                        if ((esc >> b) & 1ull) continue;  // an escaped backslash escapes nothing
+                        if (b == 63u) carry = 1;
+                        else esc |= 1ull << (b + 1u);
+                    }
+                    const bool e = (esc >> lane) & 1ull;
+                    const bool ok_e = (c == '"') | (c == '\\') | (c == '/') | (c == 'b') | (c == 'f') | (c == 'n') |
+                                      (c == 'r') | (c == 't');
+                    if (ballot(in & ((c >= 0x80u) | (e & !ok_e)))) {
+                        simple = false;
+                        break;
+                    }
+                    const bool emit = in & !((c == '\\') & !e);
+                    const uint32_t mc = c == 'b' ? 8u : c == 'f' ? 12u : c == 'n' ? 10u : c == 'r' ? 13u : c == 't' ? 9u : c;
+                    const uint64_t em = ballot(emit);
+                    if (emit) st[ob + outn + mbcnt64(em)] = (uint8_t)(e ? mc : c);
+                    outn += popc64(em);
+                }
                 lds_order();
-                dl = (int)rdlane((uint32_t)dl, 0);
+                dl = (int)outn;
+                if (!simple) {
+                    dl = lane == 0 ? decode_string(st, st + raw, st + raw + 1u, st + ob) : 0;
+                    lds_order();
+                    dl = (int)rdlane((uint32_t)dl, 0);
+                }
                 if (dl > 0) {
                     for (uint32_t o = lane; o < (uint32_t)dl; o += 64u) dst[o] = st[ob + o];
                     h8 = *(const uint64_t*)(st + ob);
