@@ -103,6 +103,10 @@ EDGE_OK = [
     b'{"spec":{"n":[0.000000000000000000000000000000000001,-123456789.12345678900000000000000000,'
     b'1.00000000000000000000000000000000000000000000e-3,12345678901234.5,2.5]}}', b'{"a":2.5}', b'{"a":-7e-1}',
     b'{"spec":{"t":1.5,"u":"x\\ty","v":3.25e1,"w":"\\u00e9","x":[0.5,true,"q\\"r",-0.25]}}',
+    # strings unescaped by the whole wave (only ASCII and simple escapes), escapes across the 64-byte chunks
+    b'{"spec":{"a":"' + b'a' * 63 + b'\\"' + b'b' * 70 + b'\\\\\\n' + b'c' * 60 + b'\\t\\/\\b\\f\\r"}}',
+    b'{"spec":{"c":["' + b'\\\\' * 40 + b'","x\\"y","' + b'z' * 62 + b'\\\\\\"",' + b'"\\u00e9\\n"]}}',
+    b'{"spec":{"d":"' + b'q' * 64 + b'\\n' * 64 + b'"}}',
     b'{"spec":{"t":true,"f":false,"z":null,"a":[true,false,null]}}',
     b'{"a":null,"b":1,"metadata":{"labels":{"x":"1","y":"2"},"annotations":{"k":"v","k2":"long value here"}}}',
     b'{"metadata":{"labels":{"x":"1","y":2}},"spec":1}', b'{"metadata":{"labels":{}},"spec":1}',
