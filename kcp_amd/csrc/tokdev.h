@@ -783,6 +783,28 @@ __device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* 
     }
 }
 
+// copies this lane's n bytes at s into 4-byte aligned o as whole dwords, the last one zero past n (K0's arena
+// tails), flattened over the wave like wave_copy_flat
+__device__ void wave_copy_dwords0(bool has, const uint8_t* s, uint32_t n, uint32_t* o) {
+    const uint32_t lane = __lane_id();
+    const FlatUnits f = flat_units(has, n);
+    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const uint64_t sp = (uint64_t)(uintptr_t)s, dp = (uint64_t)(uintptr_t)o;
+    for (uint32_t b = 0; b < f.total; b += 64) {
+        const uint32_t g = b + lane;
+        const uint32_t ow = flat_owner(f, g);
+        const uint32_t first = shfl32(f.incl - units, ow), on = shfl32(n, ow);
+        const uint64_t op = shfl64(sp, ow), od = shfl64(dp, ow);
+        if (g < f.total) {
+            const uint32_t u = g - first;
+            uint32_t w = (uint32_t)ld8u((const uint8_t*)(uintptr_t)op + 4u * u);
+            const uint32_t rem = on - 4u * u;
+            if (rem < 4u) w &= (1u << (8u * rem)) - 1u;
+            ((uint32_t*)(uintptr_t)od)[u] = w;
+        }
+    }
+}
+
 // ---- float64 -> Go text (floatEncoder(64): strconv.AppendFloat(f, 'f'|'e', -1, 64)
 // with the 1e-6 / 1e21 switch and the e-09 -> e-9 clean-up).  The shortest,
 // closest (ties to even) digit string is Ryu's (Adams, PLDI 2018): this is

@@ -1080,61 +1080,19 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 tko += rdlane(kinc, 63);
                 // key bytes of the path-table entries and the long strings' tails (the bytes after the first 8,
                 // which sit in the leaf record; 4-byte aligned arena offsets, the last dword zero past the value):
-                // ONE wave-cooperative flattened copy over every lane's two spans at once, 4 bytes a unit, two blocks
-                // of 64 units per trip with both blocks' loads issued before their stores (one copy loop per string,
-                // each a chain of dependent loads, cost this phase a quarter of K0's time, profiles/r05a; two
-                // separate flattened loops paid a load round trip each, profiles/r05w)
-                {
-                    const bool tail = ar != 0u;
-                    const uint32_t tlen = tail ? (m >> 3) - GPUDIFF_INLINE_MAX : 0u;
-                    const uint32_t uk = (t && kl) ? (kl + 3u) >> 2 : 0u, u = uk + (tail ? (tlen + 3u) >> 2 : 0u);
-                    const uint32_t incl = wave_incl_scan(u), total = rdlane(incl, 63);
-                    // per lane, as 32-bit offsets: key source in the document, key destination in the blob, tail
-                    // source (bit 31: from the decoded-string area) and destination in the blob
-                    const uint32_t f_first = incl - u, f_kn = t ? kl : 0u, f_ks = kop;
-                    const uint32_t f_kd = (uint32_t)((keys + ko) - blob);
-                    const uint32_t f_ts = (dec ? 0x80000000u : 0u) | (vop + 1u + GPUDIFF_INLINE_MAX);
-                    const uint32_t f_td = tail ? (uint32_t)(segp[rg - 1u] + 16ull * Lr[rg - 1u] + my_aoff - blob) : 0u;
-                    for (uint32_t b = 0; b < total; b += 128u) {
-                        uint32_t w[2], dsto[2], nb[2];
-                        bool isk_[2], live_[2];
-#pragma unroll
-                        for (uint32_t h = 0; h < 2; h++) {
-                            const uint32_t g = b + 64u * h + lane;
-                            uint32_t ow = 0;
-#pragma unroll
-                            for (uint32_t st = 32; st >= 1; st >>= 1)
-                                if (shfl32(incl, ow + st - 1u) <= g) ow += st;
-                            ow = min(ow, 63u);
-                            const uint32_t k = g - shfl32(f_first, ow), uko = shfl32(uk, ow);
-                            const bool ik = k < uko;
-                            const uint32_t kn = shfl32(f_kn, ow), ks_ = shfl32(f_ks, ow), kd = shfl32(f_kd, ow);
-                            const uint32_t ts = shfl32(f_ts, ow), td = shfl32(f_td, ow), tl = shfl32(tlen, ow);
-                            const uint32_t kt = k - uko;  // the tail unit
-                            const uint8_t* src = ik ? d + ks_ + 4u * k
-                                                    : ((ts & 0x80000000u) ? S.str : d) + (ts & 0x7FFFFFFFu) + 4u * kt;
-                            live_[h] = g < total;
-                            isk_[h] = ik;
-                            w[h] = (uint32_t)ld8u(live_[h] ? src : d);
-                            dsto[h] = ik ? kd + 4u * k : td + 4u * kt;
-                            nb[h] = ik ? min(4u, kn - 4u * k) : min(4u, tl - 4u * kt);
-                        }
-#pragma unroll
-                        for (uint32_t h = 0; h < 2; h++) {
-                            if (live_[h]) {
-                                uint8_t* q = blob + dsto[h];
-                                if (isk_[h]) {
-                                    q[0] = (uint8_t)w[h];
-                                    if (nb[h] > 1) q[1] = (uint8_t)(w[h] >> 8);
-                                    if (nb[h] > 2) q[2] = (uint8_t)(w[h] >> 16);
-                                    if (nb[h] > 3) q[3] = (uint8_t)(w[h] >> 24);
-                                } else {
-                                    *(uint32_t*)q = nb[h] < 4u ? w[h] & ((1u << (8u * nb[h])) - 1u) : w[h];
-                                }
-                            }
-                        }
-                    }
+                // wave-cooperative flattened copies over every lane's span at once (one copy loop per string,
+                // each a chain of dependent loads, cost this phase a quarter of K0's time, profiles/r05a)
+                wave_copy_flat(t && kl, d + kop, kl, keys + ko);
+                const bool tail = ar != 0u;
+                const uint8_t* tsrc = nullptr;
+                uint32_t* tdst = nullptr;
+                uint32_t tlen = 0;
+                if (tail) {
+                    tsrc = (dec ? (S.str + vop + 1) : (d + vop + 1)) + GPUDIFF_INLINE_MAX;
+                    tlen = (m >> 3) - GPUDIFF_INLINE_MAX;
+                    tdst = (uint32_t*)(segp[rg - 1u] + 16ull * Lr[rg - 1u] + my_aoff);
                 }
+                wave_copy_dwords0(tail, tsrc, tlen, tdst);
             }
             // zero each arena's tail pad (its values end 4-byte aligned; the arena is a multiple of 16)
             for (uint32_t g = 0; g < 2; g++) {
