@@ -827,8 +827,14 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 const uint32_t par = cy & 0xFFu;
                 const uint64_t hp = hl[par];
                 const uint64_t ph = par == 0u ? seed : hp;
-                const uint64_t hk = hash_key_w(ph, (cy >> 16) & 31u, c0w, c1w, c2w, c3w), hx = hash_index_w(ph, cx);
-                const uint64_t hh = (cy & (1u << 13)) ? hk : hx;
+                // one XXH64 over the component's words, selected: 0x01 u32le(klen) key bytes | 0x02 u32le(index)
+                // (hash_key_w / hash_index_w, tokdev.h)
+                const bool isk = (cy & (1u << 13)) != 0u;
+                const uint32_t kl = (cy >> 16) & 31u;
+                const uint64_t W0 = isk ? 0x01ull | ((uint64_t)kl << 8) | (c0w << 40) : 0x02ull | ((uint64_t)cx << 8);
+                const uint64_t W1 = isk ? (c0w >> 24) | (c1w << 40) : 0ull, W2 = isk ? (c1w >> 24) | (c2w << 40) : 0ull;
+                const uint64_t W3 = isk ? (c2w >> 24) | (c3w << 40) : 0ull;
+                const uint64_t hh = xxh64_small(ph, isk ? kl + 5u : 5u, W0, W1, W2, W3);
                 const uint32_t wi = clive ? ci : 0u;
                 S.h[wi] = hh;
                 hl[wi] = hh;
