@@ -44,7 +44,7 @@ constexpr uint32_t kLdsPerWave = 5120;
 constexpr uint32_t kLdsSort = 384;  // node keys sorted in LDS up to this many (12 B each)
 constexpr uint32_t kLdsOrder = 768;  // phase 3b's depth order in LDS up to this many nodes (4 B each, behind 2 KiB)
 constexpr uint32_t kLdsHash = 256;   // ... and up to this many nodes their hashes too (order 1 KiB + hashes 2 KiB)
-constexpr uint32_t kRank = 128;      // phase 4 ranks up to this many node keys in LDS (no sort arrays)
+constexpr uint32_t kRank = 256;      // phase 4 ranks up to this many node keys in LDS (no sort arrays)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -476,7 +476,7 @@ __device__ __forceinline__ uint32_t win16_at(uint64_t w0, uint64_t w1, uint32_t 
     return (uint32_t)((((w0 & ~m) | (w1 & m)) >> (8u * (k & 7u))) & 0xFFu);
 }
 // K0's sort of up to kRank node keys: keys[j] & mask (j < ns) are node j + 1's key, in LDS (phase 3b's hashes).
-// Lane k ranks keys k and k + 64 by counting the keys below each -- all ns read two at a time by broadcast -- and
+// Lane k ranks keys k, k + 64, ... by counting the keys below each -- all ns read two at a time by broadcast -- and
 // writes its nodes' ids to their ranks in ids. Ranks are a permutation when the keys are distinct; an equal pair (a
 // duplicate or a collision under the seed) or a key equal to the root's hash sets GPUDIFF_TOK_HASH instead, as the
 // bitonic path's check does
@@ -524,7 +524,8 @@ __device__ __forceinline__ void rank_sort_n(const uint64_t* keys, uint64_t mask,
 __device__ __forceinline__ void rank_sort(const uint64_t* keys, uint64_t mask, uint16_t* ids, uint32_t ns,
                                           uint32_t lane, uint64_t root, uint32_t& status) {
     if (ns <= 64u) rank_sort_n<1>(keys, mask, ids, ns, lane, root, status);
-    else rank_sort_n<2>(keys, mask, ids, ns, lane, root, status);
+    else if (ns <= 128u) rank_sort_n<2>(keys, mask, ids, ns, lane, root, status);
+    else rank_sort_n<4>(keys, mask, ids, ns, lane, root, status);
 }
 
 // K0's values pass: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or

@@ -910,7 +910,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
     uint32_t* sidx = ns <= kLdsSort ? (uint32_t*)(lds + 8 * kLdsSort) : S.sidx;
     // up to kRank nodes: ranked straight from phase 3b's hashes in LDS into a u16 node order (the node records and
     // hash inputs stay in LDS for phase 5); more: the keys sorted with their node ids
-    const bool rk = ns <= kRank;
+    const bool rk = ns <= kRank && h_in_lds;  // (the hashes must be in LDS: nn <= kLdsHash)
     uint16_t* const ids16 = (uint16_t*)(lds + 2304);
     if (status == GPUDIFF_TOK_OK && ns) {
         const uint64_t root = seed & mask;

@@ -117,6 +117,11 @@ EDGE_OK = [
     b'{"spec":{"big":"' + b'x' * 5000 + b'"}}',
     b'{"spec":{"esc":"' + b'\\"' * 700 + b'"}}',
     b'{"spec":{"arr":[' + b",".join(b"%d" % i for i in range(300)) + b']}}',
+    # around phase 4's rank-sort bound (256 node keys with the hashes in LDS) and the LDS hash bound (256 nodes)
+    b'{"spec":{"arr":[' + b",".join(b"%d" % i for i in range(199)) + b']}}',
+    b'{"spec":{"arr":[' + b",".join(b"%d" % i for i in range(253)) + b']}}',
+    b'{"spec":{"arr":[' + b",".join(b"%d" % i for i in range(254)) + b']}}',
+    b'{"spec":{' + b",".join(b'"k%03d":"v%d"' % (i, i) for i in range(200)) + b'}}',
     b'{"spec":' + b'[' * 200 + b'1' + b']' * 200 + b'}',
     b'{"spec":{"obj":{' + b",".join(b'"k%03d":{"v":"val%d","n":%d}' % (i, i, i) for i in range(150)) + b'}}}',
     b'\n\t {"spec" : { "a" : [ 1 , 2 ] , "b" : "c" } , "status" : { "ok" : true } }\r\n',
