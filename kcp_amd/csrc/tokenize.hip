@@ -663,7 +663,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 ld32u(d + aop, d + len + kTokSlack, w0, w1, w2, w3);
                 uint32_t tag = GPUDIFF_TAG_NULL;
                 uint64_t v = 0;
-                const uint32_t e = parse_atom_win(d + aop, d + len, w0, w1, w2, w3, &tag, &v);
+                uint32_t e = 0;
+                if (parse_num_w32(w0, w1, w2, w3, len - aop, &tag, &v))
+                    e = parse_atom_mem(d + aop, d + len, &tag, &v);
                 if (e) {
                     err = e;
                 } else {

@@ -103,6 +103,14 @@ EDGE_OK = [
     b'{"spec":{"n":[0.000000000000000000000000000000000001,-123456789.12345678900000000000000000,'
     b'1.00000000000000000000000000000000000000000000e-3,12345678901234.5,2.5]}}', b'{"a":2.5}', b'{"a":-7e-1}',
     b'{"spec":{"t":1.5,"u":"x\\ty","v":3.25e1,"w":"\\u00e9","x":[0.5,true,"q\\"r",-0.25]}}',
+    # the slow-atom pass's predicated parser: 16-18 digit integers, exponent forms, numbers filling the 32-byte window,
+    # every delimiter after a number, zeros in every position
+    b'{"spec":{"i":[1234567890123456,-12345678901234567,123456789012345678,-999999999999999999,'
+    b'1000000000000000000,-1000000000000000000],"e":[1e05,1E+05,1e-05,0e0,-0e5,0.0e0,-0.000e-7,10e1,1.50e+02]}}',
+    b'{"spec":{"w":[1.234567890123456789000000000e1,-0.0000000000000000000000000012345,0.00000000000000000000000000001,'
+    b'123456789.0000000000000000000000e-3,-1234567890123456789000000000000]}}',
+    b'{"spec":{"d":[1.5 ,2.5\t,3.5\n,4.5\r,5.5],"o":{"a":6.5},"p":{"b":7.5 },"q":[8.5]}}',
+    b'{"spec":{"z":[100.001,0.100,1000000000000000000000e-21,12345678901234567890e-10,0.5e-0]}}',
     # strings unescaped by the whole wave (only ASCII and simple escapes), escapes across the 64-byte chunks
     b'{"spec":{"a":"' + b'a' * 63 + b'\\"' + b'b' * 70 + b'\\\\\\n' + b'c' * 60 + b'\\t\\/\\b\\f\\r"}}',
     b'{"spec":{"c":["' + b'\\\\' * 40 + b'","x\\"y","' + b'z' * 62 + b'\\\\\\"",' + b'"\\u00e9\\n"]}}',
@@ -146,6 +154,12 @@ EDGE_DEFER = [
     (b'{"a" 1}', G.TOK_SYNTAX), (b'{"a":1}x', G.TOK_SYNTAX), (b'{"a":1} {}', G.TOK_SYNTAX),
     (b'{"a":"x}', G.TOK_SYNTAX), (b'{"a":tru}', G.TOK_SYNTAX), (b'{"a":01}', G.TOK_SYNTAX),
     (b'{"a":-}', G.TOK_SYNTAX), (b'{"a":1.}', G.TOK_SYNTAX), (b'{"a":.5}', G.TOK_SYNTAX),
+    (b'{"a":1.e5}', G.TOK_SYNTAX), (b'{"a":1e+}', G.TOK_SYNTAX), (b'{"a":1ee5}', G.TOK_SYNTAX),
+    (b'{"a":1.5.5}', G.TOK_SYNTAX), (b'{"a":--1}', G.TOK_SYNTAX), (b'{"a":+1}', G.TOK_SYNTAX),
+    (b'{"a":1e5.5}', G.TOK_SYNTAX), (b'{"a":-.5}', G.TOK_SYNTAX), (b'{"a":0x10}', G.TOK_SYNTAX),
+    (b'{"a":1.5e+-3}', G.TOK_SYNTAX), (b'{"a":00.5}', G.TOK_SYNTAX), (b'{"a":-01.5}', G.TOK_SYNTAX),
+    (b'{"a":1.5E}', G.TOK_SYNTAX), (b'{"a":2.5x}', G.TOK_SYNTAX), (b'{"a":12345678901234567.5q}', G.TOK_SYNTAX),
+    (b'{"a":1.23456789012345678901}', G.TOK_NUMBER),
     (b'{"a":[1 2]}', G.TOK_SYNTAX), (b'{"a":{"b":1]}', G.TOK_SYNTAX), (b'{a:1}', G.TOK_SYNTAX),
     (b'{"a":1', G.TOK_SYNTAX), (b'{"a":truex}', G.TOK_SYNTAX), (b'{"a":"b"c}', G.TOK_SYNTAX),
     (b'\xef\xbb\xbf{"a":1}', G.TOK_SYNTAX), (b'{"a":\\"b"}', G.TOK_SYNTAX), (b'{"a":1}}', G.TOK_SYNTAX),
