@@ -194,6 +194,51 @@ __device__ __forceinline__ uint64_t xxh64_small(uint64_t seed, uint32_t L, uint6
     }
     return xavalanche(h);
 }
+// xxh64_small for a wave of lanes hashing at once (K0's small-document level loop): a step that no lane of the
+// wave takes is skipped by a uniform branch on a ballot (most path components are keys of at most 10 bytes or
+// indices: one word step and the tail; each step skipped saves two to three 64-bit multiplies of the wave)
+__device__ __forceinline__ uint64_t xxh64_small_wave(uint64_t seed, uint32_t L, uint64_t W0, uint64_t W1, uint64_t W2,
+                                                     uint64_t W3) {
+    uint64_t h = seed + XP5;
+    if (__builtin_amdgcn_ballot_w64(L >= 32u)) {  // a 27-byte key: exactly one stripe
+        const uint64_t v1 = xround(seed + XP1 + XP2, W0), v2 = xround(seed + XP2, W1), v3 = xround(seed, W2),
+                       v4 = xround(seed - XP1, W3);
+        const uint64_t hs = xmerge(xmerge(xmerge(xmerge(xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18),
+                                                        v1), v2), v3), v4);
+        h = L >= 32u ? hs : h;
+    }
+    h += L;
+    const uint32_t rem = L & 31u, n8 = rem >> 3;
+    if (__builtin_amdgcn_ballot_w64(n8 > 0u)) {
+        const uint64_t hn = xrotl(h ^ xround(0, W0), 27) * XP1 + XP4;
+        h = n8 > 0u ? hn : h;
+    }
+    if (__builtin_amdgcn_ballot_w64(n8 > 1u)) {
+        const uint64_t hn = xrotl(h ^ xround(0, W1), 27) * XP1 + XP4;
+        h = n8 > 1u ? hn : h;
+    }
+    if (__builtin_amdgcn_ballot_w64(n8 > 2u)) {
+        const uint64_t hn = xrotl(h ^ xround(0, W2), 27) * XP1 + XP4;
+        h = n8 > 2u ? hn : h;
+    }
+    uint64_t wr = n8 == 0u ? W0 : n8 == 1u ? W1 : n8 == 2u ? W2 : W3;
+    uint32_t r = rem & 7u;
+    const bool four = r >= 4u;
+    if (__builtin_amdgcn_ballot_w64(four)) {
+        const uint64_t h4 = xrotl(h ^ ((uint64_t)(uint32_t)wr * XP1), 23) * XP2 + XP3;
+        h = four ? h4 : h;
+    }
+    wr = four ? wr >> 32 : wr;
+    r = four ? r - 4u : r;
+#pragma unroll
+    for (uint32_t k = 0; k < 3u; k++) {
+        if (__builtin_amdgcn_ballot_w64(k < r)) {
+            const uint64_t hk = xrotl(h ^ (((wr >> (8u * k)) & 0xFFu) * XP5), 11) * XP1;
+            h = k < r ? hk : h;
+        }
+    }
+    return xavalanche(h);
+}
 // hash_key over a key of at most 27 bytes held in registers: w0..w3 = the 32 bytes at the key (ld32u); word i >= 1
 // of the component holds key bytes [8i - 5, 8i + 3), the high five bytes of w[i - 1] and the low three of w[i]
 __device__ __forceinline__ uint64_t hash_key_w(uint64_t seed, uint32_t klen, uint64_t w0, uint64_t w1, uint64_t w2,

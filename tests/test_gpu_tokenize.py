@@ -111,6 +111,9 @@ EDGE_OK = [
     b'123456789.0000000000000000000000e-3,-1234567890123456789000000000000]}}',
     b'{"spec":{"d":[1.5 ,2.5\t,3.5\n,4.5\r,5.5],"o":{"a":6.5},"p":{"b":7.5 },"q":[8.5]}}',
     b'{"spec":{"z":[100.001,0.100,1000000000000000000000e-21,12345678901234567890e-10,0.5e-0]}}',
+    # keys of every length up to the small-document bound (27 bytes: a 32-byte hash stream, one XXH64 stripe) beside
+    # array indices in the same levels
+    b'{"spec":{' + b",".join(b'"%s":[%d,{"%s":%d}]' % (b"k" * n, n, b"q" * (27 - n), n) for n in range(28)) + b'}}',
     # strings unescaped by the whole wave (only ASCII and simple escapes), escapes across the 64-byte chunks
     b'{"spec":{"a":"' + b'a' * 63 + b'\\"' + b'b' * 70 + b'\\\\\\n' + b'c' * 60 + b'\\t\\/\\b\\f\\r"}}',
     b'{"spec":{"c":["' + b'\\\\' * 40 + b'","x\\"y","' + b'z' * 62 + b'\\\\\\"",' + b'"\\u00e9\\n"]}}',
