@@ -881,10 +881,11 @@ __device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* 
             const uint32_t w = (uint32_t)ld8u((const uint8_t*)(uintptr_t)op + k);
             uint8_t* q = (uint8_t*)(uintptr_t)od + k;
             const uint32_t nb = min(4u, on - k);
+            // four stores without a branch: a byte past the span stores byte 0 again (same lane, same value)
             q[0] = (uint8_t)w;
-            if (nb > 1) q[1] = (uint8_t)(w >> 8);
-            if (nb > 2) q[2] = (uint8_t)(w >> 16);
-            if (nb > 3) q[3] = (uint8_t)(w >> 24);
+            q[nb > 1u ? 1u : 0u] = (uint8_t)(nb > 1u ? w >> 8 : w);
+            q[nb > 2u ? 2u : 0u] = (uint8_t)(nb > 2u ? w >> 16 : w);
+            q[nb > 3u ? 3u : 0u] = (uint8_t)(nb > 3u ? w >> 24 : w);
         }
     }
 }

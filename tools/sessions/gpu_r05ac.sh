@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 5 (ac): K0's slow-atom pass with the predicated number parser and the level loop's XXH64 skipping steps no
-# lane takes -- byte-identical tests, blob diff, then K0's rate A/B: both, the parser alone, neither (same box,
+# Round 5 (ac): K0: key-byte copies without per-byte branches, the level loop's XXH64 skipping steps no lane takes,
+# the slow-atom pass's predicated number parser -- byte-identical tests, blob diff, then K0's rate A/B: all three,
+# without the copy change, the parser alone, none (same box,
 # interleaved).
 set -o pipefail
 O=gpurun_out/r05ac; mkdir -p $O
@@ -10,7 +11,7 @@ tail -1 $O/pytest_tok.log
 timeout -k 10 200 python -u tools/k0_diff.py > $O/k0_diff.txt 2>&1 || { tail -20 $O/k0_diff.txt; exit 1; }
 grep differing $O/k0_diff.txt | cut -c1-200
 for r in 1 2; do
-  for v in new parser base; do
+  for v in new hash parser base; do
     L=""; [ $v != new ] && L="--lib kcp_amd/_exp/libgpudiff_$v.so"
     timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/k0kt_${v}_r$r -o k0 --output-format csv -- python tools/k0_bench.py --profile $L > $O/k0_bench_${v}_r$r.json 2> $O/k0_bench_${v}_r$r.log || { tail -20 $O/k0_bench_${v}_r$r.log; exit 1; }
   done
