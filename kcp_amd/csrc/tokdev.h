@@ -194,51 +194,6 @@ __device__ __forceinline__ uint64_t xxh64_small(uint64_t seed, uint32_t L, uint6
     }
     return xavalanche(h);
 }
-// xxh64_small for a wave of lanes hashing at once (K0's small-document level loop): a step that no lane of the
-// wave takes is skipped by a uniform branch on a ballot (most path components are keys of at most 10 bytes or
-// indices: one word step and the tail; each step skipped saves two to three 64-bit multiplies of the wave)
-__device__ __forceinline__ uint64_t xxh64_small_wave(uint64_t seed, uint32_t L, uint64_t W0, uint64_t W1, uint64_t W2,
-                                                     uint64_t W3) {
-    uint64_t h = seed + XP5;
-    if (__builtin_amdgcn_ballot_w64(L >= 32u)) {  // a 27-byte key: exactly one stripe
-        const uint64_t v1 = xround(seed + XP1 + XP2, W0), v2 = xround(seed + XP2, W1), v3 = xround(seed, W2),
-                       v4 = xround(seed - XP1, W3);
-        const uint64_t hs = xmerge(xmerge(xmerge(xmerge(xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18),
-                                                        v1), v2), v3), v4);
-        h = L >= 32u ? hs : h;
-    }
-    h += L;
-    const uint32_t rem = L & 31u, n8 = rem >> 3;
-    if (__builtin_amdgcn_ballot_w64(n8 > 0u)) {
-        const uint64_t hn = xrotl(h ^ xround(0, W0), 27) * XP1 + XP4;
-        h = n8 > 0u ? hn : h;
-    }
-    if (__builtin_amdgcn_ballot_w64(n8 > 1u)) {
-        const uint64_t hn = xrotl(h ^ xround(0, W1), 27) * XP1 + XP4;
-        h = n8 > 1u ? hn : h;
-    }
-    if (__builtin_amdgcn_ballot_w64(n8 > 2u)) {
-        const uint64_t hn = xrotl(h ^ xround(0, W2), 27) * XP1 + XP4;
-        h = n8 > 2u ? hn : h;
-    }
-    uint64_t wr = n8 == 0u ? W0 : n8 == 1u ? W1 : n8 == 2u ? W2 : W3;
-    uint32_t r = rem & 7u;
-    const bool four = r >= 4u;
-    if (__builtin_amdgcn_ballot_w64(four)) {
-        const uint64_t h4 = xrotl(h ^ ((uint64_t)(uint32_t)wr * XP1), 23) * XP2 + XP3;
-        h = four ? h4 : h;
-    }
-    wr = four ? wr >> 32 : wr;
-    r = four ? r - 4u : r;
-#pragma unroll
-    for (uint32_t k = 0; k < 3u; k++) {
-        if (__builtin_amdgcn_ballot_w64(k < r)) {
-            const uint64_t hk = xrotl(h ^ (((wr >> (8u * k)) & 0xFFu) * XP5), 11) * XP1;
-            h = k < r ? hk : h;
-        }
-    }
-    return xavalanche(h);
-}
 // hash_key over a key of at most 27 bytes held in registers: w0..w3 = the 32 bytes at the key (ld32u); word i >= 1
 // of the component holds key bytes [8i - 5, 8i + 3), the high five bytes of w[i - 1] and the low three of w[i]
 __device__ __forceinline__ uint64_t hash_key_w(uint64_t seed, uint32_t klen, uint64_t w0, uint64_t w1, uint64_t w2,
@@ -576,7 +531,7 @@ __device__ __forceinline__ void rank_sort(const uint64_t* keys, uint64_t mask, u
 // K0's values pass: the common atoms -- true, false, null and integers of at most 15 digits ending in a delimiter or
 // the document's end -- from the 16-byte register window w0, w1 at the atom (left: bytes to the document's end).
 // 0: decided (tag, val); 1: not decided here -- floats, exponents, longer numbers, any syntax doubt go to
-// K0's slow-atom pass (parse_num_w32, else parse_atom_mem), whose answers are parse_atom_core's by construction.
+// parse_atom_win (K0's slow-atom pass), whose answers are parse_atom_mem's, so results are by construction.
 __device__ __forceinline__ uint32_t parse_atom_fast(uint64_t w0, uint64_t w1, uint64_t left, uint32_t* tag,
                                                     uint64_t* val) {
     const uint32_t avail = left < 16u ? (uint32_t)left : 16u;
@@ -616,83 +571,23 @@ __device__ __forceinline__ uint32_t parse_atom_fast(uint64_t w0, uint64_t w1, ui
     *val = d0 ? 0ull - v : v;
     return 0u;
 }
-// K0's slow-atom pass, the common numbers without a per-digit branch: -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?
-// ending in a delimiter or the document's end inside the 32-byte window w0..w3 (left: bytes to the document's end),
-// as 32 predicated steps of one uniform loop. Returns 0 with tag / val when it decides (an integer of at most 18
-// digits, or a float of at most 19 significant digits that decimal_to_double converts exactly), 1 otherwise:
-// parse_atom_mem then decides from memory, so the results are parse_atom_core's by construction (the window parse
-// this replaced, parse_atom_core over the window, switched the exec mask at every digit of its loops)
-__device__ __forceinline__ uint32_t parse_num_w32(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint64_t left,
-                                                  uint32_t* tag, uint64_t* val) {
-    const bool neg = (w0 & 0xFFu) == '-';
-    uint32_t ph = 0;  // 0 integer digits, 1 fraction digits, 2 exponent sign or digit, 3 exponent digits, 4 done
-    bool bad = false, eneg = false, too_many = false;
-    uint32_t n_int = 0, n_frac = 0, n_exp = 0, nsig = 0, nsig_last = 0, tz = 0, first = 0;
-    uint64_t wall = 0, wlast = 0;
-    uint32_t ex = 0;
-    const uint32_t lim = left < 32u ? (uint32_t)left : 32u;
-#pragma unroll 1
-    for (uint32_t s = 0; s < 32u; s++) {
-        const uint64_t ws = s < 8u ? w0 : s < 16u ? w1 : s < 24u ? w2 : w3;
-        const uint32_t c = (uint32_t)((ws >> (8u * (s & 7u))) & 0xFFu);
-        const bool at = (s >= (neg ? 1u : 0u)) & (ph < 4u);  // this byte belongs to the number's text
-        const bool past = s >= lim;                          // the document ended before this byte
-        const uint32_t dv = c - '0';
-        const bool dig = !past & (dv < 10u);
-        const bool dlm = past | (c == ' ') | (c == '\t') | (c == '\n') | (c == '\r') | (c == ',') | (c == '}') |
-                         (c == ']') | (c == ':') | (c == '"') | (c == '{') | (c == '[');
-        const bool dot = !past & (c == '.'), ee = !past & ((c | 0x20u) == 'e');
-        const bool sgn = !past & ((c == '+') | (c == '-'));
-        const bool mdig = at & dig & (ph <= 1u);  // mantissa digit: counted from the first nonzero one
-        const bool nz = mdig & (dv != 0u);
-        const bool counting = mdig & ((nsig > 0u) | nz);
-        wall = (counting & (nsig < 19u)) ? wall * 10u + dv : wall;
-        too_many = too_many | (nz & (nsig >= 19u));
-        nsig = counting ? nsig + 1u : nsig;
-        wlast = nz ? wall : wlast;
-        nsig_last = nz ? nsig : nsig_last;
-        tz = mdig ? (nz ? 0u : tz + 1u) : tz;
-        const bool idig = at & (ph == 0u) & dig;
-        first = (idig & (n_int == 0u)) ? dv + 1u : first;  // 1 + the first integer digit
-        bad = bad | (idig & (first == 1u) & (n_int > 0u));  // a leading zero followed by a digit
-        n_int = idig ? n_int + 1u : n_int;
-        n_frac = (at & (ph == 1u) & dig) ? n_frac + 1u : n_frac;
-        const bool edig = at & dig & (ph >= 2u);
-        ex = edig ? (ex < 100000u ? ex * 10u + dv : ex) : ex;
-        n_exp = edig ? n_exp + 1u : n_exp;
-        eneg = eneg | (at & (ph == 2u) & (c == '-'));
-        const bool ok = (dig & (ph != 4u)) | ((ph == 0u) & dot & (n_int > 0u)) |
-                        ((ph <= 1u) & ee & ((ph == 0u) ? n_int > 0u : n_frac > 0u)) | ((ph == 2u) & sgn) |
-                        (dlm & (((ph == 0u) & (n_int > 0u)) | ((ph == 1u) & (n_frac > 0u)) |
-                                ((ph == 3u) & (n_exp > 0u))));
-        bad = bad | (at & !ok);
-        uint32_t nph = ph;
-        nph = (at & (ph == 0u) & dot) ? 1u : nph;
-        nph = (at & (ph <= 1u) & ee) ? 2u : nph;
-        nph = (at & (ph == 2u) & (sgn | dig)) ? 3u : nph;
-        nph = (at & dlm) ? 4u : nph;
-        ph = nph;
-    }
-    if (bad | (ph != 4u)) return 1u;  // not the common form, or longer than the window
-    if ((n_frac | n_exp) == 0u) {
-        // an integer (strconv.ParseInt): at most 18 digits cannot overflow; longer ones keep parse_atom_core's rules
-        if (n_int > 18u) return 1u;
-        *tag = GPUDIFF_TAG_INT;
-        const uint64_t v = nsig ? wall : 0ull;
-        *val = neg ? 0ull - v : v;
-        return 0u;
-    }
-    *tag = GPUDIFF_TAG_FLOAT;
-    if (nsig_last == 0u) {
-        *val = 0;  // +-0.0 -> +0.0 (Go ==)
-        return 0u;
-    }
-    if (too_many) return 1u;
-    const int64_t e10 = (eneg ? -(int64_t)ex : (int64_t)ex) - (int64_t)n_frac + (int64_t)tz;
-    uint64_t bits;
-    if (!decimal_to_double(wlast, e10, neg, &bits)) return 1u;
-    *val = bits;
-    return 0u;
+// any atom from the 32-byte register window w at p (ld32u); one that runs past the window is parsed from memory
+__device__ __forceinline__ uint32_t parse_atom_win(const uint8_t* p, const uint8_t* end, uint64_t w0, uint64_t w1,
+                                                   uint64_t w2, uint64_t w3, uint32_t* tag, uint64_t* val) {
+    bool spill = false;
+    const uint32_t e = parse_atom_core(
+        [&](uint64_t j) -> uint32_t {
+            // past the window: 0xFF, neither a digit, a sign, '.', 'e' nor a delimiter -- the parse stops there and
+            // the atom is parsed again from memory (selects, no branch)
+            const bool past = j >= 32u;
+            spill |= past;
+            const uint32_t k = (uint32_t)j & 31u;  // selects by mask, as win16_at
+            const uint64_t m8 = 0ull - (uint64_t)((k >> 3) & 1u), m16 = 0ull - (uint64_t)((k >> 4) & 1u);
+            const uint64_t lo = (w0 & ~m8) | (w1 & m8), hi = (w2 & ~m8) | (w3 & m8);
+            return past ? 0xFFu : (uint32_t)((((lo & ~m16) | (hi & m16)) >> (8u * (k & 7u))) & 0xFFu);
+        },
+        (uint64_t)(end - p), tag, val);
+    return spill ? parse_atom_mem(p, end, tag, val) : e;
 }
 
 // ---- K10 (write path) helpers: Go 1.16 encodeState.string(s, escapeHTML=true)
@@ -881,11 +776,10 @@ __device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* 
             const uint32_t w = (uint32_t)ld8u((const uint8_t*)(uintptr_t)op + k);
             uint8_t* q = (uint8_t*)(uintptr_t)od + k;
             const uint32_t nb = min(4u, on - k);
-            // four stores without a branch: a byte past the span stores byte 0 again (same lane, same value)
             q[0] = (uint8_t)w;
-            q[nb > 1u ? 1u : 0u] = (uint8_t)(nb > 1u ? w >> 8 : w);
-            q[nb > 2u ? 2u : 0u] = (uint8_t)(nb > 2u ? w >> 16 : w);
-            q[nb > 3u ? 3u : 0u] = (uint8_t)(nb > 3u ? w >> 24 : w);
+            if (nb > 1) q[1] = (uint8_t)(w >> 8);
+            if (nb > 2) q[2] = (uint8_t)(w >> 16);
+            if (nb > 3) q[3] = (uint8_t)(w >> 24);
         }
     }
 }

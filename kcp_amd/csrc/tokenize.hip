@@ -663,9 +663,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 ld32u(d + aop, d + len + kTokSlack, w0, w1, w2, w3);
                 uint32_t tag = GPUDIFF_TAG_NULL;
                 uint64_t v = 0;
-                uint32_t e = 0;
-                if (parse_num_w32(w0, w1, w2, w3, len - aop, &tag, &v))
-                    e = parse_atom_mem(d + aop, d + len, &tag, &v);
+                const uint32_t e = parse_atom_win(d + aop, d + len, w0, w1, w2, w3, &tag, &v);
                 if (e) {
                     err = e;
                 } else {
@@ -836,7 +834,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 const uint64_t W0 = isk ? 0x01ull | ((uint64_t)kl << 8) | (c0w << 40) : 0x02ull | ((uint64_t)cx << 8);
                 const uint64_t W1 = isk ? (c0w >> 24) | (c1w << 40) : 0ull, W2 = isk ? (c1w >> 24) | (c2w << 40) : 0ull;
                 const uint64_t W3 = isk ? (c2w >> 24) | (c3w << 40) : 0ull;
-                const uint64_t hh = xxh64_small_wave(ph, isk ? kl + 5u : 5u, W0, W1, W2, W3);
+                const uint64_t hh = xxh64_small(ph, isk ? kl + 5u : 5u, W0, W1, W2, W3);
                 const uint32_t wi = clive ? ci : 0u;
                 S.h[wi] = hh;
                 hl[wi] = hh;
