@@ -186,57 +186,58 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const uint32_t keep = (1u << (8u * nv)) - 1u;
             x = (x & keep) | (0x20202020u & ~keep);
         }
-        uint32_t Qn = 0, Sn = 0, Wn = 0, Cn = 0, Mn = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            const uint32_t c = (x >> (8u * j)) & 0xFFu, cb = c & 0xDFu;
-            // (bitwise | of the compares: a short-circuit || became a branch per term)
-            Qn |= (uint32_t)(c == '"') << j;
-            Sn |= (uint32_t)((cb == '[') | (cb == ']') | (c == ':') | (c == ',')) << j;
-            Wn |= (uint32_t)((c == ' ') | (c == '\n') | (c == '\r') | (c == '\t')) << j;
-            Cn |= (uint32_t)(c < 0x20u) << j;
-            Mn |= (uint32_t)((c == '\\') | (c >= 0x80u)) << j;
-        }
+        // byte classes of the lane's four bytes at once (SWAR): a class is a mask with bit 8j + 7 set for byte j.
+        // nz7(v) has bit 8j + 7 set iff byte j of v is nonzero (no carry crosses a byte); x ^ c for each class byte
+        // c, the classes' nz7 ANDed, the complement's high bits = the bytes equal to one of them (half the VALU and a
+        // third of the scalar work of per-byte compares, whose lane masks the scalar unit combined)
+        constexpr uint32_t K8 = 0x80808080u;
+        auto nz7 = [](uint32_t v) -> uint32_t { return ((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v; };
+        const uint32_t xb = x & 0xDFDFDFDFu;  // '[' ']' and '{' '}' fold together
+        const uint32_t Qn = K8 & ~nz7(x ^ 0x22222222u);
+        const uint32_t Sn = K8 & ~(nz7(xb ^ 0x5B5B5B5Bu) & nz7(xb ^ 0x5D5D5D5Du) & nz7(x ^ 0x3A3A3A3Au) & nz7(x ^ 0x2C2C2C2Cu));
+        const uint32_t Wn = K8 & ~(nz7(x ^ 0x20202020u) & nz7(x ^ 0x0A0A0A0Au) & nz7(x ^ 0x0D0D0D0Du) & nz7(x ^ 0x09090909u));
+        const uint32_t Cn = K8 & ~nz7(x & 0xE0E0E0E0u);                      // < 0x20
+        const uint32_t Mn = (K8 & ~nz7(x ^ 0x5C5C5C5Cu)) | (x & K8);         // '\\' or >= 0x80
         if (esc_carry || ballot(Mn != 0u)) return false;
         const uint64_t odd = ballot(__builtin_popcount(Qn) & 1u);
         const uint32_t P = (str_par + mbcnt64(odd)) & 1u;  // parity of the quotes before this lane
-        uint32_t px = Qn ^ (Qn << 1);
-        px = (px ^ (px << 2)) & 0xFu;                      // inclusive prefix parity within the lane
-        const uint32_t In = px ^ (P ? 0xFu : 0u);          // in a string (opening quote in, closing out)
+        uint32_t px = Qn ^ (Qn << 8);
+        px = px ^ (px << 16);                               // inclusive prefix parity within the lane
+        const uint32_t In = px ^ (P ? K8 : 0u);             // in a string (opening quote in, closing out)
         str_par = (str_par + popc64(odd)) & 1u;
-        const uint32_t opens = Qn & In, closes = Qn & ~In & 0xFu;
-        const uint32_t atom = ~In & ~Qn & ~Sn & ~Wn & 0xFu;
-        const uint32_t prev = wave_shr1((atom >> 3) & 1u, (uint32_t)atom_carry);  // byte 3 of the lane below
-        const uint32_t astart = atom & ~(((atom << 1) | prev) & 0xFu);
-        atom_carry = rdlane((atom >> 3) & 1u, 63);
+        const uint32_t opens = Qn & In, closes = Qn & ~In;
+        const uint32_t atom = K8 & ~In & ~Qn & ~Sn & ~Wn;
+        const uint32_t prev = wave_shr1(atom >> 31, (uint32_t)atom_carry);  // byte 3 of the lane below
+        const uint32_t astart = atom & ~((atom << 8) | (prev << 7));
+        atom_carry = rdlane(atom >> 31, 63);
         if (ballot((Cn & In & ~opens) != 0u)) ctl_in_string = true;
         const uint32_t Tn = (Sn & ~In) | Qn | astart;
         const uint32_t tc = __builtin_popcount(Tn);
         const uint64_t c0 = ballot(tc & 1u), c1 = ballot(tc & 2u), c2 = ballot(tc & 4u);
         const uint32_t pre = mbcnt64(c0) + 2u * mbcnt64(c1) + 4u * mbcnt64(c2);
-        const uint32_t j1 = opens ? (uint32_t)__builtin_ctz(opens) : 4u;  // most lanes hold at most one opening
+        const uint32_t j1 = opens ? (uint32_t)__builtin_ctz(opens) >> 3 : 4u;  // most lanes hold at most one opening
         // (every lane reads its keyword window -- LDS reads and compares, no branch; the result is used only at an
         // opening quote)
         const uint32_t kw1 = keyword(p4 + j1);
         const uint32_t op2 = opens & (opens - 1u);
         uint32_t kw2 = 0u;
-        if (ballot(op2 != 0u)) kw2 = keyword(p4 + (op2 ? (uint32_t)__builtin_ctz(op2) : 0u));  // uniform test
+        if (ballot(op2 != 0u)) kw2 = keyword(p4 + (op2 ? (uint32_t)__builtin_ctz(op2) >> 3 : 0u));  // uniform test
         // every lane stores four words: a byte that starts no token writes slot len + 1, which no token uses (a
         // document of len bytes has at most len tokens, tok_cap = len + 2) -- stores without a branch each
         uint32_t k = ntok + pre;
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {
-            const bool tj = (Tn >> j) & 1u;
-            const uint32_t code = ((closes >> j) & 1u) ? TK_CLOSEQ
-                                  : ((opens >> j) & 1u) ? (j == j1 ? kw1 : kw2) : (x >> (8u * j)) & 0xFFu;
+            const bool tj = (Tn >> (8u * j + 7u)) & 1u;
+            const uint32_t code = ((closes >> (8u * j + 7u)) & 1u) ? TK_CLOSEQ
+                                  : ((opens >> (8u * j + 7u)) & 1u) ? (j == j1 ? kw1 : kw2) : (x >> (8u * j)) & 0xFFu;
             S.tok[tj ? k : len + 1u] = (code << 24) | (p4 + j);
             k += tj ? 1u : 0u;
         }
         const uint64_t om = ballot(opens != 0u);
         if (om) {  // the last opening quote of the block (a later step may mark its string slow)
             const uint32_t L = 63u - (uint32_t)__builtin_clzll(om);
-            const uint32_t jl = opens ? 31u - (uint32_t)__builtin_clz(opens) : 0u;
-            last_open_idx = rdlane(ntok + pre + __builtin_popcount(Tn & ((1u << jl) - 1u)), L);
+            const uint32_t jl = opens ? (31u - (uint32_t)__builtin_clz(opens)) >> 3 : 0u;
+            last_open_idx = rdlane(ntok + pre + __builtin_popcount(Tn & ((1u << (8u * jl)) - 1u)), L);
             last_open_pos = b + 4u * L + rdlane(jl, L);
         }
         ntok += popc64(c0) + 2u * popc64(c1) + 4u * popc64(c2);
@@ -1115,6 +1116,27 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             o.n_tab = Nt;
         }
     }
+#if defined(K0_PROBE_VALU) || defined(K0_PROBE_SALU)
+    // timing-only builds (tools/sessions: the marginal cost of a vector / scalar instruction per document): 1024
+    // extra instructions of one kind per document, 8 per iteration of a scalar loop
+    {
+        uint32_t pa = lane ^ status, pb = nn;
+        uint32_t sa = __builtin_amdgcn_readfirstlane(pa), sb = __builtin_amdgcn_readfirstlane(pb);
+        (void)sb;
+        for (uint32_t q = 0; q < 128u + (nn >> 30); q++) {
+#if defined(K0_PROBE_VALU)
+            __asm__ volatile("v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n"
+                             "v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1"
+                             : "+v"(pa) : "v"(pb));
+#else
+            __asm__ volatile("s_mov_b32 %0, %1\n s_mov_b32 %0, %1\n s_mov_b32 %0, %1\n s_mov_b32 %0, %1\n"
+                             "s_mov_b32 %0, %1\n s_mov_b32 %0, %1\n s_mov_b32 %0, %1\n s_mov_b32 %0, %1"
+                             : "+s"(sa) : "s"(sb));
+#endif
+        }
+        if ((pa ^ sa) == 0x9E3779B9u) o.n_nodes ^= 0x80000000u;  // never taken in practice: keeps the chains live
+    }
+#endif
     o.status = status;
     if (lane == 0) out[doc_i] = o;
     mark(5);
