@@ -61,26 +61,29 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, uint32_t src) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        uint32_t o = shfl32(v, lane >= d ? lane - d : lane);
-        if (lane >= d) v += o;
-    }
-    return v;
+// inclusive wave scans in six DPP steps (row_shr 1, 2, 4, 8 within each 16-lane row, then row_bcast 15 / 31 carry
+// rows 0 and 0-1 into the rows after them): register-to-register, where the ds_bpermute form paid six LDS round
+// trips and their waits. A lane whose DPP source does not exist, or whose row the row mask leaves out, keeps `id`
+template <class Op>
+__device__ __forceinline__ uint32_t dpp_incl_scan(uint32_t x, uint32_t id, Op op) {
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x111, 0xF, 0xF, false));  // row_shr:1
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x112, 0xF, 0xF, false));  // row_shr:2
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x114, 0xF, 0xF, false));  // row_shr:4
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x118, 0xF, 0xF, false));  // row_shr:8
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return x;
 }
-// wave reductions: every lane ends with the total, so the result is returned through readfirstlane -- a scalar the
-// compiler knows to be uniform (loop bounds and branches on it stay scalar instead of becoming exec-mask loops)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    return dpp_incl_scan(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+// wave reductions: the scan's last lane, read into a scalar the compiler knows to be uniform (loop bounds and
+// branches on it stay scalar instead of becoming exec-mask loops). Every lane must be active
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, (int)d);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    return rdlane(wave_incl_scan(v), 63);
 }
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, (int)d));
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    return rdlane(dpp_incl_scan(v, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; }), 63);
 }
 // the same reductions left in vector registers (K10 / K11 / K13's phases: their register allocation was tuned so)
 __device__ __forceinline__ uint32_t wave_sum_v(uint32_t v) {
@@ -1020,9 +1023,7 @@ __device__ __forceinline__ uint32_t wave_min_v(uint32_t v) {
     return v;
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (uint32_t d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)d));
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    return rdlane(dpp_incl_scan(v, ~0u, [](uint32_t a, uint32_t b) { return a < b ? a : b; }), 63);
 }
 constexpr uint32_t MF_HIDDEN = 1u, MF_CUSTOM = 2u, MF_HASVIS = 4u, MF_VIS = 8u, MF_FLOAT = 16u;
 constexpr uint32_t MF_VCLEAN = 32u, MF_KCLEAN = 64u;  // string value / key written as its own bytes

@@ -399,11 +399,16 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const int32_t lmax = (int32_t)wave_max(live ? (uint32_t)(lvl + 0x40000000) : 0u) - 0x40000000;
             // levels of enclosing containers (lmin - 1 ..) and of this batch's opens (.. lmax)
             const int32_t lo = max(lmin - 1, 0), hi = min(lmax, (int32_t)kMaxDepth - 1);
+            const uint64_t m_live = ballot(live);
             for (int32_t L = lo; L <= hi; L++) {
                 const bool at_l = is_o && lvl == L;
                 const bool at1 = live && lvl == L + 1;
-                const uint64_t m_ol = ballot(at_l), m_ch = ballot(at1 && is_node);
-                if (!m_ol && !ballot(at1)) continue;
+                // the level masks as compare masks ANDed on the scalar unit (a ballot of a combined predicate
+                // re-materialised it in a VGPR and compared it again: two vector instructions a ballot)
+                const uint64_t eq0 = __builtin_amdgcn_uicmp((uint32_t)lvl, (uint32_t)L, 32);       // ICMP_EQ
+                const uint64_t eq1 = __builtin_amdgcn_uicmp((uint32_t)lvl, (uint32_t)(L + 1), 32);
+                const uint64_t m_ol = m_o & eq0, m_ch = m_node & eq1;
+                if (!m_ol && !(m_live & eq1)) continue;
                 LvlEnt st = lvt[L];
                 const uint32_t nb = st.cnt1 + mbcnt64(m_ch);  // level-(L+1) nodes before this token
                 if (at_l) my_base = nb;
