@@ -478,43 +478,51 @@ __device__ __forceinline__ uint32_t win16_at(uint64_t w0, uint64_t w1, uint32_t 
     const uint64_t m = 0ull - (uint64_t)((k >> 3) & 1u);
     return (uint32_t)((((w0 & ~m) | (w1 & m)) >> (8u * (k & 7u))) & 0xFFu);
 }
-// K0's sort of up to kRank node keys: keys[j] & mask (j < ns) are node j + 1's key, in LDS (phase 3b's hashes; the
-// mask keeps at most GPUDIFF_PATH_HASH_BITS = 32 bits, so keys compare as 32-bit words). Lane k ranks keys k, k + 64,
-// ... by counting the keys below each -- all ns read two at a time by broadcast -- and writes its nodes' ids to their
-// ranks in ids. Distinct keys rank to a permutation; an equal pair (a duplicate or a collision under the seed) ranks
-// twice to one slot, so a lane that reads back another node's id there -- or holds the root's hash -- sets
-// GPUDIFF_TOK_HASH, as the bitonic path's check does
+// K0's sort of up to kRank node keys: keys[j] & mask (j < ns) are node j + 1's key, in LDS (phase 3b's hashes).
+// Lane k ranks keys k, k + 64, ... by counting the keys below each -- all ns read two at a time by broadcast -- and
+// writes its nodes' ids to their ranks in ids. Ranks are a permutation when the keys are distinct; an equal pair (a
+// duplicate or a collision under the seed) or a key equal to the root's hash sets GPUDIFF_TOK_HASH instead, as the
+// bitonic path's check does
 template <int NK>
 __device__ __forceinline__ void rank_sort_n(const uint64_t* keys, uint64_t mask, uint16_t* ids, uint32_t ns,
                                             uint32_t lane, uint64_t root, uint32_t& status) {
-    const uint32_t* const k32 = (const uint32_t*)keys;  // little-endian: word 2j is key j's low half
-    const uint32_t m = (uint32_t)mask;
-    uint32_t k[NK], r[NK];
+    uint64_t k[NK];
+    uint32_t r[NK], e[NK];
 #pragma unroll
     for (int q = 0; q < NK; q++) {
-        k[q] = lane + 64u * q < ns ? k32[2u * (lane + 64u * q)] & m : 0u;
+        k[q] = lane + 64u * q < ns ? keys[lane + 64u * q] & mask : 0ull;
         r[q] = 0u;
+        e[q] = 0u;
     }
     const uint32_t np = ns & ~1u;
     for (uint32_t j = 0; j < np; j += 2) {
-        const uint32_t a = k32[2u * j] & m, b = k32[2u * j + 2u] & m;
+        const uint64_t a = keys[j] & mask, b = keys[j + 1] & mask;
 #pragma unroll
-        for (int q = 0; q < NK; q++) r[q] += (uint32_t)(a < k[q]) + (uint32_t)(b < k[q]);
+        for (int q = 0; q < NK; q++) {
+            r[q] += (uint32_t)(a < k[q]) + (uint32_t)(b < k[q]);
+            e[q] += (uint32_t)(a == k[q]) + (uint32_t)(b == k[q]);
+        }
     }
     if (np < ns) {
-        const uint32_t a = k32[2u * np] & m;
+        const uint64_t a = keys[np] & mask;
 #pragma unroll
-        for (int q = 0; q < NK; q++) r[q] += (uint32_t)(a < k[q]);
+        for (int q = 0; q < NK; q++) {
+            r[q] += (uint32_t)(a < k[q]);
+            e[q] += (uint32_t)(a == k[q]);
+        }
+    }
+    bool dup = false;
+#pragma unroll
+    for (int q = 0; q < NK; q++)
+        if (lane + 64u * q < ns && (e[q] > 1u || k[q] == root)) dup = true;
+    if (__builtin_amdgcn_ballot_w64(dup)) {
+        status = GPUDIFF_TOK_HASH;
+        return;
     }
 #pragma unroll
     for (int q = 0; q < NK; q++)
         if (lane + 64u * q < ns) ids[r[q]] = (uint16_t)(lane + 64u * q + 1u);
-    __asm__ volatile("" ::: "memory");  // (a wave's LDS accesses complete in order: the reads see every write)
-    bool dup = false;
-#pragma unroll
-    for (int q = 0; q < NK; q++)
-        if (lane + 64u * q < ns && (ids[r[q]] != (uint16_t)(lane + 64u * q + 1u) || k[q] == (uint32_t)root)) dup = true;
-    if (__builtin_amdgcn_ballot_w64(dup)) status = GPUDIFF_TOK_HASH;
+    __asm__ volatile("" ::: "memory");
 }
 __device__ __forceinline__ void rank_sort(const uint64_t* keys, uint64_t mask, uint16_t* ids, uint32_t ns,
                                           uint32_t lane, uint64_t root, uint32_t& status) {

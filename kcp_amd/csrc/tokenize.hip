@@ -841,8 +841,10 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 const uint64_t W1 = isk ? (c0w >> 24) | (c1w << 40) : 0ull, W2 = isk ? (c1w >> 24) | (c2w << 40) : 0ull;
                 const uint64_t W3 = isk ? (c2w >> 24) | (c3w << 40) : 0ull;
                 const uint64_t hh = xxh64_small(ph, isk ? kl + 5u : 5u, W0, W1, W2, W3);
+                // (LDS only: a small document's later phases read its hashes from hl -- phase 4 ranks them there,
+                // phase 5's tiny path reads them there -- so they are not stored to the scratch's hash area too)
+                static_assert(kRank + 1u >= kLdsHash, "a small document's phases 4-5 take the LDS (tiny) paths");
                 const uint32_t wi = clive ? ci : 0u;
-                S.h[wi] = hh;
                 hl[wi] = hh;
             }
             lds_order();  // the next level reads these hashes
