@@ -394,7 +394,9 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             const bool empty = is_o && cn1 == (code == '{' ? (uint32_t)'}' : (uint32_t)']');
             // per-lane results of the level loop
             uint32_t e_id = NONE, e_info = 0u, my_info = code == '[' ? LF_ARR : 0u, my_base = 0u, comp = 0u, reg = R_NONE;
-            bool bad_lab = false, bad_ann = false;
+            // (flags carried across the level loop as 0/1 words: a loop-carried bool became a lane mask merged with
+            // exec by three scalar instructions an iteration)
+            uint32_t bad_lab = 0u, bad_ann = 0u;
             const int32_t lmin = (int32_t)wave_min_u32(live ? (uint32_t)(lvl + 0x40000000) : 0x7FFFFFFFu) - 0x40000000;
             const int32_t lmax = (int32_t)wave_max(live ? (uint32_t)(lvl + 0x40000000) : 0u) - 0x40000000;
             // levels of enclosing containers (lmin - 1 ..) and of this batch's opens (.. lmax)
@@ -446,8 +448,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                     }
                     comp = nd ? comp_n : comp;
                     reg = nd ? reg_n : reg;
-                    bad_lab = nd ? bl : bad_lab;
-                    bad_ann = nd ? ba : bad_ann;
+                    bad_lab = nd ? (uint32_t)bl : bad_lab;
+                    bad_ann = nd ? (uint32_t)ba : bad_ann;
                     my_info = nd ? ((code == '[' ? LF_ARR : 0u) | (reg_n << 1) | fl) : my_info;
                 }
                 // the table entry for level L
@@ -516,8 +518,8 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             if (m_lab) labels_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_lab));
             if (m_ann) annot_node = rdlane(id, 63u - (uint32_t)__builtin_clzll(m_ann));
             if (ballot(is_node & (lvl == 1) & (cp3 == TK_KEY_STATUS)) & upto) has_status = true;
-            if (ballot(bad_lab) & upto) labels_ok = false;
-            if (ballot(bad_ann) & upto) annot_ok = false;
+            if (ballot(bad_lab != 0u) & upto) labels_ok = false;
+            if (ballot(bad_ann != 0u) & upto) annot_ok = false;
             nn += popc64(ok_node);
             if (m_err) {
                 status = rdlane(err, (uint32_t)__builtin_ctzll(m_err));
@@ -809,11 +811,11 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
         };
         uint32_t ci = 0, cy = 0, cx = 0;
         uint64_t c0w = 0, c1w = 0, c2w = 0, c3w = 0;
-        bool clive = false;
+        uint32_t clive = 0u;  // (0/1, not a loop-carried bool: see the tree phase)
         auto load_step = [&](uint32_t d_, uint32_t j_, uint32_t b_, uint32_t& i_, uint32_t& y_, uint32_t& x_,
-                             uint64_t& w0_, uint64_t& w1_, uint64_t& w2_, uint64_t& w3_, bool& live_) {
+                             uint64_t& w0_, uint64_t& w1_, uint64_t& w2_, uint64_t& w3_, uint32_t& live_) {
             // every lane loads (a lane past the step reads entry 0 and the document's first bytes): no branch
-            live_ = (d_ <= max_depth) && (j_ + lane < rdlane(cnt, min(d_, 31u)));
+            live_ = ((d_ <= max_depth) & (j_ + lane < rdlane(cnt, min(d_, 31u)))) ? 1u : 0u;
             i_ = ord16[live_ ? b_ + j_ + lane : 0u];
             const uint2 in = hin[i_];
             y_ = live_ ? in.y : 0u;
@@ -826,7 +828,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
             next_step(nd, nj, nb);
             uint32_t ni, ny, nx;
             uint64_t n0w, n1w, n2w, n3w;
-            bool nlive;
+            uint32_t nlive;
             load_step(nd, nj, nb, ni, ny, nx, n0w, n1w, n2w, n3w, nlive);
             {
                 // every lane hashes; a lane past the step writes slot 0 (the root's, read by nothing after this)
