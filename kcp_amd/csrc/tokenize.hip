@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 }
                 st.cnt1 += popc64(m_ch);
                 if (m_ch) max_depth = max(max_depth, (uint32_t)L + 1u);
-                if (lane == 0) lvt[L] = st;
+                lvt[L] = st;  // every lane: the same 16 bytes to one address (no exec-mask branch)
                 lds_order();
             }
             // grammar: each token against its predecessor (cp1; 0 before the first token)
