@@ -416,10 +416,7 @@ __global__ __launch_bounds__(256, MINW) void k_encode_docs(const TokDoc* __restr
                 if (at_l) my_base = nb;
                 const uint64_t below = m_ol & mask_lt(lane);
                 const uint32_t e = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
-                // (info < 128 and base < 2^24 -- node ids stay under node_cap = len / 2 + 2, len <= 2^24 -- share one
-                // cross-lane read)
-                const uint32_t x_id = shfl32(id, e), x_ib = shfl32(my_info | (my_base << 7), e);
-                const uint32_t x_info = x_ib & 0x7Fu, x_base = x_ib >> 7;
+                const uint32_t x_id = shfl32(id, e), x_info = shfl32(my_info, e), x_base = shfl32(my_base, e);
                 // the parent of this level's tokens (selects; the depth tests are uniform: L is a scalar)
                 const uint32_t p_id = below ? x_id : st.id, p_info = below ? x_info : st.info;
                 const uint32_t p_base = below ? x_base : st.base;
