@@ -622,7 +622,7 @@ def main():
                                     "time -- a format-independent work rate (24-B records), not a fraction of peak"},
                          "diff_pass": {"ms": pass_ms, "achieved": achieved_pass, "frac": achieved_pass / HBM_PEAK_GBPS,
                                        "def": "format bytes over the whole diff pass (K2..K6)"},
-                         "k2_source_hash": src_hash,
+                         "k2_source_hash": src_hash, "build_id": G.BUILD_ID,
                          # the physical rate: HBM counter bytes (FETCH_SIZE x 2 + WRITE_SIZE per K2 launch) over
                          # this run's K2 time -- what the memory system moved, whatever the byte definition
                          # (with no PMC summary of these K2 sources and this workload, the bytes K2's format
@@ -646,6 +646,9 @@ def main():
                        "gather": gather_check},
             "ingest_s": t_gen,
             "box": box_id(),
+            # the loaded library's content hash of its sources (gpudiff_build_id; the loader refused it unless
+            # it equals the shipped sources' hash, kcp_amd/buildinfo.py)
+            "build_id": G.BUILD_ID, "build_verified": G.BUILD_VERIFIED,
         }
         print(json.dumps(line), flush=True)
     if collective:

@@ -167,4 +167,6 @@ def run(args):
     }
     nb.close()
     eng.close()
+    from kcp_amd import gpudiff as _G
+    line["build_id"] = _G.BUILD_ID  # the loaded library's source hash (kcp_amd/buildinfo.py)
     print(json.dumps(line), flush=True)

@@ -271,6 +271,8 @@ def run(args):
                    "sample_bit_exact_vs_oracle": sample_ok},
         "cpu_baseline": cpu,
     }
+    from kcp_amd import gpudiff as _G
+    line["build_id"] = _G.BUILD_ID  # the loaded library's source hash (kcp_amd/buildinfo.py)
     print(json.dumps(line), flush=True)
     st.free()
     eng.close()

@@ -132,4 +132,6 @@ def run(args):
     }
     rb.close()
     eng.close()
+    from kcp_amd import gpudiff as _G
+    line["build_id"] = _G.BUILD_ID  # the loaded library's source hash (kcp_amd/buildinfo.py)
     print(json.dumps(line), flush=True)

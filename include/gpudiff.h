@@ -190,6 +190,10 @@ typedef struct gpudiff_timings {
 /* ---- library ---- */
 const char* gpudiff_strerror(int err);
 int gpudiff_abi_version(void);
+/* 16 hex digits: SHA-256 over the contents of every source, header, map and build script the library was
+ * compiled from (kcp_amd/buildinfo.py).  A binding that ships the sources recomputes it and refuses a
+ * library built from anything else; the bench line carries it as `build_id`. */
+const char* gpudiff_build_id(void);
 int gpudiff_device_count(int* n);
 
 /* ---- context ---- */

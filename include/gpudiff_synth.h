@@ -42,6 +42,8 @@ typedef struct gpudiff_synth_cfg {
 typedef struct gpudiff_synth gpudiff_synth;
 
 /* plans the population and the LPT shard of `rank` among `world` ranks (clusters by pair count) */
+/* the build ID of this library (the same content hash as gpudiff_build_id, kcp_amd/buildinfo.py) */
+const char* gpudiff_synth_build_id(void);
 int gpudiff_synth_open(const gpudiff_synth_cfg* cfg, int world, int rank, gpudiff_synth** out);
 /* the same with the clusters LPT-packed by cluster_weight[n_clusters] (NULL = pair count), the rule of
  * gpudiff_shard_lpt: SURVEY.md §8(e) balances ranks by Σ B_pair (gpudiff_synth_cluster_bytes) */

@@ -14,6 +14,8 @@ from typing import Any, Iterable, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
+from . import buildinfo
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpudiff.so")
 
@@ -244,6 +246,7 @@ _P = C.c_void_p
 SIGNATURES = [
     ("gpudiff_strerror", C.c_char_p, [C.c_int]),
     ("gpudiff_abi_version", C.c_int, []),
+    ("gpudiff_build_id", C.c_char_p, []),
     ("gpudiff_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("gpudiff_open", C.c_int, [C.POINTER(Opts), C.POINTER(_P)]),
     ("gpudiff_close", None, [_P]),
@@ -359,9 +362,21 @@ def _load() -> C.CDLL:
     if got != ABI_VERSION:
         raise ImportError("%s has ABI %d, this binding needs %d (rebuild with kcp_amd/build.py)"
                           % (LIB_PATH, got, ABI_VERSION))
+    # ...and a library built from other sources than the ones shipped beside it is refused too: the ID is a
+    # content hash of every source, header and build flag (kcp_amd/buildinfo.py), never an mtime
+    global BUILD_ID, BUILD_VERIFIED
+    BUILD_ID = lib.gpudiff_build_id().decode()
+    if buildinfo.sources_present():
+        want = buildinfo.source_id()
+        if BUILD_ID != want:
+            raise ImportError("%s was built from other sources (build ID %s, the shipped sources hash to %s): "
+                              "rebuild with kcp_amd/build.py" % (LIB_PATH, BUILD_ID, want))
+        BUILD_VERIFIED = True
     return lib
 
 
+BUILD_ID = ""          # gpudiff_build_id() of the loaded library
+BUILD_VERIFIED = False  # True when it equals the shipped sources' content hash
 _lib = _load()
 
 

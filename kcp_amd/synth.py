@@ -27,6 +27,7 @@ _P = C.c_void_p
 _SIGS = [
     ("gpudiff_synth_open", C.c_int, [C.POINTER(SynthCfg), C.c_int, C.c_int, C.POINTER(_P)]),
     ("gpudiff_synth_open_ex", C.c_int, [C.POINTER(SynthCfg), C.c_int, C.c_int, C.c_void_p, C.POINTER(_P)]),
+    ("gpudiff_synth_build_id", C.c_char_p, []),
     ("gpudiff_synth_cluster_sizes", C.c_int, [C.POINTER(SynthCfg), C.c_void_p]),
     ("gpudiff_synth_cluster_bytes", C.c_int, [C.POINTER(SynthCfg), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
     ("gpudiff_synth_local_ids", C.c_int, [_P, C.c_void_p]),
@@ -50,6 +51,12 @@ _lib = C.CDLL(SYNTH_PATH)
 for _n, _r, _a in _SIGS:
     getattr(_lib, _n).restype = _r
     getattr(_lib, _n).argtypes = _a
+# the generator must come from the same sources as the engine it feeds (kcp_amd/buildinfo.py)
+from .gpudiff import BUILD_ID as _ENGINE_BUILD_ID  # noqa: E402
+
+if _lib.gpudiff_synth_build_id().decode() != _ENGINE_BUILD_ID:
+    raise ImportError("%s has build ID %s, libgpudiff.so %s: rebuild with kcp_amd/build.py"
+                      % (SYNTH_PATH, _lib.gpudiff_synth_build_id().decode(), _ENGINE_BUILD_ID))
 
 # SURVEY.md §8(d) populations
 CONFIGS = {

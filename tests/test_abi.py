@@ -91,3 +91,56 @@ def test_open_rejects_removed_tuning_bits():
         assert ei.value.code == G.E_INVAL, hex(bad)
     for ok in (0, G.OPT_TIMING, G.OPT_K2_TIMELINE, 12 << G.OPT_ARENA_SHIFT, G.OPT_DEVICE_ENCODE):
         G.Engine(device=G.DEVICE_NONE, flags=ok).close()
+
+
+def test_build_id_equals_shipped_sources():
+    """The loaded library's gpudiff_build_id() is the content hash of the sources beside it (VERDICT r5 #3)."""
+    from kcp_amd import buildinfo, gpudiff as G
+    from kcp_amd import synth as S
+    assert G.BUILD_VERIFIED
+    assert G.BUILD_ID == buildinfo.source_id() == G.lib().gpudiff_build_id().decode()
+    assert S._lib.gpudiff_synth_build_id().decode() == G.BUILD_ID
+    assert len(G.BUILD_ID) == 16 and int(G.BUILD_ID, 16) >= 0
+
+
+def _copy_tree(dst):
+    import shutil
+    for d in ("kcp_amd", "include"):
+        shutil.copytree(os.path.join(ROOT, d), os.path.join(dst, d),
+                        ignore=shutil.ignore_patterns("_build", "__pycache__"))
+
+
+def _import_in(tree):
+    import subprocess
+    import sys
+    return subprocess.run([sys.executable, "-c", "import kcp_amd.gpudiff as G; print(G.BUILD_ID, G.BUILD_VERIFIED)"],
+                          cwd=tree, capture_output=True, text=True, timeout=120)
+
+
+def test_stale_library_is_refused(tmp_path):
+    """A library pushed beside sources it was not built from is refused at import, whatever the mtimes say:
+    a copy of the tree with one header's content changed (and its mtime set back before the library's)
+    no longer loads; the untouched copy does."""
+    _copy_tree(str(tmp_path))
+    ok = _import_in(str(tmp_path))
+    assert ok.returncode == 0, ok.stderr
+    assert ok.stdout.split() == [__import__("kcp_amd").gpudiff.BUILD_ID, "True"]
+    hdr = tmp_path / "kcp_amd" / "csrc" / "engine.h"
+    hdr.write_text(hdr.read_text() + "\n// an edit the library was not built from\n")
+    lib_m = os.path.getmtime(tmp_path / "kcp_amd" / "libgpudiff.so")
+    os.utime(hdr, (lib_m - 3600, lib_m - 3600))
+    bad = _import_in(str(tmp_path))
+    assert bad.returncode != 0
+    assert "built from other sources" in bad.stderr
+
+
+def test_build_id_hashes_contents_not_mtimes(tmp_path):
+    from kcp_amd import buildinfo
+    _copy_tree(str(tmp_path))
+    a = buildinfo.source_id(str(tmp_path))
+    for rel, _ in buildinfo.input_files():
+        os.utime(tmp_path / rel, (1, 1))
+    assert buildinfo.source_id(str(tmp_path)) == a == buildinfo.source_id()
+    f = tmp_path / "include" / "gpudiff_format.h"
+    f.write_bytes(f.read_bytes() + b" ")
+    assert buildinfo.source_id(str(tmp_path)) != a

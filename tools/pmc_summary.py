@@ -61,6 +61,7 @@ def main():
         workload=bench["config"]["workload"],
         kernel=kname,
         k2_source_hash=rl.get("k2_source_hash"),
+        build_id=bench.get("build_id", rl.get("build_id")),
         algorithmic_bytes_per_launch=alg,
         survey_bytes_per_launch=rl.get("bytes_per_launch") if "format" in rl else None,
         hbm_bytes_per_launch=k2.get("hbm_bytes"),
