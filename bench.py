@@ -151,6 +151,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0,
                     help="config5: sustained replay time (SURVEY.md 8(d): >= 10 s); 0 = --batches batches")
     ap.add_argument("--warmup-batches", type=int, default=4, help="config5: untimed batches")
+    ap.add_argument("--zero-copy", action="store_true",
+                    help="config5: every timed batch's new objects sit in one engine-pinned buffer in the upload "
+                         "layout (the watch reader writes each event's JSON there): no staging copy")
     ap.add_argument("--encode", default="device", choices=["device", "host"],
                     help="config5: encode events on the GPU (K0, raw JSON up) or on the host")
     ap.add_argument("--pairs", type=int, default=0, help="override population size (default: the config's)")

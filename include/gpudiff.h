@@ -39,7 +39,8 @@
 extern "C" {
 #endif
 
-#define GPUDIFF_ABI_VERSION 5  /* 5: the tuning option bits removed (GPUDIFF_OPT_KNOWN); result slots own their counts */
+#define GPUDIFF_ABI_VERSION 6  /* 6: bit 0x100 (the K2 timeline build) retired: gpudiff_k2_profile selects that build;
+                                   5: the tuning option bits removed (GPUDIFF_OPT_KNOWN); result slots own their counts */
 
 enum {
     GPUDIFF_OK = 0,
@@ -97,16 +98,15 @@ enum {
 /* context option flags (any other bit: gpudiff_open returns GPUDIFF_E_INVAL).  Round 5 removed the A/B tuning
  * bits of earlier rounds whose measurements rejected them (DESIGN.md §5-§6 keep the numbers):
  * 0x2 two upload streams, 0x4 index-order final round, 0x8 pipelined K4 join, 0x10-0x80 tail shapes, bits 9-20
- * kernel variants / blocks per CU / segmented passes, bits 26-31 K0 occupancy, items per wave, deep-join bounds. */
+ * kernel variants / blocks per CU / segmented passes, bits 26-31 K0 occupancy, items per wave, deep-join bounds.
+ * ABI 6 retired 0x100 (ABI 5's K2 timeline bit, ABI 4's K2 variant bit): refused like the rest, so no caller of
+ * either meaning gets the other; the timeline build is selected by gpudiff_k2_profile. */
 #define GPUDIFF_OPT_TIMING 0x1u          /* record per-kernel HIP event times (gpudiff_last_timings) */
-#define GPUDIFF_OPT_K2_TIMELINE 0x100u   /* profiling hook: the decision kernel's per-wave timeline build
-                                            (gpudiff_k2_profile buffer; tools/k2_wave_profile.py) */
 #define GPUDIFF_OPT_ARENA_SHIFT 21u      /* 4 bits, test hook: shrink the per-wave path arena 2^k-fold (forces
                                             pairs through the deferred K4 path) */
 #define GPUDIFF_OPT_DEVICE_ENCODE 0x2000000u /* gpudiff_submit / single-pair helpers: raw JSON up, kernel K0
                                                 encodes (as GPUDIFF_STORE_DEVICE_ENCODE does for the store) */
-#define GPUDIFF_OPT_KNOWN (GPUDIFF_OPT_TIMING | GPUDIFF_OPT_K2_TIMELINE | (0xFu << GPUDIFF_OPT_ARENA_SHIFT) | \
-                           GPUDIFF_OPT_DEVICE_ENCODE)
+#define GPUDIFF_OPT_KNOWN (GPUDIFF_OPT_TIMING | (0xFu << GPUDIFF_OPT_ARENA_SHIFT) | GPUDIFF_OPT_DEVICE_ENCODE)
 
 #define GPUDIFF_DEVICE_CURRENT (-1)
 #define GPUDIFF_DEVICE_NONE (-2)   /* host-only context: encoding only */
@@ -159,7 +159,9 @@ typedef struct gpudiff_result {
     void* internal_;
 } gpudiff_result;
 
-/* device-side view of a diffed batch (for RCCL gathers; pointers are HBM) */
+/* device-side view of a diffed batch (for RCCL gathers; pointers are HBM).  The pointers belong to the batch's
+ * current result slot: after gpudiff_dbatch_result_slot switches slots, fetch the view again (counts included --
+ * a slot owns its counts since ABI 5). */
 typedef struct gpudiff_device_view {
     const uint8_t* pair_flags;
     const uint32_t* spec_dirty_ids;
@@ -345,7 +347,8 @@ typedef struct gpudiff_store_stats {
      * enqueue of copies and kernels; and the store's part of gpudiff_wait */
     float submit_wait_ms, submit_docs_ms, submit_copy_ms, submit_enqueue_ms, finish_ms;
     uint32_t timing_batches; /* batches the means are over */
-    uint32_t zero_copy_batches; /* gpudiff_submit batches uploaded straight from a gpudiff_host_alloc buffer */
+    uint32_t zero_copy_batches; /* batches uploaded straight from a gpudiff_host_alloc buffer (gpudiff_submit's
+                                    device-encode pairs, or this store's device-encode events) */
     uint64_t space_conservative; /* device-encode: deferred events reported dirty (GPUDIFF_DECODE_ERROR, slot
                                     emptied) because the space could not take their re-encoded blobs */
 } gpudiff_store_stats;
@@ -380,9 +383,14 @@ void gpudiff_store_free(gpudiff_ctx* ctx, gpudiff_store* st);
  * buffer, in pair order (old_0, new_0, old_1, new_1, ...), each at a 16-B aligned address and followed by at
  * least its staged span -- len + 32 bytes rounded up to 16 -- before the next document (the last one's span and
  * 32 more bytes inside the buffer) is uploaded straight from it: no staging copy.  The engine zeroes each
- * document's padding up to that span (those bytes are its to write).  Any other layout takes the staging copy;
- * results are identical either way (gpudiff_store_stats.zero_copy_batches counts the zero-copy ones).  The
- * buffer must stay untouched until gpudiff_wait on the ticket returns; gpudiff_close frees what is left. */
+ * document's padding up to that span (those bytes are its to write).  The same holds for gpudiff_store_submit on
+ * a GPUDIFF_STORE_DEVICE_ENCODE store (the watch stream's events rendered straight into engine-pinned memory):
+ * the documents the store encodes -- per event, in submit order, its old object when the slot is seen for the
+ * first time, then its new object -- lie in ONE such buffer in that order, 16-B aligned, each followed by its
+ * staged span before the next (gaps allowed; old objects the store does not encode may lie anywhere).  Any
+ * other layout takes the staging copy; results are identical either way
+ * (gpudiff_store_stats.zero_copy_batches counts the zero-copy ones).  The buffer must stay untouched until
+ * gpudiff_wait on the ticket returns; gpudiff_close frees what is left. */
 int gpudiff_host_alloc(gpudiff_ctx* ctx, size_t bytes, void** out);
 int gpudiff_host_free(gpudiff_ctx* ctx, void* p);
 
@@ -412,12 +420,13 @@ int gpudiff_encode_object_host(const uint8_t* doc, size_t len, uint32_t seed, ui
  * previous call (scan, tree, values, hashes, sort, blob, -, -); enable != 0
  * keeps recording */
 int gpudiff_k0_profile(gpudiff_ctx* ctx, int enable, uint64_t* ticks8);
-/* profiling hook: the decision kernel's per-wave timeline, recorded by the GPUDIFF_OPT_K2_TIMELINE build of
- * the default kernel (the same kernel plus timestamps): 12 u64 per wave (start, end of the first
+/* profiling hook: the decision kernel's per-wave timeline.  While a buffer is installed (dev_buf != NULL) this
+ * context's passes run the timeline build of the decision kernel (the same kernel plus timestamps), writing 12
+ * u64 per wave (start, end of the first
  * item, items, start of the last item, end, streaming ticks, join ticks, hardware CU id, then ticks
  * spent per item on its rows, between its rows and its first pass, after its joins, and from one
  * item's end to the next one's start; 100 MHz) into device memory dev_buf of cap_waves records;
- * dev_buf NULL stops recording */
+ * dev_buf NULL stops recording and returns the context to the default build */
 int gpudiff_k2_profile(gpudiff_ctx* ctx, uint64_t* dev_buf, uint32_t cap_waves);
 
 /* ---- write path: the request body for a dirty object ----

@@ -110,7 +110,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.slice_cnt = d->slice_cnt;
     b.slice_weq = d->slice_weq;
     b.hash_mask = c->hash_mask;
-    b.k2_timeline = (c->flags & GPUDIFF_OPT_K2_TIMELINE) ? 1u : 0u;
+    b.k2_timeline = c->k2_timeline ? 1u : 0u;
     b.tail_perm = d->tail_perm;
     b.tail_perm_key = &d->tail_perm_key;
     b.rows_gen = d->rows_gen;

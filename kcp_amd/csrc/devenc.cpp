@@ -119,6 +119,7 @@ int gpudiff_k2_profile(gpudiff_ctx* c, uint64_t* dev_buf, uint32_t cap_waves) {
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(k2_profile(dev_buf, cap_waves));
+    c->k2_timeline = dev_buf != nullptr;
     return GPUDIFF_OK;
 }
 

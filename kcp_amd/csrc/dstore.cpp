@@ -854,6 +854,35 @@ int dstore_submit(gpudiff_ctx* c, DStore* s, const gpudiff_event* ev, size_t n, 
         add_doc(e.new_json, e.new_len, e.slot, (uint32_t)i, e);
         new_json_bytes += e.new_len;
     }
+    if (!s->pair_mode && nd) {
+        // Store-mode zero copy: the documents this submit encodes -- per event, its old object on a
+        // slot's first sighting, then its new one -- lie in one gpudiff_host_alloc buffer in that order, each 16-B
+        // aligned and followed by its staged span, so the buffer's range is the staged layout (gaps between the
+        // documents, e.g. old objects the store does not encode, are uploaded but never read).  No staging copy.
+        auto step = [](size_t len) -> uint64_t { return (len + kTokSlack + 15) & ~15ull; };
+        uint8_t* zb = nullptr;
+        uint64_t zn = 0;
+        if (find_host_buf(c, src[0], &zb, &zn) && zn > kTokSlack) {
+            const uint8_t* zend = zb + zn - kTokSlack;  // the upload runs kTokSlack past the last document's span
+            const uint8_t* at = src[0];
+            bool ok = true;
+            for (uint32_t k = 0; k < nd && ok; k++) {
+                const uint8_t* p = src[k];
+                ok = p >= at && !((uintptr_t)p & 15u) && p + step(docs[k].json_len) <= zend;
+                at = p + step(docs[k].json_len);
+            }
+            if (ok) {
+                zsrc = src[0];
+                for (uint32_t k = 0; k < nd; k++) {
+                    docs[k].json_off = (uint64_t)(src[k] - zsrc);
+                    // the staged span's padding, as the staging copy writes it (gpudiff.h: engine-owned)
+                    memset((uint8_t*)src[k] + docs[k].json_len, 0, step(docs[k].json_len) - docs[k].json_len);
+                }
+                jbytes = (uint64_t)(at - zsrc);
+                s->st.zero_copy_batches++;
+            }
+        }
+    }
     jbytes += kTokSlack;
     if (!zsrc && (rc = grow_pinned(&R.hjson, &R.hjson_cap, jbytes))) return rc;
     const uint8_t* hsrc = zsrc ? zsrc : R.hjson;

@@ -130,6 +130,7 @@ struct gpudiff_ctx {
     bool own_stream = false;
     uint32_t threads = 1;
     uint32_t flags = 0;
+    bool k2_timeline = false;  // gpudiff_k2_profile installed a buffer: the timeline build of K2 runs
     EncodeConfig ecfg;
     uint64_t hash_mask = ~0ULL;
     std::vector<std::unique_ptr<PairEncoder>> encoders;

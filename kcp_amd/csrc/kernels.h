@@ -49,7 +49,7 @@ struct DiffBuffers {
     uint64_t* out_h;
     uint8_t* out_k;
     uint64_t hash_mask;
-    uint32_t k2_timeline;       // GPUDIFF_OPT_K2_TIMELINE: the per-wave timeline build of K2 (profiling hook)
+    uint32_t k2_timeline;       // gpudiff_k2_profile installed a buffer: the per-wave timeline build of K2
     uint32_t* tail_perm;        // K2's largest-first final round: its order (device, kK2LptMax u32)
     struct TailPermKey* tail_perm_key;  // (host) the rows and launch shape tail_perm was computed for
     uint64_t rows_gen;          // bumped whenever the batch's rows change (appends, resets, store batches)
@@ -97,7 +97,7 @@ hipError_t launch_slot_owners(hipStream_t s, const DiffBuffers& b);
 hipError_t launch_join(hipStream_t s, const DiffBuffers& b, uint32_t c0, uint32_t c1, const uint4* before,
                        const uint4* after);
 hipError_t launch_emit(hipStream_t s, const DiffBuffers& b);
-// profiling hook: the GPUDIFF_OPT_K2_TIMELINE build of K2 writes 12 u64 per wave (start, first item end, items,
+// profiling hook: the timeline build (gpudiff_k2_profile) of K2 writes 12 u64 per wave (start, first item end, items,
 // last item start, end, streaming ticks, join ticks, hw id, rows, pre, post, ticket ticks) into dev_buf
 // (cap_waves waves); nullptr disables
 hipError_t k2_profile(uint64_t* dev_buf, uint32_t cap_waves);

@@ -228,21 +228,38 @@ __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t*
 }
 
 // ---------------------------------------------------------------- K4
-struct RegionView {
-    const uint32_t* keys;
-    const uint64_t* vals;
-    const uint32_t* metas;
-    const uint8_t* arena;
-    uint32_t L;
+// The joins read the pool (global memory) or, for a small pair K2 staged, the wave's LDS (stage_pair): the same
+// code over address-space-typed pointers, so each form keeps its own addressing (global loads with a scalar base,
+// or 32-bit LDS addresses) instead of 64-bit flat addresses for both.
+template <bool LDS> struct Mem {
+    typedef const uint8_t u8;
+    typedef const uint32_t u32;
+    typedef const uint64_t u64;
+};
+template <> struct Mem<true> {
+    typedef const __attribute__((address_space(3))) uint8_t u8;
+    typedef const __attribute__((address_space(3))) uint32_t u32;
+    typedef const __attribute__((address_space(3))) uint64_t u64;
 };
 
-__device__ __forceinline__ RegionView region_view(const uint8_t* pool, uint64_t off, uint32_t sl, uint32_t sar,
-                                                  bool status, uint32_t L) {
-    const uint8_t* seg = pool + off + (status ? seg_bytes(sl, sar) : 0);
-    RegionView v;
-    v.vals = (const uint64_t*)seg;  // vals u64 | keys u32 | metas u32 | arena (include/gpudiff_format.h)
-    v.keys = (const uint32_t*)(seg + 8ull * L);
-    v.metas = (const uint32_t*)(seg + 12ull * L);
+template <bool LDS>
+struct RegionViewT {
+    typename Mem<LDS>::u32* keys;
+    typename Mem<LDS>::u64* vals;
+    typename Mem<LDS>::u32* metas;
+    typename Mem<LDS>::u8* arena;
+    uint32_t L;
+};
+typedef RegionViewT<false> RegionView;
+
+template <bool LDS = false>
+__device__ __forceinline__ RegionViewT<LDS> region_view(typename Mem<LDS>::u8* pool, uint64_t off, uint32_t sl,
+                                                        uint32_t sar, bool status, uint32_t L) {
+    typename Mem<LDS>::u8* seg = pool + off + (status ? seg_bytes(sl, sar) : 0);
+    RegionViewT<LDS> v;
+    v.vals = (typename Mem<LDS>::u64*)seg;  // vals u64 | keys u32 | metas u32 | arena (include/gpudiff_format.h)
+    v.keys = (typename Mem<LDS>::u32*)(seg + 8ull * L);
+    v.metas = (typename Mem<LDS>::u32*)(seg + 12ull * L);
     v.arena = seg + 16ull * L;
     v.L = L;
     return v;
@@ -269,7 +286,8 @@ __device__ __forceinline__ uint32_t tile_lower_bound(uint32_t x, uint32_t tile, 
 // addresses), finding a dword's owner lane by a cross-lane binary search over
 // the prefix sums.  No load reaches past a tail's padded end.  Returns true in
 // the lanes whose tail differs.
-__device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a, const uint8_t* arena_b,
+template <bool LDS>
+__device__ bool confirm_values(bool need, typename Mem<LDS>::u8* arena_a, uint32_t off_a, typename Mem<LDS>::u8* arena_b,
                                uint32_t off_b, uint32_t len, uint32_t lane) {
     const uint32_t n4 = need ? (len + 3u) >> 2 : 0u;
     const uint32_t incl = wave_incl_scan(n4);
@@ -297,8 +315,8 @@ __device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a
             const uint32_t first = shfl32(incl - n4, own[u]);
             if (act[u]) {
                 const uint32_t k = g - first;
-                xa[u] = *(const uint32_t*)(arena_a + oa + 4u * k);
-                xb[u] = *(const uint32_t*)(arena_b + ob + 4u * k);
+                xa[u] = *(typename Mem<LDS>::u32*)(arena_a + oa + 4u * k);
+                xb[u] = *(typename Mem<LDS>::u32*)(arena_b + ob + 4u * k);
             }
         }
 #pragma unroll
@@ -331,8 +349,8 @@ __device__ __forceinline__ bool wire_equal_number(uint32_t ma, uint64_t xa, uint
 // Merge-join of one region; returns the number of paths emitted.  Emission
 // order = ascending key (the union of both sorted key lists).  *weq_all: every
 // emitted path is a CHANGED leaf with wire_equal_number values (wave-uniform).
-template <bool EMIT>
-__device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_t region_bit,
+template <bool EMIT, bool LDS = false>
+__device__ uint32_t join_region(const RegionViewT<LDS>& A, const RegionViewT<LDS>& B, uint8_t region_bit,
                                 uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
                                 uint32_t lane, bool* weq_all) {
     uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
@@ -370,7 +388,7 @@ __device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_
         const bool matchA = inA && jA < nb && kbj == ka;
         bool differ = matchA && (ma != mbj || xa != xbj);
         // equal head (the first 8 bytes, in vals) and length: confirm the tails in the arenas
-        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
+        differ |= confirm_values<LDS>(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
         // resolve B keys against the A window
         const uint32_t iB = tile_lower_bound(kb, ka, na);
         const uint32_t kai = shfl32(ka, min(iB, 63u));
@@ -423,20 +441,20 @@ __device__ __forceinline__ uint32_t sentinel_noop_bits(uint32_t flags_a) {
     return (flags_a & GPUDIFF_OBJ_HAS_STATUS) ? 0u : NOOP_STATUS;
 }
 
-template <bool EMIT>
-__device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
+template <bool EMIT, bool LDS = false>
+__device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, typename Mem<LDS>::u8* pool, uint64_t mask,
                               uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane, uint32_t* noop) {
     uint32_t n = 0;
     bool spec_weq = true, stat_weq = true;
     if (f & F_JSPEC) {
-        RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
-        RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
-        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
+        RegionViewT<LDS> A = region_view<LDS>(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
+        RegionViewT<LDS> B = region_view<LDS>(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
+        n += join_region<EMIT, LDS>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
     }
     if (f & F_JSTAT) {
-        RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
-        RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
-        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
+        RegionViewT<LDS> A = region_view<LDS>(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
+        RegionViewT<LDS> B = region_view<LDS>(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
+        n += join_region<EMIT, LDS>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
     }
     const bool stat_ok = stat_weq && (!(f & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
     *noop = (((f & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) | (((f & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u);
@@ -448,6 +466,39 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8
         n += 1;
     }
     return n;
+}
+
+// A small dirty pair's joined segments staged in the wave's LDS before K2 joins it (round 6): per
+// side, [spec start, end of the last joined region) -- 16-B aligned, a multiple of 16 bytes -- with every 16-B load
+// of both sides issued before the first is stored, so the join waits for ONE HBM round trip instead of one per
+// 64-key window and per long-value confirmation pass (config2's ConfigMaps/Secrets: 4-5 dependent trips of a few us
+// each under a full streaming load, 29% of a K2 wave's busy time, profiles/r06a/config2/wave_c2.json).
+constexpr uint32_t kJoinLdsSide = 4096;  // bytes per side: 4 x 16 B per lane
+__device__ __forceinline__ uint32_t staged_side_bytes(uint32_t f, uint32_t spec_l, uint32_t spec_ar, uint32_t stat_l,
+                                                      uint32_t stat_ar) {
+    return (uint32_t)((f & F_JSTAT) ? seg_bytes(spec_l, spec_ar) + seg_bytes(stat_l, stat_ar) : seg_bytes(spec_l, spec_ar));
+}
+__device__ __forceinline__ void stage_pair(uint8_t* lds, const uint8_t* pool, uint64_t off_a, uint32_t bytes_a,
+                                           uint64_t off_b, uint32_t bytes_b, uint32_t lane) {
+    // the previous staged join's LDS reads are done before the DMA overwrites them (LDS runs a wave's operations in
+    // order; the fence keeps the compiler from sinking those reads below the loads)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // direct-to-LDS loads (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane k at base + 16 k, no VGPRs)
+#pragma unroll
+    for (uint32_t u = 0; u < kJoinLdsSide / 1024u; u++) {
+        const uint32_t i = 1024u * u + 16u * lane;
+        if (1024u * u < bytes_a && i < bytes_a)
+            __builtin_amdgcn_global_load_lds((const void*)(pool + off_a + i),
+                                             (__attribute__((address_space(3))) void*)(lds + 1024u * u), 16, 0, 0);
+        if (1024u * u < bytes_b && i < bytes_b)
+            __builtin_amdgcn_global_load_lds((const void*)(pool + off_b + i),
+                                             (__attribute__((address_space(3))) void*)(lds + kJoinLdsSide + 1024u * u),
+                                             16, 0, 0);
+    }
+    // landed in LDS before any lane reads another's bytes (the join's windows and arenas)
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 }
 
 // ---------------------------------------------------------------- K3 compaction
@@ -841,7 +892,7 @@ __host__ __device__ inline uint32_t k2_tail_chunks(uint32_t nch, uint32_t nwaves
 // current item, so the launch ends when the work does, not when the wave with
 // the heaviest static share of items does; the last k2_tail_chunks() chunks are
 // handed out as 8-pair items, so the final round of items is short too.
-// K2 per-wave timeline (PROF: the GPUDIFF_OPT_K2_TIMELINE build only, tools/k2_wave_profile.py): 12 u64 per wave --
+// K2 per-wave timeline (PROF: the timeline build only, selected by gpudiff_k2_profile, tools/k2_wave_profile.py): 12 u64 per wave --
 // start, end of the first item, items, start of the last item, end, streaming ticks, join ticks,
 // hardware id (wall clock: 100 MHz)
 __device__ uint64_t* g_k2_prof;
@@ -862,14 +913,27 @@ struct HelpSlot {
     uint32_t p0, cnt;  // its pairs
     uint64_t mis_s, mis_t;
 };
+// The slot protocol's ordering is stated in the memory model, not left to LDS executing a wave's
+// operations in order: the owner's field stores are ordered before its closing gen store by release, and a helper's
+// gen loads are acquires, so a helper that reads the same even gen before and after the fields (g1 == g2 == g, read
+// AFTER its helpers increment) read the fields of that publication; the owner cannot republish while helpers != 0
+// (it waits for 0 with acquire loads), so the fields stay put while the helper streams.  Mismatch bits go in with
+// release ORs before the helper's release decrement, and the owner reads them after its acquire load of helpers == 0.
+// All workgroup scope: LDS only, no cache maintenance.
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ uint64_t lds_ld64(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_or64(uint64_t* p, uint64_t v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_add(uint32_t* p, uint32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 template <int U, int MINB, bool PROF = false, bool HELP = false>
@@ -895,6 +959,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
     __shared__ HelpSlot help_slots[HELP ? 4 : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t join_lds[4][2 * kJoinLdsSide];  // stage_pair, one area per wave
+    uint8_t* const my_lds = join_lds[threadIdx.x >> 6];
     [[maybe_unused]] HelpSlot* const my = &help_slots[HELP ? (threadIdx.x >> 6) : 0];
     if constexpr (HELP) {
         if (lane == 0) {
@@ -1061,13 +1127,13 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             }
             for (uint32_t base = 0; base < total;) {
                 uint32_t nb = 0;
-                if (lane == 0) nb = atomicAdd(&my->cursor, 64u * U);
+                if (lane == 0) nb = lds_add(&my->cursor, 64u * U);
                 stream_pass(base, total, incl, first, n1, adj_a, adj_b, off_a, off_b, mis_s, mis_t);
                 base = uni(__builtin_amdgcn_readlane(nb, 0));
             }
             if (lane == 0) {
-                atomicOr((unsigned long long*)&my->mis_s, (unsigned long long)mis_s);
-                atomicOr((unsigned long long*)&my->mis_t, (unsigned long long)mis_t);
+                lds_or64(&my->mis_s, mis_s);
+                lds_or64(&my->mis_t, mis_t);
             }
             while (uni(lds_ld(&my->helpers)) != 0u) __builtin_amdgcn_s_sleep(1);
             const uint64_t ms = lds_ld64(&my->mis_s), mt = lds_ld64(&my->mis_t);
@@ -1094,8 +1160,26 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                      (stat_dirty && !has_st_b ? F_SENT : 0u) | (((v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu) ? F_SEED : 0u);
             mycap = (spec_dirty ? v1.x + v1.y : 0u) + (stat_dirty ? v2.x + v2.y + (has_st_b ? 0u : 1u) : 0u);
         }
-        // ---- changed paths of the dirty pairs, in pair order, into this wave's arena
-        for (uint64_t dm = ballot((myflag & (F_SPEC | F_STATUS)) != 0u); dm; dm &= dm - 1) {
+        // ---- changed paths of the dirty pairs into this wave's arena.  First every pair whose only path is the
+        // status-absent sentinel (every ConfigMap/Secret update: all of config2), one entry a lane, in one step
+        const bool sent_only = valid && !err && (myflag & F_SENT) && !(myflag & (F_JSPEC | F_JSTAT));
+        const uint64_t sm = ballot(sent_only);
+        uint64_t done = 0;
+        if (sm && used + popc64(sm) <= arena_per_wave) {
+            if (sent_only) {
+                const uint32_t src = wbase + used + popc64(sm & mask_lt(lane));
+                ah[src] = (myflag & F_SEED) ? status_sentinel_hash((v3.x >> GPUDIFF_OBJ_SEED_SHIFT) & 0xFFu, mask) : sent0;
+                ak[src] = GPUDIFF_PATH_REGION_STATUS | GPUDIFF_PATH_STATUS_ABSENT;
+                mycap = 0;  // no K4 scratch slot needed
+                mysrc = src;
+                mycnt = 1;
+                mynoop = sentinel_noop_bits(v3.x);
+            }
+            used += popc64(sm);
+            done = sm;
+        }
+        // ... then the others one at a time, in pair order
+        for (uint64_t dm = ballot((myflag & (F_SPEC | F_STATUS)) != 0u) & ~done; dm; dm &= dm - 1) {
             const uint32_t k = (uint32_t)__builtin_ctzll(dm);
             const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)myflag, (int)k);
             const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)mycap, (int)k);
@@ -1106,8 +1190,17 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
                     // dead during the join
-                    const gpudiff_pair_row r = rows[p0 + k];
-                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
+                    gpudiff_pair_row r = rows[p0 + k];
+                    const uint32_t sa = staged_side_bytes(fk, r.spec_l_a, r.spec_ar_a, r.stat_l_a, r.stat_ar_a);
+                    const uint32_t sb = staged_side_bytes(fk, r.spec_l_b, r.spec_ar_b, r.stat_l_b, r.stat_ar_b);
+                    if (sa <= kJoinLdsSide && sb <= kJoinLdsSide) {  // small pair: joined from LDS
+                        stage_pair(my_lds, pool, r.off_a, sa, r.off_b, sb, lane);
+                        r.off_a = 0;
+                        r.off_b = kJoinLdsSide;
+                        pc = join_pair<true, true>(r, fk, (Mem<true>::u8*)my_lds, mask, ah, ak, src, lane, &nb);
+                    } else {
+                        pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
+                    }
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
                     const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
                     nb = sentinel_noop_bits(fa);
@@ -1181,9 +1274,8 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 const uint32_t g = uni(lds_ld(&h->gen));
                 if ((g & 1u) || uni(lds_ld(&h->cursor)) >= uni(lds_ld(&h->total))) continue;
                 any = true;
-                if (lane == 0) atomicAdd(&h->helpers, 1u);
-                __asm__ volatile("" ::: "memory");
-                const uint32_t g1 = uni(lds_ld(&h->gen));
+                if (lane == 0) lds_add(&h->helpers, 1u);
+                const uint32_t g1 = uni(lds_ld(&h->gen));  // after the increment: the owner cannot republish now
                 const uint32_t hp0 = uni(lds_ld(&h->p0)), hcnt = uni(lds_ld(&h->cnt)), htot = uni(lds_ld(&h->total));
                 const uint32_t g2 = uni(lds_ld(&h->gen));
                 if (g1 == g && g2 == g) {  // the item published at gen g: its geometry from its rows
@@ -1214,18 +1306,17 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                     uint64_t ms = 0, mt = 0;
                     for (;;) {
                         uint32_t nb = 0;
-                        if (lane == 0) nb = atomicAdd(&h->cursor, 64u * U);
+                        if (lane == 0) nb = lds_add(&h->cursor, 64u * U);
                         nb = uni(__builtin_amdgcn_readlane(nb, 0));
                         if (nb >= htot) break;
                         stream_pass(nb, htot, incl, first, n1, adj_a, adj_b, off_a, off_b, ms, mt);
                     }
                     if (lane == 0) {
-                        if (ms) atomicOr((unsigned long long*)&h->mis_s, (unsigned long long)ms);
-                        if (mt) atomicOr((unsigned long long*)&h->mis_t, (unsigned long long)mt);
+                        if (ms) lds_or64(&h->mis_s, ms);
+                        if (mt) lds_or64(&h->mis_t, mt);
                     }
                 }
-                __asm__ volatile("" ::: "memory");
-                if (lane == 0) atomicSub(&h->helpers, 1u);
+                if (lane == 0) __hip_atomic_fetch_sub(&h->helpers, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
     }
@@ -1359,7 +1450,7 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
 
 // The decision kernels: 8 x 16-B chunks a side in flight per lane at 3 waves/SIMD (139 VGPRs) by default, 16 at
 // 2 waves/SIMD for deep pairs (>= kK2BigPairBytes a pair on average), each also as the per-wave timeline build
-// (GPUDIFF_OPT_K2_TIMELINE, tools/k2_wave_profile.py).  In-process A/B (profiles/r04p): 8 in flight beat round
+// (gpudiff_k2_profile, tools/k2_wave_profile.py).  In-process A/B (profiles/r04p): 8 in flight beat round
 // 3's 4 at 4 waves on every shape -- config3 10M K2 8.21 vs 8.28 ms, the N = 8 share 1.147 vs 1.164, config4 1.080
 // vs 1.091 -- and 16 wins only on deep pairs (config4 1.043 ms, but config3 8.44 and the share 1.195): when the
 // items are 16-256 KiB the last round's waves stream alone and their own loads in flight set the tail's rate.

@@ -644,14 +644,32 @@ int gpudiff_write_plan_get_ex(gpudiff_ctx* c, gpudiff_ticket ticket, uint32_t mo
         if (to[k].status != GPUDIFF_TOK_OK) def.push_back((uint32_t)k);
     std::vector<uint64_t> hoff(def.size() + 1, 0);
     for (size_t k = 0; k < def.size(); k++) hoff[k + 1] = hoff[k] + docs[def[k]].json_len;
-    std::vector<uint8_t> hjson(hoff.back());
+    std::vector<uint8_t> hjson;
     if (!def.empty()) {
-        hipError_t e = hipSuccess;
-        for (size_t k = 0; k < def.size() && e == hipSuccess; k++)
-            if (docs[def[k]].json_len)
-                e = hipMemcpyAsync(hjson.data() + hoff[k], sp.djson + docs[def[k]].json_off, docs[def[k]].json_len,
-                                   hipMemcpyDeviceToHost, c->stream);
+        // one gather on the device (K7's 16-B copies: staged documents start 16-B aligned and their spans run at
+        // least 16 bytes past their ends), then ONE copy back -- not a pageable round trip per document
+        std::vector<BlobMove> mv(def.size());
+        uint64_t gb = 0;
+        for (size_t k = 0; k < def.size(); k++) {
+            const TokDoc& d = docs[def[k]];
+            mv[k] = BlobMove{d.json_off, gb, ((uint64_t)d.json_len + 15u) & ~15ull};
+            hoff[k] = gb;
+            gb += mv[k].bytes;
+        }
+        hjson.resize(gb);
+        void *d_mv = nullptr, *d_gather = nullptr;
+        hipError_t e = hipMalloc(&d_mv, mv.size() * sizeof(BlobMove));
+        if (e == hipSuccess) e = hipMalloc(&d_gather, std::max<uint64_t>(gb, 16));
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_mv, mv.data(), mv.size() * sizeof(BlobMove), hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess)
+            e = launch_move_blobs(c->stream, sp.djson, (uint8_t*)d_gather, (const BlobMove*)d_mv, (uint32_t)mv.size());
+        // the staged JSON's read marker again, behind the last read of it (k0_done covers every read)
+        if (e == hipSuccess && dstore_staged_mark_read(c, ticket)) e = hipErrorUnknown;
+        if (e == hipSuccess) e = hipMemcpyAsync(hjson.data(), d_gather, gb, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        for (void* q : {d_mv, d_gather})
+            if (q) (void)hipFree(q);
         if (e != hipSuccess) {
             gd::g_last_hip_error = hipGetErrorString(e);
             return GPUDIFF_E_DEVICE;

@@ -19,7 +19,7 @@ from . import buildinfo
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgpudiff.so")
 
-ABI_VERSION = 5  # GPUDIFF_ABI_VERSION of include/gpudiff.h
+ABI_VERSION = 6  # GPUDIFF_ABI_VERSION of include/gpudiff.h
 OK = 0
 E_INVAL, E_NOMEM, E_DEVICE, E_NODEVICE, E_CAPACITY, E_STATE, E_DECODE, E_NOTFOUND = range(-1, -9, -1)
 
@@ -28,7 +28,6 @@ PATH_CHANGED, PATH_ADDED, PATH_REMOVED, PATH_STATUS_ABSENT = 0, 1, 2, 3
 PATH_REGION_STATUS = 0x80
 OPT_TIMING = 0x1
 OPT_DEVICE_ENCODE = 0x2000000
-OPT_K2_TIMELINE = 0x100  # profiling hook: K2's per-wave timeline build (k2_profile)
 OPT_ARENA_SHIFT = 21  # test hook: 4 bits, the K2 wave arenas shrunk 2^k-fold (forces the deferred K4 path)
 DEVICE_CURRENT, DEVICE_NONE = -1, -2
 
@@ -119,6 +118,45 @@ class PinnedJson:
         if self.ptr:
             _chk(_lib.gpudiff_host_free(self.eng.ctx, self.ptr), "gpudiff_host_free")
             self.ptr = None
+
+
+class PinnedDocs:
+    """Documents in one gpudiff_host_alloc buffer, each at a 16-B aligned offset followed by its staged span (the
+    zero-copy layout of gpudiff.h gpudiff_host_alloc): what a watch-stream reader produces when it writes each
+    event's JSON straight into engine-pinned memory.  `ptrs[i]` is document i's address.  Free it (or the engine)
+    once every submit that reads it has been waited."""
+
+    def __init__(self, eng: "Engine", lens):
+        lens = np.asarray(lens, dtype=np.uint64)
+        self.offs, self.nbytes = zero_copy_layout(lens)
+        self.lens = lens
+        p = C.c_void_p()
+        _chk(_lib.gpudiff_host_alloc(eng.ctx, self.nbytes, C.byref(p)), "gpudiff_host_alloc")
+        self.eng, self.ptr = eng, p.value
+        self.view = np.ctypeslib.as_array(C.cast(self.ptr, C.POINTER(C.c_uint8)), (self.nbytes,))
+        self.ptrs = self.offs + np.uint64(self.ptr)
+
+    @classmethod
+    def of_bytes(cls, eng: "Engine", docs):
+        docs = [bytes(d) for d in docs]
+        pd = cls(eng, [len(d) for d in docs])
+        for o, d in zip(pd.offs.tolist(), docs):
+            pd.view[o:o + len(d)] = np.frombuffer(d, np.uint8)
+        return pd
+
+    @classmethod
+    def of_ranges(cls, eng: "Engine", buf: np.ndarray, starts, lens):
+        """Document i = buf[starts[i] : starts[i] + lens[i]] (the render step; untimed in the benches)."""
+        pd = cls(eng, lens)
+        src = np.ascontiguousarray(buf)
+        for o, a, n in zip(pd.offs.tolist(), np.asarray(starts).tolist(), np.asarray(lens).tolist()):
+            pd.view[o:o + n] = src[a:a + n]
+        return pd
+
+    def free(self):
+        if self.ptr and self.eng.ctx:
+            _chk(_lib.gpudiff_host_free(self.eng.ctx, self.ptr), "gpudiff_host_free")
+        self.ptr = None
 
 
 class PairRow(C.Structure):
@@ -592,13 +630,39 @@ class ObjectStore:
                 arr[i].old_len = len(ob)
         return arr, n, keep
 
-    def submit(self, items) -> int:
-        arr, n, keep = self.events(items)
-        return self.submit_raw(arr, n, keep)
+    def submit(self, items, zero_copy: bool = False) -> int:
+        """zero_copy (device-encode stores): every event's documents -- its old object when given, then its new one --
+        are first written into one gpudiff_host_alloc buffer in the zero-copy layout, which the store uploads with
+        no staging copy (old objects the store does not encode are uploaded but never read)."""
+        if not zero_copy:
+            arr, n, keep = self.events(items)
+            return self.submit_raw(arr, n, keep)
+        docs, slots = [], []
+        for it in items:
+            if it[2] is not None:
+                docs.append(to_json_bytes(it[2]))
+            docs.append(to_json_bytes(it[1]))
+        pd = PinnedDocs.of_bytes(self.engine, docs)
+        n = len(items)
+        arr = (Event * max(n, 1))()
+        k = 0
+        for i, it in enumerate(items):
+            arr[i].slot = it[0]
+            arr[i].pair_id = it[3] if len(it) > 3 else i
+            arr[i].cluster_id = it[4] if len(it) > 4 else 0
+            if it[2] is not None:
+                arr[i].old_json, arr[i].old_len = int(pd.ptrs[k]), int(pd.lens[k])
+                k += 1
+            arr[i].new_json, arr[i].new_len = int(pd.ptrs[k]), int(pd.lens[k])
+            k += 1
+        return self.submit_raw(arr, n, pd)
 
     def submit_raw(self, arr, n, keep=None) -> int:
         t = C.c_uint64()
         _chk(_lib.gpudiff_store_submit(self.engine.ctx, self.h, arr, n, C.byref(t)), "gpudiff_store_submit")
+        old = self._keep[self._k]
+        if old is not None and isinstance(old[1], PinnedDocs):
+            old[1].free()  # its batch was waited before this submit could reuse the ring slot
         self._keep[self._k] = (arr, keep)
         self._k ^= 1
         return t.value
@@ -615,6 +679,10 @@ class ObjectStore:
         if self.h:
             _lib.gpudiff_store_free(self.engine.ctx, self.h)
             self.h = C.c_void_p(0)
+        for k in self._keep:
+            if k is not None and isinstance(k[1], PinnedDocs):
+                k[1].free()
+        self._keep = [None, None]
 
     def __del__(self):
         try:
@@ -849,7 +917,8 @@ class Engine:
         return list(out)
 
     def k2_profile(self, dev_ptr: int, cap_waves: int):
-        """Record K2 variant 14's per-wave timeline into device memory (8 u64 per wave); 0 stops."""
+        """Run K2's timeline build and record its per-wave timeline into device memory (12 u64 per wave); 0 stops
+        recording and returns the context to the default build."""
         _chk(_lib.gpudiff_k2_profile(self.ctx, dev_ptr or None, cap_waves), "gpudiff_k2_profile")
 
     # ---- single pair drop-ins

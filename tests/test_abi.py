@@ -39,7 +39,7 @@ def test_host_only_context_refuses_device_work():
     with pytest.raises(G.GpuDiffError) as ei:
         e.submit([(b"{}", b"{}")])
     assert ei.value.code == G.E_NODEVICE
-    assert G.lib().gpudiff_abi_version() == G.ABI_VERSION == 5
+    assert G.lib().gpudiff_abi_version() == G.ABI_VERSION == 6
     # pinned zero-copy buffers need a device; freeing a pointer the context never handed out is refused
     import ctypes as C
     p = C.c_void_p()
@@ -85,11 +85,11 @@ def test_open_rejects_removed_tuning_bits():
     """ABI 5: the tuning bits of earlier rounds are gone; gpudiff_open refuses any bit outside
     GPUDIFF_OPT_KNOWN (timing, the K2 timeline hook, the arena test hook, device encode) instead of ignoring it."""
     from kcp_amd import gpudiff as G
-    for bad in (0x2, 0x4, 0x8, 0x80, 14 << 8, 3 << 16, 0x100000, 1 << 26, 1 << 28, 1 << 30):
+    for bad in (0x2, 0x4, 0x8, 0x80, 0x100, 14 << 8, 3 << 16, 0x100000, 1 << 26, 1 << 28, 1 << 30):
         with pytest.raises(G.GpuDiffError) as ei:
             G.Engine(device=G.DEVICE_NONE, flags=bad)
         assert ei.value.code == G.E_INVAL, hex(bad)
-    for ok in (0, G.OPT_TIMING, G.OPT_K2_TIMELINE, 12 << G.OPT_ARENA_SHIFT, G.OPT_DEVICE_ENCODE):
+    for ok in (0, G.OPT_TIMING, 12 << G.OPT_ARENA_SHIFT, G.OPT_DEVICE_ENCODE):
         G.Engine(device=G.DEVICE_NONE, flags=ok).close()
 
 

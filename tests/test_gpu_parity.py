@@ -10,6 +10,7 @@ import random
 
 import numpy as np
 import pytest
+import torch
 
 from kcp_amd import gpudiff as G
 from oracle import gpudiff_oracle as O
@@ -311,17 +312,24 @@ def test_submit_pipelining(eng):
 @pytest.mark.parametrize("timeline", [False, True], ids=["default", "timeline_build"])
 def test_k2_kernels_bit_exact(timeline):
     """The four decision kernels -- 8 chunks a side in flight (mixed pairs) and 16 (deep pairs, >= 16 KiB a pair),
-    each also as the per-wave timeline build (GPUDIFF_OPT_K2_TIMELINE) -- against the oracle, with joins in K2
-    and with every join deferred to K4."""
+    each also as the per-wave timeline build (selected while gpudiff_k2_profile has a buffer installed) -- against
+    the oracle, with joins in K2 and with every join deferred to K4."""
     pairs, _, _ = make_pairs(1200, seed=31, mutate_frac=0.3, pretty_frac=0)
     deep, _, _ = make_pairs(120, seed=32, mix=(("crd", 1.0),), mutate_frac=0.5, crd_leaves=2500, pretty_frac=0)
     for shrink in (0, 12):
-        e = G.Engine(device=0, flags=(G.OPT_K2_TIMELINE if timeline else 0) | (shrink << G.OPT_ARENA_SHIFT))
+        e = G.Engine(device=0, flags=shrink << G.OPT_ARENA_SHIFT)
+        if timeline:
+            prof = torch.zeros(12 << 16, dtype=torch.int64, device="cuda")
+            e.k2_profile(prof.data_ptr(), 1 << 16)
         assert_matches(e.diff_pairs(pairs), pairs)
         hb = e.encode(deep)
         assert hb.info().pool_bytes / len(deep) > 2 * 16384  # the deep-pair kernel
         hb.free()
         assert_matches(e.diff_pairs(deep), deep)
+        if timeline:
+            e.sync()
+            assert int((prof.view(-1, 12)[:, 4] != 0).sum()) > 0  # the timeline build ran and recorded waves
+            e.k2_profile(0, 0)
         e.close()
 
 

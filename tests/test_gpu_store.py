@@ -6,7 +6,9 @@ events on one slot inside a batch, forced path-hash collisions (8-bit
 hashes: re-seeds through old_json), compactions of the two spaces, Delete
 events (forget) and undecodable new objects.  Every test runs in both modes:
 host encoding, and device encoding (raw JSON up, kernel K0 encodes, the host
-re-does only the events K0 defers)."""
+re-does only the events K0 defers) -- and device encoding with the events' JSON
+written into one engine-pinned buffer in the zero-copy layout (no staging
+copy, VERDICT r5 #2)."""
 import copy
 import json
 import random
@@ -20,7 +22,7 @@ from tests.workload import _noise, configmap, crd, deployment, mutate
 
 pytestmark = pytest.mark.gpu
 
-MODES = pytest.mark.parametrize("dev", [False, True], ids=["host_encode", "device_encode"])
+MODES = pytest.mark.parametrize("dev", [False, True, "zc"], ids=["host_encode", "device_encode", "device_zero_copy"])
 
 
 def _obj(rnd, i):
@@ -72,11 +74,14 @@ def _stream(seed, n_slots, n_batches, per_batch):
     return out
 
 
-def _run(eng, st, stream, drop_old=False):
+def _run(eng, st, stream, drop_old=False, zc=False):
+    z0 = st.stats().zero_copy_batches
     for evs, pairs in stream:
         items = [(s, nj, None if drop_old else oj, i, s % 7) for i, (s, nj, oj) in enumerate(evs)]
-        res = eng.wait(st.submit(items))
+        res = eng.wait(st.submit(items, zero_copy=zc))
         assert_matches(res, pairs, hash_bits=eng.path_hash_bits)
+    # zero copy: every batch uploaded straight from its pinned buffer
+    assert st.stats().zero_copy_batches - z0 == (len(stream) if zc else 0)
 
 
 @MODES
@@ -85,8 +90,8 @@ def test_replay_matches_oracle(drop_old, dev):
     """Events on 60 slots, 6 batches of 150 (many slots get several events
     per batch: they chain)."""
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=60, space_bytes=64 << 20, max_events=256, device_encode=dev)
-    _run(e, st, _stream(1, 60, 6, 150), drop_old)
+    st = e.object_store(max_slots=60, space_bytes=64 << 20, max_events=256, device_encode=bool(dev))
+    _run(e, st, _stream(1, 60, 6, 150), drop_old, zc=dev == "zc")
     s = st.stats()
     assert s.events == 900 and s.live_slots == 60 and s.collisions_unresolved == 0
     assert s.deferred == 0 or drop_old  # regular objects: K0 encodes and K0c confirms every event
@@ -99,8 +104,8 @@ def test_compaction_keeps_results_exact(dev):
     """A space of 512 KiB forces compactions while batches still read blobs of
     the previous versions."""
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=40, space_bytes=512 << 10, max_events=128, device_encode=dev)
-    _run(e, st, _stream(2, 40, 12, 60))
+    st = e.object_store(max_slots=40, space_bytes=512 << 10, max_events=128, device_encode=bool(dev))
+    _run(e, st, _stream(2, 40, 12, 60), zc=dev == "zc")
     s = st.stats()
     assert s.compactions >= 3, s.compactions
     assert s.used_bytes <= 512 << 10
@@ -114,8 +119,8 @@ def test_compaction_keeps_path_tables(dev):
     every batch, K0c confirms every event after the moves (no false collision
     defers one to the host)."""
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=40, space_bytes=2 << 20, max_events=128, device_encode=dev)
-    _run(e, st, _stream(6, 40, 40, 60))
+    st = e.object_store(max_slots=40, space_bytes=2 << 20, max_events=128, device_encode=bool(dev))
+    _run(e, st, _stream(6, 40, 40, 60), zc=dev == "zc")
     s = st.stats()
     assert s.compactions >= 2, s.compactions
     assert s.deferred == 0 and s.reseeded == 0
@@ -126,8 +131,8 @@ def test_compaction_keeps_path_tables(dev):
 @MODES
 def test_forced_collisions_reseed_through_old_json(dev):
     e = G.Engine(device=0, encode_threads=2, path_hash_bits=8)
-    st = e.object_store(max_slots=30, space_bytes=64 << 20, max_events=128, device_encode=dev)
-    _run(e, st, _stream(3, 30, 5, 80))
+    st = e.object_store(max_slots=30, space_bytes=64 << 20, max_events=128, device_encode=bool(dev))
+    _run(e, st, _stream(3, 30, 5, 80), zc=dev == "zc")
     s = st.stats()
     assert s.reseeded > 0 and s.collisions_unresolved == 0
     st.free()
@@ -141,8 +146,8 @@ def test_path_tables_exact_at_16_bits(dev):
     device, tab_agree on the host) catch every such collision exactly and the
     pair is re-encoded from old_json, so every result equals the oracle's."""
     e = G.Engine(device=0, encode_threads=4, path_hash_bits=16)
-    st = e.object_store(max_slots=40, space_bytes=64 << 20, max_events=256, device_encode=dev)
-    _run(e, st, _stream(9, 40, 6, 120))
+    st = e.object_store(max_slots=40, space_bytes=64 << 20, max_events=256, device_encode=bool(dev))
+    _run(e, st, _stream(9, 40, 6, 120), zc=dev == "zc")
     s = st.stats()
     assert s.reseeded > 0 and s.collisions_unresolved == 0
     st.free()
@@ -159,19 +164,20 @@ def test_adversarial_collisions_never_equal(dev):
     from tests.test_path_table import adversarial_pairs
     pairs = adversarial_pairs(16)
     e = G.Engine(device=0, encode_threads=2, path_hash_bits=16)
-    st = e.object_store(max_slots=8, space_bytes=8 << 20, max_events=16, device_encode=dev)
+    st = e.object_store(max_slots=8, space_bytes=8 << 20, max_events=16, device_encode=bool(dev))
     olds = [json.dumps(a, separators=(",", ":")).encode() for a, _b in pairs]
     news = [json.dumps(b, separators=(",", ":")).encode() for _a, b in pairs]
     k = len(pairs)
     # first sightings (slots 0..k-1 and k..2k-1 hold the old versions), diffed against {}
-    r = e.wait(st.submit([(i, olds[i % k], None, i) for i in range(2 * k)]))
+    zc = dev == "zc"
+    r = e.wait(st.submit([(i, olds[i % k], None, i) for i in range(2 * k)], zero_copy=zc))
     assert_matches(r, [(b"{}", olds[i % k]) for i in range(2 * k)], hash_bits=16)
     # the new versions with old_json (slots 0..k-1): the oracle's results
-    r = e.wait(st.submit([(i, news[i], olds[i], i) for i in range(k)]))
+    r = e.wait(st.submit([(i, news[i], olds[i], i) for i in range(k)], zero_copy=zc))
     exp = assert_matches(r, [(olds[i], news[i]) for i in range(k)], hash_bits=16)
     assert all(x["spec_dirty"] and x["seed"] != 0 for x in exp)
     # without old_json (slots k..2k-1): conservative, never equal
-    r = e.wait(st.submit([(k + i, news[i], None, i) for i in range(k)]))
+    r = e.wait(st.submit([(k + i, news[i], None, i) for i in range(k)], zero_copy=zc))
     assert r.pair_flags.tolist() == [G.SPEC_DIRTY | G.STATUS_DIRTY | G.DECODE_ERROR] * k
     s = st.stats()
     assert s.collisions_unresolved == k
@@ -182,7 +188,7 @@ def test_adversarial_collisions_never_equal(dev):
 @MODES
 def test_forget_and_decode_error(dev):
     e = G.Engine(device=0, encode_threads=1)
-    st = e.object_store(max_slots=4, space_bytes=1 << 20, max_events=16, device_encode=dev)
+    st = e.object_store(max_slots=4, space_bytes=1 << 20, max_events=16, device_encode=bool(dev))
     rnd = random.Random(4)
     a = deployment(rnd, 0, 0)
     aj = json.dumps(a).encode()
@@ -211,15 +217,16 @@ def test_forget_and_decode_error(dev):
 @MODES
 def test_two_submits_in_flight(dev):
     e = G.Engine(device=0, encode_threads=4)
-    st = e.object_store(max_slots=50, space_bytes=32 << 20, max_events=200, device_encode=dev)
+    st = e.object_store(max_slots=50, space_bytes=32 << 20, max_events=200, device_encode=bool(dev))
     stream = _stream(5, 50, 4, 120)
     tickets = []
     for k, (evs, pairs) in enumerate(stream):
         items = [(s, nj, oj, i) for i, (s, nj, oj) in enumerate(evs)]
-        tickets.append(st.submit(items))
+        tickets.append(st.submit(items, zero_copy=dev == "zc"))
         if k >= 1:
             assert_matches(e.wait(tickets[k - 1]), stream[k - 1][1])
     assert_matches(e.wait(tickets[-1]), stream[-1][1])
+    assert st.stats().zero_copy_batches == (len(stream) if dev == "zc" else 0)
     st.free()
     e.close()
 
@@ -268,7 +275,7 @@ def test_device_encode_deferrals_exact(drop_old):
     stream = _raw_stream(11, 40, 6, 120)
     for dev in (False, True):
         e = G.Engine(device=0, encode_threads=4)
-        st = e.object_store(max_slots=40, space_bytes=32 << 20, max_events=256, device_encode=dev)
+        st = e.object_store(max_slots=40, space_bytes=32 << 20, max_events=256, device_encode=bool(dev))
         for evs, pairs in stream:
             items = [(s, nj, None if drop_old else oj, i, s % 5) for i, (s, nj, oj) in enumerate(evs)]
             res = e.wait(st.submit(items))
@@ -330,3 +337,53 @@ def test_device_store_space_pressure_stays_usable():
         docs = [prev[i] for i in range(8)]
     st.free()
     e.close()
+
+
+def test_zero_copy_store_layout_rules():
+    """Store-mode zero copy takes a batch only in the documented layout: the documents the store encodes in
+    submit order inside one engine-pinned buffer, 16-B aligned, each followed by its staged span.  Old objects the
+    store does not encode may lie anywhere (here: outside the buffer); any other layout (documents out of order)
+    takes the staging copy.  Results equal the oracle's either way."""
+    e = G.Engine(device=0, encode_threads=2)
+    st = e.object_store(max_slots=64, space_bytes=32 << 20, max_events=64, device_encode=True)
+    stream = _stream(21, 32, 3, 40)
+    # batch 0: every event staged zero-copy (old objects in the buffer too, first sightings among them)
+    evs, pairs = stream[0]
+    assert_matches(e.wait(st.submit([(s, nj, oj, i) for i, (s, nj, oj) in enumerate(evs)], zero_copy=True)), pairs)
+    assert st.stats().zero_copy_batches == 1
+    # batch 1: only the new objects in the buffer, the old objects as ordinary host memory -- still zero copy (a
+    # slot seen before reads its old object only on a collision; a first sighting here has none)
+    evs, pairs = stream[1]
+    news = G.PinnedDocs.of_bytes(e, [nj for _, nj, _ in evs])
+    items = [(s, int(news.ptrs[i]), int(news.lens[i]), C_buf(oj)) for i, (s, nj, oj) in enumerate(evs)]
+    arr, n = _events_raw(items)
+    assert_matches(e.wait(st.submit_raw(arr, n, (news, items))), pairs)
+    assert st.stats().zero_copy_batches == 2
+    # batch 2: the same documents written in reverse order -- not the layout: staged, same results
+    evs, pairs = stream[2]
+    rev = G.PinnedDocs.of_bytes(e, [nj for _, nj, _ in reversed(evs)])
+    items = [(s, int(rev.ptrs[len(evs) - 1 - i]), int(rev.lens[len(evs) - 1 - i]), C_buf(oj) if oj else None)
+             for i, (s, nj, oj) in enumerate(evs)]
+    arr, n = _events_raw(items)
+    assert_matches(e.wait(st.submit_raw(arr, n, (rev, items))), pairs)
+    assert st.stats().zero_copy_batches == 2
+    st.free()
+    news.free()
+    rev.free()
+    e.close()
+
+
+def C_buf(b):
+    import ctypes
+    return ctypes.create_string_buffer(b, len(b)) if b is not None else None
+
+
+def _events_raw(items):
+    """[(slot, new_ptr, new_len, old ctypes buffer or None)] -> (Event array, n)."""
+    import ctypes
+    arr = (G.Event * len(items))()
+    for i, (s, p, ln, old) in enumerate(items):
+        arr[i].slot, arr[i].pair_id, arr[i].new_json, arr[i].new_len = s, i, p, ln
+        if old is not None:
+            arr[i].old_json, arr[i].old_len = ctypes.cast(old, ctypes.c_void_p), len(old)
+    return arr, len(items)

@@ -1,7 +1,7 @@
 """K2's per-wave timeline on MI355X: where a diff pass loses time against a pure stream.
 
 Ingests config3 (optionally resized) like bench.py, times the default K2 ("variant0") and then runs its
-timeline build ("variant14", GPUDIFF_OPT_K2_TIMELINE: the same kernel plus wall-clock stamps, 100 MHz), recording
+timeline build ("variant14", selected by gpudiff_k2_profile: the same kernel plus wall-clock stamps, 100 MHz), recording
 per wave: start, end of
 its first item, items taken, start of its last item, end, ticks spent streaming and in the join.
 
@@ -43,9 +43,12 @@ def main():
     pop = S.Population(cfg, 1, 0)
     n = pop.n
     out = {"pairs": n}
-    for variant in (0, 14):  # 14: the timeline build (GPUDIFF_OPT_K2_TIMELINE; the record names of earlier rounds)
-        eng = G.Engine(device=0, encode_threads=args.threads, stream=stream.cuda_stream, timing=True,
-                       flags=(G.OPT_K2_TIMELINE if variant == 14 else 0) | args.flags)
+    for variant in (0, 14):  # 14: the timeline build (installed buffer; the record names of earlier rounds)
+        eng = G.Engine(device=0, encode_threads=args.threads, stream=stream.cuda_stream, timing=True, flags=args.flags)
+        cap = 1 << 16
+        buf = torch.zeros(cap * 12, dtype=torch.int64, device=dev)
+        if variant == 14:  # the timeline build runs while a buffer is installed (gpudiff_k2_profile)
+            eng.k2_profile(buf.data_ptr(), cap)
         first = pop.chunk(eng, 0, min(262144, n), args.threads)
         per_pair = first.pool_bytes / max(1, min(262144, n))
         db = eng.device_batch(int(per_pair * n * (1.4 if args.config == "config4" else 1.15)) + (64 << 20), n)
@@ -68,9 +71,7 @@ def main():
         rec = {"k2_ms": tm.compare_ms, "pass_ms": tm.total_ms, "join_ms": tm.join_ms, "emit_ms": tm.emit_ms,
                "compact_ms": tm.compact_ms, "format_bytes": db.stats().compare_bytes}
         if variant == 14:
-            cap = 1 << 16
-            buf = torch.zeros(cap * 12, dtype=torch.int64, device=dev)
-            eng.k2_profile(buf.data_ptr(), cap)
+            buf.zero_()
             eng.diff(db)
             eng.sync()
             eng.k2_profile(0, 0)
