@@ -478,10 +478,24 @@ def main():
         # the timed loop overlaps passes, so a kernel's event span there includes waiting for CUs the other
         # pass holds: the roofline's kernel times come from isolated passes of the same batch (untimed)
         eng.timing_reset()
-        for _ in range(args.calib_passes):
-            eng.diff(db)
-            eng.sync()
+        # one rank at a time: in the one-GPU rehearsal every rank's passes share the device, and
+        # two ranks' "isolated" passes running together measured each other (K3 0.83 ms vs 0.12 alone)
+        for r in range(world if collective else 1):
+            if r == rank:
+                for _ in range(args.calib_passes):
+                    eng.diff(db)
+                    eng.sync()
+            if collective:
+                dist.barrier()
     tm = eng.timings()
+    per_rank_ms = None
+    if collective:  # every rank's kernel times of its isolated passes (the rehearsal's per-rank K3, item 5)
+        t = torch.tensor([tm.compare_ms, tm.compact_ms, tm.join_ms, tm.emit_ms, tm.total_ms], dtype=torch.float64,
+                         device=comm_dev)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_rank_ms = [dict(zip(("compare", "compact", "join_exposed", "emit", "diff_pass"),
+                                [round(float(x), 4) for x in a.tolist()])) for a in allt]
     log("timed region: %d steps in %.3f s" % (args.steps, dt))
     gather_check = None
     if gather is not None:
@@ -642,7 +656,7 @@ def main():
                                       % args.calib_passes) if args.pipeline == 2 else "the timed loop's passes",
                            "compare_all_launches": tm.compare_ms, "compact": tm.compact_ms,
                            "join_exposed": tm.join_ms, "emit": tm.emit_ms, "diff_pass": tm.total_ms,
-                           "passes": tm.n_passes},
+                           "passes": tm.n_passes, "per_rank": per_rank_ms},
             "cpu_baseline": cpu,
             "json_in": json_in,
             "checks": {"full_size": full_check, "sample": sample_check, "three_way": three_way,

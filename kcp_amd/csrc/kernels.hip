@@ -526,16 +526,25 @@ __device__ __forceinline__ void join_whole(uint64_t wm, uint32_t p, uint32_t d, 
                                            const gpudiff_pair_row* __restrict__ rows, const uint8_t* __restrict__ pool,
                                            uint64_t mask, uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
                                            uint32_t* __restrict__ path_count, uint8_t* __restrict__ noop_d,
-                                           uint32_t lane) {
+                                           uint32_t lane, uint8_t* lds) {
     for (; wm; wm &= wm - 1) {
         const uint32_t k = (uint32_t)__builtin_ctzll(wm);
         const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)p, (int)k);
         const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)k);
         const uint32_t sok = (uint32_t)__builtin_amdgcn_readlane((int)so, (int)k);
         const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k);
-        const gpudiff_pair_row r = rows[pk];
-        uint32_t nb = 0;
-        const uint32_t cnt = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
+        gpudiff_pair_row r = rows[pk];
+        uint32_t nb = 0, cnt;
+        const uint32_t sa = staged_side_bytes(fk, r.spec_l_a, r.spec_ar_a, r.stat_l_a, r.stat_ar_a);
+        const uint32_t sb = staged_side_bytes(fk, r.spec_l_b, r.spec_ar_b, r.stat_l_b, r.stat_ar_b);
+        if ((fk & (F_JSPEC | F_JSTAT)) && sa <= kJoinLdsSide && sb <= kJoinLdsSide) {  // small pair: from LDS
+            stage_pair(lds, pool, r.off_a, sa, r.off_b, sb, lane);
+            r.off_a = 0;
+            r.off_b = kJoinLdsSide;
+            cnt = join_pair<true, true>(r, fk, (Mem<true>::u8*)lds, mask, sh, sk, sok, lane, &nb);
+        } else {
+            cnt = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
+        }
         if (lane == 0) {
             path_count[dk] = cnt;
             noop_d[dk] = (uint8_t)nb;
@@ -562,6 +571,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint64_t lt = mask_lt(lane);
+    __shared__ __attribute__((aligned(16))) uint8_t join_lds[4][2 * kJoinLdsSide];  // join_whole's staging, per wave
+    uint8_t* const my_lds = join_lds[threadIdx.x >> 6];
     for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
         const uint32_t p = (c << 6) + lane;
         const bool valid = p < n;
@@ -603,7 +614,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                 noop_d[d] = nbits[p];
             }
         }
-        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane);
+        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane, my_lds);
     }
 }
 
@@ -623,6 +634,8 @@ __global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t ndirty = summary[2];
     if (summary[6] == 0u) return;
+    __shared__ __attribute__((aligned(16))) uint8_t join_lds[4][2 * kJoinLdsSide];  // join_whole's staging, per wave
+    uint8_t* const my_lds = join_lds[threadIdx.x >> 6];
     for (uint32_t c = wave; c < (ndirty + 63u) >> 6; c += nwaves) {
         const uint32_t d = (c << 6) + lane;
         const uint32_t p = d < ndirty ? dirty_idx[d] : 0u;
@@ -634,7 +647,7 @@ __global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__
             const uint32_t cap = caps[p];
             whole = place_deferred(d, so, cap, scratch_cap, slot_owner) && cap <= kJoinSlice;
         }
-        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane);
+        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane, my_lds);
     }
 }
 
