@@ -116,7 +116,8 @@ def run(args):
 
     cpu = None
     if not args.no_cpu_baseline:
-        T = len(os.sched_getaffinity(0))
+        from bench import cpu_threads, host_cores
+        T = cpu_threads(*host_cores()[::2])  # affinity capped by the cgroup quota
         n_c = min(N, 20 * args.cpu_sample)
         hp = G.HostPairs(pairs[:n_c], kinds[:n_c])
         hp.classify(threads=T)  # warm

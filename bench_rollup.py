@@ -44,7 +44,8 @@ def run(args):
     from kcp_amd import synth as S
 
     torch.cuda.set_device(0)
-    ncpu = len(os.sched_getaffinity(0))
+    from bench import cpu_threads, host_cores
+    ncpu = cpu_threads(*host_cores()[::2])  # affinity capped by the cgroup quota: the cores it can run at once
     threads = args.threads or max(1, min(16, ncpu))
     t0 = time.time()
     docs, roots = S.rollup_population(args.roots, args.leaves)

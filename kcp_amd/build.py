@@ -39,7 +39,11 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"--off
 # atomicAdd as an item starts and reads it only at the item's end; the optimizer's broadcast of the
 # returned value (readfirstlane + per-lane prefix) waited for the atomic's round trip right where it
 # was issued -- a full, queue-loaded HBM latency at the start of every item.
-FILE_FLAGS = {"kernels.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
+# tokenize.hip: no promotion of private arrays to LDS.  LLVM moved the marshal mode's (K10) per-lane arrays into
+# 5 KiB of LDS per one-wave workgroup, which halved K10's resident waves: 9.28 -> 6.45 ms per 131k bodies without it
+# (profiles/r06h, interleaved A/B; K0 / K11 / K13 have no promoted arrays and are unchanged)
+FILE_FLAGS = {"kernels.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"],
+              "tokenize.hip": ["-mllvm", "-disable-promote-alloca-to-lds"]}
 
 
 def _digest(parts, files):

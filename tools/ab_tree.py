@@ -3,7 +3,7 @@ built in-tree here and shipped with the snapshot; tools/ab_tree.py run times the
 over rounds, on the same box.
 
     python tools/ab_tree.py make NAME [--rev REV] [--patch FILE]   # ab/NAME from git REV (default: the working tree)
-    python tools/ab_tree.py run NAME1,NAME2,... --config config2 [--rounds 3] [--pairs N] [-- extra k2_time args]
+    python tools/ab_tree.py run NAME1,NAME2,... --config config2 [--rounds 3] [--pairs N] [--script bench.py] [-- args]
 
 --patch FILE: a Python file with `def patch(root)` that edits the tree's sources before the build.  `.` as a NAME in
 run is the repo itself.  ab/ is git-ignored; delete it when done (it is shipped to the GPU box while it exists).
@@ -19,7 +19,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 AB = os.path.join(ROOT, "ab")
-PARTS = ["kcp_amd", "include", "tools/k2_time.py"]
+PARTS = ["kcp_amd", "include", "tools/k2_time.py", "bench.py", "bench_upsert.py", "bench_rollup.py", "bench_negotiate.py",
+         "bench_replay.py"]
 
 
 def make(name, rev, patch):
@@ -54,12 +55,13 @@ def make(name, rev, patch):
     print("ab/%s built" % name)
 
 
-def run(names, config, rounds, pairs, extra, timeout):
-    env = dict(os.environ, KCP_AB_MAIN=ROOT)
+def run(names, config, rounds, pairs, extra, timeout, script):
+    # the tree's own package first (its script's directory), the main repo after it for oracle/ and tests/
+    env = dict(os.environ, KCP_AB_MAIN=ROOT, PYTHONPATH=ROOT)
     for r in range(rounds):
         for nm in names:
             tree = ROOT if nm == "." else os.path.join(AB, nm)
-            cmd = [sys.executable, os.path.join(tree, "tools", "k2_time.py"), "--config", config] + (
+            cmd = [sys.executable, os.path.join(tree, script), "--config", config] + (
                 ["--pairs", str(pairs)] if pairs else []) + extra
             t0 = time.time()
             p = subprocess.run(cmd, cwd=tree, env=env, capture_output=True, text=True, timeout=timeout)
@@ -81,12 +83,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=0)
     ap.add_argument("--timeout", type=int, default=240)
+    ap.add_argument("--script", default="tools/k2_time.py", help="e.g. bench.py (any script printing a JSON line)")
     args, extra = ap.parse_known_args()
     extra = [a for a in extra if a != "--"]
     if args.cmd == "make":
         make(args.names, args.rev, args.patch)
     else:
-        run(args.names.split(","), args.config, args.rounds, args.pairs, extra, args.timeout)
+        run(args.names.split(","), args.config, args.rounds, args.pairs, extra, args.timeout, args.script)
 
 
 if __name__ == "__main__":
