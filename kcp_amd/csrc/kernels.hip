@@ -1057,6 +1057,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         if (lane == 0) tt = atomicAdd(ctr_tail, 1u);
         return tail0 + uni(__builtin_amdgcn_readlane(tt, 0));
     };
+    // The default kernel takes its next main ticket once the item's first pass is in flight (round 6): issued at the
+    // item's start, the atomic's queue-loaded round trip was waited for together with the item's rows (vmcnt counts
+    // in order).  Prefetching the next item's rows as well cut the per-item latency from 6.3 to 2.5 us in the
+    // timeline but measured neutral (profiles/r06j): the saved time went into slower streaming -- the pass is
+    // bandwidth-bound, not latency-bound.
     for (uint32_t it = wave, tk = 0; it < nitems; it = advance(it, tk)) {
         // the item this ticket stands for: in the largest-first round, one pair (the permuted order)
         const bool lpt = lpt_r && it >= n_main;
@@ -1066,7 +1071,7 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t im = lpt ? 0u : (r2 && it >= n_main2) ? n_main2 + tail_perm[lpt_pairs + (it - n_main2)] : it;
         const bool tail = !lpt && im >= n_full;
         // the next main ticket: fetched while this item streams
-        if (it < n_main && lane == 0) tk = atomicAdd(ctr, 1u);
+        if (HELP && it < n_main && lane == 0) tk = atomicAdd(ctr, 1u);
         [[maybe_unused]] uint64_t tp_i = 0;
         if constexpr (PROF) {
             tp_i = wall_clock64();
@@ -1080,7 +1085,10 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
         const uint32_t c = lpt ? lp >> 6 : c_begin + (tail ? nch - tail_c : 0u) + (j >> ish);
         const uint32_t per = 64u >> ish;
         const uint32_t p0 = lpt ? lp : (c << 6) + (j & ((1u << ish) - 1u)) * per;
-        if (p0 >= n) continue;
+        if (p0 >= n) {  // an item past the batch's end: still take the next ticket (advance() reads it)
+            if (!HELP && it < n_main && lane == 0) tk = atomicAdd(ctr, 1u);
+            continue;
+        }
         const uint32_t cnt = min(per, n - p0);
         const bool valid = lane < cnt;
         // ---- rows: lane k holds pair p0 + k
@@ -1153,8 +1161,12 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
             mis_s = ((uint64_t)uni((uint32_t)(ms >> 32)) << 32) | uni((uint32_t)ms);
             mis_t = ((uint64_t)uni((uint32_t)(mt >> 32)) << 32) | uni((uint32_t)mt);
         } else {
-            for (uint32_t base = 0; base < total; base += 64u * U)
+            uint32_t pass = 0;
+            for (uint32_t base = 0; base < total; base += 64u * U, pass++) {
                 stream_pass(base, total, incl, first, n1, adj_a, adj_b, off_a, off_b, mis_s, mis_t);
+                if (pass == 0 && it < n_main && lane == 0) tk = atomicAdd(ctr, 1u);  // back by the next pass
+            }
+            if (pass == 0 && it < n_main && lane == 0) tk = atomicAdd(ctr, 1u);  // an item with nothing to stream
         }
         [[maybe_unused]] uint64_t tp_s1 = 0;
         if constexpr (PROF) {
