@@ -972,8 +972,6 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
     bool deferred = false;
     const uint64_t sent0 = status_sentinel_hash(0, mask);
     __shared__ HelpSlot help_slots[HELP ? 4 : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t join_lds[4][2 * kJoinLdsSide];  // stage_pair, one area per wave
-    uint8_t* const my_lds = join_lds[threadIdx.x >> 6];
     [[maybe_unused]] HelpSlot* const my = &help_slots[HELP ? (threadIdx.x >> 6) : 0];
     if constexpr (HELP) {
         if (lane == 0) {
@@ -1215,17 +1213,11 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
                     // dead during the join
-                    gpudiff_pair_row r = rows[p0 + k];
-                    const uint32_t sa = staged_side_bytes(fk, r.spec_l_a, r.spec_ar_a, r.stat_l_a, r.stat_ar_a);
-                    const uint32_t sb = staged_side_bytes(fk, r.spec_l_b, r.spec_ar_b, r.stat_l_b, r.stat_ar_b);
-                    if (sa <= kJoinLdsSide && sb <= kJoinLdsSide) {  // small pair: joined from LDS
-                        stage_pair(my_lds, pool, r.off_a, sa, r.off_b, sb, lane);
-                        r.off_a = 0;
-                        r.off_b = kJoinLdsSide;
-                        pc = join_pair<true, true>(r, fk, (Mem<true>::u8*)my_lds, mask, ah, ak, src, lane, &nb);
-                    } else {
-                        pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
-                    }
+                    // (joining small pairs from an LDS-staged copy here cut config2's join time per item 32 -> 15 us
+                    // but raised K2 to 137 VGPRs, 3 waves/SIMD: config3 at 10M lost 3.5%, profiles/r06n -- K3's
+                    // whole deferrals keep that staging, K2 joins from global memory)
+                    const gpudiff_pair_row r = rows[p0 + k];
+                    pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
                     const uint32_t fa = (uint32_t)__builtin_amdgcn_readlane((int)v3.x, (int)k);
                     nb = sentinel_noop_bits(fa);

@@ -66,7 +66,7 @@ def main():
         k += 1
     eng.sync()
     res = eng.wait(eng.diff(db))
-    out = {"config": args.config, "pairs": n, "build_id": G.BUILD_ID, "tree": HERE,
+    out = {"config": args.config, "pairs": n, "build_id": getattr(G, "BUILD_ID", None), "tree": HERE,
            "format_bytes": db.stats().compare_bytes}
     if parts:
         c_flags = np.concatenate([q[0] for q in parts])
