@@ -228,38 +228,21 @@ __global__ __launch_bounds__(256) void k_scan_apply(const V* in, const uint32_t*
 }
 
 // ---------------------------------------------------------------- K4
-// The joins read the pool (global memory) or, for a small pair K2 staged, the wave's LDS (stage_pair): the same
-// code over address-space-typed pointers, so each form keeps its own addressing (global loads with a scalar base,
-// or 32-bit LDS addresses) instead of 64-bit flat addresses for both.
-template <bool LDS> struct Mem {
-    typedef const uint8_t u8;
-    typedef const uint32_t u32;
-    typedef const uint64_t u64;
-};
-template <> struct Mem<true> {
-    typedef const __attribute__((address_space(3))) uint8_t u8;
-    typedef const __attribute__((address_space(3))) uint32_t u32;
-    typedef const __attribute__((address_space(3))) uint64_t u64;
-};
-
-template <bool LDS>
-struct RegionViewT {
-    typename Mem<LDS>::u32* keys;
-    typename Mem<LDS>::u64* vals;
-    typename Mem<LDS>::u32* metas;
-    typename Mem<LDS>::u8* arena;
+struct RegionView {
+    const uint32_t* keys;
+    const uint64_t* vals;
+    const uint32_t* metas;
+    const uint8_t* arena;
     uint32_t L;
 };
-typedef RegionViewT<false> RegionView;
 
-template <bool LDS = false>
-__device__ __forceinline__ RegionViewT<LDS> region_view(typename Mem<LDS>::u8* pool, uint64_t off, uint32_t sl,
-                                                        uint32_t sar, bool status, uint32_t L) {
-    typename Mem<LDS>::u8* seg = pool + off + (status ? seg_bytes(sl, sar) : 0);
-    RegionViewT<LDS> v;
-    v.vals = (typename Mem<LDS>::u64*)seg;  // vals u64 | keys u32 | metas u32 | arena (include/gpudiff_format.h)
-    v.keys = (typename Mem<LDS>::u32*)(seg + 8ull * L);
-    v.metas = (typename Mem<LDS>::u32*)(seg + 12ull * L);
+__device__ __forceinline__ RegionView region_view(const uint8_t* pool, uint64_t off, uint32_t sl, uint32_t sar,
+                                                  bool status, uint32_t L) {
+    const uint8_t* seg = pool + off + (status ? seg_bytes(sl, sar) : 0);
+    RegionView v;
+    v.vals = (const uint64_t*)seg;  // vals u64 | keys u32 | metas u32 | arena (include/gpudiff_format.h)
+    v.keys = (const uint32_t*)(seg + 8ull * L);
+    v.metas = (const uint32_t*)(seg + 12ull * L);
     v.arena = seg + 16ull * L;
     v.L = L;
     return v;
@@ -286,8 +269,7 @@ __device__ __forceinline__ uint32_t tile_lower_bound(uint32_t x, uint32_t tile, 
 // addresses), finding a dword's owner lane by a cross-lane binary search over
 // the prefix sums.  No load reaches past a tail's padded end.  Returns true in
 // the lanes whose tail differs.
-template <bool LDS>
-__device__ bool confirm_values(bool need, typename Mem<LDS>::u8* arena_a, uint32_t off_a, typename Mem<LDS>::u8* arena_b,
+__device__ bool confirm_values(bool need, const uint8_t* arena_a, uint32_t off_a, const uint8_t* arena_b,
                                uint32_t off_b, uint32_t len, uint32_t lane) {
     const uint32_t n4 = need ? (len + 3u) >> 2 : 0u;
     const uint32_t incl = wave_incl_scan(n4);
@@ -315,8 +297,8 @@ __device__ bool confirm_values(bool need, typename Mem<LDS>::u8* arena_a, uint32
             const uint32_t first = shfl32(incl - n4, own[u]);
             if (act[u]) {
                 const uint32_t k = g - first;
-                xa[u] = *(typename Mem<LDS>::u32*)(arena_a + oa + 4u * k);
-                xb[u] = *(typename Mem<LDS>::u32*)(arena_b + ob + 4u * k);
+                xa[u] = *(const uint32_t*)(arena_a + oa + 4u * k);
+                xb[u] = *(const uint32_t*)(arena_b + ob + 4u * k);
             }
         }
 #pragma unroll
@@ -349,8 +331,8 @@ __device__ __forceinline__ bool wire_equal_number(uint32_t ma, uint64_t xa, uint
 // Merge-join of one region; returns the number of paths emitted.  Emission
 // order = ascending key (the union of both sorted key lists).  *weq_all: every
 // emitted path is a CHANGED leaf with wire_equal_number values (wave-uniform).
-template <bool EMIT, bool LDS = false>
-__device__ uint32_t join_region(const RegionViewT<LDS>& A, const RegionViewT<LDS>& B, uint8_t region_bit,
+template <bool EMIT>
+__device__ uint32_t join_region(const RegionView& A, const RegionView& B, uint8_t region_bit,
                                 uint64_t* __restrict__ out_h, uint8_t* __restrict__ out_k, uint32_t out_base,
                                 uint32_t lane, bool* weq_all) {
     uint32_t ia = 0, ib = 0, arA = 0, arB = 0, outpos = 0;
@@ -388,7 +370,7 @@ __device__ uint32_t join_region(const RegionViewT<LDS>& A, const RegionViewT<LDS
         const bool matchA = inA && jA < nb && kbj == ka;
         bool differ = matchA && (ma != mbj || xa != xbj);
         // equal head (the first 8 bytes, in vals) and length: confirm the tails in the arenas
-        differ |= confirm_values<LDS>(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
+        differ |= confirm_values(matchA && !differ && meta_long(ma), A.arena, offA, B.arena, obj, (ma >> 3) - 8u, lane);
         // resolve B keys against the A window
         const uint32_t iB = tile_lower_bound(kb, ka, na);
         const uint32_t kai = shfl32(ka, min(iB, 63u));
@@ -441,20 +423,20 @@ __device__ __forceinline__ uint32_t sentinel_noop_bits(uint32_t flags_a) {
     return (flags_a & GPUDIFF_OBJ_HAS_STATUS) ? 0u : NOOP_STATUS;
 }
 
-template <bool EMIT, bool LDS = false>
-__device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, typename Mem<LDS>::u8* pool, uint64_t mask,
+template <bool EMIT>
+__device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, const uint8_t* pool, uint64_t mask,
                               uint64_t* out_h, uint8_t* out_k, uint32_t base, uint32_t lane, uint32_t* noop) {
     uint32_t n = 0;
     bool spec_weq = true, stat_weq = true;
     if (f & F_JSPEC) {
-        RegionViewT<LDS> A = region_view<LDS>(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
-        RegionViewT<LDS> B = region_view<LDS>(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
-        n += join_region<EMIT, LDS>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
+        RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, false, r.spec_l_a);
+        RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, false, r.spec_l_b);
+        n += join_region<EMIT>(A, B, 0, out_h, out_k, base + n, lane, &spec_weq);
     }
     if (f & F_JSTAT) {
-        RegionViewT<LDS> A = region_view<LDS>(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
-        RegionViewT<LDS> B = region_view<LDS>(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
-        n += join_region<EMIT, LDS>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
+        RegionView A = region_view(pool, r.off_a, r.spec_l_a, r.spec_ar_a, true, r.stat_l_a);
+        RegionView B = region_view(pool, r.off_b, r.spec_l_b, r.spec_ar_b, true, r.stat_l_b);
+        n += join_region<EMIT>(A, B, GPUDIFF_PATH_REGION_STATUS, out_h, out_k, base + n, lane, &stat_weq);
     }
     const bool stat_ok = stat_weq && (!(f & F_SENT) || !(r.flags_a & GPUDIFF_OBJ_HAS_STATUS));
     *noop = (((f & F_SPEC) && spec_weq) ? NOOP_SPEC : 0u) | (((f & F_STATUS) && stat_ok) ? NOOP_STATUS : 0u);
@@ -466,39 +448,6 @@ __device__ uint32_t join_pair(const gpudiff_pair_row& r, uint32_t f, typename Me
         n += 1;
     }
     return n;
-}
-
-// A small dirty pair's joined segments staged in the wave's LDS before K2 joins it (round 6): per
-// side, [spec start, end of the last joined region) -- 16-B aligned, a multiple of 16 bytes -- with every 16-B load
-// of both sides issued before the first is stored, so the join waits for ONE HBM round trip instead of one per
-// 64-key window and per long-value confirmation pass (config2's ConfigMaps/Secrets: 4-5 dependent trips of a few us
-// each under a full streaming load, 29% of a K2 wave's busy time, profiles/r06a/config2/wave_c2.json).
-constexpr uint32_t kJoinLdsSide = 4096;  // bytes per side: 4 x 16 B per lane
-__device__ __forceinline__ uint32_t staged_side_bytes(uint32_t f, uint32_t spec_l, uint32_t spec_ar, uint32_t stat_l,
-                                                      uint32_t stat_ar) {
-    return (uint32_t)((f & F_JSTAT) ? seg_bytes(spec_l, spec_ar) + seg_bytes(stat_l, stat_ar) : seg_bytes(spec_l, spec_ar));
-}
-__device__ __forceinline__ void stage_pair(uint8_t* lds, const uint8_t* pool, uint64_t off_a, uint32_t bytes_a,
-                                           uint64_t off_b, uint32_t bytes_b, uint32_t lane) {
-    // the previous staged join's LDS reads are done before the DMA overwrites them (LDS runs a wave's operations in
-    // order; the fence keeps the compiler from sinking those reads below the loads)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    // direct-to-LDS loads (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane k at base + 16 k, no VGPRs)
-#pragma unroll
-    for (uint32_t u = 0; u < kJoinLdsSide / 1024u; u++) {
-        const uint32_t i = 1024u * u + 16u * lane;
-        if (1024u * u < bytes_a && i < bytes_a)
-            __builtin_amdgcn_global_load_lds((const void*)(pool + off_a + i),
-                                             (__attribute__((address_space(3))) void*)(lds + 1024u * u), 16, 0, 0);
-        if (1024u * u < bytes_b && i < bytes_b)
-            __builtin_amdgcn_global_load_lds((const void*)(pool + off_b + i),
-                                             (__attribute__((address_space(3))) void*)(lds + kJoinLdsSide + 1024u * u),
-                                             16, 0, 0);
-    }
-    // landed in LDS before any lane reads another's bytes (the join's windows and arenas)
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
 }
 
 // ---------------------------------------------------------------- K3 compaction
@@ -526,25 +475,16 @@ __device__ __forceinline__ void join_whole(uint64_t wm, uint32_t p, uint32_t d, 
                                            const gpudiff_pair_row* __restrict__ rows, const uint8_t* __restrict__ pool,
                                            uint64_t mask, uint64_t* __restrict__ sh, uint8_t* __restrict__ sk,
                                            uint32_t* __restrict__ path_count, uint8_t* __restrict__ noop_d,
-                                           uint32_t lane, uint8_t* lds) {
+                                           uint32_t lane) {
     for (; wm; wm &= wm - 1) {
         const uint32_t k = (uint32_t)__builtin_ctzll(wm);
         const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)p, (int)k);
         const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)k);
         const uint32_t sok = (uint32_t)__builtin_amdgcn_readlane((int)so, (int)k);
         const uint32_t fk = (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k);
-        gpudiff_pair_row r = rows[pk];
-        uint32_t nb = 0, cnt;
-        const uint32_t sa = staged_side_bytes(fk, r.spec_l_a, r.spec_ar_a, r.stat_l_a, r.stat_ar_a);
-        const uint32_t sb = staged_side_bytes(fk, r.spec_l_b, r.spec_ar_b, r.stat_l_b, r.stat_ar_b);
-        if ((fk & (F_JSPEC | F_JSTAT)) && sa <= kJoinLdsSide && sb <= kJoinLdsSide) {  // small pair: from LDS
-            stage_pair(lds, pool, r.off_a, sa, r.off_b, sb, lane);
-            r.off_a = 0;
-            r.off_b = kJoinLdsSide;
-            cnt = join_pair<true, true>(r, fk, (Mem<true>::u8*)lds, mask, sh, sk, sok, lane, &nb);
-        } else {
-            cnt = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
-        }
+        const gpudiff_pair_row r = rows[pk];
+        uint32_t nb = 0;
+        const uint32_t cnt = join_pair<true>(r, fk, pool, mask, sh, sk, sok, lane, &nb);
         if (lane == 0) {
             path_count[dk] = cnt;
             noop_d[dk] = (uint8_t)nb;
@@ -571,8 +511,6 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
     const uint32_t wave = uni((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint64_t lt = mask_lt(lane);
-    __shared__ __attribute__((aligned(16))) uint8_t join_lds[4][2 * kJoinLdsSide];  // join_whole's staging, per wave
-    uint8_t* const my_lds = join_lds[threadIdx.x >> 6];
     for (uint32_t c = c_begin + wave; c < c_end; c += nwaves) {
         const uint32_t p = (c << 6) + lane;
         const bool valid = p < n;
@@ -614,7 +552,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
                 noop_d[d] = nbits[p];
             }
         }
-        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane, my_lds);
+        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane);
     }
 }
 
@@ -634,8 +572,6 @@ __global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t ndirty = summary[2];
     if (summary[6] == 0u) return;
-    __shared__ __attribute__((aligned(16))) uint8_t join_lds[4][2 * kJoinLdsSide];  // join_whole's staging, per wave
-    uint8_t* const my_lds = join_lds[threadIdx.x >> 6];
     for (uint32_t c = wave; c < (ndirty + 63u) >> 6; c += nwaves) {
         const uint32_t d = (c << 6) + lane;
         const uint32_t p = d < ndirty ? dirty_idx[d] : 0u;
@@ -647,7 +583,7 @@ __global__ __launch_bounds__(256) void k_slot_owners(const uint8_t* __restrict__
             const uint32_t cap = caps[p];
             whole = place_deferred(d, so, cap, scratch_cap, slot_owner) && cap <= kJoinSlice;
         }
-        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane, my_lds);
+        join_whole(ballot(whole), p, d, so, f, rows, pool, mask, sh, sk, path_count, noop_d, lane);
     }
 }
 
@@ -1213,9 +1149,9 @@ __global__ __launch_bounds__(256, MINB) void k_compare_flat(const gpudiff_pair_r
                 if (fk & (F_JSPEC | F_JSTAT)) {
                     // the row again, as a scalar load (just read: an L2 hit), so the row registers are
                     // dead during the join
-                    // (joining small pairs from an LDS-staged copy here cut config2's join time per item 32 -> 15 us
-                    // but raised K2 to 137 VGPRs, 3 waves/SIMD: config3 at 10M lost 3.5%, profiles/r06n -- K3's
-                    // whole deferrals keep that staging, K2 joins from global memory)
+                    // (joining small pairs from a copy staged in LDS by direct-to-LDS loads cut config2's join time
+                    // per item 32 -> 15 us but raised K2 to 137 VGPRs, 3 waves/SIMD: config3 at 10M lost 3.5%,
+                    // profiles/r06m, r06n; staging K3's whole deferrals cost K3 4.5 us a pass in LDS occupancy)
                     const gpudiff_pair_row r = rows[p0 + k];
                     pc = join_pair<true>(r, fk, pool, mask, ah, ak, src, lane, &nb);
                 } else if (fk & F_SENT) {  // status-absent only (every ConfigMap/Secret update)
@@ -1465,7 +1401,7 @@ hipError_t launch_move_blobs(hipStream_t s, const uint8_t* src, uint8_t* dst, co
     return hipGetLastError();
 }
 
-// The decision kernels: 8 x 16-B chunks a side in flight per lane at 3 waves/SIMD (139 VGPRs) by default, 16 at
+// The decision kernels: 8 x 16-B chunks a side in flight per lane at 4 waves/SIMD (123 VGPRs, round 6) by default, 16 at
 // 2 waves/SIMD for deep pairs (>= kK2BigPairBytes a pair on average), each also as the per-wave timeline build
 // (gpudiff_k2_profile, tools/k2_wave_profile.py).  In-process A/B (profiles/r04p): 8 in flight beat round
 // 3's 4 at 4 waves on every shape -- config3 10M K2 8.21 vs 8.28 ms, the N = 8 share 1.147 vs 1.164, config4 1.080
