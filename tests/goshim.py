@@ -319,3 +319,31 @@ class Batcher:
                 stale_tick = True  # the timer fired during the flush and Reset does not drain it
             deadline = now + self.window
         return self.enqueued
+
+
+# ---------------------------------------------------------------- gpudiff.go Batcher.submitStored (store path)
+def stage_stored(evs, seen: set, pinned: bool = True):
+    """gpudiff.go submitStored for one flush of store events [(slot, old_json or None, new_json)] whose new object
+    is an *unstructured.Unstructured (the others never reach the store).  On a device-encode store (pinned) the
+    documents the store encodes go into ONE engine-pinned buffer in the zero-copy layout, in order: a slot's old
+    object when the slot is new to the store (`seen`, the Go Store.seen mirror, updated here), then the new object
+    (an untransferable one as the undecodable "{"); every other old object -- read only on a collision -- goes into a
+    plain buffer of its own.  Returns (pinned bytes, plain bytes, [(slot, new (off, len), old (off, len) or None,
+    old in the pinned buffer)])."""
+    jb, jold = JsonBuf(pinned), JsonBuf(False)
+    entries = []
+    for slot, old, new in evs:
+        o, in_jb = None, False
+        tree_old = informer_object(old) if old is not None else None
+        if slot not in seen:
+            o = jb.add(tree_old)
+            in_jb = o is not None
+        else:
+            o = jold.add(tree_old)
+        seen.add(slot)
+        n = jb.add(informer_object(new))
+        if n is None:
+            n = jb.raw(b"{")  # undecodable: reported dirty, slot emptied
+        entries.append((slot, n, o, in_jb))
+    jb.tail()
+    return bytes(jb.buf), bytes(jold.buf), entries

@@ -4,6 +4,7 @@ value the predicates compare (Go int64 vs float64 included, specsyncer.go:36;
 SURVEY.md A.4 rows 7/8/9/25/26), so the oracle and the product's host encoder
 see the same thing through it as through the original JSON.  The GPU half is
 tests/test_gpu_goshim.py."""
+import json
 import math
 import random
 import struct
@@ -267,3 +268,29 @@ def test_pinned_flush_buffers_meet_the_zero_copy_layout():
             nxt = docs[k + 1][0] if k + 1 < len(docs) else len(buf) - 32
             assert off % 16 == 0 and nxt >= off + span and not any(buf[off + n:off + span])
         assert len(buf) == docs[-1][0] + ((docs[-1][1] + 47) & ~15) + 32
+
+
+def test_stored_flush_layout_matches_the_store_zero_copy_rule():
+    """gpudiff.go submitStored on a device-encode store: per event in order, the slot's old object when the slot is
+    new to the store, then the new object, in the pinned buffer's zero-copy layout (16-B aligned, zeroed spans,
+    32-byte tail); old objects of slots the store has seen go to the plain buffer (read only on a collision)."""
+    rnd = random.Random(12)
+    docs = [json.dumps({"kind": "ConfigMap", "metadata": {"name": "c%d" % i}, "data": {"k": "v" * rnd.randrange(1, 90)}},
+                       separators=(",", ":")).encode() for i in range(40)]
+    seen = set()
+    for batch in range(3):
+        evs = [(s, docs[(s + batch) % 40] if rnd.random() < 0.8 else None, docs[(s + batch + 1) % 40])
+               for s in rnd.sample(range(16), 10)]
+        first = {s for s, _, _ in evs if s not in seen}
+        pin, plain, entries = gs.stage_stored(evs, seen)
+        order = []
+        for slot, n, o, in_jb in entries:
+            assert in_jb == (slot in first and o is not None)
+            if in_jb:
+                order.append(o)
+            order.append(n)
+        for k, (off, ln) in enumerate(order):
+            span = (ln + 32 + 15) & ~15
+            nxt = order[k + 1][0] if k + 1 < len(order) else len(pin) - 32
+            assert off % 16 == 0 and nxt >= off + span and not any(pin[off + ln:off + span])
+        assert all(s in seen for s, _, _ in evs)

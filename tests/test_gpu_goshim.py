@@ -55,3 +55,48 @@ def test_shim_one_pair_drop_ins():
         assert eng.spec_equal(*sp) == (not r["spec_dirty"]), name
         assert eng.status_equal(*sp) == (not r["status_dirty"]), name
     eng.close()
+
+
+def test_stored_flushes_upload_zero_copy():
+    """The Go batcher's store flushes (tests/goshim.py stage_stored, gpudiff.go submitStored) written into
+    engine-pinned memory are uploaded without the staging copy (every batch counts as zero-copy) and decide every
+    event as the oracle does on (previous version, new version)."""
+    import ctypes as C
+    import json
+    import random
+    rnd = random.Random(14)
+
+    def doc(i, v):
+        return json.dumps({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "c%d" % i, "namespace": "ns"},
+                           "data": {"k": "v%d" % v, "pad": "x" * rnd.randrange(1, 200)}}, separators=(",", ":")).encode()
+
+    e = G.Engine(device=0, encode_threads=2)
+    st = e.object_store(max_slots=32, space_bytes=16 << 20, max_events=64, device_encode=True)
+    cur, seen = {}, set()
+    for batch in range(4):
+        evs, pairs = [], []
+        for s in rnd.sample(range(24), 16):
+            new = doc(s, rnd.randrange(3))
+            old = cur.get(s)
+            evs.append((s, old, new))
+            pairs.append((old if old is not None else b"{}", new))
+            cur[s] = new
+        pin, plain, entries = S.stage_stored(evs, seen)
+        p = C.c_void_p()
+        assert G.lib().gpudiff_host_alloc(e.ctx, len(pin), C.byref(p)) == G.OK
+        C.memmove(p.value, pin, len(pin))
+        pb = C.create_string_buffer(plain, max(1, len(plain)))
+        arr = (G.Event * len(entries))()
+        for i, (slot, n, o, in_jb) in enumerate(entries):
+            arr[i].slot, arr[i].pair_id = slot, i
+            arr[i].new_json, arr[i].new_len = p.value + n[0], n[1]
+            if o is not None:
+                base = p.value if in_jb else C.addressof(pb)
+                arr[i].old_json, arr[i].old_len = base + o[0], o[1]
+        z0 = st.stats().zero_copy_batches
+        r = e.wait(st.submit_raw(arr, len(entries), (pb,)))
+        assert st.stats().zero_copy_batches == z0 + 1
+        assert_matches(r, pairs)
+        G.lib().gpudiff_host_free(e.ctx, p)
+    st.free()
+    e.close()
