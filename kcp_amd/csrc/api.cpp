@@ -111,6 +111,7 @@ static DiffBuffers buffers_of(gpudiff_ctx* c, gpudiff_dbatch* d) {
     b.slice_weq = d->slice_weq;
     b.hash_mask = c->hash_mask;
     b.k2_timeline = c->k2_timeline ? 1u : 0u;
+    b.k2_shared = 0u;
     b.tail_perm = d->tail_perm;
     b.tail_perm_key = &d->tail_perm_key;
     b.rows_gen = d->rows_gen;
@@ -408,6 +409,7 @@ int gpudiff_dbatch_create_view(gpudiff_ctx* c, const gpudiff_dbatch* base, gpudi
         dfree_all(d.get());
         return rc;
     }
+    base->views.push_back(d.get());
     *out = d.release();
     return GPUDIFF_OK;
 }
@@ -628,6 +630,10 @@ int gpudiff_shard_lpt(const uint64_t* weights, uint32_t n_clusters, uint32_t wor
 
 void gpudiff_dbatch_free(gpudiff_ctx* c, gpudiff_dbatch* d) {
     if (!d) return;
+    if (d->base) {
+        auto& v = d->base->views;
+        v.erase(std::remove(v.begin(), v.end(), d), v.end());
+    }
     if (c && c->has_device) {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
@@ -681,6 +687,23 @@ int gpudiff_diff(gpudiff_ctx* c, gpudiff_dbatch* d, gpudiff_ticket* ticket) {
     }
     hipStream_t ms = c->stream;
     DiffBuffers b = buffers_of(c, d);
+    // Two passes in flight (a view and its base diffed by two contexts): while another pass over the population is
+    // still running, this pass's K2 launches half its resident grid.  A full-occupancy K2 grid holds every CU slot
+    // until its drain, so the other pass's K2 could not start before this one ended -- the two passes ran back to
+    // back (rocprofv3 trace, profiles/r06z); with half grids both stream at once and each fills the other's drain.
+    // An isolated pass (the other one done) launches the full grid, and so does a large pass, whose drain is a
+    // small part of it: two-in-flight step -5% on config2 (1M pairs, 5.2 GB a pass) and -4.5% on the N = 8 share of
+    // config3 (1.25M pairs, 6.4 GB), +1% on config3 at 10M (51 GB) -- profiles/r06aa.
+    constexpr uint64_t kHalfGridMaxBytes = 16ull << 30;
+    if (d->compare_bytes && d->compare_bytes <= kHalfGridMaxBytes) {
+        const gpudiff_dbatch* fam = d->base ? d->base : d;
+        auto busy = [&](const gpudiff_dbatch* m) {
+            return m != d && m->done && m->ticket && hipEventQuery(m->done) == hipErrorNotReady;
+        };
+        bool shared = busy(fam);
+        for (const gpudiff_dbatch* v : fam->views) shared = shared || busy(v);
+        b.k2_shared = shared ? 1u : 0u;
+    }
     uint4* total = (uint4*)d->summary;  // summary[0..3]: n_spec, n_status, n_dirty, scratch cap
     if (ev) HIPCHK(hipEventRecord(ev[0], ms));
     if (d->n_pairs == 0) {

@@ -108,6 +108,9 @@ struct gpudiff_dbatch {
     // gpudiff_dbatch_create_view: this batch diffs `base`'s resident pairs (pool, rows, pair IDs borrowed,
     // refreshed at every diff) into its own outputs, so two passes over one population can be in flight
     const gpudiff_dbatch* base = nullptr;
+    // a base's live views (gpudiff_dbatch_create_view registers, gpudiff_dbatch_free removes): the passes of one
+    // population that can be in flight together -- K2 launches half its grid while another of them is running
+    mutable std::vector<gpudiff_dbatch*> views;
     int device = -1;
     uint32_t* tail_perm = nullptr;  // K2's largest-first final round (kernels.h DiffBuffers)
     gd::TailPermKey tail_perm_key;

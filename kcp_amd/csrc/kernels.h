@@ -50,6 +50,7 @@ struct DiffBuffers {
     uint8_t* out_k;
     uint64_t hash_mask;
     uint32_t k2_timeline;       // gpudiff_k2_profile installed a buffer: the per-wave timeline build of K2
+    uint32_t k2_shared;         // another pass over the same population is in flight: K2 takes half the chip
     uint32_t* tail_perm;        // K2's largest-first final round: its order (device, kK2LptMax u32)
     struct TailPermKey* tail_perm_key;  // (host) the rows and launch shape tail_perm was computed for
     uint64_t rows_gen;          // bumped whenever the batch's rows change (appends, resets, store batches)

@@ -637,7 +637,7 @@ class ObjectStore:
         if not zero_copy:
             arr, n, keep = self.events(items)
             return self.submit_raw(arr, n, keep)
-        docs, slots = [], []
+        docs = []
         for it in items:
             if it[2] is not None:
                 docs.append(to_json_bytes(it[2]))
