@@ -1449,8 +1449,10 @@ static uint32_t k2_cap_blocks(const DiffBuffers& b) {
             n = 4;
         occ[v] = n;
     }
-    // another pass over the population in flight (DiffBuffers::k2_shared): half the resident grid, so both fit
-    return 256u * (uint32_t)(b.k2_shared ? std::max(1, occ[v] / 2) : occ[v]);
+    // another pass over the population in flight (DiffBuffers::k2_shared): half the resident grid, so both fit --
+    // the default kernel only: the deep-pair kernel's 2 waves/SIMD halved lost 7% of config4's two-in-flight step
+    // (profiles/r06ac)
+    return 256u * (uint32_t)((b.k2_shared && !(v & 1u)) ? std::max(1, occ[v] / 2) : occ[v]);
 }
 
 // Deep pairs (>= 16 KiB of compared bytes on average: config4's 8-64 KiB objects) are split below
