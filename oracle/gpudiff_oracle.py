@@ -94,13 +94,17 @@ def _go_decode_rune(b: bytes, i: int) -> Tuple[int, int]:
     return acc, size
 
 
+_HEX_DIGITS = frozenset(b"0123456789abcdefABCDEF")
+
+
 def _getu4(b: bytes, i: int) -> int:
     if i + 6 > len(b) or b[i] != 0x5C or b[i + 1] != ord('u'):
         return -1
-    try:
-        return int(b[i + 2:i + 6].decode('ascii'), 16)
-    except ValueError:
+    h = b[i + 2:i + 6]
+    # four hex digits exactly (decode.go getu4); int(..., 16) alone would also take whitespace, a sign or '_'
+    if any(c not in _HEX_DIGITS for c in h):
         return -1
+    return int(h.decode('ascii'), 16)
 
 
 class _Parser:
