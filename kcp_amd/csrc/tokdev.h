@@ -339,6 +339,42 @@ __device__ int decode_string(const uint8_t* p, const uint8_t* q, const uint8_t* 
     }
     return (int)(o - dst);
 }
+// K11 / K13: decode_string(p, p + raw, end, dst) >= 0 -- whether Go decodes the string -- decided by the whole wave
+// (every lane gets the answer): a lane per byte over coalesced loads instead of one lane's dependent byte-by-byte
+// loop.  Bytes are paired with escapes as decode_string pairs them (a backslash not itself escaped escapes the next
+// byte; a \u's four digits hold no backslash, or the string is invalid anyway), so it fails exactly on a control byte,
+// an invalid escape or a \u without four hex digits (the closing quote, never a digit, bounds them); a string with a
+// non-ASCII byte (UTF-8 validity) is decided by lane 0's decode_string
+__device__ bool wave_string_ok(const uint8_t* p, uint32_t raw, const uint8_t* end, uint8_t* dst, uint32_t lane) {
+    bool bad = false, hi = false;
+    uint64_t carry = 0;
+    for (uint32_t o = 0; o < raw; o += 64u) {
+        const uint32_t k = o + lane;
+        const bool in = k < raw;
+        const uint32_t c = in ? p[k] : 0x20u;
+        const uint64_t bs = ballot(in & (c == '\\'));
+        uint64_t esc = carry;  // byte 0 of this chunk escaped by the previous chunk's last byte
+        carry = 0;
+        for (uint64_t m = bs; m; m &= m - 1) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            if ((esc >> b) & 1ull) continue;  // an escaped backslash escapes nothing
+            if (b == 63u) carry = 1;
+            else esc |= 1ull << (b + 1u);
+        }
+        const bool e = in & (((esc >> lane) & 1ull) != 0ull);
+        const bool ok_e = (c == '"') | (c == '\\') | (c == '/') | (c == 'b') | (c == 'f') | (c == 'n') | (c == 'r') |
+                          (c == 't') | (c == 'u');
+        bool ubad = false;
+        if (e & (c == 'u'))
+            ubad = (hexv(p[k + 1]) | hexv(p[k + 2]) | hexv(p[k + 3]) | hexv(p[k + 4])) < 0;
+        bad |= in & ((c < 0x20u) | (e & !ok_e) | ubad);
+        hi |= in & (c >= 0x80u);
+    }
+    if (ballot(bad)) return false;
+    if (!ballot(hi)) return true;
+    const int dl = lane == 0 ? decode_string(p, p + raw, end, dst) : 0;
+    return (int)rdlane((uint32_t)dl, 0) >= 0;
+}
 
 // literal / number (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error.  at(k) is the
 // atom's k-th byte, read only for k < left (the bytes to the document's end)
@@ -573,6 +609,15 @@ __device__ __forceinline__ uint32_t parse_atom_fast(uint64_t w0, uint64_t w1, ui
     *tag = GPUDIFF_TAG_INT;
     *val = d0 ? 0ull - v : v;
     return 0u;
+}
+// K11 / K13: parse_atom_mem's answer, from a 16-byte window when parse_atom_fast decides the atom (the common
+// literals and short integers: two word loads instead of a dependent load per byte); p + 23 must be readable, as a
+// document is to kTokSlack bytes past its end
+__device__ __forceinline__ uint32_t parse_atom_quick(const uint8_t* p, const uint8_t* end, uint32_t* tag, uint64_t* val) {
+    uint64_t w0, w1;
+    ld16u(p, &w0, &w1);
+    if (parse_atom_fast(w0, w1, (uint64_t)(end - p), tag, val) == 0u) return GPUDIFF_TOK_OK;
+    return parse_atom_mem(p, end, tag, val);
 }
 // any atom from the 32-byte register window w at p (ld32u); one that runs past the window is parsed from memory
 __device__ __forceinline__ uint32_t parse_atom_win(const uint8_t* p, const uint8_t* end, uint64_t w0, uint64_t w1,
@@ -1033,16 +1078,41 @@ constexpr int kModeEncode = 0, kModeMarshal = 1, kModeRollup = 2, kModeNegotiate
 // K11 (roll-up mode): Go's struct field lookup for an ASCII key -- 0 no
 // match, 1 exact, 2 equal only under ASCII case folding (encoding/json
 // fold.go; the device never sees non-ASCII keys: they are slow strings)
-__device__ __forceinline__ uint32_t field_fold(const uint8_t* k, uint32_t kl, const char* name, uint32_t nl) {
-    if (kl != nl) return 0u;
-    bool exact = true;
-    for (uint32_t i = 0; i < nl; i++) {
-        const uint32_t a = k[i], b = (uint8_t)name[i];
-        if (a == b) continue;
-        exact = false;
-        if ((a ^ b) != 0x20u || (a | 0x20u) - 'a' > 25u) return 0u;
+//
+// The key's first 32 bytes are loaded once as four words (KeyWin, ld32u) and every name is compared from registers
+// (a byte loop paid a dependent load per matching byte, per name).  A byte matches when it is equal, or differs by
+// 0x20 at a letter of the name (then both are the same letter: the byte loop's (a ^ b) == 0x20 && (a | 0x20) is a
+// letter).  Names are <= 32 bytes, constants after inlining.
+struct KeyWin {
+    uint64_t w[4];
+    uint32_t kl;
+};
+__device__ __forceinline__ KeyWin key_window(const uint8_t* kp, uint32_t kl, const uint8_t* lim) {
+    KeyWin K;
+    ld32u(kp, lim, K.w[0], K.w[1], K.w[2], K.w[3]);
+    K.kl = kl;
+    return K;
+}
+__device__ __forceinline__ uint32_t field_fold(const KeyWin& K, const char* name, uint32_t nl) {
+    if (K.kl != nl) return 0u;
+    uint64_t diff = 0, nonfold = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        if (8u * j >= nl) break;
+        uint64_t nw = 0, lm = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 8; b++) {
+            if (8u * j + b >= nl) break;
+            const uint32_t c = (uint8_t)name[8u * j + b];
+            nw |= (uint64_t)c << (8u * b);
+            if ((c | 0x20u) - 'a' <= 25u) lm |= 0x20ull << (8u * b);
+        }
+        const uint64_t valid = nl >= 8u * j + 8u ? ~0ull : (1ull << (8u * (nl - 8u * j))) - 1ull;
+        const uint64_t x = (K.w[j] ^ nw) & valid;
+        diff |= x;
+        nonfold |= x & ~lm;
     }
-    return exact ? 1u : 2u;
+    return diff == 0ull ? 1u : nonfold == 0ull ? 2u : 0u;
 }
 // appsv1.DeploymentStatus counters summed by deployment.go:79-85, in RollOut.v order
 __device__ __forceinline__ const char* roll_field(uint32_t k) {
