@@ -1134,14 +1134,28 @@ __device__ __forceinline__ int64_t neg_days_from_civil(int64_t y, uint32_t m, ui
     const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
     return era * 146097 + doe - 719468;
 }
+// The bytes come from a 40-byte register window (six aligned word loads issued together; a byte loop's early exits
+// made each load wait for the last): the strict shape is at most 35 bytes (nine fraction digits and an offset), so a
+// longer string is never it, and a document is readable to kTokSlack bytes past its end.
 __device__ __forceinline__ bool neg_parse_time(const uint8_t* s, uint32_t l, int64_t* sec, int32_t* nsec) {
-    if (l < 20u) return false;
-    auto dg = [&](uint32_t i) -> uint32_t { return (uint32_t)s[i] - '0'; };
+    if (l < 20u || l > 35u) return false;
+    const uintptr_t a = (uintptr_t)s;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2], x3 = q[3], x4 = q[4], x5 = q[5];
+    auto fw = [&](uint64_t lo, uint64_t hi) -> uint64_t { return (lo >> sh) | ((hi << 1) << (63u - sh)); };
+    const uint64_t w0 = fw(x0, x1), w1 = fw(x1, x2), w2 = fw(x2, x3), w3 = fw(x3, x4), w4 = fw(x4, x5);
+    auto at = [&](uint32_t i) -> uint32_t {  // i < 40: selects, no private array
+        const uint32_t k = i >> 3;
+        const uint64_t v = k == 0u ? w0 : k == 1u ? w1 : k == 2u ? w2 : k == 3u ? w3 : w4;
+        return (uint32_t)(v >> (8u * (i & 7u))) & 0xFFu;
+    };
+    auto dg = [&](uint32_t i) -> uint32_t { return at(i) - '0'; };
     const uint32_t dpos[14] = {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18};
 #pragma unroll
     for (uint32_t k = 0; k < 14; k++)
         if (dg(dpos[k]) > 9u) return false;
-    if (s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':' || s[16] != ':') return false;
+    if (at(4) != '-' || at(7) != '-' || at(10) != 'T' || at(13) != ':' || at(16) != ':') return false;
     const uint32_t year = dg(0) * 1000u + dg(1) * 100u + dg(2) * 10u + dg(3);
     const uint32_t mon = dg(5) * 10u + dg(6), day = dg(8) * 10u + dg(9);
     const uint32_t hh = dg(11) * 10u + dg(12), mi = dg(14) * 10u + dg(15), ss = dg(17) * 10u + dg(18);
@@ -1151,7 +1165,7 @@ __device__ __forceinline__ bool neg_parse_time(const uint8_t* s, uint32_t l, int
     if (day > dim) return false;
     uint32_t p = 19u;
     int32_t ns = 0;
-    if (s[p] == '.' && p + 1u < l && dg(p + 1u) <= 9u) {
+    if (at(p) == '.' && p + 1u < l && dg(p + 1u) <= 9u) {
         uint32_t n = 0;
         p++;
         while (p < l && dg(p) <= 9u) {
@@ -1162,14 +1176,14 @@ __device__ __forceinline__ bool neg_parse_time(const uint8_t* s, uint32_t l, int
         for (uint32_t k = n; k < 9u; k++) ns *= 10;
     }
     int64_t off = 0;
-    if (p < l && s[p] == 'Z') {
+    if (p < l && at(p) == 'Z') {
         p++;
     } else {
-        if (p + 6u != l || (s[p] != '+' && s[p] != '-') || s[p + 3u] != ':' || dg(p + 1u) > 9u || dg(p + 2u) > 9u ||
+        if (p + 6u != l || (at(p) != '+' && at(p) != '-') || at(p + 3u) != ':' || dg(p + 1u) > 9u || dg(p + 2u) > 9u ||
             dg(p + 4u) > 9u || dg(p + 5u) > 9u)
             return false;
         off = ((int64_t)(dg(p + 1u) * 10u + dg(p + 2u)) * 60 + (int64_t)(dg(p + 4u) * 10u + dg(p + 5u))) * 60;
-        if (s[p] == '-') off = -off;
+        if (at(p) == '-') off = -off;
         p += 6u;
     }
     if (p != l) return false;
