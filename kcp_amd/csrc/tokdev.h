@@ -339,15 +339,19 @@ __device__ int decode_string(const uint8_t* p, const uint8_t* q, const uint8_t* 
     }
     return (int)(o - dst);
 }
-// K11 / K13: decode_string(p, p + raw, end, dst) >= 0 -- whether Go decodes the string -- decided by the whole wave
-// (every lane gets the answer): a lane per byte over coalesced loads instead of one lane's dependent byte-by-byte
-// loop.  Bytes are paired with escapes as decode_string pairs them (a backslash not itself escaped escapes the next
-// byte; a \u's four digits hold no backslash, or the string is invalid anyway), so it fails exactly on a control byte,
-// an invalid escape or a \u without four hex digits (the closing quote, never a digit, bounds them); a string with a
-// non-ASCII byte (UTF-8 validity) is decided by lane 0's decode_string
-__device__ bool wave_string_ok(const uint8_t* p, uint32_t raw, const uint8_t* end, uint8_t* dst, uint32_t lane) {
-    bool bad = false, hi = false;
+// decode_string(p, p + raw, end, dst) by the whole wave (every lane gets the answer): a lane per byte over coalesced
+// loads instead of one lane's dependent byte-by-byte loop.  Bytes are paired with escapes as decode_string pairs them
+// (a backslash not itself escaped escapes the next byte; a \u's four digits hold no backslash, or the string is
+// invalid anyway), so it fails exactly on a control byte, an invalid escape or a \u without four hex digits (the
+// closing quote, never a digit, bounds them).  WRITE (K10): the decoded bytes go to dst -- an escaped byte maps to
+// its character, its backslash emits nothing -- and the length is returned; a string with a \u escape or a
+// non-ASCII byte is decoded by lane 0's decode_string instead.  !WRITE (K11 / K13): only the verdict (>= 0 or -1);
+// lane 0's decode_string decides only the UTF-8 validity of a string with a non-ASCII byte.
+template <bool WRITE>
+__device__ int wave_decode_string(const uint8_t* p, uint32_t raw, const uint8_t* end, uint8_t* dst, uint32_t lane) {
+    bool bad = false, hard = false;
     uint64_t carry = 0;
+    uint32_t outn = 0;
     for (uint32_t o = 0; o < raw; o += 64u) {
         const uint32_t k = o + lane;
         const bool in = k < raw;
@@ -368,12 +372,24 @@ __device__ bool wave_string_ok(const uint8_t* p, uint32_t raw, const uint8_t* en
         if (e & (c == 'u'))
             ubad = (hexv(p[k + 1]) | hexv(p[k + 2]) | hexv(p[k + 3]) | hexv(p[k + 4])) < 0;
         bad |= in & ((c < 0x20u) | (e & !ok_e) | ubad);
-        hi |= in & (c >= 0x80u);
+        hard |= in & ((c >= 0x80u) | (WRITE & e & (c == 'u')));
+        if constexpr (WRITE) {
+            if (ballot(hard)) break;  // lane 0's decode_string decides the whole string (its errors included)
+            const bool emit = in & !((c == '\\') & !e);
+            const uint32_t mc = c == 'b' ? 8u : c == 'f' ? 12u : c == 'n' ? 10u : c == 'r' ? 13u : c == 't' ? 9u : c;
+            const uint64_t em = ballot(emit);
+            if (emit) dst[outn + mbcnt64(em)] = (uint8_t)(e ? mc : c);
+            outn += popc64(em);
+        }
     }
-    if (ballot(bad)) return false;
-    if (!ballot(hi)) return true;
+    if (ballot(bad)) return -1;
+    if (!ballot(hard)) return (int)outn;
     const int dl = lane == 0 ? decode_string(p, p + raw, end, dst) : 0;
-    return (int)rdlane((uint32_t)dl, 0) >= 0;
+    return (int)rdlane((uint32_t)dl, 0);
+}
+__device__ __forceinline__ bool wave_string_ok(const uint8_t* p, uint32_t raw, const uint8_t* end, uint8_t* dst,
+                                               uint32_t lane) {
+    return wave_decode_string<false>(p, raw, end, dst, lane) >= 0;
 }
 
 // literal / number (json.cpp value + number): tag + canonical 8 bytes, or a GPUDIFF_TOK_* error.  at(k) is the

@@ -159,3 +159,27 @@ def test_negotiate_string_validity():
         assert st.n_host == len(strs) - sum(ok), (st.n_host, len(strs) - sum(ok))
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["spec", "status"])
+def test_upsert_string_decode(mode):
+    """K10 decodes escaped strings by the whole wave (wave_decode_string<true>) and re-escapes them: every body equals
+    the host path's, and the device emits exactly the bodies whose strings decode without UTF-8 repair."""
+    from tests import upsert_cases as UC
+    from tests.test_gpu_upsert import _check as upsert_check
+    strs, ok = _strings_with_flags(700, 95)
+    base, _ = S.rollup_population(1, 1, seed=96)
+    if mode == "spec":
+        m, old = UC.SPEC, b'"IfNotPresent"'
+    else:
+        m, old = UC.STATUS, b'"Deployment has minimum availability."'
+    assert old in base[1]
+    docs = [base[1].replace(old, b'"' + s + b'"', 1) for s in strs]
+    eng = G.Engine(device=0)
+    try:
+        codes = upsert_check(eng, docs, m, must_device=False)
+        bad = [(i, codes[i], strs[i]) for i in range(len(strs)) if (codes[i] == G.TOK_OK) != ok[i]]
+        assert not bad, (len(bad), bad[:5])
+    finally:
+        eng.close()
