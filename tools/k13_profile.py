@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """K13 phase profile (run on the GPU box): where a wave's time goes when it
 extracts the negotiation classifier's fields of an APIResourceImport /
-NegotiatedAPIResource -- structural scan, tree walk, passes N0-N4
+NegotiatedAPIResource -- structural scan, tree walk, the N0-N4 sweep (one slot since round 6)
 (per-phase wall-clock ticks summed over waves)."""
 import os
 import sys
@@ -26,9 +26,8 @@ for on in (False, True):
     dt = time.time() - t
     prof = eng.k0_profile(False)
     print("profile=%s: K13+K14 %.2f ms for %d docs" % (on, dt * 1e3, n))
-tot = sum(prof[:7])
-for k, nm in [(0, "scan"), (1, "tree"), (3, "N0 atoms/escapes"), (4, "N1 root members"), (5, "N2 metadata/conds"),
-              (6, "N3 maps/elements"), (2, "N4 cond fields+out")]:
+tot = sum(prof[:3])
+for k, nm in [(0, "scan"), (1, "tree"), (2, "N0-N4 sweep + out")]:
     print("  %-18s %6.1f%%  %.2f us/doc-wave" % (nm, 100.0 * prof[k] / max(1, tot), prof[k] / 100.0 / n))
 nb.close()
 eng.close()
