@@ -766,8 +766,8 @@ __device__ __forceinline__ void wave_esc_put(uint8_t* o, const uint8_t* s, uint3
 }
 constexpr uint32_t kLongString = 16;
 
-// ---- flattened string passes (K10): every lane's string (at most one per lane) is cut into 4-byte
-// units laid end to end; each pass the wave takes 64 consecutive units, a unit's owner lane found by a
+// ---- flattened string passes (K10, K0's keys): every lane's string (at most one per lane) is cut into 8-byte
+// units (4-byte ones for wave_copy_dwords0) laid end to end; each pass the wave takes 64 consecutive units, a unit's owner lane found by a
 // binary search over the inclusive unit prefix (as K2 does over 16-B chunks), so a window's strings of
 // any length cost sum(len) / 256 passes instead of one pass per long string plus the longest short one.
 // Unit loads read up to 15 bytes past a string (ld8u): the JSON and decoded-string buffers keep that slack.
@@ -782,6 +782,21 @@ __device__ __forceinline__ FlatUnits flat_units(bool has, uint32_t n) {
     const uint32_t incl = wave_incl_scan(units);
     return FlatUnits{incl, rdlane(incl, 63)};
 }
+// 8-byte units (wave_esc_extra, wave_copy_flat: half the passes of 4-byte ones, each still one ld8u per lane)
+__device__ __forceinline__ FlatUnits flat_units8(bool has, uint32_t n) {
+    const uint32_t units = has ? (n + 7u) >> 3 : 0u;
+    const uint32_t incl = wave_incl_scan(units);
+    return FlatUnits{incl, rdlane(incl, 63)};
+}
+// any byte of x that Go's HTML-safe string encoder does not write as itself: < 0x20, >= 0x80, '"', '\\', '<', '>',
+// '&' (SWAR: exact as to "any", which is all the caller asks before its per-byte pass)
+__device__ __forceinline__ bool swar_has_esc(uint64_t x) {
+    constexpr uint64_t L = 0x0101010101010101ull, H = 0x8080808080808080ull;
+    auto has0 = [&](uint64_t v) -> uint64_t { return (v - L) & ~v & H; };
+    const uint64_t lt20 = (x - 0x20u * L) & ~x & H;
+    return ((x & H) | lt20 | has0(x ^ ('"' * L)) | has0(x ^ ('\\' * L)) | has0(x ^ ('<' * L)) | has0(x ^ ('>' * L)) |
+            has0(x ^ ('&' * L))) != 0ull;
+}
 // owner lane of unit g (the first lane whose inclusive prefix exceeds g; 63 past the end)
 __device__ __forceinline__ uint32_t flat_owner(const FlatUnits& f, uint32_t g) {
     uint32_t o = 0;
@@ -794,8 +809,8 @@ __device__ __forceinline__ uint32_t flat_owner(const FlatUnits& f, uint32_t g) {
 // 0 iff every byte is written as it is
 __device__ uint32_t wave_esc_extra(bool has, const uint8_t* s, uint32_t n) {
     const uint32_t lane = __lane_id();
-    const FlatUnits f = flat_units(has, n);
-    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const FlatUnits f = flat_units8(has, n);
+    const uint32_t units = has ? (n + 7u) >> 3 : 0u;
     const uint64_t sp = (uint64_t)(uintptr_t)s;
     int32_t acc = 0;
     for (uint32_t b = 0; b < f.total; b += 64) {
@@ -805,15 +820,18 @@ __device__ uint32_t wave_esc_extra(bool has, const uint8_t* s, uint32_t n) {
         const uint64_t op = shfl64(sp, o);
         int32_t extra = 0;
         if (g < f.total) {
-            const uint32_t k = 4u * (g - first);
+            const uint32_t k = 8u * (g - first);
             const uint8_t* p = (const uint8_t*)(uintptr_t)op;
-            const uint32_t w = (uint32_t)ld8u(p + k);
-            const uint32_t nb = min(4u, on - k);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++) {
-                const uint32_t c = (w >> (8u * j)) & 0xFFu;
-                const bool plain = c >= 0x20u && c < 0x80u && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&';
-                if (j < nb && !plain) extra += (int32_t)esc_unit(p, on, k + j) - 1;
+            const uint64_t w = ld8u(p + k);
+            const uint32_t nb = min(8u, on - k);
+            // the bytes past the string read as 'a' (plain)
+            const uint64_t keep = nb >= 8u ? ~0ull : (1ull << (8u * nb)) - 1ull;
+            if (swar_has_esc((w & keep) | (0x6161616161616161ull & ~keep))) {  // rare: the bytes one by one
+                for (uint32_t j = 0; j < nb; j++) {
+                    const uint32_t c = (uint32_t)(w >> (8u * j)) & 0xFFu;
+                    const bool plain = c >= 0x20u && c < 0x80u && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&';
+                    if (!plain) extra += (int32_t)esc_unit(p, on, k + j) - 1;
+                }
             }
         }
         for (uint64_t m = __ballot(extra != 0); m; m &= m - 1) {  // escapes are rare
@@ -827,8 +845,8 @@ __device__ uint32_t wave_esc_extra(bool has, const uint8_t* s, uint32_t n) {
 // copies this lane's string s[0, n) to o[0, n) (strings that need no escaping)
 __device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* o) {
     const uint32_t lane = __lane_id();
-    const FlatUnits f = flat_units(has, n);
-    const uint32_t units = has ? (n + 3u) >> 2 : 0u;
+    const FlatUnits f = flat_units8(has, n);
+    const uint32_t units = has ? (n + 7u) >> 3 : 0u;
     const uint64_t sp = (uint64_t)(uintptr_t)s, dp = (uint64_t)(uintptr_t)o;
     for (uint32_t b = 0; b < f.total; b += 64) {
         const uint32_t g = b + lane;
@@ -836,14 +854,14 @@ __device__ void wave_copy_flat(bool has, const uint8_t* s, uint32_t n, uint8_t* 
         const uint32_t first = shfl32(f.incl - units, ow), on = shfl32(n, ow);
         const uint64_t op = shfl64(sp, ow), od = shfl64(dp, ow);
         if (g < f.total) {
-            const uint32_t k = 4u * (g - first);
-            const uint32_t w = (uint32_t)ld8u((const uint8_t*)(uintptr_t)op + k);
+            const uint32_t k = 8u * (g - first);
+            const uint64_t w = ld8u((const uint8_t*)(uintptr_t)op + k);
             uint8_t* q = (uint8_t*)(uintptr_t)od + k;
-            const uint32_t nb = min(4u, on - k);
+            const uint32_t nb = min(8u, on - k);
             q[0] = (uint8_t)w;
-            if (nb > 1) q[1] = (uint8_t)(w >> 8);
-            if (nb > 2) q[2] = (uint8_t)(w >> 16);
-            if (nb > 3) q[3] = (uint8_t)(w >> 24);
+#pragma unroll
+            for (uint32_t j = 1; j < 8; j++)
+                if (nb > j) q[j] = (uint8_t)(w >> (8u * j));
         }
     }
 }
